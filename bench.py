@@ -1,0 +1,154 @@
+#!/usr/bin/env python
+"""Headline benchmark: Llama-3-8B INT4 (sym_int4) decode tokens/s + first-token
+latency on N MI355X GPUs (BASELINE.json metric).
+
+One process per GPU (torchrun).  Each rank serves its own replica (data-
+parallel serving, weak scaling: fixed batch per GPU): random-init weights of
+the exact Llama-3-8B architecture are generated and quantized to sym_int4 on
+the GPU, a synthetic prompt batch is prefilled (first-token latency), then
+decode steps are replayed from one captured hipGraph.  W untimed warmup steps,
+then EXACTLY K timed decode steps bracketed by barrier + synchronize; the
+slowest rank's time is reported.  Every timed step runs the full model
+(32 layers + lm_head + argmax) for the whole batch.
+
+    python bench.py --gpus 1 --steps 64 --warmup 8
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+# reference's closest published single-request 7B-class decode number:
+# vLLM output token throughput, Qwen2.5-7B, 1 request, 1024 in / 512 out,
+# Intel Arc (docs/mddocs/DockerGuides/vllm_docker_quickstart.md:236)
+BASELINE_TOK_S = 30.01
+
+
+def llama3_8b_config():
+    from transformers import LlamaConfig
+    return LlamaConfig(
+        vocab_size=128256, hidden_size=4096, intermediate_size=14336, num_hidden_layers=32,
+        num_attention_heads=32, num_key_value_heads=8, max_position_embeddings=131072,
+        rms_norm_eps=1e-5, tie_word_embeddings=False,
+        rope_parameters={"rope_type": "llama3", "rope_theta": 500000.0, "factor": 8.0,
+                         "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                         "original_max_position_embeddings": 8192},
+    )
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "8")))
+    ap.add_argument("--prompt-len", type=int, default=1024)
+    ap.add_argument("--qtype", default="sym_int4")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--layers", type=int, default=None, help="debug only: fewer layers (invalid for the metric)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import ipex_llm_amd.ops as ops
+    ops.require()
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.engine.runner import Engine, DecodeStep
+    from ipex_llm_amd.models.cache import SequenceState
+
+    cfg = llama3_8b_config()
+    if args.layers:
+        cfg.num_hidden_layers = args.layers
+    t_build = time.perf_counter()
+    model = random_native_model(cfg, args.qtype, dev, torch.bfloat16, seed=1234 + rank)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t_build
+
+    B, P = args.batch, args.prompt_len
+    max_len = P + args.warmup + args.steps + 8
+    eng = Engine(model)
+    eng._ensure_cache(B, max_len)
+    g = torch.Generator().manual_seed(7 + rank)
+    prompts = torch.randint(0, cfg.vocab_size, (B, P), generator=g)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # ---- first-token latency (prefill of the whole batch + first token),
+    # 1 warm-up + 3 trials (reference all-in-one harness semantics)
+    nblk = (max_len + eng.block_size - 1) // eng.block_size
+    ftl = []
+    for trial in range(4):
+        eng.cache.allocator = type(eng.cache.allocator)(eng.cache.num_blocks)
+        seqs = [SequenceState(eng.cache.allocator.alloc(nblk)) for _ in range(B)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        first = []
+        for b in range(B):
+            lg = eng.prefill(seqs[b], prompts[b])
+            first.append(torch.argmax(lg, -1))
+        cur = torch.cat(first)
+        torch.cuda.synchronize()
+        if trial:
+            ftl.append((time.perf_counter() - t0) * 1e3)
+
+    # ---- decode: graph-captured step, W warmup + K timed
+    st = eng.decode_step_obj(seqs, max_len, greedy=True, use_graph=not args.no_graph)
+    st.set_state(cur, torch.tensor([s.length for s in seqs], device=dev))
+    for _ in range(args.warmup):
+        st.step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st.step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tok = st.next_ids.clone()
+
+    t = torch.tensor([dt, sum(ftl) / len(ftl)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt, ftl_ms = t.tolist()
+    ms_step = dt / args.steps * 1e3
+    value = B * world * args.steps / dt
+    if rank == 0:
+        out = {
+            "metric": "decode tokens/sec + first-token latency, Llama-3-8B INT4 at 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": round(value / BASELINE_TOK_S, 2), "dtype": "bf16",
+            "data": "synthetic (random prompt ids, random-init weights of the Llama-3-8B architecture)",
+            "config": {"model": "Llama-3-8B", "qtype": args.qtype, "global_batch": B * world,
+                       "batch_per_gpu": B, "seq_len": P, "parallelism": f"dp{world}",
+                       "hipgraph": not args.no_graph, "layers": cfg.num_hidden_layers},
+            "first_token_latency_ms": round(ftl_ms, 2),
+            "decode_ms_per_token": round(ms_step, 4),
+            "per_sequence_tokens_per_s": round(1e3 / ms_step, 2),
+            "baseline": {"value": BASELINE_TOK_S, "source": "vllm_docker_quickstart.md:236 (Qwen2.5-7B, 1 req, Arc)"},
+            "build_s": round(t_build, 1), "sample_next_ids": tok[:4].tolist(),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,103 @@
+"""In-tree build of the native library ``ipex_llm_amd/_C.so``.
+
+Three kinds of translation units, compiled in parallel:
+  * ``csrc/hip/*.hip``   gfx950 kernels       -> hipcc --offload-arch=gfx950
+  * ``csrc/cpu/*.cpp``   host quantizers/GEMM -> g++ -O3 -fopenmp (no torch)
+  * ``csrc/torch/*.cpp`` torch.library ops    -> hipcc (host C++, torch headers)
+and linked into one shared object loaded with ``torch.ops.load_library``.
+Objects are cached under ``build/obj`` and rebuilt when the source or any
+header under ``csrc`` is newer.  Usage: ``python -m ipex_llm_amd._build``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+import time
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OBJ = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(PKG, "_C.so")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+
+
+def _torch_paths():
+    import torch  # noqa: F401  (import only for the paths)
+    tdir = os.path.dirname(torch.__file__)
+    return (os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include"),
+            os.path.join(tdir, "lib"))
+
+
+def _headers_mtime() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True) + \
+        glob.glob(os.path.join(CSRC, "**", "*.cuh"), recursive=True)
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _cmd(src: str, obj: str):
+    tinc, tapi, _ = _torch_paths()
+    common = ["-O3", "-fPIC", "-std=c++17", "-I", CSRC]
+    if src.endswith(".hip"):
+        return [HIPCC, f"--offload-arch={ARCH}", "-Wno-pass-failed", *common, "-c", src, "-o", obj]
+    if "/cpu/" in src:
+        return ["g++", *common, "-fopenmp", "-march=x86-64-v3", "-c", src, "-o", obj]
+    pyinc = sysconfig.get_paths()["include"]
+    return [HIPCC, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-D_GLIBCXX_USE_CXX11_ABI=1",
+            "-Wno-unused-result", "-Wno-deprecated-declarations",
+            "-I", tinc, "-I", tapi, "-I", pyinc, "-c", src, "-o", obj]
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")) +
+                  glob.glob(os.path.join(CSRC, "cpu", "*.cpp")) +
+                  glob.glob(os.path.join(CSRC, "torch", "*.cpp")))
+
+
+def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    hdr = _headers_mtime()
+    todo, objs = [], []
+    for src in sources():
+        rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
+        obj = os.path.join(OBJ, rel + ".o")
+        objs.append(obj)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
+            todo.append((src, obj))
+    jobs = jobs or min(8, max(1, (os.cpu_count() or 4)))
+    t0 = time.time()
+    if todo:
+        def run(so):
+            src, obj = so
+            cmd = _cmd(src, obj)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+            if verbose:
+                print(f"[build] {os.path.relpath(src, ROOT)}", flush=True)
+            return src
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(run, todo))
+    need_link = todo or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs)
+    if need_link:
+        _, _, tlib = _torch_paths()
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB + ".tmp",
+               f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip", "-fopenmp",
+               f"-Wl,-rpath,{tlib}"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(LIB + ".tmp", LIB)
+    if verbose:
+        print(f"[build] {LIB} ({len(todo)} objects rebuilt, {time.time() - t0:.1f}s)", flush=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True, force="--force" in sys.argv)

@@ -1,0 +1,468 @@
+// Decode / short-query attention over a paged KV cache (flash-decoding).
+//
+// Reference ops: xe_addons.sdp / sdp_fp8 (decode, q_len <= 32, native GQA;
+// models/common.py:250-286), gemma2_sdp (softcap, sliding window;
+// models/gemma2.py:133-155) and the vLLM-XPU paged_attention_v1/v2 GQA
+// kernels (VLLM_PATCH:3380-3460).
+//
+// MI355X design: one wave64 per (batch, kv-head, 64-key split).  All query
+// rows that share the kv head (GQA group x new tokens, R <= 16) are handled
+// by the same wave, so every K/V byte is read from HBM once.  QK^T: lane =
+// key, the K row is streamed in 16-B pieces and dotted against the q rows
+// held in LDS (broadcast reads).  Softmax per row with wave64 shuffles.  PV:
+// lane = head dim, V rows are read coalesced (one row per wave instruction).
+// Per-split (m, l, o) partials are merged by a second small kernel.  Sequence
+// lengths and block tables are device tensors: the launch geometry depends
+// only on the max length bucket, so the whole thing is hipGraph-capturable.
+#include "../common/quant_block.h"
+#include "illm_device.h"
+#include "kernels.h"
+
+namespace illm {
+
+constexpr int SPLIT = 64;
+constexpr int RMAX = 16;
+
+template <typename T, int KVF>
+__device__ __forceinline__ void kv_load8(const uint8_t* p, float scale, float* v) {
+  if constexpr (KVF == 0) {
+    uint4 u = *(const uint4*)p;
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      v[2 * i] = to_f32<T>(w[i] & 0xffff);
+      v[2 * i + 1] = to_f32<T>(w[i] >> 16);
+    }
+  } else {
+    uint2 u = *(const uint2*)p;
+    uint32_t w[2] = {u.x, u.y};
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      auto f0 = KVF == 1 ? __builtin_amdgcn_cvt_pk_f32_bf8(w[i], false) : __builtin_amdgcn_cvt_pk_f32_fp8(w[i], false);
+      auto f1 = KVF == 1 ? __builtin_amdgcn_cvt_pk_f32_bf8(w[i], true) : __builtin_amdgcn_cvt_pk_f32_fp8(w[i], true);
+      v[4 * i + 0] = f0[0] * scale;
+      v[4 * i + 1] = f0[1] * scale;
+      v[4 * i + 2] = f1[0] * scale;
+      v[4 * i + 3] = f1[1] * scale;
+    }
+  }
+}
+
+template <typename T, int KVF>
+__device__ __forceinline__ float kv_load1(const uint8_t* base, size_t idx, float scale) {
+  if constexpr (KVF == 0) return to_f32<T>(((const uint16_t*)base)[idx]);
+  else if constexpr (KVF == 1) return hd_e5m2_to_f32(base[idx]) * scale;
+  else return hd_e4m3_to_f32(base[idx]) * scale;
+}
+
+template <typename T, int D, int KVF>
+__global__ void __launch_bounds__(64) attn_decode_kernel(const AttnDecodeArgs a) {
+  constexpr int EB = KVF == 0 ? 2 : 1;  // bytes per cached element
+  constexpr int DV = (D + 63) / 64;     // head dims per lane in PV
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x;
+  const int len = a.seq_lens[b];
+  const int k0 = split * SPLIT;
+  if (k0 >= len) return;
+  const int group = a.Hq / a.Hkv;
+  const int R = group * a.Tq;  // rows: r = t * group + gi
+
+  __shared__ float qs[RMAX][D];
+  __shared__ float ps[RMAX][SPLIT];
+
+  // q rows of this kv head -> LDS (f32)
+  for (int i = lane; i < R * D; i += 64) {
+    const int r = i / D, d = i % D;
+    const int t = r / group, h = kvh * group + r % group;
+    qs[r][d] = to_f32<T>(a.q[(((size_t)b * a.Tq + t) * a.Hq + h) * D + d]);
+  }
+  __syncthreads();
+
+  const int blk = a.block_tables[(size_t)b * a.max_blocks + k0 / a.bs];
+  const size_t base = (((size_t)blk * a.Hkv + kvh) * a.bs + (k0 % a.bs)) * D;
+  const uint8_t* kb = a.k_cache + base * EB;
+  const uint8_t* vb = a.v_cache + base * EB;
+
+  // ---- S = q k^T : lane = key
+  const int key = k0 + lane;
+  const bool kin = key < len;
+  float s[RMAX];
+#pragma unroll
+  for (int r = 0; r < RMAX; r++) s[r] = 0.f;
+  if (kin) {
+    const uint8_t* krow = kb + (size_t)lane * D * EB;
+#pragma unroll 4
+    for (int c = 0; c < D; c += 8) {
+      float kv[8];
+      kv_load8<T, KVF>(krow + c * EB, a.k_scale, kv);
+#pragma unroll
+      for (int r = 0; r < RMAX; r++) {
+        if (r < R) {
+          float acc = s[r];
+#pragma unroll
+          for (int i = 0; i < 8; i++) acc += qs[r][c + i] * kv[i];
+          s[r] = acc;
+        }
+      }
+    }
+  }
+  const int qpos0 = len - a.Tq;  // absolute position of query token 0
+#pragma unroll
+  for (int r = 0; r < RMAX; r++) {
+    if (r >= R) break;
+    const int t = r / group, h = kvh * group + r % group;
+    const int qpos = qpos0 + t;
+    float v = s[r] * a.scale;
+    if (a.softcap > 0.f) v = a.softcap * tanhf(v / a.softcap);
+    if (a.alibi) v += a.alibi[h] * (float)key;
+    bool ok = kin && key <= qpos;
+    if (a.sliding_window > 0 && key <= qpos - a.sliding_window) ok = false;
+    s[r] = ok ? v : -INFINITY;
+  }
+
+  // ---- softmax pieces per row
+  float m[RMAX], l[RMAX];
+#pragma unroll
+  for (int r = 0; r < RMAX; r++) {
+    if (r >= R) break;
+    m[r] = wave_max(s[r]);
+    const float p = m[r] == -INFINITY ? 0.f : __expf(s[r] - m[r]);
+    l[r] = wave_sum(p);
+    ps[r][lane] = p;
+  }
+  __syncthreads();
+
+  // ---- O = P V : lane = head dim
+  float o[RMAX][DV];
+#pragma unroll
+  for (int r = 0; r < RMAX; r++)
+#pragma unroll
+    for (int j = 0; j < DV; j++) o[r][j] = 0.f;
+  const int nk = min(SPLIT, len - k0);
+  for (int kk = 0; kk < nk; kk++) {
+    float vv[DV];
+#pragma unroll
+    for (int j = 0; j < DV; j++) {
+      const int d = lane + 64 * j;
+      vv[j] = (d < D) ? kv_load1<T, KVF>(vb, (size_t)kk * D + d, a.v_scale) : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < RMAX; r++) {
+      if (r < R) {
+        const float p = ps[r][kk];
+#pragma unroll
+        for (int j = 0; j < DV; j++) o[r][j] += p * vv[j];
+      }
+    }
+  }
+
+  // ---- partials
+#pragma unroll
+  for (int r = 0; r < RMAX; r++) {
+    if (r >= R) break;
+    const int t = r / group, h = kvh * group + r % group;
+    const size_t row = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit + split;
+#pragma unroll
+    for (int j = 0; j < DV; j++) {
+      const int d = lane + 64 * j;
+      if (d < D) a.part_o[row * D + d] = o[r][j];
+    }
+    if (lane == 0) {
+      a.part_ml[row * 2] = m[r];
+      a.part_ml[row * 2 + 1] = l[r];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// v2: MFMA flash-decoding for D in {64, 128, 256}.  One wave per 64-key split.
+// Every K and V byte of the split is requested up front (16 + 16 x 16-B
+// loads per lane, 1 KiB per wave instruction), so the wave pays one memory
+// latency instead of one per key.
+//   S^T = K Q^T on 16x16x32 MFMA: A = K rows (key on the lane, 16 B of one
+//   key row per lane straight from HBM), B = Q^T (query row on the lane).
+//   The result puts (key = 16 kt + 4 g + i, row = lane & 15) in registers,
+//   so the softmax row max/sum is a 16-value register reduction + 2 shuffles.
+//   O = P V on the VALU: lane (dg = lane & 15, kg = lane >> 4) owns D/16
+//   head dims of 16 keys; P comes back through 4 KiB of LDS; the 4 key
+//   groups are summed with 2 shuffles.
+// ---------------------------------------------------------------------------
+template <typename T, int KVF>
+__device__ __forceinline__ uint4 kv_frag8(const uint8_t* p) {
+  // 8 cached elements -> 8 x 16-bit A/B fragment (f32 scale applied later)
+  if constexpr (KVF == 0) {
+    return *(const uint4*)p;
+  } else {
+    const uint2 u = *(const uint2*)p;
+    uint4 r;
+    constexpr bool BF = std::is_same<T, BF16>::value;
+    if constexpr (KVF == 1) {
+      if constexpr (BF) {
+        r.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(u.x, 1.0f, false));
+        r.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(u.x, 1.0f, true));
+        r.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(u.y, 1.0f, false));
+        r.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(u.y, 1.0f, true));
+      } else {
+        r.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(u.x, 1.0f, false));
+        r.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(u.x, 1.0f, true));
+        r.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(u.y, 1.0f, false));
+        r.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(u.y, 1.0f, true));
+      }
+    } else {
+      if constexpr (BF) {
+        r.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(u.x, 1.0f, false));
+        r.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(u.x, 1.0f, true));
+        r.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(u.y, 1.0f, false));
+        r.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(u.y, 1.0f, true));
+      } else {
+        r.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(u.x, 1.0f, false));
+        r.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(u.x, 1.0f, true));
+        r.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(u.y, 1.0f, false));
+        r.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(u.y, 1.0f, true));
+      }
+    }
+    return r;
+  }
+}
+
+template <typename T, int D, int KVF, int RT>
+__global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs a) {
+  constexpr int EB = KVF == 0 ? 2 : 1;
+  constexpr int KSTEP = D / 32;       // MFMA k-steps over the head dim
+  constexpr int DPL = D / 16;         // head dims per lane in P.V
+  constexpr int VCH = DPL / 8 > 0 ? DPL / 8 : 1;  // 8-element fragments per key per lane
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
+  const int len = a.seq_lens[b];
+  const int k0 = split * SPLIT;
+  if (k0 >= len) return;
+  const int nk = min(SPLIT, len - k0);
+  const int group = a.Hq / a.Hkv;
+  const int R = group * a.Tq;
+
+  __shared__ float ps[SPLIT][RT];
+
+  const int blk = a.block_tables[(size_t)b * a.max_blocks + k0 / a.bs];
+  const size_t base = (((size_t)blk * a.Hkv + kvh) * a.bs + (k0 % a.bs)) * D;
+  const uint8_t* kb = a.k_cache + base * EB;
+  const uint8_t* vb = a.v_cache + base * EB;
+
+  // ---- issue every load of the split
+  uint4 kf[4][KSTEP];
+#pragma unroll
+  for (int kt = 0; kt < 4; kt++) {
+    const int kk = min(kt * 16 + r16, nk - 1);
+#pragma unroll
+    for (int s = 0; s < KSTEP; s++) kf[kt][s] = kv_frag8<T, KVF>(kb + ((size_t)kk * D + 32 * s + 8 * g) * EB);
+  }
+  const int dg = r16, kg = g;
+  uint4 vf[16][VCH];
+  if constexpr (DPL >= 8) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int kk = min(4 * i + kg, nk - 1);
+#pragma unroll
+      for (int c = 0; c < VCH; c++) vf[i][c] = kv_frag8<T, KVF>(vb + ((size_t)kk * D + DPL * dg + 8 * c) * EB);
+    }
+  }
+  uint4 qf[KSTEP];
+  {
+    const int row = r16 < R ? r16 : 0;
+    const int t = row / group, h = kvh * group + row % group;
+    const uint16_t* qr = a.q + (((size_t)b * a.Tq + t) * a.Hq + h) * D;
+#pragma unroll
+    for (int s = 0; s < KSTEP; s++) {
+      uint4 v = *(const uint4*)(qr + 32 * s + 8 * g);
+      qf[s] = r16 < R ? v : make_uint4(0, 0, 0, 0);
+    }
+  }
+
+  // ---- S^T tiles: lane holds (key = 16 kt + 4 g + i, row = r16)
+  f32x4 st[4];
+#pragma unroll
+  for (int kt = 0; kt < 4; kt++) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KSTEP; s++) acc = mfma16<T>(kf[kt][s], qf[s], acc);
+    st[kt] = acc;
+  }
+  const int row = r16;
+  const int t = row / group;
+  const int h = kvh * group + (row % group);
+  const int qpos = len - a.Tq + t;
+  const float sc = a.scale * (KVF ? a.k_scale : 1.f);
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 4; kt++) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int kk = kt * 16 + 4 * g + i;
+      const int key = k0 + kk;
+      float v = st[kt][i] * sc;
+      if (a.softcap > 0.f) v = a.softcap * tanhf(v / a.softcap);
+      if (a.alibi && row < R) v += a.alibi[h] * (float)key;
+      bool ok = row < R && kk < nk && key <= qpos;
+      if (a.sliding_window > 0 && key <= qpos - a.sliding_window) ok = false;
+      v = ok ? v : -INFINITY;
+      st[kt][i] = v;
+      m = fmaxf(m, v);
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 4; kt++) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const float p = m == -INFINITY ? 0.f : __expf(st[kt][i] - m);
+      l += p;
+      if (row < RT) ps[kt * 16 + 4 * g + i][row] = p;
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  __syncthreads();
+
+  // ---- O = P V: lane (dg, kg) owns dims [DPL*dg, DPL*dg + DPL) of keys 4i + kg
+  float o[RT][DPL];
+#pragma unroll
+  for (int r = 0; r < RT; r++)
+#pragma unroll
+    for (int d = 0; d < DPL; d++) o[r][d] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int kk = 4 * i + kg;
+    float v[DPL];
+    if constexpr (DPL >= 8) {
+#pragma unroll
+      for (int c = 0; c < VCH; c++) {
+        const uint32_t w[4] = {vf[i][c].x, vf[i][c].y, vf[i][c].z, vf[i][c].w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          v[8 * c + 2 * e] = to_f32<T>(w[e] & 0xffff);
+          v[8 * c + 2 * e + 1] = to_f32<T>(w[e] >> 16);
+        }
+      }
+    } else {
+      const int kc = min(kk, nk - 1);
+#pragma unroll
+      for (int d = 0; d < DPL; d++) v[d] = kv_load1<T, KVF>(vb, (size_t)kc * D + DPL * dg + d, 1.f);
+    }
+#pragma unroll
+    for (int r = 0; r < RT; r++) {
+      const float p = ps[kk][r];
+#pragma unroll
+      for (int d = 0; d < DPL; d++) o[r][d] += p * v[d];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RT; r++)
+#pragma unroll
+    for (int d = 0; d < DPL; d++) {
+      float x = o[r][d];
+      x += __shfl_xor(x, 16, 64);
+      x += __shfl_xor(x, 32, 64);
+      o[r][d] = x;
+    }
+  const float vs = KVF ? a.v_scale : 1.f;
+  if (kg == 0) {
+#pragma unroll
+    for (int r = 0; r < RT; r++) {
+      if (r < R) {
+        const int tt = r / group, hh = kvh * group + r % group;
+        const size_t prow = (((size_t)b * a.Hq + hh) * a.Tq + tt) * a.nsplit + split;
+        float* po = a.part_o + prow * D + DPL * dg;
+#pragma unroll
+        for (int d = 0; d < DPL; d += 4)
+          *(float4*)(po + d) = make_float4(o[r][d] * vs, o[r][d + 1] * vs, o[r][d + 2] * vs, o[r][d + 3] * vs);
+      }
+    }
+  }
+  if (g == 0 && row < R) {
+    const size_t prow = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit + split;
+    a.part_ml[prow * 2] = m;
+    a.part_ml[prow * 2 + 1] = l;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) attn_combine_kernel(const AttnDecodeArgs a) {
+  const int h = blockIdx.x, t = blockIdx.y, b = blockIdx.z, lane = threadIdx.x;
+  const int len = a.seq_lens[b];
+  const int ns = min(a.nsplit, (len + SPLIT - 1) / SPLIT);
+  const size_t row0 = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit;
+  // split weights computed lane-parallel (all loads in flight together), kept
+  // in LDS; then every lane sums its head dims with independent loads.
+  __shared__ float wsh[1024];
+  float M = -INFINITY;
+  for (int s = lane; s < ns; s += 64) M = fmaxf(M, a.part_ml[(row0 + s) * 2]);
+  M = wave_max(M);
+  float L = 0.f;
+  for (int s = lane; s < ns; s += 64) {
+    const float2 ml = *(const float2*)(a.part_ml + (row0 + s) * 2);
+    const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
+    L += w * ml.y;
+    if (s < 1024) wsh[s] = w;
+  }
+  L = wave_sum(L);
+  __syncthreads();
+  const float invL = L > 0.f ? 1.f / L : 0.f;
+  uint16_t* out = a.out + (((size_t)b * a.Tq + t) * a.Hq + h) * a.D;
+  const float* po = a.part_o + row0 * a.D;
+  for (int d = lane; d < a.D; d += 64) {
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+    int s = 0;
+    for (; s + 4 <= ns; s += 4) {
+      const float v0 = po[(size_t)(s + 0) * a.D + d], v1 = po[(size_t)(s + 1) * a.D + d];
+      const float v2 = po[(size_t)(s + 2) * a.D + d], v3 = po[(size_t)(s + 3) * a.D + d];
+      acc0 += wsh[s] * v0;
+      acc1 += wsh[s + 1] * v1;
+      acc2 += wsh[s + 2] * v2;
+      acc3 += wsh[s + 3] * v3;
+    }
+    for (; s < ns; s++) acc0 += wsh[s] * po[(size_t)s * a.D + d];
+    out[d] = from_f32<T>((acc0 + acc1 + acc2 + acc3) * invL);
+  }
+}
+
+template <typename T, int D, int RT>
+static void launch_v2(const AttnDecodeArgs& a, hipStream_t st) {
+  dim3 grid(a.nsplit, a.Hkv, a.B);
+  if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT>), grid, dim3(64), 0, st, a);
+  else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT>), grid, dim3(64), 0, st, a);
+  else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT>), grid, dim3(64), 0, st, a);
+  hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
+}
+
+template <typename T, int D>
+static void launch_d(const AttnDecodeArgs& a, hipStream_t st) {
+  const int R = (a.Hq / a.Hkv) * a.Tq;
+  if constexpr (D == 64 || D == 128 || D == 256) {
+    if (R <= 4) return launch_v2<T, D, 4>(a, st);
+    if (R <= 8) return launch_v2<T, D, 8>(a, st);
+    if (D <= 128) return launch_v2<T, D, 16>(a, st);
+  }
+  dim3 grid(a.nsplit, a.Hkv, a.B);
+  if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_kernel<T, D, 1>), grid, dim3(64), 0, st, a);
+  else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_kernel<T, D, 2>), grid, dim3(64), 0, st, a);
+  else hipLaunchKernelGGL((attn_decode_kernel<T, D, 0>), grid, dim3(64), 0, st, a);
+  hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
+}
+
+template <typename T>
+static void launch_t(const AttnDecodeArgs& a, hipStream_t st) {
+  switch (a.D) {
+    case 64: launch_d<T, 64>(a, st); break;
+    case 80: launch_d<T, 80>(a, st); break;
+    case 96: launch_d<T, 96>(a, st); break;
+    case 128: launch_d<T, 128>(a, st); break;
+    case 256: launch_d<T, 256>(a, st); break;
+  }
+}
+
+void launch_attn_decode(bool bf16, const AttnDecodeArgs& a, hipStream_t st) {
+  if (bf16) launch_t<BF16>(a, st); else launch_t<F16>(a, st);
+}
+
+}  // namespace illm

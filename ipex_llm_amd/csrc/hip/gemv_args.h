@@ -1,0 +1,56 @@
+// Host/device-shared argument block and enums of the low-bit GEMV
+// (lowbit_gemv.cuh).  No device code: included by the torch op wrappers.
+#pragma once
+#include <stdint.h>
+
+#include "../common/formats.h"
+
+namespace illm {
+
+enum GemvEpi : int { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_GLU = 2 };
+enum DecKind : int {
+  DK_INT4S = 0,  // sym_int4 / woq_int4
+  DK_INT4A = 1,  // asym_int4
+  DK_LUT4 = 2,   // nf4 / nf3 (LDS pair table)
+  DK_FP4 = 3,    // fp4 e2m1 (hardware converter)
+  DK_INT8S = 4,  // sym_int8 / sym_int5 (signed byte)
+  DK_INT8A = 5,  // asym_int5 (unsigned byte + min)
+  DK_FP8E4 = 6,  // fp8_e4m3 / fp6 (e3m2 grid stored as e4m3)
+  DK_FP8E5 = 7,  // fp8_e5m2
+};
+
+// constexpr functions are implicitly host+device under clang HIP
+constexpr int dk_bits(int dk) { return dk <= DK_FP4 ? 4 : 8; }
+constexpr bool dk_has_min(int dk) { return dk == DK_INT4A || dk == DK_INT8A; }
+constexpr bool dk_needx(int dk) {
+  return dk == DK_INT4S || dk == DK_INT4A || dk == DK_INT8S || dk == DK_INT8A;
+}
+inline int fmt_to_dk(int fmt) {
+  switch (fmt) {
+    case FMT_SYM_INT4: return DK_INT4S;
+    case FMT_ASYM_INT4: return DK_INT4A;
+    case FMT_NF4: case FMT_NF3: return DK_LUT4;
+    case FMT_FP4: return DK_FP4;
+    case FMT_SYM_INT8: case FMT_SYM_INT5: return DK_INT8S;
+    case FMT_ASYM_INT5: return DK_INT8A;
+    case FMT_FP8E4: case FMT_FP6: return DK_FP8E4;
+    case FMT_FP8E5: return DK_FP8E5;
+  }
+  return -1;
+}
+
+struct GemvArgs {
+  const uint16_t* x;  // [M, ldx] activations (bf16/f16 bits)
+  int M, K, ldx;
+  const uint8_t* codes;    // device blob code plane
+  const uint16_t* scales;  // device blob scale plane (fp16)
+  const uint16_t* mins;    // device blob min plane (fp16) or null
+  int N, KC;               // logical out features, K chunks (Kp / 128)
+  void* out;               // EPI_STORE/GLU: T [M, ldo]; EPI_PARTIAL: f32 [ks][M][N]
+  int ldo;
+  const uint16_t* bias;    // T [N] or null (EPI_STORE only)
+  int act;                 // EPI_GLU: 0 = silu, 1 = gelu(tanh)
+  int lut_fmt;             // DK_LUT4: FMT_NF4 / FMT_NF3
+};
+
+}  // namespace illm

@@ -1,0 +1,102 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+// Wave64 everywhere: lane = threadIdx.x & 63.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "../common/formats.h"
+
+namespace illm {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// dtype tags: activations travel as raw 16-bit patterns
+struct BF16 {};
+struct F16 {};
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  // round-to-nearest-even; NaN stays NaN (hipcc lowers the cast to v_cvt_pk_bf16_f32)
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t v) {
+  return (float)__builtin_bit_cast(_Float16, v);
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
+
+template <typename T> __device__ __forceinline__ float to_f32(uint16_t v);
+template <> __device__ __forceinline__ float to_f32<BF16>(uint16_t v) { return bf16_to_f32(v); }
+template <> __device__ __forceinline__ float to_f32<F16>(uint16_t v) { return f16_to_f32(v); }
+template <typename T> __device__ __forceinline__ uint16_t from_f32(float f);
+template <> __device__ __forceinline__ uint16_t from_f32<BF16>(float f) { return f32_to_bf16(f); }
+template <> __device__ __forceinline__ uint16_t from_f32<F16>(float f) { return f32_to_f16(f); }
+
+// pack two f32 into one dword of two 16-bit values (lo = a)
+template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b);
+template <> __device__ __forceinline__ uint32_t pack2<BF16>(float a, float b) {
+  return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+}
+template <> __device__ __forceinline__ uint32_t pack2<F16>(float a, float b) {
+  return (uint32_t)f32_to_f16(a) | ((uint32_t)f32_to_f16(b) << 16);
+}
+
+// 16x16x32 MFMA on raw 16-byte fragments
+template <typename T>
+__device__ __forceinline__ f32x4 mfma16(const uint4& a, const uint4& b, f32x4 c);
+template <>
+__device__ __forceinline__ f32x4 mfma16<BF16>(const uint4& a, const uint4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma16<F16>(const uint4& a, const uint4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// wave-level reductions (wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-level sum for blockDim.x == NT (multiple of 64); smem >= NT/64 floats
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* smem) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (NT == 64) return v;
+  __syncthreads();
+  if (l == 0) smem[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) t += smem[i];
+  return t;
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float gelu_tanh_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+}  // namespace illm
+
+#define ILLM_CHECK_LAUNCH() (void)hipGetLastError()

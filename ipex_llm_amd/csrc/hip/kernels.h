@@ -1,0 +1,94 @@
+// Host-callable launchers of the gfx950 kernels.  Implemented in the .hip
+// files of this directory; called from the torch op wrappers
+// (csrc/torch/ops_hip.cpp).  Pure HIP API: no torch headers here, so the
+// kernel translation units compile in seconds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace illm {
+
+}  // namespace illm
+#include "gemv_args.h"
+namespace illm {
+
+// ---- low-bit GEMV / skinny GEMM (lowbit_gemv.cuh) -------------------------
+// dk = decoder kind (fmt_to_dk), mt = ceil(M/16) in {1,2,4}
+template <int DK>
+void launch_gemv_dk(bool bf16, int mt, int epi, dim3 grid, const GemvArgs& a, hipStream_t st);
+// v2 (M <= 16, x staged in LDS): grid = (ceil(NT / (4 * TPW)), ksplit), shmem = M * (Kwg + 8) * 2
+template <int DK>
+void launch_gemv2_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
+
+// ---- norms (norm.hip) ------------------------------------------------------
+struct NormArgs {
+  const uint16_t* x;       // [M, H] input (ignored when partials != null)
+  const float* partials;   // [nsplit, M, H] f32 GEMV partial slabs or null
+  int nsplit;
+  uint16_t* residual;      // [M, H] residual stream (in/out) or null
+  const uint16_t* w;       // [H]
+  uint16_t* out;           // [M, H]
+  int M, H;
+  float eps;
+  int unit_offset;         // gemma: x * (1 + w)
+  int store_residual;
+};
+void launch_add_rms_norm(bool bf16, const NormArgs& a, hipStream_t st);
+void launch_layer_norm(bool bf16, const uint16_t* x, const uint16_t* w, const uint16_t* b,
+                       uint16_t* out, int M, int H, float eps, hipStream_t st);
+
+// ---- rotary embedding + KV-cache append (rope_kv.hip) --------------------
+struct RopeKVArgs {
+  const uint16_t* qkv;     // [T, (Hq + 2 Hkv) * D] fused projection output
+  int ld_qkv;
+  uint16_t* q_out;         // [T, Hq, D]
+  uint8_t* k_cache;        // paged cache [nblocks, Hkv, bs, D] (elem = kv_bytes)
+  uint8_t* v_cache;
+  const int64_t* slots;    // [T] cache slot = block * bs + offset; <0 = skip
+  const int64_t* pos;      // [T] rotary position
+  const float* inv_freq;   // [rot_dim / 2]  (used when cos_sin is null)
+  const float* cos_sin;    // [max_pos, rot_dim / 2, 2] precomputed f32 table or null
+  const uint16_t* q_norm;  // [D] per-head RMSNorm weight (qwen3) or null
+  const uint16_t* k_norm;
+  float norm_eps;
+  float attn_scale_q;      // multiply q by this (1.0 = none)
+  int T, Hq, Hkv, D, rot_dim, bs;
+  int interleaved;         // 0 = rotate_half (NeoX/llama), 1 = pairwise (GPT-J/GLM)
+  int kv_fp8;              // 0 = same dtype as activations, 1 = fp8 e5m2, 2 = fp8 e4m3
+  float k_scale, v_scale;  // fp8 KV scales (value = code * scale)
+};
+void launch_rope_kv(bool bf16, const RopeKVArgs& a, hipStream_t st);
+
+// ---- decode / short-query attention (attention.hip) -----------------------
+struct AttnDecodeArgs {
+  const uint16_t* q;        // [B, Tq, Hq, D]
+  const uint8_t* k_cache;   // [nblocks, Hkv, bs, D]
+  const uint8_t* v_cache;
+  const int32_t* block_tables;  // [B, max_blocks]
+  const int32_t* seq_lens;      // [B] total keys incl. the Tq new ones
+  int max_blocks;
+  float* part_o;            // [B, Hq, Tq, nsplit, D]
+  float* part_ml;           // [B, Hq, Tq, nsplit, 2]
+  uint16_t* out;            // [B, Tq, Hq, D]
+  int B, Tq, Hq, Hkv, D, bs, nsplit;
+  float scale, softcap;     // softcap > 0: gemma2 tanh soft-capping
+  int sliding_window;       // > 0: attend to the last W keys only
+  int kv_fp8;
+  float k_scale, v_scale;
+  const float* alibi;       // [Hq] slopes or null
+};
+void launch_attn_decode(bool bf16, const AttnDecodeArgs& a, hipStream_t st);
+
+// ---- elementwise & misc (misc.hip) ------------------------------------------
+void launch_glu(bool bf16, const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act,
+                hipStream_t st);
+void launch_quantize_device(int fmt, int in_kind, const void* w, int64_t n, int64_t k,
+                            uint8_t* blob, int search, hipStream_t st);
+void launch_dequantize_device(bool bf16, int fmt, const uint8_t* blob, int64_t n, int64_t k,
+                              uint16_t* out, hipStream_t st);
+void launch_reduce_partials(bool bf16, const float* ws, int nsplit, const uint16_t* bias,
+                            uint16_t* out, int M, int N, int ldo, hipStream_t st);
+void launch_moe_topk(const float* logits, int T, int E, int k, int renorm, int scoring,
+                     float* topk_w, int32_t* topk_ids, hipStream_t st);
+
+}  // namespace illm

@@ -1,0 +1,543 @@
+// Low-bit weight x bf16/f16 activation "skinny GEMM" for M <= 64 rows
+// (decode, batched decode, speculative verify) on gfx950 MFMA.
+//
+// Reference op: xe_linear.forward_new / xe_batch.batch_forward /
+// xe_linear.mlp_forward_xpu (SRC/transformers/low_bit_linear.py:698-708,
+// models/common.py:146-161).  Design is MI355X-first:
+//   * weights are pre-tiled (formats.h) so one wave64 streams a 16-row x
+//     128-k chunk with ONE global_load_dwordx4 per lane (1 KiB per wave,
+//     fully coalesced); no LDS round trip for the weight stream;
+//   * dequant happens in registers straight into the MFMA A fragment
+//     (int4: the bf16 0x4300|q / f16 0x6400|q magic, fp4/fp8: the gfx950
+//     v_cvt_scalef32_pk_* converters, nf4: a 256-entry pair table in LDS);
+//   * the zero-point/offset of integer formats is folded in with one extra
+//     MFMA against an all-ones A fragment (sum of x per block) instead of
+//     per-element VALU subtracts;
+//   * per-64-block scales are applied on the 4 f32 accumulators per lane;
+//   * 4 waves per workgroup split K; partials are reduced through LDS; a
+//     workgroup-level split-K over blockIdx.y writes f32 partial slabs that
+//     are summed by the consumer (fused add+RMSNorm) kernel.
+#pragma once
+#include <type_traits>
+
+#include "../common/quant_block.h"
+#include "gemv_args.h"
+#include "illm_device.h"
+
+namespace illm {
+
+template <typename T> struct Magic;
+template <> struct Magic<BF16> {
+  static constexpr uint32_t k4 = 0x43004300u;  // bf16(128 + q)
+  static constexpr float off = 128.f;
+  static constexpr uint32_t one2 = 0x3F803F80u;
+};
+template <> struct Magic<F16> {
+  static constexpr uint32_t k4 = 0x64006400u;  // f16(1024 + q)
+  static constexpr float off = 1024.f;
+  static constexpr uint32_t one2 = 0x3C003C00u;
+};
+
+// ---- decoders: one 8-code group (k-step) -> 16-byte A fragment ------------
+template <int DK, typename T>
+__device__ __forceinline__ uint4 decode4(uint32_t u, const uint32_t* lut2) {
+  uint4 r;
+  if constexpr (DK == DK_INT4S || DK == DK_INT4A) {
+    r.x = (u & 0x000F000Fu) | Magic<T>::k4;
+    r.y = ((u >> 4) & 0x000F000Fu) | Magic<T>::k4;
+    r.z = ((u >> 8) & 0x000F000Fu) | Magic<T>::k4;
+    r.w = ((u >> 12) & 0x000F000Fu) | Magic<T>::k4;
+  } else if constexpr (DK == DK_FP4) {
+    if constexpr (std::is_same<T, BF16>::value) {
+      r.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(u, 1.0f, 0));
+      r.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(u, 1.0f, 1));
+      r.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(u, 1.0f, 2));
+      r.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(u, 1.0f, 3));
+    } else {
+      r.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 0));
+      r.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 1));
+      r.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 2));
+      r.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 3));
+    }
+  } else {  // DK_LUT4
+    r.x = lut2[u & 0xff];
+    r.y = lut2[(u >> 8) & 0xff];
+    r.z = lut2[(u >> 16) & 0xff];
+    r.w = lut2[u >> 24];
+  }
+  return r;
+}
+
+template <int DK, typename T>
+__device__ __forceinline__ uint32_t dec8_pair(uint32_t u, bool hi) {
+  if constexpr (DK == DK_FP8E4) {
+    if constexpr (std::is_same<T, BF16>::value)
+      return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(u, 1.0f, true)
+                                             : __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(u, 1.0f, false));
+    else
+      return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(u, 1.0f, true)
+                                             : __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(u, 1.0f, false));
+  } else if constexpr (DK == DK_FP8E5) {
+    if constexpr (std::is_same<T, BF16>::value)
+      return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(u, 1.0f, true)
+                                             : __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(u, 1.0f, false));
+    else
+      return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(u, 1.0f, true)
+                                             : __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(u, 1.0f, false));
+  } else {
+    // integer bytes: signed codes are biased by 128 (xor 0x80) so every code
+    // is an exact small non-negative integer in bf16/f16
+    if constexpr (DK == DK_INT8S) u ^= 0x80808080u;
+    const int sh = hi ? 16 : 0;
+    return pack2<T>((float)((u >> sh) & 0xff), (float)((u >> (sh + 8)) & 0xff));
+  }
+}
+
+// 8 bytes (two dwords) -> 16-byte A fragment
+template <int DK, typename T>
+__device__ __forceinline__ uint4 decode8(uint32_t lo, uint32_t hi) {
+  uint4 r;
+  r.x = dec8_pair<DK, T>(lo, false);
+  r.y = dec8_pair<DK, T>(lo, true);
+  r.z = dec8_pair<DK, T>(hi, false);
+  r.w = dec8_pair<DK, T>(hi, true);
+  return r;
+}
+
+// per-block coefficients: acc += cd * P + cx * X
+template <int DK, typename T>
+__device__ __forceinline__ void block_coef(float d, float m, float& cd, float& cx) {
+  cd = d;
+  if constexpr (DK == DK_INT4S) cx = -(Magic<T>::off + 8.f) * d;
+  else if constexpr (DK == DK_INT4A) cx = m - Magic<T>::off * d;
+  else if constexpr (DK == DK_INT8S) cx = -128.f * d;
+  else if constexpr (DK == DK_INT8A) cx = m;
+  else cx = 0.f;
+}
+
+template <int DK, typename T, int MT, int EPI>
+__global__ void __launch_bounds__(256) lowbit_gemv_kernel(const GemvArgs a) {
+  constexpr int BITS = dk_bits(DK);
+  constexpr bool NEEDX = dk_needx(DK);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  __shared__ float4 red[4][MT][64];
+  __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
+  if constexpr (DK == DK_LUT4) {
+    const int i = threadIdx.x;
+    lut2[i] = pack2<T>(hd_lut4(a.lut_fmt, i & 15), hd_lut4(a.lut_fmt, i >> 4));
+    __syncthreads();
+  }
+
+  int tile, wk, nwk;
+  if constexpr (EPI == EPI_GLU) {
+    tile = blockIdx.x * 2 + (wave >> 1);
+    wk = blockIdx.y * 2 + (wave & 1);
+    nwk = gridDim.y * 2;
+  } else {
+    tile = blockIdx.x;
+    wk = blockIdx.y * 4 + wave;
+    nwk = gridDim.y * 4;
+  }
+  const int cpw = (a.KC + nwk - 1) / nwk;
+  const int c0 = wk * cpw;
+  const int c1 = min(a.KC, c0 + cpw);
+
+  // activation row pointers (clamped, masked after load)
+  const uint16_t* xr[MT];
+  bool mok[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; mt++) {
+    int m = mt * 16 + r16;
+    mok[mt] = m < a.M;
+    xr[mt] = a.x + (size_t)(mok[mt] ? m : 0) * a.ldx;
+  }
+  const uint4 ones = make_uint4(Magic<T>::one2, Magic<T>::one2, Magic<T>::one2, Magic<T>::one2);
+
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; mt++) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const size_t tbase = (size_t)tile * a.KC;
+  // Software pipeline: a ring of PF chunks is always in flight.  Loads are
+  // issued unconditionally (clamped index: tail re-loads are L2 hits) so
+  // hipcc keeps counted vmcnt waits instead of branching around loads.
+  struct Chunk {
+    uint4 q0, q1, sc, mn;
+    uint4 xb[4][MT];
+  };
+  auto load_chunk = [&](Chunk& ch, int c) {
+    c = min(c, c1 - 1);
+    if constexpr (BITS == 4) {
+      ch.q0 = *(const uint4*)(a.codes + ((tbase + c) * 64 + lane) * 16);
+    } else {
+      ch.q0 = *(const uint4*)(a.codes + (((tbase + c) * 2 + 0) * 64 + lane) * 16);
+      ch.q1 = *(const uint4*)(a.codes + (((tbase + c) * 2 + 1) * 64 + lane) * 16);
+    }
+    ch.sc = *(const uint4*)(a.scales + (tbase + c) * 32 + g * 8);
+    if constexpr (dk_has_min(DK)) ch.mn = *(const uint4*)(a.mins + (tbase + c) * 32 + g * 8);
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const int kk = c * 128 + 32 * s + 8 * g;
+      const bool kok = kk < a.K;
+#pragma unroll
+      for (int mt = 0; mt < MT; mt++) {
+        const uint4 B = *(const uint4*)(xr[mt] + (kok ? kk : 0));
+        ch.xb[s][mt] = (mok[mt] && kok) ? B : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto compute_chunk = [&](const Chunk& ch) {
+#pragma unroll
+    for (int blk = 0; blk < 2; blk++) {
+      f32x4 P[MT], X[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; mt++) {
+        P[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        X[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ss++) {
+        const int s = blk * 2 + ss;
+        uint4 A;
+        if constexpr (BITS == 4) {
+          const uint32_t u = s == 0 ? ch.q0.x : (s == 1 ? ch.q0.y : (s == 2 ? ch.q0.z : ch.q0.w));
+          A = decode4<DK, T>(u, lut2);
+        } else {
+          const uint4& qq = blk == 0 ? ch.q0 : ch.q1;
+          A = ss == 0 ? decode8<DK, T>(qq.x, qq.y) : decode8<DK, T>(qq.z, qq.w);
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++) {
+          P[mt] = mfma16<T>(A, ch.xb[s][mt], P[mt]);
+          if constexpr (NEEDX) X[mt] = mfma16<T>(ones, ch.xb[s][mt], X[mt]);
+        }
+      }
+      // this 64-block's scales: lane rows n = 4g + i
+      const uint32_t s01 = blk == 0 ? ch.sc.x : ch.sc.z, s23 = blk == 0 ? ch.sc.y : ch.sc.w;
+      const float d[4] = {f16_to_f32(s01 & 0xffff), f16_to_f32(s01 >> 16), f16_to_f32(s23 & 0xffff),
+                          f16_to_f32(s23 >> 16)};
+      float mm[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (dk_has_min(DK)) {
+        const uint32_t m01 = blk == 0 ? ch.mn.x : ch.mn.z, m23 = blk == 0 ? ch.mn.y : ch.mn.w;
+        mm[0] = f16_to_f32(m01 & 0xffff); mm[1] = f16_to_f32(m01 >> 16);
+        mm[2] = f16_to_f32(m23 & 0xffff); mm[3] = f16_to_f32(m23 >> 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        float cd, cx;
+        block_coef<DK, T>(d[i], mm[i], cd, cx);
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++) {
+          acc[mt][i] += cd * P[mt][i];
+          if constexpr (NEEDX) acc[mt][i] += cx * X[mt][i];
+        }
+      }
+    }
+  };
+  constexpr int PF = MT == 1 ? 4 : 2;
+  if (c0 < c1) {
+    Chunk ring[PF];
+#pragma unroll
+    for (int u = 0; u < PF; u++) load_chunk(ring[u], c0 + u);
+    for (int c = c0; c < c1; c += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; u++) {
+        if (c + u < c1) compute_chunk(ring[u]);
+        load_chunk(ring[u], c + u + PF);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int mt = 0; mt < MT; mt++) red[wave][mt][lane] = make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
+  __syncthreads();
+  if (wave != 0) return;
+
+  if constexpr (EPI == EPI_GLU) {
+    // tile pair p: rows of tile 2p are gate rows, tile 2p+1 up rows
+    const int p = blockIdx.x;
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++) {
+      const int m = mt * 16 + r16;
+      float4 g0 = red[0][mt][lane], g1 = red[1][mt][lane], u0 = red[2][mt][lane], u1 = red[3][mt][lane];
+      float gv[4] = {g0.x + g1.x, g0.y + g1.y, g0.z + g1.z, g0.w + g1.w};
+      float uv[4] = {u0.x + u1.x, u0.y + u1.y, u0.z + u1.z, u0.w + u1.w};
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) o[i] = (a.act == 0 ? silu_f(gv[i]) : gelu_tanh_f(gv[i])) * uv[i];
+      const int n0 = p * 16 + 4 * g;
+      if (m < a.M && n0 < a.N) {
+        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+        if (n0 + 3 < a.N) {
+          *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+        } else {
+          for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++) {
+      const int m = mt * 16 + r16;
+      float4 v0 = red[0][mt][lane], v1 = red[1][mt][lane], v2 = red[2][mt][lane], v3 = red[3][mt][lane];
+      float o[4] = {v0.x + v1.x + v2.x + v3.x, v0.y + v1.y + v2.y + v3.y,
+                    v0.z + v1.z + v2.z + v3.z, v0.w + v1.w + v2.w + v3.w};
+      const int n0 = tile * 16 + 4 * g;
+      if (m >= a.M || n0 >= a.N) continue;
+      if constexpr (EPI == EPI_PARTIAL) {
+        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
+        if (n0 + 3 < a.N && (a.N & 3) == 0) {
+          *(float4*)ws = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+          for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[i];
+        }
+      } else {
+        if (a.bias) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[i] += (n0 + i < a.N) ? to_f32<T>(a.bias[n0 + i]) : 0.f;
+        }
+        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+        if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) {
+          *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+        } else {
+          for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// v2 (M <= 16): x staged once per workgroup in LDS, whole tiles per wave.
+//   * the workgroup's activation slice x[0:M, kbase:kbase+Kwg] is loaded with
+//     full 16-B vectors (M*Kwg*2/4096 instructions per thread instead of one
+//     masked fragment load per lane per k-step), read back as MFMA B fragments
+//     with ds_read_b128;
+//   * each wave owns TPW whole 16-row tiles over the workgroup's K range, so
+//     there is no cross-wave reduction; TPW = 2 for the GLU epilogue (gate
+//     tile + up tile in the same lanes -> act(g) * u in registers);
+//   * only weights + scales live in the register prefetch ring (8 VGPRs per
+//     tile-chunk) -> PF = 8 chunks in flight per tile at ~100 VGPRs.
+// Split-K across workgroups (gridDim.y) writes f32 partial slabs.
+// ---------------------------------------------------------------------------
+template <int DK, typename T, int EPI, int TPW>
+__global__ void __launch_bounds__(256) lowbit_gemv2_kernel(const GemvArgs a) {
+  constexpr int BITS = dk_bits(DK);
+  constexpr bool NEEDX = dk_needx(DK);
+  constexpr int PF = 8 / TPW;
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
+  __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  const int nks = gridDim.y;
+  const int cpk = (a.KC + nks - 1) / nks;
+  const int c0 = blockIdx.y * cpk;
+  const int c1 = min(a.KC, c0 + cpk);
+  const int kbase = c0 * 128;
+  const int kw = (c1 - c0) * 128;
+  const int lds_ld = kw + 8;  // +16 B row pad: rows land on different banks
+  const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
+  const int tile0 = (blockIdx.x * 4 + wave) * TPW;
+  const bool wave_on = tile0 < NT && c0 < c1;
+
+  // ---- 1. issue the weight prefetch ring first (it does not depend on x)
+  struct Chunk {
+    uint4 q[TPW][BITS / 4];
+    uint4 sc[TPW];
+    uint4 mn[TPW];
+  };
+  auto load_chunk = [&](Chunk& ch, int c) {
+    c = min(c, c1 - 1);
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      const int tile = min(tile0 + t, NT - 1);
+      const size_t tc = (size_t)tile * a.KC + c;
+      if constexpr (BITS == 4) {
+        ch.q[t][0] = *(const uint4*)(a.codes + (tc * 64 + lane) * 16);
+      } else {
+        ch.q[t][0] = *(const uint4*)(a.codes + ((tc * 2 + 0) * 64 + lane) * 16);
+        ch.q[t][1] = *(const uint4*)(a.codes + ((tc * 2 + 1) * 64 + lane) * 16);
+      }
+      ch.sc[t] = *(const uint4*)(a.scales + tc * 32 + g * 8);
+      if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint4*)(a.mins + tc * 32 + g * 8);
+    }
+  };
+  Chunk ring[PF];
+  if (wave_on) {
+#pragma unroll
+    for (int u = 0; u < PF; u++) load_chunk(ring[u], c0 + u);
+  }
+
+  // ---- 2. stage x[0:M, kbase:kbase+kw] into LDS (zero-fill beyond K)
+  if constexpr (DK == DK_LUT4) {
+    lut2[threadIdx.x] = pack2<T>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
+  }
+  {
+    const int vpr = kw / 8;  // 16-B vectors per row
+    for (int v = threadIdx.x; v < a.M * vpr; v += 256) {
+      const int m = v / vpr, kk = (v % vpr) * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (kbase + kk < a.K) val = *(const uint4*)(a.x + (size_t)m * a.ldx + kbase + kk);
+      *(uint4*)(xs + m * lds_ld + kk) = val;
+    }
+  }
+  __syncthreads();
+  if (!wave_on) return;
+
+  const uint4 ones = make_uint4(Magic<T>::one2, Magic<T>::one2, Magic<T>::one2, Magic<T>::one2);
+  const bool mok = r16 < a.M;
+  const uint16_t* xrow = xs + (mok ? r16 : 0) * lds_ld + 8 * g;
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute_chunk = [&](const Chunk& ch, int c) {
+    const uint16_t* xc = xrow + (c - c0) * 128;
+    uint4 B[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const uint4 v = *(const uint4*)(xc + 32 * s);
+      B[s] = mok ? v : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+#pragma unroll
+      for (int blk = 0; blk < 2; blk++) {
+        f32x4 P = {0.f, 0.f, 0.f, 0.f}, X = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ss = 0; ss < 2; ss++) {
+          const int s = blk * 2 + ss;
+          uint4 A;
+          if constexpr (BITS == 4) {
+            const uint4& q0 = ch.q[t][0];
+            const uint32_t u = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
+            A = decode4<DK, T>(u, lut2);
+          } else {
+            const uint4& qq = ch.q[t][blk];
+            A = ss == 0 ? decode8<DK, T>(qq.x, qq.y) : decode8<DK, T>(qq.z, qq.w);
+          }
+          P = mfma16<T>(A, B[s], P);
+          if constexpr (NEEDX) X = mfma16<T>(ones, B[s], X);
+        }
+        const uint32_t s01 = blk == 0 ? ch.sc[t].x : ch.sc[t].z, s23 = blk == 0 ? ch.sc[t].y : ch.sc[t].w;
+        const float d[4] = {f16_to_f32(s01 & 0xffff), f16_to_f32(s01 >> 16), f16_to_f32(s23 & 0xffff),
+                            f16_to_f32(s23 >> 16)};
+        float mm[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (dk_has_min(DK)) {
+          const uint32_t m01 = blk == 0 ? ch.mn[t].x : ch.mn[t].z, m23 = blk == 0 ? ch.mn[t].y : ch.mn[t].w;
+          mm[0] = f16_to_f32(m01 & 0xffff); mm[1] = f16_to_f32(m01 >> 16);
+          mm[2] = f16_to_f32(m23 & 0xffff); mm[3] = f16_to_f32(m23 >> 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          float cd, cx;
+          block_coef<DK, T>(d[i], mm[i], cd, cx);
+          acc[t][i] += cd * P[i];
+          if constexpr (NEEDX) acc[t][i] += cx * X[i];
+        }
+      }
+    }
+  };
+
+  // Steady state: unconditional loads (hipcc keeps exact counted vmcnt
+  // waits); the last < 2*PF chunks run a guarded tail, so no chunk is
+  // re-read past c1.
+  const int c1u = __builtin_amdgcn_readfirstlane(c1);
+  int c = __builtin_amdgcn_readfirstlane(c0);
+  for (; c + 2 * PF <= c1u; c += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; u++) {
+      compute_chunk(ring[u], c + u);
+      load_chunk(ring[u], c + u + PF);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PF; u++) {
+    if (c + u < c1u) {
+      compute_chunk(ring[u], c + u);
+      if (c + u + PF < c1u) load_chunk(ring[u], c + u + PF);
+    }
+  }
+  c += PF;
+#pragma unroll
+  for (int u = 0; u < PF; u++)
+    if (c + u < c1u) compute_chunk(ring[u], c + u);
+
+  // ---- epilogue: lane holds rows 16*tile + 4g + i, column m = r16
+  const int m = r16;
+  if (m >= a.M) return;
+  if constexpr (EPI == EPI_GLU) {
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const float gv = acc[0][i], uv = acc[TPW - 1][i];
+      o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
+    }
+    const int n0 = (tile0 / 2) * 16 + 4 * g;
+    if (n0 < a.N) {
+      uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+      if (n0 + 3 < a.N) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+      else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      const int n0 = (tile0 + t) * 16 + 4 * g;
+      if (tile0 + t >= NT || n0 >= a.N) continue;
+      float o[4] = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
+      if constexpr (EPI == EPI_PARTIAL) {
+        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
+        if (n0 + 3 < a.N && (a.N & 3) == 0) *(float4*)ws = make_float4(o[0], o[1], o[2], o[3]);
+        else for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[i];
+      } else {
+        if (a.bias) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[i] += (n0 + i < a.N) ? to_f32<T>(a.bias[n0 + i]) : 0.f;
+        }
+        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+        if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+        else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+      }
+    }
+  }
+}
+
+template <int DK>
+void launch_gemv2_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+#define L2K(TT, E, TP) hipLaunchKernelGGL((lowbit_gemv2_kernel<DK, TT, E, TP>), grid, dim3(256), shmem, st, a)
+  if (bf16) {
+    if (epi == EPI_STORE) L2K(BF16, EPI_STORE, 1);
+    else if (epi == EPI_PARTIAL) L2K(BF16, EPI_PARTIAL, 1);
+    else L2K(BF16, EPI_GLU, 2);
+  } else {
+    if (epi == EPI_STORE) L2K(F16, EPI_STORE, 1);
+    else if (epi == EPI_PARTIAL) L2K(F16, EPI_PARTIAL, 1);
+    else L2K(F16, EPI_GLU, 2);
+  }
+#undef L2K
+}
+
+template <int DK, typename T, int MT>
+inline void launch_gemv_t(int epi, dim3 grid, const GemvArgs& a, hipStream_t st) {
+  if (epi == EPI_STORE) hipLaunchKernelGGL((lowbit_gemv_kernel<DK, T, MT, EPI_STORE>), grid, dim3(256), 0, st, a);
+  else if (epi == EPI_PARTIAL) hipLaunchKernelGGL((lowbit_gemv_kernel<DK, T, MT, EPI_PARTIAL>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((lowbit_gemv_kernel<DK, T, MT, EPI_GLU>), grid, dim3(256), 0, st, a);
+}
+
+template <int DK>
+void launch_gemv_dk(bool bf16, int mt, int epi, dim3 grid, const GemvArgs& a, hipStream_t st) {
+  if (bf16) {
+    if (mt == 1) launch_gemv_t<DK, BF16, 1>(epi, grid, a, st);
+    else if (mt == 2) launch_gemv_t<DK, BF16, 2>(epi, grid, a, st);
+    else launch_gemv_t<DK, BF16, 4>(epi, grid, a, st);
+  } else {
+    if (mt == 1) launch_gemv_t<DK, F16, 1>(epi, grid, a, st);
+    else if (mt == 2) launch_gemv_t<DK, F16, 2>(epi, grid, a, st);
+    else launch_gemv_t<DK, F16, 4>(epi, grid, a, st);
+  }
+}
+
+}  // namespace illm

@@ -1,0 +1,246 @@
+// Elementwise / small kernels: GLU activation, on-device quantize-on-load and
+// dequant, split-K partial reduction, MoE router top-k.
+//
+// Reference ops: xe_addons.mlp_silu_mul_inplaced (models/qwen2.py:325-329),
+// xe_linear.dequant (low_bit_linear.py:566-570), xe_addons.moe_softmax_topk /
+// moe_group_topk (models/common.py:342-375), ggml_quantize_tensor done on
+// the GPU instead of the host (low_bit_linear.py:180).
+#include "../common/quant_block.h"
+#include "illm_device.h"
+#include "kernels.h"
+
+namespace illm {
+
+// ---- GLU: out[m, i] = act(gu[m, i]) * gu[m, I + i] ---------------------------
+template <typename T>
+__global__ void glu_kernel(const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act) {
+  const int64_t n8 = (int64_t)M * I / 8;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n8;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = v * 8;
+    const int m = (int)(e / I), i = (int)(e % I);
+    const uint4 g = *(const uint4*)(gu + (size_t)m * ld + i);
+    const uint4 u = *(const uint4*)(gu + (size_t)m * ld + I + i);
+    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, uw[4] = {u.x, u.y, u.z, u.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      float g0 = to_f32<T>(gw[j] & 0xffff), g1 = to_f32<T>(gw[j] >> 16);
+      float u0 = to_f32<T>(uw[j] & 0xffff), u1 = to_f32<T>(uw[j] >> 16);
+      // HF: act(gate) rounded to dtype, then * up rounded
+      g0 = to_f32<T>(from_f32<T>(act == 0 ? silu_f(g0) : gelu_tanh_f(g0)));
+      g1 = to_f32<T>(from_f32<T>(act == 0 ? silu_f(g1) : gelu_tanh_f(g1)));
+      o[j] = pack2<T>(g0 * u0, g1 * u1);
+    }
+    *(uint4*)(out + (size_t)m * I + i) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+void launch_glu(bool bf16, const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act,
+                hipStream_t st) {
+  const int64_t n8 = (int64_t)M * I / 8;
+  const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
+  if (bf16) hipLaunchKernelGGL(glu_kernel<BF16>, dim3(blocks), dim3(256), 0, st, gu, ld, out, M, I, act);
+  else hipLaunchKernelGGL(glu_kernel<F16>, dim3(blocks), dim3(256), 0, st, gu, ld, out, M, I, act);
+}
+
+// ---- quantize on device: dense [n, k] -> MI355X tiled blob ------------------
+__device__ __forceinline__ float load_in(const void* w, int kind, size_t i) {
+  if (kind == 0) return ((const float*)w)[i];
+  if (kind == 1) return bf16_to_f32(((const uint16_t*)w)[i]);
+  return f16_to_f32(((const uint16_t*)w)[i]);
+}
+
+__global__ void quantize_device_kernel(int fmt, int kind, const void* w, int64_t n, int64_t k,
+                                       uint8_t* blob, int search) {
+  const int64_t nb = k / QBLOCK;
+  const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (id >= n * nb) return;
+  const int64_t row = id / nb, b = id % nb;
+  float x[QBLOCK];
+  for (int i = 0; i < QBLOCK; i++) x[i] = load_in(w, kind, (size_t)row * k + b * QBLOCK + i);
+  uint8_t codes[QBLOCK];
+  float d, m;
+  hd_quant_block(fmt, x, nullptr, search != 0, codes, &d, &m);
+
+  const int bits = fmt_bits(fmt);
+  const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
+  const int64_t t = row / TILE_N;
+  const int r = (int)(row % TILE_N);
+  const int64_t c = b / 2;
+  const int blk = (int)(b % 2);
+  uint8_t* dcode = blob;
+  uint16_t* dscale = (uint16_t*)(blob + dev_code_bytes(fmt, n, k));
+  uint16_t* dmin = dscale + dev_scale_elems(n, k);
+  if (bits == 4) {
+    for (int ss = 0; ss < 2; ss++) {
+      const int s = 2 * blk + ss;
+      for (int g = 0; g < 4; g++) {
+        uint32_t u = 0;
+        for (int j = 0; j < 8; j++) u |= (uint32_t)(codes[32 * ss + 8 * g + j] & 15) << (4 * dev_nib_pos(fmt, j));
+        const int l = g * 16 + r;
+        ((uint32_t*)(dcode + ((t * KC + c) * 64 + l) * 16))[s] = u;
+      }
+    }
+  } else {
+    for (int g = 0; g < 4; g++) {
+      const int l = g * 16 + r;
+      uint8_t* o = dcode + (((t * KC + c) * 2 + blk) * 64 + l) * 16;
+      uint32_t wv[4];
+      for (int q = 0; q < 4; q++) {
+        const int ss = q / 2, j0 = (q % 2) * 4;
+        const uint8_t* cc = codes + 32 * ss + 8 * g + j0;
+        wv[q] = (uint32_t)cc[0] | ((uint32_t)cc[1] << 8) | ((uint32_t)cc[2] << 16) | ((uint32_t)cc[3] << 24);
+      }
+      *(uint4*)o = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    }
+  }
+  const int64_t so = (t * KC + c) * 32 + (r / 4) * 8 + blk * 4 + (r % 4);
+  dscale[so] = hd_f32_to_f16(d);
+  if (fmt_has_min(fmt)) dmin[so] = hd_f32_to_f16(m);
+}
+
+void launch_quantize_device(int fmt, int in_kind, const void* w, int64_t n, int64_t k,
+                            uint8_t* blob, int search, hipStream_t st) {
+  hipMemsetAsync(blob, 0, dev_total_bytes(fmt, n, k), st);
+  const int64_t tot = n * (k / QBLOCK);
+  hipLaunchKernelGGL(quantize_device_kernel, dim3((unsigned)((tot + 127) / 128)), dim3(128), 0, st, fmt,
+                     in_kind, w, n, k, blob, search);
+}
+
+// ---- dequantize on device: tiled blob -> dense [n, k] ------------------------
+template <typename T>
+__global__ void dequantize_device_kernel(int fmt, const uint8_t* blob, int64_t n, int64_t k,
+                                         uint16_t* out) {
+  const int64_t nb = k / QBLOCK;
+  const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (id >= n * nb) return;
+  const int64_t row = id / nb, b = id % nb;
+  const int bits = fmt_bits(fmt);
+  const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
+  const int64_t t = row / TILE_N;
+  const int r = (int)(row % TILE_N);
+  const int64_t c = b / 2;
+  const int blk = (int)(b % 2);
+  const uint8_t* dcode = blob;
+  const uint16_t* dscale = (const uint16_t*)(blob + dev_code_bytes(fmt, n, k));
+  const uint16_t* dmin = dscale + dev_scale_elems(n, k);
+  const int64_t so = (t * KC + c) * 32 + (r / 4) * 8 + blk * 4 + (r % 4);
+  const float d = f16_to_f32(dscale[so]);
+  const float m = fmt_has_min(fmt) ? f16_to_f32(dmin[so]) : 0.f;
+  uint16_t* o = out + (size_t)row * k + b * QBLOCK;
+  for (int ss = 0; ss < 2; ss++) {
+    const int s = 2 * blk + ss;
+    for (int g = 0; g < 4; g++) {
+      const int l = g * 16 + r;
+      for (int j = 0; j < 8; j++) {
+        int code;
+        if (bits == 4) {
+          const uint32_t u = ((const uint32_t*)(dcode + ((t * KC + c) * 64 + l) * 16))[s];
+          code = (u >> (4 * dev_nib_pos(fmt, j))) & 15;
+        } else {
+          code = dcode[(((t * KC + c) * 2 + blk) * 64 + l) * 16 + ss * 8 + j];
+        }
+        o[32 * ss + 8 * g + j] = from_f32<T>(hd_code_value(fmt, code) * d + m);
+      }
+    }
+  }
+}
+
+void launch_dequantize_device(bool bf16, int fmt, const uint8_t* blob, int64_t n, int64_t k,
+                              uint16_t* out, hipStream_t st) {
+  const int64_t tot = n * (k / QBLOCK);
+  dim3 grid((unsigned)((tot + 127) / 128));
+  if (bf16) hipLaunchKernelGGL(dequantize_device_kernel<BF16>, grid, dim3(128), 0, st, fmt, blob, n, k, out);
+  else hipLaunchKernelGGL(dequantize_device_kernel<F16>, grid, dim3(128), 0, st, fmt, blob, n, k, out);
+}
+
+// ---- sum split-K partial slabs (+bias) -> T ----------------------------------
+template <typename T>
+__global__ void reduce_partials_kernel(const float* ws, int nsplit, const uint16_t* bias,
+                                       uint16_t* out, int M, int N, int ldo) {
+  const int64_t tot = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < tot;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i / N), n = (int)(i % N);
+    float acc = 0.f;
+    for (int s = 0; s < nsplit; s++) acc += ws[(size_t)s * tot + i];
+    if (bias) acc += to_f32<T>(bias[n]);
+    out[(size_t)m * ldo + n] = from_f32<T>(acc);
+  }
+}
+
+void launch_reduce_partials(bool bf16, const float* ws, int nsplit, const uint16_t* bias,
+                            uint16_t* out, int M, int N, int ldo, hipStream_t st) {
+  const int64_t tot = (int64_t)M * N;
+  const int blocks = (int)std::min<int64_t>((tot + 255) / 256, 2048);
+  if (bf16) hipLaunchKernelGGL(reduce_partials_kernel<BF16>, dim3(blocks), dim3(256), 0, st, ws, nsplit, bias, out, M, N, ldo);
+  else hipLaunchKernelGGL(reduce_partials_kernel<F16>, dim3(blocks), dim3(256), 0, st, ws, nsplit, bias, out, M, N, ldo);
+}
+
+// ---- MoE router: softmax / sigmoid + top-k (+renormalise) --------------------
+// one wave per token, E <= 512
+__global__ void __launch_bounds__(64) moe_topk_kernel(const float* logits, int T, int E, int k,
+                                                      int renorm, int scoring, float* topk_w,
+                                                      int32_t* topk_ids) {
+  const int t = blockIdx.x, lane = threadIdx.x;
+  constexpr int PER = 8;
+  float v[PER];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const int e = lane + 64 * j;
+    v[j] = e < E ? logits[(size_t)t * E + e] : -INFINITY;
+    mx = fmaxf(mx, v[j]);
+  }
+  if (scoring == 0) {
+    mx = wave_max(mx);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      v[j] = (lane + 64 * j) < E ? __expf(v[j] - mx) : 0.f;
+      s += v[j];
+    }
+    s = wave_sum(s);
+#pragma unroll
+    for (int j = 0; j < PER; j++) v[j] /= s;
+  } else {
+#pragma unroll
+    for (int j = 0; j < PER; j++) v[j] = (lane + 64 * j) < E ? 1.f / (1.f + __expf(-v[j])) : -1.f;
+  }
+  float tot = 0.f;
+  for (int i = 0; i < k; i++) {
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      const int e = lane + 64 * j;
+      if (e < E && (v[j] > best || (v[j] == best && e < bi))) { best = v[j]; bi = e; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+#pragma unroll
+    for (int j = 0; j < PER; j++)
+      if (lane + 64 * j == bi) v[j] = -INFINITY;
+    if (lane == 0) {
+      topk_w[(size_t)t * k + i] = best;
+      topk_ids[(size_t)t * k + i] = bi;
+    }
+    tot += best;
+  }
+  if (renorm && lane == 0) {
+    for (int i = 0; i < k; i++) topk_w[(size_t)t * k + i] /= tot;
+  }
+}
+
+void launch_moe_topk(const float* logits, int T, int E, int k, int renorm, int scoring,
+                     float* topk_w, int32_t* topk_ids, hipStream_t st) {
+  hipLaunchKernelGGL(moe_topk_kernel, dim3(T), dim3(64), 0, st, logits, T, E, k, renorm, scoring,
+                     topk_w, topk_ids);
+}
+
+}  // namespace illm

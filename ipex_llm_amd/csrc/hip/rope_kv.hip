@@ -1,0 +1,107 @@
+// Fused rotary embedding + KV-cache append for the decode/prefill step.
+//
+// Reference ops: xe_addons.rotary_half_inplaced / rotary_two_inplaced /
+// rotary_*_with_cache_inplaced (models/common.py:354-367, llama.py:158-162,
+// chatglm2.py:251) and the KV write of kv.py / models/utils.py:65-74
+// (append_kv_cache) + quantize_key_value (utils.py:133-191).
+//
+// One wave64 per (head, token): q/k/v rows come straight from the fused QKV
+// projection output; q is rotated (optionally per-head RMS-normalised first,
+// qwen3) and written contiguous; k is rotated and v copied into the paged KV
+// cache at slots[t] (block * bs + offset), in the activation dtype or fp8.
+// Positions and slots are device tensors, so the kernel is graph-capturable.
+#include "../common/quant_block.h"
+#include "illm_device.h"
+#include "kernels.h"
+
+namespace illm {
+
+__device__ __forceinline__ void store_kv(uint8_t* base, size_t idx, float v, int kv_fp8, float scale,
+                                         bool bf16) {
+  if (kv_fp8 == 1) {
+    base[idx] = hd_f32_to_e5m2(v / scale);
+  } else if (kv_fp8 == 2) {
+    base[idx] = hd_f32_to_e4m3(v / scale);
+  } else {
+    ((uint16_t*)base)[idx] = bf16 ? f32_to_bf16(v) : f32_to_f16(v);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
+  const int h = blockIdx.x, t = blockIdx.y, lane = threadIdx.x;
+  const int D = a.D, half = a.rot_dim / 2;
+  const bool is_q = h < a.Hq, is_k = !is_q && h < a.Hq + a.Hkv;
+  const uint16_t* src = a.qkv + (size_t)t * a.ld_qkv + (size_t)h * D;
+  constexpr bool BF = std::is_same<T, BF16>::value;
+
+  // per-head RMSNorm (qwen3 q_norm / k_norm): sum of squares over D
+  const uint16_t* nw = is_q ? a.q_norm : (is_k ? a.k_norm : nullptr);
+  float inv = 1.f;
+  if (nw) {
+    float ss = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      float v = to_f32<T>(src[d]);
+      ss += v * v;
+    }
+    ss = wave_sum(ss);
+    inv = rsqrtf(ss / (float)D + a.norm_eps);
+  }
+  auto val = [&](int d) -> float {
+    float v = to_f32<T>(src[d]);
+    if (nw) v = to_f32<T>(from_f32<T>(to_f32<T>(nw[d]) * to_f32<T>(from_f32<T>(v * inv))));
+    return v;
+  };
+
+  const float p = (float)a.pos[t];
+  int64_t slot = 0;
+  uint8_t* cache = nullptr;
+  float cscale = 1.f;
+  if (!is_q) {
+    slot = a.slots[t];
+    if (slot < 0) return;
+    cache = is_k ? a.k_cache : a.v_cache;
+    cscale = is_k ? a.k_scale : a.v_scale;
+  }
+  const int hk = is_q ? h : (is_k ? h - a.Hq : h - a.Hq - a.Hkv);
+  const size_t crow = is_q ? 0 : (((size_t)(slot / a.bs) * a.Hkv + hk) * a.bs + (size_t)(slot % a.bs)) * D;
+  uint16_t* qdst = is_q ? a.q_out + ((size_t)t * a.Hq + h) * D : nullptr;
+
+  auto put = [&](int d, float v) {
+    if (is_q) qdst[d] = from_f32<T>(v * a.attn_scale_q);
+    else store_kv(cache, crow + d, v, a.kv_fp8, cscale, BF);
+  };
+
+  if (is_q || is_k) {
+    for (int i = lane; i < half; i += 64) {
+      int d0, d1;
+      if (a.interleaved) { d0 = 2 * i; d1 = 2 * i + 1; }
+      else { d0 = i; d1 = i + half; }
+      float s, c;
+      if (a.cos_sin) {
+        const float2 cs = ((const float2*)a.cos_sin)[(size_t)a.pos[t] * half + i];
+        c = cs.x;
+        s = cs.y;
+      } else {
+        sincosf(p * a.inv_freq[i], &s, &c);
+      }
+      // HF casts cos/sin to the activation dtype before the rotation
+      c = to_f32<T>(from_f32<T>(c));
+      s = to_f32<T>(from_f32<T>(s));
+      const float x0 = val(d0), x1 = val(d1);
+      put(d0, to_f32<T>(from_f32<T>(x0 * c)) - to_f32<T>(from_f32<T>(x1 * s)));
+      put(d1, to_f32<T>(from_f32<T>(x1 * c)) + to_f32<T>(from_f32<T>(x0 * s)));
+    }
+    for (int d = a.rot_dim + lane; d < D; d += 64) put(d, val(d));
+  } else {
+    for (int d = lane; d < D; d += 64) put(d, to_f32<T>(src[d]));
+  }
+}
+
+void launch_rope_kv(bool bf16, const RopeKVArgs& a, hipStream_t st) {
+  dim3 grid(a.Hq + 2 * a.Hkv, a.T);
+  if (bf16) hipLaunchKernelGGL(rope_kv_kernel<BF16>, grid, dim3(64), 0, st, a);
+  else hipLaunchKernelGGL(rope_kv_kernel<F16>, grid, dim3(64), 0, st, a);
+}
+
+}  // namespace illm

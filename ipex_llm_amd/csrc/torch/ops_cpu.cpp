@@ -1,0 +1,130 @@
+// torch.library registration of the ipex_llm_amd op namespace + CPU impls.
+// GPU impls live in ops_hip.cpp; meta ("fake") impls are registered from
+// Python (ipex_llm_amd/ops/_meta.py) for torch.compile / graph tracing.
+#include <ATen/ATen.h>
+#include <torch/library.h>
+
+#include "../common/formats.h"
+#include "../cpu/quant_api.h"
+
+using at::Tensor;
+
+namespace {
+
+void check_fmt(int64_t fmt) { TORCH_CHECK(fmt >= 0 && fmt < illm::FMT_COUNT, "bad low-bit fmt ", fmt); }
+
+struct Planes {
+  uint8_t* codes;
+  uint16_t* scales;
+  uint16_t* mins;
+};
+Planes canon_planes(const Tensor& blob, int64_t fmt, int64_t n, int64_t k) {
+  uint8_t* b = blob.data_ptr<uint8_t>();
+  Planes p;
+  p.codes = b;
+  p.scales = (uint16_t*)(b + illm::canon_code_bytes((int)fmt, n, k));
+  p.mins = illm::fmt_has_min((int)fmt) ? p.scales + illm::canon_scale_elems(n, k) : nullptr;
+  return p;
+}
+
+Tensor quantize_cpu(const Tensor& w, int64_t fmt, const c10::optional<Tensor>& imatrix,
+                    bool scale_search) {
+  check_fmt(fmt);
+  TORCH_CHECK(w.dim() == 2, "quantize expects [n, k]");
+  const int64_t n = w.size(0), k = w.size(1);
+  TORCH_CHECK(k % illm::QBLOCK == 0, "in_features must be a multiple of ", illm::QBLOCK);
+  Tensor wf = w.to(at::kFloat).contiguous();
+  Tensor blob = at::empty({illm::canon_total_bytes((int)fmt, n, k)}, w.options().dtype(at::kByte));
+  Planes p = canon_planes(blob, fmt, n, k);
+  Tensor im;
+  const float* imp = nullptr;
+  if (imatrix.has_value() && imatrix->defined()) {
+    im = imatrix->to(at::kFloat).contiguous();
+    TORCH_CHECK(im.numel() == k, "imatrix must have in_features elements");
+    imp = im.data_ptr<float>();
+  }
+  illm_quantize((int)fmt, wf.data_ptr<float>(), n, k, imp, scale_search ? 1 : 0, p.codes, p.scales,
+                p.mins);
+  return blob;
+}
+
+Tensor dequantize_cpu(const Tensor& blob, int64_t fmt, int64_t n, int64_t k) {
+  check_fmt(fmt);
+  Tensor b = blob.contiguous();
+  TORCH_CHECK(b.numel() >= illm::canon_total_bytes((int)fmt, n, k), "blob too small");
+  Planes p = canon_planes(b, fmt, n, k);
+  Tensor out = at::empty({n, k}, b.options().dtype(at::kFloat));
+  illm_dequantize((int)fmt, p.codes, p.scales, p.mins, n, k, out.data_ptr<float>());
+  return out;
+}
+
+Tensor repack_to_device(const Tensor& canon, int64_t fmt, int64_t n, int64_t k) {
+  check_fmt(fmt);
+  Tensor b = canon.contiguous();
+  Planes p = canon_planes(b, fmt, n, k);
+  Tensor dev = at::zeros({illm::dev_total_bytes((int)fmt, n, k)}, b.options());
+  illm_repack_to_device((int)fmt, p.codes, p.scales, p.mins, n, k, dev.data_ptr<uint8_t>());
+  return dev;
+}
+
+Tensor repack_from_device(const Tensor& dev, int64_t fmt, int64_t n, int64_t k) {
+  check_fmt(fmt);
+  Tensor d = dev.contiguous();
+  Tensor canon = at::zeros({illm::canon_total_bytes((int)fmt, n, k)}, d.options());
+  Planes p = canon_planes(canon, fmt, n, k);
+  illm_repack_from_device((int)fmt, d.data_ptr<uint8_t>(), n, k, p.codes, p.scales, p.mins);
+  return canon;
+}
+
+Tensor linear_cpu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k) {
+  check_fmt(fmt);
+  TORCH_CHECK(x.size(-1) == k, "x last dim must equal in_features");
+  Tensor xf = x.reshape({-1, k}).to(at::kFloat).contiguous();
+  Tensor b = blob.contiguous();
+  Planes p = canon_planes(b, fmt, n, k);
+  Tensor y = at::empty({xf.size(0), n}, xf.options());
+  illm_cpu_gemm((int)fmt, xf.data_ptr<float>(), xf.size(0), p.codes, p.scales, p.mins, n, k,
+                y.data_ptr<float>());
+  auto shape = x.sizes().vec();
+  shape.back() = n;
+  return y.view(shape);
+}
+
+Tensor to_fp8_bytes(const Tensor& x, bool e5m2) {
+  Tensor xf = x.to(at::kFloat).contiguous();
+  Tensor out = at::empty(xf.sizes(), xf.options().dtype(at::kByte));
+  illm_f32_to_fp8(xf.data_ptr<float>(), xf.numel(), e5m2 ? 1 : 0, out.data_ptr<uint8_t>());
+  return out;
+}
+
+}  // namespace
+
+TORCH_LIBRARY(ipex_llm_amd, m) {
+  // host library
+  m.def("quantize_cpu(Tensor w, int fmt, Tensor? imatrix, bool scale_search) -> Tensor");
+  m.def("dequantize_cpu(Tensor blob, int fmt, int n, int k) -> Tensor");
+  m.def("repack_to_device(Tensor canon, int fmt, int n, int k) -> Tensor");
+  m.def("repack_from_device(Tensor dev, int fmt, int n, int k) -> Tensor");
+  m.def("linear_cpu(Tensor x, Tensor blob, int fmt, int n, int k) -> Tensor");
+  m.def("to_fp8_bytes(Tensor x, bool e5m2) -> Tensor");
+  // device kernels (ops_hip.cpp)
+  m.def("quantize_device(Tensor w, int fmt, bool scale_search) -> Tensor");
+  m.def("dequantize_device(Tensor blob, int fmt, int n, int k, ScalarType dtype) -> Tensor");
+  m.def("gemv(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias, int epi, int ksplit, int act) -> Tensor");
+  m.def("add_rms_norm(Tensor? x, Tensor? partials, Tensor(a!)? residual, Tensor w, float eps, bool unit_offset, bool store_residual) -> Tensor");
+  m.def("layer_norm(Tensor x, Tensor? w, Tensor? b, float eps) -> Tensor");
+  m.def("rope_kv(Tensor qkv, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slots, Tensor pos, Tensor inv_freq, Tensor? q_norm, Tensor? k_norm, float norm_eps, float q_scale, int Hq, int Hkv, int D, int rot_dim, bool interleaved, int kv_fp8, float k_scale, float v_scale) -> ()");
+  m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int kv_fp8, float k_scale, float v_scale, Tensor? alibi) -> Tensor");
+  m.def("glu(Tensor gu, int act) -> Tensor");
+  m.def("reduce_partials(Tensor ws, Tensor? bias, ScalarType dtype) -> Tensor");
+  m.def("moe_topk(Tensor logits, int k, bool renorm, int scoring) -> (Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
+  m.impl("quantize_cpu", &quantize_cpu);
+  m.impl("dequantize_cpu", &dequantize_cpu);
+  m.impl("repack_to_device", &repack_to_device);
+  m.impl("repack_from_device", &repack_from_device);
+  m.impl("linear_cpu", &linear_cpu);
+  m.impl("to_fp8_bytes", &to_fp8_bytes);
+}

@@ -1,0 +1,355 @@
+// GPU (HIP, gfx950) implementations of the ipex_llm_amd ops.  Thin shape
+// checking + launch on torch's current HIP stream (so everything is
+// capturable in a hipGraph via torch.cuda.graph).
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+#include "../common/formats.h"
+#include "../hip/kernels.h"
+#include "../hip/gemv_args.h"
+
+using at::Tensor;
+
+namespace {
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+inline bool is_bf16(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf,
+              "activations must be bf16 or fp16, got ", t.scalar_type());
+  return t.scalar_type() == at::kBFloat16;
+}
+inline const uint16_t* p16(const Tensor& t) { return (const uint16_t*)t.data_ptr(); }
+inline uint16_t* m16(Tensor& t) { return (uint16_t*)t.data_ptr(); }
+template <typename O>
+inline const uint16_t* p16o(const O& t) {
+  return (t.has_value() && t->defined()) ? (const uint16_t*)t->data_ptr() : nullptr;
+}
+
+Tensor quantize_device(const Tensor& w, int64_t fmt, bool scale_search) {
+  TORCH_CHECK(w.is_cuda() && w.dim() == 2, "quantize_device expects a 2-D GPU tensor");
+  c10::DeviceGuard g(w.device());
+  const int64_t n = w.size(0), k = w.size(1);
+  TORCH_CHECK(k % illm::QBLOCK == 0, "in_features must be a multiple of 64");
+  Tensor wc = w.contiguous();
+  int kind = 0;
+  if (wc.scalar_type() == at::kBFloat16) kind = 1;
+  else if (wc.scalar_type() == at::kHalf) kind = 2;
+  else wc = wc.to(at::kFloat);
+  Tensor blob = at::empty({illm::dev_total_bytes((int)fmt, n, k)}, wc.options().dtype(at::kByte));
+  illm::launch_quantize_device((int)fmt, kind, wc.data_ptr(), n, k, blob.data_ptr<uint8_t>(),
+                               scale_search ? 1 : 0, cur_stream());
+  return blob;
+}
+
+Tensor dequantize_device(const Tensor& blob, int64_t fmt, int64_t n, int64_t k, at::ScalarType dt) {
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "dequantize_device: bf16/fp16 output");
+  c10::DeviceGuard g(blob.device());
+  Tensor out = at::empty({n, k}, blob.options().dtype(dt));
+  illm::launch_dequantize_device(dt == at::kBFloat16, (int)fmt, blob.data_ptr<uint8_t>(), n, k,
+                                 m16(out), cur_stream());
+  return out;
+}
+
+#define ILLM_DK_SWITCH(fmt, CALL)                                           \
+  switch (illm::fmt_to_dk(fmt)) {                                            \
+    case illm::DK_INT4S: { constexpr int DKV = illm::DK_INT4S; CALL; } break; \
+    case illm::DK_INT4A: { constexpr int DKV = illm::DK_INT4A; CALL; } break; \
+    case illm::DK_LUT4: { constexpr int DKV = illm::DK_LUT4; CALL; } break;   \
+    case illm::DK_FP4: { constexpr int DKV = illm::DK_FP4; CALL; } break;     \
+    case illm::DK_INT8S: { constexpr int DKV = illm::DK_INT8S; CALL; } break; \
+    case illm::DK_INT8A: { constexpr int DKV = illm::DK_INT8A; CALL; } break; \
+    case illm::DK_FP8E4: { constexpr int DKV = illm::DK_FP8E4; CALL; } break; \
+    case illm::DK_FP8E5: { constexpr int DKV = illm::DK_FP8E5; CALL; } break; \
+    default: TORCH_CHECK(false, "gemv: unsupported fmt ", fmt);              \
+  }
+
+void launch_gemv_any(int fmt, bool bf16, int mt, int epi, dim3 grid, const illm::GemvArgs& a) {
+  hipStream_t st = cur_stream();
+  ILLM_DK_SWITCH(fmt, illm::launch_gemv_dk<DKV>(bf16, mt, epi, grid, a, st));
+}
+void launch_gemv2_any(int fmt, bool bf16, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a) {
+  hipStream_t st = cur_stream();
+  ILLM_DK_SWITCH(fmt, illm::launch_gemv2_dk<DKV>(bf16, epi, grid, shmem, a, st));
+}
+
+int64_t auto_ksplit(int64_t NT, int64_t KC) {
+  int64_t ks = 1;
+  while (NT * ks < 768 && KC >= 4 * 2 * (ks * 2)) ks *= 2;
+  return ks;
+}
+
+// v2 launch geometry: workgroups = 4 waves x TPW tiles; split K so that
+// there are >= ~320 workgroups, each wave keeps >= 4 chunks, and the LDS x
+// slice (M * Kwg * 2 B) stays <= 64 KiB.
+int64_t v2_ksplit(int64_t M, int64_t NT, int64_t KC, int tpw) {
+  const int64_t wgs = (NT + 4 * tpw - 1) / (4 * tpw);
+  int64_t ks = 1;
+  auto lds = [&](int64_t k) { return M * (((KC + k - 1) / k) * 128 + 8) * 2; };
+  while ((wgs * ks < 320 && KC / (ks * 2) >= 4) || lds(ks) > 65536) ks *= 2;
+  return ks;
+}
+
+Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k,
+            const c10::optional<Tensor>& bias, int64_t epi, int64_t ksplit, int64_t act) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda(), "gemv: GPU tensors expected");
+  TORCH_CHECK(x.size(-1) == k, "gemv: x last dim ", x.size(-1), " != in_features ", k);
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  const int64_t M = xc.numel() / k;
+  TORCH_CHECK(M >= 1 && M <= 64, "gemv handles 1..64 rows, got ", M);
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemv: weight blob too small");
+  const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  const bool force_v1 = getenv("ILLM_GEMV_V1") != nullptr;
+  const bool v2 = M <= 16 && !force_v1;
+
+  illm::GemvArgs a{};
+  a.x = p16(xc);
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.codes = blob.data_ptr<uint8_t>();
+  a.scales = (const uint16_t*)(a.codes + illm::dev_code_bytes((int)fmt, n, k));
+  a.mins = illm::fmt_has_min((int)fmt) ? a.scales + illm::dev_scale_elems(n, k) : nullptr;
+  a.KC = (int)KC;
+  a.act = (int)act;
+  a.lut_fmt = (int)fmt;
+  a.bias = nullptr;
+
+  auto out_shape = xc.sizes().vec();
+  if (epi == illm::EPI_GLU) {
+    TORCH_CHECK(n % 32 == 0, "GLU weights must have a multiple of 32 rows");
+    out_shape.back() = n / 2;
+    Tensor out = at::empty(out_shape, xc.options());
+    a.N = (int)(n / 2);
+    a.out = out.data_ptr();
+    a.ldo = (int)(n / 2);
+    const size_t shmem = (size_t)M * (KC * 128 + 8) * 2;
+    if (v2 && shmem <= 65536) {
+      launch_gemv2_any((int)fmt, bf16, illm::EPI_GLU, dim3((unsigned)((NT + 7) / 8), 1), shmem, a);
+    } else {
+      launch_gemv_any((int)fmt, bf16, mt, illm::EPI_GLU, dim3((unsigned)(NT / 2), 1), a);
+    }
+    return out;
+  }
+  a.N = (int)n;
+  if (ksplit <= 0) ksplit = v2 ? v2_ksplit(M, NT, KC, 1) : auto_ksplit(NT, KC);
+  ksplit = std::min<int64_t>(ksplit, KC);
+  const int64_t cpk = (KC + ksplit - 1) / ksplit;
+  const size_t shmem = (size_t)M * (cpk * 128 + 8) * 2;
+  const bool use_v2 = v2 && shmem <= 65536;
+  auto launch = [&](int e) {
+    if (use_v2) launch_gemv2_any((int)fmt, bf16, e, dim3((unsigned)((NT + 3) / 4), (unsigned)ksplit), shmem, a);
+    else launch_gemv_any((int)fmt, bf16, mt, e, dim3((unsigned)NT, (unsigned)ksplit), a);
+  };
+  if (epi == illm::EPI_PARTIAL || ksplit > 1) {
+    Tensor ws = at::empty({ksplit, M, n}, xc.options().dtype(at::kFloat));
+    a.out = ws.data_ptr();
+    a.ldo = (int)n;
+    launch(illm::EPI_PARTIAL);
+    if (epi == illm::EPI_PARTIAL) return ws;
+    out_shape.back() = n;
+    Tensor out = at::empty(out_shape, xc.options());
+    illm::launch_reduce_partials(bf16, ws.data_ptr<float>(), (int)ksplit, p16o(bias), m16(out), (int)M,
+                                 (int)n, (int)n, cur_stream());
+    return out;
+  }
+  out_shape.back() = n;
+  Tensor out = at::empty(out_shape, xc.options());
+  a.out = out.data_ptr();
+  a.ldo = (int)n;
+  a.bias = p16o(bias);
+  launch(illm::EPI_STORE);
+  return out;
+}
+
+Tensor add_rms_norm(const c10::optional<Tensor>& x, const c10::optional<Tensor>& partials,
+                    const c10::optional<Tensor>& residual, const Tensor& w, double eps,
+                    bool unit_offset, bool store_residual) {
+  c10::DeviceGuard g(w.device());
+  const bool bf16 = is_bf16(w);
+  const int64_t H = w.numel();
+  TORCH_CHECK(H % 8 == 0 && H <= 8 * 256 * 8, "rms_norm hidden size must be a multiple of 8 and <= 16384");
+  illm::NormArgs a{};
+  int64_t M;
+  std::vector<int64_t> shape;
+  if (partials.has_value() && partials->defined()) {
+    TORCH_CHECK(partials->dim() == 3 && partials->size(2) == H, "partials must be [ks, M, H]");
+    a.partials = partials->data_ptr<float>();
+    a.nsplit = (int)partials->size(0);
+    M = partials->size(1);
+    shape = {M, H};
+    if (residual.has_value() && residual->defined()) shape = residual->sizes().vec();
+  } else {
+    TORCH_CHECK(x.has_value() && x->defined(), "add_rms_norm needs x or partials");
+    TORCH_CHECK(x->is_contiguous(), "x must be contiguous");
+    a.x = p16(*x);
+    M = x->numel() / H;
+    shape = x->sizes().vec();
+  }
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->is_contiguous() && residual->numel() == M * H, "residual shape mismatch");
+    a.residual = (uint16_t*)residual->data_ptr();
+  }
+  Tensor out = at::empty(shape, w.options());
+  a.w = p16(w);
+  a.out = m16(out);
+  a.M = (int)M;
+  a.H = (int)H;
+  a.eps = (float)eps;
+  a.unit_offset = unit_offset;
+  a.store_residual = store_residual;
+  if (M > 0) illm::launch_add_rms_norm(bf16, a, cur_stream());
+  return out;
+}
+
+Tensor layer_norm(const Tensor& x, const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
+                  double eps) {
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  const int64_t H = xc.size(-1), M = xc.numel() / H;
+  TORCH_CHECK(H % 8 == 0 && H <= 16384, "layer_norm hidden size must be a multiple of 8");
+  Tensor out = at::empty_like(xc);
+  if (M > 0) illm::launch_layer_norm(bf16, p16(xc), p16o(w), p16o(b), m16(out), (int)M, (int)H, (float)eps, cur_stream());
+  return out;
+}
+
+void rope_kv(const Tensor& qkv, Tensor& q_out, Tensor& k_cache, Tensor& v_cache, const Tensor& slots,
+             const Tensor& pos, const Tensor& inv_freq, const c10::optional<Tensor>& q_norm,
+             const c10::optional<Tensor>& k_norm, double norm_eps, double q_scale, int64_t Hq,
+             int64_t Hkv, int64_t D, int64_t rot_dim, bool interleaved, int64_t kv_fp8,
+             double k_scale, double v_scale) {
+  c10::DeviceGuard g(qkv.device());
+  const bool bf16 = is_bf16(qkv);
+  TORCH_CHECK(qkv.stride(-1) == 1, "qkv last dim must be contiguous");
+  const int64_t T = qkv.numel() / qkv.size(-1);
+  TORCH_CHECK(slots.scalar_type() == at::kLong && pos.scalar_type() == at::kLong, "slots/pos int64");
+  TORCH_CHECK(inv_freq.scalar_type() == at::kFloat, "inv_freq must be f32");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == Hkv && k_cache.size(3) == D, "k_cache must be [nblocks, Hkv, bs, D]");
+  illm::RopeKVArgs a{};
+  a.qkv = p16(qkv);
+  a.ld_qkv = (int)qkv.size(-1);
+  a.q_out = m16(q_out);
+  a.k_cache = (uint8_t*)k_cache.data_ptr();
+  a.v_cache = (uint8_t*)v_cache.data_ptr();
+  a.slots = slots.data_ptr<int64_t>();
+  a.pos = pos.data_ptr<int64_t>();
+  if (inv_freq.dim() == 3) {
+    TORCH_CHECK(inv_freq.size(1) == rot_dim / 2 && inv_freq.size(2) == 2, "cos_sin table must be [P, rot/2, 2]");
+    a.cos_sin = inv_freq.data_ptr<float>();
+  } else {
+    a.inv_freq = inv_freq.data_ptr<float>();
+  }
+  a.q_norm = p16o(q_norm);
+  a.k_norm = p16o(k_norm);
+  a.norm_eps = (float)norm_eps;
+  a.attn_scale_q = (float)q_scale;
+  a.T = (int)T;
+  a.Hq = (int)Hq;
+  a.Hkv = (int)Hkv;
+  a.D = (int)D;
+  a.rot_dim = (int)rot_dim;
+  a.bs = (int)k_cache.size(2);
+  a.interleaved = interleaved;
+  a.kv_fp8 = (int)kv_fp8;
+  a.k_scale = (float)k_scale;
+  a.v_scale = (float)v_scale;
+  if (T > 0) illm::launch_rope_kv(bf16, a, cur_stream());
+}
+
+Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                   const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
+                   int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& alibi) {
+  c10::DeviceGuard g(q.device());
+  const bool bf16 = is_bf16(q);
+  TORCH_CHECK(q.dim() == 4 && q.is_contiguous(), "q must be contiguous [B, Tq, Hq, D]");
+  const int64_t B = q.size(0), Tq = q.size(1), Hq = q.size(2), D = q.size(3);
+  const int64_t Hkv = k_cache.size(1), bs = k_cache.size(2);
+  TORCH_CHECK(Hq % Hkv == 0 && (Hq / Hkv) * Tq <= 16, "attn_decode: (Hq/Hkv)*Tq must be <= 16");
+  TORCH_CHECK(bs % 64 == 0, "KV block size must be a multiple of 64");
+  TORCH_CHECK(D == 64 || D == 80 || D == 96 || D == 128 || D == 256, "unsupported head_dim ", D);
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt, "int32 tables");
+  illm::AttnDecodeArgs a{};
+  Tensor po = at::empty({B, Hq, Tq, nsplit, D}, q.options().dtype(at::kFloat));
+  Tensor pml = at::empty({B, Hq, Tq, nsplit, 2}, q.options().dtype(at::kFloat));
+  Tensor out = at::empty_like(q);
+  a.q = p16(q);
+  a.k_cache = (const uint8_t*)k_cache.data_ptr();
+  a.v_cache = (const uint8_t*)v_cache.data_ptr();
+  a.block_tables = block_tables.data_ptr<int32_t>();
+  a.seq_lens = seq_lens.data_ptr<int32_t>();
+  a.max_blocks = (int)block_tables.size(1);
+  a.part_o = po.data_ptr<float>();
+  a.part_ml = pml.data_ptr<float>();
+  a.out = m16(out);
+  a.B = (int)B;
+  a.Tq = (int)Tq;
+  a.Hq = (int)Hq;
+  a.Hkv = (int)Hkv;
+  a.D = (int)D;
+  a.bs = (int)bs;
+  a.nsplit = (int)nsplit;
+  a.scale = (float)scale;
+  a.softcap = (float)softcap;
+  a.sliding_window = (int)window;
+  a.kv_fp8 = (int)kv_fp8;
+  a.k_scale = (float)k_scale;
+  a.v_scale = (float)v_scale;
+  a.alibi = (alibi.has_value() && alibi->defined()) ? alibi->data_ptr<float>() : nullptr;
+  illm::launch_attn_decode(bf16, a, cur_stream());
+  return out;
+}
+
+Tensor glu(const Tensor& gu, int64_t act) {
+  c10::DeviceGuard g(gu.device());
+  const bool bf16 = is_bf16(gu);
+  Tensor x = gu.contiguous();
+  const int64_t I2 = x.size(-1), M = x.numel() / I2, I = I2 / 2;
+  TORCH_CHECK(I % 8 == 0, "glu: intermediate size must be a multiple of 8");
+  auto shape = x.sizes().vec();
+  shape.back() = I;
+  Tensor out = at::empty(shape, x.options());
+  if (M > 0) illm::launch_glu(bf16, p16(x), (int)I2, m16(out), (int)M, (int)I, (int)act, cur_stream());
+  return out;
+}
+
+Tensor reduce_partials(const Tensor& ws, const c10::optional<Tensor>& bias, at::ScalarType dt) {
+  c10::DeviceGuard g(ws.device());
+  const int64_t ks = ws.size(0), M = ws.size(1), N = ws.size(2);
+  Tensor out = at::empty({M, N}, ws.options().dtype(dt));
+  illm::launch_reduce_partials(dt == at::kBFloat16, ws.data_ptr<float>(), (int)ks, p16o(bias), m16(out),
+                               (int)M, (int)N, (int)N, cur_stream());
+  return out;
+}
+
+std::tuple<Tensor, Tensor> moe_topk(const Tensor& logits, int64_t k, bool renorm, int64_t scoring) {
+  c10::DeviceGuard g(logits.device());
+  Tensor l = logits.to(at::kFloat).contiguous();
+  const int64_t E = l.size(-1), T = l.numel() / E;
+  TORCH_CHECK(E <= 512 && k <= E, "moe_topk: E <= 512");
+  Tensor w = at::empty({T, k}, l.options());
+  Tensor ids = at::empty({T, k}, l.options().dtype(at::kInt));
+  if (T > 0) illm::launch_moe_topk(l.data_ptr<float>(), (int)T, (int)E, (int)k, renorm, (int)scoring,
+                                   w.data_ptr<float>(), ids.data_ptr<int32_t>(), cur_stream());
+  return {w, ids};
+}
+
+}  // namespace
+
+TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
+  m.impl("quantize_device", &quantize_device);
+  m.impl("dequantize_device", &dequantize_device);
+  m.impl("gemv", &gemv);
+  m.impl("add_rms_norm", &add_rms_norm);
+  m.impl("layer_norm", &layer_norm);
+  m.impl("rope_kv", &rope_kv);
+  m.impl("attn_decode", &attn_decode);
+  m.impl("glu", &glu);
+  m.impl("reduce_partials", &reduce_partials);
+  m.impl("moe_topk", &moe_topk);
+}

@@ -1,0 +1,239 @@
+"""Decode-step execution with hipGraph capture + a generate() loop.
+
+The reference issues ~300 kernel launches per token eagerly from Python and
+has no graph capture (vLLM runs --enforce-eager).  Here the
+whole decode step -- embedding, all layers, lm_head and greedy argmax --
+is captured once per (batch, max_blocks) into a hipGraph via
+``torch.cuda.CUDAGraph`` (HIP graphs on ROCm) and replayed per token.  The
+step advances its own position counter on the device, derives the KV slot
+from the block table on the device, and feeds its argmax back as the next
+input, so back-to-back replays need no host<->device traffic at all.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..models.cache import PagedKVCache, SequenceState, make_block_table, slots_for
+from ..models.decoder import AttnMeta, NativeCausalLM
+
+SPLIT = 64
+
+
+def nsplit_for(max_len: int) -> int:
+    return max(1, (max_len + SPLIT - 1) // SPLIT)
+
+
+class DecodeStep:
+    """Static-buffer decode step (B sequences, 1 new token each)."""
+
+    def __init__(self, model: NativeCausalLM, cache: PagedKVCache, block_tables: torch.Tensor,
+                 max_len: int, greedy: bool = True, use_graph: bool = True):
+        self.model, self.cache = model, cache
+        dev = model.device
+        self.B = block_tables.shape[0]
+        self.block_tables = block_tables.to(dev, torch.int32).contiguous()
+        self.ids = torch.zeros(self.B, dtype=torch.long, device=dev)
+        self.pos = torch.zeros(self.B, dtype=torch.long, device=dev)
+        self.nsplit = nsplit_for(max_len)
+        self.greedy = greedy
+        self.logits: Optional[torch.Tensor] = None
+        self.next_ids = torch.zeros(self.B, dtype=torch.long, device=dev)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.use_graph = use_graph and dev.type == "cuda"
+
+    def _body(self):
+        bs = self.cache.bs
+        blk = torch.gather(self.block_tables, 1, (self.pos // bs).unsqueeze(1)).squeeze(1).long()
+        slots = blk * bs + self.pos % bs
+        seq_lens = (self.pos + 1).to(torch.int32)
+        meta = AttnMeta(self.B, 1, self.block_tables, seq_lens, self.nsplit)
+        logits = self.model.forward_tokens(self.ids, self.pos, slots, meta, self.cache)
+        self.logits = logits
+        if self.greedy:
+            nxt = torch.argmax(logits, dim=-1)
+            self.next_ids.copy_(nxt)
+            self.ids.copy_(nxt)
+        self.pos.add_(1)
+
+    def capture(self):
+        if not self.use_graph:
+            return
+        # warm up on a side stream (allocator + kernel JIT), then capture.
+        # The warm-up really executes (writes K/V): point it at the last slot
+        # of each sequence's allocation, which generation never reaches.
+        ids0, pos0 = self.ids.clone(), self.pos.clone()
+        self.pos.fill_(self.block_tables.shape[1] * self.cache.bs - 1)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._body()
+        torch.cuda.current_stream().wait_stream(s)
+        self.ids.copy_(ids0)
+        self.pos.fill_(self.block_tables.shape[1] * self.cache.bs - 1)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._body()
+        # capture does not execute; restore state written by warm-up
+        self.ids.copy_(ids0)
+        self.pos.copy_(pos0)
+
+    def set_state(self, ids: torch.Tensor, pos: torch.Tensor):
+        self.ids.copy_(ids)
+        self.pos.copy_(pos)
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._body()
+        return self.next_ids
+
+
+@dataclass
+class GenTiming:
+    first_cost: float = 0.0            # s, prefill + first token
+    rest_costs: List[float] = field(default_factory=list)
+
+    @property
+    def rest_cost_mean(self) -> float:
+        return sum(self.rest_costs) / max(1, len(self.rest_costs))
+
+
+def _sample(logits: torch.Tensor, do_sample: bool, temperature: float, top_k: int, top_p: float,
+            generator=None) -> torch.Tensor:
+    if not do_sample:
+        return torch.argmax(logits, dim=-1)
+    x = logits.float() / max(temperature, 1e-5)
+    if top_k and top_k > 0:
+        kth = torch.topk(x, min(top_k, x.shape[-1]), dim=-1).values[..., -1:]
+        x = x.masked_fill(x < kth, float("-inf"))
+    if top_p and top_p < 1.0:
+        sx, si = torch.sort(x, descending=True, dim=-1)
+        cp = torch.softmax(sx, -1).cumsum(-1)
+        drop = cp - torch.softmax(sx, -1) > top_p
+        sx = sx.masked_fill(drop, float("-inf"))
+        x = torch.full_like(x, float("-inf")).scatter(-1, si, sx)
+    return torch.multinomial(torch.softmax(x, -1), 1, generator=generator).squeeze(-1)
+
+
+def apply_repetition_penalty(logits, seqs, penalty):
+    if penalty == 1.0:
+        return logits
+    for b, s in enumerate(seqs):
+        idx = torch.tensor(sorted(set(s)), device=logits.device, dtype=torch.long)
+        sc = logits[b, idx]
+        logits[b, idx] = torch.where(sc > 0, sc / penalty, sc * penalty)
+    return logits
+
+
+class Engine:
+    """Owns a model + KV cache; runs prefill and (graph) decode."""
+
+    def __init__(self, model: NativeCausalLM, block_size: int = 64, kv_fp8: int = 0):
+        self.model = model
+        self.block_size = block_size
+        self.kv_fp8 = kv_fp8
+        self._steps: Dict[Tuple[int, int], DecodeStep] = {}
+        self.cache: Optional[PagedKVCache] = None
+        self._cache_key = None
+
+    def _ensure_cache(self, batch: int, max_len: int):
+        blocks = batch * ((max_len + self.block_size - 1) // self.block_size)
+        if self.cache is None or self.cache.num_blocks < blocks:
+            self.cache = self.model.make_cache(max_len, batch, self.block_size, self.kv_fp8, num_blocks=blocks)
+            self._steps.clear()
+        else:
+            self.cache.allocator = type(self.cache.allocator)(self.cache.num_blocks)
+        return self.cache
+
+    @torch.no_grad()
+    def prefill(self, seq: SequenceState, ids: torch.Tensor, start: int = 0) -> torch.Tensor:
+        """Run ids (1-D) for one sequence from position ``start``; returns last logits [1, V]."""
+        m, c = self.model, self.cache
+        dev = m.device
+        n = ids.numel()
+        pos = torch.arange(start, start + n, device=dev)
+        slots = slots_for(seq, start, n, c.bs).to(dev)
+        L = start + n
+        bt = make_block_table([seq], len(seq.blocks), dev)
+        meta = AttnMeta(1, n, bt, torch.tensor([L], dtype=torch.int32, device=dev), nsplit_for(L), [L])
+        logits = m.forward_tokens(ids.to(dev), pos, slots, meta, c,
+                                  logits_idx=torch.tensor([n - 1], device=dev))
+        seq.length = L
+        return logits
+
+    @torch.no_grad()
+    def decode_step_obj(self, seqs: List[SequenceState], max_len: int, greedy: bool, use_graph: bool):
+        key = (len(seqs), max(len(s.blocks) for s in seqs), greedy, use_graph)
+        st = self._steps.get(key)
+        bt = make_block_table(seqs, key[1], self.model.device)
+        if st is None:
+            st = DecodeStep(self.model, self.cache, bt, key[1] * self.block_size, greedy, use_graph)
+            st.capture()
+            self._steps[key] = st
+        else:
+            st.block_tables.copy_(bt)
+        return st
+
+    @torch.no_grad()
+    def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int = 32, min_new_tokens: int = 0,
+                 do_sample: bool = False, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
+                 repetition_penalty: float = 1.0, eos_token_id=None, streamer=None, use_graph: bool = True,
+                 timing: Optional[GenTiming] = None, generator=None) -> List[List[int]]:
+        dev = self.model.device
+        B = len(prompts)
+        max_len = max(len(p) for p in prompts) + max_new_tokens + 1
+        self._ensure_cache(B, max_len)
+        nblk = (max_len + self.block_size - 1) // self.block_size
+        seqs = [SequenceState(self.cache.allocator.alloc(nblk)) for _ in range(B)]
+        eos = set([eos_token_id] if isinstance(eos_token_id, int) else (eos_token_id or []))
+        sync = (lambda: torch.cuda.synchronize()) if dev.type == "cuda" else (lambda: None)
+        t0 = time.perf_counter()
+        last = []
+        for b, p in enumerate(prompts):
+            lg = self.prefill(seqs[b], torch.tensor(list(p), dtype=torch.long))
+            lg = apply_repetition_penalty(lg, [list(p)], repetition_penalty)
+            last.append(_sample(lg, do_sample, temperature, top_k, top_p, generator))
+        cur = torch.cat(last).to(dev)
+        out = [list(p) for p in prompts]
+        done = [False] * B
+        toks = cur.tolist()
+        for b in range(B):
+            out[b].append(toks[b])
+            done[b] = toks[b] in eos and min_new_tokens <= 1
+        sync()
+        if timing is not None:
+            timing.first_cost = time.perf_counter() - t0
+        if streamer is not None:
+            streamer.put(torch.tensor(toks))
+        greedy = not do_sample and repetition_penalty == 1.0
+        st = self.decode_step_obj(seqs, max_len, greedy, use_graph)
+        st.set_state(cur, torch.tensor([s.length for s in seqs], device=dev))
+        for i in range(1, max_new_tokens):
+            if all(done):
+                break
+            t1 = time.perf_counter()
+            nxt = st.step()
+            if not greedy:
+                lg = apply_repetition_penalty(st.logits.clone(), out, repetition_penalty)
+                nxt = _sample(lg, do_sample, temperature, top_k, top_p, generator)
+                st.ids.copy_(nxt)
+            toks = nxt.tolist()
+            if timing is not None:
+                timing.rest_costs.append(time.perf_counter() - t1)
+            for b in range(B):
+                if not done[b]:
+                    out[b].append(toks[b])
+                    if toks[b] in eos and i + 1 >= min_new_tokens:
+                        done[b] = True
+            if streamer is not None:
+                streamer.put(torch.tensor(toks))
+        if streamer is not None:
+            streamer.end()
+        for s in seqs:
+            self.cache.allocator.release(s.blocks)
+        return out

@@ -1,0 +1,185 @@
+"""Build a :class:`NativeCausalLM` from an HF config / model / state dict.
+
+* ``spec_from_config``     HF config -> DecoderSpec (per model_type quirks)
+* ``native_from_hf``       converted HF model -> NativeCausalLM sharing its
+                           (already low-bit) modules -- the ``_optimize_post``
+                           step of the reference (convert.py:1275-2139)
+* ``random_native_model``  random-init weights generated and quantized on
+                           the GPU layer by layer (BASELINE: synthetic data /
+                           random-init weights; an 8B model builds in seconds)
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..quantize import qtypes as Q
+from ..transformers.low_bit_linear import LowBitLinear, DenseLinear
+from .decoder import (DecoderSpec, NativeAttention, NativeCausalLM, NativeLayer, NativeMLP,
+                      compute_inv_freq, interleave_glu_rows)
+
+# model types executed by the native decoder (others fall back to the HF
+# forward with low-bit linears, like the reference does for e.g. mixtral)
+NATIVE_DENSE = {"llama", "mistral", "qwen2", "qwen3", "gemma", "gemma2", "phi3", "internlm2", "yi",
+                "aquila", "starcoder2_llama", "olmo2", "granite", "deepseek", "minicpm", "stablelm",
+                "baichuan", "yuan"}
+NATIVE_MOE = {"mixtral", "qwen2_moe", "qwen3_moe"}
+
+
+def _get(cfg, *names, default=None):
+    for n in names:
+        v = getattr(cfg, n, None)
+        if v is not None:
+            return v
+    return default
+
+
+def spec_from_config(cfg) -> DecoderSpec:
+    mt = getattr(cfg, "model_type", "llama")
+    H = cfg.hidden_size
+    nh = cfg.num_attention_heads
+    nkv = _get(cfg, "num_key_value_heads", default=nh)
+    hd = _get(cfg, "head_dim", default=H // nh) or H // nh
+    prf = _get(cfg, "partial_rotary_factor", default=1.0)
+    act_name = _get(cfg, "hidden_act", "hidden_activation", default="silu")
+    spec = DecoderSpec(
+        model_type=mt, hidden_size=H, num_layers=cfg.num_hidden_layers, num_heads=nh, num_kv_heads=nkv,
+        head_dim=hd, intermediate_size=_get(cfg, "intermediate_size", default=4 * H),
+        vocab_size=cfg.vocab_size, rms_eps=_get(cfg, "rms_norm_eps", "layer_norm_eps", default=1e-6),
+        rot_dim=int(hd * prf), max_position=_get(cfg, "max_position_embeddings", default=8192),
+        qkv_bias=bool(_get(cfg, "attention_bias", default=mt in ("qwen2", "qwen2_moe"))),
+        mlp_bias=bool(_get(cfg, "mlp_bias", default=False)),
+        qk_norm=mt in ("qwen3", "qwen3_moe", "olmo2"),
+        act=0 if "silu" in str(act_name) or "swish" in str(act_name) else 1,
+        tie_embeddings=bool(_get(cfg, "tie_word_embeddings", default=False)),
+    )
+    if mt in ("qwen2", "qwen2_moe"):
+        spec.qkv_bias = True
+    if mt in ("gemma", "gemma2", "gemma3_text"):
+        spec.embed_scale = math.sqrt(H)
+        spec.norm_unit_offset = True
+        spec.tie_embeddings = True
+    if mt in ("gemma2", "gemma3_text"):
+        spec.sandwich_norm = True
+        spec.attn_softcap = _get(cfg, "attn_logit_softcapping", default=0.0) or 0.0
+        spec.final_softcap = _get(cfg, "final_logit_softcapping", default=0.0) or 0.0
+        qps = _get(cfg, "query_pre_attn_scalar", default=None)
+        if qps:
+            spec.query_scale = qps ** -0.5
+    sw = _get(cfg, "sliding_window", default=None)
+    use_sw = _get(cfg, "use_sliding_window", default=mt in ("mistral", "mixtral", "gemma2", "phi3"))
+    if sw and use_sw:
+        spec.sliding_window = int(sw)
+        if mt == "gemma2":  # alternate local / global layers
+            spec.sliding_window_layers = [(i % 2 == 0) for i in range(spec.num_layers)]
+    if mt in NATIVE_MOE:
+        spec.num_experts = _get(cfg, "num_local_experts", "num_experts", default=0)
+        spec.top_k = _get(cfg, "num_experts_per_tok", default=2)
+        spec.moe_intermediate = _get(cfg, "moe_intermediate_size", default=spec.intermediate_size)
+        spec.norm_topk = bool(_get(cfg, "norm_topk_prob", default=mt == "mixtral"))
+        spec.shared_expert_intermediate = _get(cfg, "shared_expert_intermediate_size", default=0) or 0
+        step = _get(cfg, "decoder_sparse_step", default=1) or 1
+        only = _get(cfg, "mlp_only_layers", default=[]) or []
+        spec.moe_layer_mask = [(i not in only) and ((i + 1) % step == 0) for i in range(spec.num_layers)]
+    return spec
+
+
+def lowbit_from_dense(w: torch.Tensor, qtype, device, bias: Optional[torch.Tensor] = None,
+                      imatrix=None) -> nn.Module:
+    qtype = Q.resolve_qtype(qtype)
+    if Q.is_dense(qtype):
+        dt = torch.bfloat16 if qtype == Q.BF16 else torch.float16
+        m = DenseLinear(w.shape[1], w.shape[0], bias is not None, dt, "meta")
+        m.weight = nn.Parameter(w.to(device, dt), requires_grad=False)
+        if bias is not None:
+            m.bias = nn.Parameter(bias.to(device, dt), requires_grad=False)
+        return m
+    m = LowBitLinear(w.shape[1], w.shape[0], qtype, bias=False, device="meta")
+    m.load_dense(w, device=device, imatrix=imatrix)
+    if bias is not None:
+        m.bias = nn.Parameter(bias.detach().to(device), requires_grad=False)
+    return m
+
+
+@torch.no_grad()
+def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat16, seed: int = 0,
+                        lm_head_qtype=None, std: float = 0.02) -> NativeCausalLM:
+    """Random-init model of ``cfg``'s architecture, quantized on ``device``."""
+    spec = spec_from_config(cfg)
+    s = spec
+    g = torch.Generator(device=device).manual_seed(seed)
+
+    def rnd(*shape, scale=std):
+        return (torch.randn(*shape, generator=g, device=device, dtype=torch.float32) * scale).to(dtype)
+
+    def ones_ish(n):
+        return (1.0 + rnd(n, scale=0.02).float()).to(dtype) if not s.norm_unit_offset else rnd(n, scale=0.02)
+
+    nq, nkv = s.num_heads * s.head_dim, s.num_kv_heads * s.head_dim
+    layers = []
+    for _ in range(s.num_layers):
+        wqkv = rnd(nq + 2 * nkv, s.hidden_size)
+        bqkv = rnd(nq + 2 * nkv) if s.qkv_bias else None
+        qkv = lowbit_from_dense(wqkv, qtype, device, bqkv)
+        del wqkv
+        o = lowbit_from_dense(rnd(s.hidden_size, nq), qtype, device)
+        gu = lowbit_from_dense(interleave_glu_rows(rnd(s.intermediate_size, s.hidden_size),
+                                                   rnd(s.intermediate_size, s.hidden_size)), qtype, device)
+        down = lowbit_from_dense(rnd(s.hidden_size, s.intermediate_size), qtype, device)
+        attn = NativeAttention(s, qkv, o, ones_ish(s.head_dim) if s.qk_norm else None,
+                               ones_ish(s.head_dim) if s.qk_norm else None, s.sliding_window)
+        layers.append(NativeLayer(s, attn, NativeMLP(s, gu, down), ones_ish(s.hidden_size),
+                                  ones_ish(s.hidden_size)))
+        torch.cuda.empty_cache() if torch.device(device).type == "cuda" else None
+    embed = rnd(s.vocab_size, s.hidden_size)
+    head_w = embed if s.tie_embeddings else rnd(s.vocab_size, s.hidden_size)
+    lm_head = lowbit_from_dense(head_w, lm_head_qtype or qtype, device)
+    inv_freq, att_scale = compute_inv_freq(cfg, s.head_dim, s.rot_dim or s.head_dim)
+    s.rope_attention_scaling = att_scale
+    model = NativeCausalLM(s, embed, layers, ones_ish(s.hidden_size), lm_head, inv_freq.to(device), dtype)
+    return model.eval()
+
+
+def _module_weight(m: nn.Module):
+    return m.weight if not isinstance(m, LowBitLinear) else None
+
+
+def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
+    """Wrap a converted HF CausalLM (qkv_proj / gate_up_proj merged by
+    ``_optimize_pre``, linears already low-bit) into a NativeCausalLM that
+    shares its parameters.  Returns None for unsupported layouts."""
+    cfg = hf_model.config
+    spec = spec_from_config(cfg)
+    base = getattr(hf_model, "model", None)
+    if base is None or not hasattr(base, "layers"):
+        return None
+    layers = []
+    for i, L in enumerate(base.layers):
+        at = L.self_attn
+        if not hasattr(at, "qkv_proj") or not hasattr(L.mlp, "gate_up_proj"):
+            return None
+        qn = getattr(at, "q_norm", None)
+        kn = getattr(at, "k_norm", None)
+        sw = spec.sliding_window
+        if spec.sliding_window_layers is not None:
+            sw = spec.sliding_window if spec.sliding_window_layers[i] else 0
+        attn = NativeAttention(spec, at.qkv_proj, at.o_proj, qn.weight.data if qn is not None else None,
+                               kn.weight.data if kn is not None else None, sw)
+        mlp = NativeMLP(spec, L.mlp.gate_up_proj, L.mlp.down_proj)
+        pre_ff = getattr(L, "pre_feedforward_layernorm", None)
+        post_ff = getattr(L, "post_feedforward_layernorm", None)
+        layers.append(NativeLayer(spec, attn, mlp, L.input_layernorm.weight.data,
+                                  L.post_attention_layernorm.weight.data,
+                                  pre_ff.weight.data if pre_ff is not None else None,
+                                  post_ff.weight.data if post_ff is not None else None))
+    emb = base.embed_tokens.weight.data
+    lm_head = hf_model.get_output_embeddings()
+    inv_freq, att_scale = compute_inv_freq(cfg, spec.head_dim, spec.rot_dim or spec.head_dim)
+    spec.rope_attention_scaling = att_scale
+    model = NativeCausalLM(spec, emb, layers, base.norm.weight.data, lm_head, inv_freq.to(emb.device),
+                           dtype or emb.dtype)
+    return model.eval()

@@ -1,0 +1,326 @@
+"""Native decoder-only LM executed on the ipex_llm_amd kernels.
+
+One arch-spec-driven implementation covers the llama family the reference
+optimizes with per-model forwards (``SRC/transformers/models/llama.py``,
+``mistral``, ``qwen2.py``, ``qwen3.py``, ``gemma.py``, ``gemma2.py``,
+``phi3.py``, ``yuan``/``internlm2``-style fused projections, ``mixtral`` /
+``qwen2_moe`` / ``qwen3_moe.py`` MoE blocks ...).  Differences between those
+models are data (``DecoderSpec``), not code.
+
+Per layer and decode step the GPU work is:
+  rms_norm(+residual)          add_rms_norm kernel (fused with the previous
+                               projection's split-K partial reduction)
+  qkv projection               low-bit skinny GEMM (MFMA)
+  RoPE + KV append             rope_kv kernel (paged cache, device positions)
+  attention                    flash-decoding kernel over the paged cache
+  o projection                 low-bit skinny GEMM -> f32 split-K partials
+  gate/up + SiLU*up            low-bit skinny GEMM with the GLU epilogue
+  down projection              low-bit skinny GEMM -> partials -> next norm
+so the whole step is ~9 launches per layer, no host synchronisation, and is
+captured once per (batch, max_len bucket) as a hipGraph (engine/graph.py).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import reference as R
+from ..transformers.low_bit_linear import LowBitLinear, DenseLinear
+
+
+@dataclass
+class DecoderSpec:
+    model_type: str
+    hidden_size: int
+    num_layers: int
+    num_heads: int
+    num_kv_heads: int
+    head_dim: int
+    intermediate_size: int
+    vocab_size: int
+    rms_eps: float = 1e-6
+    rot_dim: Optional[int] = None
+    rope_interleaved: bool = False
+    max_position: int = 8192
+    qkv_bias: bool = False
+    o_bias: bool = False
+    mlp_bias: bool = False
+    qk_norm: bool = False
+    act: int = 0                      # 0 silu, 1 gelu(tanh)
+    tie_embeddings: bool = False
+    embed_scale: float = 1.0
+    norm_unit_offset: bool = False
+    sliding_window: int = 0
+    sliding_window_layers: Optional[List[bool]] = None
+    attn_softcap: float = 0.0
+    final_softcap: float = 0.0
+    sandwich_norm: bool = False
+    query_scale: Optional[float] = None
+    rope_attention_scaling: float = 1.0
+    # MoE
+    num_experts: int = 0
+    top_k: int = 0
+    moe_intermediate: int = 0
+    norm_topk: bool = True
+    shared_expert_intermediate: int = 0
+    moe_layer_mask: Optional[List[bool]] = None
+
+    @property
+    def scale(self) -> float:
+        return self.query_scale if self.query_scale is not None else 1.0 / math.sqrt(self.head_dim)
+
+    def is_moe_layer(self, i: int) -> bool:
+        if self.num_experts <= 0:
+            return False
+        return True if self.moe_layer_mask is None else self.moe_layer_mask[i]
+
+
+def compute_inv_freq(hf_config, head_dim: int, rot_dim: int):
+    """inv_freq (+ attention scaling) via the HF rope registry when present."""
+    try:
+        from transformers.modeling_rope_utils import ROPE_INIT_FUNCTIONS
+        params = getattr(hf_config, "rope_parameters", None) or getattr(hf_config, "rope_scaling", None) or {}
+        rtype = params.get("rope_type", params.get("type", "default")) if isinstance(params, dict) else "default"
+        if rtype != "default" and rtype in ROPE_INIT_FUNCTIONS:
+            inv, scale = ROPE_INIT_FUNCTIONS[rtype](hf_config, "cpu")
+            return inv.float(), float(scale)
+        theta = params.get("rope_theta", None) if isinstance(params, dict) else None
+    except Exception:  # pragma: no cover - transformers layout differences
+        theta = None
+    theta = theta or getattr(hf_config, "rope_theta", 10000.0)
+    inv = 1.0 / (theta ** (torch.arange(0, rot_dim, 2, dtype=torch.float32) / rot_dim))
+    return inv, 1.0
+
+
+@dataclass
+class AttnMeta:
+    """Per-step attention metadata; all tensors are device tensors."""
+    B: int
+    Tq: int
+    block_tables: torch.Tensor      # int32 [B, max_blocks]
+    seq_lens: torch.Tensor          # int32 [B] (keys incl. the new tokens)
+    nsplit: int
+    seq_lens_host: Optional[List[int]] = None
+
+
+def interleave_glu_rows(gate: torch.Tensor, up: torch.Tensor, tile: int = 16) -> torch.Tensor:
+    """[I, K] gate + [I, K] up -> [2I, K] with 16-row tiles alternating
+    (gate tile p, up tile p, ...): the layout the GLU-epilogue GEMV expects."""
+    I, K = gate.shape
+    assert I % tile == 0, "intermediate size must be a multiple of 16"
+    return torch.stack([gate.view(I // tile, tile, K), up.view(I // tile, tile, K)], 1).reshape(2 * I, K)
+
+
+def deinterleave_glu(gu: torch.Tensor, tile: int = 16):
+    shp = gu.shape[:-1]
+    I = gu.shape[-1] // 2
+    x = gu.reshape(-1, I // tile, 2, tile)
+    return x[:, :, 0].reshape(*shp, I), x[:, :, 1].reshape(*shp, I)
+
+
+def _ksplit(n: int, k: int) -> int:
+    nt, kc = (n + 15) // 16, (k + 127) // 128
+    ks = 1
+    while nt * ks < 768 and kc >= 4 * 2 * (ks * 2):
+        ks *= 2
+    return ks
+
+
+class NativeAttention(nn.Module):
+    def __init__(self, spec: DecoderSpec, qkv_proj: nn.Module, o_proj: nn.Module,
+                 q_norm: Optional[torch.Tensor] = None, k_norm: Optional[torch.Tensor] = None,
+                 sliding_window: int = 0):
+        super().__init__()
+        self.spec = spec
+        self.qkv_proj, self.o_proj = qkv_proj, o_proj
+        self.q_norm = nn.Parameter(q_norm, requires_grad=False) if q_norm is not None else None
+        self.k_norm = nn.Parameter(k_norm, requires_grad=False) if k_norm is not None else None
+        self.sliding_window = sliding_window
+
+
+class NativeMLP(nn.Module):
+    """gate_up_proj holds the tile-interleaved [gate; up] rows."""
+
+    def __init__(self, spec: DecoderSpec, gate_up_proj: nn.Module, down_proj: nn.Module):
+        super().__init__()
+        self.spec = spec
+        self.gate_up_proj, self.down_proj = gate_up_proj, down_proj
+
+
+class NativeLayer(nn.Module):
+    def __init__(self, spec, attn, mlp, ln1, ln2, pre_ff=None, post_ff=None):
+        super().__init__()
+        self.self_attn, self.mlp = attn, mlp
+        self.input_layernorm = nn.Parameter(ln1, requires_grad=False)
+        self.post_attention_layernorm = nn.Parameter(ln2, requires_grad=False)
+        self.pre_feedforward_layernorm = nn.Parameter(pre_ff, requires_grad=False) if pre_ff is not None else None
+        self.post_feedforward_layernorm = nn.Parameter(post_ff, requires_grad=False) if post_ff is not None else None
+
+
+def linear(x: torch.Tensor, mod: nn.Module) -> torch.Tensor:
+    return mod(x)
+
+
+class NativeCausalLM(nn.Module):
+    def __init__(self, spec: DecoderSpec, embed: torch.Tensor, layers: List[NativeLayer], norm: torch.Tensor,
+                 lm_head: nn.Module, inv_freq: torch.Tensor, dtype=torch.bfloat16):
+        super().__init__()
+        self.spec = spec
+        self.dtype = dtype
+        self.embed_tokens = nn.Parameter(embed, requires_grad=False)
+        self.layers = nn.ModuleList(layers)
+        self.norm = nn.Parameter(norm, requires_grad=False)
+        self.lm_head = lm_head
+        self.register_buffer("inv_freq", inv_freq.float(), persistent=False)
+        self.rope_cache: Optional[torch.Tensor] = None
+        self.tp_group = None
+
+    def ensure_rope_cache(self, max_pos: int):
+        """f32 [max_pos, rot/2, 2] cos/sin table (HF fp32 formula, incl. the
+        rope attention scaling) so the RoPE kernel does a lookup, not sincos."""
+        if self.rope_cache is not None and self.rope_cache.shape[0] >= max_pos and \
+                self.rope_cache.device == self.inv_freq.device:
+            return self.rope_cache
+        n = max(max_pos, 256)
+        pos = torch.arange(n, device=self.inv_freq.device, dtype=torch.float32)
+        freqs = pos[:, None] * self.inv_freq[None, :]
+        sc = self.spec.rope_attention_scaling
+        self.rope_cache = torch.stack([freqs.cos() * sc, freqs.sin() * sc], -1).contiguous()
+        return self.rope_cache
+
+    @property
+    def device(self):
+        return self.embed_tokens.device
+
+    # ------------------------------------------------------------------ cache
+    def make_cache(self, max_tokens: int, batch: int = 1, block_size: int = 64, kv_fp8: int = 0,
+                   num_blocks: Optional[int] = None):
+        from .cache import PagedKVCache
+        s = self.spec
+        nblk = num_blocks or batch * ((max_tokens + block_size - 1) // block_size)
+        self.ensure_rope_cache(max_tokens + 1)
+        return PagedKVCache(s.num_layers, nblk, s.num_kv_heads, s.head_dim, block_size, self.dtype,
+                            self.device, kv_fp8)
+
+    # ------------------------------------------------------------------ pieces
+    def _attention(self, li: int, attn: NativeAttention, q: torch.Tensor, meta: AttnMeta, cache) -> torch.Tensor:
+        s = self.spec
+        T = q.shape[0]
+        group = s.num_heads // s.num_kv_heads
+        softcap = s.attn_softcap
+        window = attn.sliding_window
+        kc, vc = cache.k[li], cache.v[li]
+        if meta.Tq * group <= 16:
+            o = ops.attn_decode(q.view(meta.B, meta.Tq, s.num_heads, s.head_dim), kc, vc, meta.block_tables,
+                                meta.seq_lens, meta.nsplit, s.scale, softcap, window, cache.kv_fp8,
+                                cache.k_scale, cache.v_scale, None, meta.seq_lens_host)
+            return o.view(T, s.num_heads * s.head_dim)
+        # prefill / long query chunk: gather the sequence's keys and use SDPA
+        lens = meta.seq_lens_host if meta.seq_lens_host is not None else meta.seq_lens.tolist()
+        qv = q.view(meta.B, meta.Tq, s.num_heads, s.head_dim)
+        outs = []
+        for b in range(meta.B):
+            L = int(lens[b])
+            kk = ops.api.gather_kv(kc, meta.block_tables, b, L, cache.kv_fp8, cache.k_scale, q.dtype)
+            vv = ops.api.gather_kv(vc, meta.block_tables, b, L, cache.kv_fp8, cache.v_scale, q.dtype)
+            if softcap or not q.is_cuda:
+                outs.append(R.attention(qv[b:b + 1], kk[None], vv[None], True, s.scale, softcap, window))
+                continue
+            qq = qv[b].transpose(0, 1)[None]                 # [1, Hq, Tq, D]
+            k4 = kk.transpose(0, 1)[None]
+            v4 = vv.transpose(0, 1)[None]
+            Tq = qq.shape[2]
+            if Tq == L and not window:
+                o = F.scaled_dot_product_attention(qq, k4, v4, is_causal=True, scale=s.scale, enable_gqa=True)
+            else:
+                qpos = (L - Tq) + torch.arange(Tq, device=q.device)
+                kpos = torch.arange(L, device=q.device)
+                mask = kpos[None, :] <= qpos[:, None]
+                if window:
+                    mask &= kpos[None, :] > (qpos[:, None] - window)
+                o = F.scaled_dot_product_attention(qq, k4, v4, attn_mask=mask, scale=s.scale, enable_gqa=True)
+            outs.append(o[0].transpose(0, 1)[None])
+        return torch.cat(outs, 0).reshape(T, s.num_heads * s.head_dim)
+
+    def _proj_residual_norm(self, x, proj, residual, norm_w, post_norm_w=None):
+        """residual += proj(x); return rms_norm(residual) * norm_w."""
+        s = self.spec
+        fused = (x.is_cuda and isinstance(proj, LowBitLinear) and proj.bias is None and proj.mp_group is None
+                 and post_norm_w is None and x.shape[0] <= ops.GEMV_MAX_M and self.tp_group is None)
+        if fused:
+            part = ops.gemv_partials(x, proj.weight, proj.fmt, proj.out_features, proj.in_features, 0)
+            out, _ = ops.add_rms_norm(None, residual, norm_w, s.rms_eps, partials=part,
+                                      unit_offset=s.norm_unit_offset)
+            return out
+        y = proj(x)
+        if self.tp_group is not None and not getattr(proj, "mp_group", None):
+            from ..parallel.comm import all_reduce_inplace
+            y = all_reduce_inplace(y, self.tp_group)
+        if post_norm_w is not None:
+            y = ops.rms_norm(y, post_norm_w, s.rms_eps, s.norm_unit_offset)
+        out, _ = ops.add_rms_norm(y.contiguous(), residual, norm_w, s.rms_eps, unit_offset=s.norm_unit_offset)
+        return out
+
+    def _mlp(self, x, mlp: nn.Module):
+        s = self.spec
+        if not isinstance(mlp, NativeMLP):
+            return mlp(x)                                   # MoE / custom block returns down-proj input
+        gu = mlp.gate_up_proj
+        if x.is_cuda and isinstance(gu, LowBitLinear) and gu.bias is None and x.shape[0] <= ops.GEMV_MAX_M \
+                and ops.native_gpu(x):
+            return ops.gemv_glu(x, gu.weight, gu.fmt, gu.out_features, gu.in_features, s.act)
+        y = gu(x)
+        g, u = deinterleave_glu(y)
+        a = F.silu(g) if s.act == 0 else F.gelu(g, approximate="tanh")
+        return (a * u).contiguous()
+
+    # ------------------------------------------------------------------ forward
+    def forward_tokens(self, ids: torch.Tensor, pos: torch.Tensor, slots: torch.Tensor, meta: AttnMeta,
+                       cache, logits_idx: Optional[torch.Tensor] = None, return_hidden: bool = False):
+        """ids/pos/slots: [T] (T = B * Tq, sequence-major).  Returns logits
+        [len(logits_idx) or T, vocab] in f32."""
+        s = self.spec
+        h = F.embedding(ids, self.embed_tokens)
+        if s.embed_scale != 1.0:
+            h = h * torch.tensor(s.embed_scale, dtype=h.dtype, device=h.device)
+        residual = h.contiguous()
+        x = ops.rms_norm(residual, self.layers[0].input_layernorm, s.rms_eps, s.norm_unit_offset)
+        T = ids.shape[0]
+        rope = self.rope_cache if self.rope_cache is not None else self.inv_freq
+        for li, layer in enumerate(self.layers):
+            attn = layer.self_attn
+            qkv = attn.qkv_proj(x)
+            q = torch.empty(T, s.num_heads, s.head_dim, dtype=qkv.dtype, device=qkv.device)
+            ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,
+                        s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved, attn.q_norm, attn.k_norm,
+                        s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale, cache.v_scale)
+            a = self._attention(li, attn, q, meta, cache)
+            if s.sandwich_norm:
+                x = self._proj_residual_norm(a, attn.o_proj, residual, layer.pre_feedforward_layernorm,
+                                             post_norm_w=layer.post_attention_layernorm)
+            else:
+                x = self._proj_residual_norm(a, attn.o_proj, residual, layer.post_attention_layernorm)
+            act = self._mlp(x, layer.mlp)
+            nxt = self.layers[li + 1].input_layernorm if li + 1 < len(self.layers) else self.norm
+            if isinstance(layer.mlp, NativeMLP):
+                x = self._proj_residual_norm(act, layer.mlp.down_proj, residual, nxt,
+                                             post_norm_w=layer.post_feedforward_layernorm)
+            else:
+                y = act
+                if layer.post_feedforward_layernorm is not None:
+                    y = ops.rms_norm(y, layer.post_feedforward_layernorm, s.rms_eps, s.norm_unit_offset)
+                x, _ = ops.add_rms_norm(y.contiguous(), residual, nxt, s.rms_eps, unit_offset=s.norm_unit_offset)
+        if return_hidden:
+            return x
+        if logits_idx is not None:
+            x = x.index_select(0, logits_idx)
+        logits = self.lm_head(x.contiguous())
+        if s.final_softcap:
+            logits = torch.tanh(logits.float() / s.final_softcap) * s.final_softcap
+        return logits.float()

@@ -1,0 +1,78 @@
+"""Fake (meta) implementations of the native ops, so torch.compile / export
+and meta-device shape propagation can trace through them."""
+from __future__ import annotations
+
+import torch
+from torch.library import register_fake
+
+from ..quantize.qtypes import FMT_ASYM_INT4, FMT_ASYM_INT5
+from .reference import dev_sizes
+
+
+def _dev_total(fmt, n, k):
+    c, s = dev_sizes(fmt, n, k)
+    return c + 2 * s * (2 if fmt in (FMT_ASYM_INT4, FMT_ASYM_INT5) else 1)
+
+
+@register_fake("ipex_llm_amd::quantize_device")
+def _(w, fmt, scale_search):
+    return w.new_empty((_dev_total(fmt, w.shape[0], w.shape[1]),), dtype=torch.uint8)
+
+
+@register_fake("ipex_llm_amd::dequantize_device")
+def _(blob, fmt, n, k, dtype):
+    return blob.new_empty((n, k), dtype=dtype)
+
+
+@register_fake("ipex_llm_amd::gemv")
+def _(x, blob, fmt, n, k, bias, epi, ksplit, act):
+    M = x.numel() // k
+    if epi == 1:
+        return x.new_empty((max(ksplit, 1), M, n), dtype=torch.float32)
+    shape = list(x.shape)
+    shape[-1] = n // 2 if epi == 2 else n
+    return x.new_empty(shape)
+
+
+@register_fake("ipex_llm_amd::add_rms_norm")
+def _(x, partials, residual, w, eps, unit_offset, store_residual):
+    if x is not None:
+        return torch.empty_like(x)
+    if residual is not None:
+        return torch.empty_like(residual)
+    return w.new_empty((partials.shape[1], w.shape[0]))
+
+
+@register_fake("ipex_llm_amd::layer_norm")
+def _(x, w, b, eps):
+    return torch.empty_like(x)
+
+
+@register_fake("ipex_llm_amd::rope_kv")
+def _(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, q_norm, k_norm, norm_eps, q_scale, Hq, Hkv,
+      D, rot_dim, interleaved, kv_fp8, k_scale, v_scale):
+    return None
+
+
+@register_fake("ipex_llm_amd::attn_decode")
+def _(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, kv_fp8, k_scale,
+      v_scale, alibi):
+    return torch.empty_like(q)
+
+
+@register_fake("ipex_llm_amd::glu")
+def _(gu, act):
+    shape = list(gu.shape)
+    shape[-1] //= 2
+    return gu.new_empty(shape)
+
+
+@register_fake("ipex_llm_amd::reduce_partials")
+def _(ws, bias, dtype):
+    return ws.new_empty(ws.shape[1:], dtype=dtype)
+
+
+@register_fake("ipex_llm_amd::moe_topk")
+def _(logits, k, renorm, scoring):
+    T = logits.numel() // logits.shape[-1]
+    return logits.new_empty((T, k), dtype=torch.float32), logits.new_empty((T, k), dtype=torch.int32)

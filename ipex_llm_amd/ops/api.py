@@ -1,0 +1,216 @@
+"""Typed entry points over ``torch.ops.ipex_llm_amd`` with device dispatch.
+
+GPU tensors always go to the HIP kernels (see ``ops.native_gpu``); CPU
+tensors use the C++ host library where one exists (quantizers, low-bit GEMM)
+and the torch references otherwise.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import reference as R
+
+__all__ = [
+    "quantize", "dequantize", "repack_to_device", "repack_from_device", "lowbit_matmul",
+    "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
+    "attn_decode", "glu", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
+]
+
+
+def _ops():
+    from . import require
+    return require()
+
+
+def _native(t: torch.Tensor) -> bool:
+    from . import native_gpu
+    return native_gpu(t)
+
+
+# ------------------------------------------------------------ quantization
+def quantize(w: torch.Tensor, fmt: int, imatrix: Optional[torch.Tensor] = None,
+             scale_search: bool = False) -> torch.Tensor:
+    """Dense [n, k] -> packed blob.  GPU input -> MI355X tiled layout
+    (quantized on device); CPU input -> canonical planar layout (C++)."""
+    if _native(w) and imatrix is None:
+        return _ops().quantize_device(w, fmt, scale_search)
+    if w.is_cuda:
+        return _ops().repack_to_device(_ops().quantize_cpu(w.cpu(), fmt, imatrix, scale_search),
+                                       fmt, w.shape[0], w.shape[1]).to(w.device)
+    return _ops().quantize_cpu(w, fmt, imatrix, scale_search)
+
+
+def dequantize(blob: torch.Tensor, fmt: int, n: int, k: int, dtype=torch.float32,
+               device_layout: Optional[bool] = None) -> torch.Tensor:
+    device_layout = blob.is_cuda if device_layout is None else device_layout
+    if device_layout:
+        if _native(blob) and dtype in (torch.bfloat16, torch.float16):
+            return _ops().dequantize_device(blob, fmt, n, k, dtype)
+        return R.dequantize_device_blob(blob, fmt, n, k).to(dtype)
+    if blob.is_cuda:
+        return R.dequantize_canonical(blob, fmt, n, k).to(dtype)
+    return _ops().dequantize_cpu(blob, fmt, n, k).to(dtype)
+
+
+def repack_to_device(canon: torch.Tensor, fmt: int, n: int, k: int) -> torch.Tensor:
+    return _ops().repack_to_device(canon.cpu(), fmt, n, k)
+
+
+def repack_from_device(dev: torch.Tensor, fmt: int, n: int, k: int) -> torch.Tensor:
+    return _ops().repack_from_device(dev.cpu(), fmt, n, k)
+
+
+def to_fp8_bytes(x: torch.Tensor, e5m2: bool) -> torch.Tensor:
+    return _ops().to_fp8_bytes(x.cpu(), e5m2)
+
+
+# ------------------------------------------------------------ low-bit GEMM
+GEMV_MAX_M = 64
+
+
+def lowbit_matmul(x: torch.Tensor, blob: torch.Tensor, fmt: int, n: int, k: int,
+                  bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ W^T (+ bias) for a packed weight W[n, k]."""
+    if x.is_cuda:
+        if _native(x):
+            M = x.numel() // k
+            if M <= GEMV_MAX_M:
+                return _ops().gemv(x, blob, fmt, n, k, bias, 0, 0, 0)
+            from .gemm import lowbit_gemm
+            return lowbit_gemm(x, blob, fmt, n, k, bias)
+        w = R.dequantize_device_blob(blob, fmt, n, k).to(x.dtype)
+        return F.linear(x, w, bias)
+    y = _ops().linear_cpu(x, blob, fmt, n, k)
+    if bias is not None:
+        y = y + bias.float()
+    return y.to(x.dtype)
+
+
+def gemv_partials(x, blob, fmt, n, k, ksplit: int) -> torch.Tensor:
+    """f32 split-K partial slabs [ksplit, M, n] (summed by add_rms_norm)."""
+    return _ops().gemv(x, blob, fmt, n, k, None, 1, ksplit, 0)
+
+
+def gemv_glu(x, blob, fmt, n, k, act: int = 0) -> torch.Tensor:
+    """act(x @ Wg^T) * (x @ Wu^T) for a tile-interleaved gate/up weight."""
+    return _ops().gemv(x, blob, fmt, n, k, None, 2, 1, act)
+
+
+def reduce_partials(ws, bias=None, dtype=torch.bfloat16):
+    return _ops().reduce_partials(ws, bias, dtype)
+
+
+# ------------------------------------------------------------ norms / act
+def add_rms_norm(x: Optional[torch.Tensor], residual: Optional[torch.Tensor], w: torch.Tensor,
+                 eps: float, partials: Optional[torch.Tensor] = None,
+                 unit_offset: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """residual += x (or the sum of GEMV partials); returns (rms_norm(residual), residual).
+    On GPU the residual is updated in place."""
+    if _native(w):
+        out = _ops().add_rms_norm(x, partials, residual, w, eps, unit_offset, True)
+        return out, residual
+    if partials is not None:
+        x = partials.sum(0).to(w.dtype).view_as(residual) if residual is not None else partials.sum(0).to(w.dtype)
+    normed, new_res = R.add_rms_norm(x, residual, w, eps, unit_offset)
+    if residual is not None:
+        residual.copy_(new_res)
+    return normed, residual
+
+
+def rms_norm(x, w, eps, unit_offset=False):
+    if _native(x):
+        return _ops().add_rms_norm(x.contiguous(), None, None, w, eps, unit_offset, False)
+    return R.rms_norm(x, w, eps, unit_offset)
+
+
+def layer_norm(x, w, b, eps):
+    if _native(x) and x.shape[-1] % 8 == 0:
+        return _ops().layer_norm(x, w, b, eps)
+    return R.layer_norm(x, w, b, eps)
+
+
+def glu(gu, act=0):
+    if _native(gu) and (gu.shape[-1] // 2) % 8 == 0:
+        return _ops().glu(gu, act)
+    return R.glu(gu, act)
+
+
+def moe_topk(logits, k, renorm=True, scoring=0):
+    if _native(logits) and logits.shape[-1] <= 512:
+        return _ops().moe_topk(logits, k, renorm, scoring)
+    return R.moe_topk(logits, k, renorm, scoring)
+
+
+# ------------------------------------------------------------ attention
+def rope_kv(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, Hq, Hkv, D, rot_dim=None,
+            interleaved=False, q_norm=None, k_norm=None, norm_eps=1e-6, q_scale=1.0,
+            kv_fp8=0, k_scale=1.0, v_scale=1.0):
+    """Rotate q/k of a fused QKV projection, write q to q_out [T, Hq, D] and
+    k/v into the paged cache [nblocks, Hkv, bs, D] at ``slots``."""
+    rot_dim = rot_dim or D
+    if _native(qkv):
+        _ops().rope_kv(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, q_norm, k_norm, norm_eps,
+                       q_scale, Hq, Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale)
+        return q_out
+    T = qkv.numel() // qkv.shape[-1]
+    x = qkv.reshape(T, Hq + 2 * Hkv, D)
+    q, k, v = x[:, :Hq], x[:, Hq:Hq + Hkv], x[:, Hq + Hkv:]
+    if q_norm is not None:
+        q = R.rms_norm(q, q_norm, norm_eps)
+    if k_norm is not None:
+        k = R.rms_norm(k, k_norm, norm_eps)
+    if inv_freq.dim() == 3:  # precomputed [P, rot/2, 2] table
+        cs = inv_freq[pos.long()]
+        cos = torch.cat([cs[..., 0]] * 2, -1).to(qkv.dtype)
+        sin = torch.cat([cs[..., 1]] * 2, -1).to(qkv.dtype)
+    else:
+        cos, sin = R.rope_cos_sin(pos, inv_freq[: rot_dim // 2], qkv.dtype)
+    if interleaved:
+        cos = torch.cat([cos[:, : rot_dim // 2]] * 2, -1)
+        sin = torch.cat([sin[:, : rot_dim // 2]] * 2, -1)
+    q = R.apply_rope(q, cos, sin, interleaved, rot_dim)
+    k = R.apply_rope(k, cos, sin, interleaved, rot_dim)
+    q_out.view(T, Hq, D).copy_(q * q_scale if q_scale != 1.0 else q)
+    bs = k_cache.shape[2]
+    ok = slots >= 0
+    s = slots[ok]
+    blk, off = s // bs, s % bs
+    if kv_fp8:
+        k_cache[blk, :, off] = to_fp8_bytes((k[ok] / k_scale).float(), kv_fp8 == 1).to(k_cache.device)
+        v_cache[blk, :, off] = to_fp8_bytes((v[ok] / v_scale).float(), kv_fp8 == 1).to(v_cache.device)
+    else:
+        k_cache[blk, :, off] = k[ok].to(k_cache.dtype)
+        v_cache[blk, :, off] = v[ok].to(v_cache.dtype)
+    return q_out
+
+
+def gather_kv(cache, block_tables, b, L, kv_fp8=0, scale=1.0, dtype=torch.bfloat16):
+    """[L, Hkv, D] view of sequence b's cached keys/values (reference path)."""
+    bs = cache.shape[2]
+    nblk = (L + bs - 1) // bs
+    blks = block_tables[b, :nblk].long()
+    x = cache[blks].permute(0, 2, 1, 3).reshape(nblk * bs, cache.shape[1], cache.shape[3])[:L]
+    if kv_fp8:
+        tab = R.code_table(6 if kv_fp8 == 1 else 5).to(x.device)
+        x = (tab[x.long()] * scale).to(dtype)
+    return x
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap=0.0, window=0,
+                kv_fp8=0, k_scale=1.0, v_scale=1.0, alibi=None, seq_lens_host=None):
+    """q [B, Tq, Hq, D] against the paged cache -> [B, Tq, Hq, D]."""
+    if _native(q):
+        return _ops().attn_decode(q.contiguous(), k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
+                                  softcap, window, kv_fp8, k_scale, v_scale, alibi)
+    B = q.shape[0]
+    lens = seq_lens_host if seq_lens_host is not None else seq_lens.tolist()
+    outs = []
+    for b in range(B):
+        L = int(lens[b])
+        kk = gather_kv(k_cache, block_tables, b, L, kv_fp8, k_scale, q.dtype)
+        vv = gather_kv(v_cache, block_tables, b, L, kv_fp8, v_scale, q.dtype)
+        outs.append(R.attention(q[b:b + 1], kk[None], vv[None], True, scale, softcap, window, None, alibi))
+    return torch.cat(outs, 0)

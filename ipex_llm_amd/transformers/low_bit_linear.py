@@ -1,0 +1,264 @@
+"""Low-bit linear layers (the FP4Params / LowBitLinear equivalents).
+
+Reference: ``SRC/transformers/low_bit_linear.py`` -- ``FP4Params`` (332-491),
+``MatMulLowBit`` (532-602), ``LowBitLinear`` (605-755), ``FP16Linear`` /
+``BF16Linear`` (758-948).
+
+MI355X design:
+  * the packed weight is ONE uint8 blob per layer (codes | fp16 scales |
+    fp16 mins).  On the host it is kept in the canonical planar layout (what
+    checkpoints store); on the GPU in the MFMA-fragment tiled layout of
+    ``csrc/common/formats.h``.  ``Module._apply`` converts between the two
+    when the module changes device, so ``model.to("cuda")`` just works;
+  * quantization is lazy: a dense weight placed with ``LowBitLinear.from_linear``
+    is quantized on the device it lands on (C++ on the host, a HIP kernel on
+    the GPU, so loading an 8B model quantizes in well under a second);
+  * forward dispatches to the HIP skinny-GEMM (M <= 64) / GEMM kernels or to
+    the C++ CPU GEMM;
+  * training: ``MatMulLowBit`` gives ``grad_x`` through an on-device dequant
+    (the base weight is frozen, as in QLoRA).
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..quantize import qtypes as Q
+
+
+def _dev_total(fmt, n, k):
+    from ..ops.reference import dev_sizes
+    c, s = dev_sizes(fmt, n, k)
+    return c + 2 * s * (2 if fmt in (Q.FMT_ASYM_INT4, Q.FMT_ASYM_INT5) else 1)
+
+
+def _canon_total(fmt, n, k):
+    from ..ops.reference import canon_sizes
+    c, s = canon_sizes(fmt, n, k)
+    return c + 2 * s * (2 if fmt in (Q.FMT_ASYM_INT4, Q.FMT_ASYM_INT5) else 1)
+
+
+class MatMulLowBit(torch.autograd.Function):
+    """y = x W^T with a frozen low-bit W; backward gives grad_x only
+    (reference: low_bit_linear.py:532-602)."""
+
+    @staticmethod
+    def forward(ctx, x, blob, fmt, n, k, layer):
+        ctx.fmt, ctx.n, ctx.k = fmt, n, k
+        ctx.save_for_backward(blob)
+        ctx.xdtype = x.dtype
+        return ops.lowbit_matmul(x, blob, fmt, n, k)
+
+    @staticmethod
+    def backward(ctx, grad_y):
+        (blob,) = ctx.saved_tensors
+        grad_x = None
+        if ctx.needs_input_grad[0]:
+            dt = grad_y.dtype if grad_y.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16
+            w = ops.dequantize(blob, ctx.fmt, ctx.n, ctx.k, dtype=dt)
+            grad_x = torch.matmul(grad_y.to(w.dtype), w).to(ctx.xdtype)
+        return grad_x, None, None, None, None, None
+
+
+class LowBitLinear(nn.Module):
+    """nn.Linear replacement holding a packed low-bit weight."""
+
+    def __init__(self, in_features: int, out_features: int, qtype="sym_int4", bias: bool = True,
+                 device=None, dtype=None, mp_group=None, enable_xetla=False, optimize_lm_head=False,
+                 act_order=False, enable_scale_search=False):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.qtype = Q.resolve_qtype(qtype)
+        fmt = Q.get_format(self.qtype)
+        if fmt is None:
+            raise ValueError(f"{Q.qtype_name(self.qtype)} is a dense type; use FP16Linear/BF16Linear")
+        self.fmt = fmt.fmt
+        if in_features % fmt.k_align:
+            raise ValueError(f"in_features={in_features} must be a multiple of {fmt.k_align}")
+        device = torch.device(device) if device is not None else torch.device("cpu")
+        nbytes = _dev_total(self.fmt, out_features, in_features) if device.type == "cuda" else \
+            _canon_total(self.fmt, out_features, in_features)
+        self.weight = nn.Parameter(torch.zeros(nbytes, dtype=torch.uint8, device=device), requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(out_features, dtype=dtype or torch.float32, device=device)) \
+            if bias else None
+        self.mp_group = mp_group          # row-parallel TP group: all-reduce after the GEMM
+        self.optimize_lm_head = optimize_lm_head
+        self.act_order = act_order
+        self.g_idx_map = None             # GPTQ act-order input permutation
+        self.enable_scale_search = enable_scale_search
+        self.compute_dtype = None
+
+    # ------------------------------------------------------------ construction
+    @classmethod
+    @torch.no_grad()
+    def from_linear(cls, linear: nn.Module, qtype="sym_int4", device=None, imatrix=None,
+                    enable_scale_search=False, mp_group=None, optimize_lm_head=False):
+        w = linear.weight.data
+        n, k = w.shape
+        dev = torch.device(device) if device is not None else w.device
+        m = cls(k, n, qtype, bias=getattr(linear, "bias", None) is not None, device="meta",
+                mp_group=mp_group, optimize_lm_head=optimize_lm_head, enable_scale_search=enable_scale_search)
+        m.load_dense(w, device=dev, imatrix=imatrix)
+        if linear.bias is not None:
+            m.bias = nn.Parameter(linear.bias.data.detach().to(dev).clone(), requires_grad=False)
+        return m
+
+    @torch.no_grad()
+    def load_dense(self, w: torch.Tensor, device=None, imatrix=None):
+        """Quantize a dense [out, in] weight into this module (on ``device``)."""
+        dev = torch.device(device) if device is not None else w.device
+        if dev.type == "cuda":
+            wq = w.to(dev)
+            if wq.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+                wq = wq.float()
+            blob = ops.quantize(wq, self.fmt, imatrix, self.enable_scale_search)
+        else:
+            blob = ops.quantize(w.float().cpu(), self.fmt, imatrix, self.enable_scale_search)
+        self.weight = nn.Parameter(blob, requires_grad=False)
+
+    @property
+    def device_layout(self) -> bool:
+        return self.weight.is_cuda
+
+    def dequantize(self, dtype=torch.float32) -> torch.Tensor:
+        return ops.dequantize(self.weight, self.fmt, self.out_features, self.in_features, dtype)
+
+    def canonical_blob(self) -> torch.Tensor:
+        if self.weight.is_cuda:
+            return ops.repack_from_device(self.weight, self.fmt, self.out_features, self.in_features)
+        return self.weight.data
+
+    # ------------------------------------------------------------ device moves
+    def _apply(self, fn, recurse=True):
+        w = self.weight
+        if w is not None and w.device.type != "meta":
+            probe = fn(torch.empty(0, dtype=torch.uint8, device=w.device))
+            tgt = probe.device
+            if tgt.type != w.device.type:
+                n, k = self.out_features, self.in_features
+                if tgt.type == "cuda":
+                    new = ops.repack_to_device(w.data.cpu(), self.fmt, n, k).to(tgt)
+                else:
+                    new = ops.repack_from_device(w.data, self.fmt, n, k)
+                self.weight = nn.Parameter(new, requires_grad=False)
+                if self.bias is not None:
+                    self.bias = nn.Parameter(fn(self.bias.data), requires_grad=self.bias.requires_grad)
+                return self
+        return super()._apply(fn, recurse)
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        # checkpoints always hold the portable canonical layout
+        destination[prefix + "weight"] = self.canonical_blob().cpu() if not keep_vars else self.weight
+        if self.bias is not None:
+            destination[prefix + "bias"] = self.bias if keep_vars else self.bias.detach()
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        key = prefix + "weight"
+        if key in state_dict:
+            blob = state_dict[key]
+            n, k = self.out_features, self.in_features
+            if blob.dtype != torch.uint8:
+                # a dense checkpoint tensor: quantize it now
+                self.load_dense(blob.view(n, k), device=self.weight.device if self.weight.device.type != "meta" else "cpu")
+            else:
+                blob = blob.reshape(-1)
+                tgt = self.weight.device
+                if blob.numel() != _canon_total(self.fmt, n, k):
+                    error_msgs.append(f"{key}: blob has {blob.numel()} bytes, expected "
+                                      f"{_canon_total(self.fmt, n, k)} for {Q.qtype_name(self.qtype)} [{n}, {k}]")
+                    return
+                if tgt.type == "cuda":
+                    new = ops.repack_to_device(blob, self.fmt, n, k).to(tgt)
+                else:
+                    new = blob.clone()
+                self.weight = nn.Parameter(new, requires_grad=False)
+        elif strict:
+            missing_keys.append(key)
+        bkey = prefix + "bias"
+        if self.bias is not None:
+            if bkey in state_dict:
+                b = state_dict[bkey]
+                dev = self.bias.device if self.bias.device.type != "meta" else self.weight.device
+                self.bias = nn.Parameter(b.detach().to(dev).clone(), requires_grad=False)
+            elif strict:
+                missing_keys.append(bkey)
+
+    # ------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.optimize_lm_head and x.dim() == 3 and x.shape[1] > 10 and not self.training:
+            # last-token-only lm_head (reference: reshape_lm_head_input, :282-289)
+            x = x[:, -1:, :]
+        if self.g_idx_map is not None:
+            x = x.index_select(-1, self.g_idx_map)
+        in_dtype = x.dtype
+        if x.is_cuda and x.dtype not in (torch.bfloat16, torch.float16):
+            x = x.to(self.compute_dtype or torch.float16)
+        bias = self.bias
+        if bias is not None and bias.dtype != x.dtype:
+            bias = bias.to(x.dtype)
+        if self.training and torch.is_grad_enabled() and x.requires_grad:
+            y = MatMulLowBit.apply(x, self.weight, self.fmt, self.out_features, self.in_features, self)
+            if bias is not None:
+                y = y + bias
+        else:
+            y = ops.lowbit_matmul(x, self.weight, self.fmt, self.out_features, self.in_features,
+                                  None if self.mp_group is not None else bias)
+        if self.mp_group is not None:
+            from ..parallel.comm import all_reduce_inplace
+            y = all_reduce_inplace(y, self.mp_group)
+            if bias is not None:
+                y = y + bias
+        return y.to(in_dtype) if y.dtype != in_dtype else y
+
+    def extra_repr(self):
+        return (f"in_features={self.in_features}, out_features={self.out_features}, "
+                f"qtype={Q.qtype_name(self.qtype)}, bias={self.bias is not None}")
+
+
+class DenseLinear(nn.Module):
+    """fp16/bf16 linear (FP16Linear / BF16Linear equivalent) with optional
+    row-parallel all-reduce (reference: low_bit_linear.py:758-948)."""
+
+    def __init__(self, in_features, out_features, bias=True, dtype=torch.float16, device=None, mp_group=None):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features, dtype=dtype, device=device),
+                                   requires_grad=False)
+        self.bias = nn.Parameter(torch.empty(out_features, dtype=dtype, device=device), requires_grad=False) \
+            if bias else None
+        self.mp_group = mp_group
+        self.qtype = Q.BF16 if dtype == torch.bfloat16 else Q.FP16
+
+    @classmethod
+    def from_linear(cls, linear, dtype=torch.float16, device=None, mp_group=None):
+        m = cls(linear.in_features, linear.out_features, linear.bias is not None, dtype, "meta", mp_group)
+        dev = device or linear.weight.device
+        m.weight = nn.Parameter(linear.weight.data.to(dev, dtype), requires_grad=False)
+        if linear.bias is not None:
+            m.bias = nn.Parameter(linear.bias.data.to(dev, dtype), requires_grad=False)
+        return m
+
+    def forward(self, x):
+        y = F.linear(x.to(self.weight.dtype), self.weight, None if self.mp_group else self.bias)
+        if self.mp_group is not None:
+            from ..parallel.comm import all_reduce_inplace
+            y = all_reduce_inplace(y, self.mp_group)
+            if self.bias is not None:
+                y = y + self.bias
+        return y.to(x.dtype)
+
+
+FP16Linear = DenseLinear
+
+
+class BF16Linear(DenseLinear):
+    def __init__(self, in_features, out_features, bias=True, dtype=torch.bfloat16, device=None, mp_group=None):
+        super().__init__(in_features, out_features, bias, torch.bfloat16, device, mp_group)

@@ -1,0 +1,167 @@
+"""Numerics of the gfx950 HIP kernels against plain-PyTorch fp32 references."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from ipex_llm_amd import ops
+from ipex_llm_amd.ops import reference as R
+from ipex_llm_amd.quantize import get_format
+
+FMTS = ["sym_int4", "asym_int4", "nf4", "fp4", "nf3", "sym_int8", "fp8_e4m3", "fp8_e5m2",
+        "sym_int5", "asym_int5", "fp6"]
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("name", FMTS)
+def test_quantize_device_matches_host(cuda, name):
+    f = get_format(name).fmt
+    n, k = 96, 384
+    w = torch.randn(n, k) * 0.05
+    host = ops.repack_to_device(ops.quantize(w, f), f, n, k)
+    dev = torch.ops.ipex_llm_amd.quantize_device(w.to(cuda), f, False).cpu()
+    dq_h = R.dequantize_device_blob(host, f, n, k)
+    dq_d = R.dequantize_device_blob(dev, f, n, k)
+    # identical rounding rules on host and device; allow rare 1-code flips
+    assert (dq_h != dq_d).float().mean().item() < 1e-3
+    assert _rel(dq_d, w) < (0.25 if name == "nf3" else 0.15)
+
+
+@pytest.mark.parametrize("name", FMTS)
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 40])
+@pytest.mark.parametrize("v1", [False, True])
+def test_gemv_formats(cuda, name, dtype, M, v1, monkeypatch):
+    if v1:
+        monkeypatch.setenv("ILLM_GEMV_V1", "1")
+    f = get_format(name).fmt
+    torch.manual_seed(0)
+    for n, k in [(256, 512), (80, 320)]:
+        w = torch.randn(n, k, device=cuda) * 0.05
+        blob = ops.quantize(w, f)
+        x = torch.randn(M, k, device=cuda).to(dtype)
+        ref = R.lowbit_linear_ref(x, blob.cpu(), f, n, k).to(cuda)
+        y = torch.ops.ipex_llm_amd.gemv(x, blob, f, n, k, None, 0, 1, 0)
+        assert y.shape == (M, n) and y.dtype == dtype
+        assert _rel(y, ref) < 1e-2, (name, dtype, M, n, k)
+        ws = torch.ops.ipex_llm_amd.gemv(x, blob, f, n, k, None, 1, 2, 0)
+        # LUT formats carry bf16/f16-rounded code values into the MFMA
+        tol = 5e-3 if name in ("nf4", "nf3") else 1e-3
+        assert _rel(ws.sum(0), ref) < tol
+        b = torch.randn(n, device=cuda).to(dtype)
+        yb = torch.ops.ipex_llm_amd.gemv(x, blob, f, n, k, b, 0, 0, 0)
+        assert _rel(yb, ref + b.float()) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 3, 33])
+def test_gemv_glu(cuda, M):
+    from ipex_llm_amd.models.decoder import interleave_glu_rows
+    I, k = 128, 256
+    g = torch.randn(I, k, device=cuda) * 0.05
+    u = torch.randn(I, k, device=cuda) * 0.05
+    f = get_format("sym_int4").fmt
+    blob = ops.quantize(interleave_glu_rows(g, u), f)
+    x = torch.randn(M, k, device=cuda).bfloat16()
+    full = R.lowbit_linear_ref(x, blob.cpu(), f, 2 * I, k).to(cuda)
+    gg, uu = full.view(M, I // 16, 2, 16)[:, :, 0].reshape(M, I), full.view(M, I // 16, 2, 16)[:, :, 1].reshape(M, I)
+    ref = torch.nn.functional.silu(gg) * uu
+    y = ops.gemv_glu(x, blob, f, 2 * I, k, 0)
+    assert _rel(y, ref) < 2e-2
+
+
+def test_lowbit_gemm_prefill(cuda):
+    f = get_format("sym_int4").fmt
+    n, k, M = 384, 512, 200
+    w = torch.randn(n, k, device=cuda) * 0.05
+    blob = ops.quantize(w, f)
+    x = torch.randn(M, k, device=cuda).bfloat16()
+    ref = R.lowbit_linear_ref(x, blob.cpu(), f, n, k).to(cuda)
+    y = ops.lowbit_matmul(x, blob, f, n, k)
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_add_rms_norm(cuda, dtype):
+    M, H = 7, 4096
+    x = torch.randn(M, H, device=cuda).to(dtype)
+    res = torch.randn(M, H, device=cuda).to(dtype)
+    w = (1 + 0.1 * torch.randn(H, device=cuda)).to(dtype)
+    ref_n, ref_r = R.add_rms_norm(x, res, w, 1e-5)
+    r2 = res.clone()
+    out, _ = ops.add_rms_norm(x, r2, w, 1e-5)
+    assert torch.equal(r2, ref_r)
+    assert _rel(out, ref_n) < 5e-3
+    # partial-slab path
+    parts = torch.randn(4, M, H, device=cuda) * 0.3
+    r3 = res.clone()
+    out2, _ = ops.add_rms_norm(None, r3, w, 1e-5, partials=parts)
+    ref2, rr2 = R.add_rms_norm(parts.sum(0).to(dtype), res, w, 1e-5)
+    assert _rel(r3, rr2) < 5e-3 and _rel(out2, ref2) < 5e-3
+    assert _rel(ops.rms_norm(x, w, 1e-5), R.rms_norm(x, w, 1e-5)) < 5e-3
+
+
+@pytest.mark.parametrize("interleaved", [False, True])
+@pytest.mark.parametrize("kv_fp8", [0, 1])
+def test_rope_kv(cuda, interleaved, kv_fp8):
+    T, Hq, Hkv, D, bs = 5, 8, 2, 128, 64
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=cuda).bfloat16()
+    pos = torch.tensor([0, 3, 17, 100, 1000], device=cuda)
+    slots = torch.tensor([0, 70, 5, 130, 200], device=cuda)
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    store = torch.uint8 if kv_fp8 else torch.bfloat16
+    kc = torch.zeros(4, Hkv, bs, D, device=cuda, dtype=store)
+    vc = torch.zeros_like(kc)
+    q = torch.empty(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.rope_kv(qkv, q, kc, vc, slots, pos, inv, Hq, Hkv, D, interleaved=interleaved, kv_fp8=kv_fp8)
+    kc2, vc2 = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q2 = torch.empty(T, Hq, D, dtype=torch.bfloat16)
+    ops.rope_kv(qkv.cpu(), q2, kc2, vc2, slots.cpu(), pos.cpu(), inv.cpu(), Hq, Hkv, D, interleaved=interleaved,
+                kv_fp8=kv_fp8)
+    assert _rel(q.cpu(), q2) < 1e-2
+    if kv_fp8:
+        tab = R.code_table(6)
+        assert _rel(tab[kc.cpu().long()], tab[kc2.long()]) < 5e-2
+    else:
+        assert _rel(kc.cpu(), kc2) < 1e-2 and torch.equal(vc.cpu(), vc2)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("Tq", [1, 3])
+@pytest.mark.parametrize("kv_fp8", [0, 1])
+def test_attn_decode(cuda, D, Tq, kv_fp8):
+    torch.manual_seed(1)
+    B, Hq, Hkv, bs = 3, 8, 2, 64
+    lens = [5, 130, 700]
+    nblk_per = 12
+    perm = torch.randperm(B * nblk_per)
+    bt = perm.view(B, nblk_per).int().to(cuda)
+    store = torch.uint8 if kv_fp8 else torch.bfloat16
+    if kv_fp8:
+        kc = torch.randint(0, 120, (B * nblk_per, Hkv, bs, D), device=cuda, dtype=torch.uint8)
+        vc = torch.randint(0, 120, (B * nblk_per, Hkv, bs, D), device=cuda, dtype=torch.uint8)
+        kc = kc | (torch.randint(0, 2, kc.shape, device=cuda, dtype=torch.uint8) << 7)
+    else:
+        kc = torch.randn(B * nblk_per, Hkv, bs, D, device=cuda).bfloat16()
+        vc = torch.randn(B * nblk_per, Hkv, bs, D, device=cuda).bfloat16()
+    q = torch.randn(B, Tq, Hq, D, device=cuda).bfloat16()
+    seq = torch.tensor(lens, device=cuda, dtype=torch.int32)
+    nsplit = math.ceil(max(lens) / 64) + 2
+    out = ops.attn_decode(q, kc, vc, bt, seq, nsplit, D ** -0.5, kv_fp8=kv_fp8)
+    for b, L in enumerate(lens):
+        kk = ops.api.gather_kv(kc, bt, b, L, kv_fp8, 1.0, torch.float32)
+        vv = ops.api.gather_kv(vc, bt, b, L, kv_fp8, 1.0, torch.float32)
+        ref = R.attention(q[b:b + 1].float(), kk[None], vv[None], True, D ** -0.5)
+        assert _rel(out[b:b + 1], ref) < 1e-2, (b, L)
+
+
+def test_moe_topk(cuda):
+    logits = torch.randn(9, 64, device=cuda)
+    w, ids = ops.moe_topk(logits, 4, True, 0)
+    rw, rids = R.moe_topk(logits, 4, True, 0)
+    assert torch.equal(ids.cpu(), rids.cpu())
+    assert torch.allclose(w, rw, atol=1e-5)

@@ -1,0 +1,129 @@
+"""Micro-benchmarks of the hot HIP kernels at Llama-3-8B decode shapes.
+
+Prints time per call and effective HBM bandwidth; run on the GPU box:
+    python tools/bench_kernels.py [--m 1,8]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ipex_llm_amd import ops  # noqa: E402
+from ipex_llm_amd.quantize import get_format  # noqa: E402
+
+
+def timeit(fn, iters=50, warm=5, graph=True):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        g.replay()
+        en.record()
+        torch.cuda.synchronize()
+        return st.elapsed_time(en) / iters * 1e3
+    # flush-free but each call streams >= L2 size; use events
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(iters):
+        fn()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", default="1,8")
+    ap.add_argument("--qtype", default="sym_int4")
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    ops.require()
+    f = get_format(args.qtype).fmt
+    res = []
+    shapes = [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
+              ("lm_head", 128256, 4096)]
+    # several copies so consecutive calls do not hit in the 256 MB MALL
+    for M in [int(x) for x in args.m.split(",")]:
+        for name, n, k in shapes:
+            copies = max(1, int(math.ceil(600e6 / (n * k * 0.5))))
+            blobs = [ops.quantize(torch.randn(n, k, device=dev, dtype=torch.bfloat16) * 0.02, f) for _ in range(copies)]
+            x = torch.randn(M, k, device=dev, dtype=torch.bfloat16)
+            nbytes = blobs[0].numel()
+            i = [0]
+
+            def run_store():
+                i[0] = (i[0] + 1) % copies
+                return ops.lowbit_matmul(x, blobs[i[0]], f, n, k)
+
+            def run_part(ks):
+                def r():
+                    i[0] = (i[0] + 1) % copies
+                    return ops.gemv_partials(x, blobs[i[0]], f, n, k, ks)
+                return r
+
+            def run_glu():
+                i[0] = (i[0] + 1) % copies
+                return ops.gemv_glu(x, blobs[i[0]], f, n, k, 0)
+
+            cands = {"store_auto": run_store}
+            for ks in (0, 1, 2, 4, 8):
+                cands[f"partial_ks{ks}"] = run_part(ks)
+            if name == "gate_up":
+                cands["glu"] = run_glu
+            for cn, fn in cands.items():
+                us = timeit(fn)
+                res.append({"M": M, "op": name, "n": n, "k": k, "variant": cn, "us": round(us, 2),
+                            "TBps": round(nbytes / us / 1e6, 3)})
+                print(json.dumps(res[-1]), flush=True)
+            del blobs
+            torch.cuda.empty_cache()
+    # attention decode
+    for B in (1, 8):
+        for L in (1024, 4096):
+            Hq, Hkv, D, bs = 32, 8, 128, 64
+            nblk = B * ((L + bs) // bs + 1)
+            kc = torch.randn(nblk, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
+            vc = torch.randn_like(kc)
+            bt = torch.arange(nblk, device=dev, dtype=torch.int32).view(B, -1)
+            q = torch.randn(B, 1, Hq, D, device=dev, dtype=torch.bfloat16)
+            seq = torch.full((B,), L, device=dev, dtype=torch.int32)
+            ns = (L + 63) // 64
+            us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, seq, ns, D ** -0.5))
+            kvb = 2 * B * Hkv * L * D * 2
+            res.append({"op": "attn_decode", "B": B, "L": L, "us": round(us, 2), "TBps": round(kvb / us / 1e6, 3)})
+            print(json.dumps(res[-1]), flush=True)
+    # norms / rope
+    for M in (1, 8):
+        H = 4096
+        res_ = torch.randn(M, H, device=dev, dtype=torch.bfloat16)
+        w = torch.ones(H, device=dev, dtype=torch.bfloat16)
+        parts = torch.randn(4, M, H, device=dev)
+        us = timeit(lambda: ops.add_rms_norm(None, res_, w, 1e-5, partials=parts))
+        res.append({"op": "add_rms_norm_part4", "M": M, "us": round(us, 2)})
+        print(json.dumps(res[-1]), flush=True)
+        qkv = torch.randn(M, 6144, device=dev, dtype=torch.bfloat16)
+        qo = torch.empty(M, 32, 128, device=dev, dtype=torch.bfloat16)
+        kc = torch.zeros(64, 8, 64, 128, device=dev, dtype=torch.bfloat16)
+        vc = torch.zeros_like(kc)
+        slots = torch.arange(M, device=dev) * 7
+        pos = torch.arange(M, device=dev) + 100
+        tab = torch.randn(4096, 64, 2, device=dev)
+        us = timeit(lambda: ops.rope_kv(qkv, qo, kc, vc, slots, pos, tab, 32, 8, 128))
+        res.append({"op": "rope_kv", "M": M, "us": round(us, 2)})
+        print(json.dumps(res[-1]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
