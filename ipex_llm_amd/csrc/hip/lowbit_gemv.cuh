@@ -322,11 +322,11 @@ __global__ void __launch_bounds__(256) lowbit_gemv_kernel(const GemvArgs a) {
 //     tile-chunk) -> PF = 8 chunks in flight per tile at ~100 VGPRs.
 // Split-K across workgroups (gridDim.y) writes f32 partial slabs.
 // ---------------------------------------------------------------------------
-template <int DK, typename T, int EPI, int TPW>
+template <int DK, typename T, int EPI, int TPW, int PFX = 4>
 __global__ void __launch_bounds__(256) lowbit_gemv2_kernel(const GemvArgs a) {
   constexpr int BITS = dk_bits(DK);
   constexpr bool NEEDX = dk_needx(DK);
-  constexpr int PF = 8 / TPW;
+  constexpr int PF = PFX / TPW;
   extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
   __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -456,10 +456,8 @@ __global__ void __launch_bounds__(256) lowbit_gemv2_kernel(const GemvArgs a) {
   }
 #pragma unroll
   for (int u = 0; u < PF; u++) {
-    if (c + u < c1u) {
-      compute_chunk(ring[u], c + u);
-      if (c + u + PF < c1u) load_chunk(ring[u], c + u + PF);
-    }
+    if (c + u < c1u) compute_chunk(ring[u], c + u);
+    load_chunk(ring[u], c + u + PF);  // clamped: unconditional keeps exact vmcnt counting
   }
   c += PF;
 #pragma unroll
@@ -508,6 +506,13 @@ __global__ void __launch_bounds__(256) lowbit_gemv2_kernel(const GemvArgs a) {
 template <int DK>
 void launch_gemv2_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
 #define L2K(TT, E, TP) hipLaunchKernelGGL((lowbit_gemv2_kernel<DK, TT, E, TP>), grid, dim3(256), shmem, st, a)
+  // tuning experiments: ILLM_GEMV_VARIANT=1 -> PF 8, 2 -> TPW 2 (PF 4 each), 3 -> PF 2
+  static const char* var = getenv("ILLM_GEMV_VARIANT");
+  if (var && bf16 && epi == EPI_PARTIAL) {
+    if (var[0] == '1') { hipLaunchKernelGGL((lowbit_gemv2_kernel<DK, BF16, EPI_PARTIAL, 1, 8>), grid, dim3(256), shmem, st, a); return; }
+    if (var[0] == '2') { dim3 g2((grid.x + 1) / 2, grid.y); hipLaunchKernelGGL((lowbit_gemv2_kernel<DK, BF16, EPI_PARTIAL, 2, 8>), g2, dim3(256), shmem, st, a); return; }
+    if (var[0] == '3') { hipLaunchKernelGGL((lowbit_gemv2_kernel<DK, BF16, EPI_PARTIAL, 1, 2>), grid, dim3(256), shmem, st, a); return; }
+  }
   if (bf16) {
     if (epi == EPI_STORE) L2K(BF16, EPI_STORE, 1);
     else if (epi == EPI_PARTIAL) L2K(BF16, EPI_PARTIAL, 1);
@@ -518,6 +523,512 @@ void launch_gemv2_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs
     else L2K(F16, EPI_GLU, 2);
   }
 #undef L2K
+}
+
+// ---------------------------------------------------------------------------
+// v3 (M <= 16): 4 waves split K, each wave stages ITS x slice in a private
+// LDS region with 16-B vector loads, streams TPW tiles x (its K range) of
+// weights through a PF-deep register ring, and the 4 partial tiles are summed
+// through LDS before a single-pass epilogue.  Many small work units (~8
+// chunks per wave) measured best against the HBM probe
+// (tools/probe/stream_probe.hip): load balance and ramp/drain, not depth,
+// limit GEMV-sized (8-64 MB) streams.
+// ---------------------------------------------------------------------------
+template <int DK, typename T, int EPI, int TPW, int PFX = 4>
+__global__ void __launch_bounds__(256) lowbit_gemv3_kernel(const GemvArgs a) {
+  constexpr int BITS = dk_bits(DK);
+  constexpr bool NEEDX = dk_needx(DK);
+  constexpr int PF = PFX;
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
+  __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // K range of this workgroup (split-K over gridDim.y) and of this wave
+  const int nks = gridDim.y;
+  const int cpk = (a.KC + nks - 1) / nks;
+  const int cw0 = blockIdx.y * cpk;
+  const int cw1 = min(a.KC, cw0 + cpk);
+  const int cpw = (cw1 - cw0 + 3) / 4;
+  const int c0 = __builtin_amdgcn_readfirstlane(min(cw1, cw0 + wave * cpw));
+  const int c1 = __builtin_amdgcn_readfirstlane(min(cw1, c0 + cpw));
+  const int kw = cpw * 128;
+  const int lds_ld = kw + 8;  // +16 B row pad
+  uint16_t* xw = xs + wave * a.M * lds_ld;
+  const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
+  const int tile0 = blockIdx.x * TPW;
+
+  struct Chunk {
+    uint4 q[TPW][BITS / 4];
+    uint4 sc[TPW];
+    uint4 mn[TPW];
+  };
+  auto load_chunk = [&](Chunk& ch, int c) {
+    c = min(c, c1 - 1);
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      const int tile = min(tile0 + t, NT - 1);
+      const size_t tc = (size_t)tile * a.KC + c;
+      if constexpr (BITS == 4) {
+        ch.q[t][0] = *(const uint4*)(a.codes + (tc * 64 + lane) * 16);
+      } else {
+        ch.q[t][0] = *(const uint4*)(a.codes + ((tc * 2 + 0) * 64 + lane) * 16);
+        ch.q[t][1] = *(const uint4*)(a.codes + ((tc * 2 + 1) * 64 + lane) * 16);
+      }
+      ch.sc[t] = *(const uint4*)(a.scales + tc * 32 + g * 8);
+      if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint4*)(a.mins + tc * 32 + g * 8);
+    }
+  };
+  const bool wave_on = c0 < c1;
+  Chunk ring[PF];
+  if (wave_on) {
+#pragma unroll
+    for (int u = 0; u < PF; u++) load_chunk(ring[u], c0 + u);
+    // this wave's x slice -> its private LDS rows (zero beyond K)
+    const int kb = c0 * 128, vpr = (c1 - c0) * 16;
+    for (int v = lane; v < a.M * vpr; v += 64) {
+      const int m = v / vpr, kk = (v % vpr) * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (kb + kk < a.K) val = *(const uint4*)(a.x + (size_t)m * a.ldx + kb + kk);
+      *(uint4*)(xw + m * lds_ld + kk) = val;
+    }
+  }
+  if constexpr (DK == DK_LUT4) {
+    lut2[threadIdx.x] = pack2<T>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  const uint4 ones = make_uint4(Magic<T>::one2, Magic<T>::one2, Magic<T>::one2, Magic<T>::one2);
+  const bool mok = r16 < a.M;
+  const uint16_t* xrow = xw + (mok ? r16 : 0) * lds_ld + 8 * g;
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute_chunk = [&](const Chunk& ch, int c) {
+    const uint16_t* xc = xrow + (c - c0) * 128;
+    uint4 B[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const uint4 v = *(const uint4*)(xc + 32 * s);
+      B[s] = mok ? v : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+#pragma unroll
+      for (int blk = 0; blk < 2; blk++) {
+        f32x4 P = {0.f, 0.f, 0.f, 0.f}, X = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ss = 0; ss < 2; ss++) {
+          const int s = blk * 2 + ss;
+          uint4 A;
+          if constexpr (BITS == 4) {
+            const uint4& q0 = ch.q[t][0];
+            const uint32_t u = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
+            A = decode4<DK, T>(u, lut2);
+          } else {
+            const uint4& qq = ch.q[t][blk];
+            A = ss == 0 ? decode8<DK, T>(qq.x, qq.y) : decode8<DK, T>(qq.z, qq.w);
+          }
+          P = mfma16<T>(A, B[s], P);
+          if constexpr (NEEDX) X = mfma16<T>(ones, B[s], X);
+        }
+        const uint32_t s01 = blk == 0 ? ch.sc[t].x : ch.sc[t].z, s23 = blk == 0 ? ch.sc[t].y : ch.sc[t].w;
+        const float d[4] = {f16_to_f32(s01 & 0xffff), f16_to_f32(s01 >> 16), f16_to_f32(s23 & 0xffff),
+                            f16_to_f32(s23 >> 16)};
+        float mm[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (dk_has_min(DK)) {
+          const uint32_t m01 = blk == 0 ? ch.mn[t].x : ch.mn[t].z, m23 = blk == 0 ? ch.mn[t].y : ch.mn[t].w;
+          mm[0] = f16_to_f32(m01 & 0xffff); mm[1] = f16_to_f32(m01 >> 16);
+          mm[2] = f16_to_f32(m23 & 0xffff); mm[3] = f16_to_f32(m23 >> 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          float cd, cx;
+          block_coef<DK, T>(d[i], mm[i], cd, cx);
+          acc[t][i] += cd * P[i];
+          if constexpr (NEEDX) acc[t][i] += cx * X[i];
+        }
+      }
+    }
+  };
+
+  if (wave_on) {
+    int c = c0;
+    for (; c + 2 * PF <= c1; c += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; u++) {
+        compute_chunk(ring[u], c + u);
+        load_chunk(ring[u], c + u + PF);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PF; u++) {
+      if (c + u < c1) compute_chunk(ring[u], c + u);
+      load_chunk(ring[u], c + u + PF);
+    }
+    c += PF;
+#pragma unroll
+    for (int u = 0; u < PF; u++)
+      if (c + u < c1) compute_chunk(ring[u], c + u);
+  }
+
+  // ---- cross-wave reduction through LDS (reuses the x staging region)
+  __syncthreads();
+  float4* red = (float4*)xs;  // [4 waves][TPW][64 lanes]
+#pragma unroll
+  for (int t = 0; t < TPW; t++) red[(wave * TPW + t) * 64 + lane] = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+  __syncthreads();
+  if (wave != 0) return;
+  float o[TPW][4];
+#pragma unroll
+  for (int t = 0; t < TPW; t++) {
+    float4 s = red[t * 64 + lane];
+#pragma unroll
+    for (int w = 1; w < 4; w++) {
+      const float4 v = red[(w * TPW + t) * 64 + lane];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    o[t][0] = s.x; o[t][1] = s.y; o[t][2] = s.z; o[t][3] = s.w;
+  }
+  const int m = r16;
+  if (m >= a.M) return;
+  if constexpr (EPI == EPI_GLU) {
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) r[i] = (a.act == 0 ? silu_f(o[0][i]) : gelu_tanh_f(o[0][i])) * o[TPW - 1][i];
+    const int n0 = (tile0 / 2) * 16 + 4 * g;
+    if (n0 < a.N) {
+      uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+      if (n0 + 3 < a.N) *(uint2*)y = make_uint2(pack2<T>(r[0], r[1]), pack2<T>(r[2], r[3]));
+      else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(r[i]);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      const int n0 = (tile0 + t) * 16 + 4 * g;
+      if (tile0 + t >= NT || n0 >= a.N) continue;
+      if constexpr (EPI == EPI_PARTIAL) {
+        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
+        if (n0 + 3 < a.N && (a.N & 3) == 0) *(float4*)ws = make_float4(o[t][0], o[t][1], o[t][2], o[t][3]);
+        else for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[t][i];
+      } else {
+        if (a.bias) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[t][i] += (n0 + i < a.N) ? to_f32<T>(a.bias[n0 + i]) : 0.f;
+        }
+        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+        if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0)
+          *(uint2*)y = make_uint2(pack2<T>(o[t][0], o[t][1]), pack2<T>(o[t][2], o[t][3]));
+        else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[t][i]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// v4 (M <= 16): pre-scaled f16 A fragments, one MFMA accumulator per tile.
+// v1-v3 accumulate each 64-element block in a fresh MFMA accumulator and then
+// read it out (v_accvgpr_read) to apply the block scale: a dependent
+// MFMA -> VALU chain per block that, at the ~2 waves/SIMD a GEMV grid gives,
+// is not hidden.  Here the block scale (and min) is applied to the decoded
+// weights with packed f16 VALU (exact (q-8) via the 0x6400 magic, then one
+// rounding of (q-8)*d), so all chunks of a tile chain into ONE accumulator,
+// the all-ones offset MFMA disappears and there is no per-block readout.
+// Activations are converted to f16 while being staged into LDS (clamped to
+// the f16 range), accumulation stays f32, outputs are written in T.
+// ---------------------------------------------------------------------------
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ uint32_t as_u(h2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t bytes01(uint32_t u) { return __builtin_amdgcn_perm(0u, u, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t bytes23(uint32_t u) { return __builtin_amdgcn_perm(0u, u, 0x0c030c02u); }
+
+// scaled A fragment (8 f16) for one k-step; d2 / m2 = (d, d) / (m, m)
+template <int DK>
+__device__ __forceinline__ uint4 scaled_a4(uint32_t u, h2 d2, h2 m2, const uint32_t* lut2) {
+  uint32_t w[4];
+  if constexpr (DK == DK_INT4S || DK == DK_INT4A) {
+    w[0] = (u & 0x000F000Fu) | 0x64006400u;
+    w[1] = ((u >> 4) & 0x000F000Fu) | 0x64006400u;
+    w[2] = ((u >> 8) & 0x000F000Fu) | 0x64006400u;
+    w[3] = ((u >> 12) & 0x000F000Fu) | 0x64006400u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if constexpr (DK == DK_INT4S) w[i] = as_u((as_h2(w[i]) - h2{(_Float16)1032.f, (_Float16)1032.f}) * d2);
+      else w[i] = as_u(__builtin_elementwise_fma(as_h2(w[i]) - h2{(_Float16)1024.f, (_Float16)1024.f}, d2, m2));
+    }
+  } else {
+    if constexpr (DK == DK_FP4) {
+      w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 0));
+      w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 1));
+      w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 2));
+      w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 3));
+    } else {  // DK_LUT4: f16 pair table
+      w[0] = lut2[u & 0xff];
+      w[1] = lut2[(u >> 8) & 0xff];
+      w[2] = lut2[(u >> 16) & 0xff];
+      w[3] = lut2[u >> 24];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = as_u(as_h2(w[i]) * d2);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int DK>
+__device__ __forceinline__ uint4 scaled_a8(uint32_t lo, uint32_t hi, h2 d2, h2 m2) {
+  uint32_t w[4];
+  if constexpr (DK == DK_FP8E4 || DK == DK_FP8E5) {
+    if constexpr (DK == DK_FP8E4) {
+      w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(lo, 1.0f, false));
+      w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(lo, 1.0f, true));
+      w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(hi, 1.0f, false));
+      w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(hi, 1.0f, true));
+    } else {
+      w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(lo, 1.0f, false));
+      w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(lo, 1.0f, true));
+      w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(hi, 1.0f, false));
+      w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(hi, 1.0f, true));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = as_u(as_h2(w[i]) * d2);
+  } else {
+    // bytes -> f16(1024 + byte) via v_perm + magic; signed codes biased by 128
+    if constexpr (DK == DK_INT8S) { lo ^= 0x80808080u; hi ^= 0x80808080u; }
+    w[0] = bytes01(lo) | 0x64006400u;
+    w[1] = bytes23(lo) | 0x64006400u;
+    w[2] = bytes01(hi) | 0x64006400u;
+    w[3] = bytes23(hi) | 0x64006400u;
+    const _Float16 off = DK == DK_INT8S ? (_Float16)1152.f : (_Float16)1024.f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if constexpr (DK == DK_INT8S) w[i] = as_u((as_h2(w[i]) - h2{off, off}) * d2);
+      else w[i] = as_u(__builtin_elementwise_fma(as_h2(w[i]) - h2{off, off}, d2, m2));
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int DK, typename T, int EPI, int TPW, int PF = 4>
+__global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
+  constexpr int BITS = dk_bits(DK);
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
+  __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  const int nks = gridDim.y;
+  const int cpk = (a.KC + nks - 1) / nks;
+  const int c0 = blockIdx.y * cpk;
+  const int c1 = min(a.KC, c0 + cpk);
+  const int kbase = c0 * 128;
+  const int kw = (c1 - c0) * 128;
+  const int lds_ld = kw + 8;
+  const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
+  const int tile0 = (blockIdx.x * 4 + wave) * TPW;
+  const bool wave_on = tile0 < NT && c0 < c1;
+
+  struct Chunk {
+    uint4 q[TPW][BITS / 4];
+    uint4 sc[TPW];
+    uint4 mn[TPW];
+  };
+  auto load_chunk = [&](Chunk& ch, int c) {
+    c = min(c, c1 - 1);
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      const int tile = min(tile0 + t, NT - 1);
+      const size_t tc = (size_t)tile * a.KC + c;
+      if constexpr (BITS == 4) {
+        ch.q[t][0] = *(const uint4*)(a.codes + (tc * 64 + lane) * 16);
+      } else {
+        ch.q[t][0] = *(const uint4*)(a.codes + ((tc * 2 + 0) * 64 + lane) * 16);
+        ch.q[t][1] = *(const uint4*)(a.codes + ((tc * 2 + 1) * 64 + lane) * 16);
+      }
+      // the 16 B holding this lane's A-row (r16) scales for both blocks
+      ch.sc[t] = *(const uint4*)(a.scales + tc * 32 + (r16 >> 2) * 8);
+      if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint4*)(a.mins + tc * 32 + (r16 >> 2) * 8);
+    }
+  };
+  Chunk ring[PF];
+  if (wave_on) {
+#pragma unroll
+    for (int u = 0; u < PF; u++) load_chunk(ring[u], c0 + u);
+  }
+  if constexpr (DK == DK_LUT4) {
+    lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
+  }
+  {  // stage x[0:M, kbase:kbase+kw] -> LDS as f16
+    const int vpr = kw / 8;
+    for (int v = threadIdx.x; v < a.M * vpr; v += 256) {
+      const int m = v / vpr, kk = (v % vpr) * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (kbase + kk < a.K) {
+        val = *(const uint4*)(a.x + (size_t)m * a.ldx + kbase + kk);
+        if constexpr (std::is_same<T, BF16>::value) {
+          uint32_t w[4] = {val.x, val.y, val.z, val.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const float lo = fminf(fmaxf(bf16_to_f32(w[i] & 0xffff), -65504.f), 65504.f);
+            const float hi = fminf(fmaxf(bf16_to_f32(w[i] >> 16), -65504.f), 65504.f);
+            w[i] = pack2<F16>(lo, hi);
+          }
+          val = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+      *(uint4*)(xs + m * lds_ld + kk) = val;
+    }
+  }
+  __syncthreads();
+  if (!wave_on) return;
+
+  const bool mok = r16 < a.M;
+  const uint16_t* xrow = xs + (mok ? r16 : 0) * lds_ld + 8 * g;
+  const int rr = r16 & 3;
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto pick = [&](const uint4& v, int blk) -> h2 {
+    // half (blk*4 + rr) of the 16-B scale group, broadcast to both lanes of an h2
+    const uint32_t wlo = blk == 0 ? v.x : v.z, whi = blk == 0 ? v.y : v.w;
+    const uint32_t w = rr < 2 ? wlo : whi;
+    const uint32_t h = (rr & 1) ? (w >> 16) : (w & 0xffffu);
+    return as_h2(h | (h << 16));
+  };
+  auto compute_chunk = [&](const Chunk& ch, int c) {
+    const uint16_t* xc = xrow + (c - c0) * 128;
+    uint4 B[4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const uint4 v = *(const uint4*)(xc + 32 * s);
+      B[s] = mok ? v : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+#pragma unroll
+      for (int blk = 0; blk < 2; blk++) {
+        const h2 d2 = pick(ch.sc[t], blk);
+        h2 m2 = h2{(_Float16)0.f, (_Float16)0.f};
+        if constexpr (dk_has_min(DK)) m2 = pick(ch.mn[t], blk);
+#pragma unroll
+        for (int ss = 0; ss < 2; ss++) {
+          const int s = blk * 2 + ss;
+          uint4 A;
+          if constexpr (BITS == 4) {
+            const uint4& q0 = ch.q[t][0];
+            const uint32_t u = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
+            A = scaled_a4<DK>(u, d2, m2, lut2);
+          } else {
+            const uint4& qq = ch.q[t][blk];
+            A = ss == 0 ? scaled_a8<DK>(qq.x, qq.y, d2, m2) : scaled_a8<DK>(qq.z, qq.w, d2, m2);
+          }
+          acc[t] = mfma16<F16>(A, B[s], acc[t]);
+        }
+      }
+    }
+  };
+
+  const int c1u = __builtin_amdgcn_readfirstlane(c1);
+  int c = __builtin_amdgcn_readfirstlane(c0);
+  for (; c + 2 * PF <= c1u; c += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; u++) {
+      compute_chunk(ring[u], c + u);
+      load_chunk(ring[u], c + u + PF);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PF; u++) {
+    if (c + u < c1u) compute_chunk(ring[u], c + u);
+    load_chunk(ring[u], c + u + PF);
+  }
+  c += PF;
+#pragma unroll
+  for (int u = 0; u < PF; u++)
+    if (c + u < c1u) compute_chunk(ring[u], c + u);
+
+  // ---- epilogue: lane holds rows 16*tile + 4g + i, column m = r16
+  const int m = r16;
+  if (m >= a.M) return;
+  if constexpr (EPI == EPI_GLU) {
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const float gv = acc[0][i], uv = acc[TPW - 1][i];
+      o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
+    }
+    const int n0 = (tile0 / 2) * 16 + 4 * g;
+    if (n0 < a.N) {
+      uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+      if (n0 + 3 < a.N) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+      else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      const int n0 = (tile0 + t) * 16 + 4 * g;
+      if (tile0 + t >= NT || n0 >= a.N) continue;
+      float o[4] = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
+      if constexpr (EPI == EPI_PARTIAL) {
+        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
+        if (n0 + 3 < a.N && (a.N & 3) == 0) *(float4*)ws = make_float4(o[0], o[1], o[2], o[3]);
+        else for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[i];
+      } else {
+        if (a.bias) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[i] += (n0 + i < a.N) ? to_f32<T>(a.bias[n0 + i]) : 0.f;
+        }
+        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+        if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+        else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+      }
+    }
+  }
+}
+
+template <int DK>
+void launch_gemv4_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+#define L4K(TT, E, TP)                                                                              \
+  do {                                                                                              \
+    static bool attr = false;                                                                       \
+    if (!attr) {                                                                                    \
+      (void)hipFuncSetAttribute((const void*)lowbit_gemv4_kernel<DK, TT, E, TP>,                    \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);            \
+      attr = true;                                                                                  \
+    }                                                                                               \
+    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, TT, E, TP>), grid, dim3(256), shmem, st, a);       \
+  } while (0)
+  if (bf16) {
+    if (epi == EPI_STORE) L4K(BF16, EPI_STORE, 1);
+    else if (epi == EPI_PARTIAL) L4K(BF16, EPI_PARTIAL, 1);
+    else L4K(BF16, EPI_GLU, 2);
+  } else {
+    if (epi == EPI_STORE) L4K(F16, EPI_STORE, 1);
+    else if (epi == EPI_PARTIAL) L4K(F16, EPI_PARTIAL, 1);
+    else L4K(F16, EPI_GLU, 2);
+  }
+#undef L4K
+}
+
+template <int DK>
+void launch_gemv3_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+#define L3K(TT, E, TP) hipLaunchKernelGGL((lowbit_gemv3_kernel<DK, TT, E, TP>), grid, dim3(256), shmem, st, a)
+  if (bf16) {
+    if (epi == EPI_STORE) L3K(BF16, EPI_STORE, 1);
+    else if (epi == EPI_PARTIAL) L3K(BF16, EPI_PARTIAL, 1);
+    else L3K(BF16, EPI_GLU, 2);
+  } else {
+    if (epi == EPI_STORE) L3K(F16, EPI_STORE, 1);
+    else if (epi == EPI_PARTIAL) L3K(F16, EPI_PARTIAL, 1);
+    else L3K(F16, EPI_GLU, 2);
+  }
+#undef L3K
 }
 
 template <int DK, typename T, int MT>

@@ -147,12 +147,58 @@ __global__ void dequantize_device_kernel(int fmt, const uint8_t* blob, int64_t n
   }
 }
 
+// Coalesced variant: one lane per 16-B code vector of the tiled blob (the
+// same lane mapping the GEMV uses), so the code plane is read with full
+// 1 KiB wave loads and each lane writes 8-element (16-B) row segments.
+template <typename T>
+__global__ void __launch_bounds__(256) dequantize_tiled_kernel(int fmt, const uint8_t* blob, int64_t n,
+                                                               int64_t k, uint16_t* out) {
+  const int bits = fmt_bits(fmt);
+  const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
+  const int64_t NT = pad_to(n, TILE_N) / TILE_N;
+  const int64_t vec = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;  // (t, c, [h], lane)
+  const int64_t nvec = NT * KC * (bits == 4 ? 1 : 2) * 64;
+  if (vec >= nvec) return;
+  const int l = (int)(vec & 63);
+  const int64_t tcv = vec >> 6;
+  const int h = bits == 4 ? 0 : (int)(tcv & 1);
+  const int64_t tc = bits == 4 ? tcv : (tcv >> 1);
+  const int64_t t = tc / KC, c = tc % KC;
+  const int r = l & 15, g = l >> 4;
+  const int64_t row = t * TILE_N + r;
+  if (row >= n) return;
+  const uint4 q = *(const uint4*)(blob + vec * 16);
+  const uint16_t* dscale = (const uint16_t*)(blob + dev_code_bytes(fmt, n, k));
+  const uint16_t* dmin = dscale + dev_scale_elems(n, k);
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  // 4-bit: dword s = k-step s (block s/2); 8-bit half h: k-steps 2h, 2h+1 (block h)
+  for (int ss = 0; ss < (bits == 4 ? 4 : 2); ss++) {
+    const int s = bits == 4 ? ss : 2 * h + ss;
+    const int blk = s >> 1;
+    const int64_t kk = c * CHUNK_K + 32 * s + 8 * g;
+    if (kk >= k) continue;
+    const int64_t so = (t * KC + c) * 32 + (r / 4) * 8 + blk * 4 + (r % 4);
+    const float d = f16_to_f32(dscale[so]);
+    const float m = fmt_has_min(fmt) ? f16_to_f32(dmin[so]) : 0.f;
+    float v[8];
+    for (int j = 0; j < 8; j++) {
+      int code;
+      if (bits == 4) code = (w[s] >> (4 * dev_nib_pos(fmt, j))) & 15;
+      else code = (w[2 * ss + (j >> 2)] >> (8 * (j & 3))) & 0xff;
+      v[j] = hd_code_value(fmt, code) * d + m;
+    }
+    *(uint4*)(out + (size_t)row * k + kk) = make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]),
+                                                       pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
+  }
+}
+
 void launch_dequantize_device(bool bf16, int fmt, const uint8_t* blob, int64_t n, int64_t k,
                               uint16_t* out, hipStream_t st) {
-  const int64_t tot = n * (k / QBLOCK);
-  dim3 grid((unsigned)((tot + 127) / 128));
-  if (bf16) hipLaunchKernelGGL(dequantize_device_kernel<BF16>, grid, dim3(128), 0, st, fmt, blob, n, k, out);
-  else hipLaunchKernelGGL(dequantize_device_kernel<F16>, grid, dim3(128), 0, st, fmt, blob, n, k, out);
+  const int bits = fmt_bits(fmt);
+  const int64_t nvec = (pad_to(n, TILE_N) / TILE_N) * (pad_to(k, CHUNK_K) / CHUNK_K) * (bits == 4 ? 1 : 2) * 64;
+  dim3 grid((unsigned)((nvec + 255) / 256));
+  if (bf16) hipLaunchKernelGGL(dequantize_tiled_kernel<BF16>, grid, dim3(256), 0, st, fmt, blob, n, k, out);
+  else hipLaunchKernelGGL(dequantize_tiled_kernel<F16>, grid, dim3(256), 0, st, fmt, blob, n, k, out);
 }
 
 // ---- sum split-K partial slabs (+bias) -> T ----------------------------------

@@ -35,10 +35,12 @@ def test_quantize_device_matches_host(cuda, name):
 @pytest.mark.parametrize("name", FMTS)
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M", [1, 5, 16, 17, 40])
-@pytest.mark.parametrize("v1", [False, True])
-def test_gemv_formats(cuda, name, dtype, M, v1, monkeypatch):
-    if v1:
+@pytest.mark.parametrize("ver", [4, 2, 1])
+def test_gemv_formats(cuda, name, dtype, M, ver, monkeypatch):
+    if ver == 1:
         monkeypatch.setenv("ILLM_GEMV_V1", "1")
+    else:
+        monkeypatch.setenv("ILLM_GEMV_VER", str(ver))
     f = get_format(name).fmt
     torch.manual_seed(0)
     for n, k in [(256, 512), (80, 320)]:
@@ -51,7 +53,7 @@ def test_gemv_formats(cuda, name, dtype, M, v1, monkeypatch):
         assert _rel(y, ref) < 1e-2, (name, dtype, M, n, k)
         ws = torch.ops.ipex_llm_amd.gemv(x, blob, f, n, k, None, 1, 2, 0)
         # LUT formats carry bf16/f16-rounded code values into the MFMA
-        tol = 5e-3 if name in ("nf4", "nf3") else 1e-3
+        tol = 5e-3 if name in ("nf4", "nf3") or ver == 4 else 1e-3
         assert _rel(ws.sum(0), ref) < tol
         b = torch.randn(n, device=cuda).to(dtype)
         yb = torch.ops.ipex_llm_amd.gemv(x, blob, f, n, k, b, 0, 0, 0)

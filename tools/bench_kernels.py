@@ -47,6 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", default="1,8")
     ap.add_argument("--qtype", default="sym_int4")
+    ap.add_argument("--only", default="")
     args = ap.parse_args()
     dev = torch.device("cuda")
     ops.require()
@@ -78,7 +79,7 @@ def main():
                 return ops.gemv_glu(x, blobs[i[0]], f, n, k, 0)
 
             cands = {"store_auto": run_store}
-            for ks in (0, 1, 2, 4, 8):
+            for ks in ((0,) if args.only else (0, 1, 2, 4, 8)):
                 cands[f"partial_ks{ks}"] = run_part(ks)
             if name == "gate_up":
                 cands["glu"] = run_glu
@@ -89,6 +90,8 @@ def main():
                 print(json.dumps(res[-1]), flush=True)
             del blobs
             torch.cuda.empty_cache()
+    if args.only == "gemv":
+        return
     # attention decode
     for B in (1, 8):
         for L in (1024, 4096):
