@@ -1,0 +1,251 @@
+"""Model converter: graph surgery + low-bit module swap + forward swap.
+
+Reference: ``SRC/transformers/convert.py`` -- ``ggml_convert_low_bit``
+(1092-1204) = ``_optimize_pre`` (890-1089: merge qkv, split/pad MLP ...) ->
+``_replace_with_low_bit_linear`` (472-752) -> ``_optimize_post`` (1275-2139:
+per-arch forward replacement).
+
+Here:
+  * ``_optimize_pre`` merges q/k/v into ``qkv_proj`` and gate/up into a
+    16-row-tile-interleaved ``gate_up_proj`` (the layout the fused GLU GEMV
+    epilogue consumes) for every architecture the native decoder runs;
+  * ``_replace_with_low_bit_linear`` swaps ``nn.Linear`` for
+    :class:`LowBitLinear` (quantized by the C++ host library, or on the GPU
+    when the model already lives there);
+  * ``_optimize_post`` attaches the native MI355X decoder
+    (:mod:`ipex_llm_amd.models`) as the model's forward/generate for the
+    supported architectures; everything else keeps its HF forward running on
+    low-bit linears + our RMSNorm kernel (like the reference's generic path).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import types
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from ..quantize import qtypes as Q
+from .low_bit_linear import BF16Linear, DenseLinear, LowBitLinear
+
+logger = logging.getLogger("ipex_llm_amd")
+
+# architectures whose decoder runs on the native engine
+NATIVE_ARCHS = {"llama", "mistral", "qwen2", "qwen3", "gemma", "gemma2", "phi3", "internlm2", "yi",
+                "aquila", "granite", "olmo2", "stablelm", "minicpm", "starcoder2"}
+MOE_ARCHS = {"mixtral", "qwen2_moe", "qwen3_moe"}
+
+
+# ----------------------------------------------------------------- pre
+def _interleave(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    from ..models.decoder import interleave_glu_rows
+    return interleave_glu_rows(gate, up)
+
+
+def _merge_linears(mods: List[nn.Linear], interleave_glu: bool = False) -> nn.Linear:
+    has_bias = mods[0].bias is not None
+    dev, dt = mods[0].weight.device, mods[0].weight.dtype
+    if interleave_glu:
+        w = _interleave(mods[0].weight.data, mods[1].weight.data)
+        b = None
+    else:
+        w = torch.cat([m.weight.data for m in mods], 0)
+        b = torch.cat([m.bias.data for m in mods], 0) if has_bias else None
+    out = nn.Linear(w.shape[1], w.shape[0], bias=has_bias, device="meta", dtype=dt)
+    out.weight = nn.Parameter(w, requires_grad=False)
+    if has_bias:
+        out.bias = nn.Parameter(b, requires_grad=False)
+    return out
+
+
+def _merge_qkv(attn: nn.Module):
+    if hasattr(attn, "qkv_proj") or not all(hasattr(attn, n) for n in ("q_proj", "k_proj", "v_proj")):
+        return
+    attn.qkv_proj = _merge_linears([attn.q_proj, attn.k_proj, attn.v_proj])
+    del attn.q_proj, attn.k_proj, attn.v_proj
+
+
+def _merge_gate_up(mlp: nn.Module):
+    if hasattr(mlp, "gate_up_proj") and not getattr(mlp, "_illm_interleaved", False):
+        # phi3-style fused [gate; up] -> tile-interleaved
+        w = mlp.gate_up_proj.weight.data
+        I = w.shape[0] // 2
+        mlp.gate_up_proj.weight = nn.Parameter(_interleave(w[:I], w[I:]), requires_grad=False)
+        mlp._illm_interleaved = True
+        return
+    if not all(hasattr(mlp, n) for n in ("gate_proj", "up_proj")):
+        return
+    if mlp.gate_proj.bias is not None:
+        return
+    mlp.gate_up_proj = _merge_linears([mlp.gate_proj, mlp.up_proj], interleave_glu=True)
+    mlp._illm_interleaved = True
+    del mlp.gate_proj, mlp.up_proj
+
+
+def _phi3_split_qkv(attn):
+    # phi3 ships qkv_proj already fused in [q; k; v] order: nothing to do
+    return
+
+
+def _optimize_pre(model: nn.Module, qtype: int):
+    """Per-arch weight rewrites before quantization (reference convert.py:890-1089)."""
+    mt = getattr(getattr(model, "config", None), "model_type", None)
+    if mt not in NATIVE_ARCHS:
+        return model
+    base = getattr(model, "model", None)
+    layers = getattr(base, "layers", None)
+    if layers is None:
+        return model
+    for layer in layers:
+        attn = getattr(layer, "self_attn", None) or getattr(layer, "attention", None)
+        if attn is not None:
+            _merge_qkv(attn)
+        mlp = getattr(layer, "mlp", None) or getattr(layer, "feed_forward", None)
+        if mlp is not None and mlp.__class__.__name__.lower().find("moe") < 0:
+            I = getattr(getattr(mlp, "gate_proj", None), "out_features", None) or \
+                (getattr(getattr(mlp, "gate_up_proj", None), "out_features", 0) // 2)
+            if I and I % 16 == 0:
+                _merge_gate_up(mlp)
+    model._illm_pre = True
+    return model
+
+
+# ----------------------------------------------------------------- module swap
+def _is_linear(m: nn.Module) -> bool:
+    return isinstance(m, nn.Linear) and not isinstance(m, (LowBitLinear, DenseLinear))
+
+
+def _convert_one(module: nn.Linear, qtype: int, device, imatrix=None, mp_group=None, lm_head=False,
+                 enable_scale_search=False, convert_shape_only=False):
+    if Q.is_dense(qtype):
+        dt = torch.bfloat16 if qtype == Q.BF16 else torch.float16
+        return DenseLinear.from_linear(module, dt, device, mp_group)
+    fmt = Q.get_format(qtype)
+    if module.in_features % fmt.k_align:
+        return None
+    if convert_shape_only or module.weight.device.type == "meta":
+        m = LowBitLinear(module.in_features, module.out_features, qtype, module.bias is not None,
+                         device="meta", mp_group=mp_group, optimize_lm_head=lm_head)
+        return m
+    return LowBitLinear.from_linear(module, qtype, device=device, imatrix=imatrix, mp_group=mp_group,
+                                    optimize_lm_head=lm_head, enable_scale_search=enable_scale_search)
+
+
+def _replace_with_low_bit_linear(model: nn.Module, qtype: int, modules_to_not_convert=None, prefix="",
+                                 device=None, imatrix_data: Optional[Dict] = None, mixed_precision=False,
+                                 convert_shape_only=False, enable_scale_search=False):
+    """Recursively replace nn.Linear (reference convert.py:472-752)."""
+    skip = set(modules_to_not_convert or [])
+    n_conv = 0
+    for name, child in list(model.named_children()):
+        full = f"{prefix}.{name}" if prefix else name
+        if name in skip or full in skip:
+            continue
+        if _is_linear(child):
+            q = qtype
+            is_head = name == "lm_head" or full.endswith("lm_head")
+            if is_head and mixed_precision and qtype in (Q.SYM_INT4, Q.ASYM_INT4, Q.WOQ_INT4, Q.NF4, Q.FP4):
+                q = Q.SYM_INT8
+            im = imatrix_data.get(full) if imatrix_data else None
+            new = _convert_one(child, q, device, im, getattr(child, "mp_group", None), is_head,
+                               enable_scale_search, convert_shape_only)
+            if new is not None:
+                setattr(model, name, new)
+                n_conv += 1
+                del child
+        else:
+            n_conv += _replace_with_low_bit_linear(child, qtype, modules_to_not_convert, full, device, imatrix_data,
+                                                   mixed_precision, convert_shape_only, enable_scale_search)
+    return n_conv
+
+
+# ----------------------------------------------------------------- post
+def _rmsnorm_forward(self, hidden_states):
+    from .. import ops
+    w = self.weight
+    eps = getattr(self, "variance_epsilon", None) or getattr(self, "eps", 1e-6)
+    if hidden_states.is_cuda and hidden_states.dtype == w.dtype and hidden_states.shape[-1] % 8 == 0:
+        return ops.rms_norm(hidden_states.contiguous(), w, eps)
+    from ..ops import reference as R
+    return R.rms_norm(hidden_states, w.to(hidden_states.dtype), eps)
+
+
+def _patch_norms(model: nn.Module):
+    for m in model.modules():
+        cls = m.__class__.__name__
+        if cls.endswith("RMSNorm") and hasattr(m, "weight") and "Gemma" not in cls:
+            m.forward = types.MethodType(_rmsnorm_forward, m)
+
+
+def _optimize_post(model: nn.Module):
+    """Swap in the native MI355X decoder for supported architectures."""
+    mt = getattr(getattr(model, "config", None), "model_type", None)
+    _patch_norms(model)
+    if mt in NATIVE_ARCHS and getattr(model, "_illm_pre", False):
+        from .hf_native import attach_native
+        attach_native(model)
+    return model
+
+
+# ----------------------------------------------------------------- entry
+def ggml_convert_low_bit(model: nn.Module, qtype="sym_int4", optimize_model: bool = True, device=None,
+                         modules_to_not_convert=None, convert_shape_only: bool = False,
+                         imatrix_data=None, embedding_qtype=None, mixed_precision: bool = False,
+                         cpu_embedding: bool = False, disk_embedding: bool = False,
+                         enable_scale_search: bool = False, torch_dtype=None):
+    """Quantize ``model`` in place and install optimized forwards."""
+    qtype = Q.resolve_qtype(qtype)
+    if qtype in (Q.SYM_INT4, Q.WOQ_INT4):
+        qtype = Q.SYM_INT4 if qtype == Q.SYM_INT4 else Q.WOQ_INT4
+    modules_to_not_convert = list(modules_to_not_convert or [])
+    if optimize_model:
+        _optimize_pre(model, qtype)
+    if qtype in (Q.TORCH_FP8E4, Q.TORCH_FP8E5):
+        qtype = Q.FP8E4 if qtype == Q.TORCH_FP8E4 else Q.FP8E5
+    if qtype in (Q.MOFQ4, Q.MOFQ8):
+        qtype = _pick_mixed_format(model, qtype)
+    n = _replace_with_low_bit_linear(model, qtype, modules_to_not_convert, "", device, imatrix_data,
+                                     mixed_precision, convert_shape_only, enable_scale_search)
+    if n == 0:
+        logger.warning("ggml_convert_low_bit: no linear layer converted")
+    if embedding_qtype is not None or cpu_embedding or disk_embedding:
+        from .embedding import replace_embeddings
+        replace_embeddings(model, embedding_qtype, cpu_embedding, disk_embedding)
+    if torch_dtype is not None and torch_dtype != "auto" and not convert_shape_only:
+        _cast_non_linear(model, torch_dtype)
+    if optimize_model:
+        _optimize_post(model)
+    model._illm_qtype = qtype
+    if hasattr(model, "config"):
+        model.config.bigdl_transformers_low_bit = Q.qtype_name(qtype)
+    return model
+
+
+def _cast_non_linear(model, dtype):
+    for m in model.modules():
+        if isinstance(m, (LowBitLinear,)):
+            continue
+        for pn, p in list(m.named_parameters(recurse=False)):
+            if p.is_floating_point() and p.dtype != dtype:
+                p.data = p.data.to(dtype)
+
+
+def _pick_mixed_format(model, qtype):
+    """mixed_fp4 / mixed_fp8: choose per model the lower-MSE of (sym_int4, fp4)
+    or (sym_int8, fp8_e4m3) on a sample of linear weights (reference
+    low_bit_linear.py:373-408 does it per tensor)."""
+    from .. import ops
+    cands = (Q.SYM_INT4, Q.FP4) if qtype == Q.MOFQ4 else (Q.SYM_INT8, Q.FP8E4)
+    err = {c: 0.0 for c in cands}
+    lin = [m for m in model.modules() if isinstance(m, nn.Linear)][:8]
+    for m in lin:
+        w = m.weight.data.float().cpu()
+        if w.shape[1] % 64:
+            continue
+        for c in cands:
+            f = Q.get_format(c).fmt
+            dq = ops.dequantize(ops.quantize(w, f), f, w.shape[0], w.shape[1])
+            err[c] += (dq - w).pow(2).mean().item()
+    return min(cands, key=lambda c: err[c])

@@ -1,0 +1,290 @@
+"""HF-compatible AutoModel API with low-bit loading.
+
+Reference: ``SRC/transformers/model.py`` -- ``_BaseAutoModelClass``
+(``from_pretrained`` 106-388, ``from_gguf`` 391-408, ``load_convert``
+411-528, ``load_low_bit`` 532-788), ``save_low_bit`` (59-103) and the
+AutoModel* subclasses (791-833).
+
+Usage (one import change from HF)::
+
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    model = AutoModelForCausalLM.from_pretrained(path, load_in_4bit=True).to("cuda")
+    model.save_low_bit("llama-int4")
+    model = AutoModelForCausalLM.load_low_bit("llama-int4").to("cuda")
+
+The low-bit checkpoint keeps the portable canonical (GGML-style planar)
+layout (``model.safetensors``), ``config.json`` carries
+``bigdl_transformers_low_bit`` (reference key) and ``illm_low_bit.json`` the
+conversion flags needed to rebuild the module tree before loading.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import logging
+import os
+import types
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from ..quantize import qtypes as Q
+from .convert import ggml_convert_low_bit
+
+logger = logging.getLogger("ipex_llm_amd")
+LOW_BIT_META = "illm_low_bit.json"
+
+
+def _resolve_qtype_from_kwargs(kwargs):
+    load_in_4bit = kwargs.pop("load_in_4bit", False)
+    load_in_8bit = kwargs.pop("load_in_8bit", False)
+    load_in_low_bit = kwargs.pop("load_in_low_bit", None)
+    qc = kwargs.pop("quantization_config", None)
+    q = None
+    if qc is not None:
+        d = qc if isinstance(qc, dict) else (qc.to_dict() if hasattr(qc, "to_dict") else vars(qc))
+        method = str(d.get("quant_method", "")).lower()
+        if method in ("gptq", "awq"):
+            q = "asym_int4"
+            kwargs["_illm_prequant"] = (method, d)
+        elif d.get("load_in_4bit") or d.get("bnb_4bit_quant_type"):
+            q = "nf4" if d.get("bnb_4bit_quant_type", "nf4") == "nf4" else "sym_int4"
+        elif d.get("load_in_8bit"):
+            q = "sym_int8"
+    if load_in_low_bit is not None:
+        q = load_in_low_bit
+    elif load_in_4bit and q is None:
+        q = "sym_int4"
+    elif load_in_8bit and q is None:
+        q = "sym_int8"
+    return q
+
+
+def save_low_bit(self, save_dir: str, *args, **kwargs):
+    """Write config + portable low-bit weights (reference model.py:59-103)."""
+    os.makedirs(save_dir, exist_ok=True)
+    from safetensors.torch import save_file
+    sd = {}
+    for k, v in self.state_dict().items():
+        sd[k] = v.detach().cpu().contiguous()
+    # de-duplicate shared storage (tied weights) for safetensors
+    seen = {}
+    for k in list(sd):
+        key = (sd[k].data_ptr(), sd[k].numel(), sd[k].dtype)
+        if key in seen and sd[k].numel() > 0:
+            sd[k] = sd[k].clone()
+        seen[key] = k
+    save_file(sd, os.path.join(save_dir, "model.safetensors"), metadata={"format": "pt"})
+    cfg = getattr(self, "config", None)
+    if cfg is not None:
+        cfg.bigdl_transformers_low_bit = Q.qtype_name(getattr(self, "_illm_qtype", Q.SYM_INT4))
+        cfg.save_pretrained(save_dir)
+    meta = {"qtype": Q.qtype_name(getattr(self, "_illm_qtype", Q.SYM_INT4)),
+            "optimize_model": bool(getattr(self, "_illm_pre", False)),
+            "modules_to_not_convert": getattr(self, "_illm_skip", []),
+            "mixed_precision": bool(getattr(self, "_illm_mixed", False)),
+            "format": "ipex_llm_amd/canonical-planar-v1"}
+    with open(os.path.join(save_dir, LOW_BIT_META), "w") as f:
+        json.dump(meta, f, indent=2)
+    gc = getattr(self, "generation_config", None)
+    if gc is not None:
+        try:
+            gc.save_pretrained(save_dir)
+        except Exception:  # pragma: no cover
+            pass
+
+
+def _attach(model, qtype, flags):
+    model.save_low_bit = types.MethodType(save_low_bit, model)
+    model._illm_qtype = Q.resolve_qtype(qtype)
+    model._illm_skip = list(flags.get("modules_to_not_convert") or [])
+    model._illm_mixed = bool(flags.get("mixed_precision", False))
+    return model
+
+
+def _reinit_meta_buffers(model: nn.Module, config):
+    """Non-persistent buffers (rotary inv_freq) stay on meta after an
+    empty-weights build: re-create those modules on the host."""
+    for name, mod in list(model.named_modules()):
+        metas = [b for b in mod.buffers(recurse=False) if b.device.type == "meta"]
+        if not metas:
+            continue
+        try:
+            new = mod.__class__(config=config)
+        except Exception:
+            try:
+                new = mod.__class__(config)
+            except Exception:
+                continue
+        parent = model.get_submodule(name.rsplit(".", 1)[0]) if "." in name else model
+        setattr(parent, name.rsplit(".", 1)[-1], new)
+
+
+class _BaseAutoModelClass:
+    HF_Model = None
+
+    @classmethod
+    def from_pretrained(cls, *args, **kwargs):
+        path = kwargs.pop("pretrained_model_name_or_path", None) if not args else args[0]
+        args = args[1:] if args else ()
+        qtype = _resolve_qtype_from_kwargs(kwargs)
+        optimize_model = kwargs.pop("optimize_model", True)
+        modules_to_not_convert = kwargs.pop("modules_to_not_convert", None)
+        speculative = kwargs.pop("speculative", False)
+        pp_stages = kwargs.pop("pipeline_parallel_stages", 1)
+        imatrix = kwargs.pop("imatrix", None)
+        embedding_qtype = kwargs.pop("embedding_qtype", None)
+        mixed_precision = kwargs.pop("mixed_precision", False)
+        cpu_embedding = kwargs.pop("cpu_embedding", False)
+        disk_embedding = kwargs.pop("disk_embedding", False)
+        kv_fp8 = kwargs.pop("kv_cache_fp8", None)
+        kwargs.pop("model_hub", None)
+        prequant = kwargs.pop("_illm_prequant", None)
+        torch_dtype = kwargs.pop("torch_dtype", kwargs.pop("dtype", "auto"))
+        if qtype is None:
+            return cls.HF_Model.from_pretrained(path, *args, torch_dtype=torch_dtype, **kwargs)
+        kwargs.setdefault("low_cpu_mem_usage", True)
+        if prequant is not None:
+            from ..gptq import load_gptq_model
+            model = load_gptq_model(cls.HF_Model, path, prequant, torch_dtype=torch_dtype, **kwargs)
+        else:
+            model = cls.HF_Model.from_pretrained(path, *args, torch_dtype=torch_dtype, **kwargs)
+        model = model.to("cpu")
+        imatrix_data = None
+        if imatrix is not None:
+            from ..quantize.imatrix import load_imatrix
+            imatrix_data = load_imatrix(imatrix, model)
+        ggml_convert_low_bit(model, qtype, optimize_model, None, modules_to_not_convert,
+                             imatrix_data=imatrix_data, embedding_qtype=embedding_qtype,
+                             mixed_precision=mixed_precision, cpu_embedding=cpu_embedding,
+                             disk_embedding=disk_embedding)
+        _attach(model, qtype, {"modules_to_not_convert": modules_to_not_convert,
+                               "mixed_precision": mixed_precision})
+        if kv_fp8 or os.environ.get("IPEX_LLM_QUANTIZE_KV_CACHE", "0") == "1":
+            model._illm_kv_fp8 = True
+        if speculative:
+            from ..generation.speculative import enable_self_speculative
+            enable_self_speculative(model, path, torch_dtype=torch_dtype, **kwargs)
+        if pp_stages > 1:
+            from ..parallel.pipeline import pipeline_parallel
+            model = pipeline_parallel(model, pp_stages)
+        return model
+
+    @classmethod
+    def from_gguf(cls, fpath: str, optimize_model: bool = True, cpu_embedding: bool = False,
+                  low_bit: str = "sym_int4"):
+        """Load a GGUF file (reference model.py:391-408 / gguf/api.py)."""
+        from ..gguf.api import load_gguf_model
+        model, tokenizer = load_gguf_model(fpath, dtype=torch.float16)
+        ggml_convert_low_bit(model, low_bit, optimize_model, cpu_embedding=cpu_embedding)
+        _attach(model, low_bit, {})
+        return model, tokenizer
+
+    @classmethod
+    def load_convert(cls, q_k, optimize_model, *args, **kwargs):
+        kwargs["load_in_low_bit"] = q_k
+        kwargs["optimize_model"] = optimize_model
+        return cls.from_pretrained(*args, **kwargs)
+
+    @classmethod
+    def load_low_bit(cls, pretrained_model_name_or_path, *model_args, **kwargs):
+        """Rebuild the module tree on meta, convert shapes only, stream the
+        saved blobs in (reference model.py:532-788)."""
+        from accelerate import init_empty_weights
+        from safetensors.torch import load_file
+        from transformers import AutoConfig
+        path = pretrained_model_name_or_path
+        trust = kwargs.pop("trust_remote_code", False)
+        torch_dtype = kwargs.pop("torch_dtype", kwargs.pop("dtype", None))
+        kwargs.pop("optimize_model", None)
+        config = AutoConfig.from_pretrained(path, trust_remote_code=trust)
+        meta_path = os.path.join(path, LOW_BIT_META)
+        flags = json.load(open(meta_path)) if os.path.exists(meta_path) else {}
+        qtype = flags.get("qtype") or getattr(config, "bigdl_transformers_low_bit", "sym_int4")
+        dt = torch_dtype if isinstance(torch_dtype, torch.dtype) else \
+            getattr(config, "torch_dtype", None) or torch.float16
+        if isinstance(dt, str):
+            dt = getattr(torch, dt)
+        with init_empty_weights():
+            model = cls.HF_Model.from_config(config, torch_dtype=dt, trust_remote_code=trust)
+        ggml_convert_low_bit(model, qtype, flags.get("optimize_model", True), None,
+                             flags.get("modules_to_not_convert"), convert_shape_only=True,
+                             mixed_precision=flags.get("mixed_precision", False))
+        wfile = os.path.join(path, "model.safetensors")
+        if os.path.exists(wfile):
+            sd = load_file(wfile)
+        else:
+            sd = torch.load(os.path.join(path, "pytorch_model.bin"), map_location="cpu", weights_only=True)
+        missing, unexpected = model.load_state_dict(sd, strict=False, assign=True)
+        if getattr(config, "tie_word_embeddings", False) and hasattr(model, "tie_weights"):
+            try:
+                model.tie_weights()
+            except Exception:  # pragma: no cover
+                pass
+        _reinit_meta_buffers(model, config)
+        still_meta = [n for n, p in model.named_parameters() if p.device.type == "meta"]
+        if still_meta:
+            raise RuntimeError(f"load_low_bit: parameters left uninitialised: {still_meta[:5]}")
+        _attach(model, qtype, flags)
+        from .convert import _optimize_post
+        if flags.get("optimize_model", True):
+            _optimize_post(model)
+        try:
+            from transformers import GenerationConfig
+            model.generation_config = GenerationConfig.from_pretrained(path)
+        except Exception:
+            pass
+        return model.eval()
+
+
+def _hf(name):
+    import transformers
+    return getattr(transformers, name)
+
+
+class _Lazy(type):
+    def __getattribute__(cls, item):
+        if item == "HF_Model":
+            return _hf(type.__getattribute__(cls, "_hf_name"))
+        return type.__getattribute__(cls, item)
+
+
+class AutoModelForCausalLM(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModelForCausalLM"
+
+
+class AutoModel(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModel"
+
+
+class AutoModelForSpeechSeq2Seq(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModelForSpeechSeq2Seq"
+
+
+class AutoModelForSeq2SeqLM(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModelForSeq2SeqLM"
+
+
+class AutoModelForSequenceClassification(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModelForSequenceClassification"
+
+
+class AutoModelForMaskedLM(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModelForMaskedLM"
+
+
+class AutoModelForQuestionAnswering(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModelForQuestionAnswering"
+
+
+class AutoModelForNextSentencePrediction(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModelForNextSentencePrediction"
+
+
+class AutoModelForMultipleChoice(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModelForMultipleChoice"
+
+
+class AutoModelForTokenClassification(_BaseAutoModelClass, metaclass=_Lazy):
+    _hf_name = "AutoModelForTokenClassification"

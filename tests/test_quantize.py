@@ -1,0 +1,78 @@
+"""Low-bit formats: C++ host quantizers vs the torch references, layout
+round trips and error bounds (CPU)."""
+import pytest
+import torch
+
+from ipex_llm_amd import ops
+from ipex_llm_amd.ops import reference as R
+from ipex_llm_amd.quantize import get_format, resolve_qtype, qtypes as Q
+
+FMTS = ["sym_int4", "woq_int4", "asym_int4", "nf4", "fp4", "nf3", "sym_int8", "fp8_e4m3", "fp8_e5m2",
+        "sym_int5", "asym_int5", "fp6"]
+ERR = {"nf3": 0.25, "sym_int8": 0.01, "fp8_e4m3": 0.04, "fp8_e5m2": 0.07, "sym_int5": 0.07, "asym_int5": 0.07,
+       "fp6": 0.07}
+
+
+@pytest.mark.parametrize("name", FMTS)
+def test_roundtrip_and_layouts(name):
+    torch.manual_seed(0)
+    f = get_format(name).fmt
+    n, k = 40, 320          # exercises row (16) and K (128) padding of the tiled layout
+    w = torch.randn(n, k)
+    blob = ops.quantize(w, f)
+    dq = ops.dequantize(blob, f, n, k)
+    assert torch.equal(dq, R.dequantize_canonical(blob, f, n, k))
+    dev = ops.repack_to_device(blob, f, n, k)
+    assert torch.equal(dq, R.dequantize_device_blob(dev, f, n, k))
+    assert torch.equal(ops.repack_from_device(dev, f, n, k), blob)
+    err = ((dq - w).norm() / w.norm()).item()
+    assert err < ERR.get(name, 0.16), err
+
+
+def test_qtype_registry_matches_reference_ids():
+    assert resolve_qtype("sym_int4") == 2 and resolve_qtype("asym_int4") == 3
+    assert resolve_qtype("nf4") == 10 and resolve_qtype("fp8") == 19 and resolve_qtype("woq_int4") == 34
+    assert resolve_qtype("gguf_q4k_m") == 102
+    assert get_format("q4_k").name == "asym_int4"
+
+
+def test_sym_int4_q4_0_convention():
+    # the max-|x| element of a block maps to code 0 (= -8 d), ggml q4_0 style
+    w = torch.zeros(1, 64)
+    w[0, 5] = -3.0
+    w[0, 7] = 1.0
+    f = get_format("sym_int4").fmt
+    dq = ops.dequantize(ops.quantize(w, f), f, 1, 64)
+    assert abs(dq[0, 5].item() + 3.0) < 1e-3
+
+
+def test_fp8_matches_torch_rne():
+    x = torch.randn(4096) * 10
+    for e5m2, dt in ((False, torch.float8_e4m3fn), (True, torch.float8_e5m2)):
+        ours = ops.to_fp8_bytes(x, e5m2)
+        ref = x.to(dt).view(torch.uint8)
+        assert torch.equal(ours, ref)
+
+
+def test_imatrix_and_scale_search_reduce_error():
+    torch.manual_seed(1)
+    w = torch.randn(64, 256)
+    f = get_format("sym_int4").fmt
+    base = (ops.dequantize(ops.quantize(w, f), f, 64, 256) - w).pow(2).mean()
+    srch = (ops.dequantize(ops.quantize(w, f, scale_search=True), f, 64, 256) - w).pow(2).mean()
+    assert srch <= base
+    imat = torch.rand(256) + 0.1
+    q = ops.quantize(w, f, imatrix=imat)
+    assert q.numel() == ops.quantize(w, f).numel()
+
+
+def test_cpu_lowbit_gemm_matches_reference():
+    torch.manual_seed(2)
+    for name in ("sym_int4", "asym_int4", "nf4", "sym_int8", "fp8_e4m3"):
+        f = get_format(name).fmt
+        w = torch.randn(96, 256) * 0.05
+        blob = ops.quantize(w, f)
+        x = torch.randn(5, 256)
+        ref = x @ R.dequantize_canonical(blob, f, 96, 256).t()
+        y = ops.lowbit_matmul(x, blob, f, 96, 256)
+        assert torch.allclose(y, ref, rtol=1e-4, atol=1e-4)
