@@ -10,19 +10,20 @@
 //
 // Device ("tiled") blob, MI355X gfx950 MFMA fragment order.  N is padded to
 // a multiple of 16 rows, K to a multiple of 128.  Tile t = n/16, chunk
-// c = k/128, KC = Kp/128.  One wave64 reads one (t, c) chunk with one
-// global_load_dwordx4 per lane (4-bit) -> 1 KiB contiguous per wave:
+// c = k/128, KC = Kp/128.  Records R(t,c) of dev_chunk_bytes(f) bytes are
+// stored in (t, c) order; one wave64 streams one record with one
+// global_load_dwordx4 per lane per KiB of codes:
 //   lane l: A-operand row r = l & 15, k-group g = l >> 4
-//   4-bit: 16 B at ((t*KC + c)*64 + l)*16; dword s (0..3) = k-step s, holds
+//   4-bit: 16 B at R + l*16; dword s (0..3) = k-step s, holds
 //          the 8 codes k = 128c + 32s + 8g + j; nibble position p holds
-//          element j = perm4(p) (so (u >> 4q) & 0x000F000F yields the packed
-//          pair (2q, 2q+1) of the bf16 A fragment).
-//   8-bit: 32 B per lane per chunk, two 16-B halves h at
-//          (((t*KC + c)*2 + h)*64 + l)*16; half h holds k-steps 2h, 2h+1,
-//          each as 8 bytes in element order.
-//   scales: fp16 [t][c][rg=0..3][blk=0..1][row=0..3] (64 B per chunk), where
-//          rg/row index the MFMA C-fragment rows n = 16t + 4rg + row.
-//   mins  : same layout, separate plane after scales.
+//          element j = dev_nib_pos (so (u >> 4q) & 0x000F000F yields the
+//          packed pair (2q, 2q+1) of the A fragment).
+//   8-bit: 32 B per lane, two 16-B halves h at R + (h*64 + l)*16; half h
+//          holds k-steps 2h, 2h+1, each as 8 bytes in element order.
+//   scales: 32 fp16 at R + dev_code_chunk(f), index dev_scale_idx(r, blk) =
+//          [row][blk]: one dword per row holds both blocks, so an A-fragment
+//          lane (row r) loads 4 B and a C-fragment lane group (rows 4g..4g+3) 16 B.
+//   mins  : 32 fp16 right after the scales (asym formats only).
 #pragma once
 #include <stdint.h>
 
@@ -85,17 +86,20 @@ static const float kFP4[16] = {0.0f, 0.5f, 1.0f, 1.5f, 2.0f, 3.0f, 4.0f, 6.0f,
 constexpr int64_t canon_code_bytes(int f, int64_t n, int64_t k) { return n * k * fmt_bits(f) / 8; }
 constexpr int64_t canon_scale_elems(int64_t n, int64_t k) { return n * (k / QBLOCK); }
 constexpr int64_t pad_to(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
-constexpr int64_t dev_code_bytes(int f, int64_t n, int64_t k) {
-  return pad_to(n, TILE_N) * pad_to(k, CHUNK_K) * fmt_bits(f) / 8;
+// Device record of one (tile, chunk): the codes (1 KiB 4-bit / 2 KiB 8-bit),
+// then its 32 fp16 scales (64 B) and, for asym formats, 32 fp16 mins (64 B).
+// Keeping a chunk's scales next to its codes makes the weight stream one
+// contiguous sequence per wave (no second stream over a separate scale plane).
+constexpr int64_t dev_code_chunk(int f) { return fmt_bits(f) == 4 ? 1024 : 2048; }
+constexpr int64_t dev_chunk_bytes(int f) { return dev_code_chunk(f) + 64 * (fmt_has_min(f) ? 2 : 1); }
+constexpr int64_t dev_rec_total(int f, int64_t n, int64_t k) {
+  return pad_to(n, TILE_N) / TILE_N * (pad_to(k, CHUNK_K) / CHUNK_K) * dev_chunk_bytes(f);
 }
-constexpr int64_t dev_scale_elems(int64_t n, int64_t k) {
-  return pad_to(n, TILE_N) * (pad_to(k, CHUNK_K) / QBLOCK);
-}
+// fp16 index (within the record's scale block) of (row-in-tile r, block-in-chunk blk)
+constexpr int dev_scale_idx(int r, int blk) { return r * 2 + blk; }
 constexpr int64_t canon_total_bytes(int f, int64_t n, int64_t k) {
   return canon_code_bytes(f, n, k) + canon_scale_elems(n, k) * 2 * (fmt_has_min(f) ? 2 : 1);
 }
-constexpr int64_t dev_total_bytes(int f, int64_t n, int64_t k) {
-  return dev_code_bytes(f, n, k) + dev_scale_elems(n, k) * 2 * (fmt_has_min(f) ? 2 : 1);
-}
+constexpr int64_t dev_total_bytes(int f, int64_t n, int64_t k) { return dev_rec_total(f, n, k); }
 
 }  // namespace illm

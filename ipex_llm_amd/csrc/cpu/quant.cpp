@@ -86,17 +86,16 @@ void illm_repack_to_device(int fmt, const uint8_t* codes, const uint16_t* scales
   const int64_t Np = pad_to(n, TILE_N), Kp = pad_to(k, CHUNK_K);
   const int64_t KC = Kp / CHUNK_K, NT = Np / TILE_N;
   const int64_t nb = k / QBLOCK;
-  uint8_t* dcode = dev;
-  uint16_t* dscale = (uint16_t*)(dev + dev_code_bytes(fmt, n, k));
-  uint16_t* dmin = dscale + dev_scale_elems(n, k);
+  const int64_t CB = dev_chunk_bytes(fmt);
 #pragma omp parallel for collapse(2) schedule(static)
   for (int64_t t = 0; t < NT; t++) {
     for (int64_t c = 0; c < KC; c++) {
+      uint8_t* rec = dev + (t * KC + c) * CB;
       for (int l = 0; l < 64; l++) {
         int r = l & 15, g = l >> 4;
         int64_t row = t * TILE_N + r;
         if (bits == 4) {
-          uint32_t* out = (uint32_t*)(dcode + ((t * KC + c) * 64 + l) * 16);
+          uint32_t* out = (uint32_t*)(rec + l * 16);
           for (int s = 0; s < 4; s++) {
             uint32_t u = 0;
             for (int j = 0; j < 8; j++) {
@@ -108,7 +107,7 @@ void illm_repack_to_device(int fmt, const uint8_t* codes, const uint16_t* scales
           }
         } else {
           for (int h = 0; h < 2; h++) {
-            uint8_t* out = dcode + (((t * KC + c) * 2 + h) * 64 + l) * 16;
+            uint8_t* out = rec + (h * 64 + l) * 16;
             for (int ss = 0; ss < 2; ss++) {
               int s = 2 * h + ss;
               for (int j = 0; j < 8; j++) {
@@ -119,16 +118,17 @@ void illm_repack_to_device(int fmt, const uint8_t* codes, const uint16_t* scales
           }
         }
       }
-      for (int rg = 0; rg < 4; rg++)
-        for (int blk = 0; blk < 2; blk++)
-          for (int rr = 0; rr < 4; rr++) {
-            int64_t row = t * TILE_N + rg * 4 + rr;
-            int64_t b = c * 2 + blk;
-            int64_t o = (t * KC + c) * 32 + rg * 8 + blk * 4 + rr;
-            bool in = row < n && b < nb;
-            dscale[o] = in ? scales[row * nb + b] : 0;
-            if (fmt_has_min(fmt)) dmin[o] = (in && mins) ? mins[row * nb + b] : 0;
-          }
+      uint16_t* dscale = (uint16_t*)(rec + dev_code_chunk(fmt));
+      uint16_t* dmin = dscale + 32;
+      for (int r = 0; r < TILE_N; r++)
+        for (int blk = 0; blk < 2; blk++) {
+          int64_t row = t * TILE_N + r;
+          int64_t b = c * 2 + blk;
+          int o = dev_scale_idx(r, blk);
+          bool in = row < n && b < nb;
+          dscale[o] = in ? scales[row * nb + b] : 0;
+          if (fmt_has_min(fmt)) dmin[o] = (in && mins) ? mins[row * nb + b] : 0;
+        }
     }
   }
 }
@@ -139,9 +139,7 @@ void illm_repack_from_device(int fmt, const uint8_t* dev, int64_t n, int64_t k, 
   const int bits = fmt_bits(fmt);
   const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
   const int64_t nb = k / QBLOCK;
-  const uint8_t* dcode = dev;
-  const uint16_t* dscale = (const uint16_t*)(dev + dev_code_bytes(fmt, n, k));
-  const uint16_t* dmin = dscale + dev_scale_elems(n, k);
+  const int64_t CB = dev_chunk_bytes(fmt);
 #pragma omp parallel for schedule(static)
   for (int64_t row = 0; row < n; row++) {
     int64_t t = row / TILE_N;
@@ -149,11 +147,12 @@ void illm_repack_from_device(int fmt, const uint8_t* dev, int64_t n, int64_t k, 
     uint8_t* crow = codes + row * k * bits / 8;
     for (int64_t kk = 0; kk < k; kk++) {
       int64_t c = kk / CHUNK_K;
+      const uint8_t* rec = dev + (t * KC + c) * CB;
       int kin = (int)(kk % CHUNK_K);
       int s = kin / 32, g = (kin % 32) / 8, j = kin % 8;
       int l = g * 16 + r;
       if (bits == 4) {
-        const uint32_t* in = (const uint32_t*)(dcode + ((t * KC + c) * 64 + l) * 16);
+        const uint32_t* in = (const uint32_t*)(rec + l * 16);
         int code = (in[s] >> (4 * dev_nib_pos(fmt, j))) & 15;
         int64_t b = kk / QBLOCK, jj = kk % QBLOCK;
         uint8_t& byte = crow[b * 32 + (jj & 31)];
@@ -161,16 +160,15 @@ void illm_repack_from_device(int fmt, const uint8_t* dev, int64_t n, int64_t k, 
         else byte = (uint8_t)((byte & 0x0f) | (code << 4));
       } else {
         int h = s / 2, ss = s % 2;
-        crow[kk] = dcode[(((t * KC + c) * 2 + h) * 64 + l) * 16 + ss * 8 + j];
+        crow[kk] = rec[(h * 64 + l) * 16 + ss * 8 + j];
       }
     }
     for (int64_t b = 0; b < nb; b++) {
       int64_t c = b / 2;
-      int blk = (int)(b % 2);
-      int rg = r / 4, rr = r % 4;
-      int64_t o = (t * KC + c) * 32 + rg * 8 + blk * 4 + rr;
+      const uint16_t* dscale = (const uint16_t*)(dev + (t * KC + c) * CB + dev_code_chunk(fmt));
+      int o = dev_scale_idx(r, (int)(b % 2));
       scales[row * nb + b] = dscale[o];
-      if (mins && fmt_has_min(fmt)) mins[row * nb + b] = dmin[o];
+      if (mins && fmt_has_min(fmt)) mins[row * nb + b] = dscale[32 + o];
     }
   }
 }

@@ -22,6 +22,9 @@ enum DecKind : int {
 // constexpr functions are implicitly host+device under clang HIP
 constexpr int dk_bits(int dk) { return dk <= DK_FP4 ? 4 : 8; }
 constexpr bool dk_has_min(int dk) { return dk == DK_INT4A || dk == DK_INT8A; }
+// bytes of one (tile, chunk) record and its code part (formats.h)
+constexpr int dk_code_chunk(int dk) { return dk_bits(dk) * 256; }
+constexpr int dk_chunk_bytes(int dk) { return dk_code_chunk(dk) + 64 * (dk_has_min(dk) ? 2 : 1); }
 constexpr bool dk_needx(int dk) {
   return dk == DK_INT4S || dk == DK_INT4A || dk == DK_INT8S || dk == DK_INT8A;
 }
@@ -42,9 +45,7 @@ inline int fmt_to_dk(int fmt) {
 struct GemvArgs {
   const uint16_t* x;  // [M, ldx] activations (bf16/f16 bits)
   int M, K, ldx;
-  const uint8_t* codes;    // device blob code plane
-  const uint16_t* scales;  // device blob scale plane (fp16)
-  const uint16_t* mins;    // device blob min plane (fp16) or null
+  const uint8_t* w;        // device blob: (tile, chunk) records (formats.h)
   int N, KC;               // logical out features, K chunks (Kp / 128)
   void* out;               // EPI_STORE/GLU: T [M, ldo]; EPI_PARTIAL: f32 [ks][M][N]
   int ldo;

@@ -16,13 +16,10 @@ namespace illm {
 // dk = decoder kind (fmt_to_dk), mt = ceil(M/16) in {1,2,4}
 template <int DK>
 void launch_gemv_dk(bool bf16, int mt, int epi, dim3 grid, const GemvArgs& a, hipStream_t st);
-// v2 (M <= 16, x staged in LDS): grid = (ceil(NT / (4 * TPW)), ksplit), shmem = M * (Kwg + 8) * 2
-template <int DK>
-void launch_gemv2_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
+// v4 (M <= 16, x staged in LDS as f16): grid = (ceil(NT / (4 * TPW)), ksplit),
+// shmem = M * (Kwg + 8) * 2 <= 150 KiB
 template <int DK>
 void launch_gemv4_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
-template <int DK>
-void launch_gemv3_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
 
 // ---- norms (norm.hip) ------------------------------------------------------
 struct NormArgs {

@@ -5,8 +5,9 @@
 // xe_linear.mlp_forward_xpu (SRC/transformers/low_bit_linear.py:698-708,
 // models/common.py:146-161).  Design is MI355X-first:
 //   * weights are pre-tiled (formats.h) so one wave64 streams a 16-row x
-//     128-k chunk with ONE global_load_dwordx4 per lane (1 KiB per wave,
-//     fully coalesced); no LDS round trip for the weight stream;
+//     128-k chunk record with ONE global_load_dwordx4 per lane per KiB of
+//     codes (fully coalesced) plus one 16-B scale load from the same record;
+//     no LDS round trip for the weight stream;
 //   * dequant happens in registers straight into the MFMA A fragment
 //     (int4: the bf16 0x4300|q / f16 0x6400|q magic, fp4/fp8: the gfx950
 //     v_cvt_scalef32_pk_* converters, nf4: a 256-entry pair table in LDS);
@@ -14,9 +15,12 @@
 //     MFMA against an all-ones A fragment (sum of x per block) instead of
 //     per-element VALU subtracts;
 //   * per-64-block scales are applied on the 4 f32 accumulators per lane;
-//   * 4 waves per workgroup split K; partials are reduced through LDS; a
-//     workgroup-level split-K over blockIdx.y writes f32 partial slabs that
-//     are summed by the consumer (fused add+RMSNorm) kernel.
+//   * two kernels: lowbit_gemv4_kernel (M <= 16, the decode hot path: x in
+//     LDS, pre-scaled f16 A fragments, one accumulator per tile) and
+//     lowbit_gemv_kernel (17..64 rows: MT 16-row M tiles per wave, 4 waves
+//     split K and reduce through LDS);
+//   * a workgroup-level split-K over blockIdx.y writes f32 partial slabs that
+//     are summed by the consumer (fused add+RMSNorm / reduce) kernel.
 #pragma once
 #include <type_traits>
 
@@ -169,14 +173,12 @@ __global__ void __launch_bounds__(256) lowbit_gemv_kernel(const GemvArgs a) {
   };
   auto load_chunk = [&](Chunk& ch, int c) {
     c = min(c, c1 - 1);
-    if constexpr (BITS == 4) {
-      ch.q0 = *(const uint4*)(a.codes + ((tbase + c) * 64 + lane) * 16);
-    } else {
-      ch.q0 = *(const uint4*)(a.codes + (((tbase + c) * 2 + 0) * 64 + lane) * 16);
-      ch.q1 = *(const uint4*)(a.codes + (((tbase + c) * 2 + 1) * 64 + lane) * 16);
-    }
-    ch.sc = *(const uint4*)(a.scales + (tbase + c) * 32 + g * 8);
-    if constexpr (dk_has_min(DK)) ch.mn = *(const uint4*)(a.mins + (tbase + c) * 32 + g * 8);
+    const uint8_t* rec = a.w + (tbase + c) * (size_t)dk_chunk_bytes(DK);
+    ch.q0 = *(const uint4*)(rec + lane * 16);
+    if constexpr (BITS == 8) ch.q1 = *(const uint4*)(rec + 1024 + lane * 16);
+    // C-fragment rows 4g..4g+3: one dword (blk0 | blk1 << 16) per row
+    ch.sc = *(const uint4*)(rec + dk_code_chunk(DK) + g * 16);
+    if constexpr (dk_has_min(DK)) ch.mn = *(const uint4*)(rec + dk_code_chunk(DK) + 64 + g * 16);
 #pragma unroll
     for (int s = 0; s < 4; s++) {
       const int kk = c * 128 + 32 * s + 8 * g;
@@ -215,14 +217,13 @@ __global__ void __launch_bounds__(256) lowbit_gemv_kernel(const GemvArgs a) {
         }
       }
       // this 64-block's scales: lane rows n = 4g + i
-      const uint32_t s01 = blk == 0 ? ch.sc.x : ch.sc.z, s23 = blk == 0 ? ch.sc.y : ch.sc.w;
-      const float d[4] = {f16_to_f32(s01 & 0xffff), f16_to_f32(s01 >> 16), f16_to_f32(s23 & 0xffff),
-                          f16_to_f32(s23 >> 16)};
+      const int sh = blk * 16;
+      const float d[4] = {f16_to_f32((ch.sc.x >> sh) & 0xffff), f16_to_f32((ch.sc.y >> sh) & 0xffff),
+                          f16_to_f32((ch.sc.z >> sh) & 0xffff), f16_to_f32((ch.sc.w >> sh) & 0xffff)};
       float mm[4] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (dk_has_min(DK)) {
-        const uint32_t m01 = blk == 0 ? ch.mn.x : ch.mn.z, m23 = blk == 0 ? ch.mn.y : ch.mn.w;
-        mm[0] = f16_to_f32(m01 & 0xffff); mm[1] = f16_to_f32(m01 >> 16);
-        mm[2] = f16_to_f32(m23 & 0xffff); mm[3] = f16_to_f32(m23 >> 16);
+        mm[0] = f16_to_f32((ch.mn.x >> sh) & 0xffff); mm[1] = f16_to_f32((ch.mn.y >> sh) & 0xffff);
+        mm[2] = f16_to_f32((ch.mn.z >> sh) & 0xffff); mm[3] = f16_to_f32((ch.mn.w >> sh) & 0xffff);
       }
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -310,428 +311,13 @@ __global__ void __launch_bounds__(256) lowbit_gemv_kernel(const GemvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// v2 (M <= 16): x staged once per workgroup in LDS, whole tiles per wave.
-//   * the workgroup's activation slice x[0:M, kbase:kbase+Kwg] is loaded with
-//     full 16-B vectors (M*Kwg*2/4096 instructions per thread instead of one
-//     masked fragment load per lane per k-step), read back as MFMA B fragments
-//     with ds_read_b128;
-//   * each wave owns TPW whole 16-row tiles over the workgroup's K range, so
-//     there is no cross-wave reduction; TPW = 2 for the GLU epilogue (gate
-//     tile + up tile in the same lanes -> act(g) * u in registers);
-//   * only weights + scales live in the register prefetch ring (8 VGPRs per
-//     tile-chunk) -> PF = 8 chunks in flight per tile at ~100 VGPRs.
-// Split-K across workgroups (gridDim.y) writes f32 partial slabs.
-// ---------------------------------------------------------------------------
-template <int DK, typename T, int EPI, int TPW, int PFX = 4>
-__global__ void __launch_bounds__(256) lowbit_gemv2_kernel(const GemvArgs a) {
-  constexpr int BITS = dk_bits(DK);
-  constexpr bool NEEDX = dk_needx(DK);
-  constexpr int PF = PFX / TPW;
-  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
-  __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, r16 = lane & 15;
-
-  const int nks = gridDim.y;
-  const int cpk = (a.KC + nks - 1) / nks;
-  const int c0 = blockIdx.y * cpk;
-  const int c1 = min(a.KC, c0 + cpk);
-  const int kbase = c0 * 128;
-  const int kw = (c1 - c0) * 128;
-  const int lds_ld = kw + 8;  // +16 B row pad: rows land on different banks
-  const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
-  const int tile0 = (blockIdx.x * 4 + wave) * TPW;
-  const bool wave_on = tile0 < NT && c0 < c1;
-
-  // ---- 1. issue the weight prefetch ring first (it does not depend on x)
-  struct Chunk {
-    uint4 q[TPW][BITS / 4];
-    uint4 sc[TPW];
-    uint4 mn[TPW];
-  };
-  auto load_chunk = [&](Chunk& ch, int c) {
-    c = min(c, c1 - 1);
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-      const int tile = min(tile0 + t, NT - 1);
-      const size_t tc = (size_t)tile * a.KC + c;
-      if constexpr (BITS == 4) {
-        ch.q[t][0] = *(const uint4*)(a.codes + (tc * 64 + lane) * 16);
-      } else {
-        ch.q[t][0] = *(const uint4*)(a.codes + ((tc * 2 + 0) * 64 + lane) * 16);
-        ch.q[t][1] = *(const uint4*)(a.codes + ((tc * 2 + 1) * 64 + lane) * 16);
-      }
-      ch.sc[t] = *(const uint4*)(a.scales + tc * 32 + g * 8);
-      if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint4*)(a.mins + tc * 32 + g * 8);
-    }
-  };
-  Chunk ring[PF];
-  if (wave_on) {
-#pragma unroll
-    for (int u = 0; u < PF; u++) load_chunk(ring[u], c0 + u);
-  }
-
-  // ---- 2. stage x[0:M, kbase:kbase+kw] into LDS (zero-fill beyond K)
-  if constexpr (DK == DK_LUT4) {
-    lut2[threadIdx.x] = pack2<T>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
-  }
-  {
-    const int vpr = kw / 8;  // 16-B vectors per row
-    for (int v = threadIdx.x; v < a.M * vpr; v += 256) {
-      const int m = v / vpr, kk = (v % vpr) * 8;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (kbase + kk < a.K) val = *(const uint4*)(a.x + (size_t)m * a.ldx + kbase + kk);
-      *(uint4*)(xs + m * lds_ld + kk) = val;
-    }
-  }
-  __syncthreads();
-  if (!wave_on) return;
-
-  const uint4 ones = make_uint4(Magic<T>::one2, Magic<T>::one2, Magic<T>::one2, Magic<T>::one2);
-  const bool mok = r16 < a.M;
-  const uint16_t* xrow = xs + (mok ? r16 : 0) * lds_ld + 8 * g;
-  f32x4 acc[TPW];
-#pragma unroll
-  for (int t = 0; t < TPW; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute_chunk = [&](const Chunk& ch, int c) {
-    const uint16_t* xc = xrow + (c - c0) * 128;
-    uint4 B[4];
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-      const uint4 v = *(const uint4*)(xc + 32 * s);
-      B[s] = mok ? v : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-#pragma unroll
-      for (int blk = 0; blk < 2; blk++) {
-        f32x4 P = {0.f, 0.f, 0.f, 0.f}, X = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ss = 0; ss < 2; ss++) {
-          const int s = blk * 2 + ss;
-          uint4 A;
-          if constexpr (BITS == 4) {
-            const uint4& q0 = ch.q[t][0];
-            const uint32_t u = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
-            A = decode4<DK, T>(u, lut2);
-          } else {
-            const uint4& qq = ch.q[t][blk];
-            A = ss == 0 ? decode8<DK, T>(qq.x, qq.y) : decode8<DK, T>(qq.z, qq.w);
-          }
-          P = mfma16<T>(A, B[s], P);
-          if constexpr (NEEDX) X = mfma16<T>(ones, B[s], X);
-        }
-        const uint32_t s01 = blk == 0 ? ch.sc[t].x : ch.sc[t].z, s23 = blk == 0 ? ch.sc[t].y : ch.sc[t].w;
-        const float d[4] = {f16_to_f32(s01 & 0xffff), f16_to_f32(s01 >> 16), f16_to_f32(s23 & 0xffff),
-                            f16_to_f32(s23 >> 16)};
-        float mm[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (dk_has_min(DK)) {
-          const uint32_t m01 = blk == 0 ? ch.mn[t].x : ch.mn[t].z, m23 = blk == 0 ? ch.mn[t].y : ch.mn[t].w;
-          mm[0] = f16_to_f32(m01 & 0xffff); mm[1] = f16_to_f32(m01 >> 16);
-          mm[2] = f16_to_f32(m23 & 0xffff); mm[3] = f16_to_f32(m23 >> 16);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          float cd, cx;
-          block_coef<DK, T>(d[i], mm[i], cd, cx);
-          acc[t][i] += cd * P[i];
-          if constexpr (NEEDX) acc[t][i] += cx * X[i];
-        }
-      }
-    }
-  };
-
-  // Steady state: unconditional loads (hipcc keeps exact counted vmcnt
-  // waits); the last < 2*PF chunks run a guarded tail, so no chunk is
-  // re-read past c1.
-  const int c1u = __builtin_amdgcn_readfirstlane(c1);
-  int c = __builtin_amdgcn_readfirstlane(c0);
-  for (; c + 2 * PF <= c1u; c += PF) {
-#pragma unroll
-    for (int u = 0; u < PF; u++) {
-      compute_chunk(ring[u], c + u);
-      load_chunk(ring[u], c + u + PF);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < PF; u++) {
-    if (c + u < c1u) compute_chunk(ring[u], c + u);
-    load_chunk(ring[u], c + u + PF);  // clamped: unconditional keeps exact vmcnt counting
-  }
-  c += PF;
-#pragma unroll
-  for (int u = 0; u < PF; u++)
-    if (c + u < c1u) compute_chunk(ring[u], c + u);
-
-  // ---- epilogue: lane holds rows 16*tile + 4g + i, column m = r16
-  const int m = r16;
-  if (m >= a.M) return;
-  if constexpr (EPI == EPI_GLU) {
-    float o[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const float gv = acc[0][i], uv = acc[TPW - 1][i];
-      o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
-    }
-    const int n0 = (tile0 / 2) * 16 + 4 * g;
-    if (n0 < a.N) {
-      uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
-      if (n0 + 3 < a.N) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
-      else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
-    }
-  } else {
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-      const int n0 = (tile0 + t) * 16 + 4 * g;
-      if (tile0 + t >= NT || n0 >= a.N) continue;
-      float o[4] = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
-      if constexpr (EPI == EPI_PARTIAL) {
-        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
-        if (n0 + 3 < a.N && (a.N & 3) == 0) *(float4*)ws = make_float4(o[0], o[1], o[2], o[3]);
-        else for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[i];
-      } else {
-        if (a.bias) {
-#pragma unroll
-          for (int i = 0; i < 4; i++) o[i] += (n0 + i < a.N) ? to_f32<T>(a.bias[n0 + i]) : 0.f;
-        }
-        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
-        if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
-        else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
-      }
-    }
-  }
-}
-
-template <int DK>
-void launch_gemv2_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
-#define L2K(TT, E, TP) hipLaunchKernelGGL((lowbit_gemv2_kernel<DK, TT, E, TP>), grid, dim3(256), shmem, st, a)
-  // tuning experiments: ILLM_GEMV_VARIANT=1 -> PF 8, 2 -> TPW 2 (PF 4 each), 3 -> PF 2
-  static const char* var = getenv("ILLM_GEMV_VARIANT");
-  if (var && bf16 && epi == EPI_PARTIAL) {
-    if (var[0] == '1') { hipLaunchKernelGGL((lowbit_gemv2_kernel<DK, BF16, EPI_PARTIAL, 1, 8>), grid, dim3(256), shmem, st, a); return; }
-    if (var[0] == '2') { dim3 g2((grid.x + 1) / 2, grid.y); hipLaunchKernelGGL((lowbit_gemv2_kernel<DK, BF16, EPI_PARTIAL, 2, 8>), g2, dim3(256), shmem, st, a); return; }
-    if (var[0] == '3') { hipLaunchKernelGGL((lowbit_gemv2_kernel<DK, BF16, EPI_PARTIAL, 1, 2>), grid, dim3(256), shmem, st, a); return; }
-  }
-  if (bf16) {
-    if (epi == EPI_STORE) L2K(BF16, EPI_STORE, 1);
-    else if (epi == EPI_PARTIAL) L2K(BF16, EPI_PARTIAL, 1);
-    else L2K(BF16, EPI_GLU, 2);
-  } else {
-    if (epi == EPI_STORE) L2K(F16, EPI_STORE, 1);
-    else if (epi == EPI_PARTIAL) L2K(F16, EPI_PARTIAL, 1);
-    else L2K(F16, EPI_GLU, 2);
-  }
-#undef L2K
-}
-
-// ---------------------------------------------------------------------------
-// v3 (M <= 16): 4 waves split K, each wave stages ITS x slice in a private
-// LDS region with 16-B vector loads, streams TPW tiles x (its K range) of
-// weights through a PF-deep register ring, and the 4 partial tiles are summed
-// through LDS before a single-pass epilogue.  Many small work units (~8
-// chunks per wave) measured best against the HBM probe
-// (tools/probe/stream_probe.hip): load balance and ramp/drain, not depth,
-// limit GEMV-sized (8-64 MB) streams.
-// ---------------------------------------------------------------------------
-template <int DK, typename T, int EPI, int TPW, int PFX = 4>
-__global__ void __launch_bounds__(256) lowbit_gemv3_kernel(const GemvArgs a) {
-  constexpr int BITS = dk_bits(DK);
-  constexpr bool NEEDX = dk_needx(DK);
-  constexpr int PF = PFX;
-  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
-  __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, r16 = lane & 15;
-
-  // K range of this workgroup (split-K over gridDim.y) and of this wave
-  const int nks = gridDim.y;
-  const int cpk = (a.KC + nks - 1) / nks;
-  const int cw0 = blockIdx.y * cpk;
-  const int cw1 = min(a.KC, cw0 + cpk);
-  const int cpw = (cw1 - cw0 + 3) / 4;
-  const int c0 = __builtin_amdgcn_readfirstlane(min(cw1, cw0 + wave * cpw));
-  const int c1 = __builtin_amdgcn_readfirstlane(min(cw1, c0 + cpw));
-  const int kw = cpw * 128;
-  const int lds_ld = kw + 8;  // +16 B row pad
-  uint16_t* xw = xs + wave * a.M * lds_ld;
-  const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
-  const int tile0 = blockIdx.x * TPW;
-
-  struct Chunk {
-    uint4 q[TPW][BITS / 4];
-    uint4 sc[TPW];
-    uint4 mn[TPW];
-  };
-  auto load_chunk = [&](Chunk& ch, int c) {
-    c = min(c, c1 - 1);
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-      const int tile = min(tile0 + t, NT - 1);
-      const size_t tc = (size_t)tile * a.KC + c;
-      if constexpr (BITS == 4) {
-        ch.q[t][0] = *(const uint4*)(a.codes + (tc * 64 + lane) * 16);
-      } else {
-        ch.q[t][0] = *(const uint4*)(a.codes + ((tc * 2 + 0) * 64 + lane) * 16);
-        ch.q[t][1] = *(const uint4*)(a.codes + ((tc * 2 + 1) * 64 + lane) * 16);
-      }
-      ch.sc[t] = *(const uint4*)(a.scales + tc * 32 + g * 8);
-      if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint4*)(a.mins + tc * 32 + g * 8);
-    }
-  };
-  const bool wave_on = c0 < c1;
-  Chunk ring[PF];
-  if (wave_on) {
-#pragma unroll
-    for (int u = 0; u < PF; u++) load_chunk(ring[u], c0 + u);
-    // this wave's x slice -> its private LDS rows (zero beyond K)
-    const int kb = c0 * 128, vpr = (c1 - c0) * 16;
-    for (int v = lane; v < a.M * vpr; v += 64) {
-      const int m = v / vpr, kk = (v % vpr) * 8;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (kb + kk < a.K) val = *(const uint4*)(a.x + (size_t)m * a.ldx + kb + kk);
-      *(uint4*)(xw + m * lds_ld + kk) = val;
-    }
-  }
-  if constexpr (DK == DK_LUT4) {
-    lut2[threadIdx.x] = pack2<T>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
-    __syncthreads();
-  } else {
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
-    __builtin_amdgcn_wave_barrier();
-  }
-
-  const uint4 ones = make_uint4(Magic<T>::one2, Magic<T>::one2, Magic<T>::one2, Magic<T>::one2);
-  const bool mok = r16 < a.M;
-  const uint16_t* xrow = xw + (mok ? r16 : 0) * lds_ld + 8 * g;
-  f32x4 acc[TPW];
-#pragma unroll
-  for (int t = 0; t < TPW; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute_chunk = [&](const Chunk& ch, int c) {
-    const uint16_t* xc = xrow + (c - c0) * 128;
-    uint4 B[4];
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-      const uint4 v = *(const uint4*)(xc + 32 * s);
-      B[s] = mok ? v : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-#pragma unroll
-      for (int blk = 0; blk < 2; blk++) {
-        f32x4 P = {0.f, 0.f, 0.f, 0.f}, X = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ss = 0; ss < 2; ss++) {
-          const int s = blk * 2 + ss;
-          uint4 A;
-          if constexpr (BITS == 4) {
-            const uint4& q0 = ch.q[t][0];
-            const uint32_t u = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
-            A = decode4<DK, T>(u, lut2);
-          } else {
-            const uint4& qq = ch.q[t][blk];
-            A = ss == 0 ? decode8<DK, T>(qq.x, qq.y) : decode8<DK, T>(qq.z, qq.w);
-          }
-          P = mfma16<T>(A, B[s], P);
-          if constexpr (NEEDX) X = mfma16<T>(ones, B[s], X);
-        }
-        const uint32_t s01 = blk == 0 ? ch.sc[t].x : ch.sc[t].z, s23 = blk == 0 ? ch.sc[t].y : ch.sc[t].w;
-        const float d[4] = {f16_to_f32(s01 & 0xffff), f16_to_f32(s01 >> 16), f16_to_f32(s23 & 0xffff),
-                            f16_to_f32(s23 >> 16)};
-        float mm[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (dk_has_min(DK)) {
-          const uint32_t m01 = blk == 0 ? ch.mn[t].x : ch.mn[t].z, m23 = blk == 0 ? ch.mn[t].y : ch.mn[t].w;
-          mm[0] = f16_to_f32(m01 & 0xffff); mm[1] = f16_to_f32(m01 >> 16);
-          mm[2] = f16_to_f32(m23 & 0xffff); mm[3] = f16_to_f32(m23 >> 16);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          float cd, cx;
-          block_coef<DK, T>(d[i], mm[i], cd, cx);
-          acc[t][i] += cd * P[i];
-          if constexpr (NEEDX) acc[t][i] += cx * X[i];
-        }
-      }
-    }
-  };
-
-  if (wave_on) {
-    int c = c0;
-    for (; c + 2 * PF <= c1; c += PF) {
-#pragma unroll
-      for (int u = 0; u < PF; u++) {
-        compute_chunk(ring[u], c + u);
-        load_chunk(ring[u], c + u + PF);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < PF; u++) {
-      if (c + u < c1) compute_chunk(ring[u], c + u);
-      load_chunk(ring[u], c + u + PF);
-    }
-    c += PF;
-#pragma unroll
-    for (int u = 0; u < PF; u++)
-      if (c + u < c1) compute_chunk(ring[u], c + u);
-  }
-
-  // ---- cross-wave reduction through LDS (reuses the x staging region)
-  __syncthreads();
-  float4* red = (float4*)xs;  // [4 waves][TPW][64 lanes]
-#pragma unroll
-  for (int t = 0; t < TPW; t++) red[(wave * TPW + t) * 64 + lane] = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
-  __syncthreads();
-  if (wave != 0) return;
-  float o[TPW][4];
-#pragma unroll
-  for (int t = 0; t < TPW; t++) {
-    float4 s = red[t * 64 + lane];
-#pragma unroll
-    for (int w = 1; w < 4; w++) {
-      const float4 v = red[(w * TPW + t) * 64 + lane];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    o[t][0] = s.x; o[t][1] = s.y; o[t][2] = s.z; o[t][3] = s.w;
-  }
-  const int m = r16;
-  if (m >= a.M) return;
-  if constexpr (EPI == EPI_GLU) {
-    float r[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) r[i] = (a.act == 0 ? silu_f(o[0][i]) : gelu_tanh_f(o[0][i])) * o[TPW - 1][i];
-    const int n0 = (tile0 / 2) * 16 + 4 * g;
-    if (n0 < a.N) {
-      uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
-      if (n0 + 3 < a.N) *(uint2*)y = make_uint2(pack2<T>(r[0], r[1]), pack2<T>(r[2], r[3]));
-      else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(r[i]);
-    }
-  } else {
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-      const int n0 = (tile0 + t) * 16 + 4 * g;
-      if (tile0 + t >= NT || n0 >= a.N) continue;
-      if constexpr (EPI == EPI_PARTIAL) {
-        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
-        if (n0 + 3 < a.N && (a.N & 3) == 0) *(float4*)ws = make_float4(o[t][0], o[t][1], o[t][2], o[t][3]);
-        else for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[t][i];
-      } else {
-        if (a.bias) {
-#pragma unroll
-          for (int i = 0; i < 4; i++) o[t][i] += (n0 + i < a.N) ? to_f32<T>(a.bias[n0 + i]) : 0.f;
-        }
-        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
-        if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0)
-          *(uint2*)y = make_uint2(pack2<T>(o[t][0], o[t][1]), pack2<T>(o[t][2], o[t][3]));
-        else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[t][i]);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // v4 (M <= 16): pre-scaled f16 A fragments, one MFMA accumulator per tile.
-// v1-v3 accumulate each 64-element block in a fresh MFMA accumulator and then
+// x[0:M, K-slice] is staged once per workgroup in LDS (16-B vector loads,
+// read back as MFMA B fragments with ds_read_b128); each wave owns TPW whole
+// 16-row tiles over the workgroup's K range (TPW = 2 for GLU: gate tile + up
+// tile in the same lanes -> act(g) * u in registers), so there is no
+// cross-wave reduction, and only weight records live in the PF-deep register
+// prefetch ring.  Why pre-scaled: v1 accumulates each 64-element block in a fresh MFMA accumulator and then
 // read it out (v_accvgpr_read) to apply the block scale: a dependent
 // MFMA -> VALU chain per block that, at the ~2 waves/SIMD a GEMV grid gives,
 // is not hidden.  Here the block scale (and min) is applied to the decoded
@@ -835,24 +421,20 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
 
   struct Chunk {
     uint4 q[TPW][BITS / 4];
-    uint4 sc[TPW];
-    uint4 mn[TPW];
+    uint32_t sc[TPW];
+    uint32_t mn[TPW];
   };
   auto load_chunk = [&](Chunk& ch, int c) {
     c = min(c, c1 - 1);
 #pragma unroll
     for (int t = 0; t < TPW; t++) {
       const int tile = min(tile0 + t, NT - 1);
-      const size_t tc = (size_t)tile * a.KC + c;
-      if constexpr (BITS == 4) {
-        ch.q[t][0] = *(const uint4*)(a.codes + (tc * 64 + lane) * 16);
-      } else {
-        ch.q[t][0] = *(const uint4*)(a.codes + ((tc * 2 + 0) * 64 + lane) * 16);
-        ch.q[t][1] = *(const uint4*)(a.codes + ((tc * 2 + 1) * 64 + lane) * 16);
-      }
-      // the 16 B holding this lane's A-row (r16) scales for both blocks
-      ch.sc[t] = *(const uint4*)(a.scales + tc * 32 + (r16 >> 2) * 8);
-      if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint4*)(a.mins + tc * 32 + (r16 >> 2) * 8);
+      const uint8_t* rec = a.w + ((size_t)tile * a.KC + c) * dk_chunk_bytes(DK);
+      ch.q[t][0] = *(const uint4*)(rec + lane * 16);
+      if constexpr (BITS == 8) ch.q[t][1] = *(const uint4*)(rec + 1024 + lane * 16);
+      // this lane's A-row (r16) scales of both blocks: one dword
+      ch.sc[t] = *(const uint32_t*)(rec + dk_code_chunk(DK) + r16 * 4);
+      if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint32_t*)(rec + dk_code_chunk(DK) + 64 + r16 * 4);
     }
   };
   Chunk ring[PF];
@@ -889,17 +471,13 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
 
   const bool mok = r16 < a.M;
   const uint16_t* xrow = xs + (mok ? r16 : 0) * lds_ld + 8 * g;
-  const int rr = r16 & 3;
   f32x4 acc[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto pick = [&](const uint4& v, int blk) -> h2 {
-    // half (blk*4 + rr) of the 16-B scale group, broadcast to both lanes of an h2
-    const uint32_t wlo = blk == 0 ? v.x : v.z, whi = blk == 0 ? v.y : v.w;
-    const uint32_t w = rr < 2 ? wlo : whi;
-    const uint32_t h = (rr & 1) ? (w >> 16) : (w & 0xffffu);
-    return as_h2(h | (h << 16));
+  auto pick = [&](uint32_t v, int blk) -> h2 {
+    // broadcast half blk of the row's scale dword to both halves of an h2
+    return as_h2(__builtin_amdgcn_perm(0u, v, blk == 0 ? 0x01000100u : 0x03020302u));
   };
   auto compute_chunk = [&](const Chunk& ch, int c) {
     const uint16_t* xc = xrow + (c - c0) * 128;
@@ -1014,21 +592,6 @@ void launch_gemv4_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs
     else L4K(F16, EPI_GLU, 2);
   }
 #undef L4K
-}
-
-template <int DK>
-void launch_gemv3_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
-#define L3K(TT, E, TP) hipLaunchKernelGGL((lowbit_gemv3_kernel<DK, TT, E, TP>), grid, dim3(256), shmem, st, a)
-  if (bf16) {
-    if (epi == EPI_STORE) L3K(BF16, EPI_STORE, 1);
-    else if (epi == EPI_PARTIAL) L3K(BF16, EPI_PARTIAL, 1);
-    else L3K(BF16, EPI_GLU, 2);
-  } else {
-    if (epi == EPI_STORE) L3K(F16, EPI_STORE, 1);
-    else if (epi == EPI_PARTIAL) L3K(F16, EPI_PARTIAL, 1);
-    else L3K(F16, EPI_GLU, 2);
-  }
-#undef L3K
 }
 
 template <int DK, typename T, int MT>

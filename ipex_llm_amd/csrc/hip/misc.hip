@@ -69,9 +69,8 @@ __global__ void quantize_device_kernel(int fmt, int kind, const void* w, int64_t
   const int r = (int)(row % TILE_N);
   const int64_t c = b / 2;
   const int blk = (int)(b % 2);
-  uint8_t* dcode = blob;
-  uint16_t* dscale = (uint16_t*)(blob + dev_code_bytes(fmt, n, k));
-  uint16_t* dmin = dscale + dev_scale_elems(n, k);
+  uint8_t* rec = blob + (t * KC + c) * dev_chunk_bytes(fmt);
+  uint16_t* dscale = (uint16_t*)(rec + dev_code_chunk(fmt));
   if (bits == 4) {
     for (int ss = 0; ss < 2; ss++) {
       const int s = 2 * blk + ss;
@@ -79,13 +78,13 @@ __global__ void quantize_device_kernel(int fmt, int kind, const void* w, int64_t
         uint32_t u = 0;
         for (int j = 0; j < 8; j++) u |= (uint32_t)(codes[32 * ss + 8 * g + j] & 15) << (4 * dev_nib_pos(fmt, j));
         const int l = g * 16 + r;
-        ((uint32_t*)(dcode + ((t * KC + c) * 64 + l) * 16))[s] = u;
+        ((uint32_t*)(rec + l * 16))[s] = u;
       }
     }
   } else {
     for (int g = 0; g < 4; g++) {
       const int l = g * 16 + r;
-      uint8_t* o = dcode + (((t * KC + c) * 2 + blk) * 64 + l) * 16;
+      uint8_t* o = rec + (blk * 64 + l) * 16;
       uint32_t wv[4];
       for (int q = 0; q < 4; q++) {
         const int ss = q / 2, j0 = (q % 2) * 4;
@@ -95,9 +94,9 @@ __global__ void quantize_device_kernel(int fmt, int kind, const void* w, int64_t
       *(uint4*)o = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
   }
-  const int64_t so = (t * KC + c) * 32 + (r / 4) * 8 + blk * 4 + (r % 4);
+  const int so = dev_scale_idx(r, blk);
   dscale[so] = hd_f32_to_f16(d);
-  if (fmt_has_min(fmt)) dmin[so] = hd_f32_to_f16(m);
+  if (fmt_has_min(fmt)) dscale[32 + so] = hd_f32_to_f16(m);
 }
 
 void launch_quantize_device(int fmt, int in_kind, const void* w, int64_t n, int64_t k,
@@ -109,47 +108,9 @@ void launch_quantize_device(int fmt, int in_kind, const void* w, int64_t n, int6
 }
 
 // ---- dequantize on device: tiled blob -> dense [n, k] ------------------------
-template <typename T>
-__global__ void dequantize_device_kernel(int fmt, const uint8_t* blob, int64_t n, int64_t k,
-                                         uint16_t* out) {
-  const int64_t nb = k / QBLOCK;
-  const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (id >= n * nb) return;
-  const int64_t row = id / nb, b = id % nb;
-  const int bits = fmt_bits(fmt);
-  const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
-  const int64_t t = row / TILE_N;
-  const int r = (int)(row % TILE_N);
-  const int64_t c = b / 2;
-  const int blk = (int)(b % 2);
-  const uint8_t* dcode = blob;
-  const uint16_t* dscale = (const uint16_t*)(blob + dev_code_bytes(fmt, n, k));
-  const uint16_t* dmin = dscale + dev_scale_elems(n, k);
-  const int64_t so = (t * KC + c) * 32 + (r / 4) * 8 + blk * 4 + (r % 4);
-  const float d = f16_to_f32(dscale[so]);
-  const float m = fmt_has_min(fmt) ? f16_to_f32(dmin[so]) : 0.f;
-  uint16_t* o = out + (size_t)row * k + b * QBLOCK;
-  for (int ss = 0; ss < 2; ss++) {
-    const int s = 2 * blk + ss;
-    for (int g = 0; g < 4; g++) {
-      const int l = g * 16 + r;
-      for (int j = 0; j < 8; j++) {
-        int code;
-        if (bits == 4) {
-          const uint32_t u = ((const uint32_t*)(dcode + ((t * KC + c) * 64 + l) * 16))[s];
-          code = (u >> (4 * dev_nib_pos(fmt, j))) & 15;
-        } else {
-          code = dcode[(((t * KC + c) * 2 + blk) * 64 + l) * 16 + ss * 8 + j];
-        }
-        o[32 * ss + 8 * g + j] = from_f32<T>(hd_code_value(fmt, code) * d + m);
-      }
-    }
-  }
-}
-
-// Coalesced variant: one lane per 16-B code vector of the tiled blob (the
-// same lane mapping the GEMV uses), so the code plane is read with full
-// 1 KiB wave loads and each lane writes 8-element (16-B) row segments.
+// One lane per 16-B code vector of the tiled blob (the same lane mapping the
+// GEMV uses), so codes are read with full 1 KiB wave loads and each lane
+// writes 8-element (16-B) row segments.  Used by the M>64 prefill path.
 template <typename T>
 __global__ void __launch_bounds__(256) dequantize_tiled_kernel(int fmt, const uint8_t* blob, int64_t n,
                                                                int64_t k, uint16_t* out) {
@@ -167,9 +128,9 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(int fmt, const ui
   const int r = l & 15, g = l >> 4;
   const int64_t row = t * TILE_N + r;
   if (row >= n) return;
-  const uint4 q = *(const uint4*)(blob + vec * 16);
-  const uint16_t* dscale = (const uint16_t*)(blob + dev_code_bytes(fmt, n, k));
-  const uint16_t* dmin = dscale + dev_scale_elems(n, k);
+  const uint8_t* rec = blob + tc * dev_chunk_bytes(fmt);
+  const uint4 q = *(const uint4*)(rec + (h * 64 + l) * 16);
+  const uint16_t* dscale = (const uint16_t*)(rec + dev_code_chunk(fmt));
   const uint32_t w[4] = {q.x, q.y, q.z, q.w};
   // 4-bit: dword s = k-step s (block s/2); 8-bit half h: k-steps 2h, 2h+1 (block h)
   for (int ss = 0; ss < (bits == 4 ? 4 : 2); ss++) {
@@ -177,9 +138,9 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(int fmt, const ui
     const int blk = s >> 1;
     const int64_t kk = c * CHUNK_K + 32 * s + 8 * g;
     if (kk >= k) continue;
-    const int64_t so = (t * KC + c) * 32 + (r / 4) * 8 + blk * 4 + (r % 4);
+    const int so = dev_scale_idx(r, blk);
     const float d = f16_to_f32(dscale[so]);
-    const float m = fmt_has_min(fmt) ? f16_to_f32(dmin[so]) : 0.f;
+    const float m = fmt_has_min(fmt) ? f16_to_f32(dscale[32 + so]) : 0.f;
     float v[8];
     for (int j = 0; j < 8; j++) {
       int code;

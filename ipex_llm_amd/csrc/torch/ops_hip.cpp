@@ -69,49 +69,28 @@ void launch_gemv_any(int fmt, bool bf16, int mt, int epi, dim3 grid, const illm:
   hipStream_t st = cur_stream();
   ILLM_DK_SWITCH(fmt, illm::launch_gemv_dk<DKV>(bf16, mt, epi, grid, a, st));
 }
-void launch_gemv2_any(int fmt, bool bf16, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a) {
-  hipStream_t st = cur_stream();
-  ILLM_DK_SWITCH(fmt, illm::launch_gemv2_dk<DKV>(bf16, epi, grid, shmem, a, st));
-}
-
-void launch_gemv3_any(int fmt, bool bf16, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a) {
-  hipStream_t st = cur_stream();
-  ILLM_DK_SWITCH(fmt, illm::launch_gemv3_dk<DKV>(bf16, epi, grid, shmem, a, st));
-}
-
 void launch_gemv4_any(int fmt, bool bf16, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a) {
   hipStream_t st = cur_stream();
   ILLM_DK_SWITCH(fmt, illm::launch_gemv4_dk<DKV>(bf16, epi, grid, shmem, a, st));
 }
 
-// v3 geometry: 4 waves split the workgroup's K range; pick the workgroup
-// split-K so each wave streams ~8 chunks and there are >= 512 workgroups,
-// keeping the per-workgroup LDS (4 waves x M x (chunks*128 + 8) x 2 B) <= 64 KiB.
-size_t v3_shmem(int64_t M, int64_t KC, int64_t ks, int tpw) {
-  const int64_t cpk = (KC + ks - 1) / ks, cpw = (cpk + 3) / 4;
-  const size_t xs = (size_t)4 * M * (cpw * 128 + 8) * 2;
-  return std::max<size_t>(xs, (size_t)4 * tpw * 64 * 16);
-}
-int64_t v3_ksplit(int64_t M, int64_t NT, int64_t KC) {
-  int64_t ks = 1;
-  while (ks * 2 <= KC / 4 && ((KC / (4 * ks) > 12) || NT * ks < 512 || v3_shmem(M, KC, ks, 1) > 65536)) ks *= 2;
-  return ks;
-}
+constexpr size_t kMaxLds = 150 * 1024;
 
+// v1 (M > 16): split K over workgroups until there are >= 768 of them
 int64_t auto_ksplit(int64_t NT, int64_t KC) {
   int64_t ks = 1;
   while (NT * ks < 768 && KC >= 4 * 2 * (ks * 2)) ks *= 2;
   return ks;
 }
 
-// v2 launch geometry: workgroups = 4 waves x TPW tiles; split K so that
-// there are >= ~320 workgroups, each wave keeps >= 4 chunks, and the LDS x
-// slice (M * Kwg * 2 B) stays <= 64 KiB.
-int64_t v2_ksplit(int64_t M, int64_t NT, int64_t KC, int tpw) {
+// v4 geometry: workgroups = 4 waves x TPW tiles; split K so that there are
+// >= ~320 workgroups while each wave keeps >= 4 chunks, and the LDS x slice
+// (M * Kwg * 2 B) stays <= 64 KiB (occupancy: >= 2 workgroups per CU).
+int64_t v4_ksplit(int64_t M, int64_t NT, int64_t KC, int tpw) {
   const int64_t wgs = (NT + 4 * tpw - 1) / (4 * tpw);
   int64_t ks = 1;
   auto lds = [&](int64_t k) { return M * (((KC + k - 1) / k) * 128 + 8) * 2; };
-  while ((wgs * ks < 320 && KC / (ks * 2) >= 4) || lds(ks) > 65536) ks *= 2;
+  while ((wgs * ks < 320 && KC / (ks * 2) >= 4) || (lds(ks) > 65536 && ks < KC)) ks *= 2;
   return ks;
 }
 
@@ -128,20 +107,15 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
   const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
-  const bool force_v1 = getenv("ILLM_GEMV_V1") != nullptr;
-  const bool v2 = M <= 16 && !force_v1;
-  // kernel generation for M <= 16: 4 (default), 2 or 3 via ILLM_GEMV_VER (A/B experiments)
-  const char* vs = getenv("ILLM_GEMV_VER");
-  const int ver_env = vs ? atoi(vs) : 4;
+  // M <= 16 runs v4 (ILLM_GEMV_V1=1 forces the general kernel, for A/B tests)
+  const bool small = M <= 16 && getenv("ILLM_GEMV_V1") == nullptr;
 
   illm::GemvArgs a{};
   a.x = p16(xc);
   a.M = (int)M;
   a.K = (int)k;
   a.ldx = (int)k;
-  a.codes = blob.data_ptr<uint8_t>();
-  a.scales = (const uint16_t*)(a.codes + illm::dev_code_bytes((int)fmt, n, k));
-  a.mins = illm::fmt_has_min((int)fmt) ? a.scales + illm::dev_scale_elems(n, k) : nullptr;
+  a.w = blob.data_ptr<uint8_t>();
   a.KC = (int)KC;
   a.act = (int)act;
   a.lut_fmt = (int)fmt;
@@ -156,29 +130,20 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
     a.out = out.data_ptr();
     a.ldo = (int)(n / 2);
     const size_t shmem = (size_t)M * (KC * 128 + 8) * 2;
-    const size_t shmem3 = v3_shmem(M, KC, 1, 2);
-    if (v2 && ver_env == 4 && shmem <= 150 * 1024) {
+    if (small && shmem <= kMaxLds)
       launch_gemv4_any((int)fmt, bf16, illm::EPI_GLU, dim3((unsigned)((NT + 7) / 8), 1), shmem, a);
-    } else if (v2 && ver_env == 3 && shmem3 <= 65536) {
-      launch_gemv3_any((int)fmt, bf16, illm::EPI_GLU, dim3((unsigned)(NT / 2), 1), shmem3, a);
-    } else if (v2 && shmem <= 65536) {
-      launch_gemv2_any((int)fmt, bf16, illm::EPI_GLU, dim3((unsigned)((NT + 7) / 8), 1), shmem, a);
-    } else {
+    else
       launch_gemv_any((int)fmt, bf16, mt, illm::EPI_GLU, dim3((unsigned)(NT / 2), 1), a);
-    }
     return out;
   }
   a.N = (int)n;
-  if (ksplit <= 0) ksplit = !v2 ? auto_ksplit(NT, KC) : (ver_env == 3 ? v3_ksplit(M, NT, KC) : v2_ksplit(M, NT, KC, 1));
+  if (ksplit <= 0) ksplit = small ? v4_ksplit(M, NT, KC, 1) : auto_ksplit(NT, KC);
   ksplit = std::min<int64_t>(ksplit, KC);
   const int64_t cpk = (KC + ksplit - 1) / ksplit;
   const size_t shmem = (size_t)M * (cpk * 128 + 8) * 2;
-  const size_t shmem3 = v3_shmem(M, KC, ksplit, 1);
-  const int ver = !v2 ? 1 : (ver_env == 3 ? (shmem3 <= 65536 ? 3 : 1) : (shmem <= 65536 ? ver_env : 1));
+  const bool use4 = small && shmem <= kMaxLds;
   auto launch = [&](int e) {
-    if (ver == 4) launch_gemv4_any((int)fmt, bf16, e, dim3((unsigned)((NT + 3) / 4), (unsigned)ksplit), shmem, a);
-    else if (ver == 3) launch_gemv3_any((int)fmt, bf16, e, dim3((unsigned)NT, (unsigned)ksplit), shmem3, a);
-    else if (ver == 2) launch_gemv2_any((int)fmt, bf16, e, dim3((unsigned)((NT + 3) / 4), (unsigned)ksplit), shmem, a);
+    if (use4) launch_gemv4_any((int)fmt, bf16, e, dim3((unsigned)((NT + 3) / 4), (unsigned)ksplit), shmem, a);
     else launch_gemv_any((int)fmt, bf16, mt, e, dim3((unsigned)NT, (unsigned)ksplit), a);
   };
   if (epi == illm::EPI_PARTIAL || ksplit > 1) {

@@ -5,13 +5,7 @@ from __future__ import annotations
 import torch
 from torch.library import register_fake
 
-from ..quantize.qtypes import FMT_ASYM_INT4, FMT_ASYM_INT5
-from .reference import dev_sizes
-
-
-def _dev_total(fmt, n, k):
-    c, s = dev_sizes(fmt, n, k)
-    return c + 2 * s * (2 if fmt in (FMT_ASYM_INT4, FMT_ASYM_INT5) else 1)
+from .reference import dev_total as _dev_total
 
 
 @register_fake("ipex_llm_amd::quantize_device")

@@ -28,11 +28,13 @@ def _pad(v, m):
     return (v + m - 1) // m * m
 
 
-def dev_sizes(fmt, n, k):
-    npad, kpad = _pad(n, TILE_N), _pad(k, CHUNK_K)
-    code = npad * kpad * fmt_bits(fmt) // 8
-    scale = npad * (kpad // QBLOCK)
-    return code, scale
+def dev_chunk_bytes(fmt):
+    """bytes of one (tile, chunk) record: codes, 32 fp16 scales, [32 fp16 mins]."""
+    return fmt_bits(fmt) * 256 + 64 * (2 if fmt in HAS_MIN else 1)
+
+
+def dev_total(fmt, n, k):
+    return (_pad(n, TILE_N) // TILE_N) * (_pad(k, CHUNK_K) // CHUNK_K) * dev_chunk_bytes(fmt)
 
 
 def canon_sizes(fmt, n, k):
@@ -116,8 +118,9 @@ def _perm_pos(fmt):
 
 
 def device_index(fmt: int, n: int, k: int, device="cpu"):
-    """(byte offset, nibble shift, scale index) of every (row, k) element in
-    the MI355X tiled blob -- the spec of csrc/common/formats.h in torch."""
+    """(code byte offset, nibble shift, fp16 index of the scale) of every
+    (row, k) element in the MI355X tiled blob -- the spec of
+    csrc/common/formats.h in torch.  The min (asym) is 32 halves after the scale."""
     kpad = _pad(k, CHUNK_K)
     KC = kpad // CHUNK_K
     row = torch.arange(n, device=device)[:, None]
@@ -126,30 +129,29 @@ def device_index(fmt: int, n: int, k: int, device="cpu"):
     c, kin = kk // CHUNK_K, kk % CHUNK_K
     s, g, j = kin // 32, (kin % 32) // 8, kin % 8
     lane = g * 16 + r
+    rec = (t * KC + c) * dev_chunk_bytes(fmt)
     if fmt_bits(fmt) == 4:
         pos = torch.tensor(_perm_pos(fmt), device=device)[j]
-        off = ((t * KC + c) * 64 + lane) * 16 + s * 4 + pos // 2
+        off = rec + lane * 16 + s * 4 + pos // 2
         shift = 4 * (pos % 2)
     else:
-        off = (((t * KC + c) * 2 + s // 2) * 64 + lane) * 16 + (s % 2) * 8 + j
+        off = rec + ((s // 2) * 64 + lane) * 16 + (s % 2) * 8 + j
         shift = torch.zeros_like(off)
-    b = kk // QBLOCK
-    sidx = (t * KC + b // 2) * 32 + (r // 4) * 8 + (b % 2) * 4 + r % 4
+    blk = (kk // QBLOCK) % 2
+    sidx = (rec + fmt_bits(fmt) * 256) // 2 + r * 2 + blk
     return off, shift, sidx
 
 
 def dequantize_device_blob(blob: torch.Tensor, fmt: int, n: int, k: int) -> torch.Tensor:
     """MI355X tiled blob -> f32 [n, k] (pure torch reference)."""
-    blob = blob.reshape(-1)
-    cb, se = dev_sizes(fmt, n, k)
+    blob = blob.reshape(-1)[:dev_total(fmt, n, k)]
     off, shift, sidx = device_index(fmt, n, k, blob.device)
     byte = blob[off].long()
     q = (byte >> shift) & 15 if fmt_bits(fmt) == 4 else byte
-    scales = blob[cb:cb + 2 * se].view(torch.float16).float()
-    v = code_table(fmt).to(blob.device)[q] * scales[sidx]
+    halves = blob.view(torch.float16)
+    v = code_table(fmt).to(blob.device)[q] * halves[sidx].float()
     if fmt in HAS_MIN:
-        mins = blob[cb + 2 * se:cb + 4 * se].view(torch.float16).float()
-        v = v + mins[sidx]
+        v = v + halves[sidx + 32].float()
     return v
 
 

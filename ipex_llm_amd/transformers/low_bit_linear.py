@@ -33,9 +33,8 @@ from ..quantize import qtypes as Q
 
 
 def _dev_total(fmt, n, k):
-    from ..ops.reference import dev_sizes
-    c, s = dev_sizes(fmt, n, k)
-    return c + 2 * s * (2 if fmt in (Q.FMT_ASYM_INT4, Q.FMT_ASYM_INT5) else 1)
+    from ..ops.reference import dev_total
+    return dev_total(fmt, n, k)
 
 
 def _canon_total(fmt, n, k):
