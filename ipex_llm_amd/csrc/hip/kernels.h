@@ -92,4 +92,25 @@ void launch_reduce_partials(bool bf16, const float* ws, int nsplit, const uint16
 void launch_moe_topk(const float* logits, int T, int E, int k, int renorm, int scoring,
                      float* topk_w, int32_t* topk_ids, hipStream_t st);
 
+// ---- one-shot xGMI peer all-reduce (allreduce.hip) ------------------------
+constexpr int AR_MAX_RANKS = 8;
+constexpr int AR_MAX_BLOCKS = 64;
+constexpr int AR_THREADS = 512;
+// signal area: uint32 [2 parity][AR_MAX_BLOCKS][AR_MAX_RANKS], padded to 8 KiB
+constexpr int64_t AR_SIGNAL_BYTES = 8192;
+
+struct AllReduceArgs {
+  uint8_t* bufs[AR_MAX_RANKS];  // every rank's buffer base (mapped), own included
+  int rank, world;
+  const uint4* in;
+  uint4* out;
+  int64_t nvec;                 // 16-B vectors in the message
+  int64_t cap;                  // bytes per data half
+  uint32_t* counter;            // [AR_MAX_BLOCKS] local epochs
+  int* err;
+};
+
+void launch_custom_all_reduce(bool bf16, const AllReduceArgs& a, hipStream_t st);
+int custom_all_reduce_blocks(int64_t nvec);
+
 }  // namespace illm

@@ -154,11 +154,17 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
     shares its parameters.  Returns None for unsupported layouts."""
     cfg = hf_model.config
     spec = spec_from_config(cfg)
+    tp = getattr(hf_model, "_tp", None)
+    if tp is not None:                      # tensor-parallel shard: local heads
+        spec.num_heads, spec.num_kv_heads = tp["num_heads"], tp["num_kv_heads"]
     base = getattr(hf_model, "model", None)
     if base is None or not hasattr(base, "layers"):
         return None
+    pp = getattr(hf_model, "_pp", None)
     layers = []
     for i, L in enumerate(base.layers):
+        if pp is not None and not (pp["start"] <= i < pp["end"]):
+            continue                        # owned by another pipeline stage
         at = L.self_attn
         if not hasattr(at, "qkv_proj") or not hasattr(L.mlp, "gate_up_proj"):
             return None
@@ -176,10 +182,17 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
                                   L.post_attention_layernorm.weight.data,
                                   pre_ff.weight.data if pre_ff is not None else None,
                                   post_ff.weight.data if post_ff is not None else None))
-    emb = base.embed_tokens.weight.data
-    lm_head = hf_model.get_output_embeddings()
+    first = pp is None or pp["rank"] == 0
+    last = pp is None or pp["rank"] == pp["stages"] - 1
+    ln0 = layers[0].input_layernorm
+    emb = base.embed_tokens.weight.data if first else ln0.data.new_empty(0)
+    lm_head = hf_model.get_output_embeddings() if last else None
+    norm = base.norm.weight.data if last else ln0.data
     inv_freq, att_scale = compute_inv_freq(cfg, spec.head_dim, spec.rot_dim or spec.head_dim)
     spec.rope_attention_scaling = att_scale
-    model = NativeCausalLM(spec, emb, layers, base.norm.weight.data, lm_head, inv_freq.to(emb.device),
-                           dtype or emb.dtype)
+    model = NativeCausalLM(spec, emb, layers, norm, lm_head, inv_freq.to(ln0.device),
+                           dtype or (emb.dtype if first else ln0.dtype))
+    model.first_stage, model.last_stage = first, last
+    if pp is not None:
+        model.layer_offset = pp["start"]
     return model.eval()

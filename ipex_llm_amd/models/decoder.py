@@ -180,6 +180,12 @@ class NativeCausalLM(nn.Module):
         self.register_buffer("inv_freq", inv_freq.float(), persistent=False)
         self.rope_cache: Optional[torch.Tensor] = None
         self.tp_group = None
+        # pipeline-parallel stage flags (parallel/pipeline.py): a stage owns a
+        # contiguous layer range; only the first embeds, only the last has
+        # the final norm + lm_head
+        self.first_stage = True
+        self.last_stage = True
+        self.layer_offset = 0
 
     def ensure_rope_cache(self, max_pos: int):
         """f32 [max_pos, rot/2, 2] cos/sin table (HF fp32 formula, incl. the
@@ -196,7 +202,7 @@ class NativeCausalLM(nn.Module):
 
     @property
     def device(self):
-        return self.embed_tokens.device
+        return self.layers[0].input_layernorm.device
 
     # ------------------------------------------------------------------ cache
     def make_cache(self, max_tokens: int, batch: int = 1, block_size: int = 64, kv_fp8: int = 0,
@@ -205,7 +211,7 @@ class NativeCausalLM(nn.Module):
         s = self.spec
         nblk = num_blocks or batch * ((max_tokens + block_size - 1) // block_size)
         self.ensure_rope_cache(max_tokens + 1)
-        return PagedKVCache(s.num_layers, nblk, s.num_kv_heads, s.head_dim, block_size, self.dtype,
+        return PagedKVCache(len(self.layers), nblk, s.num_kv_heads, s.head_dim, block_size, self.dtype,
                             self.device, kv_fp8)
 
     # ------------------------------------------------------------------ pieces
@@ -282,14 +288,20 @@ class NativeCausalLM(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward_tokens(self, ids: torch.Tensor, pos: torch.Tensor, slots: torch.Tensor, meta: AttnMeta,
-                       cache, logits_idx: Optional[torch.Tensor] = None, return_hidden: bool = False):
+                       cache, logits_idx: Optional[torch.Tensor] = None, return_hidden: bool = False,
+                       hidden_in: Optional[torch.Tensor] = None):
         """ids/pos/slots: [T] (T = B * Tq, sequence-major).  Returns logits
-        [len(logits_idx) or T, vocab] in f32."""
+        [len(logits_idx) or T, vocab] in f32.  Pipeline stages: ``hidden_in``
+        is the previous stage's residual stream [T, H]; a non-last stage
+        returns its residual stream instead of logits."""
         s = self.spec
-        h = F.embedding(ids, self.embed_tokens)
-        if s.embed_scale != 1.0:
-            h = h * torch.tensor(s.embed_scale, dtype=h.dtype, device=h.device)
-        residual = h.contiguous()
+        if hidden_in is not None:
+            residual = hidden_in.to(self.dtype).contiguous().clone()
+        else:
+            h = F.embedding(ids, self.embed_tokens)
+            if s.embed_scale != 1.0:
+                h = h * torch.tensor(s.embed_scale, dtype=h.dtype, device=h.device)
+            residual = h.contiguous()
         x = ops.rms_norm(residual, self.layers[0].input_layernorm, s.rms_eps, s.norm_unit_offset)
         T = ids.shape[0]
         rope = self.rope_cache if self.rope_cache is not None else self.inv_freq
@@ -307,7 +319,10 @@ class NativeCausalLM(nn.Module):
             else:
                 x = self._proj_residual_norm(a, attn.o_proj, residual, layer.post_attention_layernorm)
             act = self._mlp(x, layer.mlp)
-            nxt = self.layers[li + 1].input_layernorm if li + 1 < len(self.layers) else self.norm
+            if li + 1 < len(self.layers):
+                nxt = self.layers[li + 1].input_layernorm
+            else:   # stage boundary: the next norm lives on the next stage
+                nxt = self.norm if self.last_stage else layer.input_layernorm
             if isinstance(layer.mlp, NativeMLP):
                 x = self._proj_residual_norm(act, layer.mlp.down_proj, residual, nxt,
                                              post_norm_w=layer.post_feedforward_layernorm)
@@ -316,6 +331,8 @@ class NativeCausalLM(nn.Module):
                 if layer.post_feedforward_layernorm is not None:
                     y = ops.rms_norm(y, layer.post_feedforward_layernorm, s.rms_eps, s.norm_unit_offset)
                 x, _ = ops.add_rms_norm(y.contiguous(), residual, nxt, s.rms_eps, unit_offset=s.norm_unit_offset)
+        if not self.last_stage:
+            return residual
         if return_hidden:
             return x
         if logits_idx is not None:

@@ -139,6 +139,8 @@ class _BaseAutoModelClass:
         cpu_embedding = kwargs.pop("cpu_embedding", False)
         disk_embedding = kwargs.pop("disk_embedding", False)
         kv_fp8 = kwargs.pop("kv_cache_fp8", None)
+        tensor_parallel = kwargs.pop("tensor_parallel", False)
+        tp_group = kwargs.pop("tp_group", None)
         kwargs.pop("model_hub", None)
         prequant = kwargs.pop("_illm_prequant", None)
         torch_dtype = kwargs.pop("torch_dtype", kwargs.pop("dtype", "auto"))
@@ -151,6 +153,10 @@ class _BaseAutoModelClass:
         else:
             model = cls.HF_Model.from_pretrained(path, *args, torch_dtype=torch_dtype, **kwargs)
         model = model.to("cpu")
+        if tensor_parallel or tp_group is not None:
+            # AutoTP on the dense weights; each rank quantizes only its shard
+            from ..parallel.tp import auto_tp
+            auto_tp(model, tp_group)
         imatrix_data = None
         if imatrix is not None:
             from ..quantize.imatrix import load_imatrix
