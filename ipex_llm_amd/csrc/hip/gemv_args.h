@@ -52,6 +52,11 @@ struct GemvArgs {
   const uint16_t* bias;    // T [N] or null (EPI_STORE only)
   int act;                 // EPI_GLU: 0 = silu, 1 = gelu(tanh)
   int lut_fmt;             // DK_LUT4: FMT_NF4 / FMT_NF3
+  // grouped (MoE) launch: blockIdx.z = expert; null for a plain GEMV
+  const int32_t* moe_off;  // [E + 1] pair offsets per expert
+  const int32_t* moe_rows; // [P] pair ids sorted by expert
+  int moe_xdiv;            // x row of pair p = p / moe_xdiv
+  int64_t w_stride;        // bytes between experts' weight blobs
 };
 
 }  // namespace illm

@@ -400,13 +400,29 @@ __device__ __forceinline__ uint4 scaled_a8(uint32_t lo, uint32_t hi, h2 d2, h2 m
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <int DK, typename T, int EPI, int TPW, int PF = 4>
+// MOE = grouped GEMV over experts (FlashMoE decode): blockIdx.z = expert e,
+// its token-expert pairs are moe_rows[moe_off[e] .. moe_off[e+1]) (<= 16),
+// weights at a.w + e * w_stride, x row = pair / moe_xdiv, output row = pair.
+template <int DK, typename T, int EPI, int TPW, int PF = 4, bool MOE = false>
 __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
   constexpr int BITS = dk_bits(DK);
   extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
   __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r16 = lane & 15;
+  int Mloc = a.M;
+  const uint8_t* wbase = a.w;
+  const int32_t* prow = nullptr;
+  if constexpr (MOE) {
+    const int e = blockIdx.z;
+    const int m0 = a.moe_off[e];
+    Mloc = min(16, a.moe_off[e + 1] - m0);
+    if (Mloc <= 0) return;                // expert not routed to: whole block exits
+    wbase += (size_t)e * a.w_stride;
+    prow = a.moe_rows + m0;
+  }
+  auto xrow_of = [&](int m) -> int { if constexpr (MOE) return prow[m] / a.moe_xdiv; else return m; };
+  auto orow_of = [&](int m) -> int { if constexpr (MOE) return prow[m]; else return m; };
 
   const int nks = gridDim.y;
   const int cpk = (a.KC + nks - 1) / nks;
@@ -429,7 +445,7 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
 #pragma unroll
     for (int t = 0; t < TPW; t++) {
       const int tile = min(tile0 + t, NT - 1);
-      const uint8_t* rec = a.w + ((size_t)tile * a.KC + c) * dk_chunk_bytes(DK);
+      const uint8_t* rec = wbase + ((size_t)tile * a.KC + c) * dk_chunk_bytes(DK);
       ch.q[t][0] = *(const uint4*)(rec + lane * 16);
       if constexpr (BITS == 8) ch.q[t][1] = *(const uint4*)(rec + 1024 + lane * 16);
       // this lane's A-row (r16) scales of both blocks: one dword
@@ -447,11 +463,11 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
   }
   {  // stage x[0:M, kbase:kbase+kw] -> LDS as f16
     const int vpr = kw / 8;
-    for (int v = threadIdx.x; v < a.M * vpr; v += 256) {
+    for (int v = threadIdx.x; v < Mloc * vpr; v += 256) {
       const int m = v / vpr, kk = (v % vpr) * 8;
       uint4 val = make_uint4(0, 0, 0, 0);
       if (kbase + kk < a.K) {
-        val = *(const uint4*)(a.x + (size_t)m * a.ldx + kbase + kk);
+        val = *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk);
         if constexpr (std::is_same<T, BF16>::value) {
           uint32_t w[4] = {val.x, val.y, val.z, val.w};
 #pragma unroll
@@ -469,7 +485,7 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
   __syncthreads();
   if (!wave_on) return;
 
-  const bool mok = r16 < a.M;
+  const bool mok = r16 < Mloc;
   const uint16_t* xrow = xs + (mok ? r16 : 0) * lds_ld + 8 * g;
   f32x4 acc[TPW];
 #pragma unroll
@@ -531,9 +547,9 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
   for (int u = 0; u < PF; u++)
     if (c + u < c1u) compute_chunk(ring[u], c + u);
 
-  // ---- epilogue: lane holds rows 16*tile + 4g + i, column m = r16
-  const int m = r16;
-  if (m >= a.M) return;
+  // ---- epilogue: lane holds rows 16*tile + 4g + i, column r16
+  if (r16 >= Mloc) return;
+  const int m = orow_of(r16);
   if constexpr (EPI == EPI_GLU) {
     float o[4];
 #pragma unroll
@@ -571,6 +587,28 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
 }
 
 template <int DK>
+void launch_gemv4_moe(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+#define L4M(TT, E, TP)                                                                              \
+  do {                                                                                              \
+    static bool attr = false;                                                                       \
+    if (!attr) {                                                                                    \
+      (void)hipFuncSetAttribute((const void*)lowbit_gemv4_kernel<DK, TT, E, TP, 4, true>,           \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);            \
+      attr = true;                                                                                  \
+    }                                                                                               \
+    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, TT, E, TP, 4, true>), grid, dim3(256), shmem, st, a); \
+  } while (0)
+  if (bf16) {
+    if (epi == EPI_PARTIAL) L4M(BF16, EPI_PARTIAL, 1);
+    else L4M(BF16, EPI_GLU, 2);
+  } else {
+    if (epi == EPI_PARTIAL) L4M(F16, EPI_PARTIAL, 1);
+    else L4M(F16, EPI_GLU, 2);
+  }
+#undef L4M
+}
+
+template <int DK>
 void launch_gemv4_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
 #define L4K(TT, E, TP)                                                                              \
   do {                                                                                              \
@@ -582,6 +620,10 @@ void launch_gemv4_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs
     }                                                                                               \
     hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, TT, E, TP>), grid, dim3(256), shmem, st, a);       \
   } while (0)
+  if (a.moe_off != nullptr) {
+    launch_gemv4_moe<DK>(bf16, epi, grid, shmem, a, st);
+    return;
+  }
   if (bf16) {
     if (epi == EPI_STORE) L4K(BF16, EPI_STORE, 1);
     else if (epi == EPI_PARTIAL) L4K(BF16, EPI_PARTIAL, 1);

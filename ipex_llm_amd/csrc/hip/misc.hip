@@ -250,4 +250,72 @@ void launch_moe_topk(const float* logits, int T, int E, int k, int renorm, int s
                      topk_w, topk_ids);
 }
 
+// ---- MoE routing bookkeeping (device side, graph-capturable) ---------------
+// ids [P] (P = T*k, row-major top-k) -> per-local-expert pair lists:
+// off[e]..off[e+1] index rows[], rows sorted by (expert, pair id).  Experts
+// outside [e0, e0+El) (other EP ranks) are skipped.
+__global__ void __launch_bounds__(1024) moe_align_kernel(const int32_t* ids, int P, int e0, int El,
+                                                         int32_t* off, int32_t* rows) {
+  extern __shared__ int sh[];  // cnt[El] | start[El]
+  int* cnt = sh;
+  int* start = sh + El;
+  for (int e = threadIdx.x; e < El; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const int e = ids[p] - e0;
+    if (e >= 0 && e < El) atomicAdd(&cnt[e], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < El; e++) {
+      start[e] = acc;
+      off[e] = acc;
+      acc += cnt[e];
+    }
+    off[El] = acc;
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const int id = ids[p], e = id - e0;
+    if (e < 0 || e >= El) continue;
+    int r = 0;
+    for (int q = 0; q < p; q++) r += ids[q] == id;
+    rows[start[e] + r] = p;
+  }
+}
+
+void launch_moe_align(const int32_t* ids, int P, int e0, int El, int32_t* off, int32_t* rows, hipStream_t st) {
+  hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), (size_t)2 * El * sizeof(int), st, ids, P, e0, El,
+                     off, rows);
+}
+
+// out[t, h] = sum_j w[t, j] * sum_s part[s, t*k + j, h] over local experts
+template <typename T>
+__global__ void moe_combine_kernel(const float* part, int ks, int P, const float* w, const int32_t* ids, int k,
+                                   int e0, int El, uint16_t* out, int Tn, int H) {
+  const int t = blockIdx.y;
+  const int h = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (h >= H) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j = 0; j < k; j++) {
+    const int p = t * k + j;
+    const int e = ids[p] - e0;
+    if (e < 0 || e >= El) continue;
+    const float wj = w[p];
+    for (int s = 0; s < ks; s++) {
+      const float4 v = *(const float4*)(part + ((size_t)s * P + p) * H + h);
+      acc.x += wj * v.x; acc.y += wj * v.y; acc.z += wj * v.z; acc.w += wj * v.w;
+    }
+  }
+  *(uint2*)(out + (size_t)t * H + h) = make_uint2(pack2<T>(acc.x, acc.y), pack2<T>(acc.z, acc.w));
+}
+
+void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float* w, const int32_t* ids, int k,
+                        int e0, int El, uint16_t* out, int Tn, int H, hipStream_t st) {
+  dim3 grid((unsigned)((H / 4 + 255) / 256), (unsigned)Tn);
+  if (bf16) hipLaunchKernelGGL(moe_combine_kernel<BF16>, grid, dim3(256), 0, st, part, ks, P, w, ids, k, e0, El, out, Tn, H);
+  else hipLaunchKernelGGL(moe_combine_kernel<F16>, grid, dim3(256), 0, st, part, ks, P, w, ids, k, e0, El, out, Tn, H);
+}
+
 }  // namespace illm

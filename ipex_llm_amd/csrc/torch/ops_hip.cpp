@@ -339,9 +339,101 @@ std::tuple<Tensor, Tensor> moe_topk(const Tensor& logits, int64_t k, bool renorm
   return {w, ids};
 }
 
+std::tuple<Tensor, Tensor> moe_align(const Tensor& ids, int64_t e0, int64_t num_local) {
+  c10::DeviceGuard g(ids.device());
+  Tensor idc = ids.to(at::kInt).contiguous();
+  const int64_t P = idc.numel();
+  TORCH_CHECK(num_local >= 1 && num_local <= 4096, "moe_align: 1..4096 local experts");
+  Tensor off = at::empty({num_local + 1}, idc.options());
+  Tensor rows = at::empty({std::max<int64_t>(P, 1)}, idc.options());
+  illm::launch_moe_align(idc.data_ptr<int32_t>(), (int)P, (int)e0, (int)num_local, off.data_ptr<int32_t>(),
+                         rows.data_ptr<int32_t>(), cur_stream());
+  return {off, rows};
+}
+
+// Grouped low-bit GEMV over experts (decode MoE, <= 16 tokens):
+//   epi GLU:     x [T, k] (pair p reads row p / xdiv)  -> [npairs, n/2]
+//   epi PARTIAL: x [npairs, k]                         -> f32 [ks, npairs, n]
+Tensor moe_gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, const Tensor& off,
+                const Tensor& rows, int64_t xdiv, int64_t npairs, int64_t epi, int64_t ksplit, int64_t act) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda() && blob.dim() == 2, "moe_gemv: GPU x and [E, bytes] blob");
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  TORCH_CHECK(xc.size(-1) == k, "moe_gemv: x last dim != k");
+  const int64_t rows_x = xc.numel() / k;
+  TORCH_CHECK(blob.size(1) >= illm::dev_total_bytes((int)fmt, n, k), "moe_gemv: expert blob too small");
+  const int64_t E = blob.size(0);
+  TORCH_CHECK(off.numel() == E + 1, "moe_gemv: off must have E+1 entries");
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  // rows per expert <= tokens routed in this step (each token picks an expert once)
+  const int64_t Mmax = std::min<int64_t>(16, epi == illm::EPI_GLU ? rows_x : npairs);
+  TORCH_CHECK(epi != illm::EPI_GLU || rows_x <= 16, "moe_gemv: the decode path handles <= 16 tokens");
+  illm::GemvArgs a{};
+  a.x = p16(xc);
+  a.M = (int)npairs;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.KC = (int)KC;
+  a.act = (int)act;
+  a.lut_fmt = (int)fmt;
+  a.moe_off = off.data_ptr<int32_t>();
+  a.moe_rows = rows.data_ptr<int32_t>();
+  a.moe_xdiv = (int)std::max<int64_t>(1, xdiv);
+  a.w_stride = blob.size(1);
+  if (epi == illm::EPI_GLU) {
+    TORCH_CHECK(n % 32 == 0, "GLU expert weights need a multiple of 32 rows");
+    Tensor out = at::empty({npairs, n / 2}, xc.options());
+    a.N = (int)(n / 2);
+    a.out = out.data_ptr();
+    a.ldo = (int)(n / 2);
+    const size_t shmem = (size_t)Mmax * (KC * 128 + 8) * 2;
+    TORCH_CHECK(shmem <= kMaxLds, "moe_gemv: hidden size too large for the LDS-staged GLU path");
+    launch_gemv4_any((int)fmt, bf16, illm::EPI_GLU, dim3((unsigned)((NT + 7) / 8), 1, (unsigned)E), shmem, a);
+    return out;
+  }
+  a.N = (int)n;
+  if (ksplit <= 0) {
+    ksplit = 1;
+    auto lds = [&](int64_t ks) { return Mmax * (((KC + ks - 1) / ks) * 128 + 8) * 2; };
+    while ((lds(ksplit) > 65536 || ((NT + 3) / 4) * ksplit * 2 < 256) && KC / (ksplit * 2) >= 2) ksplit *= 2;
+  }
+  ksplit = std::min<int64_t>(ksplit, KC);
+  const size_t shmem = (size_t)Mmax * (((KC + ksplit - 1) / ksplit) * 128 + 8) * 2;
+  TORCH_CHECK(shmem <= kMaxLds, "moe_gemv: K slice too large for LDS");
+  Tensor ws = at::empty({ksplit, npairs, n}, xc.options().dtype(at::kFloat));
+  a.out = ws.data_ptr();
+  a.ldo = (int)n;
+  launch_gemv4_any((int)fmt, bf16, illm::EPI_PARTIAL, dim3((unsigned)((NT + 3) / 4), (unsigned)ksplit, (unsigned)E),
+                   shmem, a);
+  return ws;
+}
+
+Tensor moe_combine(const Tensor& part, const Tensor& w, const Tensor& ids, int64_t e0, int64_t num_local,
+                   at::ScalarType dt) {
+  c10::DeviceGuard g(part.device());
+  TORCH_CHECK(part.dim() == 3 && part.scalar_type() == at::kFloat, "moe_combine: part f32 [ks, P, H]");
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "moe_combine: bf16/fp16 out");
+  const int64_t ks = part.size(0), P = part.size(1), H = part.size(2);
+  TORCH_CHECK(H % 4 == 0, "moe_combine: hidden % 4");
+  Tensor wc = w.to(at::kFloat).contiguous(), ic = ids.to(at::kInt).contiguous();
+  const int64_t k = wc.size(-1), Tn = wc.numel() / k;
+  TORCH_CHECK(Tn * k == P, "moe_combine: P != T * k");
+  Tensor out = at::empty({Tn, H}, part.options().dtype(dt));
+  illm::launch_moe_combine(dt == at::kBFloat16, part.data_ptr<float>(), (int)ks, (int)P, wc.data_ptr<float>(),
+                           ic.data_ptr<int32_t>(), (int)k, (int)e0, (int)num_local, m16(out), (int)Tn, (int)H,
+                           cur_stream());
+  return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
+  m.impl("moe_align", &moe_align);
+  m.impl("moe_gemv", &moe_gemv);
+  m.impl("moe_combine", &moe_combine);
   m.impl("quantize_device", &quantize_device);
   m.impl("dequantize_device", &dequantize_device);
   m.impl("gemv", &gemv);

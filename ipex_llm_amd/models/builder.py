@@ -148,6 +148,26 @@ def _module_weight(m: nn.Module):
     return m.weight if not isinstance(m, LowBitLinear) else None
 
 
+def _moe_from_hf(spec: DecoderSpec, block) -> Optional[nn.Module]:
+    from .moe import HFLowBitExperts, NativeMoE, SharedExpertMLP
+    ex = block.experts
+    if not isinstance(ex, HFLowBitExperts):
+        return None
+    shared, sgate = None, None
+    se = getattr(block, "shared_expert", None)
+    if se is not None:
+        if not hasattr(se, "gate_up_proj"):
+            return None
+        shared = SharedExpertMLP(se.gate_up_proj, se.down_proj, spec.act)
+        g = getattr(block, "shared_expert_gate", None)
+        sgate = g.weight.data if g is not None else None
+    ep = getattr(block, "_ep", None)
+    return NativeMoE(block.gate.weight.data, ex.gate_up, ex.down, spec.top_k,
+                     spec.norm_topk if spec.model_type != "mixtral" else True, spec.act, shared, sgate,
+                     expert_offset=ep["e0"] if ep else 0, num_experts=spec.num_experts,
+                     ep_group=ep["group"] if ep else None)
+
+
 def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
     """Wrap a converted HF CausalLM (qkv_proj / gate_up_proj merged by
     ``_optimize_pre``, linears already low-bit) into a NativeCausalLM that
@@ -166,7 +186,7 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
         if pp is not None and not (pp["start"] <= i < pp["end"]):
             continue                        # owned by another pipeline stage
         at = L.self_attn
-        if not hasattr(at, "qkv_proj") or not hasattr(L.mlp, "gate_up_proj"):
+        if not hasattr(at, "qkv_proj"):
             return None
         qn = getattr(at, "q_norm", None)
         kn = getattr(at, "k_norm", None)
@@ -175,7 +195,14 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
             sw = spec.sliding_window if spec.sliding_window_layers[i] else 0
         attn = NativeAttention(spec, at.qkv_proj, at.o_proj, qn.weight.data if qn is not None else None,
                                kn.weight.data if kn is not None else None, sw)
-        mlp = NativeMLP(spec, L.mlp.gate_up_proj, L.mlp.down_proj)
+        if hasattr(L.mlp, "experts"):
+            mlp = _moe_from_hf(spec, L.mlp)
+            if mlp is None:
+                return None
+        elif hasattr(L.mlp, "gate_up_proj"):
+            mlp = NativeMLP(spec, L.mlp.gate_up_proj, L.mlp.down_proj)
+        else:
+            return None
         pre_ff = getattr(L, "pre_feedforward_layernorm", None)
         post_ff = getattr(L, "post_feedforward_layernorm", None)
         layers.append(NativeLayer(spec, attn, mlp, L.input_layernorm.weight.data,

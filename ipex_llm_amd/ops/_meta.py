@@ -70,3 +70,20 @@ def _(ws, bias, dtype):
 def _(logits, k, renorm, scoring):
     T = logits.numel() // logits.shape[-1]
     return logits.new_empty((T, k), dtype=torch.float32), logits.new_empty((T, k), dtype=torch.int32)
+
+
+@register_fake("ipex_llm_amd::moe_align")
+def _(ids, e0, num_local):
+    return ids.new_empty((num_local + 1,), dtype=torch.int32), ids.new_empty((max(ids.numel(), 1),), dtype=torch.int32)
+
+
+@register_fake("ipex_llm_amd::moe_gemv")
+def _(x, blob, fmt, n, k, off, rows, xdiv, npairs, epi, ksplit, act):
+    if epi == 2:
+        return x.new_empty((npairs, n // 2))
+    return x.new_empty((max(ksplit, 1), npairs, n), dtype=torch.float32)
+
+
+@register_fake("ipex_llm_amd::moe_combine")
+def _(part, w, ids, e0, num_local, dtype):
+    return part.new_empty((w.numel() // w.shape[-1], part.shape[-1]), dtype=dtype)

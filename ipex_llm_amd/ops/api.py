@@ -144,6 +144,32 @@ def moe_topk(logits, k, renorm=True, scoring=0):
     return R.moe_topk(logits, k, renorm, scoring)
 
 
+def moe_align(ids, e0: int, num_local: int):
+    """top-k ids [T, k] -> (off [El+1], rows [T*k]): pair ids grouped by local
+    expert (experts outside [e0, e0+El) are skipped, for expert parallel)."""
+    if _native(ids):
+        return _ops().moe_align(ids, e0, num_local)
+    return R.moe_align(ids, e0, num_local)
+
+
+def moe_gemv_glu(x, blob, fmt, n, k, off, rows, topk: int, act: int = 0):
+    """Grouped GLU GEMV over experts: x [T, k] -> [T*topk, n/2] (pair rows)."""
+    P = x.shape[0] * topk
+    return _ops().moe_gemv(x, blob, fmt, n, k, off, rows, topk, P, 2, 1, act)
+
+
+def moe_gemv_partials(x, blob, fmt, n, k, off, rows, ksplit: int = 0):
+    """Grouped GEMV over experts on pair rows: x [P, k] -> f32 [ks, P, n]."""
+    return _ops().moe_gemv(x, blob, fmt, n, k, off, rows, 1, x.shape[0], 1, ksplit, 0)
+
+
+def moe_combine(part, w, ids, e0: int, num_local: int, dtype=torch.bfloat16):
+    """y[t] = sum_j w[t, j] * sum_s part[s, t*k+j] over local experts."""
+    if _native(part):
+        return _ops().moe_combine(part, w, ids, e0, num_local, dtype)
+    return R.moe_combine(part, w, ids, e0, num_local, dtype)
+
+
 # ------------------------------------------------------------ attention
 def rope_kv(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, Hq, Hkv, D, rot_dim=None,
             interleaved=False, q_norm=None, k_norm=None, norm_eps=1e-6, q_scale=1.0,

@@ -252,3 +252,27 @@ def lowbit_linear_ref(x, blob, fmt, n, k, bias=None, device_layout=True):
     if bias is not None:
         y = y + bias.float()
     return y
+
+
+def moe_align(ids: torch.Tensor, e0: int, num_local: int):
+    flat = ids.reshape(-1).long()
+    e = flat - e0
+    valid = (e >= 0) & (e < num_local)
+    order = torch.argsort(torch.where(valid, e, num_local) * flat.numel() + torch.arange(flat.numel(), device=flat.device))
+    counts = torch.bincount(e[valid], minlength=num_local)
+    off = torch.zeros(num_local + 1, dtype=torch.int32, device=ids.device)
+    off[1:] = counts.cumsum(0).to(torch.int32)
+    rows = order[:int(valid.sum())].to(torch.int32)
+    full = torch.zeros(max(flat.numel(), 1), dtype=torch.int32, device=ids.device)
+    full[:rows.numel()] = rows
+    return off, full
+
+
+def moe_combine(part, w, ids, e0, num_local, dtype):
+    ks, P, H = part.shape
+    k = w.shape[-1]
+    T = w.numel() // k
+    s = part.float().sum(0).view(T, k, H)
+    e = ids.reshape(T, k).long() - e0
+    valid = ((e >= 0) & (e < num_local)).float()
+    return (s * (w.reshape(T, k).float() * valid)[..., None]).sum(1).to(dtype)

@@ -92,7 +92,7 @@ def _phi3_split_qkv(attn):
 def _optimize_pre(model: nn.Module, qtype: int):
     """Per-arch weight rewrites before quantization (reference convert.py:890-1089)."""
     mt = getattr(getattr(model, "config", None), "model_type", None)
-    if mt not in NATIVE_ARCHS:
+    if mt not in NATIVE_ARCHS and mt not in MOE_ARCHS:
         return model
     base = getattr(model, "model", None)
     layers = getattr(base, "layers", None)
@@ -103,10 +103,12 @@ def _optimize_pre(model: nn.Module, qtype: int):
         if attn is not None:
             _merge_qkv(attn)
         mlp = getattr(layer, "mlp", None) or getattr(layer, "feed_forward", None)
-        if mlp is not None and mlp.__class__.__name__.lower().find("moe") < 0:
+        if mlp is not None and hasattr(mlp, "experts"):
+            mlp = getattr(mlp, "shared_expert", None)     # MoE block: only the shared expert is dense
+        if mlp is not None:
             I = getattr(getattr(mlp, "gate_proj", None), "out_features", None) or \
                 (getattr(getattr(mlp, "gate_up_proj", None), "out_features", 0) // 2)
-            if I and I % 16 == 0:
+            if I and I % 16 == 0 and isinstance(getattr(mlp, "gate_up_proj", getattr(mlp, "gate_proj", None)), nn.Linear):
                 _merge_gate_up(mlp)
     model._illm_pre = True
     return model
@@ -115,6 +117,24 @@ def _optimize_pre(model: nn.Module, qtype: int):
 # ----------------------------------------------------------------- module swap
 def _is_linear(m: nn.Module) -> bool:
     return isinstance(m, nn.Linear) and not isinstance(m, (LowBitLinear, DenseLinear))
+
+
+def _is_expert_bank(m: nn.Module) -> bool:
+    """HF fused experts (3-D gate_up_proj / down_proj parameters)"""
+    gu, dn = getattr(m, "gate_up_proj", None), getattr(m, "down_proj", None)
+    return isinstance(gu, nn.Parameter) and isinstance(dn, nn.Parameter) and gu.dim() == 3
+
+
+def _convert_experts(m: nn.Module, qtype: int, device, convert_shape_only: bool):
+    from ..models.moe import HFLowBitExperts, LowBitExperts
+    if Q.is_dense(qtype) or Q.get_format(qtype) is None:
+        return None
+    E, I2, H = m.gate_up_proj.shape
+    if H % Q.get_format(qtype).k_align or (I2 // 2) % Q.get_format(qtype).k_align or I2 % 32:
+        return None
+    if convert_shape_only or m.gate_up_proj.device.type == "meta":
+        return HFLowBitExperts(LowBitExperts(E, I2, H, qtype, "meta"), LowBitExperts(E, H, I2 // 2, qtype, "meta"))
+    return HFLowBitExperts.from_hf(m, qtype, device)
 
 
 def _convert_one(module: nn.Linear, qtype: int, device, imatrix=None, mp_group=None, lm_head=False,
@@ -143,6 +163,15 @@ def _replace_with_low_bit_linear(model: nn.Module, qtype: int, modules_to_not_co
         full = f"{prefix}.{name}" if prefix else name
         if name in skip or full in skip:
             continue
+        if _is_expert_bank(child):
+            new = _convert_experts(child, qtype, device, convert_shape_only)
+            if new is not None:
+                setattr(model, name, new)
+                n_conv += 1
+            continue
+        if _is_linear(child) and (name == "shared_expert_gate" or child.out_features < 16) and \
+                not (name == "lm_head" or full.endswith("lm_head")):
+            continue                                  # tiny gates stay dense
         if _is_linear(child):
             q = qtype
             is_head = name == "lm_head" or full.endswith("lm_head")
@@ -183,7 +212,7 @@ def _optimize_post(model: nn.Module):
     """Swap in the native MI355X decoder for supported architectures."""
     mt = getattr(getattr(model, "config", None), "model_type", None)
     _patch_norms(model)
-    if mt in NATIVE_ARCHS and getattr(model, "_illm_pre", False):
+    if (mt in NATIVE_ARCHS or mt in MOE_ARCHS) and getattr(model, "_illm_pre", False):
         from .hf_native import attach_native
         attach_native(model)
     return model

@@ -178,6 +178,9 @@ def native_generate(self, input_ids=None, attention_mask=None, generation_config
 
 
 def attach_native(model):
+    from ..models.builder import native_from_hf
+    if native_from_hf(model) is None:        # layout the native decoder cannot run: keep HF forward
+        return model
     model.forward = types.MethodType(native_forward, model)
     model.generate = types.MethodType(native_generate, model)
     model._illm_native_attached = True

@@ -140,6 +140,7 @@ class _BaseAutoModelClass:
         disk_embedding = kwargs.pop("disk_embedding", False)
         kv_fp8 = kwargs.pop("kv_cache_fp8", None)
         tensor_parallel = kwargs.pop("tensor_parallel", False)
+        expert_parallel = kwargs.pop("expert_parallel", False)
         tp_group = kwargs.pop("tp_group", None)
         kwargs.pop("model_hub", None)
         prequant = kwargs.pop("_illm_prequant", None)
@@ -157,6 +158,10 @@ class _BaseAutoModelClass:
             # AutoTP on the dense weights; each rank quantizes only its shard
             from ..parallel.tp import auto_tp
             auto_tp(model, tp_group)
+        if expert_parallel:
+            # each rank keeps (and quantizes) only its experts
+            from ..parallel.ep import shard_experts
+            shard_experts(model, None if expert_parallel is True else expert_parallel)
         imatrix_data = None
         if imatrix is not None:
             from ..quantize.imatrix import load_imatrix

@@ -123,3 +123,55 @@ def _coll_worker(rank, world, port):
 
 def test_collectives_gloo():
     _run(_coll_worker, 2)
+
+
+def _ep_worker(rank, world, port, path, want):
+    _init(rank, world, port)
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    m = AutoModelForCausalLM.from_pretrained(path, load_in_low_bit="sym_int8", torch_dtype=torch.float32,
+                                             expert_parallel=True)
+    blk = m.model.layers[0].mlp
+    assert blk.experts.num_experts == 4 // world and blk._ep["e0"] == rank * (4 // world)
+    ids = torch.tensor(want["ids"])
+    with torch.no_grad():
+        got = m(ids).logits.float()
+    ref = torch.tensor(want["logits"])
+    assert ((got - ref).norm() / ref.norm()).item() < 1e-4
+    # token-sharded prefill: all-to-all dispatch == replicated compute
+    from ipex_llm_amd.parallel.ep import ep_moe_all_to_all
+    from ipex_llm_amd.transformers.hf_native import get_native
+    nm, _ = get_native(m)
+    moe = nm.layers[0].mlp
+    x = torch.randn(6, 128, generator=torch.Generator().manual_seed(rank))
+    mine = ep_moe_all_to_all(x, moe)
+    import torch.distributed as dist
+    xs = [torch.empty_like(x) for _ in range(world)]
+    dist.all_gather(xs, x)                       # replicated-token reference
+    xa = torch.cat(xs)
+    w, ids_ = moe.route(xa)
+    part = moe._experts_loop(xa, w, ids_)
+    dist.all_reduce(part)
+    want = part[rank * 6:(rank + 1) * 6]
+    assert torch.allclose(mine, want, atol=1e-4), (mine - want).abs().max()
+    dist.destroy_process_group()
+
+
+def test_expert_parallel_matches_single(tmp_path):
+    from transformers import Qwen2MoeConfig, Qwen2MoeForCausalLM
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    torch.manual_seed(0)
+    cfg = Qwen2MoeConfig(vocab_size=256, hidden_size=128, intermediate_size=128, moe_intermediate_size=64,
+                         shared_expert_intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                         num_key_value_heads=2, num_experts=4, num_experts_per_tok=2, max_position_embeddings=256)
+    hf = Qwen2MoeForCausalLM(cfg).eval()
+    with torch.no_grad():
+        for n, p in hf.named_parameters():
+            if p.dim() == 3 or "gate" in n:
+                p.normal_(0, 0.05)
+    p = str(tmp_path / "moe")
+    hf.save_pretrained(p)
+    ids = torch.randint(0, 256, (2, 6), generator=torch.Generator().manual_seed(5))
+    m = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32)
+    with torch.no_grad():
+        logits = m(ids).logits.float()
+    _run(_ep_worker, 2, p, {"ids": ids.tolist(), "logits": logits.tolist()})
