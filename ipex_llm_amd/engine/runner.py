@@ -167,6 +167,28 @@ class Engine:
         return logits
 
     @torch.no_grad()
+    def forward_chunk(self, seq: SequenceState, tokens: Sequence[int], start: int) -> torch.Tensor:
+        """Run ``tokens`` of one sequence at positions start.. (KV written,
+        ``seq.length`` = start + n); returns f32 logits for every token [n, V].
+        Used by speculative / lookup verification: rejected tail positions are
+        simply overwritten later (the paged cache is position-addressed)."""
+        m, c = self.model, self.cache
+        dev = m.device
+        n = len(tokens)
+        pos = torch.arange(start, start + n, device=dev)
+        slots = slots_for(seq, start, n, c.bs).to(dev)
+        L = start + n
+        bt = make_block_table([seq], len(seq.blocks), dev)
+        meta = AttnMeta(1, n, bt, torch.tensor([L], dtype=torch.int32, device=dev), nsplit_for(L), [L])
+        logits = m.forward_tokens(torch.tensor(list(tokens), dtype=torch.long, device=dev), pos, slots, meta, c,
+                                  logits_idx=torch.arange(n, device=dev))
+        seq.length = L
+        return logits
+
+    def new_sequence(self, max_len: int) -> SequenceState:
+        return SequenceState(self.cache.allocator.alloc((max_len + self.block_size - 1) // self.block_size))
+
+    @torch.no_grad()
     def decode_step_obj(self, seqs: List[SequenceState], max_len: int, greedy: bool, use_graph: bool):
         key = (len(seqs), max(len(s.blocks) for s in seqs), greedy, use_graph)
         st = self._steps.get(key)

@@ -17,6 +17,7 @@ __all__ = [
     "quantize", "dequantize", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
+    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine",
 ]
 
 

@@ -156,6 +156,9 @@ def native_generate(self, input_ids=None, attention_mask=None, generation_config
     prompts = _row_tokens(input_ids, attention_mask)
     timing = GenTiming()
     lookup = prompt_lookup_num_tokens or lookahead
+    if not lookup and len(prompts) == 1:
+        from ..generation.lookup import performance_mode_lookahead
+        lookup = performance_mode_lookahead(len(prompts[0]))
     if getattr(self, "_illm_speculative", False) and not do_sample:
         from ..generation.speculative import speculative_generate
         outs = speculative_generate(self, prompts, timing=timing, streamer=streamer, **kw)

@@ -1,0 +1,50 @@
+"""Prompt-lookup and self-speculative decoding produce exactly the greedy
+output of the target model (reference: lookup.py / speculative.py)."""
+import torch
+
+
+def _tiny(tmp_path):
+    from transformers import LlamaConfig, LlamaForCausalLM
+    torch.manual_seed(0)
+    cfg = LlamaConfig(vocab_size=64, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=512)
+    m = LlamaForCausalLM(cfg).eval()
+    p = str(tmp_path / "m")
+    m.save_pretrained(p)
+    return p
+
+
+def test_lookup_matches_greedy(tmp_path):
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    p = _tiny(tmp_path)
+    m = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32)
+    # repetitive prompt: n-gram candidates exist
+    ids = torch.tensor([[5, 6, 7, 8, 9, 5, 6, 7, 8, 9, 5, 6, 7, 8, 9, 5, 6]])
+    ref = m.generate(ids, max_new_tokens=20)
+    out = m.generate(ids, max_new_tokens=20, prompt_lookup_num_tokens=4)
+    assert torch.equal(out, ref)
+    from ipex_llm_amd.transformers.hf_native import get_native
+    st = get_native(m)[1].lookup_stats
+    assert st["drafted"] > 0
+
+
+def test_candidate_table():
+    from ipex_llm_amd.generation.lookup import PromptLookupCandidates
+    g = PromptLookupCandidates(num_output_tokens=3, max_matching_ngram_size=2)
+    g.init([1, 2, 3, 4, 1, 2])
+    assert g.candidates() == [3, 4, 1]
+    g.extend([9])
+    assert g.candidates() == []
+
+
+def test_self_speculative_matches_target_greedy(tmp_path):
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    p = _tiny(tmp_path)
+    tgt = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="bf16", torch_dtype=torch.float32)
+    ids = torch.randint(0, 64, (1, 9), generator=torch.Generator().manual_seed(2))
+    ref = tgt.generate(ids, max_new_tokens=24)
+    spec = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="bf16", torch_dtype=torch.float32,
+                                                speculative=True)
+    out = spec.generate(ids, max_new_tokens=24)
+    assert torch.equal(out, ref)
+    assert spec.n_drafted > 0 and spec.n_matched > 0
