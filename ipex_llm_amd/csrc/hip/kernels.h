@@ -117,4 +117,19 @@ struct AllReduceArgs {
 void launch_custom_all_reduce(bool bf16, const AllReduceArgs& a, hipStream_t st);
 int custom_all_reduce_blocks(int64_t nvec);
 
+// ---- fused multi-tensor AdamW (optim.hip) ----------------------------------
+struct AdamWArgs {
+  const int64_t* params;       // device pointer tables, one entry per tensor
+  const int64_t* grads;
+  const int64_t* exp_avg;      // f32 moments
+  const int64_t* exp_avg_sq;
+  const int64_t* sizes;        // elements per tensor
+  const int32_t* chunk_tensor; // [nchunks] tensor of each chunk
+  const int64_t* chunk_start;  // [nchunks] first element of each chunk
+  int chunk;                   // elements per chunk
+  float lr, beta1, beta2, eps, weight_decay, bias_corr1, bias_corr2, grad_scale;
+  int param_dtype, grad_dtype; // 0 = f32, 1 = bf16
+};
+void launch_fused_adamw(const AdamWArgs& a, int nchunks, hipStream_t st);
+
 }  // namespace illm

@@ -78,9 +78,41 @@ void custom_all_reduce(const Tensor& inp, Tensor& out, c10::IntArrayRef bufs, in
                                    at::hip::getCurrentHIPStream().stream());
 }
 
+// table: int64 [5, T] = (param ptr, grad ptr, exp_avg ptr, exp_avg_sq ptr, numel)
+void fused_adamw(const Tensor& table, const Tensor& chunk_tensor, const Tensor& chunk_start, int64_t chunk,
+                 double lr, double beta1, double beta2, double eps, double weight_decay, double bc1, double bc2,
+                 double grad_scale, int64_t param_dtype, int64_t grad_dtype) {
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.dim() == 2 && table.size(0) == 5,
+              "fused_adamw: table must be int64 [5, T] on the GPU");
+  c10::DeviceGuard g(table.device());
+  const int64_t T = table.size(1);
+  const int64_t* t = table.data_ptr<int64_t>();
+  illm::AdamWArgs a{};
+  a.params = t;
+  a.grads = t + T;
+  a.exp_avg = t + 2 * T;
+  a.exp_avg_sq = t + 3 * T;
+  a.sizes = t + 4 * T;
+  a.chunk_tensor = chunk_tensor.data_ptr<int32_t>();
+  a.chunk_start = chunk_start.data_ptr<int64_t>();
+  a.chunk = (int)chunk;
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.weight_decay = (float)weight_decay;
+  a.bias_corr1 = (float)bc1;
+  a.bias_corr2 = (float)bc2;
+  a.grad_scale = (float)grad_scale;
+  a.param_dtype = (int)param_dtype;
+  a.grad_dtype = (int)grad_dtype;
+  illm::launch_fused_adamw(a, (int)chunk_tensor.numel(), at::hip::getCurrentHIPStream().stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
+  m.def("fused_adamw(Tensor table, Tensor chunk_tensor, Tensor chunk_start, int chunk, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, int param_dtype, int grad_dtype) -> ()");
   m.def("ipc_alloc(int nbytes) -> int", &ipc_alloc);
   m.def("ipc_handle(int ptr) -> Tensor", &ipc_handle);
   m.def("ipc_open(Tensor handle) -> int", &ipc_open);
@@ -89,4 +121,7 @@ TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("custom_all_reduce(Tensor inp, Tensor(a!) out, int[] bufs, int rank, Tensor(b!) counter, int cap, Tensor(c!) err) -> ()");
 }
 
-TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) { m.impl("custom_all_reduce", &custom_all_reduce); }
+TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
+  m.impl("custom_all_reduce", &custom_all_reduce);
+  m.impl("fused_adamw", &fused_adamw);
+}

@@ -1,0 +1,303 @@
+"""LoRA / QLoRA / QA-LoRA on low-bit base weights (a self-contained,
+peft-compatible API; ``peft`` is not a dependency).
+
+Reference: ``SRC/transformers/qlora.py`` -- ``LoraLowBitLinear`` (66-143:
+frozen low-bit base + LoRA A/B, QA-LoRA average-pools the input by the
+quantization group size), ``LoraBF16Linear`` (146-211), ``get_peft_model``
+(282-301), ``prepare_model_for_kbit_training`` (304-352), ``LoraConfig``
+with ``training_mode`` (254-267), ``cast_lora_weight`` (377-391).
+
+MI355X design: the base ``LowBitLinear`` runs the low-bit GEMM forward
+(decode-class GEMV for small M, dequant+GEMM for training batches) and its
+backward through ``MatMulLowBit`` (grad_x = grad_y @ dequant(W), no weight
+gradient); the adapters are plain bf16 parameters updated by the fused
+multi-tensor AdamW kernel (``training/optim.py``).  Checkpoints are
+``adapter_model.safetensors`` + ``adapter_config.json`` (peft's file names,
+so adapters interoperate).
+"""
+from __future__ import annotations
+
+import contextlib
+import json
+import math
+import os
+import re
+from dataclasses import asdict, dataclass, field
+from typing import Dict, List, Optional, Union
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..quantize import qtypes as Q
+from ..transformers.low_bit_linear import DenseLinear, LowBitLinear
+
+TRAINING_MODES = ("qlora", "lora", "qalora", "relora")
+
+
+@dataclass
+class LoraConfig:
+    r: int = 8
+    lora_alpha: int = 16
+    lora_dropout: float = 0.0
+    target_modules: Optional[Union[List[str], str]] = None
+    bias: str = "none"
+    task_type: Optional[str] = "CAUSAL_LM"
+    training_mode: str = "qlora"
+    use_rslora: bool = False
+    modules_to_save: Optional[List[str]] = None
+    init_lora_weights: bool = True
+    peft_type: str = "LORA"
+
+    def __post_init__(self):
+        if self.training_mode not in TRAINING_MODES:
+            raise ValueError(f"training_mode must be one of {TRAINING_MODES}")
+
+    @property
+    def scaling(self) -> float:
+        return self.lora_alpha / (math.sqrt(self.r) if self.use_rslora else self.r)
+
+    def to_dict(self):
+        return asdict(self)
+
+    def save_pretrained(self, path):
+        os.makedirs(path, exist_ok=True)
+        with open(os.path.join(path, "adapter_config.json"), "w") as f:
+            json.dump(self.to_dict(), f, indent=2)
+
+    @classmethod
+    def from_pretrained(cls, path):
+        with open(os.path.join(path, "adapter_config.json")) as f:
+            d = json.load(f)
+        keys = cls.__dataclass_fields__.keys()
+        return cls(**{k: v for k, v in d.items() if k in keys})
+
+
+DEFAULT_TARGETS = ["q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj",
+                   "qkv_proj", "gate_up_proj", "query_key_value", "dense", "W_pack"]
+
+
+class LoraLinear(nn.Module):
+    """base(x) + B(A(dropout(pool(x)))) * scaling over a frozen base layer
+    (LowBitLinear -> QLoRA/QA-LoRA, DenseLinear/nn.Linear -> LoRA)."""
+
+    def __init__(self, base: nn.Module, r: int, alpha: int, dropout: float = 0.0, qa_lora: bool = False,
+                 use_rslora: bool = False, dtype=torch.bfloat16):
+        super().__init__()
+        self.base_layer = base
+        for p in base.parameters():
+            p.requires_grad_(False)
+        self.in_features, self.out_features = base.in_features, base.out_features
+        self.r, self.lora_alpha = r, alpha
+        self.scaling = alpha / (math.sqrt(r) if use_rslora else r)
+        self.qa_group = 0
+        if qa_lora:
+            if not isinstance(base, LowBitLinear):
+                raise ValueError("QA-LoRA needs a low-bit base layer")
+            self.qa_group = Q.get_format(base.qtype).block
+        in_a = self.in_features // self.qa_group if self.qa_group else self.in_features
+        dev = base.weight.device if base.weight.device.type != "meta" else "cpu"
+        self.lora_A = nn.Linear(in_a, r, bias=False, device=dev, dtype=dtype)
+        self.lora_B = nn.Linear(r, self.out_features, bias=False, device=dev, dtype=dtype)
+        self.lora_dropout = nn.Dropout(dropout) if dropout > 0 else nn.Identity()
+        self.reset_lora_parameters()
+        self.merged = False
+        self.disable_adapters = False
+
+    def reset_lora_parameters(self):
+        nn.init.kaiming_uniform_(self.lora_A.weight, a=math.sqrt(5))
+        nn.init.zeros_(self.lora_B.weight)
+
+    def _pool(self, x):
+        if not self.qa_group:
+            return x
+        return x.reshape(*x.shape[:-1], self.in_features // self.qa_group, self.qa_group).mean(-1)
+
+    def forward(self, x):
+        result = self.base_layer(x)
+        if self.disable_adapters or self.merged:
+            return result
+        a = self.lora_A.weight
+        h = self._pool(self.lora_dropout(x)).to(a.dtype)
+        return result + (self.lora_B(self.lora_A(h)) * self.scaling).to(result.dtype)
+
+    def delta_weight(self) -> torch.Tensor:
+        """dense [out, in] update B @ A * scaling (QA-LoRA expanded per group)"""
+        d = (self.lora_B.weight.float() @ self.lora_A.weight.float()) * self.scaling
+        if self.qa_group:
+            d = d.repeat_interleave(self.qa_group, dim=1) / self.qa_group
+        return d
+
+    @torch.no_grad()
+    def merge(self):
+        """fold the adapter into the base weight (re-quantized for low-bit)"""
+        base = self.base_layer
+        d = self.delta_weight()
+        if isinstance(base, LowBitLinear):
+            w = base.dequantize(torch.float32) + d.to(base.weight.device)
+            base.load_dense(w, device=base.weight.device)
+        else:
+            base.weight.data += d.to(base.weight.device, base.weight.dtype)
+        self.merged = True
+
+
+def _match(name: str, targets) -> bool:
+    if targets is None:
+        targets = DEFAULT_TARGETS
+    if isinstance(targets, str):
+        return re.fullmatch(targets, name) is not None
+    leaf = name.split(".")[-1]
+    return leaf in targets or any(name.endswith("." + t) for t in targets)
+
+
+class PeftModel(nn.Module):
+    """Wrapper returned by :func:`get_peft_model` (peft.PeftModel-like)."""
+
+    def __init__(self, model: nn.Module, config: LoraConfig):
+        super().__init__()
+        self.base_model = model
+        self.peft_config = {"default": config}
+
+    def __getattr__(self, name):
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            return getattr(self.base_model, name)
+
+    def forward(self, *args, **kwargs):
+        return self.base_model(*args, **kwargs)
+
+    def generate(self, *args, **kwargs):
+        return self.base_model.generate(*args, **kwargs)
+
+    def lora_modules(self) -> Dict[str, LoraLinear]:
+        return {n: m for n, m in self.base_model.named_modules() if isinstance(m, LoraLinear)}
+
+    def adapter_state_dict(self) -> Dict[str, torch.Tensor]:
+        sd = {}
+        for n, m in self.lora_modules().items():
+            sd[f"{n}.lora_A.weight"] = m.lora_A.weight.detach().cpu().contiguous()
+            sd[f"{n}.lora_B.weight"] = m.lora_B.weight.detach().cpu().contiguous()
+        cfg = self.peft_config["default"]
+        for n, p in self.base_model.named_parameters():
+            if cfg.modules_to_save and any(s in n for s in cfg.modules_to_save) and p.requires_grad:
+                sd[n] = p.detach().cpu().contiguous()
+        return sd
+
+    def save_pretrained(self, path: str, **_):
+        from safetensors.torch import save_file
+        os.makedirs(path, exist_ok=True)
+        save_file(self.adapter_state_dict(), os.path.join(path, "adapter_model.safetensors"))
+        self.peft_config["default"].save_pretrained(path)
+
+    @torch.no_grad()
+    def load_adapter(self, path: str):
+        from safetensors.torch import load_file
+        sd = load_file(os.path.join(path, "adapter_model.safetensors"))
+        mods = self.lora_modules()
+        params = dict(self.base_model.named_parameters())
+        for k, v in sd.items():
+            if ".lora_A." in k or ".lora_B." in k:
+                mname, which = k.rsplit(".lora_", 1)
+                lin = getattr(mods[mname], "lora_" + which.split(".")[0])
+                lin.weight.copy_(v.to(lin.weight.device, lin.weight.dtype))
+            elif k in params:
+                params[k].copy_(v.to(params[k].device, params[k].dtype))
+        return self
+
+    @classmethod
+    def from_pretrained(cls, model: nn.Module, path: str, is_trainable: bool = False, **_):
+        cfg = LoraConfig.from_pretrained(path)
+        pm = get_peft_model(model, cfg)
+        pm.load_adapter(path)
+        if not is_trainable:
+            for p in pm.parameters():
+                p.requires_grad_(False)
+        return pm
+
+    @contextlib.contextmanager
+    def disable_adapter(self):
+        mods = list(self.lora_modules().values())
+        for m in mods:
+            m.disable_adapters = True
+        try:
+            yield
+        finally:
+            for m in mods:
+                m.disable_adapters = False
+
+    def merge_and_unload(self) -> nn.Module:
+        for name, m in list(self.lora_modules().items()):
+            m.merge()
+            parent = self.base_model.get_submodule(name.rsplit(".", 1)[0]) if "." in name else self.base_model
+            setattr(parent, name.rsplit(".", 1)[-1], m.base_layer)
+        return self.base_model
+
+    def get_nb_trainable_parameters(self):
+        tr = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        tot = sum(p.numel() for p in self.parameters())
+        return tr, tot
+
+    def print_trainable_parameters(self):
+        tr, tot = self.get_nb_trainable_parameters()
+        print(f"trainable params: {tr:,d} || all params: {tot:,d} || trainable%: {100 * tr / max(tot, 1):.4f}")
+
+
+def get_peft_model(model: nn.Module, config: LoraConfig, adapter_name: str = "default") -> PeftModel:
+    """Wrap every targeted linear of ``model`` with a LoRA adapter."""
+    for p in model.parameters():
+        p.requires_grad_(False)
+    qa = config.training_mode == "qalora"
+    n = 0
+    for name, mod in list(model.named_modules()):
+        for cname, child in list(mod.named_children()):
+            full = f"{name}.{cname}" if name else cname
+            if not isinstance(child, (LowBitLinear, DenseLinear, nn.Linear)) or isinstance(child, LoraLinear):
+                continue
+            if not _match(full, config.target_modules):
+                continue
+            setattr(mod, cname, LoraLinear(child, config.r, config.lora_alpha, config.lora_dropout,
+                                           qa_lora=qa and isinstance(child, LowBitLinear),
+                                           use_rslora=config.use_rslora))
+            n += 1
+    if n == 0:
+        raise ValueError(f"no module matched target_modules={config.target_modules}")
+    if config.modules_to_save:
+        for pn, p in model.named_parameters():
+            if any(s in pn for s in config.modules_to_save) and p.is_floating_point():
+                p.requires_grad_(True)
+    return PeftModel(model, config)
+
+
+def prepare_model_for_kbit_training(model: nn.Module, use_gradient_checkpointing: bool = True) -> nn.Module:
+    """Freeze the base, keep norms in fp32, make inputs require grad (so
+    checkpointed blocks backprop into the adapters) and enable gradient
+    checkpointing (reference qlora.py:304-352)."""
+    for p in model.parameters():
+        p.requires_grad_(False)
+    for m in model.modules():
+        if not list(m.children()) and not isinstance(m, (LowBitLinear, DenseLinear, nn.Linear, nn.Embedding)):
+            for p in m.parameters():
+                if p.dtype in (torch.float16, torch.bfloat16):
+                    p.data = p.data.float()
+    if use_gradient_checkpointing:
+        if hasattr(model, "enable_input_require_grads"):
+            model.enable_input_require_grads()
+        else:
+            model.get_input_embeddings().register_forward_hook(lambda m, i, o: o.requires_grad_(True))
+        if hasattr(model, "gradient_checkpointing_enable"):
+            model.gradient_checkpointing_enable(gradient_checkpointing_kwargs={"use_reentrant": False})
+    return model
+
+
+def cast_lora_weight(model: nn.Module, dtype=torch.bfloat16):
+    """adapters and bf16 layers in ``dtype``, norms in fp32 (qlora.py:377-391)"""
+    for name, m in model.named_modules():
+        if isinstance(m, LowBitLinear):
+            m.compute_dtype = dtype
+        if isinstance(m, LoraLinear):
+            m.lora_A.to(dtype)
+            m.lora_B.to(dtype)
+        if "norm" in name and not list(m.children()):
+            m.to(torch.float32)
+    return model

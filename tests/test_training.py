@@ -1,0 +1,159 @@
+"""LoRA / QLoRA / QA-LoRA / ReLoRA / LISA fine-tuning on CPU, FusedAdamW vs
+torch.optim.AdamW, adapter save/load, merge, DDP (gloo) consistency.
+Reference: example/GPU/LLM-Finetuning (QLoRA, QA-LoRA, ReLoRA, LISA)."""
+import os
+
+import pytest
+import torch
+
+
+def _model(tmp_path, qtype="sym_int4"):
+    from transformers import LlamaConfig, LlamaForCausalLM
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    torch.manual_seed(0)
+    cfg = LlamaConfig(vocab_size=128, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256)
+    p = str(tmp_path / "base")
+    if not os.path.exists(p):
+        LlamaForCausalLM(cfg).save_pretrained(p)
+    return AutoModelForCausalLM.from_pretrained(p, load_in_low_bit=qtype, optimize_model=False,
+                                                torch_dtype=torch.float32, modules_to_not_convert=["lm_head"])
+
+
+def _train(model, steps=12, lr=5e-3):
+    from ipex_llm_amd.training import FusedAdamW
+    opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=lr, weight_decay=0.0)
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(0, 128, (4, 16), generator=g)
+    losses = []
+    for _ in range(steps):
+        out = model(input_ids=ids, labels=ids)
+        out.loss.backward()
+        opt.step()
+        opt.zero_grad()
+        losses.append(out.loss.item())
+    return losses, ids
+
+
+@pytest.mark.parametrize("mode", ["qlora", "qalora", "lora"])
+def test_lora_training_reduces_loss(tmp_path, mode):
+    from ipex_llm_amd.training import LoraConfig, get_peft_model, prepare_model_for_kbit_training
+    model = _model(tmp_path, "bf16" if mode == "lora" else "sym_int4")
+    model = prepare_model_for_kbit_training(model, use_gradient_checkpointing=False)
+    pm = get_peft_model(model, LoraConfig(r=8, lora_alpha=16, target_modules=["q_proj", "v_proj", "down_proj"],
+                                          training_mode=mode))
+    tr, tot = pm.get_nb_trainable_parameters()
+    assert 0 < tr < tot
+    losses, ids = _train(pm)
+    assert losses[-1] < losses[0] - 0.05, losses
+    # adapter round trip
+    pm.save_pretrained(str(tmp_path / "adapter"))
+    from ipex_llm_amd.training import PeftModel
+    fresh = _model(tmp_path, "bf16" if mode == "lora" else "sym_int4")
+    pm2 = PeftModel.from_pretrained(fresh, str(tmp_path / "adapter"))
+    with torch.no_grad():
+        a = pm(input_ids=ids).logits
+        b = pm2(input_ids=ids).logits
+    assert torch.allclose(a, b, atol=1e-4)
+    with pm2.disable_adapter(), torch.no_grad():
+        c = pm2(input_ids=ids).logits
+    assert not torch.allclose(a, c, atol=1e-3)
+    merged = pm2.merge_and_unload()
+    with torch.no_grad():
+        d = merged(input_ids=ids).logits
+    tol = 1e-2 if mode == "lora" else 0.15     # bf16 rounding / low-bit re-quantization
+    assert ((d - a).norm() / a.norm()).item() < tol
+
+
+def test_fused_adamw_matches_torch_cpu():
+    from ipex_llm_amd.training import FusedAdamW
+    torch.manual_seed(0)
+    p1 = [torch.nn.Parameter(torch.randn(37, 5)), torch.nn.Parameter(torch.randn(100))]
+    p2 = [torch.nn.Parameter(p.detach().clone()) for p in p1]
+    o1 = FusedAdamW(p1, lr=1e-2, weight_decay=0.1)
+    o2 = torch.optim.AdamW(p2, lr=1e-2, weight_decay=0.1)
+    for _ in range(5):
+        for a, b in zip(p1, p2):
+            g = torch.randn_like(a)
+            a.grad, b.grad = g.clone(), g.clone()
+        o1.step()
+        o2.step()
+    for a, b in zip(p1, p2):
+        assert torch.allclose(a, b, atol=1e-6)
+
+
+def test_relora_restart_and_scheduler(tmp_path):
+    from ipex_llm_amd.training import FusedAdamW, LoraConfig, get_peft_model, relora_restart, ReLoRAScheduler
+    pm = get_peft_model(_model(tmp_path), LoraConfig(r=4, target_modules=["q_proj"], training_mode="relora"))
+    losses, ids = _train(pm, steps=6)
+    with torch.no_grad():
+        before = pm(input_ids=ids).logits
+    opt = FusedAdamW([p for p in pm.parameters() if p.requires_grad])
+    n = relora_restart(pm, opt)
+    assert n == 2
+    with torch.no_grad():
+        after = pm(input_ids=ids).logits            # merged into the base; adapters restarted (B = 0)
+    assert ((after - before).norm() / before.norm()).item() < 0.1
+    for m in pm.lora_modules().values():
+        assert torch.count_nonzero(m.lora_B.weight) == 0
+    sch = ReLoRAScheduler(torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=1.0), 100, 20, 5, 5)
+    lrs = []
+    for _ in range(30):
+        lrs.append(sch.get_last_lr()[0])
+        sch.optimizer.step()
+        sch.step()
+    assert lrs[0] == 0 and lrs[20] < lrs[19]          # re-warmup after the restart
+
+
+def test_lisa_switches_layers(tmp_path):
+    from ipex_llm_amd.training import LayerActivation
+    m = _model(tmp_path, "bf16")
+    act = LayerActivation(m, n_layers=1, interval_steps=2)
+    a = act.maybe_switch(0)
+    assert len(a) == 1
+    on = [any(p.requires_grad for p in L.parameters()) for L in m.model.layers]
+    assert sum(on) == 1
+    assert act.maybe_switch(1) is None
+
+
+def _ddp_worker(rank, world, port, path):
+    import os as _os
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    from ipex_llm_amd.training import FusedAdamW, LoraConfig, get_peft_model, wrap_ddp
+    m = AutoModelForCausalLM.from_pretrained(path, load_in_low_bit="sym_int4", optimize_model=False,
+                                             torch_dtype=torch.float32)
+    pm = get_peft_model(m, LoraConfig(r=4, target_modules=["q_proj", "v_proj"]))
+    torch.manual_seed(0)
+    for mod in pm.lora_modules().values():
+        mod.reset_lora_parameters()
+    ddp = wrap_ddp(pm)
+    opt = FusedAdamW([p for p in ddp.parameters() if p.requires_grad], lr=1e-2)
+    ids = torch.randint(0, 128, (2, 12), generator=torch.Generator().manual_seed(rank))
+    for _ in range(3):
+        loss = ddp(input_ids=ids, labels=ids).loss
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+    v = torch.cat([p.detach().flatten() for p in pm.parameters() if p.requires_grad])
+    vs = [torch.empty_like(v) for _ in range(world)]
+    dist.all_gather(vs, v)
+    assert torch.allclose(vs[0], vs[1]), "replicas diverged"
+    dist.destroy_process_group()
+
+
+def test_ddp_lora_replicas_stay_identical(tmp_path):
+    from tests.test_distributed import _free_port
+    import torch.multiprocessing as mp
+    _model(tmp_path)
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_ddp_worker, args=(r, 2, port, str(tmp_path / "base"))) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    assert [p.exitcode for p in ps] == [0, 0]
