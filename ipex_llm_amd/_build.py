@@ -4,6 +4,7 @@ Three kinds of translation units, compiled in parallel:
   * ``csrc/hip/*.hip``   gfx950 kernels       -> hipcc --offload-arch=gfx950
   * ``csrc/cpu/*.cpp``   host quantizers/GEMM -> g++ -O3 -fopenmp (no torch)
   * ``csrc/torch/*.cpp`` torch.library ops    -> hipcc (host C++, torch headers)
+  * ``csrc/runtime/*.cpp`` serving runtime (scheduler / block manager, torch custom classes)
 and linked into one shared object loaded with ``torch.ops.load_library``.
 Objects are cached under ``build/obj`` and rebuilt when the source or any
 header under ``csrc`` is newer.  Usage: ``python -m ipex_llm_amd._build``.
@@ -57,7 +58,8 @@ def _cmd(src: str, obj: str):
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")) +
                   glob.glob(os.path.join(CSRC, "cpu", "*.cpp")) +
-                  glob.glob(os.path.join(CSRC, "torch", "*.cpp")))
+                  glob.glob(os.path.join(CSRC, "torch", "*.cpp")) +
+                  glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
 
 
 def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> str:

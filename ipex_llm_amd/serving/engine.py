@@ -1,0 +1,247 @@
+"""Continuous-batching LLM engine for serving.
+
+Reference: ``SRC/serving/fastapi/model_worker.py`` (one request at a time
+through HF ``generate`` + ``TextIteratorStreamer``) and the vLLM engine
+integration (``SRC/vllm/xpu/engine/engine.py``).
+
+MI355X design: requests share one paged KV pool sized from free HBM (288 GB
+holds thousands of 8K-token Llama-3-8B sequences); the C++ scheduler
+(``csrc/runtime/scheduler.cpp``) decides per step which sequences are
+prefilled / decoded / preempted; every decode step is ONE batched native
+forward over all running sequences (flash-decoding over their own block
+tables), so throughput scales with concurrency instead of serialising
+requests.
+"""
+from __future__ import annotations
+
+import itertools
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from .. import ops
+from ..engine.runner import _sample, apply_repetition_penalty, nsplit_for
+from ..models.cache import PagedKVCache
+from ..models.decoder import AttnMeta, NativeCausalLM
+
+
+@dataclass
+class SamplingParams:
+    max_new_tokens: int = 32
+    min_new_tokens: int = 0
+    temperature: float = 1.0
+    top_k: int = 0
+    top_p: float = 1.0
+    do_sample: bool = False
+    repetition_penalty: float = 1.0
+    stop_token_ids: List[int] = field(default_factory=list)
+    seed: Optional[int] = None
+
+
+@dataclass
+class Request:
+    rid: int
+    prompt: List[int]
+    params: SamplingParams
+    tokens: List[int] = field(default_factory=list)     # prompt + generated
+    generated: List[int] = field(default_factory=list)
+    finished: bool = False
+    finish_reason: Optional[str] = None
+    arrival: float = 0.0
+    first_token_time: Optional[float] = None
+    on_token: Optional[Callable[[int, "Request"], None]] = None
+    generator: Optional[torch.Generator] = None
+
+
+class LLMEngine:
+    def __init__(self, model: NativeCausalLM, max_batch: int = 64, block_size: int = 64,
+                 num_blocks: Optional[int] = None, max_model_len: int = 8192, max_prefill_tokens: int = 8192,
+                 kv_fp8: int = 0, memory_fraction: float = 0.5, eos_token_id=None):
+        ops.require() if model.device.type == "cuda" else None
+        self.model = model
+        s = model.spec
+        if num_blocks is None:
+            per_tok = PagedKVCache.bytes_per_token(len(model.layers), s.num_kv_heads, s.head_dim, model.dtype, kv_fp8)
+            if model.device.type == "cuda":
+                free, _ = torch.cuda.mem_get_info(model.device)
+                budget = int(free * memory_fraction)
+            else:
+                budget = per_tok * max_batch * max_model_len // 4
+            num_blocks = max(max_batch, budget // (per_tok * block_size))
+            num_blocks = min(num_blocks, max_batch * ((max_model_len + block_size - 1) // block_size))
+        self.cache = model.make_cache(max_model_len, max_batch, block_size, kv_fp8, num_blocks=num_blocks)
+        model.ensure_rope_cache(max_model_len + 1)
+        self.sched = torch.classes.ipex_llm_amd.Scheduler(num_blocks, block_size, max_batch, max_prefill_tokens)
+        self.block_size, self.max_model_len = block_size, max_model_len
+        eos = eos_token_id if eos_token_id is not None else []
+        self.eos = set([eos] if isinstance(eos, int) else eos)
+        self.requests: Dict[int, Request] = {}
+        self._ids = itertools.count()
+        self.lock = threading.Lock()
+        self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "preemptions": 0}
+
+    # ------------------------------------------------------------ API
+    def add_request(self, prompt: List[int], params: Optional[SamplingParams] = None,
+                    on_token: Optional[Callable] = None) -> int:
+        params = params or SamplingParams()
+        if len(prompt) + params.max_new_tokens > self.max_model_len:
+            raise ValueError(f"prompt ({len(prompt)}) + max_new_tokens exceeds max_model_len={self.max_model_len}")
+        with self.lock:
+            rid = next(self._ids)
+            g = None
+            if params.seed is not None:
+                g = torch.Generator(device=self.model.device).manual_seed(params.seed)
+            r = Request(rid, list(prompt), params, tokens=list(prompt), arrival=time.perf_counter(),
+                        on_token=on_token, generator=g)
+            self.requests[rid] = r
+            self.sched.add(rid, len(prompt))
+        return rid
+
+    def abort(self, rid: int):
+        with self.lock:
+            r = self.requests.get(rid)
+            if r is not None and not r.finished:
+                self._finish(r, "abort")
+
+    def has_work(self) -> bool:
+        return any(not r.finished for r in self.requests.values())
+
+    # ------------------------------------------------------------ step
+    def _finish(self, r: Request, reason: str):
+        r.finished, r.finish_reason = True, reason
+        try:
+            self.sched.finish(r.rid)
+        except RuntimeError:
+            pass
+        if r.on_token is not None:
+            r.on_token(-1, r)
+
+    def _emit(self, r: Request, tok: int):
+        r.tokens.append(tok)
+        r.generated.append(tok)
+        if r.first_token_time is None:
+            r.first_token_time = time.perf_counter() - r.arrival
+        self.sched.grow(r.rid)
+        if r.on_token is not None:
+            r.on_token(tok, r)
+        p = r.params
+        n = len(r.generated)
+        if n >= p.max_new_tokens:
+            self._finish(r, "length")
+        elif n >= p.min_new_tokens and (tok in self.eos or tok in p.stop_token_ids):
+            self._finish(r, "stop")
+
+    def _pick(self, logits: torch.Tensor, r: Request) -> int:
+        p = r.params
+        if p.repetition_penalty != 1.0:
+            logits = apply_repetition_penalty(logits.clone(), [r.tokens], p.repetition_penalty)
+        return int(_sample(logits, p.do_sample, p.temperature, p.top_k, p.top_p, r.generator)[0])
+
+    def _block_table(self, rids: List[int]) -> torch.Tensor:
+        rows = [list(self.sched.blocks(r)) for r in rids]
+        w = max(len(x) for x in rows)
+        t = torch.zeros(len(rows), w, dtype=torch.int32)
+        for i, x in enumerate(rows):
+            t[i, :len(x)] = torch.tensor(x, dtype=torch.int32)
+        return t.to(self.model.device)
+
+    @torch.no_grad()
+    def step(self) -> int:
+        """One scheduler step: prefill admitted requests, decode all running
+        ones.  Returns the number of tokens produced."""
+        with self.lock:
+            plan = list(self.sched.schedule())
+            i1 = plan.index(-1)
+            i2 = plan.index(-1, i1 + 1)
+            i3 = plan.index(-1, i2 + 1)
+            prefill, decode, preempted, failed = plan[:i1], plan[i1 + 1:i2], plan[i2 + 1:i3], plan[i3 + 1:]
+            self.stats["preemptions"] += len(preempted)
+            for rid in failed:
+                r = self.requests[rid]
+                r.finished, r.finish_reason = True, "error: request does not fit in the KV cache"
+                if r.on_token is not None:
+                    r.on_token(-1, r)
+            m, dev, bs = self.model, self.model.device, self.block_size
+            produced = 0
+            for rid in prefill:
+                r = self.requests[rid]
+                toks = r.tokens
+                n = len(toks)
+                bt = self._block_table([rid])
+                pos = torch.arange(n, device=dev)
+                blocks = torch.tensor(list(self.sched.blocks(rid)), dtype=torch.long)
+                slots = (blocks[pos.cpu() // bs] * bs + pos.cpu() % bs).to(dev)
+                meta = AttnMeta(1, n, bt, torch.tensor([n], dtype=torch.int32, device=dev), nsplit_for(n), [n])
+                lg = m.forward_tokens(torch.tensor(toks, device=dev), pos, slots, meta, self.cache,
+                                      logits_idx=torch.tensor([n - 1], device=dev))
+                self.sched.advance(rid, n)
+                self.stats["prefill_tokens"] += n
+                self._emit(r, self._pick(lg, r))
+                produced += 1
+            if decode:
+                rs = [self.requests[rid] for rid in decode]
+                B = len(rs)
+                bt = self._block_table(decode)
+                pos_l = [int(self.sched.cached(rid)) for rid in decode]
+                pos = torch.tensor(pos_l, device=dev)
+                blk = torch.gather(bt, 1, (pos // bs).unsqueeze(1).to(torch.int64)).squeeze(1).long()
+                slots = blk * bs + pos % bs
+                seq_lens = (pos + 1).to(torch.int32)
+                meta = AttnMeta(B, 1, bt, seq_lens, nsplit_for(max(pos_l) + 1), [p + 1 for p in pos_l])
+                ids = torch.tensor([r.tokens[-1] for r in rs], device=dev)
+                lg = m.forward_tokens(ids, pos, slots, meta, self.cache)
+                greedy = all(not r.params.do_sample and r.params.repetition_penalty == 1.0 for r in rs)
+                nxt = torch.argmax(lg, -1).tolist() if greedy else None
+                for i, r in enumerate(rs):
+                    self.sched.advance(r.rid, 1)
+                    self._emit(r, nxt[i] if greedy else self._pick(lg[i:i + 1], r))
+                produced += B
+                self.stats["decode_tokens"] += B
+            self.stats["steps"] += 1
+            return produced
+
+    def generate(self, prompts: List[List[int]], params: Optional[SamplingParams] = None) -> List[List[int]]:
+        """Offline batch: submit everything, run until done (continuous batching)."""
+        rids = [self.add_request(p, params) for p in prompts]
+        while any(not self.requests[r].finished for r in rids):
+            self.step()
+        out = [self.requests[r].generated for r in rids]
+        for r in rids:
+            self.requests.pop(r, None)
+        return out
+
+
+class EngineLoop:
+    """Background thread driving ``LLMEngine.step`` for the API server."""
+
+    def __init__(self, engine: LLMEngine, idle_sleep: float = 0.002):
+        self.engine, self.idle = engine, idle_sleep
+        self._stop = threading.Event()
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.error: Optional[BaseException] = None
+
+    def start(self):
+        self.thread.start()
+        return self
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                if self.engine.has_work():
+                    self.engine.step()
+                else:
+                    time.sleep(self.idle)
+            except BaseException as e:  # pragma: no cover - surfaced to requests
+                self.error = e
+                for r in list(self.engine.requests.values()):
+                    if not r.finished:
+                        r.finished, r.finish_reason = True, f"error: {e}"
+                        if r.on_token is not None:
+                            r.on_token(-1, r)
+
+    def stop(self):
+        self._stop.set()
+        self.thread.join(timeout=5)

@@ -1,0 +1,115 @@
+"""Serving: C++ continuous-batching scheduler, LLMEngine (batched decode,
+preemption/recompute) vs the static engine, and the OpenAI/TGI HTTP API
+(reference: serving/fastapi/api_server.py, openai_protocol.py)."""
+import json
+
+import pytest
+import torch
+
+
+@pytest.fixture(scope="module")
+def native():
+    from transformers import LlamaConfig
+    from ipex_llm_amd.models.builder import random_native_model
+    cfg = LlamaConfig(vocab_size=128, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=1024)
+    return random_native_model(cfg, "sym_int8", "cpu", torch.float32, seed=0, std=0.2)
+
+
+def _sched(nb=4, bs=64, mb=8, mp=4096):
+    import ipex_llm_amd.ops as ops
+    ops.require()
+    return torch.classes.ipex_llm_amd.Scheduler(nb, bs, mb, mp)
+
+
+def _split(plan):
+    i1 = plan.index(-1); i2 = plan.index(-1, i1 + 1); i3 = plan.index(-1, i2 + 1)
+    return plan[:i1], plan[i1 + 1:i2], plan[i2 + 1:i3], plan[i3 + 1:]
+
+
+def test_scheduler_admission_preemption_failure():
+    s = _sched(nb=4, bs=64)
+    s.add(1, 100)          # 2 blocks (room for 101 tokens)
+    s.add(2, 60)           # 1 block
+    s.add(3, 300)          # can never fit in 4 blocks -> failed, queue continues
+    s.add(4, 63)           # 1 block
+    p, d, pre, f = _split(list(s.schedule()))
+    assert p == [1, 2, 4] and d == [] and f == [3] and s.num_free_blocks() == 0
+    for rid, n in ((1, 100), (2, 60), (4, 63)):
+        s.advance(rid, n); s.grow(rid)
+    p, d, pre, f = _split(list(s.schedule()))
+    assert d == [1, 2, 4] and pre == [] and p == []
+    for rid in (1, 2, 4):
+        s.advance(rid, 1); s.grow(rid)
+    # request 4 now needs a second block, the pool is empty: preempt the latest admitted (4)
+    p, d, pre, f = _split(list(s.schedule()))
+    assert pre == [4] and d == [1, 2]
+    assert s.state(4) == 0 and s.context(4) == 65 and s.cached(4) == 0
+    s.finish(1)
+    p, d, pre, f = _split(list(s.schedule()))
+    assert p == [4] and d == [2]
+
+
+def test_engine_matches_static_generate(native):
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.serving.engine import LLMEngine, SamplingParams
+    prompts = [[1, 2, 3, 4, 5], [9, 8, 7], list(range(10, 40))]
+    ref = Engine(native).generate(prompts, max_new_tokens=12, use_graph=False)
+    eng = LLMEngine(native, max_batch=8, max_model_len=256)
+    out = eng.generate(prompts, SamplingParams(max_new_tokens=12))
+    assert [p + o for p, o in zip(prompts, out)] == ref
+
+
+def test_engine_preemption_recompute(native):
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.serving.engine import LLMEngine, SamplingParams
+    prompts = [list(range(1, 60)), list(range(3, 62)), list(range(5, 64))]
+    ref = Engine(native).generate(prompts, max_new_tokens=10, use_graph=False)
+    # 4 blocks of 64: three 60-token prompts fit, but growing past 64 forces preemption
+    eng = LLMEngine(native, max_batch=8, max_model_len=256, num_blocks=4)
+    out = eng.generate(prompts, SamplingParams(max_new_tokens=10))
+    assert eng.stats["preemptions"] > 0
+    assert [p + o for p, o in zip(prompts, out)] == ref
+
+
+def _tokenizer():
+    from tokenizers import Tokenizer, models, pre_tokenizers
+    from transformers import PreTrainedTokenizerFast
+    vocab = {"<unk>": 0, "<s>": 1, "</s>": 2}
+    for i in range(3, 128):
+        vocab[f"w{i}"] = i
+    tk = Tokenizer(models.WordLevel(vocab, unk_token="<unk>"))
+    tk.pre_tokenizer = pre_tokenizers.WhitespaceSplit()
+    from tokenizers import decoders
+    tk.decoder = decoders.WordPiece(prefix="##")
+    return PreTrainedTokenizerFast(tokenizer_object=tk, unk_token="<unk>", bos_token="<s>", eos_token="</s>")
+
+
+def test_http_api(native):
+    from fastapi.testclient import TestClient
+    from ipex_llm_amd.serving.api_server import build_app
+    from ipex_llm_amd.serving.engine import LLMEngine
+    tok = _tokenizer()
+    eng = LLMEngine(native, max_batch=4, max_model_len=256, eos_token_id=None)
+    app = build_app(eng, tok, "tiny")
+    with TestClient(app) as c:
+        assert c.get("/health").json()["status"] == "ok"
+        assert c.get("/v1/models").json()["data"][0]["id"] == "tiny"
+        r = c.post("/v1/completions", json={"prompt": "w5 w6 w7", "max_tokens": 5}).json()
+        assert r["object"] == "text_completion" and r["usage"]["completion_tokens"] == 5
+        assert len(r["choices"][0]["text"].split()) >= 1
+        r2 = c.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "w9 w10"}],
+                                                   "max_tokens": 4}).json()
+        assert r2["choices"][0]["message"]["role"] == "assistant"
+        with c.stream("POST", "/v1/chat/completions", json={"messages": "w9 w10", "max_tokens": 4,
+                                                              "stream": True}) as s:
+            lines = [l for l in s.iter_lines() if l]
+        assert lines[-1] == "data: [DONE]"
+        chunks = [json.loads(l[6:]) for l in lines[:-1]]
+        assert chunks[-1]["choices"][0]["finish_reason"] == "length"
+        g = c.post("/generate", json={"inputs": "w5 w6 w7", "parameters": {"max_new_tokens": 5}}).json()
+        assert g[1] == r["choices"][0]["text"]      # same greedy continuation
+        with c.stream("POST", "/generate_stream", json={"inputs": "w5 w6 w7",
+                                                         "parameters": {"max_new_tokens": 3}}) as s:
+            ev = [json.loads(l[6:]) for l in s.iter_lines() if l]
+        assert ev[-1]["details"]["generated_tokens"] == 3
