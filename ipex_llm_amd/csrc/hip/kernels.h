@@ -96,6 +96,9 @@ void launch_moe_align(const int32_t* ids, int P, int e0, int El, int32_t* off, i
 void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float* w, const int32_t* ids, int k,
                         int e0, int El, uint16_t* out, int Tn, int H, hipStream_t st);
 
+void launch_embedding_rows(bool bf16, const uint8_t* blob, int fmt, const int64_t* ids, int T, int64_t n, int64_t k,
+                           uint16_t* out, hipStream_t st);
+
 // ---- one-shot xGMI peer all-reduce (allreduce.hip) ------------------------
 constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_BLOCKS = 64;

@@ -318,4 +318,45 @@ void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float
   else hipLaunchKernelGGL(moe_combine_kernel<F16>, grid, dim3(256), 0, st, part, ks, P, w, ids, k, e0, El, out, Tn, H);
 }
 
+// ---- low-bit embedding gather: canonical blob rows -> dense [T, k] --------------
+// (reference xe_linear.dequantize_rows, SRC/transformers/embedding.py:213-224)
+template <typename T>
+__global__ void embedding_rows_kernel(const uint8_t* blob, int fmt, const int64_t* ids, int64_t n, int64_t k,
+                                      uint16_t* out) {
+  const int t = blockIdx.y;
+  const int64_t kk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (kk >= k) return;
+  int64_t row = ids[t];
+  row = row < 0 ? 0 : (row >= n ? n - 1 : row);
+  const int bits = fmt_bits(fmt);
+  const int64_t nb = k / QBLOCK;
+  const uint8_t* codes = blob + row * (k * bits / 8);
+  const uint16_t* scales = (const uint16_t*)(blob + canon_code_bytes(fmt, n, k));
+  const uint16_t* mins = scales + canon_scale_elems(n, k);
+  float v[2];
+#pragma unroll
+  for (int e = 0; e < 2; e++) {
+    const int64_t x = kk + e;
+    const int64_t b = x / QBLOCK, j = x % QBLOCK;
+    int code;
+    if (bits == 4) {
+      const uint8_t byte = codes[b * 32 + (j & 31)];
+      code = j < 32 ? (byte & 15) : (byte >> 4);
+    } else {
+      code = codes[x];
+    }
+    const float d = f16_to_f32(scales[row * nb + b]);
+    const float m = fmt_has_min(fmt) ? f16_to_f32(mins[row * nb + b]) : 0.f;
+    v[e] = hd_code_value(fmt, code) * d + m;
+  }
+  *(uint32_t*)(out + (size_t)t * k + kk) = pack2<T>(v[0], v[1]);
+}
+
+void launch_embedding_rows(bool bf16, const uint8_t* blob, int fmt, const int64_t* ids, int T, int64_t n, int64_t k,
+                           uint16_t* out, hipStream_t st) {
+  dim3 grid((unsigned)((k / 2 + 255) / 256), (unsigned)T);
+  if (bf16) hipLaunchKernelGGL(embedding_rows_kernel<BF16>, grid, dim3(256), 0, st, blob, fmt, ids, n, k, out);
+  else hipLaunchKernelGGL(embedding_rows_kernel<F16>, grid, dim3(256), 0, st, blob, fmt, ids, n, k, out);
+}
+
 }  // namespace illm

@@ -119,6 +119,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("reduce_partials(Tensor ws, Tensor? bias, ScalarType dtype) -> Tensor");
   m.def("moe_topk(Tensor logits, int k, bool renorm, int scoring) -> (Tensor, Tensor)");
   m.def("moe_align(Tensor ids, int e0, int num_local) -> (Tensor, Tensor)");
+  m.def("embedding_lowbit(Tensor blob, int fmt, int n, int k, Tensor ids, ScalarType dtype) -> Tensor");
   m.def("moe_gemv(Tensor x, Tensor blob, int fmt, int n, int k, Tensor off, Tensor rows, int xdiv, int npairs, int epi, int ksplit, int act) -> Tensor");
   m.def("moe_combine(Tensor part, Tensor w, Tensor ids, int e0, int num_local, ScalarType dtype) -> Tensor");
 }

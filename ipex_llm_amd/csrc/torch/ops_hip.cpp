@@ -428,9 +428,26 @@ Tensor moe_combine(const Tensor& part, const Tensor& w, const Tensor& ids, int64
   return out;
 }
 
+Tensor embedding_lowbit(const Tensor& blob, int64_t fmt, int64_t n, int64_t k, const Tensor& ids,
+                        at::ScalarType dt) {
+  c10::DeviceGuard g(blob.device());
+  TORCH_CHECK(k % 64 == 0, "embedding_lowbit: hidden % 64");
+  TORCH_CHECK(blob.numel() >= illm::canon_total_bytes((int)fmt, n, k), "embedding_lowbit: blob too small");
+  Tensor idc = ids.to(at::kLong).contiguous();
+  auto shape = idc.sizes().vec();
+  shape.push_back(k);
+  Tensor out = at::empty(shape, blob.options().dtype(dt));
+  const int64_t T = idc.numel();
+  if (T > 0)
+    illm::launch_embedding_rows(dt == at::kBFloat16, blob.data_ptr<uint8_t>(), (int)fmt, idc.data_ptr<int64_t>(),
+                                (int)T, n, k, m16(out), cur_stream());
+  return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
+  m.impl("embedding_lowbit", &embedding_lowbit);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemv", &moe_gemv);
   m.impl("moe_combine", &moe_combine);

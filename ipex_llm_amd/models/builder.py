@@ -212,13 +212,18 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
     first = pp is None or pp["rank"] == 0
     last = pp is None or pp["rank"] == pp["stages"] - 1
     ln0 = layers[0].input_layernorm
-    emb = base.embed_tokens.weight.data if first else ln0.data.new_empty(0)
+    if not first:
+        emb = ln0.data.new_empty(0)
+    elif isinstance(base.embed_tokens, nn.Embedding):
+        emb = base.embed_tokens.weight.data
+    else:
+        emb = base.embed_tokens          # CPU / disk / low-bit embedding module
     lm_head = hf_model.get_output_embeddings() if last else None
     norm = base.norm.weight.data if last else ln0.data
     inv_freq, att_scale = compute_inv_freq(cfg, spec.head_dim, spec.rot_dim or spec.head_dim)
     spec.rope_attention_scaling = att_scale
     model = NativeCausalLM(spec, emb, layers, norm, lm_head, inv_freq.to(ln0.device),
-                           dtype or (emb.dtype if first else ln0.dtype))
+                           dtype or (emb.dtype if isinstance(emb, torch.Tensor) and first else ln0.dtype))
     model.first_stage, model.last_stage = first, last
     if pp is not None:
         model.layer_offset = pp["start"]

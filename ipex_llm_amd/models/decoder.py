@@ -173,7 +173,12 @@ class NativeCausalLM(nn.Module):
         super().__init__()
         self.spec = spec
         self.dtype = dtype
-        self.embed_tokens = nn.Parameter(embed, requires_grad=False)
+        if isinstance(embed, nn.Module):     # CPU / disk / low-bit embedding module
+            self.embed_module = embed
+            self.embed_tokens = None
+        else:
+            self.embed_module = None
+            self.embed_tokens = nn.Parameter(embed, requires_grad=False)
         self.layers = nn.ModuleList(layers)
         self.norm = nn.Parameter(norm, requires_grad=False)
         self.lm_head = lm_head
@@ -298,7 +303,8 @@ class NativeCausalLM(nn.Module):
         if hidden_in is not None:
             residual = hidden_in.to(self.dtype).contiguous().clone()
         else:
-            h = F.embedding(ids, self.embed_tokens)
+            h = self.embed_module(ids).to(self.dtype) if self.embed_module is not None else \
+                F.embedding(ids, self.embed_tokens)
             if s.embed_scale != 1.0:
                 h = h * torch.tensor(s.embed_scale, dtype=h.dtype, device=h.device)
             residual = h.contiguous()
