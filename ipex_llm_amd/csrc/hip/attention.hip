@@ -384,17 +384,36 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     a.part_ml[prow * 2] = m;
     a.part_ml[prow * 2 + 1] = l;
   }
+  if (a.counters == nullptr) return;
+  // ---- fused combine: the last split block of this (b, kv head) merges the
+  // partials of its R query rows (saves the combine launch; counters are
+  // reset by the merging block, so graph replays start from zero)
+  __shared__ int is_last;
+  __threadfence();
+  __syncthreads();
+  if (lane == 0) {
+    const int ns = min(a.nsplit, (len + SPLIT - 1) / SPLIT);
+    int* ctr = a.counters + (size_t)b * a.Hkv + kvh;
+    const int prev = atomicAdd(ctr, 1);
+    is_last = prev == ns - 1;
+    if (is_last) *ctr = 0;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();
+  float* wsh = &ps[0][0];        // SPLIT * RT floats of LDS, reused
+  for (int r = 0; r < R; r++) combine_row<T>(a, b, kvh * group + r % group, r / group, wsh);
 }
 
+// merge the nsplit partial (o, m, l) of one (b, h, t) row: split weights
+// lane-parallel into LDS, then every lane sums its head dims with
+// independent loads.
 template <typename T>
-__global__ void __launch_bounds__(64) attn_combine_kernel(const AttnDecodeArgs a) {
-  const int h = blockIdx.x, t = blockIdx.y, b = blockIdx.z, lane = threadIdx.x;
+__device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int h, int t, float* wsh) {
+  const int lane = threadIdx.x;
   const int len = a.seq_lens[b];
   const int ns = min(a.nsplit, (len + SPLIT - 1) / SPLIT);
   const size_t row0 = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit;
-  // split weights computed lane-parallel (all loads in flight together), kept
-  // in LDS; then every lane sums its head dims with independent loads.
-  __shared__ float wsh[1024];
   float M = -INFINITY;
   for (int s = lane; s < ns; s += 64) M = fmaxf(M, a.part_ml[(row0 + s) * 2]);
   M = wave_max(M);
@@ -424,15 +443,26 @@ __global__ void __launch_bounds__(64) attn_combine_kernel(const AttnDecodeArgs a
     for (; s < ns; s++) acc0 += wsh[s] * po[(size_t)s * a.D + d];
     out[d] = from_f32<T>((acc0 + acc1 + acc2 + acc3) * invL);
   }
+  __syncthreads();
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64) attn_combine_kernel(const AttnDecodeArgs a) {
+  __shared__ float wsh[1024];
+  combine_row<T>(a, blockIdx.z, blockIdx.x, blockIdx.y, wsh);
 }
 
 template <typename T, int D, int RT>
-static void launch_v2(const AttnDecodeArgs& a, hipStream_t st) {
+static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
+  AttnDecodeArgs a = a0;
+  // combine fused into the split kernel when the merge fits its LDS scratch
+  if (a.nsplit > SPLIT * RT) a.counters = nullptr;
   dim3 grid(a.nsplit, a.Hkv, a.B);
   if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT>), grid, dim3(64), 0, st, a);
   else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT>), grid, dim3(64), 0, st, a);
   else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT>), grid, dim3(64), 0, st, a);
-  hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
+  if (a.counters == nullptr)
+    hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
 }
 
 template <typename T, int D>

@@ -57,6 +57,13 @@ struct RopeKVArgs {
   int interleaved;         // 0 = rotate_half (NeoX/llama), 1 = pairwise (GPT-J/GLM)
   int kv_fp8;              // 0 = same dtype as activations, 1 = fp8 e5m2, 2 = fp8 e4m3
   float k_scale, v_scale;  // fp8 KV scales (value = code * scale)
+  // fused split-K reduction of the QKV GEMV: qkv = sum_s part[s] (+ bias)
+  const float* part;       // [nsplit, T, ld_qkv] f32 or null (then qkv is read)
+  int nsplit;
+  const uint16_t* bias;    // [ld_qkv] or null
+  // device-side slots (slots == null): slot = block_tables[t / tq][pos / bs] * bs + pos % bs
+  const int32_t* block_tables;
+  int max_blocks, tq;
 };
 void launch_rope_kv(bool bf16, const RopeKVArgs& a, hipStream_t st);
 
@@ -68,6 +75,7 @@ struct AttnDecodeArgs {
   const int32_t* block_tables;  // [B, max_blocks]
   const int32_t* seq_lens;      // [B] total keys incl. the Tq new ones
   int max_blocks;
+  int* counters;                // [B * Hkv] zeroed arrival counters (fused combine) or null
   float* part_o;            // [B, Hq, Tq, nsplit, D]
   float* part_ml;           // [B, Hq, Tq, nsplit, 2]
   uint16_t* out;            // [B, Tq, Hq, D]
@@ -98,6 +106,10 @@ void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float
 
 void launch_embedding_rows(bool bf16, const uint8_t* blob, int fmt, const int64_t* ids, int T, int64_t n, int64_t k,
                            uint16_t* out, hipStream_t st);
+
+void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int64_t* ids, int64_t* next_ids,
+                           int64_t* pos, const int32_t* block_tables, int max_blocks, int bs, int64_t* slots,
+                           int32_t* seq_lens, hipStream_t st);
 
 // ---- one-shot xGMI peer all-reduce (allreduce.hip) ------------------------
 constexpr int AR_MAX_RANKS = 8;

@@ -359,4 +359,66 @@ void launch_embedding_rows(bool bf16, const uint8_t* blob, int fmt, const int64_
   else hipLaunchKernelGGL(embedding_rows_kernel<F16>, grid, dim3(256), 0, st, blob, fmt, ids, n, k, out);
 }
 
+// ---- decode-step glue: greedy argmax + position / slot advance -------------------
+// One workgroup per sequence: argmax over the vocabulary (if logits given),
+// feeds the token back as the next input, advances the position and
+// precomputes the next step's KV slot and key count -- replacing ~8 small
+// framework kernels per graph-captured decode step.
+template <typename T>
+__global__ void __launch_bounds__(1024) decode_advance_kernel(const uint16_t* logits, int V, int64_t* ids,
+                                                              int64_t* next_ids, int64_t* pos,
+                                                              const int32_t* block_tables, int max_blocks, int bs,
+                                                              int64_t* slots, int32_t* seq_lens) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (logits) {
+    const uint16_t* row = logits + (size_t)b * V;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = tid; i < V; i += 1024) {
+      const float v = to_f32<T>(row[i]);
+      if (v > best) { best = v; bi = i; }       // strided scan: first max per thread
+    }
+    __shared__ float sv[16];
+    __shared__ int si[16];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bi; }
+    __syncthreads();
+    if (tid < 64) {
+      best = tid < 16 ? sv[tid] : -INFINITY;
+      bi = tid < 16 ? si[tid] : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+      }
+      if (tid == 0) {
+        if (bi == 0x7fffffff) bi = 0;            // all -inf / NaN row
+        ids[b] = bi;
+        next_ids[b] = bi;
+      }
+    }
+  }
+  if (tid == 0) {
+    const int64_t p = pos[b] + 1;
+    pos[b] = p;
+    if (slots) slots[b] = (int64_t)block_tables[(size_t)b * max_blocks + p / bs] * bs + p % bs;
+    if (seq_lens) seq_lens[b] = (int32_t)(p + 1);
+  }
+}
+
+void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int64_t* ids, int64_t* next_ids,
+                           int64_t* pos, const int32_t* block_tables, int max_blocks, int bs, int64_t* slots,
+                           int32_t* seq_lens, hipStream_t st) {
+  if (bf16) hipLaunchKernelGGL(decode_advance_kernel<BF16>, dim3(B), dim3(1024), 0, st, logits, V, ids, next_ids, pos,
+                               block_tables, max_blocks, bs, slots, seq_lens);
+  else hipLaunchKernelGGL(decode_advance_kernel<F16>, dim3(B), dim3(1024), 0, st, logits, V, ids, next_ids, pos,
+                          block_tables, max_blocks, bs, slots, seq_lens);
+}
+
 }  // namespace illm

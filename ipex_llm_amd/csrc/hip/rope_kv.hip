@@ -32,8 +32,17 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
   const int h = blockIdx.x, t = blockIdx.y, lane = threadIdx.x;
   const int D = a.D, half = a.rot_dim / 2;
   const bool is_q = h < a.Hq, is_k = !is_q && h < a.Hq + a.Hkv;
-  const uint16_t* src = a.qkv + (size_t)t * a.ld_qkv + (size_t)h * D;
+  const size_t col0 = (size_t)h * D;
+  const uint16_t* src = a.part ? nullptr : a.qkv + (size_t)t * a.ld_qkv + col0;
   constexpr bool BF = std::is_same<T, BF16>::value;
+  // projection output element d of this head (split-K partials summed here,
+  // rounded to T like the standalone GEMV output)
+  auto raw = [&](int d) -> float {
+    if (!a.part) return to_f32<T>(src[d]);
+    float s = a.bias ? to_f32<T>(a.bias[col0 + d]) : 0.f;
+    for (int k = 0; k < a.nsplit; k++) s += a.part[((size_t)k * a.T + t) * a.ld_qkv + col0 + d];
+    return to_f32<T>(from_f32<T>(s));
+  };
 
   // per-head RMSNorm (qwen3 q_norm / k_norm): sum of squares over D
   const uint16_t* nw = is_q ? a.q_norm : (is_k ? a.k_norm : nullptr);
@@ -41,14 +50,14 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
   if (nw) {
     float ss = 0.f;
     for (int d = lane; d < D; d += 64) {
-      float v = to_f32<T>(src[d]);
+      float v = raw(d);
       ss += v * v;
     }
     ss = wave_sum(ss);
     inv = rsqrtf(ss / (float)D + a.norm_eps);
   }
   auto val = [&](int d) -> float {
-    float v = to_f32<T>(src[d]);
+    float v = raw(d);
     if (nw) v = to_f32<T>(from_f32<T>(to_f32<T>(nw[d]) * to_f32<T>(from_f32<T>(v * inv))));
     return v;
   };
@@ -58,7 +67,12 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
   uint8_t* cache = nullptr;
   float cscale = 1.f;
   if (!is_q) {
-    slot = a.slots[t];
+    if (a.slots) {
+      slot = a.slots[t];
+    } else {
+      const int64_t pp = a.pos[t];
+      slot = (int64_t)a.block_tables[(size_t)(t / a.tq) * a.max_blocks + pp / a.bs] * a.bs + pp % a.bs;
+    }
     if (slot < 0) return;
     cache = is_k ? a.k_cache : a.v_cache;
     cscale = is_k ? a.k_scale : a.v_scale;
@@ -94,7 +108,7 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
     }
     for (int d = a.rot_dim + lane; d < D; d += 64) put(d, val(d));
   } else {
-    for (int d = lane; d < D; d += 64) put(d, to_f32<T>(src[d]));
+    for (int d = lane; d < D; d += 64) put(d, raw(d));
   }
 }
 

@@ -262,6 +262,65 @@ void rope_kv(const Tensor& qkv, Tensor& q_out, Tensor& k_cache, Tensor& v_cache,
   if (T > 0) illm::launch_rope_kv(bf16, a, cur_stream());
 }
 
+// Zeroed per-device arrival counters for the fused attention combine.  The
+// buffer is allocated once (outside any graph capture: the first eager call
+// of a shape allocates it) and every merging block resets its counter, so the
+// same pointer is valid across hipGraph replays.
+int* attn_counters(const c10::Device& dev, int64_t n) {
+  static std::vector<Tensor> bufs(64);
+  const int idx = dev.index() < 0 ? 0 : dev.index();
+  constexpr int64_t kCap = 1 << 16;
+  if (n > kCap) return nullptr;
+  if (!bufs[idx].defined()) {
+    bufs[idx] = at::zeros({kCap}, at::TensorOptions().device(dev).dtype(at::kInt));
+  }
+  return bufs[idx].data_ptr<int>();
+}
+
+void rope_kv_fused(const Tensor& part, const c10::optional<Tensor>& bias, Tensor& q_out, Tensor& k_cache,
+                   Tensor& v_cache, const Tensor& pos, const Tensor& block_tables, int64_t tq, const Tensor& inv_freq,
+                   const c10::optional<Tensor>& q_norm, const c10::optional<Tensor>& k_norm, double norm_eps,
+                   double q_scale, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot_dim, bool interleaved,
+                   int64_t kv_fp8, double k_scale, double v_scale) {
+  c10::DeviceGuard g(part.device());
+  const bool bf16 = is_bf16(q_out);
+  TORCH_CHECK(part.dim() == 3 && part.scalar_type() == at::kFloat && part.is_contiguous(),
+              "rope_kv_fused: part must be contiguous f32 [ks, T, N]");
+  TORCH_CHECK(part.size(2) == (Hq + 2 * Hkv) * D, "rope_kv_fused: N != (Hq + 2 Hkv) * D");
+  TORCH_CHECK(pos.scalar_type() == at::kLong && block_tables.scalar_type() == at::kInt, "pos int64, block_tables int32");
+  TORCH_CHECK(inv_freq.scalar_type() == at::kFloat, "inv_freq / cos_sin must be f32");
+  illm::RopeKVArgs a{};
+  a.part = part.data_ptr<float>();
+  a.nsplit = (int)part.size(0);
+  a.bias = p16o(bias);
+  a.ld_qkv = (int)part.size(2);
+  a.q_out = m16(q_out);
+  a.k_cache = (uint8_t*)k_cache.data_ptr();
+  a.v_cache = (uint8_t*)v_cache.data_ptr();
+  a.slots = nullptr;
+  a.block_tables = block_tables.data_ptr<int32_t>();
+  a.max_blocks = (int)block_tables.size(1);
+  a.tq = (int)tq;
+  a.pos = pos.data_ptr<int64_t>();
+  if (inv_freq.dim() == 3) a.cos_sin = inv_freq.data_ptr<float>();
+  else a.inv_freq = inv_freq.data_ptr<float>();
+  a.q_norm = p16o(q_norm);
+  a.k_norm = p16o(k_norm);
+  a.norm_eps = (float)norm_eps;
+  a.attn_scale_q = (float)q_scale;
+  a.T = (int)part.size(1);
+  a.Hq = (int)Hq;
+  a.Hkv = (int)Hkv;
+  a.D = (int)D;
+  a.rot_dim = (int)rot_dim;
+  a.bs = (int)k_cache.size(2);
+  a.interleaved = interleaved;
+  a.kv_fp8 = (int)kv_fp8;
+  a.k_scale = (float)k_scale;
+  a.v_scale = (float)v_scale;
+  if (a.T > 0) illm::launch_rope_kv(bf16, a, cur_stream());
+}
+
 Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
                    const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
                    int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& alibi) {
@@ -301,6 +360,7 @@ Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache
   a.k_scale = (float)k_scale;
   a.v_scale = (float)v_scale;
   a.alibi = (alibi.has_value() && alibi->defined()) ? alibi->data_ptr<float>() : nullptr;
+  a.counters = attn_counters(q.device(), B * Hkv);
   illm::launch_attn_decode(bf16, a, cur_stream());
   return out;
 }
@@ -444,9 +504,32 @@ Tensor embedding_lowbit(const Tensor& blob, int64_t fmt, int64_t n, int64_t k, c
   return out;
 }
 
+// logits: [B, V] bf16/f16 or undefined (sampling done by the host: only advance)
+void decode_advance(const c10::optional<Tensor>& logits, Tensor& ids, Tensor& next_ids, Tensor& pos,
+                    const Tensor& block_tables, int64_t bs, Tensor& slots, Tensor& seq_lens) {
+  c10::DeviceGuard g(pos.device());
+  const int64_t B = pos.numel();
+  TORCH_CHECK(pos.scalar_type() == at::kLong && ids.scalar_type() == at::kLong && slots.scalar_type() == at::kLong &&
+              seq_lens.scalar_type() == at::kInt && block_tables.scalar_type() == at::kInt, "decode_advance dtypes");
+  const bool has = logits.has_value() && logits->defined();
+  bool bf16 = true;
+  int V = 0;
+  if (has) {
+    bf16 = is_bf16(*logits);
+    TORCH_CHECK(logits->is_contiguous() && logits->size(0) == B, "decode_advance: logits [B, V]");
+    V = (int)logits->size(-1);
+  }
+  illm::launch_decode_advance(bf16, has ? p16(*logits) : nullptr, (int)B, V, ids.data_ptr<int64_t>(),
+                              next_ids.data_ptr<int64_t>(), pos.data_ptr<int64_t>(), block_tables.data_ptr<int32_t>(),
+                              (int)block_tables.size(1), (int)bs, slots.data_ptr<int64_t>(),
+                              seq_lens.data_ptr<int32_t>(), cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
+  m.impl("decode_advance", &decode_advance);
+  m.impl("rope_kv_fused", &rope_kv_fused);
   m.impl("embedding_lowbit", &embedding_lowbit);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemv", &moe_gemv);

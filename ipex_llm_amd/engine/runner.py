@@ -28,36 +28,61 @@ def nsplit_for(max_len: int) -> int:
 
 
 class DecodeStep:
-    """Static-buffer decode step (B sequences, 1 new token each)."""
+    """Static-buffer decode step (B sequences, 1 new token each).
+
+    On the GPU the step is: native forward (qkv GEMV -> fused RoPE/KV over
+    its split-K partials with device-side slots -> fused flash-decoding ->
+    ...) -> lm_head GEMV -> ``decode_advance`` (greedy argmax, feed back the
+    token, advance positions and precompute the next step's slots / key
+    counts).  No framework glue kernels remain inside the captured graph."""
 
     def __init__(self, model: NativeCausalLM, cache: PagedKVCache, block_tables: torch.Tensor,
                  max_len: int, greedy: bool = True, use_graph: bool = True):
+        from .. import ops
         self.model, self.cache = model, cache
         dev = model.device
         self.B = block_tables.shape[0]
         self.block_tables = block_tables.to(dev, torch.int32).contiguous()
         self.ids = torch.zeros(self.B, dtype=torch.long, device=dev)
         self.pos = torch.zeros(self.B, dtype=torch.long, device=dev)
+        self.slots = torch.zeros(self.B, dtype=torch.long, device=dev)
+        self.seq_lens = torch.ones(self.B, dtype=torch.int32, device=dev)
         self.nsplit = nsplit_for(max_len)
         self.greedy = greedy
         self.logits: Optional[torch.Tensor] = None
         self.next_ids = torch.zeros(self.B, dtype=torch.long, device=dev)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.use_graph = use_graph and dev.type == "cuda"
+        self.native_glue = dev.type == "cuda" and ops.native_gpu(self.ids)
 
-    def _body(self):
+    def _refresh(self):
+        """slots / key counts for the current positions (eager, outside the graph)"""
         bs = self.cache.bs
         blk = torch.gather(self.block_tables, 1, (self.pos // bs).unsqueeze(1)).squeeze(1).long()
-        slots = blk * bs + self.pos % bs
-        seq_lens = (self.pos + 1).to(torch.int32)
-        meta = AttnMeta(self.B, 1, self.block_tables, seq_lens, self.nsplit)
-        logits = self.model.forward_tokens(self.ids, self.pos, slots, meta, self.cache)
+        self.slots.copy_(blk * bs + self.pos % bs)
+        self.seq_lens.copy_((self.pos + 1).to(torch.int32))
+
+    def _body(self):
+        meta = AttnMeta(self.B, 1, self.block_tables, self.seq_lens, self.nsplit)
+        m = self.model
+        if self.native_glue:
+            h = m.forward_tokens(self.ids, self.pos, self.slots, meta, self.cache, return_hidden=True)
+            logits = m.lm_head(h.contiguous())
+            if m.spec.final_softcap:
+                logits = (torch.tanh(logits.float() / m.spec.final_softcap) * m.spec.final_softcap).to(h.dtype)
+            self.logits = logits
+            torch.ops.ipex_llm_amd.decode_advance(logits if self.greedy else None, self.ids, self.next_ids,
+                                                  self.pos, self.block_tables, self.cache.bs, self.slots,
+                                                  self.seq_lens)
+            return
+        logits = m.forward_tokens(self.ids, self.pos, self.slots, meta, self.cache)
         self.logits = logits
         if self.greedy:
             nxt = torch.argmax(logits, dim=-1)
             self.next_ids.copy_(nxt)
             self.ids.copy_(nxt)
         self.pos.add_(1)
+        self._refresh()
 
     def capture(self):
         if not self.use_graph:
@@ -66,24 +91,29 @@ class DecodeStep:
         # The warm-up really executes (writes K/V): point it at the last slot
         # of each sequence's allocation, which generation never reaches.
         ids0, pos0 = self.ids.clone(), self.pos.clone()
-        self.pos.fill_(self.block_tables.shape[1] * self.cache.bs - 1)
+        last = self.block_tables.shape[1] * self.cache.bs - 2
+        self.pos.fill_(last)
+        self._refresh()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             self._body()
         torch.cuda.current_stream().wait_stream(s)
         self.ids.copy_(ids0)
-        self.pos.fill_(self.block_tables.shape[1] * self.cache.bs - 1)
+        self.pos.fill_(last)
+        self._refresh()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._body()
-        # capture does not execute; restore state written by warm-up
+        # capture does not execute; restore the state written by the warm-up
         self.ids.copy_(ids0)
         self.pos.copy_(pos0)
+        self._refresh()
 
     def set_state(self, ids: torch.Tensor, pos: torch.Tensor):
         self.ids.copy_(ids)
         self.pos.copy_(pos)
+        self._refresh()
 
     def step(self):
         if self.graph is not None:

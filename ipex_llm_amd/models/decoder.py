@@ -313,11 +313,21 @@ class NativeCausalLM(nn.Module):
         rope = self.rope_cache if self.rope_cache is not None else self.inv_freq
         for li, layer in enumerate(self.layers):
             attn = layer.self_attn
-            qkv = attn.qkv_proj(x)
-            q = torch.empty(T, s.num_heads, s.head_dim, dtype=qkv.dtype, device=qkv.device)
-            ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,
-                        s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved, attn.q_norm, attn.k_norm,
-                        s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale, cache.v_scale)
+            qp = attn.qkv_proj
+            q = torch.empty(T, s.num_heads, s.head_dim, dtype=x.dtype, device=x.device)
+            if x.is_cuda and isinstance(qp, LowBitLinear) and qp.mp_group is None and T <= ops.GEMV_MAX_M \
+                    and (qp.bias is None or qp.bias.dtype == x.dtype) and ops.native_gpu(x):
+                # split-K partials reduced (+bias) inside the RoPE/KV kernel, slots from the block table
+                part = ops.gemv_partials(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, 0)
+                ops.rope_kv_fused(part, qp.bias, q, cache.k[li], cache.v[li], pos, meta.block_tables, meta.Tq, rope,
+                                  s.num_heads, s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved,
+                                  attn.q_norm, attn.k_norm, s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale,
+                                  cache.v_scale)
+            else:
+                qkv = qp(x)
+                ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,
+                            s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved, attn.q_norm, attn.k_norm,
+                            s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale, cache.v_scale)
             a = self._attention(li, attn, q, meta, cache)
             if s.sandwich_norm:
                 x = self._proj_residual_norm(a, attn.o_proj, residual, layer.pre_feedforward_layernorm,

@@ -87,3 +87,9 @@ def _(x, blob, fmt, n, k, off, rows, xdiv, npairs, epi, ksplit, act):
 @register_fake("ipex_llm_amd::moe_combine")
 def _(part, w, ids, e0, num_local, dtype):
     return part.new_empty((w.numel() // w.shape[-1], part.shape[-1]), dtype=dtype)
+
+
+@register_fake("ipex_llm_amd::rope_kv_fused")
+def _(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm, norm_eps, q_scale, Hq,
+      Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale):
+    return None

@@ -17,7 +17,7 @@ __all__ = [
     "quantize", "dequantize", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
-    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine",
+    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused",
 ]
 
 
@@ -212,6 +212,27 @@ def rope_kv(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, Hq, Hkv, D, rot_
         k_cache[blk, :, off] = k[ok].to(k_cache.dtype)
         v_cache[blk, :, off] = v[ok].to(v_cache.dtype)
     return q_out
+
+
+def rope_kv_fused(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, Hq, Hkv, D, rot_dim=None,
+                  interleaved=False, q_norm=None, k_norm=None, norm_eps=1e-6, q_scale=1.0, kv_fp8=0,
+                  k_scale=1.0, v_scale=1.0):
+    """rope_kv over the split-K partials of the QKV GEMV ([ks, T, N] f32,
+    summed + bias in the kernel) with device-side slots from the block table."""
+    rot_dim = rot_dim or D
+    if _native(part):
+        _ops().rope_kv_fused(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm,
+                             norm_eps, q_scale, Hq, Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale)
+        return q_out
+    qkv = part.sum(0)
+    if bias is not None:
+        qkv = qkv + bias.float()
+    qkv = qkv.to(q_out.dtype)
+    bs = k_cache.shape[2]
+    seq = torch.arange(pos.numel(), device=pos.device) // tq
+    slots = block_tables.long()[seq, pos // bs] * bs + pos % bs
+    return rope_kv(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, Hq, Hkv, D, rot_dim, interleaved, q_norm,
+                   k_norm, norm_eps, q_scale, kv_fp8, k_scale, v_scale)
 
 
 def gather_kv(cache, block_tables, b, L, kv_fp8=0, scale=1.0, dtype=torch.bfloat16):

@@ -29,7 +29,19 @@ def summarize(path, top=30, after=None):
         d[1] += (e - s) / 1e3
     tot = sum(v[1] for v in agg.values())
     span = (rows[-1][2] - rows[0][1]) / 1e3 if rows else 0.0
-    out = [f"kernel time {tot / 1e3:.2f} ms over {sum(v[0] for v in agg.values())} dispatches; wall span {span / 1e3:.2f} ms"]
+    # busy = union of kernel intervals; the rest of the span is launch gaps
+    busy, cur_s, cur_e = 0.0, None, None
+    for _, s, e in rows:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += (cur_e - cur_s) / 1e3
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        busy += (cur_e - cur_s) / 1e3
+    out = [f"kernel time {tot / 1e3:.2f} ms over {sum(v[0] for v in agg.values())} dispatches; wall span {span / 1e3:.2f} ms; "
+           f"GPU busy {busy / 1e3:.2f} ms; idle gaps {(span - busy) / 1e3:.2f} ms"]
     out.append(f"{'calls':>7} {'total_us':>11} {'avg_us':>9} {'pct':>6}  kernel")
     for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
         out.append(f"{c:7d} {t:11.1f} {t / c:9.2f} {100 * t / max(tot, 1e-9):6.2f}  {n[:110]}")
