@@ -57,6 +57,7 @@ struct GemvArgs {
   const int32_t* moe_rows; // [P] pair ids sorted by expert
   int moe_xdiv;            // x row of pair p = p / moe_xdiv
   int64_t w_stride;        // bytes between experts' weight blobs
+  int waves;               // v4: waves per workgroup (4 or 8; 0 = 4)
 };
 
 }  // namespace illm

@@ -403,8 +403,9 @@ __device__ __forceinline__ uint4 scaled_a8(uint32_t lo, uint32_t hi, h2 d2, h2 m
 // MOE = grouped GEMV over experts (FlashMoE decode): blockIdx.z = expert e,
 // its token-expert pairs are moe_rows[moe_off[e] .. moe_off[e+1]) (<= 16),
 // weights at a.w + e * w_stride, x row = pair / moe_xdiv, output row = pair.
-template <int DK, typename T, int EPI, int TPW, int PF = 4, bool MOE = false>
-__global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
+// ABL (profiling ablations only): 1 = no scale loads, 2 = no x staging, 3 = no dequant/MFMA math
+template <int DK, typename T, int EPI, int TPW, int PF = 4, bool MOE = false, int ABL = 0>
+__global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
   constexpr int BITS = dk_bits(DK);
   extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
   __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
@@ -432,7 +433,7 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
   const int kw = (c1 - c0) * 128;
   const int lds_ld = kw + 8;
   const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
-  const int tile0 = (blockIdx.x * 4 + wave) * TPW;
+  const int tile0 = (blockIdx.x * (int)(blockDim.x >> 6) + wave) * TPW;
   const bool wave_on = tile0 < NT && c0 < c1;
 
   struct Chunk {
@@ -449,7 +450,8 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
       ch.q[t][0] = *(const uint4*)(rec + lane * 16);
       if constexpr (BITS == 8) ch.q[t][1] = *(const uint4*)(rec + 1024 + lane * 16);
       // this lane's A-row (r16) scales of both blocks: one dword
-      ch.sc[t] = *(const uint32_t*)(rec + dk_code_chunk(DK) + r16 * 4);
+      if constexpr (ABL == 1) ch.sc[t] = 0x3c003c00u;
+      else ch.sc[t] = *(const uint32_t*)(rec + dk_code_chunk(DK) + r16 * 4);
       if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint32_t*)(rec + dk_code_chunk(DK) + 64 + r16 * 4);
     }
   };
@@ -459,11 +461,12 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
     for (int u = 0; u < PF; u++) load_chunk(ring[u], c0 + u);
   }
   if constexpr (DK == DK_LUT4) {
-    lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
+    if (threadIdx.x < 256)
+      lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
   }
-  {  // stage x[0:M, kbase:kbase+kw] -> LDS as f16
+  if (ABL != 2) {  // stage x[0:M, kbase:kbase+kw] -> LDS as f16
     const int vpr = kw / 8;
-    for (int v = threadIdx.x; v < Mloc * vpr; v += 256) {
+    for (int v = threadIdx.x; v < Mloc * vpr; v += blockDim.x) {
       const int m = v / vpr, kk = (v % vpr) * 8;
       uint4 val = make_uint4(0, 0, 0, 0);
       if (kbase + kk < a.K) {
@@ -522,7 +525,8 @@ __global__ void __launch_bounds__(256) lowbit_gemv4_kernel(const GemvArgs a) {
             const uint4& qq = ch.q[t][blk];
             A = ss == 0 ? scaled_a8<DK>(qq.x, qq.y, d2, m2) : scaled_a8<DK>(qq.z, qq.w, d2, m2);
           }
-          acc[t] = mfma16<F16>(A, B[s], acc[t]);
+          if constexpr (ABL == 3) acc[t][0] += __uint_as_float((ch.q[t][0].x ^ B[s].x ^ ch.sc[t]) & 0x3fffffffu);
+          else acc[t] = mfma16<F16>(A, B[s], acc[t]);
         }
       }
     }
@@ -596,7 +600,7 @@ void launch_gemv4_moe(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArg
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);            \
       attr = true;                                                                                  \
     }                                                                                               \
-    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, TT, E, TP, 4, true>), grid, dim3(256), shmem, st, a); \
+    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, TT, E, TP, 4, true>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a); \
   } while (0)
   if (bf16) {
     if (epi == EPI_PARTIAL) L4M(BF16, EPI_PARTIAL, 1);
@@ -618,10 +622,38 @@ void launch_gemv4_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);            \
       attr = true;                                                                                  \
     }                                                                                               \
-    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, TT, E, TP>), grid, dim3(256), shmem, st, a);       \
+    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, TT, E, TP>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);       \
   } while (0)
   if (a.moe_off != nullptr) {
     launch_gemv4_moe<DK>(bf16, epi, grid, shmem, a, st);
+    return;
+  }
+  // prefetch-depth experiments (bf16 only): ILLM_GEMV_PF=8|16
+  static const int pf_env = getenv("ILLM_GEMV_PF") ? atoi(getenv("ILLM_GEMV_PF")) : 4;
+  static const int abl_env = getenv("ILLM_GEMV_ABL") ? atoi(getenv("ILLM_GEMV_ABL")) : 0;
+  if (bf16 && abl_env && epi == EPI_PARTIAL) {
+    if (abl_env == 1) hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, BF16, EPI_PARTIAL, 1, 4, false, 1>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);
+    else if (abl_env == 2) hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, BF16, EPI_PARTIAL, 1, 4, false, 2>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);
+    else hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, BF16, EPI_PARTIAL, 1, 4, false, 3>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);
+    return;
+  }
+  if (bf16 && pf_env != 4) {
+#define L4P(E, TP, PFV)                                                                              \
+  do {                                                                                              \
+    static bool attr = false;                                                                       \
+    if (!attr) {                                                                                    \
+      (void)hipFuncSetAttribute((const void*)lowbit_gemv4_kernel<DK, BF16, E, TP, PFV>,             \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);            \
+      attr = true;                                                                                  \
+    }                                                                                               \
+    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, BF16, E, TP, PFV>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a); \
+  } while (0)
+    if (pf_env == 8) {
+      if (epi == EPI_GLU) L4P(EPI_GLU, 2, 8); else if (epi == EPI_PARTIAL) L4P(EPI_PARTIAL, 1, 8); else L4P(EPI_STORE, 1, 8);
+    } else {
+      if (epi == EPI_GLU) L4P(EPI_GLU, 2, 16); else if (epi == EPI_PARTIAL) L4P(EPI_PARTIAL, 1, 16); else L4P(EPI_STORE, 1, 16);
+    }
+#undef L4P
     return;
   }
   if (bf16) {

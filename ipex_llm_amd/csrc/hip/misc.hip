@@ -374,9 +374,30 @@ __global__ void __launch_bounds__(1024) decode_advance_kernel(const uint16_t* lo
     const uint16_t* row = logits + (size_t)b * V;
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = tid; i < V; i += 1024) {
-      const float v = to_f32<T>(row[i]);
-      if (v > best) { best = v; bi = i; }       // strided scan: first max per thread
+    // 16-B vector loads, 8 in flight per thread before any compare
+    const int nvec = ((V & 7) == 0 && (((uintptr_t)row) & 15) == 0) ? V / 8 : 0;
+    for (int v0 = tid; v0 < nvec; v0 += 1024 * 8) {
+      uint4 q[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int vi = min(v0 + u * 1024, nvec - 1);
+        q[u] = ((const uint4*)row)[vi];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int vi = v0 + u * 1024;
+        if (vi >= nvec) break;
+        const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const float x = to_f32<T>((uint16_t)(e & 1 ? w[e >> 1] >> 16 : w[e >> 1] & 0xffff));
+          if (x > best) { best = x; bi = vi * 8 + e; }
+        }
+      }
+    }
+    for (int i = nvec * 8 + tid; i < V; i += 1024) {   // tail / unaligned rows
+      const float x = to_f32<T>(row[i]);
+      if (x > best) { best = x; bi = i; }
     }
     __shared__ float sv[16];
     __shared__ int si[16];

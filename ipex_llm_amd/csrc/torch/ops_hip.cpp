@@ -86,8 +86,8 @@ int64_t auto_ksplit(int64_t NT, int64_t KC) {
 // v4 geometry: workgroups = 4 waves x TPW tiles; split K so that there are
 // >= ~320 workgroups while each wave keeps >= 4 chunks, and the LDS x slice
 // (M * Kwg * 2 B) stays <= 64 KiB (occupancy: >= 2 workgroups per CU).
-int64_t v4_ksplit(int64_t M, int64_t NT, int64_t KC, int tpw) {
-  const int64_t wgs = (NT + 4 * tpw - 1) / (4 * tpw);
+int64_t v4_ksplit(int64_t M, int64_t NT, int64_t KC, int tpw, int waves = 4) {
+  const int64_t wgs = (NT + waves * tpw - 1) / (waves * tpw) * waves / 4;   // in 4-wave units
   int64_t ks = 1;
   auto lds = [&](int64_t k) { return M * (((KC + k - 1) / k) * 128 + 8) * 2; };
   while ((wgs * ks < 320 && KC / (ks * 2) >= 4) || (lds(ks) > 65536 && ks < KC)) ks *= 2;
@@ -120,6 +120,11 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   a.act = (int)act;
   a.lut_fmt = (int)fmt;
   a.bias = nullptr;
+  // v4 workgroup size: 8 waves share one LDS copy of x (halves x traffic per tile)
+  static const int waves_env = getenv("ILLM_GEMV_WAVES") ? atoi(getenv("ILLM_GEMV_WAVES")) : 0;
+  // GLU keeps 4-wave groups: it cannot split K, and 8-wave groups halve its grid
+  const int W = waves_env ? waves_env : ((M > 2 && epi != illm::EPI_GLU) ? 8 : 4);
+  a.waves = W;
 
   auto out_shape = xc.sizes().vec();
   if (epi == illm::EPI_GLU) {
@@ -131,19 +136,19 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
     a.ldo = (int)(n / 2);
     const size_t shmem = (size_t)M * (KC * 128 + 8) * 2;
     if (small && shmem <= kMaxLds)
-      launch_gemv4_any((int)fmt, bf16, illm::EPI_GLU, dim3((unsigned)((NT + 7) / 8), 1), shmem, a);
+      launch_gemv4_any((int)fmt, bf16, illm::EPI_GLU, dim3((unsigned)((NT + 2 * W - 1) / (2 * W)), 1), shmem, a);
     else
       launch_gemv_any((int)fmt, bf16, mt, illm::EPI_GLU, dim3((unsigned)(NT / 2), 1), a);
     return out;
   }
   a.N = (int)n;
-  if (ksplit <= 0) ksplit = small ? v4_ksplit(M, NT, KC, 1) : auto_ksplit(NT, KC);
+  if (ksplit <= 0) ksplit = small ? v4_ksplit(M, NT, KC, 1, W) : auto_ksplit(NT, KC);
   ksplit = std::min<int64_t>(ksplit, KC);
   const int64_t cpk = (KC + ksplit - 1) / ksplit;
   const size_t shmem = (size_t)M * (cpk * 128 + 8) * 2;
   const bool use4 = small && shmem <= kMaxLds;
   auto launch = [&](int e) {
-    if (use4) launch_gemv4_any((int)fmt, bf16, e, dim3((unsigned)((NT + 3) / 4), (unsigned)ksplit), shmem, a);
+    if (use4) launch_gemv4_any((int)fmt, bf16, e, dim3((unsigned)((NT + W - 1) / W), (unsigned)ksplit), shmem, a);
     else launch_gemv_any((int)fmt, bf16, mt, e, dim3((unsigned)NT, (unsigned)ksplit), a);
   };
   if (epi == illm::EPI_PARTIAL || ksplit > 1) {
@@ -360,7 +365,10 @@ Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache
   a.k_scale = (float)k_scale;
   a.v_scale = (float)v_scale;
   a.alibi = (alibi.has_value() && alibi->defined()) ? alibi->data_ptr<float>() : nullptr;
-  a.counters = attn_counters(q.device(), B * Hkv);
+  // the in-kernel merge (last split block combines) is serial per head
+  // group and measured slower than the separate combine launch; opt-in only
+  static const bool fused_combine = getenv("ILLM_ATTN_FUSED_COMBINE") != nullptr;
+  a.counters = fused_combine ? attn_counters(q.device(), B * Hkv) : nullptr;
   illm::launch_attn_decode(bf16, a, cur_stream());
   return out;
 }

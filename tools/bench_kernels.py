@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--m", default="1,8")
     ap.add_argument("--qtype", default="sym_int4")
     ap.add_argument("--only", default="")
+    ap.add_argument("--ks", default="0,1,2,4,8")
     args = ap.parse_args()
     dev = torch.device("cuda")
     ops.require()
@@ -79,7 +80,7 @@ def main():
                 return ops.gemv_glu(x, blobs[i[0]], f, n, k, 0)
 
             cands = {"store_auto": run_store}
-            for ks in ((0,) if args.only else (0, 1, 2, 4, 8)):
+            for ks in ((0,) if args.only == "gemv" else [int(v) for v in args.ks.split(",")]):
                 cands[f"partial_ks{ks}"] = run_part(ks)
             if name == "gate_up":
                 cands["glu"] = run_glu
@@ -92,6 +93,11 @@ def main():
             torch.cuda.empty_cache()
     if args.only == "gemv":
         return
+    # per-kernel floor: back-to-back trivial launches inside one graph
+    t1 = torch.zeros(1, device=dev)
+    us = timeit(lambda: t1.add_(1.0), iters=200)
+    res.append({"op": "empty_kernel_floor", "us": round(us, 2)})
+    print(json.dumps(res[-1]), flush=True)
     # attention decode
     for B in (1, 8):
         for L in (1024, 4096):
