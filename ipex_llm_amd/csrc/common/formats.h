@@ -10,20 +10,22 @@
 //
 // Device ("tiled") blob, MI355X gfx950 MFMA fragment order.  N is padded to
 // a multiple of 16 rows, K to a multiple of 128.  Tile t = n/16, chunk
-// c = k/128, KC = Kp/128.  Records R(t,c) of dev_chunk_bytes(f) bytes are
-// stored in (t, c) order; one wave64 streams one record with one
-// global_load_dwordx4 per lane per KiB of codes:
+// c = k/128, KC = Kp/128.  Every tile owns one contiguous region of
+// dev_tile_bytes(f, KC) bytes (tiles in order, +16 B tail pad):
+//   [codes of chunks 0..KC-1][scales [16 rows][KC][2 blocks] fp16][mins, asym]
+// One wave64 streams one chunk with one global_load_dwordx4 per lane per
+// KiB of codes:
 //   lane l: A-operand row r = l & 15, k-group g = l >> 4
-//   4-bit: 16 B at R + l*16; dword s (0..3) = k-step s, holds
+//   4-bit: 16 B at T + c*1024 + l*16; dword s (0..3) = k-step s, holds
 //          the 8 codes k = 128c + 32s + 8g + j; nibble position p holds
 //          element j = dev_nib_pos (so (u >> 4q) & 0x000F000F yields the
 //          packed pair (2q, 2q+1) of the A fragment).
-//   8-bit: 32 B per lane, two 16-B halves h at R + (h*64 + l)*16; half h
-//          holds k-steps 2h, 2h+1, each as 8 bytes in element order.
-//   scales: 32 fp16 at R + dev_code_chunk(f), index dev_scale_idx(r, blk) =
-//          [row][blk]: one dword per row holds both blocks, so an A-fragment
-//          lane (row r) loads 4 B and a C-fragment lane group (rows 4g..4g+3) 16 B.
-//   mins  : 32 fp16 right after the scales (asym formats only).
+//   8-bit: 32 B per lane, two 16-B halves h at T + c*2048 + (h*64 + l)*16;
+//          half h holds k-steps 2h, 2h+1, each as 8 bytes in element order.
+//   scales: one dword (blk0 | blk1 << 16) per (row, chunk) at
+//          dev_scale_off(f, KC, r, c): a row's scales of 4 consecutive
+//          chunks are one 16-B load, so the decode GEMV issues one scale
+//          load per 4 code loads; mins follow the same layout (asym only).
 #pragma once
 #include <stdint.h>
 
@@ -86,20 +88,24 @@ static const float kFP4[16] = {0.0f, 0.5f, 1.0f, 1.5f, 2.0f, 3.0f, 4.0f, 6.0f,
 constexpr int64_t canon_code_bytes(int f, int64_t n, int64_t k) { return n * k * fmt_bits(f) / 8; }
 constexpr int64_t canon_scale_elems(int64_t n, int64_t k) { return n * (k / QBLOCK); }
 constexpr int64_t pad_to(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
-// Device record of one (tile, chunk): the codes (1 KiB 4-bit / 2 KiB 8-bit),
-// then its 32 fp16 scales (64 B) and, for asym formats, 32 fp16 mins (64 B).
-// Keeping a chunk's scales next to its codes makes the weight stream one
-// contiguous sequence per wave (no second stream over a separate scale plane).
+// Device tile region (see the layout comment above).
 constexpr int64_t dev_code_chunk(int f) { return fmt_bits(f) == 4 ? 1024 : 2048; }
-constexpr int64_t dev_chunk_bytes(int f) { return dev_code_chunk(f) + 64 * (fmt_has_min(f) ? 2 : 1); }
-constexpr int64_t dev_rec_total(int f, int64_t n, int64_t k) {
-  return pad_to(n, TILE_N) / TILE_N * (pad_to(k, CHUNK_K) / CHUNK_K) * dev_chunk_bytes(f);
+constexpr int64_t dev_tile_bytes(int f, int64_t KC) {
+  return KC * dev_code_chunk(f) + TILE_N * KC * 4 * (fmt_has_min(f) ? 2 : 1);
 }
-// fp16 index (within the record's scale block) of (row-in-tile r, block-in-chunk blk)
-constexpr int dev_scale_idx(int r, int blk) { return r * 2 + blk; }
+// byte offset (within a tile region) of the scale dword of (row r, chunk c)
+constexpr int64_t dev_scale_off(int f, int64_t KC, int r, int64_t c) {
+  return KC * dev_code_chunk(f) + ((int64_t)r * KC + c) * 4;
+}
+// byte offset of the min dword of (row r, chunk c) (asym formats)
+constexpr int64_t dev_min_off(int f, int64_t KC, int r, int64_t c) {
+  return dev_scale_off(f, KC, r, c) + (int64_t)TILE_N * KC * 4;
+}
 constexpr int64_t canon_total_bytes(int f, int64_t n, int64_t k) {
   return canon_code_bytes(f, n, k) + canon_scale_elems(n, k) * 2 * (fmt_has_min(f) ? 2 : 1);
 }
-constexpr int64_t dev_total_bytes(int f, int64_t n, int64_t k) { return dev_rec_total(f, n, k); }
+constexpr int64_t dev_total_bytes(int f, int64_t n, int64_t k) {
+  return pad_to(n, TILE_N) / TILE_N * dev_tile_bytes(f, pad_to(k, CHUNK_K) / CHUNK_K) + 16;
+}
 
 }  // namespace illm

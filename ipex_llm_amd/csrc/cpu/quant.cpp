@@ -86,11 +86,12 @@ void illm_repack_to_device(int fmt, const uint8_t* codes, const uint16_t* scales
   const int64_t Np = pad_to(n, TILE_N), Kp = pad_to(k, CHUNK_K);
   const int64_t KC = Kp / CHUNK_K, NT = Np / TILE_N;
   const int64_t nb = k / QBLOCK;
-  const int64_t CB = dev_chunk_bytes(fmt);
+  const int64_t TB = dev_tile_bytes(fmt, KC);
 #pragma omp parallel for collapse(2) schedule(static)
   for (int64_t t = 0; t < NT; t++) {
     for (int64_t c = 0; c < KC; c++) {
-      uint8_t* rec = dev + (t * KC + c) * CB;
+      uint8_t* tile = dev + t * TB;
+      uint8_t* rec = tile + c * dev_code_chunk(fmt);
       for (int l = 0; l < 64; l++) {
         int r = l & 15, g = l >> 4;
         int64_t row = t * TILE_N + r;
@@ -118,16 +119,14 @@ void illm_repack_to_device(int fmt, const uint8_t* codes, const uint16_t* scales
           }
         }
       }
-      uint16_t* dscale = (uint16_t*)(rec + dev_code_chunk(fmt));
-      uint16_t* dmin = dscale + 32;
       for (int r = 0; r < TILE_N; r++)
         for (int blk = 0; blk < 2; blk++) {
           int64_t row = t * TILE_N + r;
           int64_t b = c * 2 + blk;
-          int o = dev_scale_idx(r, blk);
           bool in = row < n && b < nb;
-          dscale[o] = in ? scales[row * nb + b] : 0;
-          if (fmt_has_min(fmt)) dmin[o] = (in && mins) ? mins[row * nb + b] : 0;
+          ((uint16_t*)(tile + dev_scale_off(fmt, KC, r, c)))[blk] = in ? scales[row * nb + b] : 0;
+          if (fmt_has_min(fmt))
+            ((uint16_t*)(tile + dev_min_off(fmt, KC, r, c)))[blk] = (in && mins) ? mins[row * nb + b] : 0;
         }
     }
   }
@@ -139,7 +138,7 @@ void illm_repack_from_device(int fmt, const uint8_t* dev, int64_t n, int64_t k, 
   const int bits = fmt_bits(fmt);
   const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
   const int64_t nb = k / QBLOCK;
-  const int64_t CB = dev_chunk_bytes(fmt);
+  const int64_t TB = dev_tile_bytes(fmt, KC);
 #pragma omp parallel for schedule(static)
   for (int64_t row = 0; row < n; row++) {
     int64_t t = row / TILE_N;
@@ -147,7 +146,7 @@ void illm_repack_from_device(int fmt, const uint8_t* dev, int64_t n, int64_t k, 
     uint8_t* crow = codes + row * k * bits / 8;
     for (int64_t kk = 0; kk < k; kk++) {
       int64_t c = kk / CHUNK_K;
-      const uint8_t* rec = dev + (t * KC + c) * CB;
+      const uint8_t* rec = dev + t * TB + c * dev_code_chunk(fmt);
       int kin = (int)(kk % CHUNK_K);
       int s = kin / 32, g = (kin % 32) / 8, j = kin % 8;
       int l = g * 16 + r;
@@ -165,10 +164,9 @@ void illm_repack_from_device(int fmt, const uint8_t* dev, int64_t n, int64_t k, 
     }
     for (int64_t b = 0; b < nb; b++) {
       int64_t c = b / 2;
-      const uint16_t* dscale = (const uint16_t*)(dev + (t * KC + c) * CB + dev_code_chunk(fmt));
-      int o = dev_scale_idx(r, (int)(b % 2));
-      scales[row * nb + b] = dscale[o];
-      if (mins && fmt_has_min(fmt)) mins[row * nb + b] = dscale[32 + o];
+      const uint8_t* tile = dev + t * TB;
+      scales[row * nb + b] = ((const uint16_t*)(tile + dev_scale_off(fmt, KC, r, c)))[b % 2];
+      if (mins && fmt_has_min(fmt)) mins[row * nb + b] = ((const uint16_t*)(tile + dev_min_off(fmt, KC, r, c)))[b % 2];
     }
   }
 }

@@ -22,9 +22,11 @@ enum DecKind : int {
 // constexpr functions are implicitly host+device under clang HIP
 constexpr int dk_bits(int dk) { return dk <= DK_FP4 ? 4 : 8; }
 constexpr bool dk_has_min(int dk) { return dk == DK_INT4A || dk == DK_INT8A; }
-// bytes of one (tile, chunk) record and its code part (formats.h)
+// code bytes of one (tile, chunk) and bytes of one tile region (formats.h)
 constexpr int dk_code_chunk(int dk) { return dk_bits(dk) * 256; }
-constexpr int dk_chunk_bytes(int dk) { return dk_code_chunk(dk) + 64 * (dk_has_min(dk) ? 2 : 1); }
+constexpr int64_t dk_tile_bytes(int dk, int64_t KC) {
+  return KC * dk_code_chunk(dk) + 16 * KC * 4 * (dk_has_min(dk) ? 2 : 1);
+}
 constexpr bool dk_needx(int dk) {
   return dk == DK_INT4S || dk == DK_INT4A || dk == DK_INT8S || dk == DK_INT8A;
 }
@@ -58,6 +60,7 @@ struct GemvArgs {
   int moe_xdiv;            // x row of pair p = p / moe_xdiv
   int64_t w_stride;        // bytes between experts' weight blobs
   int waves;               // v4: waves per workgroup (4 or 8; 0 = 4)
+  int cpk;                 // v4: chunks per split-K slice (multiple of 4 enables quad scale loads; 0 = derive)
 };
 
 }  // namespace illm

@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) lowbit_gemv_kernel(const GemvArgs a) {
 #pragma unroll
   for (int mt = 0; mt < MT; mt++) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const size_t tbase = (size_t)tile * a.KC;
+  const uint8_t* tptr = a.w + (size_t)tile * dk_tile_bytes(DK, a.KC);
   // Software pipeline: a ring of PF chunks is always in flight.  Loads are
   // issued unconditionally (clamped index: tail re-loads are L2 hits) so
   // hipcc keeps counted vmcnt waits instead of branching around loads.
@@ -173,12 +173,16 @@ __global__ void __launch_bounds__(256) lowbit_gemv_kernel(const GemvArgs a) {
   };
   auto load_chunk = [&](Chunk& ch, int c) {
     c = min(c, c1 - 1);
-    const uint8_t* rec = a.w + (tbase + c) * (size_t)dk_chunk_bytes(DK);
+    const uint8_t* rec = tptr + (size_t)c * dk_code_chunk(DK);
     ch.q0 = *(const uint4*)(rec + lane * 16);
     if constexpr (BITS == 8) ch.q1 = *(const uint4*)(rec + 1024 + lane * 16);
-    // C-fragment rows 4g..4g+3: one dword (blk0 | blk1 << 16) per row
-    ch.sc = *(const uint4*)(rec + dk_code_chunk(DK) + g * 16);
-    if constexpr (dk_has_min(DK)) ch.mn = *(const uint4*)(rec + dk_code_chunk(DK) + 64 + g * 16);
+    // C-fragment rows 4g..4g+3: one dword (blk0 | blk1 << 16) per row and chunk
+    const uint32_t* sp = (const uint32_t*)(tptr + (size_t)a.KC * dk_code_chunk(DK)) + (size_t)(4 * g) * a.KC + c;
+    ch.sc = make_uint4(sp[0], sp[a.KC], sp[2 * a.KC], sp[3 * a.KC]);
+    if constexpr (dk_has_min(DK)) {
+      const uint32_t* mp = sp + 16 * a.KC;
+      ch.mn = make_uint4(mp[0], mp[a.KC], mp[2 * a.KC], mp[3 * a.KC]);
+    }
 #pragma unroll
     for (int s = 0; s < 4; s++) {
       const int kk = c * 128 + 32 * s + 8 * g;
@@ -403,10 +407,14 @@ __device__ __forceinline__ uint4 scaled_a8(uint32_t lo, uint32_t hi, h2 d2, h2 m
 // MOE = grouped GEMV over experts (FlashMoE decode): blockIdx.z = expert e,
 // its token-expert pairs are moe_rows[moe_off[e] .. moe_off[e+1]) (<= 16),
 // weights at a.w + e * w_stride, x row = pair / moe_xdiv, output row = pair.
-// ABL (profiling ablations only): 1 = no scale loads, 2 = no x staging, 3 = no dequant/MFMA math
-template <int DK, typename T, int EPI, int TPW, int PF = 4, bool MOE = false, int ABL = 0>
+// QS = quad scales: the workgroup's chunk range starts at a multiple of 4 and
+// KC % 4 == 0, so a row's scales (and mins) of 4 consecutive chunks arrive in
+// ONE 16-B load per 4 code loads (one scale load per chunk measured ~10%
+// slower); the quad for chunks c+4..c+7 is fetched while c..c+3 compute.
+template <int DK, typename T, int EPI, int TPW, bool MOE = false, bool QS = true>
 __global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
   constexpr int BITS = dk_bits(DK);
+  constexpr int PF = 4;
   extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
   __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -426,7 +434,7 @@ __global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
   auto orow_of = [&](int m) -> int { if constexpr (MOE) return prow[m]; else return m; };
 
   const int nks = gridDim.y;
-  const int cpk = (a.KC + nks - 1) / nks;
+  const int cpk = a.cpk > 0 ? a.cpk : (a.KC + nks - 1) / nks;
   const int c0 = blockIdx.y * cpk;
   const int c1 = min(a.KC, c0 + cpk);
   const int kbase = c0 * 128;
@@ -435,28 +443,44 @@ __global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
   const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
   const int tile0 = (blockIdx.x * (int)(blockDim.x >> 6) + wave) * TPW;
   const bool wave_on = tile0 < NT && c0 < c1;
+  const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
+  const size_t soff = (size_t)a.KC * dk_code_chunk(DK) + (size_t)r16 * a.KC * 4;   // this row's scale dwords
+  const size_t moff = soff + (size_t)16 * a.KC * 4;
+  const uint8_t* tb[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; t++) tb[t] = wbase + (size_t)min(tile0 + t, NT - 1) * TB;
 
   struct Chunk {
     uint4 q[TPW][BITS / 4];
-    uint32_t sc[TPW];
+    uint32_t sc[TPW];     // !QS only
     uint32_t mn[TPW];
   };
   auto load_chunk = [&](Chunk& ch, int c) {
     c = min(c, c1 - 1);
 #pragma unroll
     for (int t = 0; t < TPW; t++) {
-      const int tile = min(tile0 + t, NT - 1);
-      const uint8_t* rec = wbase + ((size_t)tile * a.KC + c) * dk_chunk_bytes(DK);
+      const uint8_t* rec = tb[t] + (size_t)c * dk_code_chunk(DK);
       ch.q[t][0] = *(const uint4*)(rec + lane * 16);
       if constexpr (BITS == 8) ch.q[t][1] = *(const uint4*)(rec + 1024 + lane * 16);
-      // this lane's A-row (r16) scales of both blocks: one dword
-      if constexpr (ABL == 1) ch.sc[t] = 0x3c003c00u;
-      else ch.sc[t] = *(const uint32_t*)(rec + dk_code_chunk(DK) + r16 * 4);
-      if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint32_t*)(rec + dk_code_chunk(DK) + 64 + r16 * 4);
+      if constexpr (!QS) {
+        ch.sc[t] = *(const uint32_t*)(tb[t] + soff + (size_t)c * 4);
+        if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint32_t*)(tb[t] + moff + (size_t)c * 4);
+      }
+    }
+  };
+  uint4 sq[TPW], sqn[TPW], mq[TPW], mqn[TPW];     // quad scale / min registers
+  const int last_quad = ((c1 - 1) >> 2) << 2;
+  auto load_quad = [&](uint4 (&s)[TPW], uint4 (&m)[TPW], int c) {
+    c = min(c, last_quad);
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      s[t] = *(const uint4*)(tb[t] + soff + (size_t)c * 4);
+      if constexpr (dk_has_min(DK)) m[t] = *(const uint4*)(tb[t] + moff + (size_t)c * 4);
     }
   };
   Chunk ring[PF];
   if (wave_on) {
+    if constexpr (QS) load_quad(sq, mq, c0);
 #pragma unroll
     for (int u = 0; u < PF; u++) load_chunk(ring[u], c0 + u);
   }
@@ -464,7 +488,7 @@ __global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
     if (threadIdx.x < 256)
       lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
   }
-  if (ABL != 2) {  // stage x[0:M, kbase:kbase+kw] -> LDS as f16
+  {  // stage x[0:M, kbase:kbase+kw] -> LDS as f16
     const int vpr = kw / 8;
     for (int v = threadIdx.x; v < Mloc * vpr; v += blockDim.x) {
       const int m = v / vpr, kk = (v % vpr) * 8;
@@ -498,7 +522,9 @@ __global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
     // broadcast half blk of the row's scale dword to both halves of an h2
     return as_h2(__builtin_amdgcn_perm(0u, v, blk == 0 ? 0x01000100u : 0x03020302u));
   };
-  auto compute_chunk = [&](const Chunk& ch, int c) {
+  auto comp = [](const uint4& v, int u) -> uint32_t { return u == 0 ? v.x : (u == 1 ? v.y : (u == 2 ? v.z : v.w)); };
+  // u = position of the chunk inside its quad (static in the unrolled loops)
+  auto compute_chunk = [&](const Chunk& ch, int c, int u) {
     const uint16_t* xc = xrow + (c - c0) * 128;
     uint4 B[4];
 #pragma unroll
@@ -508,48 +534,64 @@ __global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < TPW; t++) {
+      const uint32_t scw = QS ? comp(sq[t], u) : ch.sc[t];
+      const uint32_t mnw = dk_has_min(DK) ? (QS ? comp(mq[t], u) : ch.mn[t]) : 0u;
 #pragma unroll
       for (int blk = 0; blk < 2; blk++) {
-        const h2 d2 = pick(ch.sc[t], blk);
+        const h2 d2 = pick(scw, blk);
         h2 m2 = h2{(_Float16)0.f, (_Float16)0.f};
-        if constexpr (dk_has_min(DK)) m2 = pick(ch.mn[t], blk);
+        if constexpr (dk_has_min(DK)) m2 = pick(mnw, blk);
 #pragma unroll
         for (int ss = 0; ss < 2; ss++) {
           const int s = blk * 2 + ss;
           uint4 A;
           if constexpr (BITS == 4) {
             const uint4& q0 = ch.q[t][0];
-            const uint32_t u = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
-            A = scaled_a4<DK>(u, d2, m2, lut2);
+            const uint32_t w = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
+            A = scaled_a4<DK>(w, d2, m2, lut2);
           } else {
             const uint4& qq = ch.q[t][blk];
             A = ss == 0 ? scaled_a8<DK>(qq.x, qq.y, d2, m2) : scaled_a8<DK>(qq.z, qq.w, d2, m2);
           }
-          if constexpr (ABL == 3) acc[t][0] += __uint_as_float((ch.q[t][0].x ^ B[s].x ^ ch.sc[t]) & 0x3fffffffu);
-          else acc[t] = mfma16<F16>(A, B[s], acc[t]);
+          acc[t] = mfma16<F16>(A, B[s], acc[t]);
         }
       }
     }
   };
+  auto next_quad = [&]() {
+    if constexpr (QS) {
+#pragma unroll
+      for (int t = 0; t < TPW; t++) {
+        sq[t] = sqn[t];
+        if constexpr (dk_has_min(DK)) mq[t] = mqn[t];
+      }
+    }
+  };
 
+  // Steady state: unconditional loads (hipcc keeps exact counted vmcnt
+  // waits); the last < 2*PF chunks run a guarded tail.
   const int c1u = __builtin_amdgcn_readfirstlane(c1);
   int c = __builtin_amdgcn_readfirstlane(c0);
   for (; c + 2 * PF <= c1u; c += PF) {
 #pragma unroll
     for (int u = 0; u < PF; u++) {
-      compute_chunk(ring[u], c + u);
+      compute_chunk(ring[u], c + u, u);
       load_chunk(ring[u], c + u + PF);
+      if (QS && u == 0) load_quad(sqn, mqn, c + PF);
     }
+    next_quad();
   }
 #pragma unroll
   for (int u = 0; u < PF; u++) {
-    if (c + u < c1u) compute_chunk(ring[u], c + u);
+    if (c + u < c1u) compute_chunk(ring[u], c + u, u);
     load_chunk(ring[u], c + u + PF);
+    if (QS && u == 0) load_quad(sqn, mqn, c + PF);
   }
+  next_quad();
   c += PF;
 #pragma unroll
   for (int u = 0; u < PF; u++)
-    if (c + u < c1u) compute_chunk(ring[u], c + u);
+    if (c + u < c1u) compute_chunk(ring[u], c + u, u);
 
   // ---- epilogue: lane holds rows 16*tile + 4g + i, column r16
   if (r16 >= Mloc) return;
@@ -590,82 +632,40 @@ __global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
   }
 }
 
-template <int DK>
-void launch_gemv4_moe(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
-#define L4M(TT, E, TP)                                                                              \
-  do {                                                                                              \
-    static bool attr = false;                                                                       \
-    if (!attr) {                                                                                    \
-      (void)hipFuncSetAttribute((const void*)lowbit_gemv4_kernel<DK, TT, E, TP, 4, true>,           \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);            \
-      attr = true;                                                                                  \
-    }                                                                                               \
-    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, TT, E, TP, 4, true>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a); \
-  } while (0)
-  if (bf16) {
-    if (epi == EPI_PARTIAL) L4M(BF16, EPI_PARTIAL, 1);
-    else L4M(BF16, EPI_GLU, 2);
-  } else {
-    if (epi == EPI_PARTIAL) L4M(F16, EPI_PARTIAL, 1);
-    else L4M(F16, EPI_GLU, 2);
+// launch helper: 150 KiB dynamic LDS allowed once per instantiation
+template <typename K>
+inline void launch4(K kern, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    attr = true;
   }
-#undef L4M
+  hipLaunchKernelGGL(kern, grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);
+}
+
+template <int DK, typename T, bool MOE, bool QS>
+inline void launch4_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  if (epi == EPI_STORE) launch4(lowbit_gemv4_kernel<DK, T, EPI_STORE, 1, MOE, QS>, grid, shmem, a, st);
+  else if (epi == EPI_PARTIAL) launch4(lowbit_gemv4_kernel<DK, T, EPI_PARTIAL, 1, MOE, QS>, grid, shmem, a, st);
+  else launch4(lowbit_gemv4_kernel<DK, T, EPI_GLU, 2, MOE, QS>, grid, shmem, a, st);
 }
 
 template <int DK>
 void launch_gemv4_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
-#define L4K(TT, E, TP)                                                                              \
-  do {                                                                                              \
-    static bool attr = false;                                                                       \
-    if (!attr) {                                                                                    \
-      (void)hipFuncSetAttribute((const void*)lowbit_gemv4_kernel<DK, TT, E, TP>,                    \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);            \
-      attr = true;                                                                                  \
-    }                                                                                               \
-    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, TT, E, TP>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);       \
-  } while (0)
-  if (a.moe_off != nullptr) {
-    launch_gemv4_moe<DK>(bf16, epi, grid, shmem, a, st);
-    return;
-  }
-  // prefetch-depth experiments (bf16 only): ILLM_GEMV_PF=8|16
-  static const int pf_env = getenv("ILLM_GEMV_PF") ? atoi(getenv("ILLM_GEMV_PF")) : 4;
-  static const int abl_env = getenv("ILLM_GEMV_ABL") ? atoi(getenv("ILLM_GEMV_ABL")) : 0;
-  if (bf16 && abl_env && epi == EPI_PARTIAL) {
-    if (abl_env == 1) hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, BF16, EPI_PARTIAL, 1, 4, false, 1>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);
-    else if (abl_env == 2) hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, BF16, EPI_PARTIAL, 1, 4, false, 2>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);
-    else hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, BF16, EPI_PARTIAL, 1, 4, false, 3>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);
-    return;
-  }
-  if (bf16 && pf_env != 4) {
-#define L4P(E, TP, PFV)                                                                              \
-  do {                                                                                              \
-    static bool attr = false;                                                                       \
-    if (!attr) {                                                                                    \
-      (void)hipFuncSetAttribute((const void*)lowbit_gemv4_kernel<DK, BF16, E, TP, PFV>,             \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);            \
-      attr = true;                                                                                  \
-    }                                                                                               \
-    hipLaunchKernelGGL((lowbit_gemv4_kernel<DK, BF16, E, TP, PFV>), grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a); \
-  } while (0)
-    if (pf_env == 8) {
-      if (epi == EPI_GLU) L4P(EPI_GLU, 2, 8); else if (epi == EPI_PARTIAL) L4P(EPI_PARTIAL, 1, 8); else L4P(EPI_STORE, 1, 8);
-    } else {
-      if (epi == EPI_GLU) L4P(EPI_GLU, 2, 16); else if (epi == EPI_PARTIAL) L4P(EPI_PARTIAL, 1, 16); else L4P(EPI_STORE, 1, 16);
-    }
-#undef L4P
-    return;
-  }
+  // quad scale loads need chunk ranges starting at multiples of 4
+  const int cpk = a.cpk > 0 ? a.cpk : (a.KC + (int)grid.y - 1) / (int)grid.y;
+  const bool qs = (a.KC % 4 == 0) && (cpk % 4 == 0);
+  const bool moe = a.moe_off != nullptr;
+  if (moe && epi == EPI_STORE) epi = EPI_PARTIAL;   // grouped launches write slabs or GLU rows
   if (bf16) {
-    if (epi == EPI_STORE) L4K(BF16, EPI_STORE, 1);
-    else if (epi == EPI_PARTIAL) L4K(BF16, EPI_PARTIAL, 1);
-    else L4K(BF16, EPI_GLU, 2);
+    if (moe) { if (qs) launch4_epi<DK, BF16, true, true>(epi, grid, shmem, a, st); else launch4_epi<DK, BF16, true, false>(epi, grid, shmem, a, st); }
+    else if (qs) launch4_epi<DK, BF16, false, true>(epi, grid, shmem, a, st);
+    else launch4_epi<DK, BF16, false, false>(epi, grid, shmem, a, st);
   } else {
-    if (epi == EPI_STORE) L4K(F16, EPI_STORE, 1);
-    else if (epi == EPI_PARTIAL) L4K(F16, EPI_PARTIAL, 1);
-    else L4K(F16, EPI_GLU, 2);
+    if (moe) { if (qs) launch4_epi<DK, F16, true, true>(epi, grid, shmem, a, st); else launch4_epi<DK, F16, true, false>(epi, grid, shmem, a, st); }
+    else if (qs) launch4_epi<DK, F16, false, true>(epi, grid, shmem, a, st);
+    else launch4_epi<DK, F16, false, false>(epi, grid, shmem, a, st);
   }
-#undef L4K
 }
 
 template <int DK, typename T, int MT>

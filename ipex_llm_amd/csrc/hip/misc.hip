@@ -69,8 +69,8 @@ __global__ void quantize_device_kernel(int fmt, int kind, const void* w, int64_t
   const int r = (int)(row % TILE_N);
   const int64_t c = b / 2;
   const int blk = (int)(b % 2);
-  uint8_t* rec = blob + (t * KC + c) * dev_chunk_bytes(fmt);
-  uint16_t* dscale = (uint16_t*)(rec + dev_code_chunk(fmt));
+  uint8_t* tile = blob + t * dev_tile_bytes(fmt, KC);
+  uint8_t* rec = tile + c * dev_code_chunk(fmt);
   if (bits == 4) {
     for (int ss = 0; ss < 2; ss++) {
       const int s = 2 * blk + ss;
@@ -94,9 +94,8 @@ __global__ void quantize_device_kernel(int fmt, int kind, const void* w, int64_t
       *(uint4*)o = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
   }
-  const int so = dev_scale_idx(r, blk);
-  dscale[so] = hd_f32_to_f16(d);
-  if (fmt_has_min(fmt)) dscale[32 + so] = hd_f32_to_f16(m);
+  ((uint16_t*)(tile + dev_scale_off(fmt, KC, r, c)))[blk] = hd_f32_to_f16(d);
+  if (fmt_has_min(fmt)) ((uint16_t*)(tile + dev_min_off(fmt, KC, r, c)))[blk] = hd_f32_to_f16(m);
 }
 
 void launch_quantize_device(int fmt, int in_kind, const void* w, int64_t n, int64_t k,
@@ -128,9 +127,9 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(int fmt, const ui
   const int r = l & 15, g = l >> 4;
   const int64_t row = t * TILE_N + r;
   if (row >= n) return;
-  const uint8_t* rec = blob + tc * dev_chunk_bytes(fmt);
+  const uint8_t* tile = blob + t * dev_tile_bytes(fmt, KC);
+  const uint8_t* rec = tile + c * dev_code_chunk(fmt);
   const uint4 q = *(const uint4*)(rec + (h * 64 + l) * 16);
-  const uint16_t* dscale = (const uint16_t*)(rec + dev_code_chunk(fmt));
   const uint32_t w[4] = {q.x, q.y, q.z, q.w};
   // 4-bit: dword s = k-step s (block s/2); 8-bit half h: k-steps 2h, 2h+1 (block h)
   for (int ss = 0; ss < (bits == 4 ? 4 : 2); ss++) {
@@ -138,9 +137,8 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(int fmt, const ui
     const int blk = s >> 1;
     const int64_t kk = c * CHUNK_K + 32 * s + 8 * g;
     if (kk >= k) continue;
-    const int so = dev_scale_idx(r, blk);
-    const float d = f16_to_f32(dscale[so]);
-    const float m = fmt_has_min(fmt) ? f16_to_f32(dscale[32 + so]) : 0.f;
+    const float d = f16_to_f32(((const uint16_t*)(tile + dev_scale_off(fmt, KC, r, c)))[blk]);
+    const float m = fmt_has_min(fmt) ? f16_to_f32(((const uint16_t*)(tile + dev_min_off(fmt, KC, r, c)))[blk]) : 0.f;
     float v[8];
     for (int j = 0; j < 8; j++) {
       int code;

@@ -144,7 +144,12 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   a.N = (int)n;
   if (ksplit <= 0) ksplit = small ? v4_ksplit(M, NT, KC, 1, W) : auto_ksplit(NT, KC);
   ksplit = std::min<int64_t>(ksplit, KC);
-  const int64_t cpk = (KC + ksplit - 1) / ksplit;
+  int64_t cpk = (KC + ksplit - 1) / ksplit;
+  if (small && KC % 4 == 0) {          // v4: slices start at multiples of 4 chunks (quad scale loads)
+    cpk = (cpk + 3) / 4 * 4;
+    ksplit = (KC + cpk - 1) / cpk;
+    a.cpk = (int)cpk;
+  }
   const size_t shmem = (size_t)M * (cpk * 128 + 8) * 2;
   const bool use4 = small && shmem <= kMaxLds;
   auto launch = [&](int e) {
@@ -469,7 +474,13 @@ Tensor moe_gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
     while ((lds(ksplit) > 65536 || ((NT + 3) / 4) * ksplit * 2 < 256) && KC / (ksplit * 2) >= 2) ksplit *= 2;
   }
   ksplit = std::min<int64_t>(ksplit, KC);
-  const size_t shmem = (size_t)Mmax * (((KC + ksplit - 1) / ksplit) * 128 + 8) * 2;
+  int64_t cpk = (KC + ksplit - 1) / ksplit;
+  if (KC % 4 == 0) {
+    cpk = (cpk + 3) / 4 * 4;
+    ksplit = (KC + cpk - 1) / cpk;
+    a.cpk = (int)cpk;
+  }
+  const size_t shmem = (size_t)Mmax * (cpk * 128 + 8) * 2;
   TORCH_CHECK(shmem <= kMaxLds, "moe_gemv: K slice too large for LDS");
   Tensor ws = at::empty({ksplit, npairs, n}, xc.options().dtype(at::kFloat));
   a.out = ws.data_ptr();

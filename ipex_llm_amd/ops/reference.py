@@ -28,13 +28,14 @@ def _pad(v, m):
     return (v + m - 1) // m * m
 
 
-def dev_chunk_bytes(fmt):
-    """bytes of one (tile, chunk) record: codes, 32 fp16 scales, [32 fp16 mins]."""
-    return fmt_bits(fmt) * 256 + 64 * (2 if fmt in HAS_MIN else 1)
+def dev_tile_bytes(fmt, KC):
+    """bytes of one 16-row tile region: KC code chunks, then [16][KC] scale
+    dwords, then (asym) [16][KC] min dwords."""
+    return KC * fmt_bits(fmt) * 256 + TILE_N * KC * 4 * (2 if fmt in HAS_MIN else 1)
 
 
 def dev_total(fmt, n, k):
-    return (_pad(n, TILE_N) // TILE_N) * (_pad(k, CHUNK_K) // CHUNK_K) * dev_chunk_bytes(fmt)
+    return (_pad(n, TILE_N) // TILE_N) * dev_tile_bytes(fmt, _pad(k, CHUNK_K) // CHUNK_K) + 16
 
 
 def canon_sizes(fmt, n, k):
@@ -129,7 +130,8 @@ def device_index(fmt: int, n: int, k: int, device="cpu"):
     c, kin = kk // CHUNK_K, kk % CHUNK_K
     s, g, j = kin // 32, (kin % 32) // 8, kin % 8
     lane = g * 16 + r
-    rec = (t * KC + c) * dev_chunk_bytes(fmt)
+    tile = t * dev_tile_bytes(fmt, KC)
+    rec = tile + c * fmt_bits(fmt) * 256
     if fmt_bits(fmt) == 4:
         pos = torch.tensor(_perm_pos(fmt), device=device)[j]
         off = rec + lane * 16 + s * 4 + pos // 2
@@ -138,7 +140,7 @@ def device_index(fmt: int, n: int, k: int, device="cpu"):
         off = rec + ((s // 2) * 64 + lane) * 16 + (s % 2) * 8 + j
         shift = torch.zeros_like(off)
     blk = (kk // QBLOCK) % 2
-    sidx = (rec + fmt_bits(fmt) * 256) // 2 + r * 2 + blk
+    sidx = (tile + KC * fmt_bits(fmt) * 256 + (r * KC + c) * 4) // 2 + blk
     return off, shift, sidx
 
 
@@ -151,7 +153,7 @@ def dequantize_device_blob(blob: torch.Tensor, fmt: int, n: int, k: int) -> torc
     halves = blob.view(torch.float16)
     v = code_table(fmt).to(blob.device)[q] * halves[sidx].float()
     if fmt in HAS_MIN:
-        v = v + halves[sidx + 32].float()
+        v = v + halves[sidx + TILE_N * (_pad(k, CHUNK_K) // CHUNK_K) * 2].float()
     return v
 
 
