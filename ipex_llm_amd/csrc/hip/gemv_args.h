@@ -61,6 +61,10 @@ struct GemvArgs {
   int64_t w_stride;        // bytes between experts' weight blobs
   int waves;               // v4: waves per workgroup (4 or 8; 0 = 4)
   int cpk;                 // v4: chunks per split-K slice (multiple of 4 enables quad scale loads; 0 = derive)
+  // v4 GLU-input prologue: x[m, k] = act(sum_s P[s, m, g(k)]) * sum_s P[s, m, u(k)] from the
+  // gate/up GEMV's split-K slabs P [xpart_ns, M, 2K] (16-row tile-interleaved gate/up columns)
+  const float* xpart;
+  int xpart_ns;
 };
 
 }  // namespace illm

@@ -493,7 +493,36 @@ __global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
     for (int v = threadIdx.x; v < Mloc * vpr; v += blockDim.x) {
       const int m = v / vpr, kk = (v % vpr) * 8;
       uint4 val = make_uint4(0, 0, 0, 0);
-      if (kbase + kk < a.K) {
+      if (kbase + kk < a.K && a.xpart) {
+        // fused activation of the gate/up GEMV: 8 consecutive k stay inside one 16-column tile
+        const int k0 = kbase + kk;
+        const size_t gc = (size_t)(k0 >> 4) * 32 + (k0 & 15);
+        const size_t ld = (size_t)2 * a.K;
+        float gv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, uv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int sp = 0; sp < a.xpart_ns; sp++) {
+          const float* row = a.xpart + ((size_t)sp * a.M + xrow_of(m)) * ld;
+          const float4 g0 = *(const float4*)(row + gc), g1 = *(const float4*)(row + gc + 4);
+          const float4 u0 = *(const float4*)(row + gc + 16), u1 = *(const float4*)(row + gc + 20);
+          gv[0] += g0.x; gv[1] += g0.y; gv[2] += g0.z; gv[3] += g0.w;
+          gv[4] += g1.x; gv[5] += g1.y; gv[6] += g1.z; gv[7] += g1.w;
+          uv[0] += u0.x; uv[1] += u0.y; uv[2] += u0.z; uv[3] += u0.w;
+          uv[4] += u1.x; uv[5] += u1.y; uv[6] += u1.z; uv[7] += u1.w;
+        }
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          float o2[2];
+#pragma unroll
+          for (int j = 0; j < 2; j++) {
+            const float gg = gv[2 * i + j];
+            // activation output rounded to T (what the GLU epilogue would have written)
+            const float act = to_f32<T>(from_f32<T>((a.act == 0 ? silu_f(gg) : gelu_tanh_f(gg)) * uv[2 * i + j]));
+            o2[j] = fminf(fmaxf(act, -65504.f), 65504.f);
+          }
+          w[i] = pack2<F16>(o2[0], o2[1]);
+        }
+        val = make_uint4(w[0], w[1], w[2], w[3]);
+      } else if (kbase + kk < a.K) {
         val = *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk);
         if constexpr (std::is_same<T, BF16>::value) {
           uint32_t w[4] = {val.x, val.y, val.z, val.w};

@@ -177,6 +177,51 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   return out;
 }
 
+// down-projection GEMV whose input is act(gate) * up computed on the fly from
+// the gate/up GEMV's split-K slabs (saves the GLU epilogue's unsplittable
+// launch and one [M, I] round trip); returns f32 partial slabs [ks, M, n].
+Tensor gemv_glu_in(const Tensor& part, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t act,
+                   int64_t ksplit, at::ScalarType dt) {
+  TORCH_CHECK(part.is_cuda() && blob.is_cuda() && part.dim() == 3 && part.scalar_type() == at::kFloat &&
+              part.is_contiguous(), "gemv_glu_in: part must be contiguous f32 [ns, M, 2k] on the GPU");
+  TORCH_CHECK(part.size(2) == 2 * k && k % 16 == 0, "gemv_glu_in: part width must be 2 * k");
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "gemv_glu_in: bf16/fp16 activations");
+  c10::DeviceGuard g(part.device());
+  const bool bf16 = dt == at::kBFloat16;
+  const int64_t M = part.size(1);
+  TORCH_CHECK(M >= 1 && M <= 16, "gemv_glu_in handles 1..16 rows");
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemv_glu_in: weight blob too small");
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  const int W = M > 2 ? 8 : 4;
+  illm::GemvArgs a{};
+  a.x = nullptr;
+  a.xpart = part.data_ptr<float>();
+  a.xpart_ns = (int)part.size(0);
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.KC = (int)KC;
+  a.act = (int)act;
+  a.lut_fmt = (int)fmt;
+  a.waves = W;
+  a.N = (int)n;
+  if (ksplit <= 0) ksplit = v4_ksplit(M, NT, KC, 1, W);
+  ksplit = std::min<int64_t>(ksplit, KC);
+  int64_t cpk = (KC + ksplit - 1) / ksplit;
+  if (KC % 4 == 0) cpk = (cpk + 3) / 4 * 4;
+  ksplit = (KC + cpk - 1) / cpk;
+  a.cpk = (int)cpk;
+  const size_t shmem = (size_t)M * (cpk * 128 + 8) * 2;
+  TORCH_CHECK(shmem <= kMaxLds, "gemv_glu_in: K slice too large for LDS");
+  Tensor ws = at::empty({ksplit, M, n}, part.options());
+  a.out = ws.data_ptr();
+  a.ldo = (int)n;
+  launch_gemv4_any((int)fmt, bf16, illm::EPI_PARTIAL, dim3((unsigned)((NT + W - 1) / W), (unsigned)ksplit), shmem, a);
+  return ws;
+}
+
 Tensor add_rms_norm(const c10::optional<Tensor>& x, const c10::optional<Tensor>& partials,
                     const c10::optional<Tensor>& residual, const Tensor& w, double eps,
                     bool unit_offset, bool store_residual) {
@@ -547,6 +592,7 @@ void decode_advance(const c10::optional<Tensor>& logits, Tensor& ids, Tensor& ne
 }  // namespace
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
+  m.impl("gemv_glu_in", &gemv_glu_in);
   m.impl("decode_advance", &decode_advance);
   m.impl("rope_kv_fused", &rope_kv_fused);
   m.impl("embedding_lowbit", &embedding_lowbit);

@@ -278,6 +278,17 @@ class NativeCausalLM(nn.Module):
         out, _ = ops.add_rms_norm(y.contiguous(), residual, norm_w, s.rms_eps, unit_offset=s.norm_unit_offset)
         return out
 
+    def _fused_mlp_ok(self, x, layer) -> bool:
+        mlp = layer.mlp
+        if not (x.is_cuda and isinstance(mlp, NativeMLP) and x.shape[0] <= 16 and self.tp_group is None):
+            return False
+        gu, dn = mlp.gate_up_proj, mlp.down_proj
+        return (isinstance(gu, LowBitLinear) and isinstance(dn, LowBitLinear) and gu.bias is None and dn.bias is None
+                and dn.mp_group is None and layer.post_feedforward_layernorm is None
+                and dn.in_features % 16 == 0 and self._glu_in_enabled and ops.native_gpu(x))
+
+    _glu_in_enabled = True
+
     def _mlp(self, x, mlp: nn.Module):
         s = self.spec
         if not isinstance(mlp, NativeMLP):
@@ -334,11 +345,18 @@ class NativeCausalLM(nn.Module):
                                              post_norm_w=layer.post_attention_layernorm)
             else:
                 x = self._proj_residual_norm(a, attn.o_proj, residual, layer.post_attention_layernorm)
-            act = self._mlp(x, layer.mlp)
             if li + 1 < len(self.layers):
                 nxt = self.layers[li + 1].input_layernorm
             else:   # stage boundary: the next norm lives on the next stage
                 nxt = self.norm if self.last_stage else layer.input_layernorm
+            if self._fused_mlp_ok(x, layer):
+                # gate/up split-K slabs -> down GEMV applies act(g)*u while staging its input
+                gu, dn = layer.mlp.gate_up_proj, layer.mlp.down_proj
+                pg = ops.gemv_partials(x, gu.weight, gu.fmt, gu.out_features, gu.in_features, 0)
+                pd = ops.gemv_glu_in(pg, dn.weight, dn.fmt, dn.out_features, dn.in_features, s.act, 0, x.dtype)
+                x, _ = ops.add_rms_norm(None, residual, nxt, s.rms_eps, partials=pd, unit_offset=s.norm_unit_offset)
+                continue
+            act = self._mlp(x, layer.mlp)
             if isinstance(layer.mlp, NativeMLP):
                 x = self._proj_residual_norm(act, layer.mlp.down_proj, residual, nxt,
                                              post_norm_w=layer.post_feedforward_layernorm)

@@ -93,3 +93,8 @@ def _(part, w, ids, e0, num_local, dtype):
 def _(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm, norm_eps, q_scale, Hq,
       Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale):
     return None
+
+
+@register_fake("ipex_llm_amd::gemv_glu_in")
+def _(part, blob, fmt, n, k, act, ksplit, dtype):
+    return part.new_empty((max(ksplit, 1), part.shape[1], n), dtype=torch.float32)

@@ -17,7 +17,7 @@ __all__ = [
     "quantize", "dequantize", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
-    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused",
+    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in",
 ]
 
 
@@ -98,6 +98,12 @@ def gemv_partials(x, blob, fmt, n, k, ksplit: int) -> torch.Tensor:
 def gemv_glu(x, blob, fmt, n, k, act: int = 0) -> torch.Tensor:
     """act(x @ Wg^T) * (x @ Wu^T) for a tile-interleaved gate/up weight."""
     return _ops().gemv(x, blob, fmt, n, k, None, 2, 1, act)
+
+
+def gemv_glu_in(part, blob, fmt, n, k, act: int = 0, ksplit: int = 0, dtype=torch.bfloat16) -> torch.Tensor:
+    """down-projection over act(gate)*up taken straight from the gate/up
+    GEMV's split-K slabs ``part`` [ns, M, 2k]; returns f32 slabs [ks, M, n]."""
+    return _ops().gemv_glu_in(part, blob, fmt, n, k, act, ksplit, dtype)
 
 
 def reduce_partials(ws, bias=None, dtype=torch.bfloat16):

@@ -18,3 +18,20 @@ def test_embedding_lowbit_kernel(cuda, qtype):
     out = torch.ops.ipex_llm_amd.embedding_lowbit(blob.to(cuda), fmt, 300, 256, ids.to(cuda), torch.bfloat16)
     assert out.shape == (2, 3, 256)
     assert torch.allclose(out.float().cpu(), ref[ids], atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+@pytest.mark.parametrize("qtype", ["sym_int4", "asym_int4", "sym_int8"])
+def test_gemv_glu_in_matches_glu_then_down(cuda, M, qtype):
+    """down GEMV with the activation fused into its input staging == GLU GEMV + down GEMV"""
+    fmt = Q.get_format(Q.resolve_qtype(qtype)).fmt
+    H, I = 512, 1024
+    g = torch.Generator(device="cuda").manual_seed(M)
+    gu = ops.quantize(torch.randn(2 * I, H, generator=g, device=cuda) * 0.05, fmt)
+    dn = ops.quantize(torch.randn(H, I, generator=g, device=cuda) * 0.05, fmt)
+    x = (torch.randn(M, H, generator=g, device=cuda) * 0.5).to(torch.bfloat16)
+    a = ops.gemv_glu(x, gu, fmt, 2 * I, H, 0)
+    ref = ops.gemv_partials(a, dn, fmt, H, I, 0).sum(0)
+    pg = ops.gemv_partials(x, gu, fmt, 2 * I, H, 0)
+    out = ops.gemv_glu_in(pg, dn, fmt, H, I, 0, 0, torch.bfloat16).sum(0)
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-2
