@@ -287,7 +287,9 @@ class NativeCausalLM(nn.Module):
                 and dn.mp_group is None and layer.post_feedforward_layernorm is None
                 and dn.in_features % 16 == 0 and self._glu_in_enabled and ops.native_gpu(x))
 
-    _glu_in_enabled = True
+    # measured neutral at B=1 and ~1% slower at B=8 on MI355X (the down GEMV's
+    # slab-reading prologue costs what the split gate/up GEMV saves): opt-in
+    _glu_in_enabled = __import__("os").environ.get("ILLM_FUSED_GLU_IN", "0") == "1"
 
     def _mlp(self, x, mlp: nn.Module):
         s = self.spec

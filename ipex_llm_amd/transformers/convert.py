@@ -63,12 +63,24 @@ def _merge_linears(mods: List[nn.Linear], interleave_glu: bool = False) -> nn.Li
 def _merge_qkv(attn: nn.Module):
     if hasattr(attn, "qkv_proj") or not all(hasattr(attn, n) for n in ("q_proj", "k_proj", "v_proj")):
         return
+    mods = [attn.q_proj, attn.k_proj, attn.v_proj]
+    if all(isinstance(m, LowBitLinear) for m in mods):      # pre-quantized (GPTQ/AWQ) checkpoints
+        from .low_bit_linear import lowbit_row_concat
+        if len({id(m.g_idx_map) if m.g_idx_map is not None else None for m in mods}) > 1 and \
+                any(m.g_idx_map is not None for m in mods):
+            return                                           # different act-order permutations
+        attn.qkv_proj = lowbit_row_concat(mods)
+        del attn.q_proj, attn.k_proj, attn.v_proj
+        return
+    if not all(isinstance(m, nn.Linear) for m in mods):
+        return
     attn.qkv_proj = _merge_linears([attn.q_proj, attn.k_proj, attn.v_proj])
     del attn.q_proj, attn.k_proj, attn.v_proj
 
 
 def _merge_gate_up(mlp: nn.Module):
-    if hasattr(mlp, "gate_up_proj") and not getattr(mlp, "_illm_interleaved", False):
+    if hasattr(mlp, "gate_up_proj") and not getattr(mlp, "_illm_interleaved", False) and \
+            isinstance(mlp.gate_up_proj, nn.Linear):
         # phi3-style fused [gate; up] -> tile-interleaved
         w = mlp.gate_up_proj.weight.data
         I = w.shape[0] // 2
@@ -79,7 +91,16 @@ def _merge_gate_up(mlp: nn.Module):
         return
     if mlp.gate_proj.bias is not None:
         return
-    mlp.gate_up_proj = _merge_linears([mlp.gate_proj, mlp.up_proj], interleave_glu=True)
+    if isinstance(mlp.gate_proj, LowBitLinear) and isinstance(mlp.up_proj, LowBitLinear):
+        if mlp.gate_proj.g_idx_map is not None or mlp.up_proj.g_idx_map is not None:
+            if mlp.gate_proj.g_idx_map is not mlp.up_proj.g_idx_map:
+                return
+        from .low_bit_linear import lowbit_row_concat
+        mlp.gate_up_proj = lowbit_row_concat([mlp.gate_proj, mlp.up_proj], interleave_glu=True)
+    elif isinstance(mlp.gate_proj, nn.Linear) and isinstance(mlp.up_proj, nn.Linear):
+        mlp.gate_up_proj = _merge_linears([mlp.gate_proj, mlp.up_proj], interleave_glu=True)
+    else:
+        return
     mlp._illm_interleaved = True
     del mlp.gate_proj, mlp.up_proj
 
@@ -108,7 +129,8 @@ def _optimize_pre(model: nn.Module, qtype: int):
         if mlp is not None:
             I = getattr(getattr(mlp, "gate_proj", None), "out_features", None) or \
                 (getattr(getattr(mlp, "gate_up_proj", None), "out_features", 0) // 2)
-            if I and I % 16 == 0 and isinstance(getattr(mlp, "gate_up_proj", getattr(mlp, "gate_proj", None)), nn.Linear):
+            if I and I % 16 == 0 and isinstance(getattr(mlp, "gate_up_proj", getattr(mlp, "gate_proj", None)),
+                                                (nn.Linear, LowBitLinear)):
                 _merge_gate_up(mlp)
     model._illm_pre = True
     return model

@@ -261,3 +261,50 @@ FP16Linear = DenseLinear
 class BF16Linear(DenseLinear):
     def __init__(self, in_features, out_features, bias=True, dtype=torch.bfloat16, device=None, mp_group=None):
         super().__init__(in_features, out_features, bias, torch.bfloat16, device, mp_group)
+
+
+# ---------------------------------------------------------------- canonical blob surgery
+def canon_planes(blob: torch.Tensor, fmt: int, n: int, k: int):
+    """split a canonical blob into (codes [n, k*bits/8] u8, scales [n, k/64] f16, mins or None)"""
+    from ..ops.reference import canon_sizes, fmt_bits, HAS_MIN
+    cb, se = canon_sizes(fmt, n, k)
+    b = blob.reshape(-1)
+    codes = b[:cb].view(n, k * fmt_bits(fmt) // 8)
+    scales = b[cb:cb + 2 * se].view(torch.float16).view(n, k // 64)
+    mins = b[cb + 2 * se:cb + 4 * se].view(torch.float16).view(n, k // 64) if fmt in HAS_MIN else None
+    return codes, scales, mins
+
+
+def canon_join(codes, scales, mins=None) -> torch.Tensor:
+    parts = [codes.reshape(-1), scales.contiguous().view(torch.uint8).reshape(-1)]
+    if mins is not None:
+        parts.append(mins.contiguous().view(torch.uint8).reshape(-1))
+    return torch.cat(parts)
+
+
+def lowbit_row_concat(mods, interleave_glu: bool = False) -> "LowBitLinear":
+    """Stack the output rows of low-bit linears sharing qtype / in_features
+    (merge q/k/v; gate/up with 16-row tile interleave) without re-quantizing."""
+    m0 = mods[0]
+    k, fmt = m0.in_features, m0.fmt
+    assert all(isinstance(m, LowBitLinear) and m.fmt == fmt and m.in_features == k for m in mods)
+    planes = [canon_planes(m.canonical_blob().cpu(), fmt, m.out_features, k) for m in mods]
+    if interleave_glu:
+        from ..models.decoder import interleave_glu_rows
+        cat = lambda i: None if planes[0][i] is None else interleave_glu_rows(planes[0][i], planes[1][i])  # noqa: E731
+    else:
+        cat = lambda i: None if planes[0][i] is None else torch.cat([p[i] for p in planes], 0)  # noqa: E731
+    n = sum(m.out_features for m in mods)
+    new = LowBitLinear(k, n, m0.qtype, bias=False, device="meta")
+    blob = canon_join(cat(0), cat(1), cat(2))
+    dev = m0.weight.device
+    if dev.type == "cuda":
+        blob = ops.repack_to_device(blob, fmt, n, k).to(dev)
+    new.weight = nn.Parameter(blob, requires_grad=False)
+    if any(m.bias is not None for m in mods) and not interleave_glu:
+        new.bias = nn.Parameter(torch.cat([m.bias.data if m.bias is not None else
+                                           torch.zeros(m.out_features, device=dev) for m in mods]),
+                                requires_grad=False)
+    if m0.g_idx_map is not None:
+        new.g_idx_map = m0.g_idx_map
+    return new

@@ -61,6 +61,23 @@ def _resolve_qtype_from_kwargs(kwargs):
     return q
 
 
+def _checkpoint_quant_config(path):
+    cfg_file = os.path.join(path, "config.json") if os.path.isdir(str(path)) else None
+    if cfg_file is None or not os.path.exists(cfg_file):
+        return None
+    try:
+        with open(cfg_file) as f:
+            qc = json.load(f).get("quantization_config")
+    except (OSError, ValueError):
+        return None
+    return qc if isinstance(qc, dict) else None
+
+
+def load_in_pre_quant(path) -> bool:
+    qc = _checkpoint_quant_config(path)
+    return qc is not None and str(qc.get("quant_method", "")).lower() in ("gptq", "awq")
+
+
 def save_low_bit(self, save_dir: str, *args, **kwargs):
     """Write config + portable low-bit weights (reference model.py:59-103)."""
     os.makedirs(save_dir, exist_ok=True)
@@ -144,6 +161,12 @@ class _BaseAutoModelClass:
         tp_group = kwargs.pop("tp_group", None)
         kwargs.pop("model_hub", None)
         prequant = kwargs.pop("_illm_prequant", None)
+        if prequant is None and path is not None and (qtype is not None or load_in_pre_quant(path)):
+            qc = _checkpoint_quant_config(path)
+            if qc is not None and str(qc.get("quant_method", "")).lower() in ("gptq", "awq"):
+                # GPTQ / AWQ checkpoints always load as asym_int4 (reference model.py)
+                prequant = (str(qc["quant_method"]).lower(), qc)
+                qtype = "asym_int4"
         torch_dtype = kwargs.pop("torch_dtype", kwargs.pop("dtype", "auto"))
         if qtype is None:
             return cls.HF_Model.from_pretrained(path, *args, torch_dtype=torch_dtype, **kwargs)
