@@ -1,0 +1,163 @@
+"""Build an HF model (+ tokenizer) from a GGUF file.
+
+Reference: ``SRC/transformers/gguf/api.py:21-75`` (``load_gguf_model``
+dispatching to per-family builders: llama, mistral, mixtral, baichuan,
+bloom, falcon, mpt, yuan2) and ``gguf/models/llama.py:28-129`` (config from
+the key/values, q/k row permutation undone, weights loaded tensor by
+tensor).  Here one table-driven builder covers the llama-layout families
+(llama / mistral / qwen2 / qwen3 and the MoE variants mixtral / qwen2moe /
+qwen3moe); the tokenizer is rebuilt with transformers' GGUF converters.
+Tensors are dequantized one at a time from the memory-mapped file and then
+re-quantized by ``ggml_convert_low_bit`` into the MI355X formats.
+"""
+from __future__ import annotations
+
+import re
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .reader import GGUFReader
+
+ARCH_TO_HF = {"llama": "llama", "mistral": "mistral", "qwen2": "qwen2", "qwen3": "qwen3",
+              "qwen2moe": "qwen2_moe", "qwen3moe": "qwen3_moe"}
+
+_LAYER = {
+    "attn_norm": "input_layernorm.weight",
+    "ffn_norm": "post_attention_layernorm.weight",
+    "attn_q": "self_attn.q_proj",
+    "attn_k": "self_attn.k_proj",
+    "attn_v": "self_attn.v_proj",
+    "attn_output": "self_attn.o_proj",
+    "attn_q_norm": "self_attn.q_norm.weight",
+    "attn_k_norm": "self_attn.k_norm.weight",
+    "ffn_gate": "mlp.gate_proj",
+    "ffn_up": "mlp.up_proj",
+    "ffn_down": "mlp.down_proj",
+    "ffn_gate_inp": "mlp.gate.weight",
+    "ffn_gate_shexp": "mlp.shared_expert.gate_proj",
+    "ffn_up_shexp": "mlp.shared_expert.up_proj",
+    "ffn_down_shexp": "mlp.shared_expert.down_proj",
+    "ffn_gate_inp_shexp": "mlp.shared_expert_gate.weight",
+}
+
+
+def _unpermute(w: np.ndarray, n_head: int) -> np.ndarray:
+    """undo llama.cpp's q/k row permutation (HF rotate_half -> GGUF interleaved)"""
+    out = w.shape[0]
+    return w.reshape(n_head, 2, out // n_head // 2, *w.shape[1:]).swapaxes(1, 2).reshape(w.shape)
+
+
+def _config(r: GGUFReader):
+    from transformers import AutoConfig
+    from transformers.integrations.ggml import GGUF_CONFIG_MAPPING
+    arch = r.architecture
+    mt = ARCH_TO_HF.get(arch)
+    if mt is None:
+        raise NotImplementedError(f"GGUF architecture '{arch}' is not supported")
+    kw = {}
+    mapping = GGUF_CONFIG_MAPPING.get(arch, GGUF_CONFIG_MAPPING["llama"])
+    for key, hf in mapping.items():
+        v = r.kv.get(f"{arch}.{key}")
+        if hf is not None and v is not None:
+            kw[hf] = v
+    if "vocab_size" not in kw:
+        toks = r.kv.get("tokenizer.ggml.tokens")
+        if toks is not None:
+            kw["vocab_size"] = len(toks)
+        else:
+            kw["vocab_size"] = r.tensors["token_embd.weight"].shape[1]
+    n_exp = r.kv.get(f"{arch}.expert_count")
+    if n_exp:
+        kw["num_local_experts" if mt == "mixtral" else "num_experts"] = n_exp
+        kw["num_experts_per_tok"] = r.kv.get(f"{arch}.expert_used_count", 2)
+        if mt != "mixtral":
+            ff = r.kv.get(f"{arch}.expert_feed_forward_length")
+            if ff:
+                kw["moe_intermediate_size"] = ff
+    if arch == "llama" and n_exp:
+        mt = "mixtral"
+        kw["num_local_experts"] = kw.pop("num_experts", n_exp)
+    kw.pop("head_dim", None) if mt in ("llama", "mistral", "mixtral") else None
+    kw["tie_word_embeddings"] = "output.weight" not in r.tensors
+    for t in ("bos", "eos", "padding"):
+        v = r.kv.get(f"tokenizer.ggml.{t}_token_id")
+        if v is not None:
+            kw[{"padding": "pad"}.get(t, t) + "_token_id"] = v
+    return AutoConfig.for_model(mt, **kw), mt
+
+
+def _tokenizer(r: GGUFReader):
+    try:
+        from transformers import PreTrainedTokenizerFast
+        from transformers.integrations.ggml import convert_gguf_tokenizer
+    except ImportError:  # pragma: no cover
+        return None
+    tok = {k[len("tokenizer.ggml."):]: v for k, v in r.kv.items() if k.startswith("tokenizer.ggml.")}
+    if "tokens" not in tok:
+        return None
+    arch = r.architecture if r.architecture in ("llama", "qwen2", "qwen2moe", "qwen3", "qwen3moe") else "llama"
+    try:
+        fast, extra = convert_gguf_tokenizer(arch, tok)
+    except Exception:       # unknown tokenizer model: leave to the caller
+        return None
+    return PreTrainedTokenizerFast(tokenizer_object=fast, **extra)
+
+
+def load_gguf_model(fpath: str, dtype=torch.float16, low_bit: Optional[str] = None) -> Tuple[torch.nn.Module, object]:
+    """GGUF file -> (HF CausalLM with dense ``dtype`` weights, tokenizer)."""
+    from accelerate import init_empty_weights
+    from transformers import AutoModelForCausalLM
+    r = GGUFReader(fpath)
+    cfg, mt = _config(r)
+    with init_empty_weights():
+        model = AutoModelForCausalLM.from_config(cfg, torch_dtype=dtype)
+    n_head, n_kv = cfg.num_attention_heads, getattr(cfg, "num_key_value_heads", cfg.num_attention_heads)
+    sd: Dict[str, torch.Tensor] = {}
+    experts: Dict[int, Dict[str, np.ndarray]] = {}
+    for name in r.tensors:
+        w = r.tensor(name)
+        if name == "token_embd.weight":
+            sd["model.embed_tokens.weight"] = torch.from_numpy(w)
+            continue
+        if name == "output_norm.weight":
+            sd["model.norm.weight"] = torch.from_numpy(w)
+            continue
+        if name == "output.weight":
+            sd["lm_head.weight"] = torch.from_numpy(w)
+            continue
+        m = re.match(r"blk\.(\d+)\.(\w+?)\.(weight|bias)$", name)
+        if not m:
+            continue
+        i, kind, wb = int(m.group(1)), m.group(2), m.group(3)
+        if kind in ("ffn_gate_exps", "ffn_up_exps", "ffn_down_exps"):
+            experts.setdefault(i, {})[kind] = w
+            continue
+        target = _LAYER.get(kind)
+        if target is None:
+            continue
+        if kind in ("attn_q", "attn_k") and r.architecture == "llama" and wb == "weight":
+            w = _unpermute(w, n_head if kind == "attn_q" else n_kv)
+        elif kind in ("attn_q", "attn_k") and r.architecture == "llama" and wb == "bias":
+            w = _unpermute(w[:, None], n_head if kind == "attn_q" else n_kv)[:, 0]
+        key = f"model.layers.{i}.{target}"
+        if not key.endswith((".weight", ".bias")):
+            key += "." + wb
+        if kind == "ffn_gate_inp_shexp" and w.ndim == 1:
+            w = w[None, :]
+        sd[key] = torch.from_numpy(np.ascontiguousarray(w))
+    for i, ex in experts.items():
+        g, u, d = ex["ffn_gate_exps"], ex["ffn_up_exps"], ex["ffn_down_exps"]    # [E, I, H], [E, I, H], [E, H, I]
+        sd[f"model.layers.{i}.mlp.experts.gate_up_proj"] = torch.from_numpy(np.concatenate([g, u], 1))
+        sd[f"model.layers.{i}.mlp.experts.down_proj"] = torch.from_numpy(np.ascontiguousarray(d))
+    sd = {k: v.to(dtype) for k, v in sd.items()}
+    model.load_state_dict(sd, strict=False, assign=True)
+    if cfg.tie_word_embeddings:
+        model.tie_weights()
+    from ..transformers.model import _reinit_meta_buffers
+    _reinit_meta_buffers(model, cfg)
+    missing = [n for n, p in model.named_parameters() if p.device.type == "meta"]
+    if missing:
+        raise RuntimeError(f"GGUF file lacks tensors for: {missing[:6]}")
+    return model.eval(), _tokenizer(r)

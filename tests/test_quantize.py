@@ -76,3 +76,24 @@ def test_cpu_lowbit_gemm_matches_reference():
         ref = x @ R.dequantize_canonical(blob, f, 96, 256).t()
         y = ops.lowbit_matmul(x, blob, f, 96, 256)
         assert torch.allclose(y, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_imatrix_file_roundtrip_and_weighted_quantization(tmp_path):
+    import torch
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.quantize import qtypes as Q
+    from ipex_llm_amd.quantize.imatrix import load_imatrix, read_imatrix, write_imatrix
+    torch.manual_seed(0)
+    K = 256
+    imp = torch.rand(K) ** 4 * 100 + 1e-3
+    p = str(tmp_path / "imatrix.dat")
+    write_imatrix(p, {"blk.0.attn_q.weight": imp, "blk.0.ffn_down.weight": imp}, ncall=10)
+    raw = read_imatrix(p)
+    assert torch.allclose(raw["blk.0.attn_q.weight"], imp, rtol=1e-5)
+    hf = load_imatrix(p)
+    assert "model.layers.0.self_attn.q_proj" in hf and "model.layers.0.self_attn.qkv_proj" in hf
+    # importance-weighted quantization lowers the weighted error
+    fmt = Q.get_format("sym_int4").fmt
+    w = torch.randn(64, K)
+    err = lambda blob: (((ops.dequantize(blob, fmt, 64, K) - w) ** 2) * imp).sum().item()  # noqa: E731
+    assert err(ops.quantize(w, fmt, imp, True)) < err(ops.quantize(w, fmt, None, False))
