@@ -64,6 +64,7 @@ struct RopeKVArgs {
   // device-side slots (slots == null): slot = block_tables[t / tq][pos / bs] * bs + pos % bs
   const int32_t* block_tables;
   int max_blocks, tq;
+  const int64_t* pos_offset;   // [B] (cache index = pos - offset) or null
 };
 void launch_rope_kv(bool bf16, const RopeKVArgs& a, hipStream_t st);
 
@@ -109,7 +110,7 @@ void launch_embedding_rows(bool bf16, const uint8_t* blob, int fmt, const int64_
 
 void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int64_t* ids, int64_t* next_ids,
                            int64_t* pos, const int32_t* block_tables, int max_blocks, int bs, int64_t* slots,
-                           int32_t* seq_lens, hipStream_t st);
+                           int32_t* seq_lens, const int64_t* pos_offset, hipStream_t st);
 
 // ---- one-shot xGMI peer all-reduce (allreduce.hip) ------------------------
 constexpr int AR_MAX_RANKS = 8;

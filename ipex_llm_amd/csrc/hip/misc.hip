@@ -366,7 +366,8 @@ template <typename T>
 __global__ void __launch_bounds__(1024) decode_advance_kernel(const uint16_t* logits, int V, int64_t* ids,
                                                               int64_t* next_ids, int64_t* pos,
                                                               const int32_t* block_tables, int max_blocks, int bs,
-                                                              int64_t* slots, int32_t* seq_lens) {
+                                                              int64_t* slots, int32_t* seq_lens,
+                                                              const int64_t* pos_offset) {
   const int b = blockIdx.x, tid = threadIdx.x;
   if (logits) {
     const uint16_t* row = logits + (size_t)b * V;
@@ -426,18 +427,19 @@ __global__ void __launch_bounds__(1024) decode_advance_kernel(const uint16_t* lo
   if (tid == 0) {
     const int64_t p = pos[b] + 1;
     pos[b] = p;
-    if (slots) slots[b] = (int64_t)block_tables[(size_t)b * max_blocks + p / bs] * bs + p % bs;
-    if (seq_lens) seq_lens[b] = (int32_t)(p + 1);
+    const int64_t ci = p - (pos_offset ? pos_offset[b] : 0);      // cache index
+    if (slots) slots[b] = (int64_t)block_tables[(size_t)b * max_blocks + ci / bs] * bs + ci % bs;
+    if (seq_lens) seq_lens[b] = (int32_t)(ci + 1);
   }
 }
 
 void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int64_t* ids, int64_t* next_ids,
                            int64_t* pos, const int32_t* block_tables, int max_blocks, int bs, int64_t* slots,
-                           int32_t* seq_lens, hipStream_t st) {
+                           int32_t* seq_lens, const int64_t* pos_offset, hipStream_t st) {
   if (bf16) hipLaunchKernelGGL(decode_advance_kernel<BF16>, dim3(B), dim3(1024), 0, st, logits, V, ids, next_ids, pos,
-                               block_tables, max_blocks, bs, slots, seq_lens);
+                               block_tables, max_blocks, bs, slots, seq_lens, pos_offset);
   else hipLaunchKernelGGL(decode_advance_kernel<F16>, dim3(B), dim3(1024), 0, st, logits, V, ids, next_ids, pos,
-                          block_tables, max_blocks, bs, slots, seq_lens);
+                          block_tables, max_blocks, bs, slots, seq_lens, pos_offset);
 }
 
 }  // namespace illm

@@ -70,7 +70,8 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
     if (a.slots) {
       slot = a.slots[t];
     } else {
-      const int64_t pp = a.pos[t];
+      // cache index = rotary position - per-sequence offset (compressed KV keeps fewer entries)
+      const int64_t pp = a.pos[t] - (a.pos_offset ? a.pos_offset[t / a.tq] : 0);
       slot = (int64_t)a.block_tables[(size_t)(t / a.tq) * a.max_blocks + pp / a.bs] * a.bs + pp % a.bs;
     }
     if (slot < 0) return;

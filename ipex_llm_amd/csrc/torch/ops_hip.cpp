@@ -336,7 +336,7 @@ void rope_kv_fused(const Tensor& part, const c10::optional<Tensor>& bias, Tensor
                    Tensor& v_cache, const Tensor& pos, const Tensor& block_tables, int64_t tq, const Tensor& inv_freq,
                    const c10::optional<Tensor>& q_norm, const c10::optional<Tensor>& k_norm, double norm_eps,
                    double q_scale, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot_dim, bool interleaved,
-                   int64_t kv_fp8, double k_scale, double v_scale) {
+                   int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& pos_offset) {
   c10::DeviceGuard g(part.device());
   const bool bf16 = is_bf16(q_out);
   TORCH_CHECK(part.dim() == 3 && part.scalar_type() == at::kFloat && part.is_contiguous(),
@@ -356,6 +356,7 @@ void rope_kv_fused(const Tensor& part, const c10::optional<Tensor>& bias, Tensor
   a.block_tables = block_tables.data_ptr<int32_t>();
   a.max_blocks = (int)block_tables.size(1);
   a.tq = (int)tq;
+  a.pos_offset = (pos_offset.has_value() && pos_offset->defined()) ? pos_offset->data_ptr<int64_t>() : nullptr;
   a.pos = pos.data_ptr<int64_t>();
   if (inv_freq.dim() == 3) a.cos_sin = inv_freq.data_ptr<float>();
   else a.inv_freq = inv_freq.data_ptr<float>();
@@ -570,7 +571,8 @@ Tensor embedding_lowbit(const Tensor& blob, int64_t fmt, int64_t n, int64_t k, c
 
 // logits: [B, V] bf16/f16 or undefined (sampling done by the host: only advance)
 void decode_advance(const c10::optional<Tensor>& logits, Tensor& ids, Tensor& next_ids, Tensor& pos,
-                    const Tensor& block_tables, int64_t bs, Tensor& slots, Tensor& seq_lens) {
+                    const Tensor& block_tables, int64_t bs, Tensor& slots, Tensor& seq_lens,
+                    const c10::optional<Tensor>& pos_offset) {
   c10::DeviceGuard g(pos.device());
   const int64_t B = pos.numel();
   TORCH_CHECK(pos.scalar_type() == at::kLong && ids.scalar_type() == at::kLong && slots.scalar_type() == at::kLong &&
@@ -586,7 +588,9 @@ void decode_advance(const c10::optional<Tensor>& logits, Tensor& ids, Tensor& ne
   illm::launch_decode_advance(bf16, has ? p16(*logits) : nullptr, (int)B, V, ids.data_ptr<int64_t>(),
                               next_ids.data_ptr<int64_t>(), pos.data_ptr<int64_t>(), block_tables.data_ptr<int32_t>(),
                               (int)block_tables.size(1), (int)bs, slots.data_ptr<int64_t>(),
-                              seq_lens.data_ptr<int32_t>(), cur_stream());
+                              seq_lens.data_ptr<int32_t>(),
+                              (pos_offset.has_value() && pos_offset->defined()) ? pos_offset->data_ptr<int64_t>() : nullptr,
+                              cur_stream());
 }
 
 }  // namespace

@@ -46,6 +46,7 @@ class DecodeStep:
         self.ids = torch.zeros(self.B, dtype=torch.long, device=dev)
         self.pos = torch.zeros(self.B, dtype=torch.long, device=dev)
         self.slots = torch.zeros(self.B, dtype=torch.long, device=dev)
+        self.off = torch.zeros(self.B, dtype=torch.long, device=dev)      # compressed-KV position offsets
         self.seq_lens = torch.ones(self.B, dtype=torch.int32, device=dev)
         self.nsplit = nsplit_for(max_len)
         self.greedy = greedy
@@ -58,12 +59,13 @@ class DecodeStep:
     def _refresh(self):
         """slots / key counts for the current positions (eager, outside the graph)"""
         bs = self.cache.bs
-        blk = torch.gather(self.block_tables, 1, (self.pos // bs).unsqueeze(1)).squeeze(1).long()
-        self.slots.copy_(blk * bs + self.pos % bs)
-        self.seq_lens.copy_((self.pos + 1).to(torch.int32))
+        ci = self.pos - self.off
+        blk = torch.gather(self.block_tables, 1, (ci // bs).unsqueeze(1)).squeeze(1).long()
+        self.slots.copy_(blk * bs + ci % bs)
+        self.seq_lens.copy_((ci + 1).to(torch.int32))
 
     def _body(self):
-        meta = AttnMeta(self.B, 1, self.block_tables, self.seq_lens, self.nsplit)
+        meta = AttnMeta(self.B, 1, self.block_tables, self.seq_lens, self.nsplit, pos_offset=self.off)
         m = self.model
         if self.native_glue:
             h = m.forward_tokens(self.ids, self.pos, self.slots, meta, self.cache, return_hidden=True)
@@ -73,7 +75,7 @@ class DecodeStep:
             self.logits = logits
             torch.ops.ipex_llm_amd.decode_advance(logits if self.greedy else None, self.ids, self.next_ids,
                                                   self.pos, self.block_tables, self.cache.bs, self.slots,
-                                                  self.seq_lens)
+                                                  self.seq_lens, self.off)
             return
         logits = m.forward_tokens(self.ids, self.pos, self.slots, meta, self.cache)
         self.logits = logits
@@ -110,9 +112,13 @@ class DecodeStep:
         self.pos.copy_(pos0)
         self._refresh()
 
-    def set_state(self, ids: torch.Tensor, pos: torch.Tensor):
+    def set_state(self, ids: torch.Tensor, pos: torch.Tensor, off: Optional[torch.Tensor] = None):
         self.ids.copy_(ids)
         self.pos.copy_(pos)
+        if off is not None:
+            self.off.copy_(off)
+        else:
+            self.off.zero_()
         self._refresh()
 
     def step(self):
@@ -235,7 +241,8 @@ class Engine:
     def generate(self, prompts: Sequence[Sequence[int]], max_new_tokens: int = 32, min_new_tokens: int = 0,
                  do_sample: bool = False, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
                  repetition_penalty: float = 1.0, eos_token_id=None, streamer=None, use_graph: bool = True,
-                 timing: Optional[GenTiming] = None, generator=None) -> List[List[int]]:
+                 timing: Optional[GenTiming] = None, generator=None, compress_kv: Optional[bool] = None,
+                 compress_capacity: Optional[int] = None, compress_window: Optional[int] = None) -> List[List[int]]:
         dev = self.model.device
         B = len(prompts)
         max_len = max(len(p) for p in prompts) + max_new_tokens + 1
@@ -244,10 +251,26 @@ class Engine:
         seqs = [SequenceState(self.cache.allocator.alloc(nblk)) for _ in range(B)]
         eos = set([eos_token_id] if isinstance(eos_token_id, int) else (eos_token_id or []))
         sync = (lambda: torch.cuda.synchronize()) if dev.type == "cuda" else (lambda: None)
+        from ..utils.settings import get_settings
+        cfg = get_settings()
+        compress = cfg.compress_kv_cache if compress_kv is None else compress_kv
+        cap = compress_capacity or cfg.compress_kv_capacity
+        win = compress_window or cfg.compress_kv_window
+        offs = [0] * B
         t0 = time.perf_counter()
         last = []
         for b, p in enumerate(prompts):
-            lg = self.prefill(seqs[b], torch.tensor(list(p), dtype=torch.long))
+            snap = compress and len(p) > cap
+            if snap:
+                self.model._capture_q, self.model._capture_w = {}, win
+            try:
+                lg = self.prefill(seqs[b], torch.tensor(list(p), dtype=torch.long))
+            finally:
+                qw, self.model._capture_q = self.model._capture_q, None
+            if snap:
+                from .compress_kv import snapkv_compress
+                snapkv_compress(self.model, self.cache, seqs[b], len(p), qw, cap, win)
+                offs[b] = len(p) - cap
             lg = apply_repetition_penalty(lg, [list(p)], repetition_penalty)
             last.append(_sample(lg, do_sample, temperature, top_k, top_p, generator))
         cur = torch.cat(last).to(dev)
@@ -264,7 +287,8 @@ class Engine:
             streamer.put(torch.tensor(toks))
         greedy = not do_sample and repetition_penalty == 1.0
         st = self.decode_step_obj(seqs, max_len, greedy, use_graph)
-        st.set_state(cur, torch.tensor([s.length for s in seqs], device=dev))
+        st.set_state(cur, torch.tensor([s.length + o for s, o in zip(seqs, offs)], device=dev),
+                     torch.tensor(offs, device=dev))
         for i in range(1, max_new_tokens):
             if all(done):
                 break

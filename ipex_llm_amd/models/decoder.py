@@ -107,6 +107,7 @@ class AttnMeta:
     seq_lens: torch.Tensor          # int32 [B] (keys incl. the new tokens)
     nsplit: int
     seq_lens_host: Optional[List[int]] = None
+    pos_offset: Optional[torch.Tensor] = None   # [B] cache index = pos - offset (compressed KV)
 
 
 def interleave_glu_rows(gate: torch.Tensor, up: torch.Tensor, tile: int = 16) -> torch.Tensor:
@@ -289,6 +290,8 @@ class NativeCausalLM(nn.Module):
 
     # measured neutral at B=1 and ~1% slower at B=8 on MI355X (the down GEMV's
     # slab-reading prologue costs what the split gate/up GEMV saves): opt-in
+    _capture_q = None
+    _capture_w = 32
     _glu_in_enabled = __import__("os").environ.get("ILLM_FUSED_GLU_IN", "0") == "1"
 
     def _mlp(self, x, mlp: nn.Module):
@@ -335,12 +338,14 @@ class NativeCausalLM(nn.Module):
                 ops.rope_kv_fused(part, qp.bias, q, cache.k[li], cache.v[li], pos, meta.block_tables, meta.Tq, rope,
                                   s.num_heads, s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved,
                                   attn.q_norm, attn.k_norm, s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale,
-                                  cache.v_scale)
+                                  cache.v_scale, meta.pos_offset)
             else:
                 qkv = qp(x)
                 ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,
                             s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved, attn.q_norm, attn.k_norm,
                             s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale, cache.v_scale)
+            if self._capture_q is not None:            # SnapKV observation window
+                self._capture_q[li] = q[-self._capture_w:].clone()
             a = self._attention(li, attn, q, meta, cache)
             if s.sandwich_norm:
                 x = self._proj_residual_norm(a, attn.o_proj, residual, layer.pre_feedforward_layernorm,

@@ -91,7 +91,7 @@ def _(part, w, ids, e0, num_local, dtype):
 
 @register_fake("ipex_llm_amd::rope_kv_fused")
 def _(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm, norm_eps, q_scale, Hq,
-      Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale):
+      Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale, pos_offset=None):
     return None
 
 

@@ -222,13 +222,14 @@ def rope_kv(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, Hq, Hkv, D, rot_
 
 def rope_kv_fused(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, Hq, Hkv, D, rot_dim=None,
                   interleaved=False, q_norm=None, k_norm=None, norm_eps=1e-6, q_scale=1.0, kv_fp8=0,
-                  k_scale=1.0, v_scale=1.0):
+                  k_scale=1.0, v_scale=1.0, pos_offset=None):
     """rope_kv over the split-K partials of the QKV GEMV ([ks, T, N] f32,
     summed + bias in the kernel) with device-side slots from the block table."""
     rot_dim = rot_dim or D
     if _native(part):
         _ops().rope_kv_fused(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm,
-                             norm_eps, q_scale, Hq, Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale)
+                             norm_eps, q_scale, Hq, Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale,
+                             pos_offset)
         return q_out
     qkv = part.sum(0)
     if bias is not None:
@@ -236,7 +237,8 @@ def rope_kv_fused(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, in
     qkv = qkv.to(q_out.dtype)
     bs = k_cache.shape[2]
     seq = torch.arange(pos.numel(), device=pos.device) // tq
-    slots = block_tables.long()[seq, pos // bs] * bs + pos % bs
+    ci = pos - (pos_offset[seq] if pos_offset is not None else 0)
+    slots = block_tables.long()[seq, ci // bs] * bs + ci % bs
     return rope_kv(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, Hq, Hkv, D, rot_dim, interleaved, q_norm,
                    k_norm, norm_eps, q_scale, kv_fp8, k_scale, v_scale)
 

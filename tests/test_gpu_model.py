@@ -40,3 +40,20 @@ def test_gpu_vs_cpu_logits(cuda):
     lc = ec.prefill(s2, ids).float()
     rel = ((lg - lc).norm() / lc.norm()).item()
     assert rel < 3e-2, rel
+
+
+@pytest.mark.gpu
+def test_compress_kv_graph_decode_on_gpu(cuda):
+    """compressed KV (pos_offset) through the fused RoPE + decode_advance kernels"""
+    from transformers import LlamaConfig
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models.builder import random_native_model
+    cfg = LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                      num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=4096)
+    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=0)
+    prompt = [list(range(1, 400))]
+    eager = Engine(m).generate(prompt, max_new_tokens=12, use_graph=False, compress_kv=True,
+                               compress_capacity=192, compress_window=32)
+    graph = Engine(m).generate(prompt, max_new_tokens=12, use_graph=True, compress_kv=True,
+                               compress_capacity=192, compress_window=32)
+    assert eager == graph and len(graph[0]) == 399 + 12
