@@ -228,7 +228,7 @@ class NativeCausalLM(nn.Module):
         softcap = s.attn_softcap
         window = attn.sliding_window
         kc, vc = cache.k[li], cache.v[li]
-        if meta.Tq * group <= 16:
+        if meta.Tq * group <= 16 and (s.head_dim in (64, 80, 96, 128, 256) or not q.is_cuda):
             o = ops.attn_decode(q.view(meta.B, meta.Tq, s.num_heads, s.head_dim), kc, vc, meta.block_tables,
                                 meta.seq_lens, meta.nsplit, s.scale, softcap, window, cache.kv_fp8,
                                 cache.k_scale, cache.v_scale, None, meta.seq_lens_host)

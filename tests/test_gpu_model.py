@@ -49,7 +49,7 @@ def test_compress_kv_graph_decode_on_gpu(cuda):
     from ipex_llm_amd.engine.runner import Engine
     from ipex_llm_amd.models.builder import random_native_model
     cfg = LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
-                      num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=4096)
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=4096)
     m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=0)
     prompt = [list(range(1, 400))]
     eager = Engine(m).generate(prompt, max_new_tokens=12, use_graph=False, compress_kv=True,
