@@ -242,7 +242,8 @@ class Engine:
                  do_sample: bool = False, temperature: float = 1.0, top_k: int = 0, top_p: float = 1.0,
                  repetition_penalty: float = 1.0, eos_token_id=None, streamer=None, use_graph: bool = True,
                  timing: Optional[GenTiming] = None, generator=None, compress_kv: Optional[bool] = None,
-                 compress_capacity: Optional[int] = None, compress_window: Optional[int] = None) -> List[List[int]]:
+                 compress_capacity: Optional[int] = None, compress_window: Optional[int] = None,
+                 logits_processor=None) -> List[List[int]]:
         dev = self.model.device
         B = len(prompts)
         max_len = max(len(p) for p in prompts) + max_new_tokens + 1
@@ -272,6 +273,8 @@ class Engine:
                 snapkv_compress(self.model, self.cache, seqs[b], len(p), qw, cap, win)
                 offs[b] = len(p) - cap
             lg = apply_repetition_penalty(lg, [list(p)], repetition_penalty)
+            if logits_processor is not None:
+                lg = logits_processor(torch.tensor([list(p)], device=lg.device), lg.float())
             last.append(_sample(lg, do_sample, temperature, top_k, top_p, generator))
         cur = torch.cat(last).to(dev)
         out = [list(p) for p in prompts]
@@ -285,7 +288,7 @@ class Engine:
             timing.first_cost = time.perf_counter() - t0
         if streamer is not None:
             streamer.put(torch.tensor(toks))
-        greedy = not do_sample and repetition_penalty == 1.0
+        greedy = not do_sample and repetition_penalty == 1.0 and logits_processor is None
         st = self.decode_step_obj(seqs, max_len, greedy, use_graph)
         st.set_state(cur, torch.tensor([s.length + o for s, o in zip(seqs, offs)], device=dev),
                      torch.tensor(offs, device=dev))
@@ -295,7 +298,11 @@ class Engine:
             t1 = time.perf_counter()
             nxt = st.step()
             if not greedy:
-                lg = apply_repetition_penalty(st.logits.clone(), out, repetition_penalty)
+                lg = apply_repetition_penalty(st.logits.float().clone(), out, repetition_penalty)
+                if logits_processor is not None:
+                    width = max(len(o) for o in out)
+                    ids_t = torch.tensor([o + [o[-1]] * (width - len(o)) for o in out], device=lg.device)
+                    lg = logits_processor(ids_t, lg)
                 nxt = _sample(lg, do_sample, temperature, top_k, top_p, generator)
                 st.ids.copy_(nxt)
             toks = nxt.tolist()

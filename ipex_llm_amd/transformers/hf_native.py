@@ -130,7 +130,7 @@ def native_generate(self, input_ids=None, attention_mask=None, generation_config
                     max_new_tokens=None, max_length=None, min_new_tokens=None, do_sample=None,
                     temperature=None, top_k=None, top_p=None, repetition_penalty=None, eos_token_id=None,
                     pad_token_id=None, prompt_lookup_num_tokens=None, lookahead=None, use_graph=True,
-                    **kwargs):
+                    logits_processor=None, **kwargs):
     gc = generation_config or getattr(self, "generation_config", None)
 
     def pick(v, name, default):
@@ -166,7 +166,16 @@ def native_generate(self, input_ids=None, attention_mask=None, generation_config
         from ..generation.lookup import lookup_generate
         outs = lookup_generate(eng, prompts, num_output_tokens=int(lookup), timing=timing, streamer=streamer, **kw)
     else:
-        outs = eng.generate(prompts, streamer=streamer, use_graph=use_graph, timing=timing, **kw)
+        lp = None
+        if logits_processor:
+            procs = list(logits_processor) if isinstance(logits_processor, (list, tuple)) or \
+                hasattr(logits_processor, "__iter__") else [logits_processor]
+
+            def lp(ids, scores):
+                for p in procs:
+                    scores = p(ids, scores)
+                return scores
+        outs = eng.generate(prompts, streamer=streamer, use_graph=use_graph, timing=timing, logits_processor=lp, **kw)
     self.first_cost = timing.first_cost
     self.rest_cost_mean = timing.rest_cost_mean
     self.last_timing = timing
