@@ -46,7 +46,13 @@ def _cmd(src: str, obj: str):
     tinc, tapi, _ = _torch_paths()
     common = ["-O3", "-fPIC", "-std=c++17", "-I", CSRC]
     if src.endswith(".hip"):
-        return [HIPCC, f"--offload-arch={ARCH}", "-Wno-pass-failed", *common, "-c", src, "-o", obj]
+        extra = []
+        if os.path.basename(src).startswith("gemv_"):
+            # keep the GEMV epilogue as scalar f32 FMAs: SLP-packed v_pk_fma_f32
+            # beside MFMAs costs issue cycles on gfx950 (and blocks v_fma_mix)
+            # and MFMA results in VGPRs (no v_accvgpr_read per 64-block readout)
+            extra = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]
+        return [HIPCC, f"--offload-arch={ARCH}", "-Wno-pass-failed", *extra, *common, "-c", src, "-o", obj]
     if "/cpu/" in src:
         return ["g++", *common, "-fopenmp", "-march=x86-64-v3", "-c", src, "-o", obj]
     pyinc = sysconfig.get_paths()["include"]

@@ -12,7 +12,7 @@
 // a multiple of 16 rows, K to a multiple of 128.  Tile t = n/16, chunk
 // c = k/128, KC = Kp/128.  Every tile owns one contiguous region of
 // dev_tile_bytes(f, KC) bytes (tiles in order, +16 B tail pad):
-//   [codes of chunks 0..KC-1][scales [16 rows][KC][2 blocks] fp16][mins, asym]
+//   [codes of chunks 0..KC-1][scales [KC][16 rows][2 blocks] fp16][mins, asym]
 // One wave64 streams one chunk with one global_load_dwordx4 per lane per
 // KiB of codes:
 //   lane l: A-operand row r = l & 15, k-group g = l >> 4
@@ -22,10 +22,11 @@
 //          packed pair (2q, 2q+1) of the A fragment).
 //   8-bit: 32 B per lane, two 16-B halves h at T + c*2048 + (h*64 + l)*16;
 //          half h holds k-steps 2h, 2h+1, each as 8 bytes in element order.
-//   scales: one dword (blk0 | blk1 << 16) per (row, chunk) at
-//          dev_scale_off(f, KC, r, c): a row's scales of 4 consecutive
-//          chunks are one 16-B load, so the decode GEMV issues one scale
-//          load per 4 code loads; mins follow the same layout (asym only).
+//   scales: one dword (blk0 | blk1 << 16) per (row, chunk), chunk-major
+//          ([KC][16 rows], dev_scale_off): the 4 MFMA C-fragment rows
+//          4g..4g+3 of a chunk are one 16-B load, so the decode GEMV applies
+//          block scales on the accumulator side; mins follow the same
+//          layout (asym only).
 #pragma once
 #include <stdint.h>
 
@@ -95,7 +96,7 @@ constexpr int64_t dev_tile_bytes(int f, int64_t KC) {
 }
 // byte offset (within a tile region) of the scale dword of (row r, chunk c)
 constexpr int64_t dev_scale_off(int f, int64_t KC, int r, int64_t c) {
-  return KC * dev_code_chunk(f) + ((int64_t)r * KC + c) * 4;
+  return KC * dev_code_chunk(f) + (c * TILE_N + r) * 4;
 }
 // byte offset of the min dword of (row r, chunk c) (asym formats)
 constexpr int64_t dev_min_off(int f, int64_t KC, int r, int64_t c) {

@@ -7,7 +7,9 @@
 
 namespace illm {
 
-enum GemvEpi : int { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_GLU = 2 };
+// EPI_ATOMIC: f32 atomic adds into a zero-initialised [M][N] accumulator (the
+// consumer reads ONE slab and re-zeroes it), so split-K needs no slab reduce
+enum GemvEpi : int { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_GLU = 2, EPI_ATOMIC = 3 };
 enum DecKind : int {
   DK_INT4S = 0,  // sym_int4 / woq_int4
   DK_INT4A = 1,  // asym_int4
@@ -65,6 +67,10 @@ struct GemvArgs {
   // gate/up GEMV's split-K slabs P [xpart_ns, M, 2K] (16-row tile-interleaved gate/up columns)
   const float* xpart;
   int xpart_ns;
+  // v5 int4 decode constants (set by the launcher): packed-pair nibble mask
+  // and magic exponent; runtime values so hipcc emits one v_and_or_b32
+  uint32_t nib_mask, nib_magic;
+  int pf;                  // v5 prefetch depth (4 or 8 chunks per wave)
 };
 
 }  // namespace illm

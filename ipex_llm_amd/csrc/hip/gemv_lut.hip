@@ -3,6 +3,6 @@
 namespace illm {
 template void launch_gemv_dk<DK_LUT4>(bool, int, int, dim3, const GemvArgs&, hipStream_t);
 template void launch_gemv_dk<DK_FP4>(bool, int, int, dim3, const GemvArgs&, hipStream_t);
-template void launch_gemv4_dk<DK_LUT4>(bool, int, dim3, size_t, const GemvArgs&, hipStream_t);
-template void launch_gemv4_dk<DK_FP4>(bool, int, dim3, size_t, const GemvArgs&, hipStream_t);
+template void launch_gemv5_dk<DK_LUT4>(bool, int, int, dim3, size_t, const GemvArgs&, hipStream_t);
+template void launch_gemv5_dk<DK_FP4>(bool, int, int, dim3, size_t, const GemvArgs&, hipStream_t);
 }  // namespace illm

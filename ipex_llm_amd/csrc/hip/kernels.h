@@ -16,10 +16,15 @@ namespace illm {
 // dk = decoder kind (fmt_to_dk), mt = ceil(M/16) in {1,2,4}
 template <int DK>
 void launch_gemv_dk(bool bf16, int mt, int epi, dim3 grid, const GemvArgs& a, hipStream_t st);
-// v4 (M <= 16, x staged in LDS as f16): grid = (ceil(NT / (4 * TPW)), ksplit),
-// shmem = M * (Kwg + 8) * 2 <= 150 KiB
+// v5 (M <= 16, lowbit_gemv5.cuh): workgroup = 4 waves = (4 / kw) tile groups
+// x kw k-parts; grid = (ceil(groups / (4 / kw)), ksplit[, experts]),
+// shmem = gemv5_shmem(rows, chunks per split) <= 159 KiB
 template <int DK>
-void launch_gemv4_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
+void launch_gemv5_dk(bool bf16, int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
+constexpr int gemv5_x_ld_h(int kw) { return kw + 8; }
+constexpr size_t gemv5_shmem_h(int rows, int cpk) {
+  return ((size_t)rows * gemv5_x_ld_h(cpk * 128) * 2 + 15) / 16 * 16 + (size_t)rows * cpk * 16 + 4 * 2 * 64 * 16;
+}
 
 // ---- norms (norm.hip) ------------------------------------------------------
 struct NormArgs {
@@ -33,6 +38,7 @@ struct NormArgs {
   float eps;
   int unit_offset;         // gemma: x * (1 + w)
   int store_residual;
+  int zero_partials;       // re-zero the (atomic-accumulated) partial slab after reading it
 };
 void launch_add_rms_norm(bool bf16, const NormArgs& a, hipStream_t st);
 void launch_layer_norm(bool bf16, const uint16_t* x, const uint16_t* w, const uint16_t* b,
@@ -60,6 +66,7 @@ struct RopeKVArgs {
   // fused split-K reduction of the QKV GEMV: qkv = sum_s part[s] (+ bias)
   const float* part;       // [nsplit, T, ld_qkv] f32 or null (then qkv is read)
   int nsplit;
+  int zero_part;            // re-zero part (atomic accumulator, nsplit == 1) after use
   const uint16_t* bias;    // [ld_qkv] or null
   // device-side slots (slots == null): slot = block_tables[t / tq][pos / bs] * bs + pos % bs
   const int32_t* block_tables;

@@ -15,10 +15,9 @@
 //     MFMA against an all-ones A fragment (sum of x per block) instead of
 //     per-element VALU subtracts;
 //   * per-64-block scales are applied on the 4 f32 accumulators per lane;
-//   * two kernels: lowbit_gemv4_kernel (M <= 16, the decode hot path: x in
-//     LDS, pre-scaled f16 A fragments, one accumulator per tile) and
-//     lowbit_gemv_kernel (17..64 rows: MT 16-row M tiles per wave, 4 waves
-//     split K and reduce through LDS);
+//   * two kernels: lowbit_gemv5_kernel (M <= 16, the decode hot path,
+//     lowbit_gemv5.cuh) and lowbit_gemv_kernel (17..64 rows: MT 16-row M
+//     tiles per wave, 4 waves split K and reduce through LDS);
 //   * a workgroup-level split-K over blockIdx.y writes f32 partial slabs that
 //     are summed by the consumer (fused add+RMSNorm / reduce) kernel.
 #pragma once
@@ -177,12 +176,10 @@ __global__ void __launch_bounds__(256) lowbit_gemv_kernel(const GemvArgs a) {
     ch.q0 = *(const uint4*)(rec + lane * 16);
     if constexpr (BITS == 8) ch.q1 = *(const uint4*)(rec + 1024 + lane * 16);
     // C-fragment rows 4g..4g+3: one dword (blk0 | blk1 << 16) per row and chunk
-    const uint32_t* sp = (const uint32_t*)(tptr + (size_t)a.KC * dk_code_chunk(DK)) + (size_t)(4 * g) * a.KC + c;
-    ch.sc = make_uint4(sp[0], sp[a.KC], sp[2 * a.KC], sp[3 * a.KC]);
-    if constexpr (dk_has_min(DK)) {
-      const uint32_t* mp = sp + 16 * a.KC;
-      ch.mn = make_uint4(mp[0], mp[a.KC], mp[2 * a.KC], mp[3 * a.KC]);
-    }
+    // chunk-major scale plane: rows 4g..4g+3 of chunk c are one 16-B record
+    const uint32_t* sp = (const uint32_t*)(tptr + (size_t)a.KC * dk_code_chunk(DK)) + (size_t)c * 16 + 4 * g;
+    ch.sc = *(const uint4*)sp;
+    if constexpr (dk_has_min(DK)) ch.mn = *(const uint4*)(sp + 16 * a.KC);
 #pragma unroll
     for (int s = 0; s < 4; s++) {
       const int kk = c * 128 + 32 * s + 8 * g;
@@ -314,388 +311,11 @@ __global__ void __launch_bounds__(256) lowbit_gemv_kernel(const GemvArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// v4 (M <= 16): pre-scaled f16 A fragments, one MFMA accumulator per tile.
-// x[0:M, K-slice] is staged once per workgroup in LDS (16-B vector loads,
-// read back as MFMA B fragments with ds_read_b128); each wave owns TPW whole
-// 16-row tiles over the workgroup's K range (TPW = 2 for GLU: gate tile + up
-// tile in the same lanes -> act(g) * u in registers), so there is no
-// cross-wave reduction, and only weight records live in the PF-deep register
-// prefetch ring.  Why pre-scaled: v1 accumulates each 64-element block in a fresh MFMA accumulator and then
-// read it out (v_accvgpr_read) to apply the block scale: a dependent
-// MFMA -> VALU chain per block that, at the ~2 waves/SIMD a GEMV grid gives,
-// is not hidden.  Here the block scale (and min) is applied to the decoded
-// weights with packed f16 VALU (exact (q-8) via the 0x6400 magic, then one
-// rounding of (q-8)*d), so all chunks of a tile chain into ONE accumulator,
-// the all-ones offset MFMA disappears and there is no per-block readout.
-// Activations are converted to f16 while being staged into LDS (clamped to
-// the f16 range), accumulation stays f32, outputs are written in T.
-// ---------------------------------------------------------------------------
-typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+}  // namespace illm
 
-__device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
-__device__ __forceinline__ uint32_t as_u(h2 v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ uint32_t bytes01(uint32_t u) { return __builtin_amdgcn_perm(0u, u, 0x0c010c00u); }
-__device__ __forceinline__ uint32_t bytes23(uint32_t u) { return __builtin_amdgcn_perm(0u, u, 0x0c030c02u); }
+#include "lowbit_gemv5.cuh"
 
-// scaled A fragment (8 f16) for one k-step; d2 / m2 = (d, d) / (m, m)
-template <int DK>
-__device__ __forceinline__ uint4 scaled_a4(uint32_t u, h2 d2, h2 m2, const uint32_t* lut2) {
-  uint32_t w[4];
-  if constexpr (DK == DK_INT4S || DK == DK_INT4A) {
-    w[0] = (u & 0x000F000Fu) | 0x64006400u;
-    w[1] = ((u >> 4) & 0x000F000Fu) | 0x64006400u;
-    w[2] = ((u >> 8) & 0x000F000Fu) | 0x64006400u;
-    w[3] = ((u >> 12) & 0x000F000Fu) | 0x64006400u;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      if constexpr (DK == DK_INT4S) w[i] = as_u((as_h2(w[i]) - h2{(_Float16)1032.f, (_Float16)1032.f}) * d2);
-      else w[i] = as_u(__builtin_elementwise_fma(as_h2(w[i]) - h2{(_Float16)1024.f, (_Float16)1024.f}, d2, m2));
-    }
-  } else {
-    if constexpr (DK == DK_FP4) {
-      w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 0));
-      w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 1));
-      w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 2));
-      w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 3));
-    } else {  // DK_LUT4: f16 pair table
-      w[0] = lut2[u & 0xff];
-      w[1] = lut2[(u >> 8) & 0xff];
-      w[2] = lut2[(u >> 16) & 0xff];
-      w[3] = lut2[u >> 24];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) w[i] = as_u(as_h2(w[i]) * d2);
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-template <int DK>
-__device__ __forceinline__ uint4 scaled_a8(uint32_t lo, uint32_t hi, h2 d2, h2 m2) {
-  uint32_t w[4];
-  if constexpr (DK == DK_FP8E4 || DK == DK_FP8E5) {
-    if constexpr (DK == DK_FP8E4) {
-      w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(lo, 1.0f, false));
-      w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(lo, 1.0f, true));
-      w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(hi, 1.0f, false));
-      w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(hi, 1.0f, true));
-    } else {
-      w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(lo, 1.0f, false));
-      w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(lo, 1.0f, true));
-      w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(hi, 1.0f, false));
-      w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(hi, 1.0f, true));
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) w[i] = as_u(as_h2(w[i]) * d2);
-  } else {
-    // bytes -> f16(1024 + byte) via v_perm + magic; signed codes biased by 128
-    if constexpr (DK == DK_INT8S) { lo ^= 0x80808080u; hi ^= 0x80808080u; }
-    w[0] = bytes01(lo) | 0x64006400u;
-    w[1] = bytes23(lo) | 0x64006400u;
-    w[2] = bytes01(hi) | 0x64006400u;
-    w[3] = bytes23(hi) | 0x64006400u;
-    const _Float16 off = DK == DK_INT8S ? (_Float16)1152.f : (_Float16)1024.f;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      if constexpr (DK == DK_INT8S) w[i] = as_u((as_h2(w[i]) - h2{off, off}) * d2);
-      else w[i] = as_u(__builtin_elementwise_fma(as_h2(w[i]) - h2{off, off}, d2, m2));
-    }
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// MOE = grouped GEMV over experts (FlashMoE decode): blockIdx.z = expert e,
-// its token-expert pairs are moe_rows[moe_off[e] .. moe_off[e+1]) (<= 16),
-// weights at a.w + e * w_stride, x row = pair / moe_xdiv, output row = pair.
-// QS = quad scales: the workgroup's chunk range starts at a multiple of 4 and
-// KC % 4 == 0, so a row's scales (and mins) of 4 consecutive chunks arrive in
-// ONE 16-B load per 4 code loads (one scale load per chunk measured ~10%
-// slower); the quad for chunks c+4..c+7 is fetched while c..c+3 compute.
-template <int DK, typename T, int EPI, int TPW, bool MOE = false, bool QS = true>
-__global__ void __launch_bounds__(512) lowbit_gemv4_kernel(const GemvArgs a) {
-  constexpr int BITS = dk_bits(DK);
-  constexpr int PF = 4;
-  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
-  __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, r16 = lane & 15;
-  int Mloc = a.M;
-  const uint8_t* wbase = a.w;
-  const int32_t* prow = nullptr;
-  if constexpr (MOE) {
-    const int e = blockIdx.z;
-    const int m0 = a.moe_off[e];
-    Mloc = min(16, a.moe_off[e + 1] - m0);
-    if (Mloc <= 0) return;                // expert not routed to: whole block exits
-    wbase += (size_t)e * a.w_stride;
-    prow = a.moe_rows + m0;
-  }
-  auto xrow_of = [&](int m) -> int { if constexpr (MOE) return prow[m] / a.moe_xdiv; else return m; };
-  auto orow_of = [&](int m) -> int { if constexpr (MOE) return prow[m]; else return m; };
-
-  const int nks = gridDim.y;
-  const int cpk = a.cpk > 0 ? a.cpk : (a.KC + nks - 1) / nks;
-  const int c0 = blockIdx.y * cpk;
-  const int c1 = min(a.KC, c0 + cpk);
-  const int kbase = c0 * 128;
-  const int kw = (c1 - c0) * 128;
-  const int lds_ld = kw + 8;
-  const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
-  const int tile0 = (blockIdx.x * (int)(blockDim.x >> 6) + wave) * TPW;
-  const bool wave_on = tile0 < NT && c0 < c1;
-  const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
-  const size_t soff = (size_t)a.KC * dk_code_chunk(DK) + (size_t)r16 * a.KC * 4;   // this row's scale dwords
-  const size_t moff = soff + (size_t)16 * a.KC * 4;
-  const uint8_t* tb[TPW];
-#pragma unroll
-  for (int t = 0; t < TPW; t++) tb[t] = wbase + (size_t)min(tile0 + t, NT - 1) * TB;
-
-  struct Chunk {
-    uint4 q[TPW][BITS / 4];
-    uint32_t sc[TPW];     // !QS only
-    uint32_t mn[TPW];
-  };
-  auto load_chunk = [&](Chunk& ch, int c) {
-    c = min(c, c1 - 1);
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-      const uint8_t* rec = tb[t] + (size_t)c * dk_code_chunk(DK);
-      ch.q[t][0] = *(const uint4*)(rec + lane * 16);
-      if constexpr (BITS == 8) ch.q[t][1] = *(const uint4*)(rec + 1024 + lane * 16);
-      if constexpr (!QS) {
-        ch.sc[t] = *(const uint32_t*)(tb[t] + soff + (size_t)c * 4);
-        if constexpr (dk_has_min(DK)) ch.mn[t] = *(const uint32_t*)(tb[t] + moff + (size_t)c * 4);
-      }
-    }
-  };
-  uint4 sq[TPW], sqn[TPW], mq[TPW], mqn[TPW];     // quad scale / min registers
-  const int last_quad = ((c1 - 1) >> 2) << 2;
-  auto load_quad = [&](uint4 (&s)[TPW], uint4 (&m)[TPW], int c) {
-    c = min(c, last_quad);
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-      s[t] = *(const uint4*)(tb[t] + soff + (size_t)c * 4);
-      if constexpr (dk_has_min(DK)) m[t] = *(const uint4*)(tb[t] + moff + (size_t)c * 4);
-    }
-  };
-  Chunk ring[PF];
-  if (wave_on) {
-    if constexpr (QS) load_quad(sq, mq, c0);
-#pragma unroll
-    for (int u = 0; u < PF; u++) load_chunk(ring[u], c0 + u);
-  }
-  if constexpr (DK == DK_LUT4) {
-    if (threadIdx.x < 256)
-      lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
-  }
-  {  // stage x[0:M, kbase:kbase+kw] -> LDS as f16
-    const int vpr = kw / 8;
-    for (int v = threadIdx.x; v < Mloc * vpr; v += blockDim.x) {
-      const int m = v / vpr, kk = (v % vpr) * 8;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (kbase + kk < a.K && a.xpart) {
-        // fused activation of the gate/up GEMV: 8 consecutive k stay inside one 16-column tile
-        const int k0 = kbase + kk;
-        const size_t gc = (size_t)(k0 >> 4) * 32 + (k0 & 15);
-        const size_t ld = (size_t)2 * a.K;
-        float gv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, uv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int sp = 0; sp < a.xpart_ns; sp++) {
-          const float* row = a.xpart + ((size_t)sp * a.M + xrow_of(m)) * ld;
-          const float4 g0 = *(const float4*)(row + gc), g1 = *(const float4*)(row + gc + 4);
-          const float4 u0 = *(const float4*)(row + gc + 16), u1 = *(const float4*)(row + gc + 20);
-          gv[0] += g0.x; gv[1] += g0.y; gv[2] += g0.z; gv[3] += g0.w;
-          gv[4] += g1.x; gv[5] += g1.y; gv[6] += g1.z; gv[7] += g1.w;
-          uv[0] += u0.x; uv[1] += u0.y; uv[2] += u0.z; uv[3] += u0.w;
-          uv[4] += u1.x; uv[5] += u1.y; uv[6] += u1.z; uv[7] += u1.w;
-        }
-        uint32_t w[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          float o2[2];
-#pragma unroll
-          for (int j = 0; j < 2; j++) {
-            const float gg = gv[2 * i + j];
-            // activation output rounded to T (what the GLU epilogue would have written)
-            const float act = to_f32<T>(from_f32<T>((a.act == 0 ? silu_f(gg) : gelu_tanh_f(gg)) * uv[2 * i + j]));
-            o2[j] = fminf(fmaxf(act, -65504.f), 65504.f);
-          }
-          w[i] = pack2<F16>(o2[0], o2[1]);
-        }
-        val = make_uint4(w[0], w[1], w[2], w[3]);
-      } else if (kbase + kk < a.K) {
-        val = *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk);
-        if constexpr (std::is_same<T, BF16>::value) {
-          uint32_t w[4] = {val.x, val.y, val.z, val.w};
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const float lo = fminf(fmaxf(bf16_to_f32(w[i] & 0xffff), -65504.f), 65504.f);
-            const float hi = fminf(fmaxf(bf16_to_f32(w[i] >> 16), -65504.f), 65504.f);
-            w[i] = pack2<F16>(lo, hi);
-          }
-          val = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-      }
-      *(uint4*)(xs + m * lds_ld + kk) = val;
-    }
-  }
-  __syncthreads();
-  if (!wave_on) return;
-
-  const bool mok = r16 < Mloc;
-  const uint16_t* xrow = xs + (mok ? r16 : 0) * lds_ld + 8 * g;
-  f32x4 acc[TPW];
-#pragma unroll
-  for (int t = 0; t < TPW; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto pick = [&](uint32_t v, int blk) -> h2 {
-    // broadcast half blk of the row's scale dword to both halves of an h2
-    return as_h2(__builtin_amdgcn_perm(0u, v, blk == 0 ? 0x01000100u : 0x03020302u));
-  };
-  auto comp = [](const uint4& v, int u) -> uint32_t { return u == 0 ? v.x : (u == 1 ? v.y : (u == 2 ? v.z : v.w)); };
-  // u = position of the chunk inside its quad (static in the unrolled loops)
-  auto compute_chunk = [&](const Chunk& ch, int c, int u) {
-    const uint16_t* xc = xrow + (c - c0) * 128;
-    uint4 B[4];
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-      const uint4 v = *(const uint4*)(xc + 32 * s);
-      B[s] = mok ? v : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-      const uint32_t scw = QS ? comp(sq[t], u) : ch.sc[t];
-      const uint32_t mnw = dk_has_min(DK) ? (QS ? comp(mq[t], u) : ch.mn[t]) : 0u;
-#pragma unroll
-      for (int blk = 0; blk < 2; blk++) {
-        const h2 d2 = pick(scw, blk);
-        h2 m2 = h2{(_Float16)0.f, (_Float16)0.f};
-        if constexpr (dk_has_min(DK)) m2 = pick(mnw, blk);
-#pragma unroll
-        for (int ss = 0; ss < 2; ss++) {
-          const int s = blk * 2 + ss;
-          uint4 A;
-          if constexpr (BITS == 4) {
-            const uint4& q0 = ch.q[t][0];
-            const uint32_t w = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
-            A = scaled_a4<DK>(w, d2, m2, lut2);
-          } else {
-            const uint4& qq = ch.q[t][blk];
-            A = ss == 0 ? scaled_a8<DK>(qq.x, qq.y, d2, m2) : scaled_a8<DK>(qq.z, qq.w, d2, m2);
-          }
-          acc[t] = mfma16<F16>(A, B[s], acc[t]);
-        }
-      }
-    }
-  };
-  auto next_quad = [&]() {
-    if constexpr (QS) {
-#pragma unroll
-      for (int t = 0; t < TPW; t++) {
-        sq[t] = sqn[t];
-        if constexpr (dk_has_min(DK)) mq[t] = mqn[t];
-      }
-    }
-  };
-
-  // Steady state: unconditional loads (hipcc keeps exact counted vmcnt
-  // waits); the last < 2*PF chunks run a guarded tail.
-  const int c1u = __builtin_amdgcn_readfirstlane(c1);
-  int c = __builtin_amdgcn_readfirstlane(c0);
-  for (; c + 2 * PF <= c1u; c += PF) {
-#pragma unroll
-    for (int u = 0; u < PF; u++) {
-      compute_chunk(ring[u], c + u, u);
-      load_chunk(ring[u], c + u + PF);
-      if (QS && u == 0) load_quad(sqn, mqn, c + PF);
-    }
-    next_quad();
-  }
-#pragma unroll
-  for (int u = 0; u < PF; u++) {
-    if (c + u < c1u) compute_chunk(ring[u], c + u, u);
-    load_chunk(ring[u], c + u + PF);
-    if (QS && u == 0) load_quad(sqn, mqn, c + PF);
-  }
-  next_quad();
-  c += PF;
-#pragma unroll
-  for (int u = 0; u < PF; u++)
-    if (c + u < c1u) compute_chunk(ring[u], c + u, u);
-
-  // ---- epilogue: lane holds rows 16*tile + 4g + i, column r16
-  if (r16 >= Mloc) return;
-  const int m = orow_of(r16);
-  if constexpr (EPI == EPI_GLU) {
-    float o[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const float gv = acc[0][i], uv = acc[TPW - 1][i];
-      o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
-    }
-    const int n0 = (tile0 / 2) * 16 + 4 * g;
-    if (n0 < a.N) {
-      uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
-      if (n0 + 3 < a.N) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
-      else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
-    }
-  } else {
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-      const int n0 = (tile0 + t) * 16 + 4 * g;
-      if (tile0 + t >= NT || n0 >= a.N) continue;
-      float o[4] = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
-      if constexpr (EPI == EPI_PARTIAL) {
-        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
-        if (n0 + 3 < a.N && (a.N & 3) == 0) *(float4*)ws = make_float4(o[0], o[1], o[2], o[3]);
-        else for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[i];
-      } else {
-        if (a.bias) {
-#pragma unroll
-          for (int i = 0; i < 4; i++) o[i] += (n0 + i < a.N) ? to_f32<T>(a.bias[n0 + i]) : 0.f;
-        }
-        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
-        if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
-        else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
-      }
-    }
-  }
-}
-
-// launch helper: 150 KiB dynamic LDS allowed once per instantiation
-template <typename K>
-inline void launch4(K kern, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    attr = true;
-  }
-  hipLaunchKernelGGL(kern, grid, dim3(64 * (a.waves ? a.waves : 4)), shmem, st, a);
-}
-
-template <int DK, typename T, bool MOE, bool QS>
-inline void launch4_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
-  if (epi == EPI_STORE) launch4(lowbit_gemv4_kernel<DK, T, EPI_STORE, 1, MOE, QS>, grid, shmem, a, st);
-  else if (epi == EPI_PARTIAL) launch4(lowbit_gemv4_kernel<DK, T, EPI_PARTIAL, 1, MOE, QS>, grid, shmem, a, st);
-  else launch4(lowbit_gemv4_kernel<DK, T, EPI_GLU, 2, MOE, QS>, grid, shmem, a, st);
-}
-
-template <int DK>
-void launch_gemv4_dk(bool bf16, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
-  // quad scale loads need chunk ranges starting at multiples of 4
-  const int cpk = a.cpk > 0 ? a.cpk : (a.KC + (int)grid.y - 1) / (int)grid.y;
-  const bool qs = (a.KC % 4 == 0) && (cpk % 4 == 0);
-  const bool moe = a.moe_off != nullptr;
-  if (moe && epi == EPI_STORE) epi = EPI_PARTIAL;   // grouped launches write slabs or GLU rows
-  if (bf16) {
-    if (moe) { if (qs) launch4_epi<DK, BF16, true, true>(epi, grid, shmem, a, st); else launch4_epi<DK, BF16, true, false>(epi, grid, shmem, a, st); }
-    else if (qs) launch4_epi<DK, BF16, false, true>(epi, grid, shmem, a, st);
-    else launch4_epi<DK, BF16, false, false>(epi, grid, shmem, a, st);
-  } else {
-    if (moe) { if (qs) launch4_epi<DK, F16, true, true>(epi, grid, shmem, a, st); else launch4_epi<DK, F16, true, false>(epi, grid, shmem, a, st); }
-    else if (qs) launch4_epi<DK, F16, false, true>(epi, grid, shmem, a, st);
-    else launch4_epi<DK, F16, false, false>(epi, grid, shmem, a, st);
-  }
-}
+namespace illm {
 
 template <int DK, typename T, int MT>
 inline void launch_gemv_t(int epi, dim3 grid, const GemvArgs& a, hipStream_t st) {

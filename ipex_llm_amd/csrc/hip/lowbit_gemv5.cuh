@@ -1,0 +1,469 @@
+// v5 low-bit GEMV for M <= 16 rows: the decode hot path (xe_linear.forward_new
+// / xe_batch.batch_forward / xe_linear.mlp_forward_xpu at batch <= 16,
+// SRC/transformers/low_bit_linear.py:698-708, models/common.py:146-161; the
+// FlashMoE decode GEMV moe_forward_vec, models/qwen3_moe.py:88-105).
+//
+// Why v5 (measured on MI355X with rocprofv3 PMC, gate_up 28672x4096 M=1):
+// the v4 kernel issued 24 VALU per MFMA (scale/offset applied to every
+// decoded weight with packed f16 ops, per-k-step exec-masked LDS reads) and
+// ran ~1 wave per SIMD, so it was VALU- and latency-bound at 3.0-3.5 TB/s.
+// v5 keeps the weights as raw codes in the MFMA A operand and moves all
+// per-block arithmetic to the accumulator side:
+//   * A fragment = raw code value (int4: bf16 0x4300|q = 128+q / f16
+//     0x6400|q = 1024+q via ONE v_and_or_b32 per packed pair; fp4 / fp8 via
+//     the gfx950 v_cvt_scalef32_pk_* converters; nf4/nf3 via an LDS pair
+//     table in f16), exact in the MFMA input type;
+//   * each 64-element block accumulates into a fresh 4-float P, then per
+//     row i: acc += d_i * (P_i - OFF * sx_blk) (+ min_i * sx_blk for asym),
+//     where sx_blk = sum of the block's activations, computed ONCE per
+//     workgroup while x is staged in LDS (no per-element subtract, no
+//     all-ones MFMA): ~11 VALU per k-step instead of ~25;
+//   * unused MFMA columns (m >= M) read a clamped valid row: D's column j
+//     depends only on B's column j, so no masking is needed;
+//   * KW waves of a workgroup split the chunk range of the same tile(s)
+//     and reduce through LDS, so the grid reaches 3-4 waves per SIMD
+//     without split-K slabs (the GLU cannot split K across workgroups);
+//   * scales are stored chunk-major (formats.h): one 16-B load gives the 4
+//     C-fragment rows' (blk0, blk1) scales of a chunk.
+#pragma once
+#include <type_traits>
+
+#include "../common/quant_block.h"
+#include "gemv_args.h"
+#include "illm_device.h"
+
+namespace illm {
+
+// packed-pair nibble extract (x & m) | c as ONE v_and_or_b32: hipcc splits
+// the pattern into v_and + v_or (gfx9 VOP3 takes no literal and one
+// constant-bus read), so the mask is an SGPR and the magic a VGPR operand
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m_s, uint32_t c_v) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(m_s), "v"(c_v));
+  return r;
+}
+
+template <typename C> struct Raw;
+template <> struct Raw<BF16> {
+  static constexpr uint32_t k4 = 0x43004300u;   // bf16(128 + q)
+  static constexpr float off4 = 128.f;
+};
+template <> struct Raw<F16> {
+  static constexpr uint32_t k4 = 0x64006400u;   // f16(1024 + q)
+  static constexpr float off4 = 1024.f;
+};
+
+// raw value offset per decoder: value = code_raw - OFF (before scale)
+template <int DK, typename C>
+__host__ __device__ constexpr float raw_off() {
+  return DK == DK_INT4S ? Raw<C>::off4 + 8.f
+       : DK == DK_INT4A ? Raw<C>::off4
+       : DK == DK_INT8S ? 128.f
+       : 0.f;
+}
+
+template <int DK, typename C>
+__device__ __forceinline__ uint4 raw_a4(uint32_t u, uint32_t mask_s, uint32_t magic_v, const uint32_t* lut2) {
+  uint4 r;
+  if constexpr (DK == DK_INT4S || DK == DK_INT4A) {
+    r.x = and_or(u, mask_s, magic_v);
+    r.y = and_or(u >> 4, mask_s, magic_v);
+    r.z = and_or(u >> 8, mask_s, magic_v);
+    r.w = and_or(u >> 12, mask_s, magic_v);
+  } else if constexpr (DK == DK_FP4) {
+    if constexpr (std::is_same<C, BF16>::value) {
+      r.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(u, 1.0f, 0));
+      r.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(u, 1.0f, 1));
+      r.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(u, 1.0f, 2));
+      r.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp4(u, 1.0f, 3));
+    } else {
+      r.x = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 0));
+      r.y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 1));
+      r.z = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 2));
+      r.w = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 3));
+    }
+  } else {  // DK_LUT4 (C = F16 pair table)
+    r.x = lut2[u & 0xff];
+    r.y = lut2[(u >> 8) & 0xff];
+    r.z = lut2[(u >> 16) & 0xff];
+    r.w = lut2[u >> 24];
+  }
+  return r;
+}
+
+template <int DK, typename C>
+__device__ __forceinline__ uint32_t raw_pair8(uint32_t u, bool hi) {
+  if constexpr (DK == DK_FP8E4) {
+    if constexpr (std::is_same<C, BF16>::value)
+      return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(u, 1.0f, true)
+                                             : __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(u, 1.0f, false));
+    else
+      return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(u, 1.0f, true)
+                                             : __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(u, 1.0f, false));
+  } else if constexpr (DK == DK_FP8E5) {
+    if constexpr (std::is_same<C, BF16>::value)
+      return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(u, 1.0f, true)
+                                             : __builtin_amdgcn_cvt_scalef32_pk_bf16_bf8(u, 1.0f, false));
+    else
+      return __builtin_bit_cast(uint32_t, hi ? __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(u, 1.0f, true)
+                                             : __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(u, 1.0f, false));
+  } else {
+    // integer bytes through the exact small-integer float conversion;
+    // signed codes are biased by 128 (raw_off = 128)
+    if constexpr (DK == DK_INT8S) u ^= 0x80808080u;
+    const int sh = hi ? 16 : 0;
+    return pack2<C>((float)((u >> sh) & 0xff), (float)((u >> (sh + 8)) & 0xff));
+  }
+}
+
+template <int DK, typename C>
+__device__ __forceinline__ uint4 raw_a8(uint32_t lo, uint32_t hi) {
+  return make_uint4(raw_pair8<DK, C>(lo, false), raw_pair8<DK, C>(lo, true), raw_pair8<DK, C>(hi, false),
+                    raw_pair8<DK, C>(hi, true));
+}
+
+// LDS plan of one workgroup (bytes): x slice [rows][kw + 8] in C, then per
+// (row, chunk) float4 {-OFF*sx0, -OFF*sx1, sx0, sx1}, then the KW reduction
+// area [4 waves][2 tiles][64] float4.
+__host__ __device__ constexpr int gemv5_x_ld(int kw) { return kw + 8; }
+__host__ __device__ constexpr size_t gemv5_shmem(int rows, int cpk) {
+  return ((size_t)rows * gemv5_x_ld(cpk * 128) * 2 + 15) / 16 * 16 + (size_t)rows * cpk * 16 + 4 * 2 * 64 * 16;
+}
+
+template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int PF>
+__global__ void __launch_bounds__(256) lowbit_gemv5_kernel(const GemvArgs a) {
+  using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;   // MFMA input type
+  constexpr int BITS = dk_bits(DK);
+  constexpr int TG = 4 / KW;           // tile groups per workgroup
+  constexpr float OFF = raw_off<DK, C>();
+  constexpr bool HASMIN = dk_has_min(DK);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  int Mloc = a.M;
+  const uint8_t* wbase = a.w;
+  const int32_t* prow = nullptr;
+  if constexpr (MOE) {
+    const int e = blockIdx.z;
+    const int m0 = a.moe_off[e];
+    Mloc = min(16, a.moe_off[e + 1] - m0);
+    if (Mloc <= 0) return;                // expert not routed to: the whole block exits
+    wbase += (size_t)e * a.w_stride;
+    prow = a.moe_rows + m0;
+  }
+  auto xrow_of = [&](int m) -> int { if constexpr (MOE) return prow[m] / a.moe_xdiv; else return m; };
+  auto orow_of = [&](int m) -> int { if constexpr (MOE) return prow[m]; else return m; };
+
+  const int nks = gridDim.y;
+  const int cpk = a.cpk > 0 ? a.cpk : (a.KC + nks - 1) / nks;
+  const int c0 = blockIdx.y * cpk;
+  const int c1 = min(a.KC, c0 + cpk);
+  const int kbase = c0 * 128;
+  const int kw = (c1 - c0) * 128;
+  const int ldx = gemv5_x_ld(kw);
+  uint16_t* xs = (uint16_t*)smem;
+  float4* sxs = (float4*)(smem + ((size_t)Mloc * ldx * 2 + 15) / 16 * 16);        // [Mloc][c1-c0]
+  float4* red = (float4*)((uint8_t*)sxs + (size_t)Mloc * (c1 - c0) * 16);          // [4][TPW][64]
+
+  const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
+  const int tg = wave / KW, kp = wave % KW;
+  const int tile0 = (blockIdx.x * TG + tg) * TPW;
+  const int per = (c1 - c0 + KW - 1) / KW;
+  const int wc0 = c0 + kp * per;
+  const int wc1 = min(c1, wc0 + per);
+  const bool wave_on = tile0 < NT && wc0 < wc1;
+  const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
+  const size_t soff = (size_t)a.KC * dk_code_chunk(DK) + (size_t)g * 16;   // + c * 64: rows 4g..4g+3
+  const size_t moff = soff + (size_t)16 * a.KC * 4;
+  const uint8_t* tb[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; t++) tb[t] = wbase + (size_t)min(tile0 + t, NT - 1) * TB;
+
+  struct Chunk {
+    uint4 q[TPW][BITS / 4];
+    uint4 sc[TPW];
+    uint4 mn[TPW];
+  };
+  auto load_chunk = [&](Chunk& ch, int c) {
+    c = min(c, wc1 - 1);
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      const uint8_t* rec = tb[t] + (size_t)c * dk_code_chunk(DK);
+      ch.q[t][0] = *(const uint4*)(rec + lane * 16);
+      if constexpr (BITS == 8) ch.q[t][1] = *(const uint4*)(rec + 1024 + lane * 16);
+      ch.sc[t] = *(const uint4*)(tb[t] + soff + (size_t)c * 64);
+      if constexpr (HASMIN) ch.mn[t] = *(const uint4*)(tb[t] + moff + (size_t)c * 64);
+    }
+  };
+  Chunk ring[PF];
+  if (wave_on) {
+#pragma unroll
+    for (int u = 0; u < PF; u++) load_chunk(ring[u], wc0 + u);
+  }
+  if constexpr (DK == DK_LUT4) {
+    lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
+  }
+
+  // ---- stage x[0:Mloc, kbase:kbase+kw] -> LDS in C
+  {
+    const int vpr = kw / 8;
+    for (int v = threadIdx.x; v < Mloc * vpr; v += 256) {
+      const int m = v / vpr, kk = (v % vpr) * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (kbase + kk < a.K && a.xpart) {
+        // fused activation input: x = act(gate) * up from the gate/up GEMV's split-K slabs
+        const int k0 = kbase + kk;
+        const size_t gc = (size_t)(k0 >> 4) * 32 + (k0 & 15);
+        const size_t ld = (size_t)2 * a.K;
+        float gv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, uv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int sp = 0; sp < a.xpart_ns; sp++) {
+          const float* row = a.xpart + ((size_t)sp * a.M + xrow_of(m)) * ld;
+          const float4 g0 = *(const float4*)(row + gc), g1 = *(const float4*)(row + gc + 4);
+          const float4 u0 = *(const float4*)(row + gc + 16), u1 = *(const float4*)(row + gc + 20);
+          gv[0] += g0.x; gv[1] += g0.y; gv[2] += g0.z; gv[3] += g0.w;
+          gv[4] += g1.x; gv[5] += g1.y; gv[6] += g1.z; gv[7] += g1.w;
+          uv[0] += u0.x; uv[1] += u0.y; uv[2] += u0.z; uv[3] += u0.w;
+          uv[4] += u1.x; uv[5] += u1.y; uv[6] += u1.z; uv[7] += u1.w;
+        }
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          float o2[2];
+#pragma unroll
+          for (int j = 0; j < 2; j++) {
+            const float gg = gv[2 * i + j];
+            // rounded to T: what the GLU epilogue would have written
+            float act = to_f32<T>(from_f32<T>((a.act == 0 ? silu_f(gg) : gelu_tanh_f(gg)) * uv[2 * i + j]));
+            if constexpr (std::is_same<C, F16>::value) act = fminf(fmaxf(act, -65504.f), 65504.f);
+            o2[j] = act;
+          }
+          w[i] = pack2<C>(o2[0], o2[1]);
+        }
+        val = make_uint4(w[0], w[1], w[2], w[3]);
+      } else if (kbase + kk < a.K) {
+        val = *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk);
+        if constexpr (!std::is_same<C, T>::value) {   // bf16 activations -> f16 (LUT formats)
+          uint32_t w[4] = {val.x, val.y, val.z, val.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const float lo = fminf(fmaxf(bf16_to_f32(w[i] & 0xffff), -65504.f), 65504.f);
+            const float hi = fminf(fmaxf(bf16_to_f32(w[i] >> 16), -65504.f), 65504.f);
+            w[i] = pack2<F16>(lo, hi);
+          }
+          val = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+      *(uint4*)(xs + m * ldx + kk) = val;
+    }
+  }
+  __syncthreads();
+  // ---- per (row, chunk): block sums of the staged activations
+  {
+    const int nch = c1 - c0;
+    for (int v = threadIdx.x; v < Mloc * nch * 2; v += 256) {
+      const int m = v / (nch * 2), rem = v % (nch * 2);
+      const uint16_t* p = xs + m * ldx + rem * 64;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint4 q = *(const uint4*)(p + 8 * j);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) s += to_f32<C>(w[i] & 0xffff) + to_f32<C>(w[i] >> 16);
+      }
+      float* rec = (float*)(sxs + m * nch + (rem >> 1));
+      rec[rem & 1] = -OFF * s;
+      rec[2 + (rem & 1)] = s;
+    }
+  }
+  __syncthreads();
+
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (wave_on) {
+    const int mrow = min(r16, Mloc - 1);          // unused columns read a valid row (no masking)
+    const uint16_t* xrow = xs + mrow * ldx + 8 * g;
+    const float4* srow = sxs + mrow * (c1 - c0);
+    const uint32_t mask_s = a.nib_mask, magic_v = a.nib_magic;
+
+    auto compute_chunk = [&](const Chunk& ch, int c) {
+      const uint16_t* xc = xrow + (c - c0) * 128;
+      uint4 B[4];
+#pragma unroll
+      for (int s = 0; s < 4; s++) B[s] = *(const uint4*)(xc + 32 * s);
+      const float4 sx = srow[c - c0];
+#pragma unroll
+      for (int t = 0; t < TPW; t++) {
+#pragma unroll
+        for (int blk = 0; blk < 2; blk++) {
+          f32x4 P = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ss = 0; ss < 2; ss++) {
+            const int s = blk * 2 + ss;
+            uint4 A;
+            if constexpr (BITS == 4) {
+              const uint4& q0 = ch.q[t][0];
+              const uint32_t w = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
+              A = raw_a4<DK, C>(w, mask_s, magic_v, lut2);
+            } else {
+              const uint4& qq = ch.q[t][blk];
+              A = ss == 0 ? raw_a8<DK, C>(qq.x, qq.y) : raw_a8<DK, C>(qq.z, qq.w);
+            }
+            P = mfma16<C>(A, B[s], P);
+          }
+          const float nsx = blk == 0 ? sx.x : sx.y;
+          const float sxv = blk == 0 ? sx.z : sx.w;
+          const uint32_t scw[4] = {ch.sc[t].x, ch.sc[t].y, ch.sc[t].z, ch.sc[t].w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const float d = f16_to_f32((uint16_t)(scw[i] >> (16 * blk)));
+            if constexpr (OFF != 0.f) acc[t][i] = __builtin_fmaf(d, P[i] + nsx, acc[t][i]);
+            else acc[t][i] = __builtin_fmaf(d, P[i], acc[t][i]);
+            if constexpr (HASMIN) {
+              const uint32_t mnw[4] = {ch.mn[t].x, ch.mn[t].y, ch.mn[t].z, ch.mn[t].w};
+              acc[t][i] = __builtin_fmaf(f16_to_f32((uint16_t)(mnw[i] >> (16 * blk))), sxv, acc[t][i]);
+            }
+          }
+        }
+      }
+    };
+
+    // steady state: unconditional clamped loads (hipcc keeps counted vmcnt)
+    const int c1u = __builtin_amdgcn_readfirstlane(wc1);
+    int c = __builtin_amdgcn_readfirstlane(wc0);
+    for (; c + 2 * PF <= c1u; c += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; u++) {
+        compute_chunk(ring[u], c + u);
+        load_chunk(ring[u], c + u + PF);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PF; u++) {
+      if (c + u < c1u) compute_chunk(ring[u], c + u);
+      load_chunk(ring[u], c + u + PF);
+    }
+    c += PF;
+#pragma unroll
+    for (int u = 0; u < PF; u++)
+      if (c + u < c1u) compute_chunk(ring[u], c + u);
+  }
+
+  // ---- reduce the KW k-parts of each tile group through LDS
+  if constexpr (KW > 1) {
+#pragma unroll
+    for (int t = 0; t < TPW; t++)
+      red[(wave * TPW + t) * 64 + lane] = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+    __syncthreads();
+    if (kp != 0) return;
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+#pragma unroll
+      for (int j = 1; j < KW; j++) {
+        const float4 v = red[((wave + j) * TPW + t) * 64 + lane];
+        acc[t][0] += v.x; acc[t][1] += v.y; acc[t][2] += v.z; acc[t][3] += v.w;
+      }
+    }
+  }
+  if (tile0 >= NT) return;
+
+  // ---- epilogue: lane holds rows 16*tile + 4g + i, column r16
+  if (r16 >= Mloc) return;
+  const int m = orow_of(r16);
+  if constexpr (EPI == EPI_GLU) {
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const float gv = acc[0][i], uv = acc[TPW - 1][i];
+      o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
+    }
+    const int n0 = (tile0 / 2) * 16 + 4 * g;
+    if (n0 < a.N) {
+      uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+      if (n0 + 3 < a.N) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+      else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      const int n0 = (tile0 + t) * 16 + 4 * g;
+      if (tile0 + t >= NT || n0 >= a.N) continue;
+      float o[4] = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
+      if constexpr (EPI == EPI_ATOMIC) {
+        float* ws = (float*)a.out + (size_t)m * a.N + n0;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (n0 + i < a.N) __hip_atomic_fetch_add(ws + i, o[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if constexpr (EPI == EPI_PARTIAL) {
+        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
+        if (n0 + 3 < a.N && (a.N & 3) == 0) *(float4*)ws = make_float4(o[0], o[1], o[2], o[3]);
+        else for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[i];
+      } else {
+        if (a.bias) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) o[i] += (n0 + i < a.N) ? to_f32<T>(a.bias[n0 + i]) : 0.f;
+        }
+        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
+        if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+        else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+      }
+    }
+  }
+}
+
+// launch helper: up to 159 KiB of dynamic LDS, attribute set once per instantiation
+template <typename K>
+inline void launch5(K kern, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(256), shmem, st, a);
+}
+
+template <int DK, typename T, int KW, bool MOE, int PF>
+inline void launch5_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  if (epi == EPI_STORE) launch5(lowbit_gemv5_kernel<DK, T, EPI_STORE, 1, KW, MOE, PF>, grid, shmem, a, st);
+  else if (epi == EPI_PARTIAL) launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, PF>, grid, shmem, a, st);
+  else if (epi == EPI_ATOMIC) launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, PF>, grid, shmem, a, st);
+  else launch5(lowbit_gemv5_kernel<DK, T, EPI_GLU, 2, KW, MOE, PF>, grid, shmem, a, st);
+}
+
+template <int DK, typename T, bool MOE>
+inline void launch5_kw(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a0, hipStream_t st) {
+  using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;
+  GemvArgs a = a0;
+  a.nib_mask = 0x000F000Fu;
+  a.nib_magic = Raw<C>::k4;
+  // prefetch depth: chunks in flight per wave (a.pf; 8 when a wave's range is short)
+  if (a.pf == 8) {
+    if (kw == 1) launch5_epi<DK, T, 1, MOE, 8>(epi, grid, shmem, a, st);
+    else if (kw == 2) launch5_epi<DK, T, 2, MOE, 8>(epi, grid, shmem, a, st);
+    else launch5_epi<DK, T, 4, MOE, 8>(epi, grid, shmem, a, st);
+  } else {
+    if (kw == 1) launch5_epi<DK, T, 1, MOE, 4>(epi, grid, shmem, a, st);
+    else if (kw == 2) launch5_epi<DK, T, 2, MOE, 4>(epi, grid, shmem, a, st);
+    else launch5_epi<DK, T, 4, MOE, 4>(epi, grid, shmem, a, st);
+  }
+}
+
+// grid.x = workgroups of (4 / kw) tile groups (GLU: tile pairs), grid.y = split-K
+template <int DK>
+void launch_gemv5_dk(bool bf16, int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  const bool moe = a.moe_off != nullptr;
+  if (moe && epi == EPI_STORE) epi = EPI_PARTIAL;   // grouped launches write slabs or GLU rows
+  if (bf16) {
+    if (moe) launch5_kw<DK, BF16, true>(kw, epi, grid, shmem, a, st);
+    else launch5_kw<DK, BF16, false>(kw, epi, grid, shmem, a, st);
+  } else {
+    if (moe) launch5_kw<DK, F16, true>(kw, epi, grid, shmem, a, st);
+    else launch5_kw<DK, F16, false>(kw, epi, grid, shmem, a, st);
+  }
+}
+
+}  // namespace illm

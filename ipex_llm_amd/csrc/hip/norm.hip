@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(NORM_THREADS)
     add_rms_norm_kernel(const uint16_t* __restrict__ x, const float* __restrict__ partials,
                         int nsplit, uint16_t* __restrict__ residual, const uint16_t* __restrict__ w,
                         uint16_t* __restrict__ out, int H, float eps, int unit_offset,
-                        int store_residual) {
+                        int store_residual, int zero_partials) {
   __shared__ float red[NORM_THREADS / 64];
   const int row = blockIdx.x;
   const int M = gridDim.x;
@@ -61,6 +61,11 @@ __global__ void __launch_bounds__(NORM_THREADS)
           a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
         }
         for (int i = 0; i < 8; i++) a[i] = rnd<T>(a[i]);
+        if (zero_partials) {
+          float* z = (float*)partials + (size_t)row * H + c;
+          ((float4*)z)[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+          ((float4*)z)[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       } else {
         load8<T>(x + (size_t)row * H + c, a);
       }
@@ -141,7 +146,7 @@ static void launch_add_rms(const NormArgs& a, hipStream_t st) {
 #define L_RMS(MV)                                                                             \
   hipLaunchKernelGGL((add_rms_norm_kernel<T, MV>), dim3(a.M), dim3(NORM_THREADS), 0, st, a.x, \
                      a.partials, a.nsplit, a.residual, a.w, a.out, a.H, a.eps, a.unit_offset,  \
-                     a.store_residual)
+                     a.store_residual, a.zero_partials)
   if (nv <= 1) L_RMS(1);
   else if (nv <= 2) L_RMS(2);
   else if (nv <= 4) L_RMS(4);

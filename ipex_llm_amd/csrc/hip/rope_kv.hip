@@ -74,7 +74,11 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
       const int64_t pp = a.pos[t] - (a.pos_offset ? a.pos_offset[t / a.tq] : 0);
       slot = (int64_t)a.block_tables[(size_t)(t / a.tq) * a.max_blocks + pp / a.bs] * a.bs + pp % a.bs;
     }
-    if (slot < 0) return;
+    if (slot < 0) {   // padding token: nothing to write, but keep the accumulator zeroed
+      if (a.part && a.zero_part)
+        for (int d = lane; d < D; d += 64) ((float*)a.part)[(size_t)t * a.ld_qkv + col0 + d] = 0.f;
+      return;
+    }
     cache = is_k ? a.k_cache : a.v_cache;
     cscale = is_k ? a.k_scale : a.v_scale;
   }
@@ -110,6 +114,10 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
     for (int d = a.rot_dim + lane; d < D; d += 64) put(d, val(d));
   } else {
     for (int d = lane; d < D; d += 64) put(d, raw(d));
+  }
+  if (a.part && a.zero_part) {
+    // every read of this head's columns above was made by this wave
+    for (int d = lane; d < D; d += 64) ((float*)a.part)[(size_t)t * a.ld_qkv + col0 + d] = 0.f;
   }
 }
 

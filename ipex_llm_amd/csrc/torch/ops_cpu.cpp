@@ -111,7 +111,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("quantize_device(Tensor w, int fmt, bool scale_search) -> Tensor");
   m.def("dequantize_device(Tensor blob, int fmt, int n, int k, ScalarType dtype) -> Tensor");
   m.def("gemv(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias, int epi, int ksplit, int act) -> Tensor");
-  m.def("add_rms_norm(Tensor? x, Tensor? partials, Tensor(a!)? residual, Tensor w, float eps, bool unit_offset, bool store_residual) -> Tensor");
+  m.def("add_rms_norm(Tensor? x, Tensor(b!)? partials, Tensor(a!)? residual, Tensor w, float eps, bool unit_offset, bool store_residual, bool zero_partials=False) -> Tensor");
   m.def("layer_norm(Tensor x, Tensor? w, Tensor? b, float eps) -> Tensor");
   m.def("rope_kv(Tensor qkv, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slots, Tensor pos, Tensor inv_freq, Tensor? q_norm, Tensor? k_norm, float norm_eps, float q_scale, int Hq, int Hkv, int D, int rot_dim, bool interleaved, int kv_fp8, float k_scale, float v_scale) -> ()");
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int kv_fp8, float k_scale, float v_scale, Tensor? alibi) -> Tensor");
@@ -121,7 +121,8 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("moe_align(Tensor ids, int e0, int num_local) -> (Tensor, Tensor)");
   m.def("gemv_glu_in(Tensor part, Tensor blob, int fmt, int n, int k, int act, int ksplit, ScalarType dtype) -> Tensor");
   m.def("decode_advance(Tensor? logits, Tensor(a!) ids, Tensor(b!) next_ids, Tensor(c!) pos, Tensor block_tables, int bs, Tensor(d!) slots, Tensor(e!) seq_lens, Tensor? pos_offset=None) -> ()");
-  m.def("rope_kv_fused(Tensor part, Tensor? bias, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor pos, Tensor block_tables, int tq, Tensor inv_freq, Tensor? q_norm, Tensor? k_norm, float norm_eps, float q_scale, int Hq, int Hkv, int D, int rot_dim, bool interleaved, int kv_fp8, float k_scale, float v_scale, Tensor? pos_offset=None) -> ()");
+  m.def("rope_kv_fused(Tensor(d!) part, Tensor? bias, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor pos, Tensor block_tables, int tq, Tensor inv_freq, Tensor? q_norm, Tensor? k_norm, float norm_eps, float q_scale, int Hq, int Hkv, int D, int rot_dim, bool interleaved, int kv_fp8, float k_scale, float v_scale, Tensor? pos_offset=None, bool zero_part=False) -> ()");
+  m.def("gemv_accum(Tensor x, Tensor blob, int fmt, int n, int k, Tensor(a!) acc, int ksplit) -> ()");
   m.def("embedding_lowbit(Tensor blob, int fmt, int n, int k, Tensor ids, ScalarType dtype) -> Tensor");
   m.def("moe_gemv(Tensor x, Tensor blob, int fmt, int n, int k, Tensor off, Tensor rows, int xdiv, int npairs, int epi, int ksplit, int act) -> Tensor");
   m.def("moe_combine(Tensor part, Tensor w, Tensor ids, int e0, int num_local, ScalarType dtype) -> Tensor");

@@ -69,12 +69,12 @@ void launch_gemv_any(int fmt, bool bf16, int mt, int epi, dim3 grid, const illm:
   hipStream_t st = cur_stream();
   ILLM_DK_SWITCH(fmt, illm::launch_gemv_dk<DKV>(bf16, mt, epi, grid, a, st));
 }
-void launch_gemv4_any(int fmt, bool bf16, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a) {
+void launch_gemv5_any(int fmt, bool bf16, int kw, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a) {
   hipStream_t st = cur_stream();
-  ILLM_DK_SWITCH(fmt, illm::launch_gemv4_dk<DKV>(bf16, epi, grid, shmem, a, st));
+  ILLM_DK_SWITCH(fmt, illm::launch_gemv5_dk<DKV>(bf16, kw, epi, grid, shmem, a, st));
 }
 
-constexpr size_t kMaxLds = 150 * 1024;
+constexpr size_t kMaxLds = 159 * 1024;
 
 // v1 (M > 16): split K over workgroups until there are >= 768 of them
 int64_t auto_ksplit(int64_t NT, int64_t KC) {
@@ -83,15 +83,48 @@ int64_t auto_ksplit(int64_t NT, int64_t KC) {
   return ks;
 }
 
-// v4 geometry: workgroups = 4 waves x TPW tiles; split K so that there are
-// >= ~320 workgroups while each wave keeps >= 4 chunks, and the LDS x slice
-// (M * Kwg * 2 B) stays <= 64 KiB (occupancy: >= 2 workgroups per CU).
-int64_t v4_ksplit(int64_t M, int64_t NT, int64_t KC, int tpw, int waves = 4) {
-  const int64_t wgs = (NT + waves * tpw - 1) / (waves * tpw) * waves / 4;   // in 4-wave units
-  int64_t ks = 1;
-  auto lds = [&](int64_t k) { return M * (((KC + k - 1) / k) * 128 + 8) * 2; };
-  while ((wgs * ks < 320 && KC / (ks * 2) >= 4) || (lds(ks) > 65536 && ks < KC)) ks *= 2;
-  return ks;
+// v5 geometry (M <= 16): each of `groups` tile groups (a tile, or a gate/up
+// tile pair for GLU) is streamed by kw waves of one workgroup (in-LDS
+// reduction) and, when allowed, by ks workgroups (f32 split-K slabs).
+// Measured on MI355X (tools/gemv_sweep5.sh, Llama-3-8B shapes): the x slice
+// is staged once per workgroup, so kw > 1 (fewer tiles per workgroup) only
+// pays for the unsplittable GLU at M <= 2; split-K workgroups of ~8 chunks
+// (M <= 2) / ~4 chunks (M > 2) are fastest for the slab-output projections.
+// ILLM_GEMV5_KW / ILLM_GEMV5_KS / ILLM_GEMV5_PF override (sweeps).
+struct Plan5 {
+  int kw;
+  int64_t ks, cpk;
+  size_t shmem;
+  unsigned gx;
+  int pf;
+};
+Plan5 plan5(int64_t rows, int64_t groups, int64_t KC, bool can_split, int64_t ks_req = 0, bool atomic = false) {
+  static const int kw_env = getenv("ILLM_GEMV5_KW") ? atoi(getenv("ILLM_GEMV5_KW")) : 0;
+  static const int ks_env = getenv("ILLM_GEMV5_KS") ? atoi(getenv("ILLM_GEMV5_KS")) : 0;
+  static const int pf_env = getenv("ILLM_GEMV5_PF") ? atoi(getenv("ILLM_GEMV5_PF")) : 0;
+  Plan5 p{1, 1, KC, 0, 0, 4};
+  if (!can_split) {
+    p.kw = rows <= 2 ? 4 : (rows <= 4 ? 2 : 1);
+    while (p.kw > 1 && KC / p.kw < 4) p.kw /= 2;
+  } else if (ks_req > 0) {
+    p.ks = ks_req;
+  } else {
+    const int64_t target = rows <= 2 ? 8 : 4;
+    p.ks = std::min<int64_t>(atomic ? 32 : 16, std::max<int64_t>(1, (KC + target - 1) / target));
+    // wide outputs (lm_head: 8016 tiles) already fill the chip: slabs only cost
+    while (p.ks > 1 && groups * p.ks > 4096) p.ks /= 2;
+    while (illm::gemv5_shmem_h((int)rows, (int)((KC + p.ks - 1) / p.ks)) > 65536 && p.ks < KC) p.ks *= 2;
+  }
+  if (kw_env) p.kw = kw_env;
+  if (ks_env && can_split) p.ks = ks_env;
+  p.ks = std::max<int64_t>(1, std::min<int64_t>(p.ks, KC));
+  p.cpk = (KC + p.ks - 1) / p.ks;
+  p.ks = (KC + p.cpk - 1) / p.cpk;
+  p.shmem = illm::gemv5_shmem_h((int)rows, (int)p.cpk);
+  p.pf = pf_env ? pf_env : 4;
+  const int64_t per_wg = 4 / p.kw;
+  p.gx = (unsigned)((groups + per_wg - 1) / per_wg);
+  return p;
 }
 
 Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k,
@@ -107,7 +140,7 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
   const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
-  // M <= 16 runs v4 (ILLM_GEMV_V1=1 forces the general kernel, for A/B tests)
+  // M <= 16 runs v5 (ILLM_GEMV_V1=1 forces the general kernel, for A/B tests)
   const bool small = M <= 16 && getenv("ILLM_GEMV_V1") == nullptr;
 
   illm::GemvArgs a{};
@@ -120,12 +153,6 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   a.act = (int)act;
   a.lut_fmt = (int)fmt;
   a.bias = nullptr;
-  // v4 workgroup size: 8 waves share one LDS copy of x (halves x traffic per tile)
-  static const int waves_env = getenv("ILLM_GEMV_WAVES") ? atoi(getenv("ILLM_GEMV_WAVES")) : 0;
-  // GLU keeps 4-wave groups: it cannot split K, and 8-wave groups halve its grid
-  const int W = waves_env ? waves_env : ((M > 2 && epi != illm::EPI_GLU) ? 8 : 4);
-  a.waves = W;
-
   auto out_shape = xc.sizes().vec();
   if (epi == illm::EPI_GLU) {
     TORCH_CHECK(n % 32 == 0, "GLU weights must have a multiple of 32 rows");
@@ -134,26 +161,30 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
     a.N = (int)(n / 2);
     a.out = out.data_ptr();
     a.ldo = (int)(n / 2);
-    const size_t shmem = (size_t)M * (KC * 128 + 8) * 2;
-    if (small && shmem <= kMaxLds)
-      launch_gemv4_any((int)fmt, bf16, illm::EPI_GLU, dim3((unsigned)((NT + 2 * W - 1) / (2 * W)), 1), shmem, a);
+    const Plan5 p = plan5(M, NT / 2, KC, false);
+    if (small && p.shmem <= kMaxLds)
+      a.pf = p.pf, launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_GLU, dim3(p.gx, 1), p.shmem, a);
     else
       launch_gemv_any((int)fmt, bf16, mt, illm::EPI_GLU, dim3((unsigned)(NT / 2), 1), a);
     return out;
   }
   a.N = (int)n;
-  if (ksplit <= 0) ksplit = small ? v4_ksplit(M, NT, KC, 1, W) : auto_ksplit(NT, KC);
-  ksplit = std::min<int64_t>(ksplit, KC);
-  int64_t cpk = (KC + ksplit - 1) / ksplit;
-  if (small && KC % 4 == 0) {          // v4: slices start at multiples of 4 chunks (quad scale loads)
-    cpk = (cpk + 3) / 4 * 4;
-    ksplit = (KC + cpk - 1) / cpk;
-    a.cpk = (int)cpk;
+  Plan5 p5{};
+  bool use5 = false;
+  if (small) {
+    p5 = plan5(M, NT, KC, true, ksplit);
+    use5 = p5.shmem <= kMaxLds;
   }
-  const size_t shmem = (size_t)M * (cpk * 128 + 8) * 2;
-  const bool use4 = small && shmem <= kMaxLds;
+  if (use5) {
+    ksplit = p5.ks;
+    a.cpk = (int)p5.cpk;
+    a.pf = p5.pf;
+  } else {
+    if (ksplit <= 0) ksplit = auto_ksplit(NT, KC);
+    ksplit = std::min<int64_t>(ksplit, KC);
+  }
   auto launch = [&](int e) {
-    if (use4) launch_gemv4_any((int)fmt, bf16, e, dim3((unsigned)((NT + W - 1) / W), (unsigned)ksplit), shmem, a);
+    if (use5) launch_gemv5_any((int)fmt, bf16, p5.kw, e, dim3(p5.gx, (unsigned)ksplit), p5.shmem, a);
     else launch_gemv_any((int)fmt, bf16, mt, e, dim3((unsigned)NT, (unsigned)ksplit), a);
   };
   if (epi == illm::EPI_PARTIAL || ksplit > 1) {
@@ -177,6 +208,40 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   return out;
 }
 
+// split-K GEMV accumulated with f32 atomics into acc [M, n] (zero on entry;
+// the consumer -- add_rms_norm / rope_kv_fused with zero_*=True -- reads the
+// single slab and re-zeroes it, so no ks-slab reduction is ever needed)
+void gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, Tensor& acc,
+                int64_t ksplit) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda() && acc.is_cuda(), "gemv_accum: GPU tensors expected");
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  const int64_t M = xc.numel() / k;
+  TORCH_CHECK(M >= 1 && M <= 16, "gemv_accum handles 1..16 rows, got ", M);
+  TORCH_CHECK(acc.scalar_type() == at::kFloat && acc.is_contiguous() && acc.numel() == M * n,
+              "gemv_accum: acc must be contiguous f32 [M, n]");
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemv_accum: weight blob too small");
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  illm::GemvArgs a{};
+  a.x = p16(xc);
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.KC = (int)KC;
+  a.lut_fmt = (int)fmt;
+  a.N = (int)n;
+  a.out = acc.data_ptr();
+  a.ldo = (int)n;
+  const Plan5 p = plan5(M, NT, KC, true, ksplit, true);
+  a.cpk = (int)p.cpk;
+  a.pf = p.pf;
+  TORCH_CHECK(p.shmem <= kMaxLds, "gemv_accum: K slice too large for LDS");
+  launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_ATOMIC, dim3(p.gx, (unsigned)p.ks), p.shmem, a);
+}
+
 // down-projection GEMV whose input is act(gate) * up computed on the fly from
 // the gate/up GEMV's split-K slabs (saves the GLU epilogue's unsplittable
 // launch and one [M, I] round trip); returns f32 partial slabs [ks, M, n].
@@ -193,7 +258,6 @@ Tensor gemv_glu_in(const Tensor& part, const Tensor& blob, int64_t fmt, int64_t 
   TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemv_glu_in: weight blob too small");
   const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
   const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
-  const int W = M > 2 ? 8 : 4;
   illm::GemvArgs a{};
   a.x = nullptr;
   a.xpart = part.data_ptr<float>();
@@ -205,26 +269,22 @@ Tensor gemv_glu_in(const Tensor& part, const Tensor& blob, int64_t fmt, int64_t 
   a.KC = (int)KC;
   a.act = (int)act;
   a.lut_fmt = (int)fmt;
-  a.waves = W;
   a.N = (int)n;
-  if (ksplit <= 0) ksplit = v4_ksplit(M, NT, KC, 1, W);
-  ksplit = std::min<int64_t>(ksplit, KC);
-  int64_t cpk = (KC + ksplit - 1) / ksplit;
-  if (KC % 4 == 0) cpk = (cpk + 3) / 4 * 4;
-  ksplit = (KC + cpk - 1) / cpk;
-  a.cpk = (int)cpk;
-  const size_t shmem = (size_t)M * (cpk * 128 + 8) * 2;
-  TORCH_CHECK(shmem <= kMaxLds, "gemv_glu_in: K slice too large for LDS");
+  const Plan5 p = plan5(M, NT, KC, true, ksplit);
+  ksplit = p.ks;
+  a.cpk = (int)p.cpk;
+  a.pf = p.pf;
+  TORCH_CHECK(p.shmem <= kMaxLds, "gemv_glu_in: K slice too large for LDS");
   Tensor ws = at::empty({ksplit, M, n}, part.options());
   a.out = ws.data_ptr();
   a.ldo = (int)n;
-  launch_gemv4_any((int)fmt, bf16, illm::EPI_PARTIAL, dim3((unsigned)((NT + W - 1) / W), (unsigned)ksplit), shmem, a);
+  launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_PARTIAL, dim3(p.gx, (unsigned)ksplit), p.shmem, a);
   return ws;
 }
 
 Tensor add_rms_norm(const c10::optional<Tensor>& x, const c10::optional<Tensor>& partials,
                     const c10::optional<Tensor>& residual, const Tensor& w, double eps,
-                    bool unit_offset, bool store_residual) {
+                    bool unit_offset, bool store_residual, bool zero_partials) {
   c10::DeviceGuard g(w.device());
   const bool bf16 = is_bf16(w);
   const int64_t H = w.numel();
@@ -258,6 +318,7 @@ Tensor add_rms_norm(const c10::optional<Tensor>& x, const c10::optional<Tensor>&
   a.eps = (float)eps;
   a.unit_offset = unit_offset;
   a.store_residual = store_residual;
+  a.zero_partials = zero_partials && a.partials != nullptr;
   if (M > 0) illm::launch_add_rms_norm(bf16, a, cur_stream());
   return out;
 }
@@ -336,7 +397,8 @@ void rope_kv_fused(const Tensor& part, const c10::optional<Tensor>& bias, Tensor
                    Tensor& v_cache, const Tensor& pos, const Tensor& block_tables, int64_t tq, const Tensor& inv_freq,
                    const c10::optional<Tensor>& q_norm, const c10::optional<Tensor>& k_norm, double norm_eps,
                    double q_scale, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot_dim, bool interleaved,
-                   int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& pos_offset) {
+                   int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& pos_offset,
+                   bool zero_part) {
   c10::DeviceGuard g(part.device());
   const bool bf16 = is_bf16(q_out);
   TORCH_CHECK(part.dim() == 3 && part.scalar_type() == at::kFloat && part.is_contiguous(),
@@ -347,6 +409,8 @@ void rope_kv_fused(const Tensor& part, const c10::optional<Tensor>& bias, Tensor
   illm::RopeKVArgs a{};
   a.part = part.data_ptr<float>();
   a.nsplit = (int)part.size(0);
+  a.zero_part = zero_part ? 1 : 0;
+  TORCH_CHECK(!zero_part || a.nsplit == 1, "rope_kv_fused: zero_part needs a single accumulator slab");
   a.bias = p16o(bias);
   a.ld_qkv = (int)part.size(2);
   a.q_out = m16(q_out);
@@ -508,31 +572,22 @@ Tensor moe_gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
     a.N = (int)(n / 2);
     a.out = out.data_ptr();
     a.ldo = (int)(n / 2);
-    const size_t shmem = (size_t)Mmax * (KC * 128 + 8) * 2;
-    TORCH_CHECK(shmem <= kMaxLds, "moe_gemv: hidden size too large for the LDS-staged GLU path");
-    launch_gemv4_any((int)fmt, bf16, illm::EPI_GLU, dim3((unsigned)((NT + 7) / 8), 1, (unsigned)E), shmem, a);
+    const Plan5 p = plan5(Mmax, NT / 2, KC, false);
+    TORCH_CHECK(p.shmem <= kMaxLds, "moe_gemv: hidden size too large for the LDS-staged GLU path");
+    a.pf = p.pf;
+    launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_GLU, dim3(p.gx, 1, (unsigned)E), p.shmem, a);
     return out;
   }
   a.N = (int)n;
-  if (ksplit <= 0) {
-    ksplit = 1;
-    auto lds = [&](int64_t ks) { return Mmax * (((KC + ks - 1) / ks) * 128 + 8) * 2; };
-    while ((lds(ksplit) > 65536 || ((NT + 3) / 4) * ksplit * 2 < 256) && KC / (ksplit * 2) >= 2) ksplit *= 2;
-  }
-  ksplit = std::min<int64_t>(ksplit, KC);
-  int64_t cpk = (KC + ksplit - 1) / ksplit;
-  if (KC % 4 == 0) {
-    cpk = (cpk + 3) / 4 * 4;
-    ksplit = (KC + cpk - 1) / cpk;
-    a.cpk = (int)cpk;
-  }
-  const size_t shmem = (size_t)Mmax * (cpk * 128 + 8) * 2;
-  TORCH_CHECK(shmem <= kMaxLds, "moe_gemv: K slice too large for LDS");
+  const Plan5 p = plan5(Mmax, NT, KC, true, ksplit);
+  ksplit = p.ks;
+  a.cpk = (int)p.cpk;
+  a.pf = p.pf;
+  TORCH_CHECK(p.shmem <= kMaxLds, "moe_gemv: K slice too large for LDS");
   Tensor ws = at::empty({ksplit, npairs, n}, xc.options().dtype(at::kFloat));
   a.out = ws.data_ptr();
   a.ldo = (int)n;
-  launch_gemv4_any((int)fmt, bf16, illm::EPI_PARTIAL, dim3((unsigned)((NT + 3) / 4), (unsigned)ksplit, (unsigned)E),
-                   shmem, a);
+  launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_PARTIAL, dim3(p.gx, (unsigned)ksplit, (unsigned)E), p.shmem, a);
   return ws;
 }
 
@@ -606,6 +661,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("quantize_device", &quantize_device);
   m.impl("dequantize_device", &dequantize_device);
   m.impl("gemv", &gemv);
+  m.impl("gemv_accum", &gemv_accum);
   m.impl("add_rms_norm", &add_rms_norm);
   m.impl("layer_norm", &layer_norm);
   m.impl("rope_kv", &rope_kv);

@@ -133,6 +133,13 @@ def _ksplit(n: int, k: int) -> int:
     return ks
 
 
+# rows handled by the atomic split-K GEMV (ops.gemv_accum).  Measured on
+# MI355X (Llama-3-8B decode): at batch 1 one atomic slab beats ks f32 slabs
+# (consumers read 1 slab), at batch 8 the atomic traffic (M x N x ks adds at
+# ~1.3 TB/s chip-wide) costs more than the slab reduction saves
+ACC_MAX_M = 2
+
+
 class NativeAttention(nn.Module):
     def __init__(self, spec: DecoderSpec, qkv_proj: nn.Module, o_proj: nn.Module,
                  q_norm: Optional[torch.Tensor] = None, k_norm: Optional[torch.Tensor] = None,
@@ -192,6 +199,7 @@ class NativeCausalLM(nn.Module):
         self.first_stage = True
         self.last_stage = True
         self.layer_offset = 0
+        self._acc_bufs = {}
 
     def ensure_rope_cache(self, max_pos: int):
         """f32 [max_pos, rot/2, 2] cos/sin table (HF fp32 formula, incl. the
@@ -260,11 +268,29 @@ class NativeCausalLM(nn.Module):
             outs.append(o[0].transpose(0, 1)[None])
         return torch.cat(outs, 0).reshape(T, s.num_heads * s.head_dim)
 
+    def _acc(self, n: int, t: int, device) -> torch.Tensor:
+        """Zeroed f32 [t, n] accumulator for the split-K atomic GEMV
+        (ops.gemv_accum); its consumer re-zeroes it after reading, so one
+        buffer per shape serves every layer and every hipGraph replay."""
+        key = (n, t)
+        buf = self._acc_bufs.get(key)
+        if buf is None or buf.device != device:
+            buf = torch.zeros(t, n, dtype=torch.float32, device=device)
+            self._acc_bufs[key] = buf
+        return buf
+
     def _proj_residual_norm(self, x, proj, residual, norm_w, post_norm_w=None):
         """residual += proj(x); return rms_norm(residual) * norm_w."""
         s = self.spec
         fused = (x.is_cuda and isinstance(proj, LowBitLinear) and proj.bias is None and proj.mp_group is None
                  and post_norm_w is None and x.shape[0] <= ops.GEMV_MAX_M and self.tp_group is None)
+        if fused and x.shape[0] <= ACC_MAX_M and ops.native_gpu(x):
+            # split-K f32 atomics into one zeroed slab; the norm reads + re-zeroes it
+            acc = self._acc(proj.out_features, x.shape[0], x.device)
+            ops.gemv_accum(x, proj.weight, proj.fmt, proj.out_features, proj.in_features, acc)
+            out, _ = ops.add_rms_norm(None, residual, norm_w, s.rms_eps, partials=acc.unsqueeze(0),
+                                      unit_offset=s.norm_unit_offset, zero_partials=True)
+            return out
         if fused:
             part = ops.gemv_partials(x, proj.weight, proj.fmt, proj.out_features, proj.in_features, 0)
             out, _ = ops.add_rms_norm(None, residual, norm_w, s.rms_eps, partials=part,
@@ -333,12 +359,18 @@ class NativeCausalLM(nn.Module):
             q = torch.empty(T, s.num_heads, s.head_dim, dtype=x.dtype, device=x.device)
             if x.is_cuda and isinstance(qp, LowBitLinear) and qp.mp_group is None and T <= ops.GEMV_MAX_M \
                     and (qp.bias is None or qp.bias.dtype == x.dtype) and ops.native_gpu(x):
-                # split-K partials reduced (+bias) inside the RoPE/KV kernel, slots from the block table
-                part = ops.gemv_partials(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, 0)
+                # split-K GEMV reduced (+bias) inside the RoPE/KV kernel, slots from the block table:
+                # T <= 16 accumulates with atomics into one zeroed slab (re-zeroed by the kernel)
+                if T <= ACC_MAX_M:
+                    part = self._acc(qp.out_features, T, x.device)
+                    ops.gemv_accum(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, part)
+                    part = part.unsqueeze(0)
+                else:
+                    part = ops.gemv_partials(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, 0)
                 ops.rope_kv_fused(part, qp.bias, q, cache.k[li], cache.v[li], pos, meta.block_tables, meta.Tq, rope,
                                   s.num_heads, s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved,
                                   attn.q_norm, attn.k_norm, s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale,
-                                  cache.v_scale, meta.pos_offset)
+                                  cache.v_scale, meta.pos_offset, zero_part=T <= ACC_MAX_M)
             else:
                 qkv = qp(x)
                 ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,

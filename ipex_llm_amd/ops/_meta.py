@@ -29,7 +29,7 @@ def _(x, blob, fmt, n, k, bias, epi, ksplit, act):
 
 
 @register_fake("ipex_llm_amd::add_rms_norm")
-def _(x, partials, residual, w, eps, unit_offset, store_residual):
+def _(x, partials, residual, w, eps, unit_offset, store_residual, zero_partials=False):
     if x is not None:
         return torch.empty_like(x)
     if residual is not None:
@@ -91,7 +91,12 @@ def _(part, w, ids, e0, num_local, dtype):
 
 @register_fake("ipex_llm_amd::rope_kv_fused")
 def _(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm, norm_eps, q_scale, Hq,
-      Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale, pos_offset=None):
+      Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale, pos_offset=None, zero_part=False):
+    return None
+
+
+@register_fake("ipex_llm_amd::gemv_accum")
+def _(x, blob, fmt, n, k, acc, ksplit):
     return None
 
 

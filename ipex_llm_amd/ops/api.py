@@ -17,7 +17,7 @@ __all__ = [
     "quantize", "dequantize", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
-    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in",
+    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
 ]
 
 
@@ -95,6 +95,16 @@ def gemv_partials(x, blob, fmt, n, k, ksplit: int) -> torch.Tensor:
     return _ops().gemv(x, blob, fmt, n, k, None, 1, ksplit, 0)
 
 
+def gemv_accum(x, blob, fmt, n, k, acc: torch.Tensor, ksplit: int = 0) -> torch.Tensor:
+    """acc [M, n] f32 (zero on entry) += x @ W^T via split-K f32 atomics; the
+    consumer (add_rms_norm / rope_kv_fused with zero_*=True) re-zeroes it."""
+    if _native(x):
+        _ops().gemv_accum(x, blob, fmt, n, k, acc, ksplit)
+        return acc
+    acc += lowbit_matmul(x, blob, fmt, n, k).float().view_as(acc)
+    return acc
+
+
 def gemv_glu(x, blob, fmt, n, k, act: int = 0) -> torch.Tensor:
     """act(x @ Wg^T) * (x @ Wu^T) for a tile-interleaved gate/up weight."""
     return _ops().gemv(x, blob, fmt, n, k, None, 2, 1, act)
@@ -113,14 +123,17 @@ def reduce_partials(ws, bias=None, dtype=torch.bfloat16):
 # ------------------------------------------------------------ norms / act
 def add_rms_norm(x: Optional[torch.Tensor], residual: Optional[torch.Tensor], w: torch.Tensor,
                  eps: float, partials: Optional[torch.Tensor] = None,
-                 unit_offset: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                 unit_offset: bool = False, zero_partials: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """residual += x (or the sum of GEMV partials); returns (rms_norm(residual), residual).
-    On GPU the residual is updated in place."""
+    On GPU the residual is updated in place.  zero_partials re-zeroes the
+    partial slab after reading it (atomic accumulators, gemv_accum)."""
     if _native(w):
-        out = _ops().add_rms_norm(x, partials, residual, w, eps, unit_offset, True)
+        out = _ops().add_rms_norm(x, partials, residual, w, eps, unit_offset, True, zero_partials)
         return out, residual
     if partials is not None:
         x = partials.sum(0).to(w.dtype).view_as(residual) if residual is not None else partials.sum(0).to(w.dtype)
+        if zero_partials:
+            partials.zero_()
     normed, new_res = R.add_rms_norm(x, residual, w, eps, unit_offset)
     if residual is not None:
         residual.copy_(new_res)
@@ -222,16 +235,18 @@ def rope_kv(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, Hq, Hkv, D, rot_
 
 def rope_kv_fused(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, Hq, Hkv, D, rot_dim=None,
                   interleaved=False, q_norm=None, k_norm=None, norm_eps=1e-6, q_scale=1.0, kv_fp8=0,
-                  k_scale=1.0, v_scale=1.0, pos_offset=None):
+                  k_scale=1.0, v_scale=1.0, pos_offset=None, zero_part=False):
     """rope_kv over the split-K partials of the QKV GEMV ([ks, T, N] f32,
     summed + bias in the kernel) with device-side slots from the block table."""
     rot_dim = rot_dim or D
     if _native(part):
         _ops().rope_kv_fused(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm,
                              norm_eps, q_scale, Hq, Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale,
-                             pos_offset)
+                             pos_offset, zero_part)
         return q_out
     qkv = part.sum(0)
+    if zero_part:
+        part.zero_()
     if bias is not None:
         qkv = qkv + bias.float()
     qkv = qkv.to(q_out.dtype)

@@ -140,7 +140,7 @@ def device_index(fmt: int, n: int, k: int, device="cpu"):
         off = rec + ((s // 2) * 64 + lane) * 16 + (s % 2) * 8 + j
         shift = torch.zeros_like(off)
     blk = (kk // QBLOCK) % 2
-    sidx = (tile + KC * fmt_bits(fmt) * 256 + (r * KC + c) * 4) // 2 + blk
+    sidx = (tile + KC * fmt_bits(fmt) * 256 + (c * TILE_N + r) * 4) // 2 + blk
     return off, shift, sidx
 
 

@@ -60,6 +60,31 @@ def test_gemv_formats(cuda, name, dtype, M, ver, monkeypatch):
         assert _rel(yb, ref + b.float()) < 1e-2
 
 
+@pytest.mark.parametrize("name", ["sym_int4", "asym_int4", "nf4", "fp8_e4m3", "sym_int8"])
+@pytest.mark.parametrize("M", [1, 5, 16])
+def test_gemv_accum_and_zeroing_consumers(cuda, name, M):
+    """split-K f32-atomic GEMV (v5 EPI_ATOMIC) vs the fp32 reference; the
+    norm consumer must leave the accumulator zeroed."""
+    f = get_format(name).fmt
+    torch.manual_seed(1)
+    n, k = 512, 1024
+    w = torch.randn(n, k, device=cuda) * 0.05
+    blob = ops.quantize(w, f)
+    x = torch.randn(M, k, device=cuda).bfloat16()
+    ref = R.lowbit_linear_ref(x, blob.cpu(), f, n, k).to(cuda)
+    acc = torch.zeros(M, n, device=cuda)
+    for ks in (0, 1, 8):
+        acc.zero_()
+        ops.gemv_accum(x, blob, f, n, k, acc, ks)
+        assert _rel(acc, ref) < 5e-3, (name, M, ks)
+    res = torch.randn(M, n, device=cuda).bfloat16()
+    wn = torch.rand(n, device=cuda).bfloat16() + 0.5
+    exp, _ = R.add_rms_norm(acc.bfloat16(), res.clone(), wn, 1e-5)
+    out, _ = ops.add_rms_norm(None, res, wn, 1e-5, partials=acc.unsqueeze(0), zero_partials=True)
+    assert _rel(out, exp) < 1e-2
+    assert acc.abs().max().item() == 0.0
+
+
 @pytest.mark.parametrize("M", [1, 3, 33])
 def test_gemv_glu(cuda, M):
     from ipex_llm_amd.models.decoder import interleave_glu_rows

@@ -1,0 +1,52 @@
+"""Time the decode GEMV shapes under the current ILLM_GEMV5_KW/KS env (one
+process per setting; see tools/gemv_sweep5.sh).  Prints one JSON line per
+(M, op) with microseconds and effective TB/s."""
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ipex_llm_amd import ops  # noqa: E402
+from ipex_llm_amd.quantize import get_format  # noqa: E402
+from tools.bench_kernels import timeit  # noqa: E402
+
+SHAPES = [("qkv", 6144, 4096, "part"), ("o", 4096, 4096, "part"), ("glu", 28672, 4096, "glu"),
+          ("down", 4096, 14336, "part"), ("lm_head", 128256, 4096, "store")]
+
+
+def main():
+    ms = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "1,8").split(",")]
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+    ops.require()
+    f = get_format("sym_int4").fmt
+    dev = torch.device("cuda")
+    tag = {"kw": os.environ.get("ILLM_GEMV5_KW", "auto"), "ks": os.environ.get("ILLM_GEMV5_KS", "auto")}
+    for name, n, k, kind in SHAPES:
+        if only and name not in only:
+            continue
+        copies = max(1, int(math.ceil(600e6 / (n * k * 0.5))))
+        blobs = [ops.quantize(torch.randn(n, k, device=dev, dtype=torch.bfloat16) * 0.02, f) for _ in range(copies)]
+        for M in ms:
+            x = torch.randn(M, k, device=dev, dtype=torch.bfloat16)
+            i = [0]
+
+            def run():
+                i[0] = (i[0] + 1) % copies
+                b = blobs[i[0]]
+                if kind == "glu":
+                    return ops.gemv_glu(x, b, f, n, k, 0)
+                if kind == "part":
+                    return ops.gemv_partials(x, b, f, n, k, 0)
+                return ops.lowbit_matmul(x, b, f, n, k)
+            us = timeit(run)
+            print(json.dumps({**tag, "M": M, "op": name, "us": round(us, 2),
+                              "TBps": round(blobs[0].numel() / us / 1e6, 3)}), flush=True)
+        del blobs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
