@@ -456,12 +456,12 @@ template <typename T, int D, int RT>
 static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
   AttnDecodeArgs a = a0;
   // combine fused into the split kernel when the merge fits its LDS scratch
-  if (a.nsplit > SPLIT * RT) a.counters = nullptr;
+  if (a.nsplit > SPLIT * RT || a.no_combine) a.counters = nullptr;
   dim3 grid(a.nsplit, a.Hkv, a.B);
   if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT>), grid, dim3(64), 0, st, a);
   else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT>), grid, dim3(64), 0, st, a);
   else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT>), grid, dim3(64), 0, st, a);
-  if (a.counters == nullptr)
+  if (a.counters == nullptr && !a.no_combine)
     hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
 }
 
@@ -477,7 +477,7 @@ static void launch_d(const AttnDecodeArgs& a, hipStream_t st) {
   if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_kernel<T, D, 1>), grid, dim3(64), 0, st, a);
   else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_kernel<T, D, 2>), grid, dim3(64), 0, st, a);
   else hipLaunchKernelGGL((attn_decode_kernel<T, D, 0>), grid, dim3(64), 0, st, a);
-  hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
+  if (!a.no_combine) hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
 }
 
 template <typename T>

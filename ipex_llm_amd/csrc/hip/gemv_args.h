@@ -70,7 +70,13 @@ struct GemvArgs {
   // v5 int4 decode constants (set by the launcher): packed-pair nibble mask
   // and magic exponent; runtime values so hipcc emits one v_and_or_b32
   uint32_t nib_mask, nib_magic;
-  int pf;                  // v5 prefetch depth (4 or 8 chunks per wave)
+  int nw;                  // v5 waves per workgroup (4 or 8)
+  // v5 attention-combine prologue (o_proj over flash-decoding partials): x[m, h*D + d] =
+  // sum_s w_s po[b, h, t, s, d] / L with m = b*Tq + t, split weights from pml and seq_lens
+  const float* apo;        // [B, Hq, Tq, ans, D] f32 or null
+  const float* aml;        // [B, Hq, Tq, ans, 2] (max, sum)
+  const int32_t* alens;    // [B] keys per sequence (valid splits = ceil(len / 64))
+  int ans, aD, aHq, aTq;
 };
 
 }  // namespace illm

@@ -22,8 +22,11 @@ void launch_gemv_dk(bool bf16, int mt, int epi, dim3 grid, const GemvArgs& a, hi
 template <int DK>
 void launch_gemv5_dk(bool bf16, int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
 constexpr int gemv5_x_ld_h(int kw) { return kw + 8; }
+constexpr size_t gemv5_attn_shmem_h(int rows, int cpk, int D, int ns) {
+  return (size_t)rows * ((cpk * 128 + D - 1) / D + 1) * (ns + 1) * 4;
+}
 constexpr size_t gemv5_shmem_h(int rows, int cpk) {
-  return ((size_t)rows * gemv5_x_ld_h(cpk * 128) * 2 + 15) / 16 * 16 + (size_t)rows * cpk * 16 + 4 * 2 * 64 * 16;
+  return ((size_t)rows * gemv5_x_ld_h(cpk * 128) * 2 + 15) / 16 * 16 + (size_t)rows * cpk * 16 + 8 * 2 * 64 * 16;
 }
 
 // ---- norms (norm.hip) ------------------------------------------------------
@@ -93,6 +96,7 @@ struct AttnDecodeArgs {
   int kv_fp8;
   float k_scale, v_scale;
   const float* alibi;       // [Hq] slopes or null
+  int no_combine;           // leave the split partials for the consumer (o_proj GEMV prologue)
 };
 void launch_attn_decode(bool bf16, const AttnDecodeArgs& a, hipStream_t st);
 

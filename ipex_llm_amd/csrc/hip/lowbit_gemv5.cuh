@@ -124,17 +124,23 @@ __device__ __forceinline__ uint4 raw_a8(uint32_t lo, uint32_t hi) {
 
 // LDS plan of one workgroup (bytes): x slice [rows][kw + 8] in C, then per
 // (row, chunk) float4 {-OFF*sx0, -OFF*sx1, sx0, sx1}, then the KW reduction
-// area [4 waves][2 tiles][64] float4.
+// area [<= 8 waves][2 tiles][64] float4, then (attention-combine prologue only)
+// the split weights [rows][heads of the slice][ans + 1] f32.
 __host__ __device__ constexpr int gemv5_x_ld(int kw) { return kw + 8; }
 __host__ __device__ constexpr size_t gemv5_shmem(int rows, int cpk) {
-  return ((size_t)rows * gemv5_x_ld(cpk * 128) * 2 + 15) / 16 * 16 + (size_t)rows * cpk * 16 + 4 * 2 * 64 * 16;
+  return ((size_t)rows * gemv5_x_ld(cpk * 128) * 2 + 15) / 16 * 16 + (size_t)rows * cpk * 16 + 8 * 2 * 64 * 16;
+}
+__host__ __device__ constexpr int gemv5_attn_heads(int cpk, int D) { return (cpk * 128 + D - 1) / D + 1; }
+__host__ __device__ constexpr size_t gemv5_attn_shmem(int rows, int cpk, int D, int ns) {
+  return (size_t)rows * gemv5_attn_heads(cpk, D) * (ns + 1) * 4;
 }
 
-template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int PF>
-__global__ void __launch_bounds__(256) lowbit_gemv5_kernel(const GemvArgs a) {
+template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW>
+__global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a) {
+  constexpr int PF = 4;                 // chunks in flight per wave (8 measured slower)
   using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;   // MFMA input type
   constexpr int BITS = dk_bits(DK);
-  constexpr int TG = 4 / KW;           // tile groups per workgroup
+  constexpr int TG = NW / KW;          // tile groups per workgroup (NW waves)
   constexpr float OFF = raw_off<DK, C>();
   constexpr bool HASMIN = dk_has_min(DK);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -166,6 +172,7 @@ __global__ void __launch_bounds__(256) lowbit_gemv5_kernel(const GemvArgs a) {
   uint16_t* xs = (uint16_t*)smem;
   float4* sxs = (float4*)(smem + ((size_t)Mloc * ldx * 2 + 15) / 16 * 16);        // [Mloc][c1-c0]
   float4* red = (float4*)((uint8_t*)sxs + (size_t)Mloc * (c1 - c0) * 16);          // [4][TPW][64]
+  float* aw = (float*)(red + 8 * 2 * 64);                                          // attention split weights
 
   const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
   const int tg = wave / KW, kp = wave % KW;
@@ -203,16 +210,82 @@ __global__ void __launch_bounds__(256) lowbit_gemv5_kernel(const GemvArgs a) {
     for (int u = 0; u < PF; u++) load_chunk(ring[u], wc0 + u);
   }
   if constexpr (DK == DK_LUT4) {
-    lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
+    if (threadIdx.x < 256)
+      lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
+  }
+
+  // ---- attention-combine prologue: per (row, head) split weights exp(m_s - M) / L
+  const int a_h0 = a.apo ? kbase / a.aD : 0;
+  const int a_nh = a.apo ? (kbase + kw - 1) / a.aD - a_h0 + 1 : 0;
+  if (a.apo) {
+    // 16 lanes per (row, head) pair, one split per lane (all (m, l) loads in
+    // flight at once; a serial per-thread loop was latency-bound)
+    const int sub = threadIdx.x & 15;
+    for (int v = threadIdx.x >> 4; v < Mloc * a_nh; v += NW * 4) {
+      const int m = v / a_nh, h = min(a_h0 + v % a_nh, a.aHq - 1);
+      float* wr = aw + (size_t)v * (a.ans + 1);
+      const int b = m / a.aTq, t = m % a.aTq;
+      const int ns = min(a.ans, (a.alens[b] + 63) / 64);
+      const float2* ml = (const float2*)a.aml + (((size_t)b * a.aHq + h) * a.aTq + t) * a.ans;
+      float M = -INFINITY;
+      for (int s = sub; s < ns; s += 16) M = fmaxf(M, ml[s].x);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) M = fmaxf(M, __shfl_xor(M, o, 16));
+      float L = 0.f;
+      for (int s = sub; s < a.ans; s += 16) {
+        float w = 0.f;
+        if (s < ns) {
+          const float2 q = ml[s];
+          w = q.x == -INFINITY ? 0.f : __expf(q.x - M);
+          L += w * q.y;
+        }
+        wr[s] = w;
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) L += __shfl_xor(L, o, 16);
+      if (sub == 0) wr[a.ans] = L > 0.f ? 1.f / L : 0.f;
+    }
+    __syncthreads();
   }
 
   // ---- stage x[0:Mloc, kbase:kbase+kw] -> LDS in C
   {
     const int vpr = kw / 8;
-    for (int v = threadIdx.x; v < Mloc * vpr; v += 256) {
+    for (int v = threadIdx.x; v < Mloc * vpr; v += NW * 64) {
       const int m = v / vpr, kk = (v % vpr) * 8;
       uint4 val = make_uint4(0, 0, 0, 0);
-      if (kbase + kk < a.K && a.xpart) {
+      if (kbase + kk < a.K && a.apo) {
+        // combine the flash-decoding partials of this 8-dim group (8 | D)
+        const int k0 = kbase + kk, h = k0 / a.aD, d = k0 % a.aD;
+        const int b = m / a.aTq, t = m % a.aTq;
+        const float* wr = aw + (size_t)(m * a_nh + (h - a_h0)) * (a.ans + 1);
+        const float* po = a.apo + ((((size_t)b * a.aHq + h) * a.aTq + t) * a.ans) * a.aD + d;
+        float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        // unconditional loads (a branch per split serialises them); an unused or
+        // fully masked split (w == 0) holds unwritten bytes, so select, never multiply
+#pragma unroll 4
+        for (int s = 0; s < a.ans; s++) {
+          const float w = wr[s];
+          const float4 p0 = *(const float4*)(po + (size_t)s * a.aD), p1 = *(const float4*)(po + (size_t)s * a.aD + 4);
+          const bool on = w != 0.f;
+          o[0] += on ? w * p0.x : 0.f; o[1] += on ? w * p0.y : 0.f; o[2] += on ? w * p0.z : 0.f;
+          o[3] += on ? w * p0.w : 0.f; o[4] += on ? w * p1.x : 0.f; o[5] += on ? w * p1.y : 0.f;
+          o[6] += on ? w * p1.z : 0.f; o[7] += on ? w * p1.w : 0.f;
+        }
+        const float invL = wr[a.ans];
+        uint32_t w4[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          // rounded to T: what the separate combine kernel would have written
+          float v0 = to_f32<T>(from_f32<T>(o[2 * i] * invL)), v1 = to_f32<T>(from_f32<T>(o[2 * i + 1] * invL));
+          if constexpr (std::is_same<C, F16>::value) {
+            v0 = fminf(fmaxf(v0, -65504.f), 65504.f);
+            v1 = fminf(fmaxf(v1, -65504.f), 65504.f);
+          }
+          w4[i] = pack2<C>(v0, v1);
+        }
+        val = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      } else if (kbase + kk < a.K && a.xpart) {
         // fused activation input: x = act(gate) * up from the gate/up GEMV's split-K slabs
         const int k0 = kbase + kk;
         const size_t gc = (size_t)(k0 >> 4) * 32 + (k0 & 15);
@@ -262,7 +335,7 @@ __global__ void __launch_bounds__(256) lowbit_gemv5_kernel(const GemvArgs a) {
   // ---- per (row, chunk): block sums of the staged activations
   {
     const int nch = c1 - c0;
-    for (int v = threadIdx.x; v < Mloc * nch * 2; v += 256) {
+    for (int v = threadIdx.x; v < Mloc * nch * 2; v += NW * 64) {
       const int m = v / (nch * 2), rem = v % (nch * 2);
       const uint16_t* p = xs + m * ldx + rem * 64;
       float s = 0.f;
@@ -423,15 +496,15 @@ inline void launch5(K kern, dim3 grid, size_t shmem, const GemvArgs& a, hipStrea
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(kern, grid, dim3(256), shmem, st, a);
+  hipLaunchKernelGGL(kern, grid, dim3(64 * (a.nw == 8 ? 8 : 4)), shmem, st, a);
 }
 
-template <int DK, typename T, int KW, bool MOE, int PF>
+template <int DK, typename T, int KW, bool MOE, int NW>
 inline void launch5_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
-  if (epi == EPI_STORE) launch5(lowbit_gemv5_kernel<DK, T, EPI_STORE, 1, KW, MOE, PF>, grid, shmem, a, st);
-  else if (epi == EPI_PARTIAL) launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, PF>, grid, shmem, a, st);
-  else if (epi == EPI_ATOMIC) launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, PF>, grid, shmem, a, st);
-  else launch5(lowbit_gemv5_kernel<DK, T, EPI_GLU, 2, KW, MOE, PF>, grid, shmem, a, st);
+  if (epi == EPI_STORE) launch5(lowbit_gemv5_kernel<DK, T, EPI_STORE, 1, KW, MOE, NW>, grid, shmem, a, st);
+  else if (epi == EPI_PARTIAL) launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, NW>, grid, shmem, a, st);
+  else if (epi == EPI_ATOMIC) launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, NW>, grid, shmem, a, st);
+  else launch5(lowbit_gemv5_kernel<DK, T, EPI_GLU, 2, KW, MOE, NW>, grid, shmem, a, st);
 }
 
 template <int DK, typename T, bool MOE>
@@ -440,8 +513,9 @@ inline void launch5_kw(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs&
   GemvArgs a = a0;
   a.nib_mask = 0x000F000Fu;
   a.nib_magic = Raw<C>::k4;
-  // prefetch depth: chunks in flight per wave (a.pf; 8 when a wave's range is short)
-  if (a.pf == 8) {
+  // workgroup size: 4 or 8 waves (a.nw); 8 shares one LDS copy of x among
+  // twice the tiles (the x-staging cost of kw > 1 at larger M)
+  if (a.nw == 8) {
     if (kw == 1) launch5_epi<DK, T, 1, MOE, 8>(epi, grid, shmem, a, st);
     else if (kw == 2) launch5_epi<DK, T, 2, MOE, 8>(epi, grid, shmem, a, st);
     else launch5_epi<DK, T, 4, MOE, 8>(epi, grid, shmem, a, st);
@@ -452,7 +526,7 @@ inline void launch5_kw(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs&
   }
 }
 
-// grid.x = workgroups of (4 / kw) tile groups (GLU: tile pairs), grid.y = split-K
+// grid.x = workgroups of (nw / kw) tile groups (GLU: tile pairs), grid.y = split-K
 template <int DK>
 void launch_gemv5_dk(bool bf16, int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
   const bool moe = a.moe_off != nullptr;

@@ -90,25 +90,29 @@ int64_t auto_ksplit(int64_t NT, int64_t KC) {
 // is staged once per workgroup, so kw > 1 (fewer tiles per workgroup) only
 // pays for the unsplittable GLU at M <= 2; split-K workgroups of ~8 chunks
 // (M <= 2) / ~4 chunks (M > 2) are fastest for the slab-output projections.
-// ILLM_GEMV5_KW / ILLM_GEMV5_KS / ILLM_GEMV5_PF override (sweeps).
+// ILLM_GEMV5_KW / ILLM_GEMV5_KS / ILLM_GEMV5_NW override (sweeps).
 struct Plan5 {
   int kw;
   int64_t ks, cpk;
   size_t shmem;
   unsigned gx;
-  int pf;
+  int nw;
 };
 Plan5 plan5(int64_t rows, int64_t groups, int64_t KC, bool can_split, int64_t ks_req = 0, bool atomic = false) {
   static const int kw_env = getenv("ILLM_GEMV5_KW") ? atoi(getenv("ILLM_GEMV5_KW")) : 0;
   static const int ks_env = getenv("ILLM_GEMV5_KS") ? atoi(getenv("ILLM_GEMV5_KS")) : 0;
-  static const int pf_env = getenv("ILLM_GEMV5_PF") ? atoi(getenv("ILLM_GEMV5_PF")) : 0;
-  Plan5 p{1, 1, KC, 0, 0, 4};
+  static const int nw_env = getenv("ILLM_GEMV5_NW") ? atoi(getenv("ILLM_GEMV5_NW")) : 0;
+  Plan5 p{1, 1, KC, 0, 0, 4};  // kw, ks, cpk, shmem, gx, nw
   if (!can_split) {
-    p.kw = rows <= 2 ? 4 : (rows <= 4 ? 2 : 1);
+    // GLU: M <= 2 -> 4-wave groups, 4-way K split (1 tile pair each);
+    // larger M -> 8-wave groups, 2-way K split (x staged once per 4 pairs)
+    p.kw = rows <= 2 ? 4 : 2;
+    p.nw = rows <= 2 ? 4 : 8;
     while (p.kw > 1 && KC / p.kw < 4) p.kw /= 2;
   } else if (ks_req > 0) {
     p.ks = ks_req;
   } else {
+    p.nw = rows >= 4 ? 8 : 4;     // 8-wave groups: x slice shared by 8 tiles (down M=16: 10.8 vs 15.7 us)
     const int64_t target = rows <= 2 ? 8 : 4;
     p.ks = std::min<int64_t>(atomic ? 32 : 16, std::max<int64_t>(1, (KC + target - 1) / target));
     // wide outputs (lm_head: 8016 tiles) already fill the chip: slabs only cost
@@ -121,8 +125,8 @@ Plan5 plan5(int64_t rows, int64_t groups, int64_t KC, bool can_split, int64_t ks
   p.cpk = (KC + p.ks - 1) / p.ks;
   p.ks = (KC + p.cpk - 1) / p.cpk;
   p.shmem = illm::gemv5_shmem_h((int)rows, (int)p.cpk);
-  p.pf = pf_env ? pf_env : 4;
-  const int64_t per_wg = 4 / p.kw;
+  if (nw_env) p.nw = nw_env;
+  const int64_t per_wg = p.nw / p.kw;
   p.gx = (unsigned)((groups + per_wg - 1) / per_wg);
   return p;
 }
@@ -163,7 +167,7 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
     a.ldo = (int)(n / 2);
     const Plan5 p = plan5(M, NT / 2, KC, false);
     if (small && p.shmem <= kMaxLds)
-      a.pf = p.pf, launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_GLU, dim3(p.gx, 1), p.shmem, a);
+      a.nw = p.nw, launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_GLU, dim3(p.gx, 1), p.shmem, a);
     else
       launch_gemv_any((int)fmt, bf16, mt, illm::EPI_GLU, dim3((unsigned)(NT / 2), 1), a);
     return out;
@@ -178,7 +182,7 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   if (use5) {
     ksplit = p5.ks;
     a.cpk = (int)p5.cpk;
-    a.pf = p5.pf;
+    a.nw = p5.nw;
   } else {
     if (ksplit <= 0) ksplit = auto_ksplit(NT, KC);
     ksplit = std::min<int64_t>(ksplit, KC);
@@ -237,7 +241,7 @@ void gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   a.ldo = (int)n;
   const Plan5 p = plan5(M, NT, KC, true, ksplit, true);
   a.cpk = (int)p.cpk;
-  a.pf = p.pf;
+  a.nw = p.nw;
   TORCH_CHECK(p.shmem <= kMaxLds, "gemv_accum: K slice too large for LDS");
   launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_ATOMIC, dim3(p.gx, (unsigned)p.ks), p.shmem, a);
 }
@@ -273,7 +277,7 @@ Tensor gemv_glu_in(const Tensor& part, const Tensor& blob, int64_t fmt, int64_t 
   const Plan5 p = plan5(M, NT, KC, true, ksplit);
   ksplit = p.ks;
   a.cpk = (int)p.cpk;
-  a.pf = p.pf;
+  a.nw = p.nw;
   TORCH_CHECK(p.shmem <= kMaxLds, "gemv_glu_in: K slice too large for LDS");
   Tensor ws = at::empty({ksplit, M, n}, part.options());
   a.out = ws.data_ptr();
@@ -441,9 +445,10 @@ void rope_kv_fused(const Tensor& part, const c10::optional<Tensor>& bias, Tensor
   if (a.T > 0) illm::launch_rope_kv(bf16, a, cur_stream());
 }
 
-Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
                    const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
-                   int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& alibi) {
+                   int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& alibi,
+                   bool no_combine) {
   c10::DeviceGuard g(q.device());
   const bool bf16 = is_bf16(q);
   TORCH_CHECK(q.dim() == 4 && q.is_contiguous(), "q must be contiguous [B, Tq, Hq, D]");
@@ -484,9 +489,83 @@ Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache
   // group and measured slower than the separate combine launch; opt-in only
   static const bool fused_combine = getenv("ILLM_ATTN_FUSED_COMBINE") != nullptr;
   a.counters = fused_combine ? attn_counters(q.device(), B * Hkv) : nullptr;
+  a.no_combine = no_combine ? 1 : 0;
   illm::launch_attn_decode(bf16, a, cur_stream());
+  return {out, po, pml};
+}
+
+Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                   const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
+                   int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& alibi) {
+  return std::get<0>(attn_decode_impl(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window,
+                                      kv_fp8, k_scale, v_scale, alibi, false));
+}
+
+// split kernel only: the (o, m, l) partials [B, Hq, Tq, nsplit, D] / [.., 2] are merged by the
+// o_proj GEMV's prologue (gemv_attn), which saves the combine launch
+std::tuple<Tensor, Tensor> attn_decode_split(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
+                                             const Tensor& block_tables, const Tensor& seq_lens, int64_t nsplit,
+                                             double scale, double softcap, int64_t window, int64_t kv_fp8,
+                                             double k_scale, double v_scale, const c10::optional<Tensor>& alibi) {
+  auto r = attn_decode_impl(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, kv_fp8,
+                            k_scale, v_scale, alibi, true);
+  return {std::get<1>(r), std::get<2>(r)};
+}
+
+// o_proj GEMV whose input rows are combined from the flash-decoding partials in
+// its prologue.  acc given: f32 atomics into acc [T, n] (returned); else f32
+// split-K slabs [ks, T, n].
+Tensor gemv_attn(const Tensor& po, const Tensor& pml, const Tensor& seq_lens, const Tensor& blob, int64_t fmt,
+                 int64_t n, int64_t k, const c10::optional<Tensor>& acc, int64_t ksplit, at::ScalarType dt) {
+  TORCH_CHECK(po.is_cuda() && po.dim() == 5 && po.scalar_type() == at::kFloat && po.is_contiguous(),
+              "gemv_attn: po must be f32 [B, Hq, Tq, ns, D]");
+  c10::DeviceGuard g(po.device());
+  const int64_t B = po.size(0), Hq = po.size(1), Tq = po.size(2), ns = po.size(3), D = po.size(4);
+  const int64_t M = B * Tq;
+  TORCH_CHECK(Hq * D == k && D % 8 == 0, "gemv_attn: Hq * D must equal in_features");
+  TORCH_CHECK(M >= 1 && M <= 16, "gemv_attn handles 1..16 rows");
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "gemv_attn: bf16/fp16 activations");
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemv_attn: weight blob too small");
+  const bool bf16 = dt == at::kBFloat16;
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  illm::GemvArgs a{};
+  a.apo = po.data_ptr<float>();
+  a.aml = pml.data_ptr<float>();
+  a.alens = seq_lens.data_ptr<int32_t>();
+  a.ans = (int)ns;
+  a.aD = (int)D;
+  a.aHq = (int)Hq;
+  a.aTq = (int)Tq;
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.KC = (int)KC;
+  a.lut_fmt = (int)fmt;
+  a.N = (int)n;
+  const bool atomic = acc.has_value() && acc->defined();
+  Plan5 p = plan5(M, NT, KC, true, ksplit, atomic);
+  p.shmem += illm::gemv5_attn_shmem_h((int)M, (int)p.cpk, (int)D, (int)ns);
+  TORCH_CHECK(p.shmem <= kMaxLds, "gemv_attn: LDS plan too large (too many attention splits)");
+  a.cpk = (int)p.cpk;
+  a.nw = p.nw;
+  Tensor out;
+  if (atomic) {
+    TORCH_CHECK(acc->scalar_type() == at::kFloat && acc->is_contiguous() && acc->numel() == M * n,
+                "gemv_attn: acc must be contiguous f32 [T, n]");
+    a.out = acc->data_ptr();
+    out = *acc;
+  } else {
+    out = at::empty({p.ks, M, n}, po.options());
+    a.out = out.data_ptr();
+  }
+  a.ldo = (int)n;
+  launch_gemv5_any((int)fmt, bf16, p.kw, atomic ? illm::EPI_ATOMIC : illm::EPI_PARTIAL, dim3(p.gx, (unsigned)p.ks),
+                   p.shmem, a);
   return out;
 }
+
 
 Tensor glu(const Tensor& gu, int64_t act) {
   c10::DeviceGuard g(gu.device());
@@ -574,7 +653,7 @@ Tensor moe_gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
     a.ldo = (int)(n / 2);
     const Plan5 p = plan5(Mmax, NT / 2, KC, false);
     TORCH_CHECK(p.shmem <= kMaxLds, "moe_gemv: hidden size too large for the LDS-staged GLU path");
-    a.pf = p.pf;
+    a.nw = p.nw;
     launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_GLU, dim3(p.gx, 1, (unsigned)E), p.shmem, a);
     return out;
   }
@@ -582,7 +661,7 @@ Tensor moe_gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   const Plan5 p = plan5(Mmax, NT, KC, true, ksplit);
   ksplit = p.ks;
   a.cpk = (int)p.cpk;
-  a.pf = p.pf;
+  a.nw = p.nw;
   TORCH_CHECK(p.shmem <= kMaxLds, "moe_gemv: K slice too large for LDS");
   Tensor ws = at::empty({ksplit, npairs, n}, xc.options().dtype(at::kFloat));
   a.out = ws.data_ptr();
@@ -662,6 +741,8 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("dequantize_device", &dequantize_device);
   m.impl("gemv", &gemv);
   m.impl("gemv_accum", &gemv_accum);
+  m.impl("attn_decode_split", &attn_decode_split);
+  m.impl("gemv_attn", &gemv_attn);
   m.impl("add_rms_norm", &add_rms_norm);
   m.impl("layer_norm", &layer_norm);
   m.impl("rope_kv", &rope_kv);

@@ -279,6 +279,42 @@ class NativeCausalLM(nn.Module):
             self._acc_bufs[key] = buf
         return buf
 
+    # opt-in: measured on MI355X (Llama-3-8B, L=1024) the prologue merge is
+    # replicated by every o_proj N-tile group (64x re-reads of the partials:
+    # 128 MB of L2 traffic at batch 8), costing more than the combine launch
+    # it saves (batch 1: 2.07 vs 2.06 ms/token, batch 8: 3.04 vs 2.83)
+    _attn_fuse = __import__("os").environ.get("ILLM_ATTN_OPROJ_FUSE", "0") == "1"
+
+    def _attn_oproj_fuse_ok(self, attn, q, meta) -> bool:
+        """decode attention whose split partials are merged inside the o_proj
+        GEMV prologue (no combine launch): native GPU, <= 16 rows, plain
+        low-bit o_proj, no sandwich norm / TP, bounded split count."""
+        s, o = self.spec, attn.o_proj
+        group = s.num_heads // s.num_kv_heads
+        return (self._attn_fuse and q.is_cuda and not s.sandwich_norm and self.tp_group is None
+                and q.shape[0] <= 16 and meta.Tq * group <= 16 and meta.nsplit <= 128
+                and s.head_dim in (64, 80, 96, 128, 256) and s.head_dim % 8 == 0
+                and isinstance(o, LowBitLinear) and o.bias is None and o.mp_group is None
+                and ops.native_gpu(q))
+
+    def _attn_oproj_norm(self, li, attn, q, meta, cache, residual, norm_w):
+        s, o = self.spec, attn.o_proj
+        T = q.shape[0]
+        po, pml = ops.attn_decode_split(q.view(meta.B, meta.Tq, s.num_heads, s.head_dim), cache.k[li], cache.v[li],
+                                        meta.block_tables, meta.seq_lens, meta.nsplit, s.scale, s.attn_softcap,
+                                        attn.sliding_window, cache.kv_fp8, cache.k_scale, cache.v_scale, None)
+        if T <= ACC_MAX_M:
+            acc = self._acc(o.out_features, T, q.device)
+            ops.gemv_attn(po, pml, meta.seq_lens, o.weight, o.fmt, o.out_features, o.in_features, acc, 0, q.dtype)
+            out, _ = ops.add_rms_norm(None, residual, norm_w, s.rms_eps, partials=acc.unsqueeze(0),
+                                      unit_offset=s.norm_unit_offset, zero_partials=True)
+        else:
+            part = ops.gemv_attn(po, pml, meta.seq_lens, o.weight, o.fmt, o.out_features, o.in_features, None, 0,
+                                 q.dtype)
+            out, _ = ops.add_rms_norm(None, residual, norm_w, s.rms_eps, partials=part,
+                                      unit_offset=s.norm_unit_offset)
+        return out
+
     def _proj_residual_norm(self, x, proj, residual, norm_w, post_norm_w=None):
         """residual += proj(x); return rms_norm(residual) * norm_w."""
         s = self.spec
@@ -378,11 +414,14 @@ class NativeCausalLM(nn.Module):
                             s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale, cache.v_scale)
             if self._capture_q is not None:            # SnapKV observation window
                 self._capture_q[li] = q[-self._capture_w:].clone()
-            a = self._attention(li, attn, q, meta, cache)
-            if s.sandwich_norm:
+            if self._attn_oproj_fuse_ok(attn, q, meta):
+                x = self._attn_oproj_norm(li, attn, q, meta, cache, residual, layer.post_attention_layernorm)
+            elif s.sandwich_norm:
+                a = self._attention(li, attn, q, meta, cache)
                 x = self._proj_residual_norm(a, attn.o_proj, residual, layer.pre_feedforward_layernorm,
                                              post_norm_w=layer.post_attention_layernorm)
             else:
+                a = self._attention(li, attn, q, meta, cache)
                 x = self._proj_residual_norm(a, attn.o_proj, residual, layer.post_attention_layernorm)
             if li + 1 < len(self.layers):
                 nxt = self.layers[li + 1].input_layernorm

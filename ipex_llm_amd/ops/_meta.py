@@ -103,3 +103,18 @@ def _(x, blob, fmt, n, k, acc, ksplit):
 @register_fake("ipex_llm_amd::gemv_glu_in")
 def _(part, blob, fmt, n, k, act, ksplit, dtype):
     return part.new_empty((max(ksplit, 1), part.shape[1], n), dtype=torch.float32)
+
+
+@register_fake("ipex_llm_amd::attn_decode_split")
+def _(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, kv_fp8, k_scale, v_scale, alibi):
+    B, Tq, Hq, D = q.shape
+    return (q.new_empty((B, Hq, Tq, nsplit, D), dtype=torch.float32),
+            q.new_empty((B, Hq, Tq, nsplit, 2), dtype=torch.float32))
+
+
+@register_fake("ipex_llm_amd::gemv_attn")
+def _(po, pml, seq_lens, blob, fmt, n, k, acc, ksplit, dtype):
+    M = po.shape[0] * po.shape[2]
+    if acc is not None:
+        return torch.empty_like(acc)
+    return po.new_empty((max(ksplit, 1), M, n), dtype=torch.float32)

@@ -18,6 +18,7 @@ __all__ = [
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
+    "attn_decode_split", "gemv_attn",
 ]
 
 
@@ -285,3 +286,17 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, soft
         vv = gather_kv(v_cache, block_tables, b, L, kv_fp8, v_scale, q.dtype)
         outs.append(R.attention(q[b:b + 1], kk[None], vv[None], True, scale, softcap, window, None, alibi))
     return torch.cat(outs, 0)
+
+
+def attn_decode_split(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap=0.0, window=0,
+                      kv_fp8=0, k_scale=1.0, v_scale=1.0, alibi=None):
+    """flash-decoding split kernel only: (o, m, l) partials [B, Hq, Tq, nsplit, D] / [..., 2]
+    for a consumer that merges them itself (gemv_attn)."""
+    return _ops().attn_decode_split(q.contiguous(), k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
+                                    softcap, window, kv_fp8, k_scale, v_scale, alibi)
+
+
+def gemv_attn(po, pml, seq_lens, blob, fmt, n, k, acc=None, ksplit: int = 0, dtype=torch.bfloat16):
+    """o_proj over the attention partials (combined in the GEMV prologue):
+    atomics into ``acc`` [T, n] when given, else f32 split-K slabs [ks, T, n]."""
+    return _ops().gemv_attn(po, pml, seq_lens, blob, fmt, n, k, acc, ksplit, dtype)

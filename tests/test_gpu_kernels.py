@@ -186,6 +186,36 @@ def test_attn_decode(cuda, D, Tq, kv_fp8):
         assert _rel(out[b:b + 1], ref) < 1e-2, (b, L)
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("Tq", [1, 2])
+@pytest.mark.parametrize("atomic", [False, True])
+def test_attn_split_then_gemv_attn(cuda, D, Tq, atomic):
+    """o_proj over flash-decoding partials merged in the GEMV prologue ==
+    o_proj(attn_decode(...)) (combine kernel + plain GEMV)."""
+    torch.manual_seed(2)
+    B, Hq, Hkv, bs = 3, 8, 2, 64
+    lens = [5, 130, 700]
+    nblk_per = 12
+    bt = torch.randperm(B * nblk_per).view(B, nblk_per).int().to(cuda)
+    kc = torch.randn(B * nblk_per, Hkv, bs, D, device=cuda).bfloat16()
+    vc = torch.randn(B * nblk_per, Hkv, bs, D, device=cuda).bfloat16()
+    q = torch.randn(B, Tq, Hq, D, device=cuda).bfloat16()
+    seq = torch.tensor(lens, device=cuda, dtype=torch.int32)
+    nsplit = math.ceil(max(lens) / 64) + 2
+    f = get_format("sym_int4").fmt
+    n, k = 384, Hq * D
+    blob = ops.quantize(torch.randn(n, k, device=cuda) * 0.05, f)
+    o = ops.attn_decode(q, kc, vc, bt, seq, nsplit, D ** -0.5).reshape(B * Tq, k)
+    ref = R.lowbit_linear_ref(o, blob.cpu(), f, n, k).to(cuda)
+    po, pml = ops.attn_decode_split(q, kc, vc, bt, seq, nsplit, D ** -0.5)
+    if atomic:
+        acc = torch.zeros(B * Tq, n, device=cuda)
+        y = ops.gemv_attn(po, pml, seq, blob, f, n, k, acc)
+    else:
+        y = ops.gemv_attn(po, pml, seq, blob, f, n, k).sum(0)
+    assert _rel(y, ref) < 2e-3
+
+
 def test_moe_topk(cuda):
     logits = torch.randn(9, 64, device=cuda)
     w, ids = ops.moe_topk(logits, 4, True, 0)
