@@ -97,11 +97,8 @@ def main():
         seqs = [SequenceState(eng.cache.allocator.alloc(nblk)) for _ in range(B)]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        first = []
-        for b in range(B):
-            lg = eng.prefill(seqs[b], prompts[b])
-            first.append(torch.argmax(lg, -1))
-        cur = torch.cat(first)
+        # one batched prefill of the B prompts (projections as [B*P, K] GEMMs)
+        cur = torch.argmax(eng.prefill_batch(seqs, prompts), -1)
         torch.cuda.synchronize()
         if trial:
             ftl.append((time.perf_counter() - t0) * 1e3)

@@ -1,0 +1,294 @@
+// Low-bit weight x f16/bf16 activation GEMM for prefill-size M (> 64 rows):
+// the MFMA path of xe_linear.forward_new at prefill
+// (SRC/transformers/low_bit_linear.py:704-708; the reference dequantizes
+// inside its ESIMD/XeTLA GEMM, never to a dense weight in memory).
+//
+// MI355X design (gfx950, v_mfma_f32_16x16x32_f16, wave64):
+//   * workgroup = 4 waves = a 128 (n) x 128 (m) output block; wave w owns
+//     weight tiles 2w, 2w+1 (32 rows) against all 128 tokens, so each
+//     decoded A fragment feeds 8 MFMAs and each B fragment read from LDS
+//     feeds 2;
+//   * weights stream straight from the tiled device blob (formats.h): one
+//     16-B code load per lane per (tile, 128-k chunk) is exactly the MFMA A
+//     fragment of the 4 k-steps; codes are decoded and pre-scaled in f16
+//     registers ((q - 8) * d: exact code, one rounding), never written to
+//     memory (the dequantize + hipBLASLt path wrote 2 B per weight);
+//   * activations: the 128 x 128 x-chunk is staged global -> registers ->
+//     LDS as f16 (double buffered, one chunk ahead), padded rows (272 B) so
+//     the B-fragment ds_read_b128 of 16 rows hit distinct banks;
+//   * XCD-aware block order: the 8 m-blocks of one n-block run on one XCD
+//     (ids b, b + 8, ...), so a weight chunk comes from HBM once per XCD
+//     and is re-read by the other m-blocks from that XCD's L2.
+#include <type_traits>
+
+#include "../common/quant_block.h"
+#include "gemv_args.h"
+#include "illm_device.h"
+#include "kernels.h"
+
+namespace illm {
+
+typedef _Float16 gh2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ gh2 g_as_h2(uint32_t u) { return __builtin_bit_cast(gh2, u); }
+__device__ __forceinline__ uint32_t g_as_u(gh2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t g_bytes01(uint32_t u) { return __builtin_amdgcn_perm(0u, u, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t g_bytes23(uint32_t u) { return __builtin_amdgcn_perm(0u, u, 0x0c030c02u); }
+
+// pre-scaled f16 A fragment (8 weights of one k-step); d2 / m2 = (d, d) / (min, min)
+template <int DK>
+__device__ __forceinline__ uint4 gemm_a4(uint32_t u, gh2 d2, gh2 m2, const uint32_t* lut2) {
+  uint32_t w[4];
+  if constexpr (DK == DK_INT4S || DK == DK_INT4A) {
+    w[0] = (u & 0x000F000Fu) | 0x64006400u;
+    w[1] = ((u >> 4) & 0x000F000Fu) | 0x64006400u;
+    w[2] = ((u >> 8) & 0x000F000Fu) | 0x64006400u;
+    w[3] = ((u >> 12) & 0x000F000Fu) | 0x64006400u;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if constexpr (DK == DK_INT4S) w[i] = g_as_u((g_as_h2(w[i]) - gh2{(_Float16)1032.f, (_Float16)1032.f}) * d2);
+      else w[i] = g_as_u(__builtin_elementwise_fma(g_as_h2(w[i]) - gh2{(_Float16)1024.f, (_Float16)1024.f}, d2, m2));
+    }
+  } else {
+    if constexpr (DK == DK_FP4) {
+      w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 0));
+      w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 1));
+      w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 2));
+      w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(u, 1.0f, 3));
+    } else {  // DK_LUT4
+      w[0] = lut2[u & 0xff];
+      w[1] = lut2[(u >> 8) & 0xff];
+      w[2] = lut2[(u >> 16) & 0xff];
+      w[3] = lut2[u >> 24];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = g_as_u(g_as_h2(w[i]) * d2);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int DK>
+__device__ __forceinline__ uint4 gemm_a8(uint32_t lo, uint32_t hi, gh2 d2, gh2 m2) {
+  uint32_t w[4];
+  if constexpr (DK == DK_FP8E4 || DK == DK_FP8E5) {
+    if constexpr (DK == DK_FP8E4) {
+      w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(lo, 1.0f, false));
+      w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(lo, 1.0f, true));
+      w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(hi, 1.0f, false));
+      w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(hi, 1.0f, true));
+    } else {
+      w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(lo, 1.0f, false));
+      w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(lo, 1.0f, true));
+      w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(hi, 1.0f, false));
+      w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(hi, 1.0f, true));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = g_as_u(g_as_h2(w[i]) * d2);
+  } else {
+    // bytes -> f16(1024 + byte) via v_perm + magic; signed codes biased by 128
+    if constexpr (DK == DK_INT8S) { lo ^= 0x80808080u; hi ^= 0x80808080u; }
+    w[0] = g_bytes01(lo) | 0x64006400u;
+    w[1] = g_bytes23(lo) | 0x64006400u;
+    w[2] = g_bytes01(hi) | 0x64006400u;
+    w[3] = g_bytes23(hi) | 0x64006400u;
+    const _Float16 off = DK == DK_INT8S ? (_Float16)1152.f : (_Float16)1024.f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if constexpr (DK == DK_INT8S) w[i] = g_as_u((g_as_h2(w[i]) - gh2{off, off}) * d2);
+      else w[i] = g_as_u(__builtin_elementwise_fma(g_as_h2(w[i]) - gh2{off, off}, d2, m2));
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+constexpr int GBM = 128;          // tokens per block
+constexpr int GBN = 128;          // output features per block (8 tiles)
+constexpr int GLDX = 128 + 8;     // LDS row stride of the x chunk (halves)
+
+template <int DK, typename T>
+__global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
+  constexpr int BITS = dk_bits(DK);
+  __shared__ __attribute__((aligned(16))) uint16_t xs[2][GBM * GLDX];
+  __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // XCD-aware block order: the MB m-blocks of n-block nb get ids that share id % 8
+  const int NB = (a.N + GBN - 1) / GBN, MB = (a.M + GBM - 1) / GBM;
+  const int id = blockIdx.x;
+  const int grp = id / (8 * MB), rem = id % (8 * MB);
+  const int mb = rem / 8, nb = grp * 8 + rem % 8;
+  if (nb >= NB) return;
+  const int m0 = mb * GBM;
+  const int NT = (a.N + 15) / 16;
+  const int tile0 = nb * 8 + wave * 2;
+  const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
+  const uint8_t* tb[2];
+#pragma unroll
+  for (int t = 0; t < 2; t++) tb[t] = a.w + (size_t)min(tile0 + t, NT - 1) * TB;
+  const size_t soff = (size_t)a.KC * dk_code_chunk(DK) + (size_t)r16 * 4;   // + c * 64: row r16 of chunk c
+  const size_t moff = soff + (size_t)16 * a.KC * 4;
+
+  if constexpr (DK == DK_LUT4) {
+    lut2[tid] = pack2<F16>(hd_lut4(a.lut_fmt, tid & 15), hd_lut4(a.lut_fmt, tid >> 4));
+  }
+
+  // ---- x staging: thread -> rows (tid / 16) + 16 j, 8 columns at (tid % 16) * 8
+  uint4 xr[8];
+  auto stage_load = [&](int c) {
+    const int kk = c * 128 + (tid & 15) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int m = m0 + (tid >> 4) + 16 * j;
+      const bool ok = m < a.M && kk < a.K;
+      const uint4 v = *(const uint4*)(a.x + (size_t)(ok ? m : 0) * a.ldx + (ok ? kk : 0));
+      xr[j] = ok ? v : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint4 v = xr[j];
+      if constexpr (std::is_same<T, BF16>::value) {
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const float lo = fminf(fmaxf(bf16_to_f32(w[i] & 0xffff), -65504.f), 65504.f);
+          const float hi = fminf(fmaxf(bf16_to_f32(w[i] >> 16), -65504.f), 65504.f);
+          w[i] = pack2<F16>(lo, hi);
+        }
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      *(uint4*)(&xs[buf][((tid >> 4) + 16 * j) * GLDX + (tid & 15) * 8]) = v;
+    }
+  };
+
+  // ---- weight chunk records (A fragments of 4 k-steps) + row-r16 scales
+  struct WChunk {
+    uint4 q[2][BITS / 4];
+    uint32_t sc[2], mn[2];
+  };
+  auto load_w = [&](WChunk& wc, int c) {
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const uint8_t* rec = tb[t] + (size_t)c * dk_code_chunk(DK);
+      wc.q[t][0] = *(const uint4*)(rec + lane * 16);
+      if constexpr (BITS == 8) wc.q[t][1] = *(const uint4*)(rec + 1024 + lane * 16);
+      wc.sc[t] = *(const uint32_t*)(tb[t] + soff + (size_t)c * 64);
+      if constexpr (dk_has_min(DK)) wc.mn[t] = *(const uint32_t*)(tb[t] + moff + (size_t)c * 64);
+      else wc.mn[t] = 0u;
+    }
+  };
+
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int t = 0; t < 2; t++)
+#pragma unroll
+    for (int mt = 0; mt < 8; mt++) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // weight ring: PFW chunks in flight (one chunk of MFMA work, ~1k cycles,
+  // does not cover an HBM round trip under load); loads are unconditional
+  // (clamped) so hipcc keeps counted vmcnt waits
+  constexpr int PFW = 4;
+  const int KC = a.KC;
+  auto load_wc = [&](WChunk& wc, int c) { load_w(wc, min(c, KC - 1)); };
+  WChunk ring[PFW];
+#pragma unroll
+  for (int u = 0; u < PFW; u++) load_wc(ring[u], u);
+  stage_load(0);
+  stage_store(0);
+  __syncthreads();
+
+  auto pick = [](uint32_t v, int blk) -> gh2 {
+    return g_as_h2(__builtin_amdgcn_perm(0u, v, blk == 0 ? 0x01000100u : 0x03020302u));
+  };
+  auto compute = [&](const WChunk& cur, int buf) {
+    const uint16_t* xb = &xs[buf][r16 * GLDX + 8 * g];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const int blk = s >> 1;
+      uint4 A[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const gh2 d2 = pick(cur.sc[t], blk);
+        const gh2 m2 = dk_has_min(DK) ? pick(cur.mn[t], blk) : gh2{(_Float16)0.f, (_Float16)0.f};
+        if constexpr (BITS == 4) {
+          const uint4& q0 = cur.q[t][0];
+          const uint32_t w = s == 0 ? q0.x : (s == 1 ? q0.y : (s == 2 ? q0.z : q0.w));
+          A[t] = gemm_a4<DK>(w, d2, m2, lut2);
+        } else {
+          const uint4& qq = cur.q[t][blk];
+          A[t] = (s & 1) == 0 ? gemm_a8<DK>(qq.x, qq.y, d2, m2) : gemm_a8<DK>(qq.z, qq.w, d2, m2);
+        }
+      }
+      uint4 B[8];
+#pragma unroll
+      for (int mt = 0; mt < 8; mt++) B[mt] = *(const uint4*)(xb + mt * 16 * GLDX + 32 * s);
+#pragma unroll
+      for (int mt = 0; mt < 8; mt++) {
+        acc[0][mt] = mfma16<F16>(A[0], B[mt], acc[0][mt]);
+        acc[1][mt] = mfma16<F16>(A[1], B[mt], acc[1][mt]);
+      }
+    }
+  };
+  for (int c0 = 0; c0 < KC; c0 += PFW) {
+#pragma unroll
+    for (int u = 0; u < PFW; u++) {
+      const int c = c0 + u;
+      if (c < KC) {                        // block-uniform
+        const bool more = c + 1 < KC;
+        if (more) stage_load(c + 1);
+        compute(ring[u], c & 1);
+        load_wc(ring[u], c + PFW);
+        if (more) stage_store((c + 1) & 1);
+        __syncthreads();
+      }
+    }
+  }
+
+  // ---- epilogue: lane holds out[m0 + 16 mt + r16][16 tile + 4 g + i]
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    const int tile = tile0 + t;
+    if (tile >= NT) continue;
+    const int n0 = tile * 16 + 4 * g;
+    if (n0 >= a.N) continue;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias)
+#pragma unroll
+      for (int i = 0; i < 4; i++) bv[i] = n0 + i < a.N ? to_f32<T>(a.bias[n0 + i]) : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 8; mt++) {
+      const int m = m0 + mt * 16 + r16;
+      if (m >= a.M) continue;
+      const float o[4] = {acc[t][mt][0] + bv[0], acc[t][mt][1] + bv[1], acc[t][mt][2] + bv[2],
+                          acc[t][mt][3] + bv[3]};
+      uint16_t* y = a.out + (size_t)m * a.ldo + n0;
+      if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+      else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+    }
+  }
+}
+
+template <int DK>
+static void launch_gemm_dk(bool bf16, const GemmArgs& a, hipStream_t st) {
+  const int NB = (a.N + GBN - 1) / GBN, MB = (a.M + GBM - 1) / GBM;
+  const int NBp = (NB + 7) / 8 * 8;
+  dim3 grid((unsigned)(NBp * MB));
+  if (bf16) hipLaunchKernelGGL((lowbit_gemm_kernel<DK, BF16>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((lowbit_gemm_kernel<DK, F16>), grid, dim3(256), 0, st, a);
+}
+
+void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st) {
+  switch (fmt_to_dk(fmt)) {
+    case DK_INT4S: launch_gemm_dk<DK_INT4S>(bf16, a, st); break;
+    case DK_INT4A: launch_gemm_dk<DK_INT4A>(bf16, a, st); break;
+    case DK_LUT4: launch_gemm_dk<DK_LUT4>(bf16, a, st); break;
+    case DK_FP4: launch_gemm_dk<DK_FP4>(bf16, a, st); break;
+    case DK_INT8S: launch_gemm_dk<DK_INT8S>(bf16, a, st); break;
+    case DK_INT8A: launch_gemm_dk<DK_INT8A>(bf16, a, st); break;
+    case DK_FP8E4: launch_gemm_dk<DK_FP8E4>(bf16, a, st); break;
+    case DK_FP8E5: launch_gemm_dk<DK_FP8E5>(bf16, a, st); break;
+  }
+}
+
+}  // namespace illm

@@ -29,6 +29,19 @@ constexpr size_t gemv5_shmem_h(int rows, int cpk) {
   return ((size_t)rows * gemv5_x_ld_h(cpk * 128) * 2 + 15) / 16 * 16 + (size_t)rows * cpk * 16 + 8 * 2 * 64 * 16;
 }
 
+// ---- prefill low-bit GEMM (gemm.hip): out[M, N] = x[M, K] @ W^T (+ bias), f16 MFMA
+struct GemmArgs {
+  const uint16_t* x;       // [M, ldx] T
+  int M, K, ldx;
+  const uint8_t* w;        // tiled device blob
+  int N, KC;
+  const uint16_t* bias;    // T [N] or null
+  uint16_t* out;           // [M, ldo] T
+  int ldo;
+  int lut_fmt;
+};
+void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st);
+
 // ---- norms (norm.hip) ------------------------------------------------------
 struct NormArgs {
   const uint16_t* x;       // [M, H] input (ignored when partials != null)

@@ -212,6 +212,36 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   return out;
 }
 
+// prefill-size low-bit GEMM: MFMA with in-register dequant of the tiled weight
+Tensor gemm(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, const c10::optional<Tensor>& bias) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda(), "gemm: GPU tensors expected");
+  TORCH_CHECK(x.size(-1) == k, "gemm: x last dim ", x.size(-1), " != in_features ", k);
+  TORCH_CHECK(k % 8 == 0, "gemm: in_features must be a multiple of 8");
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  const int64_t M = xc.numel() / k;
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemm: weight blob too small");
+  auto shape = xc.sizes().vec();
+  shape.back() = n;
+  Tensor out = at::empty(shape, xc.options());
+  if (M == 0) return out;
+  illm::GemmArgs a{};
+  a.x = p16(xc);
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.N = (int)n;
+  a.KC = (int)(illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K);
+  a.bias = p16o(bias);
+  a.out = m16(out);
+  a.ldo = (int)n;
+  a.lut_fmt = (int)fmt;
+  illm::launch_lowbit_gemm(bf16, (int)fmt, a, cur_stream());
+  return out;
+}
+
 // split-K GEMV accumulated with f32 atomics into acc [M, n] (zero on entry;
 // the consumer -- add_rms_norm / rope_kv_fused with zero_*=True -- reads the
 // single slab and re-zeroes it, so no ks-slab reduction is ever needed)
@@ -741,6 +771,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("dequantize_device", &dequantize_device);
   m.impl("gemv", &gemv);
   m.impl("gemv_accum", &gemv_accum);
+  m.impl("gemm", &gemm);
   m.impl("attn_decode_split", &attn_decode_split);
   m.impl("gemv_attn", &gemv_attn);
   m.impl("add_rms_norm", &add_rms_norm);

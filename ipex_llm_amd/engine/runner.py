@@ -203,6 +203,24 @@ class Engine:
         return logits
 
     @torch.no_grad()
+    def prefill_batch(self, seqs: List[SequenceState], ids: torch.Tensor) -> torch.Tensor:
+        """Prefill B equal-length prompts (ids [B, n]) in ONE forward: the
+        projections run as [B*n, K] GEMMs (weights read once for the whole
+        batch), attention per sequence.  Returns last-token logits [B, V]."""
+        m, c = self.model, self.cache
+        dev = m.device
+        B, n = ids.shape
+        pos = torch.arange(n, device=dev).repeat(B)
+        slots = torch.cat([slots_for(s, 0, n, c.bs) for s in seqs]).to(dev)
+        bt = make_block_table(seqs, max(len(s.blocks) for s in seqs), dev)
+        meta = AttnMeta(B, n, bt, torch.full((B,), n, dtype=torch.int32, device=dev), nsplit_for(n), [n] * B)
+        logits = m.forward_tokens(ids.reshape(-1).to(dev), pos, slots, meta, c,
+                                  logits_idx=torch.arange(B, device=dev) * n + (n - 1))
+        for s in seqs:
+            s.length = n
+        return logits
+
+    @torch.no_grad()
     def forward_chunk(self, seq: SequenceState, tokens: Sequence[int], start: int) -> torch.Tensor:
         """Run ``tokens`` of one sequence at positions start.. (KV written,
         ``seq.length`` = start + n); returns f32 logits for every token [n, V].

@@ -118,3 +118,10 @@ def _(po, pml, seq_lens, blob, fmt, n, k, acc, ksplit, dtype):
     if acc is not None:
         return torch.empty_like(acc)
     return po.new_empty((max(ksplit, 1), M, n), dtype=torch.float32)
+
+
+@register_fake("ipex_llm_amd::gemm")
+def _(x, blob, fmt, n, k, bias):
+    shape = list(x.shape)
+    shape[-1] = n
+    return x.new_empty(shape)
