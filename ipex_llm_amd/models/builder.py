@@ -25,8 +25,7 @@ from .decoder import (DecoderSpec, NativeAttention, NativeCausalLM, NativeLayer,
 # model types executed by the native decoder (others fall back to the HF
 # forward with low-bit linears, like the reference does for e.g. mixtral)
 NATIVE_DENSE = {"llama", "mistral", "qwen2", "qwen3", "gemma", "gemma2", "phi3", "internlm2", "yi",
-                "aquila", "starcoder2_llama", "olmo2", "granite", "deepseek", "minicpm", "stablelm",
-                "baichuan", "yuan"}
+                "aquila", "olmo2", "deepseek", "minicpm", "baichuan", "yuan"}
 NATIVE_MOE = {"mixtral", "qwen2_moe", "qwen3_moe"}
 
 

@@ -34,7 +34,9 @@ logger = logging.getLogger("ipex_llm_amd")
 
 # architectures whose decoder runs on the native engine
 NATIVE_ARCHS = {"llama", "mistral", "qwen2", "qwen3", "gemma", "gemma2", "phi3", "internlm2", "yi",
-                "aquila", "granite", "olmo2", "stablelm", "minicpm", "starcoder2"}
+                "aquila", "olmo2", "minicpm"}
+# granite (embedding/residual/logit multipliers), stablelm (partial rotary + LayerNorm) and
+# starcoder2 (biased LayerNorm MLP, no q_proj split) take the HF forward over low-bit linears.
 MOE_ARCHS = {"mixtral", "qwen2_moe", "qwen3_moe"}
 
 
@@ -70,11 +72,13 @@ def _merge_qkv(attn: nn.Module):
                 any(m.g_idx_map is not None for m in mods):
             return                                           # different act-order permutations
         attn.qkv_proj = lowbit_row_concat(mods)
+        attn._illm_qkv_split = tuple(m.out_features for m in mods)
         del attn.q_proj, attn.k_proj, attn.v_proj
         return
     if not all(isinstance(m, nn.Linear) for m in mods):
         return
     attn.qkv_proj = _merge_linears([attn.q_proj, attn.k_proj, attn.v_proj])
+    attn._illm_qkv_split = tuple(m.out_features for m in mods)
     del attn.q_proj, attn.k_proj, attn.v_proj
 
 
@@ -237,6 +241,10 @@ def _optimize_post(model: nn.Module):
     if (mt in NATIVE_ARCHS or mt in MOE_ARCHS) and getattr(model, "_illm_pre", False):
         from .hf_native import attach_native
         attach_native(model)
+        if not getattr(model, "_illm_native_attached", False):
+            # variant the native decoder cannot run: HF forward over the merged weights
+            from .hf_views import restore_hf_views
+            restore_hf_views(model)
     return model
 
 
