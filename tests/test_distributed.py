@@ -107,6 +107,54 @@ def test_pipeline_parallel_generate_matches_single(tmp_path):
     _run(_pp_worker, 2, p, {"ids": ids.tolist(), "out": out.tolist()})
 
 
+PP_PROMPTS = [list(range(3, 30)), [5, 9, 11], list(range(40, 47)), list(range(100, 161)), [7, 7, 8, 9]]
+
+
+def _ppw_run(m, world_rank0: bool = True):
+    from ipex_llm_amd.serving.engine import SamplingParams
+    from ipex_llm_amd.serving.pp_worker import PPModelWorker
+    # 2 sequences per slot, one prefill per tick, 16-token prefill chunks:
+    # exercises admission, partial prefill and decode in flight together
+    w = PPModelWorker(m, max_num_seqs=2, max_prefilled_seqs=1, prefill_chunk=16, max_model_len=128)
+    if w.is_head:
+        out = w.generate(PP_PROMPTS, SamplingParams(max_new_tokens=6))
+        w.stop()
+        return out, w.stats
+    w.serve_forever()
+    return None, w.stats
+
+
+def _ppw_worker(rank, world, port, path, want):
+    _init(rank, world, port)
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    m = AutoModelForCausalLM.from_pretrained(path, load_in_low_bit="sym_int8", torch_dtype=torch.float32,
+                                             pipeline_parallel_stages=world)
+    out, stats = _ppw_run(m)
+    if rank == 0:
+        assert out == want, (out, want)
+        assert stats["ticks"] > stats["bubbles"]
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+def test_pp_serving_worker_matches_single(tmp_path):
+    """PPModelWorker (micro-batched pipeline serving, reference
+    pipeline_parallel.py:448-927): world 1 and a 2-stage gloo pipeline both
+    reproduce the static engine's greedy tokens."""
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    from ipex_llm_amd.transformers.hf_native import get_native
+    p = str(tmp_path / "m")
+    _tiny_llama(p)
+    m = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32)
+    nm, _ = get_native(m)
+    ref = Engine(nm).generate(PP_PROMPTS, max_new_tokens=6, use_graph=False)
+    want = [r[len(q):] for r, q in zip(ref, PP_PROMPTS)]
+    single, _ = _ppw_run(nm)
+    assert single == want
+    _run(_ppw_worker, 2, p, want)
+
+
 def _coll_worker(rank, world, port):
     _init(rank, world, port)
     from ipex_llm_amd.parallel import comm
