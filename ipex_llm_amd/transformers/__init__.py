@@ -5,3 +5,4 @@ from .model import (AutoModelForCausalLM, AutoModel, AutoModelForSpeechSeq2Seq, 
                     AutoModelForQuestionAnswering, AutoModelForNextSentencePrediction,
                     AutoModelForMultipleChoice, AutoModelForTokenClassification, save_low_bit)
 from .convert import ggml_convert_low_bit  # noqa: F401
+from .hybrid import convert_model_hybrid  # noqa: F401
