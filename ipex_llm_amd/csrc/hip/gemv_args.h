@@ -77,6 +77,20 @@ struct GemvArgs {
   const float* aml;        // [B, Hq, Tq, ans, 2] (max, sum)
   const int32_t* alens;    // [B] keys per sequence (valid splits = ceil(len / 64))
   int ans, aD, aHq, aTq;
+  // v5 residual-add + RMSNorm prologue (decode, M <= 16): the input row is
+  // x = w * rms_norm(h), h = round(round(nacc) + nres), computed per workgroup
+  // over the full row (sum of squares) and staged for its K slice; workgroup
+  // (0, 0) writes h to nres_out (the caller ping-pongs residual buffers).
+  const float* nacc;       // [M, K] f32 atomic accumulator of the previous projection
+  const uint16_t* nres;    // [M, K] residual in
+  uint16_t* nres_out;      // [M, K] residual out
+  const uint16_t* nweight; // [K] norm weight
+  float neps;
+  int nunit;               // weight is stored as (w - 1) (gemma-style unit offset)
+  // workgroup (0, 0) zeroes nzero[0:nzero_n] on entry: an atomic accumulator
+  // whose readers all finished before this launch (stream order)
+  float* nzero;
+  int nzero_n;
 };
 
 }  // namespace illm

@@ -248,6 +248,60 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
     __syncthreads();
   }
 
+  // ---- zero a consumed atomic accumulator (its readers ran earlier in the stream)
+  if (a.nzero && blockIdx.x == 0 && blockIdx.y == 0) {
+    for (int i = threadIdx.x * 4; i < a.nzero_n; i += NW * 64 * 4)
+      *(float4*)(a.nzero + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  // ---- residual-add + RMSNorm prologue (replaces the standalone norm launch):
+  // h = rnd(rnd(acc) + res) exactly as add_rms_norm rounds it; every workgroup
+  // needs 1/rms of the FULL row (16 KB f32 + 8 KB residual per row, L2-resident)
+  __shared__ float ninv[16];
+  auto rnd = [](float v) { return to_f32<T>(from_f32<T>(v)); };
+  auto ni_h = [&](int m, int k, float* h) {
+    const float4* p = (const float4*)(a.nacc + (size_t)m * a.K + k);
+    const float4 p0 = p[0], p1 = p[1];
+    const uint4 r = *(const uint4*)(a.nres + (size_t)m * a.K + k);
+    const float av[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+    const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      h[2 * i] = rnd(rnd(av[2 * i]) + to_f32<T>((uint16_t)(rw[i] & 0xffff)));
+      h[2 * i + 1] = rnd(rnd(av[2 * i + 1]) + to_f32<T>((uint16_t)(rw[i] >> 16)));
+    }
+  };
+  if (a.nacc) {
+    if (threadIdx.x < 16) ninv[threadIdx.x] = 0.f;
+    __syncthreads();
+    const bool wres = a.nres_out != nullptr && blockIdx.x == 0 && blockIdx.y == 0;
+    const int vpr = a.K / 8;
+    uint16_t* xst = (uint16_t*)smem;
+    const int ldxs = gemv5_x_ld(kw);
+    for (int m = 0; m < Mloc; m++) {
+      float ss = 0.f;
+#pragma unroll 2
+      for (int v = threadIdx.x; v < vpr; v += NW * 64) {
+        float h[8];
+        ni_h(m, v * 8, h);
+#pragma unroll
+        for (int i = 0; i < 8; i++) ss += h[i] * h[i];
+        const uint4 hp =
+            make_uint4(pack2<T>(h[0], h[1]), pack2<T>(h[2], h[3]), pack2<T>(h[4], h[5]), pack2<T>(h[6], h[7]));
+        if (wres) *(uint4*)(a.nres_out + (size_t)m * a.K + v * 8) = hp;
+        // this workgroup's K slice: keep h (exact in T) in the x staging area,
+        // the staging pass below normalises it in place (no second global read)
+        const int kk = v * 8 - kbase;
+        if (kk >= 0 && kk < kw) *(uint4*)(xst + m * ldxs + kk) = hp;
+      }
+      ss = wave_sum(ss);
+      if (lane == 0) atomicAdd(&ninv[m], ss);
+    }
+    __syncthreads();
+    if (threadIdx.x < Mloc) ninv[threadIdx.x] = rsqrtf(ninv[threadIdx.x] / (float)a.K + a.neps);
+    __syncthreads();
+  }
+
   // ---- stage x[0:Mloc, kbase:kbase+kw] -> LDS in C
   {
     const int vpr = kw / 8;
@@ -315,6 +369,34 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
           w[i] = pack2<C>(o2[0], o2[1]);
         }
         val = make_uint4(w[0], w[1], w[2], w[3]);
+      } else if (kbase + kk < a.K && a.nacc) {
+        // normalised residual stream: w * rnd(h * inv), rounded to T like the norm kernel's output
+        float h[8];
+        {
+          const uint4 hq = *(const uint4*)(xs + m * ldx + kk);      // h of the prologue, exact in T
+          const uint32_t hw[4] = {hq.x, hq.y, hq.z, hq.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            h[2 * i] = to_f32<T>((uint16_t)(hw[i] & 0xffff));
+            h[2 * i + 1] = to_f32<T>((uint16_t)(hw[i] >> 16));
+          }
+        }
+        const float inv = ninv[m];
+        const uint4 wq = *(const uint4*)(a.nweight + kbase + kk);
+        const uint32_t wv[4] = {wq.x, wq.y, wq.z, wq.w};
+        uint32_t o4[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          float w0 = to_f32<T>((uint16_t)(wv[i] & 0xffff)), w1 = to_f32<T>((uint16_t)(wv[i] >> 16));
+          if (a.nunit) { w0 = rnd(1.f + w0); w1 = rnd(1.f + w1); }
+          float v0 = rnd(w0 * rnd(h[2 * i] * inv)), v1 = rnd(w1 * rnd(h[2 * i + 1] * inv));
+          if constexpr (!std::is_same<C, T>::value) {
+            v0 = fminf(fmaxf(v0, -65504.f), 65504.f);
+            v1 = fminf(fmaxf(v1, -65504.f), 65504.f);
+          }
+          o4[i] = pack2<C>(v0, v1);
+        }
+        val = make_uint4(o4[0], o4[1], o4[2], o4[3]);
       } else if (kbase + kk < a.K) {
         val = *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk);
         if constexpr (!std::is_same<C, T>::value) {   // bf16 activations -> f16 (LUT formats)

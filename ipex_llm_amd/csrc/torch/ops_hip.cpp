@@ -245,8 +245,83 @@ Tensor gemm(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
 // split-K GEMV accumulated with f32 atomics into acc [M, n] (zero on entry;
 // the consumer -- add_rms_norm / rope_kv_fused with zero_*=True -- reads the
 // single slab and re-zeroes it, so no ks-slab reduction is ever needed)
+static void set_zero(illm::GemvArgs& a, const c10::optional<Tensor>& zero) {
+  if (zero.has_value() && zero->defined()) {
+    TORCH_CHECK(zero->is_cuda() && zero->scalar_type() == at::kFloat && zero->is_contiguous() &&
+                    zero->numel() % 4 == 0, "zero: contiguous f32 buffer with a multiple of 4 elements");
+    a.nzero = zero->data_ptr<float>();
+    a.nzero_n = (int)zero->numel();
+  }
+}
+
+// Decode projection whose input is rms_norm(residual + acc_in) * w, computed in
+// the GEMV prologue (no standalone norm launch).  acc_in: the previous
+// projection's atomic accumulator [M, k] f32 (read only; the caller zeroes it
+// through a later launch's `zero`), residual -> res_out (= residual + acc_in,
+// written once).  epi: EPI_ATOMIC (out = acc_out [M, n] f32, zero on entry) or
+// EPI_GLU (returns act(gate) * up [M, n / 2] in dt).
+Tensor gemv_norm_in(const Tensor& acc_in, const Tensor& residual, Tensor& res_out, const Tensor& norm_w, double eps,
+                    bool unit_offset, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t epi,
+                    int64_t act, const c10::optional<Tensor>& acc_out, const c10::optional<Tensor>& zero) {
+  TORCH_CHECK(acc_in.is_cuda() && blob.is_cuda() && residual.is_cuda(), "gemv_norm_in: GPU tensors expected");
+  c10::DeviceGuard g(acc_in.device());
+  const bool bf16 = is_bf16(residual);
+  const int64_t M = residual.numel() / k;
+  TORCH_CHECK(M >= 1 && M <= 16, "gemv_norm_in handles 1..16 rows, got ", M);
+  TORCH_CHECK(k % 8 == 0 && norm_w.numel() == k && residual.is_contiguous() && res_out.is_contiguous() &&
+                  res_out.numel() == M * k && residual.scalar_type() == res_out.scalar_type() &&
+                  norm_w.scalar_type() == residual.scalar_type(),
+              "gemv_norm_in: residual/res_out [M, k] and norm weight [k] of one 16-bit dtype");
+  TORCH_CHECK(acc_in.scalar_type() == at::kFloat && acc_in.is_contiguous() && acc_in.numel() == M * k,
+              "gemv_norm_in: acc_in must be contiguous f32 [M, k]");
+  TORCH_CHECK(res_out.data_ptr() != residual.data_ptr(), "gemv_norm_in: res_out must not alias residual");
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemv_norm_in: weight blob too small");
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  illm::GemvArgs a{};
+  a.x = nullptr;
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.KC = (int)KC;
+  a.act = (int)act;
+  a.lut_fmt = (int)fmt;
+  a.nacc = acc_in.data_ptr<float>();
+  a.nres = p16(residual);
+  a.nres_out = m16(res_out);
+  a.nweight = p16(norm_w);
+  a.neps = (float)eps;
+  a.nunit = unit_offset ? 1 : 0;
+  set_zero(a, zero);
+  if (epi == illm::EPI_GLU) {
+    TORCH_CHECK(n % 32 == 0, "GLU weights must have a multiple of 32 rows");
+    Tensor out = at::empty({M, n / 2}, residual.options());
+    a.N = (int)(n / 2);
+    a.out = out.data_ptr();
+    a.ldo = (int)(n / 2);
+    const Plan5 p = plan5(M, NT / 2, KC, false);
+    TORCH_CHECK(p.shmem <= kMaxLds, "gemv_norm_in: K slice too large for LDS");
+    a.nw = p.nw;
+    launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_GLU, dim3(p.gx, 1), p.shmem, a);
+    return out;
+  }
+  TORCH_CHECK(epi == illm::EPI_ATOMIC && acc_out.has_value() && acc_out->defined() &&
+                  acc_out->scalar_type() == at::kFloat && acc_out->is_contiguous() && acc_out->numel() == M * n,
+              "gemv_norm_in: EPI_ATOMIC needs acc_out, contiguous f32 [M, n]");
+  a.N = (int)n;
+  a.out = acc_out->data_ptr();
+  a.ldo = (int)n;
+  const Plan5 p = plan5(M, NT, KC, true, 0, true);
+  TORCH_CHECK(p.shmem <= kMaxLds, "gemv_norm_in: K slice too large for LDS");
+  a.cpk = (int)p.cpk;
+  a.nw = p.nw;
+  launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_ATOMIC, dim3(p.gx, (unsigned)p.ks), p.shmem, a);
+  return *acc_out;
+}
+
 void gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, Tensor& acc,
-                int64_t ksplit) {
+                int64_t ksplit, const c10::optional<Tensor>& zero) {
   TORCH_CHECK(x.is_cuda() && blob.is_cuda() && acc.is_cuda(), "gemv_accum: GPU tensors expected");
   c10::DeviceGuard g(x.device());
   const bool bf16 = is_bf16(x);
@@ -272,6 +347,7 @@ void gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   const Plan5 p = plan5(M, NT, KC, true, ksplit, true);
   a.cpk = (int)p.cpk;
   a.nw = p.nw;
+  set_zero(a, zero);
   TORCH_CHECK(p.shmem <= kMaxLds, "gemv_accum: K slice too large for LDS");
   launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_ATOMIC, dim3(p.gx, (unsigned)p.ks), p.shmem, a);
 }
@@ -771,6 +847,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("dequantize_device", &dequantize_device);
   m.impl("gemv", &gemv);
   m.impl("gemv_accum", &gemv_accum);
+  m.impl("gemv_norm_in", &gemv_norm_in);
   m.impl("gemm", &gemm);
   m.impl("attn_decode_split", &attn_decode_split);
   m.impl("gemv_attn", &gemv_attn);

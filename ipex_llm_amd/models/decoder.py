@@ -268,11 +268,12 @@ class NativeCausalLM(nn.Module):
             outs.append(o[0].transpose(0, 1)[None])
         return torch.cat(outs, 0).reshape(T, s.num_heads * s.head_dim)
 
-    def _acc(self, n: int, t: int, device) -> torch.Tensor:
+    def _acc(self, n: int, t: int, device, tag: str = "") -> torch.Tensor:
         """Zeroed f32 [t, n] accumulator for the split-K atomic GEMV
-        (ops.gemv_accum); its consumer re-zeroes it after reading, so one
+        (ops.gemv_accum); its consumer re-zeroes it after reading (or a later
+        launch does, ``tag``-separated buffers of the norm-in path), so one
         buffer per shape serves every layer and every hipGraph replay."""
-        key = (n, t)
+        key = (n, t, tag)
         buf = self._acc_bufs.get(key)
         if buf is None or buf.device != device:
             buf = torch.zeros(t, n, dtype=torch.float32, device=device)
@@ -341,6 +342,27 @@ class NativeCausalLM(nn.Module):
         out, _ = ops.add_rms_norm(y.contiguous(), residual, norm_w, s.rms_eps, unit_offset=s.norm_unit_offset)
         return out
 
+    # decode (T <= ACC_MAX_M) with the residual add + RMSNorm folded into the
+    # prologue of the GEMV that consumes them (qkv, gate/up): two norm
+    # launches per layer fewer.  ILLM_NORM_IN=0 restores the standalone norms.
+    _norm_in_env = __import__("os").environ.get("ILLM_NORM_IN", "1") != "0"
+
+    def _norm_in_ok(self, ref: torch.Tensor, T: int) -> bool:
+        if not (self._norm_in_env and T <= ACC_MAX_M and ref.is_cuda and self.tp_group is None
+                and not self.spec.sandwich_norm and not self._attn_fuse and not self._glu_in_enabled
+                and self.spec.hidden_size % 8 == 0 and ops.native_gpu(ref)):
+            return False
+        ok = self.__dict__.get("_norm_in_layers")
+        if ok is None:
+            def lowbit(m, bias_ok=False):
+                return isinstance(m, LowBitLinear) and m.mp_group is None and (bias_ok or m.bias is None)
+            ok = all(isinstance(L.mlp, NativeMLP) and lowbit(L.mlp.gate_up_proj) and lowbit(L.mlp.down_proj)
+                     and lowbit(L.self_attn.o_proj) and lowbit(L.self_attn.qkv_proj, True)
+                     and (L.self_attn.qkv_proj.bias is None or L.self_attn.qkv_proj.bias.dtype == ref.dtype)
+                     and L.post_feedforward_layernorm is None for L in self.layers)
+            self.__dict__["_norm_in_layers"] = ok
+        return ok
+
     def _fused_mlp_ok(self, x, layer) -> bool:
         mlp = layer.mlp
         if not (x.is_cuda and isinstance(mlp, NativeMLP) and x.shape[0] <= 16 and self.tp_group is None):
@@ -389,6 +411,14 @@ class NativeCausalLM(nn.Module):
         x = ops.rms_norm(residual, self.layers[0].input_layernorm, s.rms_eps, s.norm_unit_offset)
         T = ids.shape[0]
         rope = self.rope_cache if self.rope_cache is not None else self.inv_freq
+        # norm-in decode: the down projection's atomic accumulator stays pending
+        # and the next layer's qkv GEMV adds + normalises it in its prologue;
+        # the residual ping-pongs between two buffers (written by one workgroup)
+        norm_in = self._norm_in_ok(residual, T)
+        pend = None                     # accumulator awaiting residual-add + norm
+        consumed = None                 # accumulator read by the last launch: zeroed by the next GEMV
+        res_pp = (residual, torch.empty_like(residual)) if norm_in else None
+        nxt_res = lambda r: res_pp[1] if r is res_pp[0] else res_pp[0]
         for li, layer in enumerate(self.layers):
             attn = layer.self_attn
             qp = attn.qkv_proj
@@ -399,7 +429,13 @@ class NativeCausalLM(nn.Module):
                 # T <= 16 accumulates with atomics into one zeroed slab (re-zeroed by the kernel)
                 if T <= ACC_MAX_M:
                     part = self._acc(qp.out_features, T, x.device)
-                    ops.gemv_accum(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, part)
+                    if pend is not None:
+                        r2 = nxt_res(residual)
+                        ops.gemv_norm_in(pend, residual, r2, layer.input_layernorm, s.rms_eps, s.norm_unit_offset,
+                                         qp.weight, qp.fmt, qp.out_features, qp.in_features, False, acc_out=part)
+                        residual, consumed, pend = r2, pend, None
+                    else:
+                        ops.gemv_accum(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, part)
                     part = part.unsqueeze(0)
                 else:
                     part = ops.gemv_partials(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, 0)
@@ -414,6 +450,30 @@ class NativeCausalLM(nn.Module):
                             s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale, cache.v_scale)
             if self._capture_q is not None:            # SnapKV observation window
                 self._capture_q[li] = q[-self._capture_w:].clone()
+            if norm_in:
+                # o_proj -> atomic slab P (zeroing the slab the qkv prologue consumed);
+                # the gate/up GEMV adds P to the residual and normalises in its prologue;
+                # down -> atomic slab D (zeroing P), pending for the next layer's qkv
+                a = self._attention(li, attn, q, meta, cache)
+                o, mlp = attn.o_proj, layer.mlp
+                H = o.out_features
+                accP, accD = self._acc(H, T, x.device, "P"), self._acc(H, T, x.device, "D")
+                ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
+                r2 = nxt_res(residual)
+                gu, dn = mlp.gate_up_proj, mlp.down_proj
+                act = ops.gemv_norm_in(accP, residual, r2, layer.post_attention_layernorm, s.rms_eps,
+                                       s.norm_unit_offset, gu.weight, gu.fmt, gu.out_features, gu.in_features, True,
+                                       s.act)
+                residual = r2
+                ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=accP)
+                consumed = None
+                if li + 1 < len(self.layers):
+                    pend = accD
+                else:   # last layer: the final (or stage-boundary) norm reads and re-zeroes D
+                    nxt = self.norm if self.last_stage else layer.input_layernorm
+                    x, _ = ops.add_rms_norm(None, residual, nxt, s.rms_eps, partials=accD.unsqueeze(0),
+                                            unit_offset=s.norm_unit_offset, zero_partials=True)
+                continue
             if self._attn_oproj_fuse_ok(attn, q, meta):
                 x = self._attn_oproj_norm(li, attn, q, meta, cache, residual, layer.post_attention_layernorm)
             elif s.sandwich_norm:

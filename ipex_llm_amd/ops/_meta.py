@@ -96,8 +96,15 @@ def _(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_no
 
 
 @register_fake("ipex_llm_amd::gemv_accum")
-def _(x, blob, fmt, n, k, acc, ksplit):
+def _(x, blob, fmt, n, k, acc, ksplit, zero=None):
     return None
+
+
+@register_fake("ipex_llm_amd::gemv_norm_in")
+def _(acc_in, residual, res_out, norm_w, eps, unit_offset, blob, fmt, n, k, epi, act, acc_out=None, zero=None):
+    if epi == 2:
+        return residual.new_empty((residual.numel() // k, n // 2))
+    return torch.empty_like(acc_out)
 
 
 @register_fake("ipex_llm_amd::gemv_glu_in")

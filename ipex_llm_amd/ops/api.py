@@ -18,7 +18,7 @@ __all__ = [
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
-    "attn_decode_split", "gemv_attn",
+    "attn_decode_split", "gemv_attn", "gemv_norm_in",
 ]
 
 
@@ -96,14 +96,41 @@ def gemv_partials(x, blob, fmt, n, k, ksplit: int) -> torch.Tensor:
     return _ops().gemv(x, blob, fmt, n, k, None, 1, ksplit, 0)
 
 
-def gemv_accum(x, blob, fmt, n, k, acc: torch.Tensor, ksplit: int = 0) -> torch.Tensor:
+def gemv_accum(x, blob, fmt, n, k, acc: torch.Tensor, ksplit: int = 0,
+               zero: Optional[torch.Tensor] = None) -> torch.Tensor:
     """acc [M, n] f32 (zero on entry) += x @ W^T via split-K f32 atomics; the
-    consumer (add_rms_norm / rope_kv_fused with zero_*=True) re-zeroes it."""
+    consumer (add_rms_norm / rope_kv_fused with zero_*=True) re-zeroes it, or
+    a later launch does through ``zero`` (a buffer whose readers are done)."""
     if _native(x):
-        _ops().gemv_accum(x, blob, fmt, n, k, acc, ksplit)
+        _ops().gemv_accum(x, blob, fmt, n, k, acc, ksplit, zero)
         return acc
+    if zero is not None:
+        zero.zero_()
     acc += lowbit_matmul(x, blob, fmt, n, k).float().view_as(acc)
     return acc
+
+
+def gemv_norm_in(acc_in: torch.Tensor, residual: torch.Tensor, res_out: torch.Tensor, norm_w: torch.Tensor,
+                 eps: float, unit_offset: bool, blob, fmt, n, k, glu: bool, act: int = 0,
+                 acc_out: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decode projection of rms_norm(residual + acc_in) * norm_w with the
+    residual add and the norm done in the GEMV prologue (no norm launch):
+    res_out = residual + acc_in; returns act(gate)*up (``glu``) or acc_out
+    += x @ W^T (atomics).  acc_in is only read; ``zero`` is zeroed first."""
+    if _native(residual):
+        return _ops().gemv_norm_in(acc_in, residual, res_out, norm_w, eps, unit_offset, blob, fmt, n, k,
+                                   2 if glu else 3, act, acc_out, zero)
+    if zero is not None:
+        zero.zero_()
+    x = acc_in.to(residual.dtype).view_as(residual)
+    normed, new_res = R.add_rms_norm(x, residual, norm_w, eps, unit_offset)
+    res_out.copy_(new_res)
+    if glu:
+        from ..models.decoder import deinterleave_glu
+        g, u = deinterleave_glu(lowbit_matmul(normed, blob, fmt, n, k))
+        return ((F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")) * u).contiguous()
+    acc_out += lowbit_matmul(normed, blob, fmt, n, k).float().view_as(acc_out)
+    return acc_out
 
 
 def gemv_glu(x, blob, fmt, n, k, act: int = 0) -> torch.Tensor:

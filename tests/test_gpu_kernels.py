@@ -85,6 +85,61 @@ def test_gemv_accum_and_zeroing_consumers(cuda, name, M):
     assert acc.abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("name", ["sym_int4", "asym_int4", "nf4", "sym_int8"])
+@pytest.mark.parametrize("M", [1, 2])
+def test_gemv_norm_in(cuda, name, M):
+    """residual-add + RMSNorm folded into the GEMV prologue (decode norm-in
+    path) vs add_rms_norm followed by the plain GEMV / GLU GEMV; the residual
+    is written once to res_out and ``zero`` is cleared."""
+    from ipex_llm_amd.models.decoder import interleave_glu_rows
+    f = get_format(name).fmt
+    torch.manual_seed(2)
+    H, n, I = 1024, 768, 256
+    acc_in = torch.randn(M, H, device=cuda) * 0.5
+    res = torch.randn(M, H, device=cuda).bfloat16()
+    wn = (torch.rand(H, device=cuda) + 0.5).bfloat16()
+    blob = ops.quantize(torch.randn(n, H, device=cuda) * 0.05, f)
+    res_ref = res.clone()
+    normed, _ = ops.add_rms_norm(None, res_ref, wn, 1e-5, partials=acc_in.unsqueeze(0))
+    acc_out, res_out = torch.zeros(M, n, device=cuda), torch.empty_like(res)
+    zero = torch.ones(4 * 33, device=cuda)
+    ops.gemv_norm_in(acc_in, res, res_out, wn, 1e-5, False, blob, f, n, H, False, acc_out=acc_out, zero=zero)
+    ref = ops.gemv_partials(normed, blob, f, n, H, 1)[0]
+    assert _rel(acc_out, ref) < 5e-3, (name, M)
+    assert torch.equal(res_out, res_ref)                     # residual + acc, rounded like add_rms_norm
+    assert zero.abs().max().item() == 0.0
+    gu = ops.quantize(interleave_glu_rows(torch.randn(I, H, device=cuda) * 0.05,
+                                          torch.randn(I, H, device=cuda) * 0.05), f)
+    res_out2 = torch.empty_like(res)
+    y = ops.gemv_norm_in(acc_in, res, res_out2, wn, 1e-5, False, gu, f, 2 * I, H, True, 0)
+    assert _rel(y, ops.gemv_glu(normed, gu, f, 2 * I, H, 0)) < 1e-2, (name, M)
+    assert torch.equal(res_out2, res_ref)
+
+
+def test_decode_norm_in_matches_standalone_norms(cuda):
+    """whole-model decode step: norm-in GEMV prologues vs standalone norms"""
+    from transformers import LlamaConfig
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.models.decoder import NativeCausalLM
+    cfg = LlamaConfig(vocab_size=512, hidden_size=512, intermediate_size=1024, num_hidden_layers=3,
+                      num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=1024)
+    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=4)
+    prompts = [list(range(1, 50)), list(range(7, 70))]
+    outs = {}
+    try:
+        for flag in (False, True):
+            NativeCausalLM._norm_in_env = flag
+            e = Engine(m)
+            t = e.generate(prompts, max_new_tokens=8, use_graph=True)
+            outs[flag] = (t, e)
+    finally:
+        NativeCausalLM._norm_in_env = True
+    assert m._norm_in_ok(torch.empty(1, 512, device=cuda, dtype=torch.bfloat16), 2)
+    same = sum(a == b for a, b in zip(sum(outs[False][0], []), sum(outs[True][0], [])))
+    assert same >= 0.95 * len(sum(outs[True][0], []))       # greedy tokens: rare last-bit ties only
+
+
 @pytest.mark.parametrize("M", [1, 3, 33])
 def test_gemv_glu(cuda, M):
     from ipex_llm_amd.models.decoder import interleave_glu_rows
