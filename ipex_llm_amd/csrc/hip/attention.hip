@@ -242,6 +242,33 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
 
   __shared__ float ps[SPLIT][RT];
 
+  // ---- fused RoPE (rq_part): q/k/v of the new token from the qkv accumulator,
+  // rounded exactly like rope_kv_fused (GEMV output in T, cos/sin in T, each
+  // product in T, q scaled then stored in T)
+  constexpr bool RQ_OK = KVF == 0 && D / 16 >= 8;
+  const bool rq = RQ_OK && a.rq_part != nullptr;
+  auto rnd = [](float v) { return to_f32<T>(from_f32<T>(v)); };
+  auto rq_raw = [&](int col) -> float {
+    float s = a.rq_bias ? to_f32<T>(a.rq_bias[col]) : 0.f;
+    s += a.rq_part[(size_t)b * a.rq_ld + col];
+    return rnd(s);
+  };
+  const int64_t rpos = rq ? a.rq_pos[b] : 0;
+  auto rq_rot = [&](int col0, int d) -> float {
+    const int half = a.rq_rot / 2;
+    if (d >= a.rq_rot) return rq_raw(col0 + d);
+    int i, d0, d1;
+    bool first;
+    if (a.rq_interleaved) { i = d >> 1; d0 = 2 * i; d1 = d0 + 1; first = (d & 1) == 0; }
+    else { first = d < half; i = first ? d : d - half; d0 = i; d1 = i + half; }
+    const float2 cs = ((const float2*)a.rq_cos_sin)[(size_t)rpos * half + i];
+    const float c = rnd(cs.x), sn = rnd(cs.y);
+    const float x0 = rq_raw(col0 + d0), x1 = rq_raw(col0 + d1);
+    return first ? rnd(x0 * c) - rnd(x1 * sn) : rnd(x1 * c) + rnd(x0 * sn);
+  };
+  const bool has_new = rq && k0 + nk == len;        // this split holds the new key (position len - 1)
+  const int colk = (a.Hq + kvh) * D, colv = (a.Hq + a.Hkv + kvh) * D;
+
   const int blk = a.block_tables[(size_t)b * a.max_blocks + k0 / a.bs];
   const size_t base = (((size_t)blk * a.Hkv + kvh) * a.bs + (k0 % a.bs)) * D;
   const uint8_t* kb = a.k_cache + base * EB;
@@ -266,7 +293,128 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     }
   }
   uint4 qf[KSTEP];
-  {
+  if (rq) {
+    // a lane's q / k dims are 32 s + 8 g + j (s < KSTEP, j < 8): with full-width
+    // rotary (rot == D) the rotation partner of chunk s is chunk s +- KSTEP/2 of
+    // the same lane, so every operand arrives in 16-B vector loads
+    auto lane_raw = [&](int col0, float (&v)[KSTEP][8]) {
+#pragma unroll
+      for (int s = 0; s < KSTEP; s++) {
+        const float4* p = (const float4*)(a.rq_part + (size_t)b * a.rq_ld + col0 + 32 * s + 8 * g);
+        const float4 f0 = p[0], f1 = p[1];
+        float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (a.rq_bias) {
+          const uint4 u = *(const uint4*)(a.rq_bias + col0 + 32 * s + 8 * g);
+          const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            bb[2 * e] = to_f32<T>((uint16_t)(w[e] & 0xffff));
+            bb[2 * e + 1] = to_f32<T>((uint16_t)(w[e] >> 16));
+          }
+        }
+        const float f[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[s][j] = rnd(bb[j] + f[j]);
+      }
+    };
+    auto lane_rot = [&](int col0, float scale_out, uint4* outf) {
+      float v[KSTEP][8];
+      lane_raw(col0, v);
+      if (a.rq_rot == D && !a.rq_interleaved) {
+        constexpr int HS = KSTEP / 2;
+        const float4* csp = (const float4*)a.rq_cos_sin + (size_t)rpos * (D / 4);   // float2 pairs, 2 per float4
+#pragma unroll
+        for (int s = 0; s < HS; s++) {
+          float cc[8], ss[8];
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            const float4 q = csp[(32 * s + 8 * g) / 2 + e];
+            cc[2 * e] = rnd(q.x); ss[2 * e] = rnd(q.y); cc[2 * e + 1] = rnd(q.z); ss[2 * e + 1] = rnd(q.w);
+          }
+          uint32_t lo[4], hi[4];
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            float r0[2], r1[2];
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+              const int j = 2 * e + t;
+              const float x0 = v[s][j], x1 = v[s + HS][j];
+              r0[t] = (rnd(x0 * cc[j]) - rnd(x1 * ss[j])) * scale_out;
+              r1[t] = (rnd(x1 * cc[j]) + rnd(x0 * ss[j])) * scale_out;
+            }
+            lo[e] = pack2<T>(r0[0], r0[1]);
+            hi[e] = pack2<T>(r1[0], r1[1]);
+          }
+          outf[s] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+          outf[s + HS] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < KSTEP; s++) {
+          uint32_t w[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            w[j] = pack2<T>(rq_rot(col0, 32 * s + 8 * g + 2 * j) * scale_out,
+                            rq_rot(col0, 32 * s + 8 * g + 2 * j + 1) * scale_out);
+          outf[s] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+    };
+    {
+      const int row = r16 < R ? r16 : 0;
+      lane_rot((kvh * group + row % group) * D, a.rq_qscale, qf);
+      if (r16 >= R)
+#pragma unroll
+        for (int s = 0; s < KSTEP; s++) qf[s] = make_uint4(0, 0, 0, 0);
+    }
+    if (has_new) {
+      // the new key / value replace the (not yet written) cache entry in
+      // registers and are appended to the paged cache for later steps
+      const int kn = nk - 1, pos = len - 1;
+      const int nb = a.block_tables[(size_t)b * a.max_blocks + pos / a.bs];
+      const size_t crow = (((size_t)nb * a.Hkv + kvh) * a.bs + (size_t)(pos % a.bs)) * D;
+      if (r16 == (kn & 15)) {
+        uint4 kq[KSTEP];
+        lane_rot(colk, 1.f, kq);
+#pragma unroll
+        for (int kt = 0; kt < 4; kt++)
+          if (kt == (kn >> 4))
+#pragma unroll
+            for (int s = 0; s < KSTEP; s++) kf[kt][s] = kq[s];
+#pragma unroll
+        for (int s = 0; s < KSTEP; s++) *(uint4*)((uint16_t*)a.k_cache + crow + 32 * s + 8 * g) = kq[s];
+      }
+      if constexpr (DPL >= 8) {
+        if (kg == (kn & 3)) {
+#pragma unroll
+          for (int c = 0; c < VCH; c++) {
+            const int d0 = DPL * dg + 8 * c;
+            const float4* p = (const float4*)(a.rq_part + (size_t)b * a.rq_ld + colv + d0);
+            const float4 f0 = p[0], f1 = p[1];
+            const float f[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+            float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (a.rq_bias) {
+              const uint4 u = *(const uint4*)(a.rq_bias + colv + d0);
+              const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+              for (int e = 0; e < 4; e++) {
+                bb[2 * e] = to_f32<T>((uint16_t)(w[e] & 0xffff));
+                bb[2 * e + 1] = to_f32<T>((uint16_t)(w[e] >> 16));
+              }
+            }
+            uint32_t w[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) w[e] = pack2<T>(rnd(bb[2 * e] + f[2 * e]), rnd(bb[2 * e + 1] + f[2 * e + 1]));
+            const uint4 vq = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+              if (i == (kn >> 2)) vf[i][c] = vq;
+            *(uint4*)((uint16_t*)a.v_cache + crow + d0) = vq;
+          }
+        }
+      }
+    }
+  } else {
     const int row = r16 < R ? r16 : 0;
     const int t = row / group, h = kvh * group + row % group;
     const uint16_t* qr = a.q + (((size_t)b * a.Tq + t) * a.Hq + h) * D;

@@ -110,6 +110,16 @@ struct AttnDecodeArgs {
   float k_scale, v_scale;
   const float* alibi;       // [Hq] slopes or null
   int no_combine;           // leave the split partials for the consumer (o_proj GEMV prologue)
+  // fused RoPE + KV append (decode, Tq == 1, bf16/f16 KV, D >= 128): q / k / v
+  // come straight from the qkv GEMV's atomic accumulator rq_part [B, rq_ld]
+  // (+ rq_bias), q/k rotated in registers; the split holding the new key
+  // uses it from registers and writes it to the cache (no rope_kv launch)
+  const float* rq_part;
+  const uint16_t* rq_bias;
+  const float* rq_cos_sin;  // [max_pos, rot / 2, 2]
+  const int64_t* rq_pos;    // [B] rotary positions
+  int rq_ld, rq_rot, rq_interleaved;
+  float rq_qscale;
 };
 void launch_attn_decode(bool bf16, const AttnDecodeArgs& a, hipStream_t st);
 

@@ -600,6 +600,66 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, cons
   return {out, po, pml};
 }
 
+// decode attention with RoPE + KV append fused in (Tq == 1): q/k/v of the new
+// token come from the qkv GEMV's atomic accumulator part [B, ld] (+ bias); no
+// rope_kv launch.  The accumulator is only read (a later launch zeroes it).
+Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin,
+                        const Tensor& pos, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
+                        const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
+                        int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt) {
+  c10::DeviceGuard g(part.device());
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "attn_decode_rope: bf16/fp16 activations");
+  TORCH_CHECK(k_cache.scalar_type() == dt && v_cache.scalar_type() == dt, "attn_decode_rope: 16-bit KV cache");
+  TORCH_CHECK(part.is_cuda() && part.dim() == 2 && part.scalar_type() == at::kFloat && part.is_contiguous(),
+              "attn_decode_rope: part must be contiguous f32 [B, ld]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.dim() == 3,
+              "attn_decode_rope: f32 cos/sin table [max_pos, rot/2, 2]");
+  TORCH_CHECK(pos.scalar_type() == at::kLong && block_tables.scalar_type() == at::kInt &&
+                  seq_lens.scalar_type() == at::kInt, "attn_decode_rope: int64 positions, int32 tables");
+  const int64_t B = part.size(0), Hkv = k_cache.size(1), bs = k_cache.size(2), D = k_cache.size(3);
+  TORCH_CHECK(part.size(1) == (Hq + 2 * Hkv) * D, "attn_decode_rope: part width != (Hq + 2 Hkv) * D");
+  TORCH_CHECK((D == 128 && Hq / Hkv <= 16) || (D == 256 && Hq / Hkv <= 8), "attn_decode_rope: head_dim/group");
+  TORCH_CHECK(Hq % Hkv == 0 && bs % 64 == 0 && rot_dim <= D && rot_dim % 2 == 0 && cos_sin.size(1) == rot_dim / 2,
+              "attn_decode_rope: geometry");
+  illm::AttnDecodeArgs a{};
+  Tensor po = at::empty({B, Hq, 1, nsplit, D}, part.options());
+  Tensor pml = at::empty({B, Hq, 1, nsplit, 2}, part.options());
+  Tensor out = at::empty({B, 1, Hq, D}, part.options().dtype(dt));
+  a.q = nullptr;
+  a.k_cache = (const uint8_t*)k_cache.data_ptr();
+  a.v_cache = (const uint8_t*)v_cache.data_ptr();
+  a.block_tables = block_tables.data_ptr<int32_t>();
+  a.seq_lens = seq_lens.data_ptr<int32_t>();
+  a.max_blocks = (int)block_tables.size(1);
+  a.part_o = po.data_ptr<float>();
+  a.part_ml = pml.data_ptr<float>();
+  a.out = m16(out);
+  a.B = (int)B;
+  a.Tq = 1;
+  a.Hq = (int)Hq;
+  a.Hkv = (int)Hkv;
+  a.D = (int)D;
+  a.bs = (int)bs;
+  a.nsplit = (int)nsplit;
+  a.scale = (float)scale;
+  a.softcap = (float)softcap;
+  a.sliding_window = (int)window;
+  a.kv_fp8 = 0;
+  a.k_scale = a.v_scale = 1.f;
+  static const bool fused_combine = getenv("ILLM_ATTN_FUSED_COMBINE") != nullptr;
+  a.counters = fused_combine ? attn_counters(part.device(), B * Hkv) : nullptr;
+  a.rq_part = part.data_ptr<float>();
+  a.rq_bias = p16o(bias);
+  a.rq_cos_sin = cos_sin.data_ptr<float>();
+  a.rq_pos = pos.data_ptr<int64_t>();
+  a.rq_ld = (int)part.size(1);
+  a.rq_rot = (int)rot_dim;
+  a.rq_interleaved = interleaved ? 1 : 0;
+  a.rq_qscale = (float)q_scale;
+  illm::launch_attn_decode(dt == at::kBFloat16, a, cur_stream());
+  return out;
+}
+
 Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
                    const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
                    int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& alibi) {
@@ -848,6 +908,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv", &gemv);
   m.impl("gemv_accum", &gemv_accum);
   m.impl("gemv_norm_in", &gemv_norm_in);
+  m.impl("attn_decode_rope", &attn_decode_rope);
   m.impl("gemm", &gemm);
   m.impl("attn_decode_split", &attn_decode_split);
   m.impl("gemv_attn", &gemv_attn);

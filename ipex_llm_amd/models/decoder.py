@@ -363,6 +363,20 @@ class NativeCausalLM(nn.Module):
             self.__dict__["_norm_in_layers"] = ok
         return ok
 
+    # decode (one new token per sequence) attention that applies RoPE to q/k
+    # from the qkv accumulator and appends the new key/value itself: one
+    # launch per layer fewer.  ILLM_ROPE_IN=0 restores the rope_kv launch.
+    _rope_in_env = __import__("os").environ.get("ILLM_ROPE_IN", "1") != "0"
+
+    def _rope_in_ok(self, meta: "AttnMeta", cache) -> bool:
+        s = self.spec
+        group = s.num_heads // s.num_kv_heads
+        # (compressed KV: seq_lens are cache lengths, the rotary position comes from pos)
+        return (self._rope_in_env and meta.Tq == 1 and cache.kv_fp8 == 0
+                and self._capture_q is None and self.rope_cache is not None
+                and ((s.head_dim == 128 and group <= 16) or (s.head_dim == 256 and group <= 8))
+                and all(L.self_attn.q_norm is None and L.self_attn.k_norm is None for L in self.layers))
+
     def _fused_mlp_ok(self, x, layer) -> bool:
         mlp = layer.mlp
         if not (x.is_cuda and isinstance(mlp, NativeMLP) and x.shape[0] <= 16 and self.tp_group is None):
@@ -418,6 +432,7 @@ class NativeCausalLM(nn.Module):
         pend = None                     # accumulator awaiting residual-add + norm
         consumed = None                 # accumulator read by the last launch: zeroed by the next GEMV
         res_pp = (residual, torch.empty_like(residual)) if norm_in else None
+        rope_in = norm_in and self._rope_in_ok(meta, cache)
         nxt_res = lambda r: res_pp[1] if r is res_pp[0] else res_pp[0]
         for li, layer in enumerate(self.layers):
             attn = layer.self_attn
@@ -436,13 +451,15 @@ class NativeCausalLM(nn.Module):
                         residual, consumed, pend = r2, pend, None
                     else:
                         ops.gemv_accum(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, part)
+                    qkv_acc = part
                     part = part.unsqueeze(0)
                 else:
                     part = ops.gemv_partials(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, 0)
-                ops.rope_kv_fused(part, qp.bias, q, cache.k[li], cache.v[li], pos, meta.block_tables, meta.Tq, rope,
-                                  s.num_heads, s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved,
-                                  attn.q_norm, attn.k_norm, s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale,
-                                  cache.v_scale, meta.pos_offset, zero_part=T <= ACC_MAX_M)
+                if not (norm_in and rope_in):
+                    ops.rope_kv_fused(part, qp.bias, q, cache.k[li], cache.v[li], pos, meta.block_tables, meta.Tq,
+                                      rope, s.num_heads, s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved,
+                                      attn.q_norm, attn.k_norm, s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale,
+                                      cache.v_scale, meta.pos_offset, zero_part=T <= ACC_MAX_M)
             else:
                 qkv = qp(x)
                 ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,
@@ -454,16 +471,27 @@ class NativeCausalLM(nn.Module):
                 # o_proj -> atomic slab P (zeroing the slab the qkv prologue consumed);
                 # the gate/up GEMV adds P to the residual and normalises in its prologue;
                 # down -> atomic slab D (zeroing P), pending for the next layer's qkv
-                a = self._attention(li, attn, q, meta, cache)
+                # rope_in: attention rotates q/k from the qkv slab itself and appends the new
+                # key/value (no rope launch); the o_proj GEMV then zeroes the qkv slab and the
+                # gate/up GEMV the slab the qkv prologue consumed
+                if rope_in:
+                    a = ops.attn_decode_rope(qkv_acc, qp.bias, self.rope_cache, pos, cache.k[li], cache.v[li],
+                                             meta.block_tables, meta.seq_lens, meta.nsplit, s.scale,
+                                             s.attn_softcap, attn.sliding_window, s.num_heads, s.rot_dim,
+                                             s.rope_interleaved, 1.0, x.dtype).view(T, -1)
+                    zero_o, zero_gu = qkv_acc, consumed
+                else:
+                    a = self._attention(li, attn, q, meta, cache)
+                    zero_o, zero_gu = consumed, None
                 o, mlp = attn.o_proj, layer.mlp
                 H = o.out_features
                 accP, accD = self._acc(H, T, x.device, "P"), self._acc(H, T, x.device, "D")
-                ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
+                ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=zero_o)
                 r2 = nxt_res(residual)
                 gu, dn = mlp.gate_up_proj, mlp.down_proj
                 act = ops.gemv_norm_in(accP, residual, r2, layer.post_attention_layernorm, s.rms_eps,
                                        s.norm_unit_offset, gu.weight, gu.fmt, gu.out_features, gu.in_features, True,
-                                       s.act)
+                                       s.act, zero=zero_gu)
                 residual = r2
                 ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=accP)
                 consumed = None

@@ -132,3 +132,9 @@ def _(x, blob, fmt, n, k, bias):
     shape = list(x.shape)
     shape[-1] = n
     return x.new_empty(shape)
+
+
+@register_fake("ipex_llm_amd::attn_decode_rope")
+def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, Hq,
+      rot_dim, interleaved, q_scale, dtype):
+    return part.new_empty((part.shape[0], 1, Hq, k_cache.shape[3]), dtype=dtype)

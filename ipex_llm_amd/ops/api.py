@@ -18,7 +18,7 @@ __all__ = [
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
-    "attn_decode_split", "gemv_attn", "gemv_norm_in",
+    "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope",
 ]
 
 
@@ -313,6 +313,16 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, soft
         vv = gather_kv(v_cache, block_tables, b, L, kv_fp8, v_scale, q.dtype)
         outs.append(R.attention(q[b:b + 1], kk[None], vv[None], True, scale, softcap, window, None, alibi))
     return torch.cat(outs, 0)
+
+
+def attn_decode_rope(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
+                     softcap, window, Hq: int, rot_dim: int, interleaved: bool, q_scale: float = 1.0,
+                     dtype=torch.bfloat16):
+    """Decode attention (one new token per sequence) with the RoPE of q/k and
+    the KV append fused in, reading q/k/v from the qkv GEMV's f32
+    accumulator ``part`` [B, (Hq + 2 Hkv) * D].  Returns [B, 1, Hq, D]."""
+    return _ops().attn_decode_rope(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit,
+                                   scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dtype)
 
 
 def attn_decode_split(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap=0.0, window=0,

@@ -116,6 +116,37 @@ def test_gemv_norm_in(cuda, name, M):
     assert torch.equal(res_out2, res_ref)
 
 
+@pytest.mark.parametrize("B,interleaved", [(1, False), (2, False), (2, True)])
+def test_attn_decode_rope_matches_rope_kv(cuda, B, interleaved):
+    """decode attention with RoPE + KV append fused in vs rope_kv_fused +
+    attn_decode: identical cache contents, same attention output"""
+    from ipex_llm_amd.engine.runner import nsplit_for
+    torch.manual_seed(3)
+    Hq, Hkv, D, bs = 8, 2, 128, 64
+    L = [70, 131][:B]
+    kc = torch.randn(4 * B, Hkv, bs, D, device=cuda).bfloat16()
+    vc = torch.randn(4 * B, Hkv, bs, D, device=cuda).bfloat16()
+    bt = torch.arange(4 * B, dtype=torch.int32, device=cuda).flip(0).view(B, 4).contiguous()
+    seq_lens = torch.tensor(L, dtype=torch.int32, device=cuda)
+    pos = (seq_lens - 1).long()
+    W = (Hq + 2 * Hkv) * D
+    part = torch.randn(B, W, device=cuda)
+    bias = (torch.randn(W, device=cuda) * 0.1).bfloat16()
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    fr = torch.arange(512, device=cuda).float()[:, None] * inv[None]
+    cs = torch.stack([fr.cos(), fr.sin()], -1).contiguous()
+    ns = nsplit_for(max(L))
+    kc1, vc1 = kc.clone(), vc.clone()
+    q = torch.empty(B, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.rope_kv_fused(part.clone().unsqueeze(0), bias, q, kc1, vc1, pos, bt, 1, cs, Hq, Hkv, D, D, interleaved)
+    ref = ops.attn_decode(q.view(B, 1, Hq, D), kc1, vc1, bt, seq_lens, ns, D ** -0.5)
+    kc2, vc2 = kc.clone(), vc.clone()
+    got = ops.attn_decode_rope(part, bias, cs, pos, kc2, vc2, bt, seq_lens, ns, D ** -0.5, 0.0, 0, Hq, D,
+                               interleaved, 1.0, torch.bfloat16)
+    assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    assert _rel(got, ref) < 1e-3
+
+
 def test_decode_norm_in_matches_standalone_norms(cuda):
     """whole-model decode step: norm-in GEMV prologues vs standalone norms"""
     from transformers import LlamaConfig
@@ -128,13 +159,16 @@ def test_decode_norm_in_matches_standalone_norms(cuda):
     prompts = [list(range(1, 50)), list(range(7, 70))]
     outs = {}
     try:
-        for flag in (False, True):
-            NativeCausalLM._norm_in_env = flag
+        for flag in (False, True, "rope"):
+            NativeCausalLM._norm_in_env = bool(flag)
+            NativeCausalLM._rope_in_env = flag == "rope"
             e = Engine(m)
             t = e.generate(prompts, max_new_tokens=8, use_graph=True)
             outs[flag] = (t, e)
     finally:
         NativeCausalLM._norm_in_env = True
+        NativeCausalLM._rope_in_env = True
+    assert outs[True][0] == outs["rope"][0]                   # fused RoPE: bit-identical decode
     assert m._norm_in_ok(torch.empty(1, 512, device=cuda, dtype=torch.bfloat16), 2)
     same = sum(a == b for a, b in zip(sum(outs[False][0], []), sum(outs[True][0], [])))
     assert same >= 0.95 * len(sum(outs[True][0], []))       # greedy tokens: rare last-bit ties only
