@@ -225,7 +225,7 @@ __device__ __forceinline__ uint4 kv_frag8(const uint8_t* p) {
   }
 }
 
-template <typename T, int D, int KVF, int RT>
+template <typename T, int D, int KVF, int RT, bool RQ = false>
 __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs a) {
   constexpr int EB = KVF == 0 ? 2 : 1;
   constexpr int KSTEP = D / 32;       // MFMA k-steps over the head dim
@@ -245,8 +245,9 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   // ---- fused RoPE (rq_part): q/k/v of the new token from the qkv accumulator,
   // rounded exactly like rope_kv_fused (GEMV output in T, cos/sin in T, each
   // product in T, q scaled then stored in T)
-  constexpr bool RQ_OK = KVF == 0 && D / 16 >= 8;
-  const bool rq = RQ_OK && a.rq_part != nullptr;
+  // separate instantiation: the plain kernel keeps its register allocation
+  constexpr bool RQ_OK = RQ && KVF == 0 && D / 16 >= 8;
+  constexpr bool rq = RQ_OK;
   auto rnd = [](float v) { return to_f32<T>(from_f32<T>(v)); };
   auto rq_raw = [&](int col) -> float {
     float s = a.rq_bias ? to_f32<T>(a.rq_bias[col]) : 0.f;
@@ -293,7 +294,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     }
   }
   uint4 qf[KSTEP];
-  if (rq) {
+  if constexpr (rq) {
     // a lane's q / k dims are 32 s + 8 g + j (s < KSTEP, j < 8): with full-width
     // rotary (rot == D) the rotation partner of chunk s is chunk s +- KSTEP/2 of
     // the same lane, so every operand arrives in 16-B vector loads
@@ -606,6 +607,14 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
   // combine fused into the split kernel when the merge fits its LDS scratch
   if (a.nsplit > SPLIT * RT || a.no_combine) a.counters = nullptr;
   dim3 grid(a.nsplit, a.Hkv, a.B);
+  if constexpr (D / 16 >= 8) {
+    if (a.rq_part != nullptr) {
+      hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true>), grid, dim3(64), 0, st, a);
+      if (a.counters == nullptr && !a.no_combine)
+        hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
+      return;
+    }
+  }
   if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT>), grid, dim3(64), 0, st, a);
   else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT>), grid, dim3(64), 0, st, a);
   else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT>), grid, dim3(64), 0, st, a);

@@ -411,26 +411,22 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
         }
       }
       *(uint4*)(xs + m * ldx + kk) = val;
-    }
-  }
-  __syncthreads();
-  // ---- per (row, chunk): block sums of the staged activations
-  {
-    const int nch = c1 - c0;
-    for (int v = threadIdx.x; v < Mloc * nch * 2; v += NW * 64) {
-      const int m = v / (nch * 2), rem = v % (nch * 2);
-      const uint16_t* p = xs + m * ldx + rem * 64;
-      float s = 0.f;
+      // per (row, 64-block) sums of the staged activations: the 8 lanes of a
+      // block are 8 consecutive threads (vpr is a multiple of 16), reduced with
+      // shuffles here instead of a second LDS pass behind another barrier
+      const uint32_t sw[4] = {val.x, val.y, val.z, val.w};
+      float bsum = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const uint4 q = *(const uint4*)(p + 8 * j);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int i = 0; i < 4; i++) s += to_f32<C>(w[i] & 0xffff) + to_f32<C>(w[i] >> 16);
+      for (int i = 0; i < 4; i++) bsum += to_f32<C>((uint16_t)(sw[i] & 0xffff)) + to_f32<C>((uint16_t)(sw[i] >> 16));
+      bsum += __shfl_xor(bsum, 1, 8);
+      bsum += __shfl_xor(bsum, 2, 8);
+      bsum += __shfl_xor(bsum, 4, 8);
+      if ((v & 7) == 0) {
+        const int blk = kk >> 6, nch = c1 - c0;
+        float* rec = (float*)(sxs + m * nch + (blk >> 1));
+        rec[blk & 1] = -OFF * bsum;
+        rec[2 + (blk & 1)] = bsum;
       }
-      float* rec = (float*)(sxs + m * nch + (rem >> 1));
-      rec[rem & 1] = -OFF * s;
-      rec[2 + (rem & 1)] = s;
     }
   }
   __syncthreads();

@@ -43,6 +43,14 @@ __global__ void __launch_bounds__(NORM_THREADS)
   __shared__ float red[NORM_THREADS / 64];
   const int row = blockIdx.x;
   const int M = gridDim.x;
+  // the weight does not depend on the row: load it first so it is not a
+  // dependent memory round trip behind the block reduction
+  uint4 wraw[MAXV];
+#pragma unroll
+  for (int j = 0; j < MAXV; j++) {
+    const int c = (threadIdx.x + j * NORM_THREADS) * 8;
+    wraw[j] = c < H ? *(const uint4*)(w + c) : make_uint4(0, 0, 0, 0);
+  }
   float v[MAXV][8];
   float ss = 0.f;
 #pragma unroll
@@ -88,7 +96,12 @@ __global__ void __launch_bounds__(NORM_THREADS)
     const int c = (threadIdx.x + j * NORM_THREADS) * 8;
     if (c < H) {
       float wv[8], o[8];
-      load8<T>(w + c, wv);
+      const uint32_t wr[4] = {wraw[j].x, wraw[j].y, wraw[j].z, wraw[j].w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        wv[2 * i] = to_f32<T>((uint16_t)(wr[i] & 0xffff));
+        wv[2 * i + 1] = to_f32<T>((uint16_t)(wr[i] >> 16));
+      }
       for (int i = 0; i < 8; i++) {
         const float ww = unit_offset ? rnd<T>(1.f + wv[i]) : wv[i];
         o[i] = ww * rnd<T>(v[j][i] * inv);
