@@ -175,7 +175,9 @@ class _BaseAutoModelClass:
             from ..gptq import load_gptq_model
             model = load_gptq_model(cls.HF_Model, path, prequant, torch_dtype=torch_dtype, **kwargs)
         else:
-            model = cls.HF_Model.from_pretrained(path, *args, torch_dtype=torch_dtype, **kwargs)
+            from .patches import remote_code_patches
+            with remote_code_patches():        # remote code importing flash_attn stays loadable
+                model = cls.HF_Model.from_pretrained(path, *args, torch_dtype=torch_dtype, **kwargs)
         model = model.to("cpu")
         if tensor_parallel or tp_group is not None:
             # AutoTP on the dense weights; each rank quantizes only its shard
@@ -232,7 +234,9 @@ class _BaseAutoModelClass:
         trust = kwargs.pop("trust_remote_code", False)
         torch_dtype = kwargs.pop("torch_dtype", kwargs.pop("dtype", None))
         kwargs.pop("optimize_model", None)
-        config = AutoConfig.from_pretrained(path, trust_remote_code=trust)
+        from .patches import remote_code_patches
+        with remote_code_patches():
+            config = AutoConfig.from_pretrained(path, trust_remote_code=trust)
         meta_path = os.path.join(path, LOW_BIT_META)
         flags = json.load(open(meta_path)) if os.path.exists(meta_path) else {}
         qtype = flags.get("qtype") or getattr(config, "bigdl_transformers_low_bit", "sym_int4")

@@ -77,3 +77,15 @@ def test_optimize_model_generic_module():
     assert isinstance(net[0], LowBitLinear) and isinstance(net[2], LowBitLinear)
     assert not isinstance(net[3], LowBitLinear) or net[3].in_features % 64 == 0
     assert ((net(x) - ref).norm() / ref.norm()).item() < 0.05
+
+
+def test_remote_code_flash_attn_import_filter(tmp_path):
+    """reference patches.py: a remote modelling file importing flash_attn still passes the import check"""
+    from ipex_llm_amd.transformers.patches import patch_flash_attn_import, remote_code_patches
+    f = tmp_path / "modeling_x.py"
+    f.write_text("import torch\nimport flash_attn\nimport einops\n")
+    import transformers.dynamic_module_utils as dmu
+    assert "flash_attn" in dmu.get_imports(str(f))
+    assert "flash_attn" not in patch_flash_attn_import(str(f))
+    with remote_code_patches():
+        assert "flash_attn" not in dmu.get_imports(str(f)) and "einops" in dmu.get_imports(str(f))
