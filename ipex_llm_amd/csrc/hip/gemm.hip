@@ -246,6 +246,29 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   }
 
   // ---- epilogue: lane holds out[m0 + 16 mt + r16][16 tile + 4 g + i]
+  if (a.glu) {
+    // the wave's two tiles are one gate/up pair (16-row interleave, tile0 even):
+    // act(gate) * up in f32, one rounding (as the decode GLU GEMV epilogue)
+    if (tile0 + 1 >= NT) return;
+    const int n0 = (tile0 / 2) * 16 + 4 * g;
+    const int I = a.N / 2;
+    if (n0 >= I) return;
+#pragma unroll
+    for (int mt = 0; mt < 8; mt++) {
+      const int m = m0 + mt * 16 + r16;
+      if (m >= a.M) continue;
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const float gv = acc[0][mt][i], uv = acc[1][mt][i];
+        o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
+      }
+      uint16_t* y = a.out + (size_t)m * a.ldo + n0;
+      if (n0 + 3 < I && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+      else for (int i = 0; i < 4 && n0 + i < I; i++) y[i] = from_f32<T>(o[i]);
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 2; t++) {
     const int tile = tile0 + t;

@@ -39,6 +39,8 @@ struct GemmArgs {
   uint16_t* out;           // [M, ldo] T
   int ldo;
   int lut_fmt;
+  int glu;                 // 1: tile-interleaved gate/up weight, out = act(gate) * up [M, N / 2]
+  int act;                 // 0 = silu, 1 = gelu(tanh)
 };
 void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st);
 

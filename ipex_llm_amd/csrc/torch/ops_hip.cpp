@@ -242,6 +242,38 @@ Tensor gemm(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   return out;
 }
 
+// prefill GEMM over a tile-interleaved gate/up weight with the activation
+// fused into the epilogue: returns act(x Wg^T) * (x Wu^T) [M, n / 2]
+Tensor gemm_glu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t act) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda(), "gemm_glu: GPU tensors expected");
+  TORCH_CHECK(x.size(-1) == k && k % 8 == 0 && n % 32 == 0, "gemm_glu: shapes");
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  const int64_t M = xc.numel() / k;
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemm_glu: weight blob too small");
+  auto shape = xc.sizes().vec();
+  shape.back() = n / 2;
+  Tensor out = at::empty(shape, xc.options());
+  if (M == 0) return out;
+  illm::GemmArgs a{};
+  a.x = p16(xc);
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.N = (int)n;
+  a.KC = (int)(illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K);
+  a.bias = nullptr;
+  a.out = m16(out);
+  a.ldo = (int)(n / 2);
+  a.lut_fmt = (int)fmt;
+  a.glu = 1;
+  a.act = (int)act;
+  illm::launch_lowbit_gemm(bf16, (int)fmt, a, cur_stream());
+  return out;
+}
+
 // split-K GEMV accumulated with f32 atomics into acc [M, n] (zero on entry;
 // the consumer -- add_rms_norm / rope_kv_fused with zero_*=True -- reads the
 // single slab and re-zeroes it, so no ks-slab reduction is ever needed)
@@ -908,6 +940,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv", &gemv);
   m.impl("gemv_accum", &gemv_accum);
   m.impl("gemv_norm_in", &gemv_norm_in);
+  m.impl("gemm_glu", &gemm_glu);
   m.impl("attn_decode_rope", &attn_decode_rope);
   m.impl("gemm", &gemm);
   m.impl("attn_decode_split", &attn_decode_split);

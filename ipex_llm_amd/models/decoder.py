@@ -266,7 +266,8 @@ class NativeCausalLM(nn.Module):
                     mask &= kpos[None, :] > (qpos[:, None] - window)
                 o = F.scaled_dot_product_attention(qq, k4, v4, attn_mask=mask, scale=s.scale, enable_gqa=True)
             outs.append(o[0].transpose(0, 1)[None])
-        return torch.cat(outs, 0).reshape(T, s.num_heads * s.head_dim)
+        o = outs[0] if len(outs) == 1 else torch.cat(outs, 0)      # (a 1-element cat is a slow strided copy)
+        return o.reshape(T, s.num_heads * s.head_dim)
 
     def _acc(self, n: int, t: int, device, tag: str = "") -> torch.Tensor:
         """Zeroed f32 [t, n] accumulator for the split-K atomic GEMV
@@ -400,6 +401,11 @@ class NativeCausalLM(nn.Module):
         if x.is_cuda and isinstance(gu, LowBitLinear) and gu.bias is None and x.shape[0] <= ops.GEMV_MAX_M \
                 and ops.native_gpu(x):
             return ops.gemv_glu(x, gu.weight, gu.fmt, gu.out_features, gu.in_features, s.act)
+        if x.is_cuda and isinstance(gu, LowBitLinear) and gu.bias is None and gu.g_idx_map is None \
+                and gu.mp_group is None and x.dtype in (torch.bfloat16, torch.float16) and ops.native_gpu(x):
+            # prefill: the activation runs in the GEMM epilogue (no [T, 2I] round trip)
+            from ..ops.gemm import lowbit_gemm_glu
+            return lowbit_gemm_glu(x.contiguous(), gu.weight, gu.fmt, gu.out_features, gu.in_features, s.act)
         y = gu(x)
         g, u = deinterleave_glu(y)
         a = F.silu(g) if s.act == 0 else F.gelu(g, approximate="tanh")

@@ -138,3 +138,10 @@ def _(x, blob, fmt, n, k, bias):
 def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, Hq,
       rot_dim, interleaved, q_scale, dtype):
     return part.new_empty((part.shape[0], 1, Hq, k_cache.shape[3]), dtype=dtype)
+
+
+@register_fake("ipex_llm_amd::gemm_glu")
+def _(x, blob, fmt, n, k, act):
+    shape = list(x.shape)
+    shape[-1] = n // 2
+    return x.new_empty(shape)

@@ -27,3 +27,16 @@ def lowbit_gemm(x, blob, fmt, n, k, bias=None):
         return ops.gemm(x, blob, fmt, n, k, bias)
     w = ops.dequantize_device(blob, fmt, n, k, x.dtype)
     return F.linear(x, w, bias)
+
+
+def lowbit_gemm_glu(x, blob, fmt, n, k, act: int = 0):
+    """act(x @ Wg^T) * (x @ Wu^T) for a tile-interleaved gate/up weight at
+    prefill M: the fused kernel applies the activation in its epilogue (no
+    [M, 2I] round trip, no elementwise launches)."""
+    ops = torch.ops.ipex_llm_amd
+    M = x.numel() // k
+    if not _USE_LIB and (M <= FUSED_MAX_M or _USE_FUSED) and hasattr(ops, "gemm_glu"):
+        return ops.gemm_glu(x, blob, fmt, n, k, act)
+    from ..models.decoder import deinterleave_glu
+    g, u = deinterleave_glu(lowbit_gemm(x, blob, fmt, n, k))
+    return ((F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")) * u).contiguous()

@@ -190,6 +190,25 @@ def test_gemv_glu(cuda, M):
     assert _rel(y, ref) < 2e-2
 
 
+@pytest.mark.parametrize("name", ["sym_int4", "nf4", "fp8_e4m3"])
+@pytest.mark.parametrize("M", [100, 700])
+def test_lowbit_gemm_glu_epilogue(cuda, name, M):
+    """prefill GEMM with act(gate) * up in the epilogue vs GEMM + torch GLU"""
+    from ipex_llm_amd.models.decoder import deinterleave_glu, interleave_glu_rows
+    from ipex_llm_amd.ops.gemm import lowbit_gemm, lowbit_gemm_glu
+    f = get_format(name).fmt
+    torch.manual_seed(4)
+    I, k = 320, 512
+    blob = ops.quantize(interleave_glu_rows(torch.randn(I, k, device=cuda) * 0.05,
+                                            torch.randn(I, k, device=cuda) * 0.05), f)
+    x = torch.randn(M, k, device=cuda).bfloat16()
+    g, u = deinterleave_glu(lowbit_gemm(x, blob, f, 2 * I, k).float())
+    for act in (0, 1):
+        ref = (torch.nn.functional.silu(g) if act == 0 else torch.nn.functional.gelu(g, approximate="tanh")) * u
+        y = lowbit_gemm_glu(x, blob, f, 2 * I, k, act)
+        assert y.shape == (M, I) and _rel(y, ref) < 1e-2, (name, M, act)
+
+
 def test_lowbit_gemm_prefill(cuda):
     f = get_format("sym_int4").fmt
     n, k, M = 384, 512, 200
