@@ -442,4 +442,43 @@ void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int6
                           block_tables, max_blocks, bs, slots, seq_lens, pos_offset);
 }
 
+// ---- RWKV-4 WKV recurrence (reference xe_linear.rwkv_linear_attention_v4,
+// models/rwkv4.py:96; HF rwkv_linear_attention_cpu semantics, f32 state in
+// max-normalised form).  One thread per (batch, channel): the time loop is a
+// true recurrence, channels are independent and coalesced across the wave.
+__global__ void __launch_bounds__(256) rwkv4_wkv_kernel(const float* __restrict__ decay,
+                                                        const float* __restrict__ first,
+                                                        const float* __restrict__ k, const float* __restrict__ v,
+                                                        float* __restrict__ out, float* num, float* den,
+                                                        float* mx, int B, int T, int C) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * C) return;
+  const int b = idx / C, c = idx % C;
+  const float w = -__expf(decay[c]), u = first[c];
+  float ns = num[idx], ds = den[idx], ms = mx[idx];
+  const size_t base = (size_t)b * T * C + c;
+  for (int t = 0; t < T; t++) {
+    const float kt = k[base + (size_t)t * C], vt = v[base + (size_t)t * C];
+    float mo = fmaxf(ms, kt + u);
+    float e1 = __expf(ms - mo), e2 = __expf(kt + u - mo);
+    out[base + (size_t)t * C] = (e1 * ns + e2 * vt) / (e1 * ds + e2);
+    const float m2 = fmaxf(ms + w, kt);
+    e1 = __expf(ms + w - m2);
+    e2 = __expf(kt - m2);
+    ns = e1 * ns + e2 * vt;
+    ds = e1 * ds + e2;
+    ms = m2;
+  }
+  num[idx] = ns;
+  den[idx] = ds;
+  mx[idx] = ms;
+}
+
+void launch_rwkv4_wkv(const float* decay, const float* first, const float* k, const float* v, float* out,
+                      float* num, float* den, float* mx, int B, int T, int C, hipStream_t st) {
+  const int n = B * C;
+  hipLaunchKernelGGL(rwkv4_wkv_kernel, dim3((n + 255) / 256), dim3(256), 0, st, decay, first, k, v, out, num, den,
+                     mx, B, T, C);
+}
+
 }  // namespace illm

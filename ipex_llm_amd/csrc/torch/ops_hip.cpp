@@ -274,6 +274,26 @@ Tensor gemm_glu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   return out;
 }
 
+// RWKV-4 WKV over [B, T, C] (f32 compute); num/den/max [B, C] f32 states updated in place
+Tensor rwkv_wkv4(const Tensor& time_decay, const Tensor& time_first, const Tensor& k, const Tensor& v, Tensor& num,
+                 Tensor& den, Tensor& mx) {
+  TORCH_CHECK(k.is_cuda() && k.dim() == 3 && v.sizes() == k.sizes(), "rwkv_wkv4: k, v [B, T, C] on the GPU");
+  c10::DeviceGuard g(k.device());
+  const int64_t B = k.size(0), T = k.size(1), C = k.size(2);
+  for (const Tensor* s : {&num, &den, &mx})
+    TORCH_CHECK(s->scalar_type() == at::kFloat && s->is_contiguous() && s->numel() == B * C,
+                "rwkv_wkv4: states must be contiguous f32 [B, C]");
+  Tensor kf = k.to(at::kFloat).contiguous(), vf = v.to(at::kFloat).contiguous();
+  Tensor w = time_decay.to(at::kFloat).contiguous(), u = time_first.to(at::kFloat).contiguous();
+  TORCH_CHECK(w.numel() == C && u.numel() == C, "rwkv_wkv4: time_decay / time_first [C]");
+  Tensor out = at::empty_like(kf);
+  if (B * C > 0 && T > 0)
+    illm::launch_rwkv4_wkv(w.data_ptr<float>(), u.data_ptr<float>(), kf.data_ptr<float>(), vf.data_ptr<float>(),
+                           out.data_ptr<float>(), num.data_ptr<float>(), den.data_ptr<float>(), mx.data_ptr<float>(),
+                           (int)B, (int)T, (int)C, cur_stream());
+  return out.to(k.scalar_type());
+}
+
 // split-K GEMV accumulated with f32 atomics into acc [M, n] (zero on entry;
 // the consumer -- add_rms_norm / rope_kv_fused with zero_*=True -- reads the
 // single slab and re-zeroes it, so no ks-slab reduction is ever needed)
@@ -941,6 +961,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv_accum", &gemv_accum);
   m.impl("gemv_norm_in", &gemv_norm_in);
   m.impl("gemm_glu", &gemm_glu);
+  m.impl("rwkv_wkv4", &rwkv_wkv4);
   m.impl("attn_decode_rope", &attn_decode_rope);
   m.impl("gemm", &gemm);
   m.impl("attn_decode_split", &attn_decode_split);

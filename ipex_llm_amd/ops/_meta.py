@@ -145,3 +145,8 @@ def _(x, blob, fmt, n, k, act):
     shape = list(x.shape)
     shape[-1] = n // 2
     return x.new_empty(shape)
+
+
+@register_fake("ipex_llm_amd::rwkv_wkv4")
+def _(time_decay, time_first, k, v, num, den, mx):
+    return torch.empty_like(k)

@@ -117,6 +117,10 @@ def _phi3_split_qkv(attn):
 def _optimize_pre(model: nn.Module, qtype: int):
     """Per-arch weight rewrites before quantization (reference convert.py:890-1089)."""
     mt = getattr(getattr(model, "config", None), "model_type", None)
+    if mt == "rwkv":
+        from ..models.rwkv import prescale_rwkv
+        prescale_rwkv(model)
+        return model
     if mt not in NATIVE_ARCHS and mt not in MOE_ARCHS:
         return model
     base = getattr(model, "model", None)
@@ -238,6 +242,9 @@ def _optimize_post(model: nn.Module):
     """Swap in the native MI355X decoder for supported architectures."""
     mt = getattr(getattr(model, "config", None), "model_type", None)
     _patch_norms(model)
+    if mt == "rwkv":
+        from ..models.rwkv import patch_rwkv
+        patch_rwkv()
     if (mt in NATIVE_ARCHS or mt in MOE_ARCHS) and getattr(model, "_illm_pre", False):
         from .hf_native import attach_native
         attach_native(model)

@@ -41,6 +41,8 @@ FAMILIES = {
     "mixtral": dict(hidden_size=H, intermediate_size=I, num_hidden_layers=L, num_attention_heads=4,
                     num_key_value_heads=2, vocab_size=V, max_position_embeddings=128, num_local_experts=4,
                     num_experts_per_tok=2),
+    "rwkv": dict(hidden_size=H, num_hidden_layers=L, attention_hidden_size=H, intermediate_size=I, vocab_size=V,
+                 context_length=128, rescale_every=1),
     "qwen2_moe": dict(hidden_size=H, intermediate_size=I, moe_intermediate_size=64,
                       shared_expert_intermediate_size=I, num_hidden_layers=L, num_attention_heads=4,
                       num_key_value_heads=2, vocab_size=V, max_position_embeddings=128, num_experts=4,

@@ -35,3 +35,35 @@ def test_gemv_glu_in_matches_glu_then_down(cuda, M, qtype):
     pg = ops.gemv_partials(x, gu, fmt, 2 * I, H, 0)
     out = ops.gemv_glu_in(pg, dn, fmt, H, I, 0, 0, torch.bfloat16).sum(0)
     assert ((out - ref).norm() / ref.norm()).item() < 1e-2
+
+
+def test_rwkv4_wkv_kernel(cuda):
+    """RWKV-4 WKV recurrence kernel vs HF rwkv_linear_attention_cpu (with and without state)"""
+    from transformers.models.rwkv.modeling_rwkv import rwkv_linear_attention_cpu
+    from ipex_llm_amd.models.rwkv import rwkv_linear_attention_native
+    torch.manual_seed(0)
+    B, T, C = 2, 37, 192
+    w, u = torch.randn(C, device=cuda), torch.randn(C, device=cuda) * 0.5
+    k, v = torch.randn(B, T, C, device=cuda), torch.randn(B, T, C, device=cuda)
+    ref, rs = rwkv_linear_attention_cpu(w, u, k, v, return_state=True)
+    got, gs = rwkv_linear_attention_native(w, u, k, v, return_state=True)
+    assert (got - ref).abs().max().item() < 1e-4
+    k2, v2 = torch.randn(B, 5, C, device=cuda), torch.randn(B, 5, C, device=cuda)
+    r2, _ = rwkv_linear_attention_cpu(w, u, k2, v2, state=[s.clone() for s in rs])
+    g2, _ = rwkv_linear_attention_native(w, u, k2, v2, state=gs)
+    assert (g2 - r2).abs().max().item() < 1e-4
+
+
+def test_rwkv_model_on_gpu_matches_cpu(cuda, tmp_path):
+    """low-bit RWKV-4 on the GPU (WKV HIP kernel via the patched HF forward) vs the same model on CPU"""
+    from transformers import RwkvConfig, RwkvForCausalLM
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    torch.manual_seed(0)
+    RwkvForCausalLM(RwkvConfig(vocab_size=128, hidden_size=128, num_hidden_layers=2, attention_hidden_size=128,
+                               intermediate_size=256, context_length=64, rescale_every=1)).save_pretrained(tmp_path)
+    ids = torch.randint(0, 128, (1, 11))
+    m = AutoModelForCausalLM.from_pretrained(str(tmp_path), load_in_low_bit="sym_int8", torch_dtype=torch.float32)
+    with torch.no_grad():
+        want = m(ids).logits
+        got = m.to(cuda)(ids.to(cuda)).logits.cpu()
+    assert ((got - want).norm() / want.norm()).item() < 1e-2
