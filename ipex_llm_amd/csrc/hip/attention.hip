@@ -599,6 +599,17 @@ template <typename T>
 __global__ void __launch_bounds__(64) attn_combine_kernel(const AttnDecodeArgs a) {
   __shared__ float wsh[1024];
   combine_row<T>(a, blockIdx.z, blockIdx.x, blockIdx.y, wsh);
+  if (a.rq_part != nullptr && blockIdx.y == 0) {
+    // fused-RoPE decode: every split has read the qkv accumulator by now, so
+    // re-zero it for the next layer's atomic GEMV (block (h, b): q head h and,
+    // for h < 2 Hkv, k/v head h)
+    float* row = (float*)a.rq_part + (size_t)blockIdx.z * a.rq_ld;
+    const int h = blockIdx.x, D = a.D;
+    for (int d = threadIdx.x * 4; d < D; d += 256) *(float4*)(row + h * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (h < 2 * a.Hkv)
+      for (int d = threadIdx.x * 4; d < D; d += 256)
+        *(float4*)(row + (a.Hq + h) * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 }
 
 template <typename T, int D, int RT>

@@ -654,7 +654,8 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, cons
 
 // decode attention with RoPE + KV append fused in (Tq == 1): q/k/v of the new
 // token come from the qkv GEMV's atomic accumulator part [B, ld] (+ bias); no
-// rope_kv launch.  The accumulator is only read (a later launch zeroes it).
+// rope_kv launch.  The combine launch re-zeroes the accumulator (part is
+// written: zero for the next atomic GEMV).
 Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin,
                         const Tensor& pos, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
                         const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
@@ -698,8 +699,7 @@ Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, c
   a.sliding_window = (int)window;
   a.kv_fp8 = 0;
   a.k_scale = a.v_scale = 1.f;
-  static const bool fused_combine = getenv("ILLM_ATTN_FUSED_COMBINE") != nullptr;
-  a.counters = fused_combine ? attn_counters(part.device(), B * Hkv) : nullptr;
+  a.counters = nullptr;          // the combine launch also re-zeroes the accumulator
   a.rq_part = part.data_ptr<float>();
   a.rq_bias = p16o(bias);
   a.rq_cos_sin = cos_sin.data_ptr<float>();

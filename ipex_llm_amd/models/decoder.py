@@ -138,6 +138,12 @@ def _ksplit(n: int, k: int) -> int:
 # (consumers read 1 slab), at batch 8 the atomic traffic (M x N x ks adds at
 # ~1.3 TB/s chip-wide) costs more than the slab reduction saves
 ACC_MAX_M = 2
+# decode batches up to this size take the fused-RoPE attention (qkv accumulated
+# atomically into one slab read by the attention, re-zeroed by its combine).
+# Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token;
+# at batch 8 the atomic qkv slab costs more than the rope launch it saves
+# (2.553 -> 2.640 ms/step), so batch > 2 keeps the split-K slabs + rope_kv
+ROPE_IN_MAX_M = 2
 
 
 class NativeAttention(nn.Module):
@@ -378,6 +384,16 @@ class NativeCausalLM(nn.Module):
                 and ((s.head_dim == 128 and group <= 16) or (s.head_dim == 256 and group <= 8))
                 and all(L.self_attn.q_norm is None and L.self_attn.k_norm is None for L in self.layers))
 
+    def _qkv_native(self, ref: torch.Tensor) -> bool:
+        """every layer's qkv projection runs the native atomic GEMV"""
+        ok = self.__dict__.get("_qkv_native_ok")
+        if ok is None:
+            ok = all(isinstance(L.self_attn.qkv_proj, LowBitLinear) and L.self_attn.qkv_proj.mp_group is None
+                     and (L.self_attn.qkv_proj.bias is None or L.self_attn.qkv_proj.bias.dtype == ref.dtype)
+                     for L in self.layers)
+            self.__dict__["_qkv_native_ok"] = ok
+        return ok and ref.is_cuda and self.tp_group is None and ops.native_gpu(ref)
+
     def _fused_mlp_ok(self, x, layer) -> bool:
         mlp = layer.mlp
         if not (x.is_cuda and isinstance(mlp, NativeMLP) and x.shape[0] <= 16 and self.tp_group is None):
@@ -438,7 +454,10 @@ class NativeCausalLM(nn.Module):
         pend = None                     # accumulator awaiting residual-add + norm
         consumed = None                 # accumulator read by the last launch: zeroed by the next GEMV
         res_pp = (residual, torch.empty_like(residual)) if norm_in else None
-        rope_in = norm_in and self._rope_in_ok(meta, cache)
+        # fused-RoPE decode attention (batch <= ROPE_IN_MAX_M, one token each): the qkv
+        # GEMV accumulates into one atomic slab that the attention reads and the
+        # combine launch re-zeroes
+        rope_in = T <= ROPE_IN_MAX_M and self._rope_in_ok(meta, cache) and self._qkv_native(residual)
         nxt_res = lambda r: res_pp[1] if r is res_pp[0] else res_pp[0]
         for li, layer in enumerate(self.layers):
             attn = layer.self_attn
@@ -448,7 +467,7 @@ class NativeCausalLM(nn.Module):
                     and (qp.bias is None or qp.bias.dtype == x.dtype) and ops.native_gpu(x):
                 # split-K GEMV reduced (+bias) inside the RoPE/KV kernel, slots from the block table:
                 # T <= 16 accumulates with atomics into one zeroed slab (re-zeroed by the kernel)
-                if T <= ACC_MAX_M:
+                if T <= ACC_MAX_M or rope_in:
                     part = self._acc(qp.out_features, T, x.device)
                     if pend is not None:
                         r2 = nxt_res(residual)
@@ -461,11 +480,16 @@ class NativeCausalLM(nn.Module):
                     part = part.unsqueeze(0)
                 else:
                     part = ops.gemv_partials(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, 0)
-                if not (norm_in and rope_in):
+                if not rope_in:
                     ops.rope_kv_fused(part, qp.bias, q, cache.k[li], cache.v[li], pos, meta.block_tables, meta.Tq,
                                       rope, s.num_heads, s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved,
                                       attn.q_norm, attn.k_norm, s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale,
                                       cache.v_scale, meta.pos_offset, zero_part=T <= ACC_MAX_M)
+                else:
+                    a_rope = ops.attn_decode_rope(qkv_acc, qp.bias, self.rope_cache, pos, cache.k[li], cache.v[li],
+                                                  meta.block_tables, meta.seq_lens, meta.nsplit, s.scale,
+                                                  s.attn_softcap, attn.sliding_window, s.num_heads, s.rot_dim,
+                                                  s.rope_interleaved, 1.0, x.dtype).view(T, -1)
             else:
                 qkv = qp(x)
                 ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,
@@ -477,27 +501,16 @@ class NativeCausalLM(nn.Module):
                 # o_proj -> atomic slab P (zeroing the slab the qkv prologue consumed);
                 # the gate/up GEMV adds P to the residual and normalises in its prologue;
                 # down -> atomic slab D (zeroing P), pending for the next layer's qkv
-                # rope_in: attention rotates q/k from the qkv slab itself and appends the new
-                # key/value (no rope launch); the o_proj GEMV then zeroes the qkv slab and the
-                # gate/up GEMV the slab the qkv prologue consumed
-                if rope_in:
-                    a = ops.attn_decode_rope(qkv_acc, qp.bias, self.rope_cache, pos, cache.k[li], cache.v[li],
-                                             meta.block_tables, meta.seq_lens, meta.nsplit, s.scale,
-                                             s.attn_softcap, attn.sliding_window, s.num_heads, s.rot_dim,
-                                             s.rope_interleaved, 1.0, x.dtype).view(T, -1)
-                    zero_o, zero_gu = qkv_acc, consumed
-                else:
-                    a = self._attention(li, attn, q, meta, cache)
-                    zero_o, zero_gu = consumed, None
+                a = a_rope if rope_in else self._attention(li, attn, q, meta, cache)
                 o, mlp = attn.o_proj, layer.mlp
                 H = o.out_features
                 accP, accD = self._acc(H, T, x.device, "P"), self._acc(H, T, x.device, "D")
-                ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=zero_o)
+                ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
                 r2 = nxt_res(residual)
                 gu, dn = mlp.gate_up_proj, mlp.down_proj
                 act = ops.gemv_norm_in(accP, residual, r2, layer.post_attention_layernorm, s.rms_eps,
                                        s.norm_unit_offset, gu.weight, gu.fmt, gu.out_features, gu.in_features, True,
-                                       s.act, zero=zero_gu)
+                                       s.act)
                 residual = r2
                 ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=accP)
                 consumed = None
@@ -508,14 +521,14 @@ class NativeCausalLM(nn.Module):
                     x, _ = ops.add_rms_norm(None, residual, nxt, s.rms_eps, partials=accD.unsqueeze(0),
                                             unit_offset=s.norm_unit_offset, zero_partials=True)
                 continue
-            if self._attn_oproj_fuse_ok(attn, q, meta):
+            if not rope_in and self._attn_oproj_fuse_ok(attn, q, meta):
                 x = self._attn_oproj_norm(li, attn, q, meta, cache, residual, layer.post_attention_layernorm)
             elif s.sandwich_norm:
-                a = self._attention(li, attn, q, meta, cache)
+                a = a_rope if rope_in else self._attention(li, attn, q, meta, cache)
                 x = self._proj_residual_norm(a, attn.o_proj, residual, layer.pre_feedforward_layernorm,
                                              post_norm_w=layer.post_attention_layernorm)
             else:
-                a = self._attention(li, attn, q, meta, cache)
+                a = a_rope if rope_in else self._attention(li, attn, q, meta, cache)
                 x = self._proj_residual_norm(a, attn.o_proj, residual, layer.post_attention_layernorm)
             if li + 1 < len(self.layers):
                 nxt = self.layers[li + 1].input_layernorm

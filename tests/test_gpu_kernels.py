@@ -156,7 +156,7 @@ def test_decode_norm_in_matches_standalone_norms(cuda):
     cfg = LlamaConfig(vocab_size=512, hidden_size=512, intermediate_size=1024, num_hidden_layers=3,
                       num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=1024)
     m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=4)
-    prompts = [list(range(1, 50)), list(range(7, 70))]
+    prompts = [list(range(1, 50)), list(range(7, 70)), list(range(3, 40)), [5] * 30]
     outs = {}
     try:
         for flag in (False, True, "rope"):
