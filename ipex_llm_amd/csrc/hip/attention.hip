@@ -14,6 +14,7 @@
 // Per-split (m, l, o) partials are merged by a second small kernel.  Sequence
 // lengths and block tables are device tensors: the launch geometry depends
 // only on the max length bucket, so the whole thing is hipGraph-capturable.
+#include <cstdlib>
 #include "../common/quant_block.h"
 #include "illm_device.h"
 #include "kernels.h"
@@ -225,7 +226,11 @@ __device__ __forceinline__ uint4 kv_frag8(const uint8_t* p) {
   }
 }
 
-template <typename T, int D, int KVF, int RT, bool RQ = false>
+// LATEV: issue the V loads after Q K^T (K registers are dead by then): fewer
+// VGPRs and the V stream overlaps the QK/softmax of the co-resident wave.
+// Chosen for grids larger than one wave per SIMD (measured on MI355X at
+// batch 8, 1088 waves: 2.564 -> 2.524 ms/step; ILLM_ATTN_LATEV=0/1 forces it)
+template <typename T, int D, int KVF, int RT, bool RQ = false, bool LATEV = false>
 __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs a) {
   constexpr int EB = KVF == 0 ? 2 : 1;
   constexpr int KSTEP = D / 32;       // MFMA k-steps over the head dim
@@ -285,14 +290,17 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   }
   const int dg = r16, kg = g;
   uint4 vf[16][VCH];
-  if constexpr (DPL >= 8) {
+  auto load_v = [&]() {
+    if constexpr (DPL >= 8) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int kk = min(4 * i + kg, nk - 1);
+      for (int i = 0; i < 16; i++) {
+        const int kk = min(4 * i + kg, nk - 1);
 #pragma unroll
-      for (int c = 0; c < VCH; c++) vf[i][c] = kv_frag8<T, KVF>(vb + ((size_t)kk * D + DPL * dg + 8 * c) * EB);
+        for (int c = 0; c < VCH; c++) vf[i][c] = kv_frag8<T, KVF>(vb + ((size_t)kk * D + DPL * dg + 8 * c) * EB);
+      }
     }
-  }
+  };
+  if constexpr (!LATEV) load_v();
   uint4 qf[KSTEP];
   if constexpr (rq) {
     // a lane's q / k dims are 32 s + 8 g + j (s < KSTEP, j < 8): with full-width
@@ -435,6 +443,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     for (int s = 0; s < KSTEP; s++) acc = mfma16<T>(kf[kt][s], qf[s], acc);
     st[kt] = acc;
   }
+  if constexpr (LATEV) load_v();
   const int row = r16;
   const int t = row / group;
   const int h = kvh * group + (row % group);
@@ -626,9 +635,24 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
       return;
     }
   }
-  if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT>), grid, dim3(64), 0, st, a);
-  else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT>), grid, dim3(64), 0, st, a);
-  else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT>), grid, dim3(64), 0, st, a);
+  static int simds = 0;
+  if (simds == 0) {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    simds = 4 * (cus > 0 ? cus : 256);
+  }
+  static const int latev_env = getenv("ILLM_ATTN_LATEV") ? atoi(getenv("ILLM_ATTN_LATEV")) : -1;
+  const bool latev = latev_env >= 0 ? latev_env == 1 : (long)a.nsplit * a.Hkv * a.B > simds;
+  if (latev) {
+    if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT, false, true>), grid, dim3(64), 0, st, a);
+    else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT, false, true>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, false, true>), grid, dim3(64), 0, st, a);
+  } else {
+    if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT>), grid, dim3(64), 0, st, a);
+    else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT>), grid, dim3(64), 0, st, a);
+  }
   if (a.counters == nullptr && !a.no_combine)
     hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
 }
