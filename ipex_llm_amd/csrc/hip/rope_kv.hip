@@ -40,8 +40,30 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
   auto raw = [&](int d) -> float {
     if (!a.part) return to_f32<T>(src[d]);
     float s = a.bias ? to_f32<T>(a.bias[col0 + d]) : 0.f;
+#pragma unroll 4
     for (int k = 0; k < a.nsplit; k++) s += a.part[((size_t)k * a.T + t) * a.ld_qkv + col0 + d];
     return to_f32<T>(from_f32<T>(s));
+  };
+  // two elements at once: both columns' split-K loads are in flight together
+  // (the per-split loads are independent; only the adds are ordered)
+  auto raw2 = [&](int d0, int d1, float& r0, float& r1) {
+    if (!a.part) {
+      r0 = to_f32<T>(src[d0]);
+      r1 = to_f32<T>(src[d1]);
+      return;
+    }
+    float s0 = a.bias ? to_f32<T>(a.bias[col0 + d0]) : 0.f;
+    float s1 = a.bias ? to_f32<T>(a.bias[col0 + d1]) : 0.f;
+    const float* pk = a.part + (size_t)t * a.ld_qkv + col0;
+    const size_t kstride = (size_t)a.T * a.ld_qkv;
+#pragma unroll 4
+    for (int k = 0; k < a.nsplit; k++) {
+      s0 += pk[d0];
+      s1 += pk[d1];
+      pk += kstride;
+    }
+    r0 = to_f32<T>(from_f32<T>(s0));
+    r1 = to_f32<T>(from_f32<T>(s1));
   };
 
   // per-head RMSNorm (qwen3 q_norm / k_norm): sum of squares over D
@@ -107,13 +129,26 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
       // HF casts cos/sin to the activation dtype before the rotation
       c = to_f32<T>(from_f32<T>(c));
       s = to_f32<T>(from_f32<T>(s));
-      const float x0 = val(d0), x1 = val(d1);
+      float x0, x1;
+      if (nw) {
+        x0 = val(d0);
+        x1 = val(d1);
+      } else {
+        raw2(d0, d1, x0, x1);
+      }
       put(d0, to_f32<T>(from_f32<T>(x0 * c)) - to_f32<T>(from_f32<T>(x1 * s)));
       put(d1, to_f32<T>(from_f32<T>(x1 * c)) + to_f32<T>(from_f32<T>(x0 * s)));
     }
     for (int d = a.rot_dim + lane; d < D; d += 64) put(d, val(d));
   } else {
-    for (int d = lane; d < D; d += 64) put(d, raw(d));
+    int d = lane;
+    for (; d + 64 < D; d += 128) {
+      float v0, v1;
+      raw2(d, d + 64, v0, v1);
+      put(d, v0);
+      put(d + 64, v1);
+    }
+    if (d < D) put(d, raw(d));
   }
   if (a.part && a.zero_part) {
     // every read of this head's columns above was made by this wave
