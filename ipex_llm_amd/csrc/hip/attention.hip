@@ -572,34 +572,56 @@ __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int 
   const int len = a.seq_lens[b];
   const int ns = min(a.nsplit, (len + SPLIT - 1) / SPLIT);
   const size_t row0 = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit;
-  float M = -INFINITY;
-  for (int s = lane; s < ns; s += 64) M = fmaxf(M, a.part_ml[(row0 + s) * 2]);
-  M = wave_max(M);
-  float L = 0.f;
-  for (int s = lane; s < ns; s += 64) {
-    const float2 ml = *(const float2*)(a.part_ml + (row0 + s) * 2);
+  float M = -INFINITY, L = 0.f;
+  if (ns <= 64) {
+    // one (m, l) pair per lane, loaded once
+    float2 ml = make_float2(-INFINITY, 0.f);
+    if (lane < ns) ml = *(const float2*)(a.part_ml + (row0 + lane) * 2);
+    M = wave_max(ml.x);
     const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
-    L += w * ml.y;
-    if (s < 1024) wsh[s] = w;
+    L = w * ml.y;
+    if (lane < ns) wsh[lane] = w;
+  } else {
+    for (int s = lane; s < ns; s += 64) M = fmaxf(M, a.part_ml[(row0 + s) * 2]);
+    M = wave_max(M);
+    for (int s = lane; s < ns; s += 64) {
+      const float2 ml = *(const float2*)(a.part_ml + (row0 + s) * 2);
+      const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
+      L += w * ml.y;
+      if (s < 1024) wsh[s] = w;
+    }
   }
   L = wave_sum(L);
   __syncthreads();
   const float invL = L > 0.f ? 1.f / L : 0.f;
   uint16_t* out = a.out + (((size_t)b * a.Tq + t) * a.Hq + h) * a.D;
   const float* po = a.part_o + row0 * a.D;
-  for (int d = lane; d < a.D; d += 64) {
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+  // two head dims per lane (d, d + 64) so both columns' split loads are in
+  // flight together: half the dependent memory round trips at D = 128
+  for (int d = lane; d < a.D; d += 128) {
+    const bool two = d + 64 < a.D;
+    const int e = two ? d + 64 : d;
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, x3 = 0.f, y0 = 0.f, y1 = 0.f, y2 = 0.f, y3 = 0.f;
     int s = 0;
     for (; s + 4 <= ns; s += 4) {
-      const float v0 = po[(size_t)(s + 0) * a.D + d], v1 = po[(size_t)(s + 1) * a.D + d];
-      const float v2 = po[(size_t)(s + 2) * a.D + d], v3 = po[(size_t)(s + 3) * a.D + d];
-      acc0 += wsh[s] * v0;
-      acc1 += wsh[s + 1] * v1;
-      acc2 += wsh[s + 2] * v2;
-      acc3 += wsh[s + 3] * v3;
+      const float* p0 = po + (size_t)s * a.D;
+      const float u0 = p0[d], u1 = p0[a.D + d], u2 = p0[2 * a.D + d], u3 = p0[3 * a.D + d];
+      const float v0 = p0[e], v1 = p0[a.D + e], v2 = p0[2 * a.D + e], v3 = p0[3 * a.D + e];
+      x0 += wsh[s] * u0;
+      x1 += wsh[s + 1] * u1;
+      x2 += wsh[s + 2] * u2;
+      x3 += wsh[s + 3] * u3;
+      y0 += wsh[s] * v0;
+      y1 += wsh[s + 1] * v1;
+      y2 += wsh[s + 2] * v2;
+      y3 += wsh[s + 3] * v3;
     }
-    for (; s < ns; s++) acc0 += wsh[s] * po[(size_t)s * a.D + d];
-    out[d] = from_f32<T>((acc0 + acc1 + acc2 + acc3) * invL);
+    for (; s < ns; s++) {
+      x0 += wsh[s] * po[(size_t)s * a.D + d];
+      y0 += wsh[s] * po[(size_t)s * a.D + e];
+    }
+    out[d] = from_f32<T>((x0 + x1 + x2 + x3) * invL);
+    if (two) out[e] = from_f32<T>((y0 + y1 + y2 + y3) * invL);
   }
   __syncthreads();
 }
