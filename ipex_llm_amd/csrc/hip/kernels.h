@@ -128,6 +128,7 @@ void launch_attn_decode(bool bf16, const AttnDecodeArgs& a, hipStream_t st);
 // ---- elementwise & misc (misc.hip) ------------------------------------------
 void launch_rwkv4_wkv(const float* decay, const float* first, const float* k, const float* v, float* out,
                       float* num, float* den, float* mx, int B, int T, int C, hipStream_t st);
+void launch_softmax_rows(bool bf16, uint16_t* x, int64_t rows, int L, hipStream_t st);
 void launch_glu(bool bf16, const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act,
                 hipStream_t st);
 void launch_quantize_device(int fmt, int in_kind, const void* w, int64_t n, int64_t k,

@@ -44,6 +44,33 @@ void launch_glu(bool bf16, const uint16_t* gu, int ld, uint16_t* out, int M, int
   else hipLaunchKernelGGL(glu_kernel<F16>, dim3(blocks), dim3(256), 0, st, gu, ld, out, M, I, act);
 }
 
+// ---- in-place row softmax (eager attention weights) -------------------------
+// Reference op: xe_addons.attn_softmax_inplaced (models/common.py:174-181).
+// One wave64 per row, four rows per workgroup; f32 math, result rounded to T.
+// A fully masked row (max = -inf) is written as zeros.
+template <typename T>
+__global__ void __launch_bounds__(256) softmax_rows_kernel(uint16_t* x, int64_t rows, int L) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+  if (row >= rows) return;   // whole wave leaves together; no block barrier below
+  const int lane = threadIdx.x & 63;
+  uint16_t* p = x + row * (int64_t)L;
+  float m = -INFINITY;
+  for (int i = lane; i < L; i += 64) m = fmaxf(m, to_f32<T>(p[i]));
+  m = wave_max(m);
+  float s = 0.f;
+  if (m != -INFINITY)
+    for (int i = lane; i < L; i += 64) s += __expf(to_f32<T>(p[i]) - m);
+  s = wave_sum(s);
+  const float inv = s > 0.f ? 1.f / s : 0.f;
+  for (int i = lane; i < L; i += 64) p[i] = from_f32<T>(s > 0.f ? __expf(to_f32<T>(p[i]) - m) * inv : 0.f);
+}
+
+void launch_softmax_rows(bool bf16, uint16_t* x, int64_t rows, int L, hipStream_t st) {
+  const int64_t blocks = (rows + 3) / 4;
+  if (bf16) hipLaunchKernelGGL(softmax_rows_kernel<BF16>, dim3((unsigned)blocks), dim3(256), 0, st, x, rows, L);
+  else hipLaunchKernelGGL(softmax_rows_kernel<F16>, dim3((unsigned)blocks), dim3(256), 0, st, x, rows, L);
+}
+
 // ---- quantize on device: dense [n, k] -> MI355X tiled blob ------------------
 __device__ __forceinline__ float load_in(const void* w, int kind, size_t i) {
   if (kind == 0) return ((const float*)w)[i];

@@ -798,6 +798,16 @@ Tensor glu(const Tensor& gu, int64_t act) {
   return out;
 }
 
+void attn_softmax_(const Tensor& x) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "attn_softmax_: contiguous bf16/fp16 GPU tensor expected");
+  TORCH_CHECK(x.dim() >= 1 && x.size(-1) > 0 && x.size(-1) < (1LL << 31), "attn_softmax_: bad row length");
+  const int64_t L = x.size(-1), rows = x.numel() / L;
+  TORCH_CHECK((rows + 3) / 4 < (1LL << 31), "attn_softmax_: too many rows");
+  if (rows > 0) illm::launch_softmax_rows(is_bf16(x), (uint16_t*)x.data_ptr(), rows, (int)L, cur_stream());
+}
+
 Tensor reduce_partials(const Tensor& ws, const c10::optional<Tensor>& bias, at::ScalarType dt) {
   c10::DeviceGuard g(ws.device());
   const int64_t ks = ws.size(0), M = ws.size(1), N = ws.size(2);
@@ -971,6 +981,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("rope_kv", &rope_kv);
   m.impl("attn_decode", &attn_decode);
   m.impl("glu", &glu);
+  m.impl("attn_softmax_", &attn_softmax_);
   m.impl("reduce_partials", &reduce_partials);
   m.impl("moe_topk", &moe_topk);
 }

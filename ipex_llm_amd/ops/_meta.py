@@ -54,6 +54,11 @@ def _(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, windo
     return torch.empty_like(q)
 
 
+@register_fake("ipex_llm_amd::attn_softmax_")
+def _(x):
+    return None
+
+
 @register_fake("ipex_llm_amd::glu")
 def _(gu, act):
     shape = list(gu.shape)

@@ -16,7 +16,7 @@ from . import reference as R
 __all__ = [
     "quantize", "dequantize", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
-    "attn_decode", "glu", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
+    "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
     "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope",
 ]
@@ -184,6 +184,15 @@ def glu(gu, act=0):
     if _native(gu) and (gu.shape[-1] // 2) % 8 == 0:
         return _ops().glu(gu, act)
     return R.glu(gu, act)
+
+
+def attn_softmax_(x: torch.Tensor) -> torch.Tensor:
+    """In-place softmax over the last dim (reference xe_addons.attn_softmax_inplaced,
+    models/common.py:174-181).  f32 math, result in x's dtype."""
+    if _native(x) and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float16):
+        _ops().attn_softmax_(x)
+        return x
+    return x.copy_(torch.softmax(x.float(), -1).to(x.dtype))
 
 
 def moe_topk(logits, k, renorm=True, scoring=0):

@@ -330,3 +330,20 @@ def test_moe_topk(cuda):
     rw, rids = R.moe_topk(logits, 4, True, 0)
     assert torch.equal(ids.cpu(), rids.cpu())
     assert torch.allclose(w, rw, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(2, 8, 1, 1), (1, 4, 7, 300), (3, 2, 5, 4097)])
+def test_attn_softmax_inplace(cuda, dtype, shape):
+    """In-place row softmax kernel vs the fp32 torch softmax (masked entries included)."""
+    torch.manual_seed(0)
+    x = (torch.randn(*shape, device=cuda) * 4).to(dtype)
+    if shape[-1] > 2:
+        x[..., ::3] = float("-inf")
+    ref = torch.softmax(x.float(), -1)
+    y = ops.attn_softmax_(x)
+    assert y.data_ptr() == x.data_ptr()
+    torch.testing.assert_close(x.float(), ref, atol=4e-3, rtol=1e-2)
+    z = torch.full((2, 33), float("-inf"), device=cuda, dtype=dtype)
+    ops.attn_softmax_(z)
+    assert (z == 0).all()

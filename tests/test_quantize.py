@@ -97,3 +97,13 @@ def test_imatrix_file_roundtrip_and_weighted_quantization(tmp_path):
     w = torch.randn(64, K)
     err = lambda blob: (((ops.dequantize(blob, fmt, 64, K) - w) ** 2) * imp).sum().item()  # noqa: E731
     assert err(ops.quantize(w, fmt, imp, True)) < err(ops.quantize(w, fmt, None, False))
+
+
+def test_attn_softmax_cpu_fallback():
+    """CPU path of ops.attn_softmax_ is the in-place fp32 softmax."""
+    import torch
+    from ipex_llm_amd import ops
+    x = torch.randn(2, 3, 17).to(torch.bfloat16)
+    ref = torch.softmax(x.float(), -1).to(torch.bfloat16)
+    y = ops.attn_softmax_(x)
+    assert y is x and torch.equal(x, ref)
