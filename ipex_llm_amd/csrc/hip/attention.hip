@@ -573,6 +573,26 @@ __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int 
   const int ns = min(a.nsplit, (len + SPLIT - 1) / SPLIT);
   const size_t row0 = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit;
   float M = -INFINITY, L = 0.f;
+  if (ns > 1024) {
+    // more splits than the LDS weight scratch holds (> 64 Ki keys): every
+    // lane recomputes the split weights it needs (rare, long-context only)
+    for (int s = lane; s < ns; s += 64) M = fmaxf(M, a.part_ml[(row0 + s) * 2]);
+    M = wave_max(M);
+    uint16_t* out = a.out + (((size_t)b * a.Tq + t) * a.Hq + h) * a.D;
+    const float* po = a.part_o + row0 * a.D;
+    for (int d = lane; d < a.D; d += 64) {
+      float x = 0.f, l = 0.f;
+      for (int s = 0; s < ns; s++) {
+        const float2 ml = *(const float2*)(a.part_ml + (row0 + s) * 2);
+        const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
+        l += w * ml.y;
+        x += w * po[(size_t)s * a.D + d];
+      }
+      out[d] = from_f32<T>(l > 0.f ? x / l : 0.f);
+    }
+    __syncthreads();
+    return;
+  }
   if (ns <= 64) {
     // one (m, l) pair per lane, loaded once
     float2 ml = make_float2(-INFINITY, 0.f);
@@ -637,9 +657,11 @@ __global__ void __launch_bounds__(64) attn_combine_kernel(const AttnDecodeArgs a
     float* row = (float*)a.rq_part + (size_t)blockIdx.z * a.rq_ld;
     const int h = blockIdx.x, D = a.D;
     for (int d = threadIdx.x * 4; d < D; d += 256) *(float4*)(row + h * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (h < 2 * a.Hkv)
+    // the 2 Hkv k/v column blocks are dealt over the Hq blocks (all of them
+    // are covered for any Hq / Hkv ratio, MHA included)
+    for (int hh = h; hh < 2 * a.Hkv; hh += a.Hq)
       for (int d = threadIdx.x * 4; d < D; d += 256)
-        *(float4*)(row + (a.Hq + h) * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+        *(float4*)(row + (a.Hq + hh) * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 

@@ -188,11 +188,15 @@ def glu(gu, act=0):
 
 def attn_softmax_(x: torch.Tensor) -> torch.Tensor:
     """In-place softmax over the last dim (reference xe_addons.attn_softmax_inplaced,
-    models/common.py:174-181).  f32 math, result in x's dtype."""
+    models/common.py:174-181).  f32 math, result in x's dtype.  A fully
+    masked row (every score -inf) comes out as zeros on both paths."""
     if _native(x) and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float16):
         _ops().attn_softmax_(x)
         return x
-    return x.copy_(torch.softmax(x.float(), -1).to(x.dtype))
+    xf = x.float()
+    y = torch.softmax(xf, -1)
+    y = torch.where(torch.isneginf(xf.amax(-1, keepdim=True)), torch.zeros_like(y), y)
+    return x.copy_(y.to(x.dtype))
 
 
 def moe_topk(logits, k, renorm=True, scoring=0):

@@ -242,6 +242,8 @@ def _optimize_post(model: nn.Module):
     """Swap in the native MI355X decoder for supported architectures."""
     mt = getattr(getattr(model, "config", None), "model_type", None)
     _patch_norms(model)
+    from .attention import patch_eager_attention
+    patch_eager_attention(model)
     if mt == "rwkv":
         from ..models.rwkv import patch_rwkv
         patch_rwkv()

@@ -116,13 +116,15 @@ def test_gemv_norm_in(cuda, name, M):
     assert torch.equal(res_out2, res_ref)
 
 
-@pytest.mark.parametrize("B,interleaved", [(1, False), (2, False), (2, True)])
-def test_attn_decode_rope_matches_rope_kv(cuda, B, interleaved):
+@pytest.mark.parametrize("B,interleaved,Hq,Hkv", [(1, False, 8, 2), (2, False, 8, 2), (2, True, 8, 2),
+                                                   (2, False, 8, 8), (1, False, 4, 4), (2, False, 4, 2)])
+def test_attn_decode_rope_matches_rope_kv(cuda, B, interleaved, Hq, Hkv):
     """decode attention with RoPE + KV append fused in vs rope_kv_fused +
-    attn_decode: identical cache contents, same attention output"""
+    attn_decode: identical cache contents, same attention output, and the
+    qkv accumulator left all zero for the next layer (MHA included)"""
     from ipex_llm_amd.engine.runner import nsplit_for
     torch.manual_seed(3)
-    Hq, Hkv, D, bs = 8, 2, 128, 64
+    D, bs = 128, 64
     L = [70, 131][:B]
     kc = torch.randn(4 * B, Hkv, bs, D, device=cuda).bfloat16()
     vc = torch.randn(4 * B, Hkv, bs, D, device=cuda).bfloat16()
@@ -141,10 +143,56 @@ def test_attn_decode_rope_matches_rope_kv(cuda, B, interleaved):
     ops.rope_kv_fused(part.clone().unsqueeze(0), bias, q, kc1, vc1, pos, bt, 1, cs, Hq, Hkv, D, D, interleaved)
     ref = ops.attn_decode(q.view(B, 1, Hq, D), kc1, vc1, bt, seq_lens, ns, D ** -0.5)
     kc2, vc2 = kc.clone(), vc.clone()
-    got = ops.attn_decode_rope(part, bias, cs, pos, kc2, vc2, bt, seq_lens, ns, D ** -0.5, 0.0, 0, Hq, D,
+    part2 = part.clone()
+    got = ops.attn_decode_rope(part2, bias, cs, pos, kc2, vc2, bt, seq_lens, ns, D ** -0.5, 0.0, 0, Hq, D,
                                interleaved, 1.0, torch.bfloat16)
     assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
     assert _rel(got, ref) < 1e-3
+    torch.cuda.synchronize()
+    assert int((part2 != 0).sum()) == 0, "qkv accumulator not re-zeroed"
+
+
+def test_attn_decode_long_context_combine(cuda):
+    """> 1024 splits (> 64 Ki keys): the combine takes its no-LDS path"""
+    torch.manual_seed(5)
+    Hq, Hkv, D, bs = 2, 1, 64, 256
+    L = 70000
+    nblk = (L + bs - 1) // bs
+    kc = torch.randn(nblk, Hkv, bs, D, device=cuda).bfloat16()
+    vc = torch.randn(nblk, Hkv, bs, D, device=cuda).bfloat16()
+    bt = torch.randperm(nblk, device=cuda).to(torch.int32).view(1, nblk)
+    seq_lens = torch.tensor([L], dtype=torch.int32, device=cuda)
+    q = torch.randn(1, 1, Hq, D, device=cuda).bfloat16()
+    ns = (L + 63) // 64
+    assert ns > 1024
+    got = ops.attn_decode(q, kc, vc, bt, seq_lens, ns, D ** -0.5)
+    kk = ops.api.gather_kv(kc, bt, 0, L).float()          # [L, Hkv, D]
+    vv = ops.api.gather_kv(vc, bt, 0, L).float()
+    s = torch.einsum("hd,ld->hl", q[0, 0].float(), kk[:, 0]) * D ** -0.5
+    ref = torch.softmax(s, -1) @ vv[:, 0]
+    assert _rel(got[0, 0].float(), ref) < 1e-2
+
+
+def test_decode_rope_in_mha_multilayer(cuda):
+    """multi-layer MHA (Hq == Hkv) decode: fused-RoPE attention path gives the
+    same tokens as the rope_kv launch path (the slab re-zeroing covers every
+    k/v head)"""
+    from transformers import LlamaConfig
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.models.decoder import NativeCausalLM
+    cfg = LlamaConfig(vocab_size=512, hidden_size=512, intermediate_size=1024, num_hidden_layers=3,
+                      num_attention_heads=4, num_key_value_heads=4, max_position_embeddings=1024)
+    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=9)
+    prompts = [list(range(1, 50))]
+    outs = {}
+    try:
+        for flag in (False, True):
+            NativeCausalLM._rope_in_env = flag
+            outs[flag] = Engine(m).generate(prompts, max_new_tokens=12, use_graph=True)
+    finally:
+        NativeCausalLM._rope_in_env = True
+    assert outs[True] == outs[False]
 
 
 def test_decode_norm_in_matches_standalone_norms(cuda):

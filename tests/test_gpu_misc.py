@@ -67,3 +67,42 @@ def test_rwkv_model_on_gpu_matches_cpu(cuda, tmp_path):
         want = m(ids).logits
         got = m.to(cuda)(ids.to(cuda)).logits.cpu()
     assert ((got - want).norm() / want.norm()).item() < 1e-2
+
+
+def test_hf_eager_family_on_gpu_uses_hip_softmax(cuda, tmp_path):
+    """eager-configured HF-forward family (phi) on the GPU: illm_eager runs
+    the in-place HIP softmax; logits stay close to the dense fp32 model"""
+    from transformers import AutoConfig, AutoModelForCausalLM as HFAuto
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    cfg = AutoConfig.for_model("phi", hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                               num_attention_heads=4, vocab_size=256, max_position_embeddings=128)
+    torch.manual_seed(0)
+    ref = HFAuto.from_config(cfg, attn_implementation="eager").eval()
+    p = str(tmp_path / "phi")
+    ref.save_pretrained(p)
+    ids = torch.randint(3, 256, (2, 16), generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        want = ref(ids).logits.float()
+    m = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="bf16", torch_dtype=torch.bfloat16,
+                                             attn_implementation="eager").to(cuda)
+    assert m.config._attn_implementation == "illm_eager"
+    seen = []
+    orig = torch.ops.ipex_llm_amd.attn_softmax_
+    import ipex_llm_amd.ops.api as api
+
+    class Spy:
+        def __getattr__(self, n):
+            return getattr(torch.ops.ipex_llm_amd, n)
+
+        def attn_softmax_(self, x):
+            seen.append(tuple(x.shape))
+            return orig(x)
+    real = api._ops
+    api._ops = lambda: Spy()
+    try:
+        with torch.no_grad():
+            got = m(ids.to(cuda)).logits.float().cpu()
+    finally:
+        api._ops = real
+    assert seen and seen[0][-2:] == (16, 16)
+    assert ((got - want).norm() / want.norm()).item() < 3e-2

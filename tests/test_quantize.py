@@ -107,3 +107,49 @@ def test_attn_softmax_cpu_fallback():
     ref = torch.softmax(x.float(), -1).to(torch.bfloat16)
     y = ops.attn_softmax_(x)
     assert y is x and torch.equal(x, ref)
+
+
+def test_attn_softmax_fully_masked_row_is_zero():
+    """a fully masked row is zeros on the fallback, as on the HIP kernel"""
+    import torch
+    from ipex_llm_amd import ops
+    x = torch.randn(3, 9).to(torch.bfloat16)
+    x[1] = float("-inf")
+    ops.attn_softmax_(x)
+    assert torch.equal(x[1], torch.zeros(9, dtype=torch.bfloat16))
+    assert torch.isfinite(x.float()).all()
+
+
+@pytest.mark.parametrize("mt", ["phi", "gpt_neox"])
+def test_hf_eager_attention_uses_illm_softmax(mt, tmp_path, monkeypatch):
+    """an eager-configured HF-forward family is routed through illm_eager
+    (ops.attn_softmax_) and keeps the dense model's logits"""
+    import torch
+    from transformers import AutoConfig, AutoModelForCausalLM as HFAuto
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    cfg = AutoConfig.for_model(mt, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                               num_attention_heads=4, vocab_size=256, max_position_embeddings=128)
+    cfg._attn_implementation = "eager"
+    torch.manual_seed(0)
+    ref = HFAuto.from_config(cfg, attn_implementation="eager").eval()
+    p = str(tmp_path / mt)
+    ref.save_pretrained(p)
+    ids = torch.randint(3, 256, (2, 12), generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        want = ref(ids).logits.float()
+    calls = []
+    orig = ops.attn_softmax_
+
+    def spy(x):
+        calls.append(x.shape)
+        return orig(x)
+    import ipex_llm_amd.transformers.attention as A
+    monkeypatch.setattr(A.ops, "attn_softmax_", spy)
+    m = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="bf16", torch_dtype=torch.float32,
+                                             attn_implementation="eager")
+    assert m.config._attn_implementation == "illm_eager"
+    with torch.no_grad():
+        got = m(ids).logits.float()
+    assert calls, "illm_eager attention not used"
+    assert ((got - want).norm() / want.norm()).item() < 2e-2
