@@ -22,8 +22,12 @@ import time
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-OBJ = os.path.join(ROOT, "build", "obj")
-LIB = os.path.join(PKG, "_C.so")
+# A/B builds: ILLM_BUILD_DEFS="-DFOO=1" ILLM_BUILD_TAG=foo -> build/obj_foo, _C_foo.so
+# (loaded with IPEX_LLM_AMD_LIB=_C_foo.so)
+_DEFS = os.environ.get("ILLM_BUILD_DEFS", "").split()
+_TAG = os.environ.get("ILLM_BUILD_TAG", "")
+OBJ = os.path.join(ROOT, "build", "obj" + (f"_{_TAG}" if _TAG else ""))
+LIB = os.path.join(PKG, f"_C_{_TAG}.so" if _TAG else "_C.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
@@ -44,7 +48,7 @@ def _headers_mtime() -> float:
 
 def _cmd(src: str, obj: str):
     tinc, tapi, _ = _torch_paths()
-    common = ["-O3", "-fPIC", "-std=c++17", "-I", CSRC]
+    common = ["-O3", "-fPIC", "-std=c++17", "-I", CSRC, *_DEFS]
     if src.endswith(".hip"):
         extra = []
         if os.path.basename(src).startswith("gemv_"):

@@ -135,6 +135,21 @@ __host__ __device__ constexpr size_t gemv5_attn_shmem(int rows, int cpk, int D, 
   return (size_t)rows * gemv5_attn_heads(cpk, D) * (ns + 1) * 4;
 }
 
+// weight stream loads: read once per decode step by one CU, so the
+// non-temporal policy (ILLM_GEMV_NT=1 at build time) is an option
+#ifndef ILLM_GEMV_NT
+#define ILLM_GEMV_NT 0
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
+#if ILLM_GEMV_NT
+  const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+#else
+  return *(const uint4*)p;
+#endif
+}
+
 template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW>
 __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a) {
   constexpr int PF = 4;                 // chunks in flight per wave (8 measured slower)
@@ -198,10 +213,10 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
 #pragma unroll
     for (int t = 0; t < TPW; t++) {
       const uint8_t* rec = tb[t] + (size_t)c * dk_code_chunk(DK);
-      ch.q[t][0] = *(const uint4*)(rec + lane * 16);
-      if constexpr (BITS == 8) ch.q[t][1] = *(const uint4*)(rec + 1024 + lane * 16);
-      ch.sc[t] = *(const uint4*)(tb[t] + soff + (size_t)c * 64);
-      if constexpr (HASMIN) ch.mn[t] = *(const uint4*)(tb[t] + moff + (size_t)c * 64);
+      ch.q[t][0] = ldw16(rec + lane * 16);
+      if constexpr (BITS == 8) ch.q[t][1] = ldw16(rec + 1024 + lane * 16);
+      ch.sc[t] = ldw16(tb[t] + soff + (size_t)c * 64);
+      if constexpr (HASMIN) ch.mn[t] = ldw16(tb[t] + moff + (size_t)c * 64);
     }
   };
   Chunk ring[PF];
@@ -505,20 +520,48 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
   }
 
   // ---- reduce the KW k-parts of each tile group through LDS
+  constexpr bool ATOMIC_T = EPI == EPI_ATOMIC && !MOE;   // block-transposed atomic epilogue
   if constexpr (KW > 1) {
 #pragma unroll
     for (int t = 0; t < TPW; t++)
       red[(wave * TPW + t) * 64 + lane] = make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
     __syncthreads();
-    if (kp != 0) return;
+    if (!ATOMIC_T && kp != 0) return;
+    if (kp == 0) {
 #pragma unroll
-    for (int t = 0; t < TPW; t++) {
+      for (int t = 0; t < TPW; t++) {
 #pragma unroll
-      for (int j = 1; j < KW; j++) {
-        const float4 v = red[((wave + j) * TPW + t) * 64 + lane];
-        acc[t][0] += v.x; acc[t][1] += v.y; acc[t][2] += v.z; acc[t][3] += v.w;
+        for (int j = 1; j < KW; j++) {
+          const float4 v = red[((wave + j) * TPW + t) * 64 + lane];
+          acc[t][0] += v.x; acc[t][1] += v.y; acc[t][2] += v.z; acc[t][3] += v.w;
+        }
       }
     }
+  }
+  if constexpr (ATOMIC_T) {
+    // split-K f32 atomics, one row segment per wave instruction: the
+    // workgroup's [Mloc][TG * TPW * 16] block goes through LDS so consecutive
+    // lanes add to consecutive columns of ONE row (a lane-per-(row, 4 cols)
+    // pattern spreads each instruction over Mloc rows; measured ~1.4x the
+    // slab-store cost at M = 8 on MI355X).  The staging reuses `red`.
+    constexpr int NTL = TG * TPW;
+    constexpr int NC = NTL * 16;                       // columns per workgroup (<= 128)
+    float* tbuf = (float*)red;                         // Mloc * NC floats <= 8 KiB
+    __syncthreads();                                   // KW partners done reading red
+    if (kp == 0 && tile0 < NT && r16 < Mloc) {
+#pragma unroll
+      for (int t = 0; t < TPW; t++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) tbuf[r16 * NC + (tg * TPW + t) * 16 + 4 * g + i] = acc[t][i];
+    }
+    __syncthreads();
+    const int nb = blockIdx.x * NC;
+    float* ws = (float*)a.out;
+    for (int v = threadIdx.x; v < Mloc * NC; v += NW * 64) {
+      const int m = v / NC, n = nb + v % NC;
+      if (n < a.N) __hip_atomic_fetch_add(ws + (size_t)m * a.N + n, tbuf[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
   }
   if (tile0 >= NT) return;
 

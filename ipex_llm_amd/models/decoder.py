@@ -133,17 +133,22 @@ def _ksplit(n: int, k: int) -> int:
     return ks
 
 
-# rows handled by the atomic split-K GEMV (ops.gemv_accum).  Measured on
-# MI355X (Llama-3-8B decode): at batch 1 one atomic slab beats ks f32 slabs
-# (consumers read 1 slab), at batch 8 the atomic traffic (M x N x ks adds at
-# ~1.3 TB/s chip-wide) costs more than the slab reduction saves
-ACC_MAX_M = 2
+# rows handled by the atomic split-K GEMV (ops.gemv_accum): its consumers
+# read ONE f32 slab instead of ks.  With the block-transposed atomic epilogue
+# (one row segment per wave instruction) the atomic GEMV costs about what the
+# slab-store one does up to 8 rows (MI355X, Llama-3-8B decode: batch 4
+# 2.191 -> 2.128 ms/step, batch 8 2.392 -> 2.382)
+ACC_MAX_M = int(__import__("os").environ.get("ILLM_ACC_MAX_M", "8"))
+# residual-add + RMSNorm folded into the consuming GEMV's prologue: every
+# workgroup re-derives the full-row norm, fine for 1-2 rows, far too much
+# redundant slab traffic at 4-8 (batch 8: 2.38 -> 3.08 ms/step)
+NORM_IN_MAX_M = int(__import__("os").environ.get("ILLM_NORM_IN_MAX_M", "2"))
 # decode batches up to this size take the fused-RoPE attention (qkv accumulated
 # atomically into one slab read by the attention, re-zeroed by its combine).
-# Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token;
-# at batch 8 the atomic qkv slab costs more than the rope launch it saves
-# (2.553 -> 2.640 ms/step), so batch > 2 keeps the split-K slabs + rope_kv
-ROPE_IN_MAX_M = 2
+# Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token,
+# batch 4 2.128 -> 2.109 ms/step; at batch 8 every split wave re-rotating q
+# costs more than the rope launch it saves (2.382 -> 2.527)
+ROPE_IN_MAX_M = int(__import__("os").environ.get("ILLM_ROPE_IN_MAX_M", "4"))
 
 
 class NativeAttention(nn.Module):
@@ -355,7 +360,7 @@ class NativeCausalLM(nn.Module):
     _norm_in_env = __import__("os").environ.get("ILLM_NORM_IN", "1") != "0"
 
     def _norm_in_ok(self, ref: torch.Tensor, T: int) -> bool:
-        if not (self._norm_in_env and T <= ACC_MAX_M and ref.is_cuda and self.tp_group is None
+        if not (self._norm_in_env and T <= min(ACC_MAX_M, NORM_IN_MAX_M) and ref.is_cuda and self.tp_group is None
                 and not self.spec.sandwich_norm and not self._attn_fuse and not self._glu_in_enabled
                 and self.spec.hidden_size % 8 == 0 and ops.native_gpu(ref)):
             return False

@@ -15,7 +15,8 @@ import threading
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         os.environ.get("IPEX_LLM_AMD_LIB", "_C.so"))
 _lock = threading.Lock()
 _loaded = False
 _load_error: Exception | None = None

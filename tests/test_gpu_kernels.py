@@ -61,13 +61,15 @@ def test_gemv_formats(cuda, name, dtype, M, ver, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["sym_int4", "asym_int4", "nf4", "fp8_e4m3", "sym_int8"])
-@pytest.mark.parametrize("M", [1, 5, 16])
-def test_gemv_accum_and_zeroing_consumers(cuda, name, M):
-    """split-K f32-atomic GEMV (v5 EPI_ATOMIC) vs the fp32 reference; the
-    norm consumer must leave the accumulator zeroed."""
+@pytest.mark.parametrize("M", [1, 5, 8, 16])
+@pytest.mark.parametrize("n", [512, 528])
+def test_gemv_accum_and_zeroing_consumers(cuda, name, M, n):
+    """split-K f32-atomic GEMV (v5 EPI_ATOMIC, block-transposed epilogue) vs
+    the fp32 reference (n = 528: a partial last tile group); the norm consumer
+    must leave the accumulator zeroed."""
     f = get_format(name).fmt
     torch.manual_seed(1)
-    n, k = 512, 1024
+    k = 1024
     w = torch.randn(n, k, device=cuda) * 0.05
     blob = ops.quantize(w, f)
     x = torch.randn(M, k, device=cuda).bfloat16()
@@ -86,7 +88,7 @@ def test_gemv_accum_and_zeroing_consumers(cuda, name, M):
 
 
 @pytest.mark.parametrize("name", ["sym_int4", "asym_int4", "nf4", "sym_int8"])
-@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("M", [1, 2, 8])
 def test_gemv_norm_in(cuda, name, M):
     """residual-add + RMSNorm folded into the GEMV prologue (decode norm-in
     path) vs add_rms_norm followed by the plain GEMV / GLU GEMV; the residual

@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--qtype", default="sym_int4")
     ap.add_argument("--only", default="")
     ap.add_argument("--ks", default="0,1,2,4,8")
+    ap.add_argument("--hot", action="store_true", help="one weight copy (MALL-resident re-reads)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     ops.require()
@@ -59,7 +60,7 @@ def main():
     # several copies so consecutive calls do not hit in the 256 MB MALL
     for M in [int(x) for x in args.m.split(",")]:
         for name, n, k in shapes:
-            copies = max(1, int(math.ceil(600e6 / (n * k * 0.5))))
+            copies = 1 if args.hot else max(1, int(math.ceil(600e6 / (n * k * 0.5))))
             blobs = [ops.quantize(torch.randn(n, k, device=dev, dtype=torch.bfloat16) * 0.02, f) for _ in range(copies)]
             x = torch.randn(M, k, device=dev, dtype=torch.bfloat16)
             nbytes = blobs[0].numel()
@@ -79,7 +80,13 @@ def main():
                 i[0] = (i[0] + 1) % copies
                 return ops.gemv_glu(x, blobs[i[0]], f, n, k, 0)
 
-            cands = {"store_auto": run_store}
+            acc = torch.zeros(M, n, device=dev, dtype=torch.float32)
+
+            def run_accum():
+                i[0] = (i[0] + 1) % copies
+                return ops.gemv_accum(x, blobs[i[0]], f, n, k, acc)
+
+            cands = {"store_auto": run_store, "accum": run_accum}
             for ks in ((0,) if args.only == "gemv" else [int(v) for v in args.ks.split(",")]):
                 cands[f"partial_ks{ks}"] = run_part(ks)
             if name == "gate_up":
