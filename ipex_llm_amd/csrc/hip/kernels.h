@@ -125,6 +125,22 @@ struct AttnDecodeArgs {
 };
 void launch_attn_decode(bool bf16, const AttnDecodeArgs& a, hipStream_t st);
 
+// ---- prefill / long-query attention over the paged cache (attn_prefill.hip)
+struct AttnPrefillArgs {
+  const uint16_t* q;            // [B * Tq, Hq, D] (sequence-major tokens)
+  const uint8_t* k_cache;       // [nblocks, Hkv, bs, D] (bf16/f16 or fp8 bytes)
+  const uint8_t* v_cache;
+  const int32_t* block_tables;  // [B, max_blocks]
+  const int32_t* seq_lens;      // [B] keys incl. the Tq new ones (query t sits at L - Tq + t)
+  uint16_t* out;                // [B * Tq, Hq, D]
+  int B, Tq, Hq, Hkv, D, bs, max_blocks;
+  float scale, softcap;
+  int sliding_window;
+  int kv_fp8;                   // 0 = 16-bit cache, 1 = e5m2, 2 = e4m3
+  float k_scale, v_scale;
+};
+void launch_attn_prefill(bool bf16, const AttnPrefillArgs& a, hipStream_t st);
+
 // ---- elementwise & misc (misc.hip) ------------------------------------------
 void launch_rwkv4_wkv(const float* decay, const float* first, const float* k, const float* v, float* out,
                       float* num, float* den, float* mx, int B, int T, int C, hipStream_t st);

@@ -719,6 +719,50 @@ Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache
                                       kv_fp8, k_scale, v_scale, alibi, false));
 }
 
+// prefill / long-query attention straight over the paged cache (attn_prefill.hip):
+// q [B * Tq, Hq, D] -> out [B * Tq, Hq, D]; query t of sequence b sits at
+// position seq_lens[b] - Tq + t (causal against everything before it)
+Tensor attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                    const Tensor& seq_lens, int64_t Tq, double scale, double softcap, int64_t window,
+                    int64_t kv_fp8, double k_scale, double v_scale) {
+  c10::DeviceGuard g(q.device());
+  TORCH_CHECK(q.dim() == 3 && q.is_contiguous(), "attn_prefill: q must be contiguous [B*Tq, Hq, D]");
+  const bool bf16 = is_bf16(q);
+  const int64_t Hq = q.size(1), D = q.size(2), Hkv = k_cache.size(1), bs = k_cache.size(2);
+  const int64_t B = block_tables.size(0);
+  TORCH_CHECK(Tq >= 1 && q.size(0) == B * Tq, "attn_prefill: q rows != B * Tq");
+  TORCH_CHECK(D == 64 || D == 128, "attn_prefill: head_dim 64 or 128");
+  TORCH_CHECK(k_cache.size(3) == D && v_cache.sizes() == k_cache.sizes(), "attn_prefill: cache shape");
+  TORCH_CHECK(Hq % Hkv == 0 && bs % 64 == 0, "attn_prefill: GQA ratio / block size (multiple of 64)");
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt &&
+                  seq_lens.numel() == B && block_tables.is_contiguous() && seq_lens.is_cuda(),
+              "attn_prefill: int32 device tables");
+  TORCH_CHECK(kv_fp8 != 0 || k_cache.scalar_type() == q.scalar_type(), "attn_prefill: KV dtype != q dtype");
+  Tensor out = at::empty_like(q);
+  illm::AttnPrefillArgs a{};
+  a.q = p16(q);
+  a.k_cache = (const uint8_t*)k_cache.data_ptr();
+  a.v_cache = (const uint8_t*)v_cache.data_ptr();
+  a.block_tables = block_tables.data_ptr<int32_t>();
+  a.seq_lens = seq_lens.data_ptr<int32_t>();
+  a.out = m16(out);
+  a.B = (int)B;
+  a.Tq = (int)Tq;
+  a.Hq = (int)Hq;
+  a.Hkv = (int)Hkv;
+  a.D = (int)D;
+  a.bs = (int)bs;
+  a.max_blocks = (int)block_tables.size(1);
+  a.scale = (float)scale;
+  a.softcap = (float)softcap;
+  a.sliding_window = (int)window;
+  a.kv_fp8 = (int)kv_fp8;
+  a.k_scale = (float)k_scale;
+  a.v_scale = (float)v_scale;
+  if (B > 0) illm::launch_attn_prefill(bf16, a, cur_stream());
+  return out;
+}
+
 // split kernel only: the (o, m, l) partials [B, Hq, Tq, nsplit, D] / [.., 2] are merged by the
 // o_proj GEMV's prologue (gemv_attn), which saves the combine launch
 std::tuple<Tensor, Tensor> attn_decode_split(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
@@ -975,6 +1019,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("attn_decode_rope", &attn_decode_rope);
   m.impl("gemm", &gemm);
   m.impl("attn_decode_split", &attn_decode_split);
+  m.impl("attn_prefill", &attn_prefill);
   m.impl("gemv_attn", &gemv_attn);
   m.impl("add_rms_norm", &add_rms_norm);
   m.impl("layer_norm", &layer_norm);

@@ -252,7 +252,13 @@ class NativeCausalLM(nn.Module):
                                 meta.seq_lens, meta.nsplit, s.scale, softcap, window, cache.kv_fp8,
                                 cache.k_scale, cache.v_scale, None, meta.seq_lens_host)
             return o.view(T, s.num_heads * s.head_dim)
-        # prefill / long query chunk: gather the sequence's keys and use SDPA
+        if q.is_cuda and s.head_dim in (64, 128) and cache.bs % 64 == 0 and self._prefill_attn_native \
+                and ops.native_gpu(q):
+            # prefill / long query chunk: flash-attention HIP kernel over the paged cache
+            o = ops.attn_prefill(q.view(T, s.num_heads, s.head_dim), kc, vc, meta.block_tables, meta.seq_lens,
+                                 meta.Tq, s.scale, softcap, window, cache.kv_fp8, cache.k_scale, cache.v_scale)
+            return o.view(T, s.num_heads * s.head_dim)
+        # other head dims: gather the sequence's keys and use SDPA
         lens = meta.seq_lens_host if meta.seq_lens_host is not None else meta.seq_lens.tolist()
         qv = q.view(meta.B, meta.Tq, s.num_heads, s.head_dim)
         outs = []
@@ -291,6 +297,9 @@ class NativeCausalLM(nn.Module):
             buf = torch.zeros(t, n, dtype=torch.float32, device=device)
             self._acc_bufs[key] = buf
         return buf
+
+    # ILLM_PREFILL_ATTN=sdpa: torch SDPA over gathered keys instead of the HIP kernel (A/B)
+    _prefill_attn_native = __import__("os").environ.get("ILLM_PREFILL_ATTN", "hip") != "sdpa"
 
     # opt-in: measured on MI355X (Llama-3-8B, L=1024) the prologue merge is
     # replicated by every o_proj N-tile group (64x re-reads of the partials:

@@ -117,6 +117,11 @@ def _(part, blob, fmt, n, k, act, ksplit, dtype):
     return part.new_empty((max(ksplit, 1), part.shape[1], n), dtype=torch.float32)
 
 
+@register_fake("ipex_llm_amd::attn_prefill")
+def _(q, k_cache, v_cache, block_tables, seq_lens, Tq, scale, softcap, window, kv_fp8, k_scale, v_scale):
+    return torch.empty_like(q)
+
+
 @register_fake("ipex_llm_amd::attn_decode_split")
 def _(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, kv_fp8, k_scale, v_scale, alibi):
     B, Tq, Hq, D = q.shape

@@ -18,7 +18,7 @@ __all__ = [
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
-    "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope",
+    "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope", "attn_prefill",
 ]
 
 
@@ -326,6 +326,29 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, soft
         vv = gather_kv(v_cache, block_tables, b, L, kv_fp8, v_scale, q.dtype)
         outs.append(R.attention(q[b:b + 1], kk[None], vv[None], True, scale, softcap, window, None, alibi))
     return torch.cat(outs, 0)
+
+
+def attn_prefill(q, k_cache, v_cache, block_tables, seq_lens, Tq: int, scale: float, softcap: float = 0.0,
+                 window: int = 0, kv_fp8: int = 0, k_scale: float = 1.0, v_scale: float = 1.0,
+                 seq_lens_host=None):
+    """Causal attention of q [B*Tq, Hq, D] (query t of sequence b at position
+    seq_lens[b] - Tq + t) against the paged cache -> [B*Tq, Hq, D].  GPU:
+    the flash-attention HIP kernel reading K/V straight from the cache
+    blocks (D in {64, 128}); otherwise the fp32 reference per sequence."""
+    D = q.shape[-1]
+    if _native(q) and D in (64, 128) and k_cache.shape[2] % 64 == 0:
+        return _ops().attn_prefill(q.contiguous(), k_cache, v_cache, block_tables, seq_lens, Tq, scale, softcap,
+                                   window, kv_fp8, k_scale, v_scale)
+    B = block_tables.shape[0]
+    lens = seq_lens_host if seq_lens_host is not None else seq_lens.tolist()
+    qv = q.view(B, Tq, q.shape[1], D)
+    outs = []
+    for b in range(B):
+        L = int(lens[b])
+        kk = gather_kv(k_cache, block_tables, b, L, kv_fp8, k_scale, q.dtype)
+        vv = gather_kv(v_cache, block_tables, b, L, kv_fp8, v_scale, q.dtype)
+        outs.append(R.attention(qv[b:b + 1], kk[None], vv[None], True, scale, softcap, window))
+    return torch.cat(outs, 0).reshape(B * Tq, q.shape[1], D).to(q.dtype)
 
 
 def attn_decode_rope(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,

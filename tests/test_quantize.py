@@ -153,3 +153,24 @@ def test_hf_eager_attention_uses_illm_softmax(mt, tmp_path, monkeypatch):
         got = m(ids).logits.float()
     assert calls, "illm_eager attention not used"
     assert ((got - want).norm() / want.norm()).item() < 2e-2
+
+
+def test_attn_prefill_cpu_fallback_matches_reference():
+    """ops.attn_prefill on CPU tensors = per-sequence fp32 reference over the paged cache"""
+    import torch
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.ops import reference as R
+    torch.manual_seed(0)
+    B, Tq, Hq, Hkv, D, bs = 2, 5, 4, 2, 64, 64
+    kc = torch.randn(4, Hkv, bs, D)
+    vc = torch.randn(4, Hkv, bs, D)
+    bt = torch.tensor([[2, 0], [1, 3]], dtype=torch.int32)
+    L = [70, 9]
+    seq = torch.tensor(L, dtype=torch.int32)
+    q = torch.randn(B * Tq, Hq, D)
+    got = ops.attn_prefill(q, kc, vc, bt, seq, Tq, 0.125)
+    for b in range(B):
+        kk = ops.api.gather_kv(kc, bt, b, L[b], 0, 1.0, torch.float32)
+        vv = ops.api.gather_kv(vc, bt, b, L[b], 0, 1.0, torch.float32)
+        ref = R.attention(q[b * Tq:(b + 1) * Tq][None], kk[None], vv[None], True, 0.125)[0]
+        assert torch.allclose(got[b * Tq:(b + 1) * Tq], ref, atol=1e-5)

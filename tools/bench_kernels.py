@@ -100,6 +100,9 @@ def main():
             torch.cuda.empty_cache()
     if args.only == "gemv":
         return
+    if args.only == "prefill":
+        prefill_attn(dev)
+        return
     # per-kernel floor: back-to-back trivial launches inside one graph
     t1 = torch.zeros(1, device=dev)
     us = timeit(lambda: t1.add_(1.0), iters=200)
@@ -139,6 +142,30 @@ def main():
         us = timeit(lambda: ops.rope_kv(qkv, qo, kc, vc, slots, pos, tab, 32, 8, 128))
         res.append({"op": "rope_kv", "M": M, "us": round(us, 2)})
         print(json.dumps(res[-1]), flush=True)
+
+
+def prefill_attn(dev):
+    """flash-attention prefill: HIP kernel over the paged cache vs torch SDPA
+    (contiguous K/V, GQA) at Llama-3-8B head geometry."""
+    import torch.nn.functional as F
+    Hq, Hkv, D, bs = 32, 8, 128, 64
+    for B, T in ((1, 1024), (1, 4096), (8, 1024)):
+        nblk = B * (T // bs)
+        kc = torch.randn(nblk, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nblk, device=dev, dtype=torch.int32).view(B, -1)
+        seq = torch.full((B,), T, device=dev, dtype=torch.int32)
+        q = torch.randn(B * T, Hq, D, device=dev, dtype=torch.bfloat16)
+        us = timeit(lambda: ops.attn_prefill(q, kc, vc, bt, seq, T, D ** -0.5), iters=20)
+        flop = 4 * B * Hq * T * T * D / 2
+        print(json.dumps({"op": "attn_prefill_hip", "B": B, "T": T, "us": round(us, 1),
+                          "TFLOPs": round(flop / us / 1e6, 1)}), flush=True)
+        k4 = kc.view(B, -1, Hkv, bs, D).permute(0, 2, 1, 3, 4).reshape(B, Hkv, T, D).contiguous()
+        v4 = vc.view(B, -1, Hkv, bs, D).permute(0, 2, 1, 3, 4).reshape(B, Hkv, T, D).contiguous()
+        q4 = q.view(B, T, Hq, D).transpose(1, 2).contiguous()
+        us = timeit(lambda: F.scaled_dot_product_attention(q4, k4, v4, is_causal=True, enable_gqa=True), iters=20)
+        print(json.dumps({"op": "attn_prefill_sdpa", "B": B, "T": T, "us": round(us, 1),
+                          "TFLOPs": round(flop / us / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
