@@ -19,6 +19,7 @@
 //   * XCD-aware block order: the 8 m-blocks of one n-block run on one XCD
 //     (ids b, b + 8, ...), so a weight chunk comes from HBM once per XCD
 //     and is re-read by the other m-blocks from that XCD's L2.
+#include <cstdlib>
 #include <type_traits>
 
 #include "../common/quant_block.h"
@@ -100,13 +101,17 @@ __device__ __forceinline__ uint4 gemm_a8(uint32_t lo, uint32_t hi, gh2 d2, gh2 m
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-constexpr int GBM = 128;          // tokens per block
-constexpr int GBN = 128;          // output features per block (8 tiles)
 constexpr int GLDX = 128 + 8;     // LDS row stride of the x chunk (halves)
 
-template <int DK, typename T>
+// WN weight tiles (16 rows each) x WM token tiles (16 rows each) per wave; the
+// 4 waves of a block sit side by side along n: block = (4 WN * 16) n x (WM * 16) m.
+//   <2, 8>: 128 n x 128 m, every x fragment read from LDS feeds 2 MFMAs;
+//   <4, 4>: 256 n x 64 m, half the LDS x traffic per MFMA (4 MFMAs per fragment)
+//           and half the x re-reads from L2, at 4 decoded weight tiles per wave.
+template <int DK, typename T, int WN, int WM, int PFW>
 __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   constexpr int BITS = dk_bits(DK);
+  constexpr int GBM = WM * 16, GBN = 4 * WN * 16;
   __shared__ __attribute__((aligned(16))) uint16_t xs[2][GBM * GLDX];
   __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -120,11 +125,11 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   if (nb >= NB) return;
   const int m0 = mb * GBM;
   const int NT = (a.N + 15) / 16;
-  const int tile0 = nb * 8 + wave * 2;
+  const int tile0 = nb * (4 * WN) + wave * WN;
   const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
-  const uint8_t* tb[2];
+  const uint8_t* tb[WN];
 #pragma unroll
-  for (int t = 0; t < 2; t++) tb[t] = a.w + (size_t)min(tile0 + t, NT - 1) * TB;
+  for (int t = 0; t < WN; t++) tb[t] = a.w + (size_t)min(tile0 + t, NT - 1) * TB;
   const size_t soff = (size_t)a.KC * dk_code_chunk(DK) + (size_t)r16 * 4;   // + c * 64: row r16 of chunk c
   const size_t moff = soff + (size_t)16 * a.KC * 4;
 
@@ -133,11 +138,11 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   }
 
   // ---- x staging: thread -> rows (tid / 16) + 16 j, 8 columns at (tid % 16) * 8
-  uint4 xr[8];
+  uint4 xr[WM];
   auto stage_load = [&](int c) {
     const int kk = c * 128 + (tid & 15) * 8;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < WM; j++) {
       const int m = m0 + (tid >> 4) + 16 * j;
       const bool ok = m < a.M && kk < a.K;
       const uint4 v = *(const uint4*)(a.x + (size_t)(ok ? m : 0) * a.ldx + (ok ? kk : 0));
@@ -146,7 +151,7 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   };
   auto stage_store = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < WM; j++) {
       uint4 v = xr[j];
       if constexpr (std::is_same<T, BF16>::value) {
         uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -164,12 +169,12 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
 
   // ---- weight chunk records (A fragments of 4 k-steps) + row-r16 scales
   struct WChunk {
-    uint4 q[2][BITS / 4];
-    uint32_t sc[2], mn[2];
+    uint4 q[WN][BITS / 4];
+    uint32_t sc[WN], mn[WN];
   };
   auto load_w = [&](WChunk& wc, int c) {
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
+    for (int t = 0; t < WN; t++) {
       const uint8_t* rec = tb[t] + (size_t)c * dk_code_chunk(DK);
       wc.q[t][0] = *(const uint4*)(rec + lane * 16);
       if constexpr (BITS == 8) wc.q[t][1] = *(const uint4*)(rec + 1024 + lane * 16);
@@ -179,16 +184,15 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
     }
   };
 
-  f32x4 acc[2][8];
+  f32x4 acc[WN][WM];
 #pragma unroll
-  for (int t = 0; t < 2; t++)
+  for (int t = 0; t < WN; t++)
 #pragma unroll
-    for (int mt = 0; mt < 8; mt++) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < WM; mt++) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // weight ring: PFW chunks in flight (one chunk of MFMA work, ~1k cycles,
   // does not cover an HBM round trip under load); loads are unconditional
   // (clamped) so hipcc keeps counted vmcnt waits
-  constexpr int PFW = 4;
   const int KC = a.KC;
   auto load_wc = [&](WChunk& wc, int c) { load_w(wc, min(c, KC - 1)); };
   WChunk ring[PFW];
@@ -206,9 +210,9 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; s++) {
       const int blk = s >> 1;
-      uint4 A[2];
+      uint4 A[WN];
 #pragma unroll
-      for (int t = 0; t < 2; t++) {
+      for (int t = 0; t < WN; t++) {
         const gh2 d2 = pick(cur.sc[t], blk);
         const gh2 m2 = dk_has_min(DK) ? pick(cur.mn[t], blk) : gh2{(_Float16)0.f, (_Float16)0.f};
         if constexpr (BITS == 4) {
@@ -220,14 +224,13 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
           A[t] = (s & 1) == 0 ? gemm_a8<DK>(qq.x, qq.y, d2, m2) : gemm_a8<DK>(qq.z, qq.w, d2, m2);
         }
       }
-      uint4 B[8];
+      uint4 B[WM];
 #pragma unroll
-      for (int mt = 0; mt < 8; mt++) B[mt] = *(const uint4*)(xb + mt * 16 * GLDX + 32 * s);
+      for (int mt = 0; mt < WM; mt++) B[mt] = *(const uint4*)(xb + mt * 16 * GLDX + 32 * s);
 #pragma unroll
-      for (int mt = 0; mt < 8; mt++) {
-        acc[0][mt] = mfma16<F16>(A[0], B[mt], acc[0][mt]);
-        acc[1][mt] = mfma16<F16>(A[1], B[mt], acc[1][mt]);
-      }
+      for (int mt = 0; mt < WM; mt++)
+#pragma unroll
+        for (int t = 0; t < WN; t++) acc[t][mt] = mfma16<F16>(A[t], B[mt], acc[t][mt]);
     }
   };
   for (int c0 = 0; c0 < KC; c0 += PFW) {
@@ -247,30 +250,33 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
 
   // ---- epilogue: lane holds out[m0 + 16 mt + r16][16 tile + 4 g + i]
   if (a.glu) {
-    // the wave's two tiles are one gate/up pair (16-row interleave, tile0 even):
+    // the wave's tiles are gate/up pairs (16-row interleave, tile0 even):
     // act(gate) * up in f32, one rounding (as the decode GLU GEMV epilogue)
-    if (tile0 + 1 >= NT) return;
-    const int n0 = (tile0 / 2) * 16 + 4 * g;
     const int I = a.N / 2;
-    if (n0 >= I) return;
 #pragma unroll
-    for (int mt = 0; mt < 8; mt++) {
-      const int m = m0 + mt * 16 + r16;
-      if (m >= a.M) continue;
-      float o[4];
+    for (int pr = 0; pr < WN / 2; pr++) {
+      if (tile0 + 2 * pr + 1 >= NT) continue;
+      const int n0 = (tile0 / 2 + pr) * 16 + 4 * g;
+      if (n0 >= I) continue;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const float gv = acc[0][mt][i], uv = acc[1][mt][i];
-        o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
+      for (int mt = 0; mt < WM; mt++) {
+        const int m = m0 + mt * 16 + r16;
+        if (m >= a.M) continue;
+        float o[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const float gv = acc[2 * pr][mt][i], uv = acc[2 * pr + 1][mt][i];
+          o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
+        }
+        uint16_t* y = a.out + (size_t)m * a.ldo + n0;
+        if (n0 + 3 < I && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
+        else for (int i = 0; i < 4 && n0 + i < I; i++) y[i] = from_f32<T>(o[i]);
       }
-      uint16_t* y = a.out + (size_t)m * a.ldo + n0;
-      if (n0 + 3 < I && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
-      else for (int i = 0; i < 4 && n0 + i < I; i++) y[i] = from_f32<T>(o[i]);
     }
     return;
   }
 #pragma unroll
-  for (int t = 0; t < 2; t++) {
+  for (int t = 0; t < WN; t++) {
     const int tile = tile0 + t;
     if (tile >= NT) continue;
     const int n0 = tile * 16 + 4 * g;
@@ -280,7 +286,7 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; i++) bv[i] = n0 + i < a.N ? to_f32<T>(a.bias[n0 + i]) : 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 8; mt++) {
+    for (int mt = 0; mt < WM; mt++) {
       const int m = m0 + mt * 16 + r16;
       if (m >= a.M) continue;
       const float o[4] = {acc[t][mt][0] + bv[0], acc[t][mt][1] + bv[1], acc[t][mt][2] + bv[2],
@@ -292,13 +298,25 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   }
 }
 
-template <int DK>
-static void launch_gemm_dk(bool bf16, const GemmArgs& a, hipStream_t st) {
+template <int DK, int WN, int WM, int PFW>
+static void launch_gemm_v(bool bf16, const GemmArgs& a, hipStream_t st) {
+  constexpr int GBM = WM * 16, GBN = 4 * WN * 16;
   const int NB = (a.N + GBN - 1) / GBN, MB = (a.M + GBM - 1) / GBM;
   const int NBp = (NB + 7) / 8 * 8;
   dim3 grid((unsigned)(NBp * MB));
-  if (bf16) hipLaunchKernelGGL((lowbit_gemm_kernel<DK, BF16>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((lowbit_gemm_kernel<DK, F16>), grid, dim3(256), 0, st, a);
+  if (bf16) hipLaunchKernelGGL((lowbit_gemm_kernel<DK, BF16, WN, WM, PFW>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((lowbit_gemm_kernel<DK, F16, WN, WM, PFW>), grid, dim3(256), 0, st, a);
+}
+
+template <int DK>
+static void launch_gemm_dk(bool bf16, const GemmArgs& a, hipStream_t st) {
+  // default 128 n x 128 m blocks (2 tiles x 8 m-tiles per wave).  ILLM_GEMM_TILE=2 selects
+  // 256 n x 64 m: half the LDS x traffic per MFMA but 268 registers -> 1 wave per SIMD;
+  // measured on MI355X (Llama-3-8B shapes, sym_int4): M = 1024 qkv/o/down +1..14 %,
+  // gate_up -12 %; M = 8192 -15..18 %
+  static const int tile_env = getenv("ILLM_GEMM_TILE") ? atoi(getenv("ILLM_GEMM_TILE")) : 0;
+  if (tile_env == 2) launch_gemm_v<DK, 4, 4, 2>(bf16, a, st);
+  else launch_gemm_v<DK, 2, 8, 4>(bf16, a, st);
 }
 
 void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st) {

@@ -163,6 +163,17 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r16 = lane & 15;
 
+  // ---- zero a consumed atomic accumulator (its readers ran earlier in the
+  // stream), spread over every workgroup of the grid (up to ~1 MB at M = 8)
+  if (a.nzero) {
+    const int nthr = NW * 64;
+    const size_t nb = (size_t)gridDim.x * gridDim.y * gridDim.z;
+    const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const size_t nv = (size_t)a.nzero_n / 4;
+    for (size_t i = bid * nthr + threadIdx.x; i < nv; i += nb * nthr)
+      ((float4*)a.nzero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
   int Mloc = a.M;
   const uint8_t* wbase = a.w;
   const int32_t* prow = nullptr;
@@ -263,11 +274,6 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
     __syncthreads();
   }
 
-  // ---- zero a consumed atomic accumulator (its readers ran earlier in the stream)
-  if (a.nzero && blockIdx.x == 0 && blockIdx.y == 0) {
-    for (int i = threadIdx.x * 4; i < a.nzero_n; i += NW * 64 * 4)
-      *(float4*)(a.nzero + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
 
   // ---- residual-add + RMSNorm prologue (replaces the standalone norm launch):
   // h = rnd(rnd(acc) + res) exactly as add_rms_norm rounds it; every workgroup

@@ -405,10 +405,12 @@ void gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
 }
 
 // down-projection GEMV whose input is act(gate) * up computed on the fly from
-// the gate/up GEMV's split-K slabs (saves the GLU epilogue's unsplittable
-// launch and one [M, I] round trip); returns f32 partial slabs [ks, M, n].
+// the gate/up GEMV's split-K slabs or atomic accumulator (saves the GLU
+// epilogue's unsplittable launch and one [M, I] round trip); returns f32
+// partial slabs [ks, M, n], or accumulates atomically into ``acc`` [M, n].
 Tensor gemv_glu_in(const Tensor& part, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t act,
-                   int64_t ksplit, at::ScalarType dt) {
+                   int64_t ksplit, at::ScalarType dt, const c10::optional<Tensor>& acc,
+                   const c10::optional<Tensor>& zero) {
   TORCH_CHECK(part.is_cuda() && blob.is_cuda() && part.dim() == 3 && part.scalar_type() == at::kFloat &&
               part.is_contiguous(), "gemv_glu_in: part must be contiguous f32 [ns, M, 2k] on the GPU");
   TORCH_CHECK(part.size(2) == 2 * k && k % 16 == 0, "gemv_glu_in: part width must be 2 * k");
@@ -432,11 +434,21 @@ Tensor gemv_glu_in(const Tensor& part, const Tensor& blob, int64_t fmt, int64_t 
   a.act = (int)act;
   a.lut_fmt = (int)fmt;
   a.N = (int)n;
-  const Plan5 p = plan5(M, NT, KC, true, ksplit);
+  const bool atomic = acc.has_value() && acc->defined();
+  const Plan5 p = plan5(M, NT, KC, true, ksplit, atomic);
   ksplit = p.ks;
   a.cpk = (int)p.cpk;
   a.nw = p.nw;
+  set_zero(a, zero);
   TORCH_CHECK(p.shmem <= kMaxLds, "gemv_glu_in: K slice too large for LDS");
+  if (atomic) {
+    TORCH_CHECK(acc->scalar_type() == at::kFloat && acc->is_contiguous() && acc->numel() == M * n,
+                "gemv_glu_in: acc must be contiguous f32 [M, n]");
+    a.out = acc->data_ptr();
+    a.ldo = (int)n;
+    launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_ATOMIC, dim3(p.gx, (unsigned)ksplit), p.shmem, a);
+    return *acc;
+  }
   Tensor ws = at::empty({ksplit, M, n}, part.options());
   a.out = ws.data_ptr();
   a.ldo = (int)n;

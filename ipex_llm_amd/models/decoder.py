@@ -408,14 +408,22 @@ class NativeCausalLM(nn.Module):
             self.__dict__["_qkv_native_ok"] = ok
         return ok and ref.is_cuda and self.tp_group is None and ops.native_gpu(ref)
 
-    def _fused_mlp_ok(self, x, layer) -> bool:
+    def _fused_mlp_ok(self, x, layer, need_env: bool = True) -> bool:
         mlp = layer.mlp
         if not (x.is_cuda and isinstance(mlp, NativeMLP) and x.shape[0] <= 16 and self.tp_group is None):
             return False
         gu, dn = mlp.gate_up_proj, mlp.down_proj
         return (isinstance(gu, LowBitLinear) and isinstance(dn, LowBitLinear) and gu.bias is None and dn.bias is None
-                and dn.mp_group is None and layer.post_feedforward_layernorm is None
-                and dn.in_features % 16 == 0 and self._glu_in_enabled and ops.native_gpu(x))
+                and gu.mp_group is None and dn.mp_group is None and layer.post_feedforward_layernorm is None
+                and dn.in_features % 16 == 0 and (self._glu_in_enabled or not need_env) and ops.native_gpu(x))
+
+    def _mlp_acc_ok(self, x, layer) -> bool:
+        """decode MLP as gate/up atomic GEMV -> down GEMV taking act(gate) * up
+        from that accumulator in its input staging (atomic out): the GLU
+        epilogue's unsplittable launch and the [T, I] round trip go away"""
+        return (self._mlp_acc_env and x.shape[0] <= ACC_MAX_M and self._fused_mlp_ok(x, layer, need_env=False))
+
+    _mlp_acc_env = __import__("os").environ.get("ILLM_MLP_ACC", "0") == "1"
 
     # measured neutral at B=1 and ~1% slower at B=8 on MI355X (the down GEMV's
     # slab-reading prologue costs what the split gate/up GEMV saves): opt-in
@@ -473,6 +481,7 @@ class NativeCausalLM(nn.Module):
         # combine launch re-zeroes
         rope_in = T <= ROPE_IN_MAX_M and self._rope_in_ok(meta, cache) and self._qkv_native(residual)
         nxt_res = lambda r: res_pp[1] if r is res_pp[0] else res_pp[0]
+        zero_next = None                # consumed atomic slab the next accumulating GEMV zeroes
         for li, layer in enumerate(self.layers):
             attn = layer.self_attn
             qp = attn.qkv_proj
@@ -489,7 +498,9 @@ class NativeCausalLM(nn.Module):
                                          qp.weight, qp.fmt, qp.out_features, qp.in_features, False, acc_out=part)
                         residual, consumed, pend = r2, pend, None
                     else:
-                        ops.gemv_accum(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, part)
+                        ops.gemv_accum(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, part,
+                                       zero=zero_next)
+                        zero_next = None
                     qkv_acc = part
                     part = part.unsqueeze(0)
                 else:
@@ -548,6 +559,23 @@ class NativeCausalLM(nn.Module):
                 nxt = self.layers[li + 1].input_layernorm
             else:   # stage boundary: the next norm lives on the next stage
                 nxt = self.norm if self.last_stage else layer.input_layernorm
+            if self._mlp_acc_ok(x, layer):
+                # gate/up atomics into one f32 slab -> down GEMV applies act(g)*u while
+                # staging its input, atomics into the norm's slab; the gate/up slab is
+                # zeroed by the next layer's qkv GEMV (all its readers are done by then)
+                gu, dn = layer.mlp.gate_up_proj, layer.mlp.down_proj
+                gacc = self._acc(gu.out_features, x.shape[0], x.device, "GU")
+                if zero_next is gacc:          # no accumulating launch in between took the zeroing
+                    gacc.zero_()
+                    zero_next = None
+                ops.gemv_accum(x, gu.weight, gu.fmt, gu.out_features, gu.in_features, gacc, 0, zero=zero_next)
+                dacc = self._acc(dn.out_features, x.shape[0], x.device)
+                ops.gemv_glu_in(gacc.unsqueeze(0), dn.weight, dn.fmt, dn.out_features, dn.in_features, s.act, 0,
+                                x.dtype, acc=dacc)
+                x, _ = ops.add_rms_norm(None, residual, nxt, s.rms_eps, partials=dacc.unsqueeze(0),
+                                        unit_offset=s.norm_unit_offset, zero_partials=True)
+                zero_next = gacc
+                continue
             if self._fused_mlp_ok(x, layer):
                 # gate/up split-K slabs -> down GEMV applies act(g)*u while staging its input
                 gu, dn = layer.mlp.gate_up_proj, layer.mlp.down_proj
@@ -564,6 +592,8 @@ class NativeCausalLM(nn.Module):
                 if layer.post_feedforward_layernorm is not None:
                     y = ops.rms_norm(y, layer.post_feedforward_layernorm, s.rms_eps, s.norm_unit_offset)
                 x, _ = ops.add_rms_norm(y.contiguous(), residual, nxt, s.rms_eps, unit_offset=s.norm_unit_offset)
+        if zero_next is not None:
+            zero_next.zero_()
         if not self.last_stage:
             return residual
         if return_hidden:

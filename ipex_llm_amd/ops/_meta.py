@@ -113,7 +113,9 @@ def _(acc_in, residual, res_out, norm_w, eps, unit_offset, blob, fmt, n, k, epi,
 
 
 @register_fake("ipex_llm_amd::gemv_glu_in")
-def _(part, blob, fmt, n, k, act, ksplit, dtype):
+def _(part, blob, fmt, n, k, act, ksplit, dtype, acc=None, zero=None):
+    if acc is not None:
+        return acc
     return part.new_empty((max(ksplit, 1), part.shape[1], n), dtype=torch.float32)
 
 

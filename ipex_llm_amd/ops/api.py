@@ -138,10 +138,24 @@ def gemv_glu(x, blob, fmt, n, k, act: int = 0) -> torch.Tensor:
     return _ops().gemv(x, blob, fmt, n, k, None, 2, 1, act)
 
 
-def gemv_glu_in(part, blob, fmt, n, k, act: int = 0, ksplit: int = 0, dtype=torch.bfloat16) -> torch.Tensor:
+def gemv_glu_in(part, blob, fmt, n, k, act: int = 0, ksplit: int = 0, dtype=torch.bfloat16,
+                acc: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None) -> torch.Tensor:
     """down-projection over act(gate)*up taken straight from the gate/up
-    GEMV's split-K slabs ``part`` [ns, M, 2k]; returns f32 slabs [ks, M, n]."""
-    return _ops().gemv_glu_in(part, blob, fmt, n, k, act, ksplit, dtype)
+    GEMV's split-K slabs (or atomic accumulator) ``part`` [ns, M, 2k];
+    returns f32 slabs [ks, M, n], or ``acc`` [M, n] += the product (atomics).
+    ``zero`` (a buffer whose readers are done) is zeroed by the launch."""
+    if _native(part):
+        return _ops().gemv_glu_in(part, blob, fmt, n, k, act, ksplit, dtype, acc, zero)
+    from ..models.decoder import deinterleave_glu
+    g, u = deinterleave_glu(part.sum(0))
+    a = ((F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")) * u).to(dtype)
+    if zero is not None:
+        zero.zero_()
+    y = lowbit_matmul(a, blob, fmt, n, k).float()
+    if acc is not None:
+        acc += y.view_as(acc)
+        return acc
+    return y.unsqueeze(0)
 
 
 def reduce_partials(ws, bias=None, dtype=torch.bfloat16):

@@ -35,6 +35,36 @@ def test_gemv_glu_in_matches_glu_then_down(cuda, M, qtype):
     pg = ops.gemv_partials(x, gu, fmt, 2 * I, H, 0)
     out = ops.gemv_glu_in(pg, dn, fmt, H, I, 0, 0, torch.bfloat16).sum(0)
     assert ((out - ref).norm() / ref.norm()).item() < 1e-2
+    # atomic form: gate/up accumulated into one slab, down accumulated atomically,
+    # and an unrelated consumed buffer zeroed by the launch
+    gacc = torch.zeros(M, 2 * I, device=cuda)
+    ops.gemv_accum(x, gu, fmt, 2 * I, H, gacc)
+    dacc = torch.zeros(M, H, device=cuda)
+    junk = torch.ones(8 * 1024 + 4, device=cuda)
+    ops.gemv_glu_in(gacc.unsqueeze(0), dn, fmt, H, I, 0, 0, torch.bfloat16, acc=dacc, zero=junk)
+    assert ((dacc - ref).norm() / ref.norm()).item() < 1e-2
+    assert junk.abs().max().item() == 0.0
+
+
+def test_decode_mlp_acc_path_matches_glu_path(cuda):
+    """batch 3..8 decode: gate/up atomics + down-with-GLU-prologue == GLU GEMV + down"""
+    from transformers import LlamaConfig
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.models.decoder import NativeCausalLM
+    cfg = LlamaConfig(vocab_size=512, hidden_size=512, intermediate_size=1024, num_hidden_layers=3,
+                      num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=1024)
+    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=4)
+    prompts = [list(range(1 + i, 40 + 3 * i)) for i in range(6)]
+    outs = {}
+    try:
+        for flag in (False, True):
+            NativeCausalLM._mlp_acc_env = flag
+            outs[flag] = Engine(m).generate(prompts, max_new_tokens=10, use_graph=True)
+    finally:
+        NativeCausalLM._mlp_acc_env = True
+    a, b = sum(outs[False], []), sum(outs[True], [])
+    assert sum(x == y for x, y in zip(a, b)) >= 0.95 * len(a)
 
 
 def test_rwkv4_wkv_kernel(cuda):

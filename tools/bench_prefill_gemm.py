@@ -29,7 +29,7 @@ def main():
     dev = torch.device("cuda")
     for qt in (sys.argv[1] if len(sys.argv) > 1 else "sym_int4").split(","):
         f = get_format(qt).fmt
-        for M in (1024, 4096):
+        for M in [int(v) for v in os.environ.get("GEMM_M", "1024,4096").split(",")]:
             for name, n, k in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336)]:
                 w = torch.randn(n, k, device=dev, dtype=torch.bfloat16) * 0.02
                 blob = ops.quantize(w, f)
