@@ -15,4 +15,9 @@ void illm_repack_from_device(int fmt, const uint8_t* dev, int64_t n, int64_t k, 
 void illm_cpu_gemm(int fmt, const float* x, int64_t m, const uint8_t* codes,
                    const uint16_t* scales, const uint16_t* mins, int64_t n, int64_t k, float* y);
 void illm_f32_to_fp8(const float* src, int64_t n, int e5m2, uint8_t* dst);
+// gemm_q4.cpp: int8-activation integer-dot path for sym_int4 / asym_int4
+// (isa: 0 = auto, 1 = AVX2, 2 = AVX-512 VNNI)
+int illm_cpu_q4_supported(int fmt);
+void illm_cpu_gemm_q4(int fmt, const float* x, int64_t m, const uint8_t* codes, const uint16_t* scales,
+                      const uint16_t* mins, int64_t n, int64_t k, float* y, int isa);
 }

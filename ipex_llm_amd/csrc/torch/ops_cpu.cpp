@@ -82,9 +82,27 @@ Tensor linear_cpu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, i
   Tensor xf = x.reshape({-1, k}).to(at::kFloat).contiguous();
   Tensor b = blob.contiguous();
   Planes p = canon_planes(b, fmt, n, k);
-  Tensor y = at::empty({xf.size(0), n}, xf.options());
-  illm_cpu_gemm((int)fmt, xf.data_ptr<float>(), xf.size(0), p.codes, p.scales, p.mins, n, k,
-                y.data_ptr<float>());
+  const int64_t M = xf.size(0);
+  // rows above this take dequantize + BLAS (reference: BIGDL_LLM_LINEAR_THRESHOLD,
+  // low_bit_linear.py:64); below it the int8-activation integer-dot kernels
+  static const int64_t thr = [] {
+    const char* e = getenv("IPEX_LLM_LINEAR_THRESHOLD");
+    if (!e) e = getenv("BIGDL_LLM_LINEAR_THRESHOLD");
+    return e ? (int64_t)atoll(e) : (int64_t)128;
+  }();
+  static const int isa = getenv("ILLM_CPU_ISA") ? atoi(getenv("ILLM_CPU_ISA")) : 0;
+  if (M > thr) {
+    Tensor w = at::empty({n, k}, xf.options());
+    illm_dequantize((int)fmt, p.codes, p.scales, p.mins, n, k, w.data_ptr<float>());
+    auto shape = x.sizes().vec();
+    shape.back() = n;
+    return at::mm(xf, w.t()).view(shape);
+  }
+  Tensor y = at::empty({M, n}, xf.options());
+  if (illm_cpu_q4_supported((int)fmt) && isa >= 0 && k % 64 == 0)
+    illm_cpu_gemm_q4((int)fmt, xf.data_ptr<float>(), M, p.codes, p.scales, p.mins, n, k, y.data_ptr<float>(), isa);
+  else
+    illm_cpu_gemm((int)fmt, xf.data_ptr<float>(), M, p.codes, p.scales, p.mins, n, k, y.data_ptr<float>());
   auto shape = x.sizes().vec();
   shape.back() = n;
   return y.view(shape);

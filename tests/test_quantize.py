@@ -174,3 +174,32 @@ def test_attn_prefill_cpu_fallback_matches_reference():
         vv = ops.api.gather_kv(vc, bt, b, L[b], 0, 1.0, torch.float32)
         ref = R.attention(q[b * Tq:(b + 1) * Tq][None], kk[None], vv[None], True, 0.125)[0]
         assert torch.allclose(got[b * Tq:(b + 1) * Tq], ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("qtype", ["sym_int4", "asym_int4"])
+@pytest.mark.parametrize("M", [1, 3, 9, 200])
+@pytest.mark.parametrize("isa", ["0", "1"])
+def test_cpu_int4_dot_gemm_matches_dequant(qtype, M, isa, monkeypatch):
+    """CPU int8-activation integer-dot kernels (AVX-512 VNNI / AVX2) and the
+    dequant + BLAS path for M above the threshold vs x @ dequant(W)^T"""
+    import subprocess
+    import sys
+    code = f"""
+import torch
+from ipex_llm_amd import ops
+from ipex_llm_amd.quantize import get_format
+f = get_format({qtype!r}).fmt
+torch.manual_seed(0)
+n, k = 96, 320
+w = torch.randn(n, k) * 0.05
+blob = ops.quantize(w, f)
+x = torch.randn({M}, k)
+y = ops.lowbit_matmul(x, blob, f, n, k)
+ref = x @ ops.dequantize(blob, f, n, k).T
+rel = ((y - ref).norm() / ref.norm()).item()
+assert rel < 1.5e-2, rel
+print("ok", rel)
+"""
+    env = dict(__import__("os").environ, ILLM_CPU_ISA=isa)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
