@@ -59,7 +59,7 @@ class Request:
 class LLMEngine:
     def __init__(self, model: NativeCausalLM, max_batch: int = 64, block_size: int = 64,
                  num_blocks: Optional[int] = None, max_model_len: int = 8192, max_prefill_tokens: int = 8192,
-                 kv_fp8: int = 0, memory_fraction: float = 0.5, eos_token_id=None):
+                 kv_fp8: int = 0, memory_fraction: float = 0.5, eos_token_id=None, use_graph: bool = True):
         ops.require() if model.device.type == "cuda" else None
         self.model = model
         s = model.spec
@@ -72,7 +72,12 @@ class LLMEngine:
                 budget = per_tok * max_batch * max_model_len // 4
             num_blocks = max(max_batch, budget // (per_tok * block_size))
             num_blocks = min(num_blocks, max_batch * ((max_model_len + block_size - 1) // block_size))
-        self.cache = model.make_cache(max_model_len, max_batch, block_size, kv_fp8, num_blocks=num_blocks)
+        # one extra block past the scheduler's pool: the scratch target of the
+        # padding rows of a captured decode step
+        self.cache = model.make_cache(max_model_len, max_batch, block_size, kv_fp8, num_blocks=num_blocks + 1)
+        self._scratch = num_blocks
+        self.use_graph = use_graph and model.device.type == "cuda" and ops.native_gpu(self.cache.k[0])
+        self._graphs: Dict[tuple, dict] = {}
         model.ensure_rope_cache(max_model_len + 1)
         self.sched = torch.classes.ipex_llm_amd.Scheduler(num_blocks, block_size, max_batch, max_prefill_tokens)
         self.block_size, self.max_model_len = block_size, max_model_len
@@ -148,6 +153,61 @@ class LLMEngine:
             t[i, :len(x)] = torch.tensor(x, dtype=torch.int32)
         return t.to(self.model.device)
 
+    # ------------------------------------------------------------ graph decode
+    @staticmethod
+    def _bucket(x: int, lo: int = 1) -> int:
+        b = lo
+        while b < x:
+            b *= 2
+        return b
+
+    def _capture(self, Bb: int, Wb: int) -> dict:
+        """hipGraph of one decode forward for Bb sequences (padded) with block
+        tables of Wb blocks: slots / key counts are derived on the device from
+        the positions, so a replay needs only ids, positions and tables."""
+        m, bs, dev = self.model, self.block_size, self.model.device
+        g = {"ids": torch.zeros(Bb, dtype=torch.long, device=dev),
+             "pos": torch.zeros(Bb, dtype=torch.long, device=dev),
+             "bt": torch.full((Bb, Wb), self._scratch, dtype=torch.int32, device=dev)}
+
+        def body():
+            pos, bt = g["pos"], g["bt"]
+            blk = torch.gather(bt, 1, (pos // bs).unsqueeze(1)).squeeze(1).long()
+            slots = blk * bs + pos % bs
+            seq_lens = (pos + 1).to(torch.int32)
+            meta = AttnMeta(Bb, 1, bt, seq_lens, nsplit_for(Wb * bs))
+            return m.forward_tokens(g["ids"], pos, slots, meta, self.cache)
+
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):            # warm-up (writes only the scratch block)
+            body()
+        torch.cuda.current_stream().wait_stream(s)
+        g["graph"] = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g["graph"]):
+            g["logits"] = body()
+        self._graphs[(Bb, Wb)] = g
+        return g
+
+    def _decode_graph(self, rids: List[int], pos_l: List[int]) -> torch.Tensor:
+        B = len(rids)
+        rows = [list(self.sched.blocks(r)) for r in rids]
+        Bb = self._bucket(B)
+        Wb = self._bucket(max(len(x) for x in rows), 4)
+        g = self._graphs.get((Bb, Wb)) or self._capture(Bb, Wb)
+        bt = torch.full((Bb, Wb), self._scratch, dtype=torch.int32)
+        for i, x in enumerate(rows):
+            bt[i, :len(x)] = torch.tensor(x, dtype=torch.int32)
+        pos = torch.zeros(Bb, dtype=torch.long)
+        pos[:B] = torch.tensor(pos_l)
+        ids = torch.zeros(Bb, dtype=torch.long)
+        ids[:B] = torch.tensor([self.requests[r].tokens[-1] for r in rids])
+        g["bt"].copy_(bt, non_blocking=True)
+        g["pos"].copy_(pos, non_blocking=True)
+        g["ids"].copy_(ids, non_blocking=True)
+        g["graph"].replay()
+        return g["logits"][:B]
+
     @torch.no_grad()
     def step(self) -> int:
         """One scheduler step: prefill admitted requests, decode all running
@@ -184,15 +244,18 @@ class LLMEngine:
             if decode:
                 rs = [self.requests[rid] for rid in decode]
                 B = len(rs)
-                bt = self._block_table(decode)
                 pos_l = [int(self.sched.cached(rid)) for rid in decode]
-                pos = torch.tensor(pos_l, device=dev)
-                blk = torch.gather(bt, 1, (pos // bs).unsqueeze(1).to(torch.int64)).squeeze(1).long()
-                slots = blk * bs + pos % bs
-                seq_lens = (pos + 1).to(torch.int32)
-                meta = AttnMeta(B, 1, bt, seq_lens, nsplit_for(max(pos_l) + 1), [p + 1 for p in pos_l])
-                ids = torch.tensor([r.tokens[-1] for r in rs], device=dev)
-                lg = m.forward_tokens(ids, pos, slots, meta, self.cache)
+                if self.use_graph:
+                    lg = self._decode_graph(decode, pos_l)
+                else:
+                    bt = self._block_table(decode)
+                    pos = torch.tensor(pos_l, device=dev)
+                    blk = torch.gather(bt, 1, (pos // bs).unsqueeze(1).to(torch.int64)).squeeze(1).long()
+                    slots = blk * bs + pos % bs
+                    seq_lens = (pos + 1).to(torch.int32)
+                    meta = AttnMeta(B, 1, bt, seq_lens, nsplit_for(max(pos_l) + 1), [p + 1 for p in pos_l])
+                    ids = torch.tensor([r.tokens[-1] for r in rs], device=dev)
+                    lg = m.forward_tokens(ids, pos, slots, meta, self.cache)
                 greedy = all(not r.params.do_sample and r.params.repetition_penalty == 1.0 for r in rs)
                 nxt = torch.argmax(lg, -1).tolist() if greedy else None
                 for i, r in enumerate(rs):
