@@ -156,6 +156,9 @@ void launch_reduce_partials(bool bf16, const float* ws, int nsplit, const uint16
 void launch_moe_topk(const float* logits, int T, int E, int k, int renorm, int scoring,
                      float* topk_w, int32_t* topk_ids, hipStream_t st);
 
+void launch_moe_group_topk(const float* logits, const float* bias, int T, int E, int k, int n_group, int topk_group,
+                           int renorm, float scale, float* topk_w, int32_t* topk_ids, hipStream_t st);
+
 void launch_moe_align(const int32_t* ids, int P, int e0, int El, int32_t* off, int32_t* rows, hipStream_t st);
 void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float* w, const int32_t* ids, int k,
                         int e0, int El, uint16_t* out, int Tn, int H, hipStream_t st);

@@ -269,6 +269,93 @@ __global__ void __launch_bounds__(64) moe_topk_kernel(const float* logits, int T
   }
 }
 
+// ---- DeepSeek-V3 group-limited router (noaux_tc): sigmoid scores, + the
+// e_score_correction_bias for the choice, groups ranked by the sum of their
+// top-2 choice scores, top-k among the experts of the top `topk_group` groups,
+// weights = un-biased scores (renormalised) * routed_scaling_factor.
+// Reference: xe_addons.moe_group_topk (models/common.py:342-351,
+// deepseek.py:274-290).  One wave per token; E <= 512, n_group <= 64.
+__global__ void __launch_bounds__(64) moe_group_topk_kernel(const float* logits, const float* bias, int T, int E,
+                                                            int k, int n_group, int topk_group, int renorm,
+                                                            float scale, float* topk_w, int32_t* topk_ids) {
+  const int t = blockIdx.x, lane = threadIdx.x;
+  constexpr int PER = 8;
+  __shared__ float sfc[512];
+  __shared__ float gsc[64];
+  __shared__ int gsel[64];
+  float sc[PER], ch[PER];
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const int e = lane + 64 * j;
+    const float l = e < E ? logits[(size_t)t * E + e] : 0.f;
+    sc[j] = 1.f / (1.f + __expf(-l));
+    ch[j] = e < E ? sc[j] + (bias ? bias[e] : 0.f) : -INFINITY;
+    if (e < E) sfc[e] = ch[j];
+  }
+  __syncthreads();
+  const int gs = E / n_group;
+  if (lane < n_group) {
+    float b1 = -INFINITY, b2 = -INFINITY;
+    for (int i = 0; i < gs; i++) {
+      const float v = sfc[lane * gs + i];
+      if (v > b1) { b2 = b1; b1 = v; } else if (v > b2) { b2 = v; }
+    }
+    gsc[lane] = b1 + (gs > 1 ? b2 : 0.f);
+    gsel[lane] = 0;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    for (int i = 0; i < topk_group; i++) {
+      int bi = -1;
+      float best = -INFINITY;
+      for (int g = 0; g < n_group; g++)
+        if (!gsel[g] && (bi < 0 || gsc[g] > best)) { best = gsc[g]; bi = g; }
+      if (bi >= 0) gsel[bi] = 1;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    const int e = lane + 64 * j;
+    if (e < E && !gsel[e / gs]) ch[j] = -INFINITY;
+  }
+  float tot = 0.f;
+  for (int i = 0; i < k; i++) {
+    float best = -INFINITY, bw = 0.f;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      const int e = lane + 64 * j;
+      if (e < E && (ch[j] > best || (ch[j] == best && e < bi))) { best = ch[j]; bi = e; bw = sc[j]; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      const float ow = __shfl_xor(bw, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; bw = ow; }
+    }
+#pragma unroll
+    for (int j = 0; j < PER; j++)
+      if (lane + 64 * j == bi) ch[j] = -INFINITY;
+    if (lane == 0) {
+      topk_w[(size_t)t * k + i] = bw;
+      topk_ids[(size_t)t * k + i] = bi;
+    }
+    tot += bw;
+  }
+  if (lane == 0) {
+    const float f = renorm ? scale / (tot + 1e-20f) : scale;
+    for (int i = 0; i < k; i++) topk_w[(size_t)t * k + i] *= f;
+  }
+}
+
+void launch_moe_group_topk(const float* logits, const float* bias, int T, int E, int k, int n_group, int topk_group,
+                           int renorm, float scale, float* topk_w, int32_t* topk_ids, hipStream_t st) {
+  hipLaunchKernelGGL(moe_group_topk_kernel, dim3(T), dim3(64), 0, st, logits, bias, T, E, k, n_group, topk_group,
+                     renorm, scale, topk_w, topk_ids);
+}
+
 void launch_moe_topk(const float* logits, int T, int E, int k, int renorm, int scoring,
                      float* topk_w, int32_t* topk_ids, hipStream_t st) {
   hipLaunchKernelGGL(moe_topk_kernel, dim3(T), dim3(64), 0, st, logits, T, E, k, renorm, scoring,

@@ -137,6 +137,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("attn_softmax_(Tensor(a!) x) -> ()");
   m.def("reduce_partials(Tensor ws, Tensor? bias, ScalarType dtype) -> Tensor");
   m.def("moe_topk(Tensor logits, int k, bool renorm, int scoring) -> (Tensor, Tensor)");
+  m.def("moe_group_topk(Tensor logits, Tensor? bias, int k, int n_group, int topk_group, bool renorm, float scale) -> (Tensor, Tensor)");
   m.def("moe_align(Tensor ids, int e0, int num_local) -> (Tensor, Tensor)");
   m.def("gemv_glu_in(Tensor part, Tensor blob, int fmt, int n, int k, int act, int ksplit, ScalarType dtype, Tensor(a!)? acc=None, Tensor(b!)? zero=None) -> Tensor");
   m.def("decode_advance(Tensor? logits, Tensor(a!) ids, Tensor(b!) next_ids, Tensor(c!) pos, Tensor block_tables, int bs, Tensor(d!) slots, Tensor(e!) seq_lens, Tensor? pos_offset=None) -> ()");

@@ -873,6 +873,27 @@ Tensor reduce_partials(const Tensor& ws, const c10::optional<Tensor>& bias, at::
   return out;
 }
 
+std::tuple<Tensor, Tensor> moe_group_topk(const Tensor& logits, const c10::optional<Tensor>& bias, int64_t k,
+                                          int64_t n_group, int64_t topk_group, bool renorm, double scale) {
+  c10::DeviceGuard g(logits.device());
+  Tensor l = logits.to(at::kFloat).contiguous();
+  const int64_t E = l.size(-1), T = l.numel() / E;
+  TORCH_CHECK(E <= 512 && k <= E && n_group >= 1 && n_group <= 64 && E % n_group == 0 && topk_group <= n_group,
+              "moe_group_topk: E <= 512, n_group <= 64 dividing E");
+  Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b.numel() == E && b.is_cuda(), "moe_group_topk: bias [E] on the GPU");
+  }
+  Tensor w = at::empty({T, k}, l.options());
+  Tensor ids = at::empty({T, k}, l.options().dtype(at::kInt));
+  if (T > 0)
+    illm::launch_moe_group_topk(l.data_ptr<float>(), b.defined() ? b.data_ptr<float>() : nullptr, (int)T, (int)E,
+                                (int)k, (int)n_group, (int)topk_group, renorm ? 1 : 0, (float)scale,
+                                w.data_ptr<float>(), ids.data_ptr<int32_t>(), cur_stream());
+  return {w, ids};
+}
+
 std::tuple<Tensor, Tensor> moe_topk(const Tensor& logits, int64_t k, bool renorm, int64_t scoring) {
   c10::DeviceGuard g(logits.device());
   Tensor l = logits.to(at::kFloat).contiguous();
@@ -1032,6 +1053,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("attn_decode_split", &attn_decode_split);
   m.impl("attn_prefill", &attn_prefill);
+  m.impl("moe_group_topk", &moe_group_topk);
   m.impl("gemv_attn", &gemv_attn);
   m.impl("add_rms_norm", &add_rms_norm);
   m.impl("layer_norm", &layer_norm);

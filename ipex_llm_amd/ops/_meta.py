@@ -77,6 +77,12 @@ def _(logits, k, renorm, scoring):
     return logits.new_empty((T, k), dtype=torch.float32), logits.new_empty((T, k), dtype=torch.int32)
 
 
+@register_fake("ipex_llm_amd::moe_group_topk")
+def _(logits, bias, k, n_group, topk_group, renorm, scale):
+    T = logits.numel() // logits.shape[-1]
+    return (logits.new_empty((T, k), dtype=torch.float32), logits.new_empty((T, k), dtype=torch.int32))
+
+
 @register_fake("ipex_llm_amd::moe_align")
 def _(ids, e0, num_local):
     return ids.new_empty((num_local + 1,), dtype=torch.int32), ids.new_empty((max(ids.numel(), 1),), dtype=torch.int32)

@@ -18,7 +18,7 @@ __all__ = [
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
-    "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope", "attn_prefill",
+    "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope", "attn_prefill", "moe_group_topk",
 ]
 
 
@@ -217,6 +217,15 @@ def moe_topk(logits, k, renorm=True, scoring=0):
     if _native(logits) and logits.shape[-1] <= 512:
         return _ops().moe_topk(logits, k, renorm, scoring)
     return R.moe_topk(logits, k, renorm, scoring)
+
+
+def moe_group_topk(logits, bias, k: int, n_group: int, topk_group: int, renorm: bool = True, scale: float = 1.0):
+    """DeepSeek-V3 group-limited routing (sigmoid + correction bias, top
+    groups by their top-2 sum, top-k, renormalise, routed scaling):
+    logits [T, E] -> (weights f32 [T, k], ids int32 [T, k])."""
+    if _native(logits) and logits.shape[-1] <= 512 and n_group <= 64:
+        return _ops().moe_group_topk(logits, bias, k, n_group, topk_group, renorm, scale)
+    return R.moe_group_topk(logits, bias, k, n_group, topk_group, renorm, scale)
 
 
 def moe_align(ids, e0: int, num_local: int):

@@ -237,6 +237,24 @@ def attention(q, k, v, causal=True, scale=None, softcap=0.0, window=0, q_offset=
     return o.transpose(1, 2).to(q.dtype)
 
 
+def moe_group_topk(logits, bias, k, n_group, topk_group, renorm=True, scale=1.0):
+    """DeepSeek-V3 noaux_tc router (HF DeepseekV3TopkRouter.forward after the logits)."""
+    lf = logits.float().reshape(-1, logits.shape[-1])
+    T, E = lf.shape
+    scores = lf.sigmoid()
+    sfc = scores + (bias.float() if bias is not None else 0.0)
+    gscore = sfc.view(T, n_group, E // n_group).topk(min(2, E // n_group), dim=-1)[0].sum(-1)
+    gidx = torch.topk(gscore, k=topk_group, dim=-1, sorted=False)[1]
+    gmask = torch.zeros_like(gscore).scatter_(1, gidx, 1.0)
+    smask = gmask.unsqueeze(-1).expand(T, n_group, E // n_group).reshape(T, E)
+    sfc = sfc.masked_fill(~smask.bool(), float("-inf"))
+    idx = torch.topk(sfc, k=k, dim=-1)[1]
+    w = scores.gather(1, idx)
+    if renorm:
+        w = w / (w.sum(-1, keepdim=True) + 1e-20)
+    return w * scale, idx.to(torch.int32)
+
+
 def moe_topk(logits, k, renorm=True, scoring=0):
     if scoring == 0:
         p = torch.softmax(logits.float(), dim=-1)

@@ -231,6 +231,25 @@ def _rmsnorm_forward(self, hidden_states):
     return R.rms_norm(hidden_states, w.to(hidden_states.dtype), eps)
 
 
+def _ds_router_forward(self, hidden_states):
+    """DeepSeek-V3 router on the group-limited top-k kernel (reference
+    deepseek.py:274-290 -> xe_addons.moe_group_topk)."""
+    from .. import ops
+    import torch.nn.functional as F
+    h = hidden_states.view(-1, self.hidden_dim)
+    logits = F.linear(h.float(), self.weight.float())
+    w, idx = ops.moe_group_topk(logits, self.e_score_correction_bias, self.top_k, self.num_group, self.topk_group,
+                                bool(self.norm_topk_prob), float(self.routed_scaling_factor))
+    return logits, w, idx.long()
+
+
+def _patch_routers(model: nn.Module):
+    for m in model.modules():
+        if m.__class__.__name__.endswith("TopkRouter") and all(
+                hasattr(m, a) for a in ("num_group", "topk_group", "e_score_correction_bias", "routed_scaling_factor")):
+            m.forward = types.MethodType(_ds_router_forward, m)
+
+
 def _patch_norms(model: nn.Module):
     for m in model.modules():
         cls = m.__class__.__name__
@@ -242,6 +261,7 @@ def _optimize_post(model: nn.Module):
     """Swap in the native MI355X decoder for supported architectures."""
     mt = getattr(getattr(model, "config", None), "model_type", None)
     _patch_norms(model)
+    _patch_routers(model)
     from .attention import patch_eager_attention
     patch_eager_attention(model)
     if mt == "rwkv":

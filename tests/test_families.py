@@ -43,6 +43,11 @@ FAMILIES = {
                     num_experts_per_tok=2),
     "rwkv": dict(hidden_size=H, num_hidden_layers=L, attention_hidden_size=H, intermediate_size=I, vocab_size=V,
                  context_length=128, rescale_every=1),
+    "deepseek_v3": dict(hidden_size=H, intermediate_size=I, moe_intermediate_size=32, num_hidden_layers=L,
+                        num_attention_heads=4, num_key_value_heads=4, vocab_size=V, max_position_embeddings=128,
+                        n_routed_experts=8, num_experts_per_tok=2, n_group=4, topk_group=2, n_shared_experts=1,
+                        first_k_dense_replace=1, q_lora_rank=32, kv_lora_rank=32, qk_rope_head_dim=16,
+                        qk_nope_head_dim=16, v_head_dim=16, rope_interleave=True),
     "qwen2_moe": dict(hidden_size=H, intermediate_size=I, moe_intermediate_size=64,
                       shared_expert_intermediate_size=I, num_hidden_layers=L, num_attention_heads=4,
                       num_key_value_heads=2, vocab_size=V, max_position_embeddings=128, num_experts=4,

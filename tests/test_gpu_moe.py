@@ -83,3 +83,49 @@ def test_expert_parallel_slices_sum_to_full(cuda):
         m = NativeMoE(router, g2, d2, k, True, 0, expert_offset=4 * r, num_experts=E)
         parts.append(m._experts_grouped(x, w, ids).float())
     assert torch.allclose(parts[0] + parts[1], y, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("E,n_group,topk_group,k", [(256, 8, 4, 8), (64, 8, 3, 6), (16, 4, 2, 2)])
+def test_moe_group_topk_kernel(cuda, E, n_group, topk_group, k):
+    """DeepSeek-V3 group-limited router kernel == HF DeepseekV3TopkRouter math"""
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.ops import reference as R
+    torch.manual_seed(E)
+    logits = torch.randn(37, E, device=cuda) * 3
+    bias = torch.randn(E, device=cuda) * 0.1
+    w, ids = ops.moe_group_topk(logits, bias, k, n_group, topk_group, True, 2.5)
+    rw, rids = R.moe_group_topk(logits, bias, k, n_group, topk_group, True, 2.5)
+    # same expert sets (order of equal scores aside) and weights per expert
+    for t in range(37):
+        got = dict(zip(ids[t].tolist(), w[t].tolist()))
+        ref = dict(zip(rids[t].tolist(), rw[t].tolist()))
+        assert set(got) == set(ref), t
+        for e in got:
+            assert abs(got[e] - ref[e]) < 1e-4
+
+
+def test_deepseek_v3_lowbit_on_gpu(cuda, tmp_path):
+    """tiny DeepSeek-V3 (MLA attention, grouped-router MoE, shared expert) in
+    sym_int8 on the GPU: router kernel + low-bit experts, logits close to dense"""
+    from transformers import AutoConfig, AutoModelForCausalLM as HFAuto
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    cfg = AutoConfig.for_model("deepseek_v3", hidden_size=128, intermediate_size=256, moe_intermediate_size=64,
+                               num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=4, vocab_size=256,
+                               max_position_embeddings=128, n_routed_experts=16, num_experts_per_tok=4, n_group=4,
+                               topk_group=2, n_shared_experts=1, first_k_dense_replace=1, q_lora_rank=64,
+                               kv_lora_rank=64, qk_rope_head_dim=16, qk_nope_head_dim=32, v_head_dim=32)
+    torch.manual_seed(0)
+    ref = HFAuto.from_config(cfg).eval()
+    with torch.no_grad():
+        for n, p in ref.named_parameters():
+            if n.endswith("mlp.gate.weight"):
+                p.normal_(0, 1.0)
+    p_ = str(tmp_path / "ds")
+    ref.save_pretrained(p_)
+    ids = torch.randint(3, 256, (1, 12), generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        want = ref(ids).logits.float()
+    m = AutoModelForCausalLM.from_pretrained(p_, load_in_low_bit="sym_int8", torch_dtype=torch.bfloat16).to(cuda)
+    with torch.no_grad():
+        got = m(ids.to(cuda)).logits.float().cpu()
+    assert ((got - want).norm() / want.norm()).item() < 6e-2
