@@ -273,6 +273,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     return first ? rnd(x0 * c) - rnd(x1 * sn) : rnd(x1 * c) + rnd(x0 * sn);
   };
   const bool has_new = rq && k0 + nk == len;        // this split holds the new key (position len - 1)
+  uint4 vnew[VCH];                                  // the new value row (re-applied after a late V load)
   const int colk = (a.Hq + kvh) * D, colv = (a.Hq + a.Hkv + kvh) * D;
 
   const int blk = a.block_tables[(size_t)b * a.max_blocks + k0 / a.bs];
@@ -415,6 +416,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
 #pragma unroll
             for (int e = 0; e < 4; e++) w[e] = pack2<T>(rnd(bb[2 * e] + f[2 * e]), rnd(bb[2 * e + 1] + f[2 * e + 1]));
             const uint4 vq = make_uint4(w[0], w[1], w[2], w[3]);
+            vnew[c] = vq;
 #pragma unroll
             for (int i = 0; i < 16; i++)
               if (i == (kn >> 2)) vf[i][c] = vq;
@@ -443,7 +445,21 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     for (int s = 0; s < KSTEP; s++) acc = mfma16<T>(kf[kt][s], qf[s], acc);
     st[kt] = acc;
   }
-  if constexpr (LATEV) load_v();
+  if constexpr (LATEV) {
+    load_v();
+    if constexpr (rq && DPL >= 8) {
+      // the cache row of the new value was written by this wave above: take it
+      // from registers, not from a load that may race the store
+      const int kn = nk - 1;
+      if (has_new && kg == (kn & 3)) {
+#pragma unroll
+        for (int c = 0; c < VCH; c++)
+#pragma unroll
+          for (int i = 0; i < 16; i++)
+            if (i == (kn >> 2)) vf[i][c] = vnew[c];
+      }
+    }
+  }
   const int row = r16;
   const int t = row / group;
   const int h = kvh * group + (row % group);
@@ -671,14 +687,6 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
   // combine fused into the split kernel when the merge fits its LDS scratch
   if (a.nsplit > SPLIT * RT || a.no_combine) a.counters = nullptr;
   dim3 grid(a.nsplit, a.Hkv, a.B);
-  if constexpr (D / 16 >= 8) {
-    if (a.rq_part != nullptr) {
-      hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true>), grid, dim3(64), 0, st, a);
-      if (a.counters == nullptr && !a.no_combine)
-        hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
-      return;
-    }
-  }
   static int simds = 0;
   if (simds == 0) {
     int dev = 0, cus = 0;
@@ -688,6 +696,15 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
   }
   static const int latev_env = getenv("ILLM_ATTN_LATEV") ? atoi(getenv("ILLM_ATTN_LATEV")) : -1;
   const bool latev = latev_env >= 0 ? latev_env == 1 : (long)a.nsplit * a.Hkv * a.B > simds;
+  if constexpr (D / 16 >= 8) {
+    if (a.rq_part != nullptr) {
+      if (latev) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, true>), grid, dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true>), grid, dim3(64), 0, st, a);
+      if (a.counters == nullptr && !a.no_combine)
+        hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
+      return;
+    }
+  }
   if (latev) {
     if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT, false, true>), grid, dim3(64), 0, st, a);
     else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT, false, true>), grid, dim3(64), 0, st, a);
