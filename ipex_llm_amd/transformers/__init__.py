@@ -3,6 +3,7 @@ from .low_bit_linear import LowBitLinear, DenseLinear, FP16Linear, BF16Linear, M
 from .model import (AutoModelForCausalLM, AutoModel, AutoModelForSpeechSeq2Seq,  # noqa: F401
                     AutoModelForSeq2SeqLM, AutoModelForSequenceClassification, AutoModelForMaskedLM,
                     AutoModelForQuestionAnswering, AutoModelForNextSentencePrediction,
-                    AutoModelForMultipleChoice, AutoModelForTokenClassification, save_low_bit)
+                    AutoModelForMultipleChoice, AutoModelForTokenClassification, AutoModelForImageTextToText,
+                    AutoModelForVision2Seq, save_low_bit)
 from .convert import ggml_convert_low_bit  # noqa: F401
 from .hybrid import convert_model_hybrid  # noqa: F401

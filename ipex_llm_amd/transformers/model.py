@@ -326,3 +326,13 @@ class AutoModelForMultipleChoice(_BaseAutoModelClass, metaclass=_Lazy):
 
 class AutoModelForTokenClassification(_BaseAutoModelClass, metaclass=_Lazy):
     _hf_name = "AutoModelForTokenClassification"
+
+
+class AutoModelForImageTextToText(_BaseAutoModelClass, metaclass=_Lazy):
+    """vision-language models (qwen2_vl, mllama, llava, ... ; reference
+    transformers/model.py Qwen2VL class and the vision examples)"""
+    _hf_name = "AutoModelForImageTextToText"
+
+
+# reference name of the same family
+AutoModelForVision2Seq = AutoModelForImageTextToText

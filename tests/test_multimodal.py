@@ -1,0 +1,82 @@
+"""Non-decoder-only families on the HF forward over low-bit linears (the
+reference optimises whisper, bert, qwen2_vl, mllama, minicpmv ... with
+per-arch forwards; here they run the HF forward, the linears low-bit):
+encoder-decoder speech (Whisper), encoders (BERT) and vision-language
+(Qwen2-VL) load through the AutoModel classes and stay close to the dense
+model.  Tiny random configs, CPU."""
+import pytest
+import torch
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+def test_whisper_speech_seq2seq_lowbit(tmp_path):
+    from transformers import WhisperConfig, WhisperForConditionalGeneration
+    from ipex_llm_amd.transformers import AutoModelForSpeechSeq2Seq
+    cfg = WhisperConfig(vocab_size=256, d_model=64, encoder_layers=2, decoder_layers=2, encoder_attention_heads=4,
+                        decoder_attention_heads=4, encoder_ffn_dim=128, decoder_ffn_dim=128, num_mel_bins=16,
+                        max_source_positions=32, max_target_positions=64, decoder_start_token_id=1, pad_token_id=0,
+                        eos_token_id=2, bos_token_id=1)
+    torch.manual_seed(0)
+    ref = WhisperForConditionalGeneration(cfg).eval()
+    p = str(tmp_path / "w")
+    ref.save_pretrained(p)
+    feats = torch.randn(1, 16, 64)
+    dec = torch.tensor([[1, 5, 9, 11]])
+    with torch.no_grad():
+        want = ref(input_features=feats, decoder_input_ids=dec).logits
+    m = AutoModelForSpeechSeq2Seq.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32)
+    with torch.no_grad():
+        got = m(input_features=feats, decoder_input_ids=dec).logits
+    assert _rel(got, want) < 5e-2
+    out = m.generate(input_features=feats, max_new_tokens=4, min_new_tokens=4, do_sample=False)
+    assert out.shape[1] >= 4
+
+
+def test_bert_encoder_lowbit(tmp_path):
+    from transformers import BertConfig, BertModel
+    from ipex_llm_amd.transformers import AutoModel
+    cfg = BertConfig(vocab_size=256, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                     intermediate_size=128, max_position_embeddings=64)
+    torch.manual_seed(0)
+    ref = BertModel(cfg).eval()
+    p = str(tmp_path / "b")
+    ref.save_pretrained(p)
+    ids = torch.randint(3, 256, (2, 12))
+    with torch.no_grad():
+        want = ref(ids).last_hidden_state
+    m = AutoModel.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32)
+    with torch.no_grad():
+        got = m(ids).last_hidden_state
+    assert _rel(got, want) < 5e-2
+
+
+def test_qwen2_vl_image_text_lowbit(tmp_path):
+    from transformers import Qwen2VLConfig, Qwen2VLForConditionalGeneration
+    from ipex_llm_amd.transformers import AutoModelForImageTextToText, AutoModelForVision2Seq
+    assert AutoModelForVision2Seq is AutoModelForImageTextToText
+    text = dict(vocab_size=256, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                num_key_value_heads=2, max_position_embeddings=256,
+                rope_scaling={"type": "mrope", "mrope_section": [2, 3, 3]})
+    vision = dict(depth=2, embed_dim=32, hidden_size=64, num_heads=4, mlp_ratio=2, patch_size=14,
+                  spatial_merge_size=2, temporal_patch_size=2, in_channels=3)
+    try:
+        cfg = Qwen2VLConfig(text_config=text, vision_config=vision, image_token_id=250, video_token_id=251,
+                            vision_start_token_id=252)
+    except TypeError as e:                          # pragma: no cover - config layout of other versions
+        pytest.skip(f"Qwen2VLConfig layout: {e}")
+    torch.manual_seed(0)
+    ref = Qwen2VLForConditionalGeneration(cfg).eval()
+    p = str(tmp_path / "vl")
+    ref.save_pretrained(p)
+    ids = torch.randint(3, 240, (1, 10))
+    with torch.no_grad():
+        want = ref(input_ids=ids).logits
+    m = AutoModelForImageTextToText.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32)
+    with torch.no_grad():
+        got = m(input_ids=ids).logits
+    assert _rel(got, want) < 5e-2
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    assert any(isinstance(x, LowBitLinear) for x in m.modules())
