@@ -24,6 +24,18 @@ namespace illm {
 constexpr int SPLIT = 64;
 constexpr int RMAX = 16;
 
+// write-through (sc1) stores / L1-bypassing (sc1) loads of the split
+// partials handed to the last-arriving split of a (batch, kv head): the
+// MI355X hand-off form "sc1 stores, s_waitcnt vmcnt(0), one agent-scope
+// atomic add per workgroup, sc1 loads by the workgroup whose add came last"
+// (no __threadfence / L2 write-back on the critical path)
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <typename T, int KVF>
 __device__ __forceinline__ void kv_load8(const uint8_t* p, float scale, float* v) {
   if constexpr (KVF == 0) {
@@ -225,6 +237,9 @@ __device__ __forceinline__ uint4 kv_frag8(const uint8_t* p) {
     return r;
   }
 }
+
+template <typename T, bool SC1 = false>
+__device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int h, int t, float* wsh);
 
 // LATEV: issue the V loads after Q K^T (K registers are dead by then): fewer
 // VGPRs and the V stream overlaps the QK/softmax of the co-resident wave.
@@ -540,6 +555,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
       o[r][d] = x;
     }
   const float vs = KVF ? a.v_scale : 1.f;
+  const bool handoff = a.counters != nullptr;
   if (kg == 0) {
 #pragma unroll
     for (int r = 0; r < RT; r++) {
@@ -547,43 +563,68 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
         const int tt = r / group, hh = kvh * group + r % group;
         const size_t prow = (((size_t)b * a.Hq + hh) * a.Tq + tt) * a.nsplit + split;
         float* po = a.part_o + prow * D + DPL * dg;
+        if (handoff) {
 #pragma unroll
-        for (int d = 0; d < DPL; d += 4)
-          *(float4*)(po + d) = make_float4(o[r][d] * vs, o[r][d + 1] * vs, o[r][d + 2] * vs, o[r][d + 3] * vs);
+          for (int d = 0; d < DPL; d++) st_sc1(po + d, o[r][d] * vs);
+        } else {
+#pragma unroll
+          for (int d = 0; d < DPL; d += 4)
+            *(float4*)(po + d) = make_float4(o[r][d] * vs, o[r][d + 1] * vs, o[r][d + 2] * vs, o[r][d + 3] * vs);
+        }
       }
     }
   }
   if (g == 0 && row < R) {
     const size_t prow = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit + split;
-    a.part_ml[prow * 2] = m;
-    a.part_ml[prow * 2 + 1] = l;
+    if (handoff) {
+      st_sc1(a.part_ml + prow * 2, m);
+      st_sc1(a.part_ml + prow * 2 + 1, l);
+    } else {
+      a.part_ml[prow * 2] = m;
+      a.part_ml[prow * 2 + 1] = l;
+    }
   }
-  if (a.counters == nullptr) return;
-  // ---- fused combine: the last split block of this (b, kv head) merges the
-  // partials of its R query rows (saves the combine launch; counters are
-  // reset by the merging block, so graph replays start from zero)
+  if (!handoff) return;
+  // ---- fused combine: the last split (one wave = one workgroup) of this
+  // (b, kv head) to arrive merges the partials of its R query rows (saves the
+  // combine launch).  The counter is reset by the merging wave, so graph
+  // replays start from zero.
   __shared__ int is_last;
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's sc1 stores are done
   __syncthreads();
   if (lane == 0) {
     const int ns = min(a.nsplit, (len + SPLIT - 1) / SPLIT);
     int* ctr = a.counters + (size_t)b * a.Hkv + kvh;
-    const int prev = atomicAdd(ctr, 1);
+    const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = prev == ns - 1;
-    if (is_last) *ctr = 0;
+    if (is_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (!is_last) return;
-  __threadfence();
   float* wsh = &ps[0][0];        // SPLIT * RT floats of LDS, reused
-  for (int r = 0; r < R; r++) combine_row<T>(a, b, kvh * group + r % group, r / group, wsh);
+  for (int r = 0; r < R; r++) combine_row<T, true>(a, b, kvh * group + r % group, r / group, wsh);
+  if constexpr (rq) {
+    // fused-RoPE decode: every split of this (b, kv head) has read its q / k / v
+    // columns of the qkv accumulator: re-zero them for the next layer's GEMV
+    float* prow = (float*)a.rq_part + (size_t)b * a.rq_ld;
+    for (int hh = kvh * group; hh < (kvh + 1) * group; hh++)
+      for (int d = lane * 4; d < D; d += 256) *(float4*)(prow + hh * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int d = lane * 4; d < D; d += 256) {
+      *(float4*)(prow + (a.Hq + kvh) * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *(float4*)(prow + (a.Hq + a.Hkv + kvh) * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
 }
 
 // merge the nsplit partial (o, m, l) of one (b, h, t) row: split weights
 // lane-parallel into LDS, then every lane sums its head dims with
 // independent loads.
-template <typename T>
+template <typename T, bool SC1>
 __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int h, int t, float* wsh) {
+  // SC1: the partials were handed over by other waves of this launch (sc1 loads)
+  auto ld = [](const float* p) -> float {
+    if constexpr (SC1) return ld_sc1(p); else return *p;
+  };
   const int lane = threadIdx.x;
   const int len = a.seq_lens[b];
   const int ns = min(a.nsplit, (len + SPLIT - 1) / SPLIT);
@@ -592,17 +633,17 @@ __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int 
   if (ns > 1024) {
     // more splits than the LDS weight scratch holds (> 64 Ki keys): every
     // lane recomputes the split weights it needs (rare, long-context only)
-    for (int s = lane; s < ns; s += 64) M = fmaxf(M, a.part_ml[(row0 + s) * 2]);
+    for (int s = lane; s < ns; s += 64) M = fmaxf(M, ld(a.part_ml + (row0 + s) * 2));
     M = wave_max(M);
     uint16_t* out = a.out + (((size_t)b * a.Tq + t) * a.Hq + h) * a.D;
     const float* po = a.part_o + row0 * a.D;
     for (int d = lane; d < a.D; d += 64) {
       float x = 0.f, l = 0.f;
       for (int s = 0; s < ns; s++) {
-        const float2 ml = *(const float2*)(a.part_ml + (row0 + s) * 2);
+        const float2 ml = make_float2(ld(a.part_ml + (row0 + s) * 2), ld(a.part_ml + (row0 + s) * 2 + 1));
         const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
         l += w * ml.y;
-        x += w * po[(size_t)s * a.D + d];
+        x += w * ld(po + (size_t)s * a.D + d);
       }
       out[d] = from_f32<T>(l > 0.f ? x / l : 0.f);
     }
@@ -612,16 +653,16 @@ __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int 
   if (ns <= 64) {
     // one (m, l) pair per lane, loaded once
     float2 ml = make_float2(-INFINITY, 0.f);
-    if (lane < ns) ml = *(const float2*)(a.part_ml + (row0 + lane) * 2);
+    if (lane < ns) ml = make_float2(ld(a.part_ml + (row0 + lane) * 2), ld(a.part_ml + (row0 + lane) * 2 + 1));
     M = wave_max(ml.x);
     const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
     L = w * ml.y;
     if (lane < ns) wsh[lane] = w;
   } else {
-    for (int s = lane; s < ns; s += 64) M = fmaxf(M, a.part_ml[(row0 + s) * 2]);
+    for (int s = lane; s < ns; s += 64) M = fmaxf(M, ld(a.part_ml + (row0 + s) * 2));
     M = wave_max(M);
     for (int s = lane; s < ns; s += 64) {
-      const float2 ml = *(const float2*)(a.part_ml + (row0 + s) * 2);
+      const float2 ml = make_float2(ld(a.part_ml + (row0 + s) * 2), ld(a.part_ml + (row0 + s) * 2 + 1));
       const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
       L += w * ml.y;
       if (s < 1024) wsh[s] = w;
@@ -641,8 +682,8 @@ __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int 
     int s = 0;
     for (; s + 4 <= ns; s += 4) {
       const float* p0 = po + (size_t)s * a.D;
-      const float u0 = p0[d], u1 = p0[a.D + d], u2 = p0[2 * a.D + d], u3 = p0[3 * a.D + d];
-      const float v0 = p0[e], v1 = p0[a.D + e], v2 = p0[2 * a.D + e], v3 = p0[3 * a.D + e];
+      const float u0 = ld(p0 + d), u1 = ld(p0 + a.D + d), u2 = ld(p0 + 2 * a.D + d), u3 = ld(p0 + 3 * a.D + d);
+      const float v0 = ld(p0 + e), v1 = ld(p0 + a.D + e), v2 = ld(p0 + 2 * a.D + e), v3 = ld(p0 + 3 * a.D + e);
       x0 += wsh[s] * u0;
       x1 += wsh[s + 1] * u1;
       x2 += wsh[s + 2] * u2;
@@ -653,8 +694,8 @@ __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int 
       y3 += wsh[s + 3] * v3;
     }
     for (; s < ns; s++) {
-      x0 += wsh[s] * po[(size_t)s * a.D + d];
-      y0 += wsh[s] * po[(size_t)s * a.D + e];
+      x0 += wsh[s] * ld(po + (size_t)s * a.D + d);
+      y0 += wsh[s] * ld(po + (size_t)s * a.D + e);
     }
     out[d] = from_f32<T>((x0 + x1 + x2 + x3) * invL);
     if (two) out[e] = from_f32<T>((y0 + y1 + y2 + y3) * invL);

@@ -556,6 +556,20 @@ void rope_kv(const Tensor& qkv, Tensor& q_out, Tensor& k_cache, Tensor& v_cache,
 // buffer is allocated once (outside any graph capture: the first eager call
 // of a shape allocates it) and every merging block resets its counter, so the
 // same pointer is valid across hipGraph replays.
+// in-kernel merge of the split partials by the last-arriving split of each
+// (batch, kv head), handed over with write-through stores + one agent-scope
+// atomic (no combine launch).  Opt-in (ILLM_ATTN_FUSED_COMBINE=1): correct,
+// but ONE wave merging R rows x D dims over all splits is a serial tail longer
+// than the parallel combine launch it replaces (MI355X, Llama-3-8B, L = 1024:
+// batch 1 1.988 -> 2.158 ms/token, batch 8 2.407 -> 2.725 ms/step).
+static bool fused_combine_on() {
+  static const bool on = [] {
+    const char* e = getenv("ILLM_ATTN_FUSED_COMBINE");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return on;
+}
+
 int* attn_counters(const c10::Device& dev, int64_t n) {
   static std::vector<Tensor> bufs(64);
   const int idx = dev.index() < 0 ? 0 : dev.index();
@@ -655,10 +669,7 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, cons
   a.k_scale = (float)k_scale;
   a.v_scale = (float)v_scale;
   a.alibi = (alibi.has_value() && alibi->defined()) ? alibi->data_ptr<float>() : nullptr;
-  // the in-kernel merge (last split block combines) is serial per head
-  // group and measured slower than the separate combine launch; opt-in only
-  static const bool fused_combine = getenv("ILLM_ATTN_FUSED_COMBINE") != nullptr;
-  a.counters = fused_combine ? attn_counters(q.device(), B * Hkv) : nullptr;
+  a.counters = fused_combine_on() ? attn_counters(q.device(), B * Hkv) : nullptr;
   a.no_combine = no_combine ? 1 : 0;
   illm::launch_attn_decode(bf16, a, cur_stream());
   return {out, po, pml};
@@ -711,7 +722,8 @@ Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, c
   a.sliding_window = (int)window;
   a.kv_fp8 = 0;
   a.k_scale = a.v_scale = 1.f;
-  a.counters = nullptr;          // the combine launch also re-zeroes the accumulator
+  // the merging split (fused combine) or the combine launch re-zeroes the accumulator
+  a.counters = fused_combine_on() ? attn_counters(part.device(), B * Hkv) : nullptr;
   a.rq_part = part.data_ptr<float>();
   a.rq_bias = p16o(bias);
   a.rq_cos_sin = cos_sin.data_ptr<float>();

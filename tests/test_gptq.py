@@ -85,4 +85,13 @@ def test_prequantized_checkpoint_loads_exactly(tmp_path, method):
     with torch.no_grad():
         want = ref.float()(ids).logits
         got = m(ids).logits
-    assert ((got - want).norm() / want.norm()).item() < 5e-3
+    # CPU low-bit linears quantize activations to int8 per 64-block (the
+    # integer-dot kernels, like ggml's q4 x q8): logits within ~1 %
+    assert ((got - want).norm() / want.norm()).item() < 2.5e-2
+    # the weights themselves load exactly (scales / zeros as fp16)
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    name = "model.layers.0.self_attn.o_proj"
+    lin = dict(m.named_modules())[name]
+    if isinstance(lin, LowBitLinear) and lin.g_idx_map is None:
+        w_ref = dict(ref.named_modules())[name].weight.data.float()
+        assert torch.allclose(lin.dequantize(torch.float32), w_ref, atol=2e-3, rtol=2e-3)

@@ -397,3 +397,35 @@ def test_attn_softmax_inplace(cuda, dtype, shape):
     z = torch.full((2, 33), float("-inf"), device=cuda, dtype=dtype)
     ops.attn_softmax_(z)
     assert (z == 0).all()
+
+
+def test_attn_decode_fused_combine_repeated_uneven(cuda):
+    """the last-arriving split merges the partials handed over by the other
+    waves of the launch (write-through stores + atomic counter): many launches
+    with uneven lengths / split counts, every output checked, the counters
+    must come back to zero (graph replays reuse them)"""
+    torch.manual_seed(11)
+    B, Hq, Hkv, D, bs = 8, 32, 8, 128, 64
+    nblk = B * 40
+    kc = torch.randn(nblk, Hkv, bs, D, device=cuda).bfloat16()
+    vc = torch.randn(nblk, Hkv, bs, D, device=cuda).bfloat16()
+    bt = torch.randperm(nblk, device=cuda).to(torch.int32).view(B, 40)
+    worst = 0.0
+    for it in range(40):
+        lens = torch.randint(1, 40 * bs, (B,), generator=torch.Generator().manual_seed(it))
+        seq = lens.to(torch.int32).to(cuda)
+        q = torch.randn(B, 1, Hq, D, device=cuda).bfloat16()
+        ns = (int(lens.max()) + 63) // 64
+        got = ops.attn_decode(q, kc, vc, bt, seq, ns, D ** -0.5)
+        ref = ops.api.attn_decode.__wrapped__(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), seq.cpu(), ns, D ** -0.5) \
+            if hasattr(ops.api.attn_decode, "__wrapped__") else None
+        if ref is None:
+            outs = []
+            for b in range(B):
+                L = int(lens[b])
+                kk = ops.api.gather_kv(kc, bt, b, L).float()
+                vv = ops.api.gather_kv(vc, bt, b, L).float()
+                outs.append(R.attention(q[b:b + 1].float(), kk[None], vv[None], True, D ** -0.5))
+            ref = torch.cat(outs, 0)
+        worst = max(worst, _rel(got.float(), ref.float()))
+    assert worst < 1e-2, worst
