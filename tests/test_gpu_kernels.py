@@ -429,3 +429,19 @@ def test_attn_decode_fused_combine_repeated_uneven(cuda):
             ref = torch.cat(outs, 0)
         worst = max(worst, _rel(got.float(), ref.float()))
     assert worst < 1e-2, worst
+
+
+def test_attn_decode_fused_combine_opt_in_subprocess(cuda):
+    """the opt-in fused combine (ILLM_ATTN_FUSED_COMBINE=1, read once per
+    process) passes the repeated uneven-length check and the MHA rope-in
+    slab-zeroing checks in a child process"""
+    import os
+    import subprocess
+    import sys
+    if os.environ.get("ILLM_ATTN_FUSED_COMBINE") == "1":
+        pytest.skip("already the child process")
+    env = dict(os.environ, ILLM_ATTN_FUSED_COMBINE="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", __file__, "-k",
+                        "fused_combine_repeated or attn_decode_rope_matches or rope_in_mha"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
