@@ -24,6 +24,8 @@
 //     A operand (V^T) comes from ds_read_b64_tr_b16 transposed reads of the
 //     row-major V tile in exactly that key order;
 //   * fp8 KV caches are converted to 16-bit while the tile is staged.
+#include <cstdlib>
+
 #include "../common/quant_block.h"
 #include "illm_device.h"
 #include "kernels.h"
@@ -69,19 +71,23 @@ __device__ __forceinline__ uint2 ds_read_tr16(const uint16_t* p) {
   return __builtin_bit_cast(uint2, v);
 }
 
-template <typename T, int D, int KVF>
+// HP = query heads per wave that share one kv head (GQA): every K fragment
+// read from LDS and every transposed V read feeds HP MFMAs.
+template <typename T, int D, int KVF, int HP>
 __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs a) {
   constexpr int EB = KVF == 0 ? 2 : 1;            // cache bytes per element
   constexpr int KSTEP = D / 32;                   // MFMA k-steps over the head dim (QK^T)
   constexpr int DT = D / 16;                      // 16-wide d tiles of O^T
   constexpr int UPT = PF_KT * D / 8 / 256;        // 8-element staging units per thread per tile
-  __shared__ __attribute__((aligned(16))) uint16_t ks[PF_KT * D];
-  __shared__ __attribute__((aligned(16))) uint16_t vs[PF_KT * D];
+  // double-buffered K / V tiles: the next tile is written while the current
+  // one is read, one workgroup barrier per tile
+  __shared__ __attribute__((aligned(16))) uint16_t ks[2][PF_KT * D];
+  __shared__ __attribute__((aligned(16))) uint16_t vs[2][PF_KT * D];
 
   const int nqb = gridDim.x;
   const int qb = nqb - 1 - blockIdx.x;            // heaviest (latest) query block first
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int kvh = h / (a.Hq / a.Hkv);
+  const int h0 = blockIdx.y * HP, b = blockIdx.z;
+  const int kvh = h0 / (a.Hq / a.Hkv);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   const int L = a.seq_lens[b];
@@ -91,18 +97,20 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
   const int qpos = p0 + min(qrow, Tq - 1);
 
   // key range of the workgroup
+  const int wg_q0 = p0 + qb * PF_QB;
   const int wg_q_last = min(Tq - 1, qb * PF_QB + PF_QB - 1);
   const int kend = min(L, p0 + wg_q_last + 1);
   int kbeg = 0;
-  if (a.sliding_window > 0) kbeg = max(0, p0 + qb * PF_QB - a.sliding_window + 1) & ~(PF_KT - 1);
+  if (a.sliding_window > 0) kbeg = max(0, wg_q0 - a.sliding_window + 1) & ~(PF_KT - 1);
   const int ntile = kend > kbeg ? (kend - kbeg + PF_KT - 1) / PF_KT : 0;
 
   // Q fragments (B operand of S^T = K Q^T): row qrow, dims 32 s + 8 g .. + 7
-  uint4 qf[KSTEP];
-  {
-    const uint16_t* qp = a.q + ((size_t)(b * Tq + min(qrow, Tq - 1)) * a.Hq + h) * D;
+  uint4 qf[HP][KSTEP];
 #pragma unroll
-    for (int s = 0; s < KSTEP; s++) qf[s] = *(const uint4*)(qp + 32 * s + 8 * g);
+  for (int j = 0; j < HP; j++) {
+    const uint16_t* qp = a.q + ((size_t)(b * Tq + min(qrow, Tq - 1)) * a.Hq + h0 + j) * D;
+#pragma unroll
+    for (int s = 0; s < KSTEP; s++) qf[j][s] = *(const uint4*)(qp + 32 * s + 8 * g);
   }
 
   // staging: unit u = tid + 256 j covers key u / (D / 8), chunk u % (D / 8)
@@ -127,117 +135,152 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
       if (k0 + r >= L) kreg[j] = vreg[j] = make_uint4(0, 0, 0, 0);
     }
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < UPT; j++) {
       const int u = tid + 256 * j;
       const int r = u / (D / 8), c = u % (D / 8);
-      *(uint4*)(ks + pf_off<D>(r, c)) = kreg[j];
-      *(uint4*)(vs + pf_off<D>(r, c)) = vreg[j];
+      *(uint4*)(ks[buf] + pf_off<D>(r, c)) = kreg[j];
+      *(uint4*)(vs[buf] + pf_off<D>(r, c)) = vreg[j];
     }
   };
 
-  f32x4 o[DT];
+  f32x4 o[HP][DT];
 #pragma unroll
-  for (int d = 0; d < DT; d++) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float mrow = -INFINITY, lpart = 0.f;
+  for (int j = 0; j < HP; j++)
+#pragma unroll
+    for (int d = 0; d < DT; d++) o[j][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrow[HP], lpart[HP];
+#pragma unroll
+  for (int j = 0; j < HP; j++) { mrow[j] = -INFINITY; lpart[j] = 0.f; }
   const float sc = a.scale;
 
-  if (ntile > 0) load_tile(0);
+  if (ntile > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
   for (int t = 0; t < ntile; t++) {
-    __syncthreads();                              // every wave done reading the previous tile
-    store_tile();
-    __syncthreads();
+    const int buf = t & 1;
     if (t + 1 < ntile) load_tile(t + 1);          // next tile in flight during the compute
     const int kt0 = kbeg + t * PF_KT;
+    const uint16_t* kb_ = ks[buf];
+    const uint16_t* vb_ = vs[buf];
+    // tiles wholly below every query row of the workgroup need no mask
+    const bool full = kt0 + PF_KT - 1 <= wg_q0 && kt0 + PF_KT <= L && a.sliding_window <= 0;
 
     // ---- S^T = K Q^T : lane holds keys 16 kb + 4 g + i of query row r16
-    f32x4 st[4];
+    f32x4 st[HP][4];
 #pragma unroll
     for (int kb = 0; kb < 4; kb++) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < HP; j++) st[j][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KSTEP; s++) {
-        const uint4 kf = *(const uint4*)(ks + pf_off<D>(16 * kb + r16, 4 * s + g));
-        acc = mfma16<T>(kf, qf[s], acc);
+        const uint4 kf = *(const uint4*)(kb_ + pf_off<D>(16 * kb + r16, 4 * s + g));
+#pragma unroll
+        for (int j = 0; j < HP; j++) st[j][kb] = mfma16<T>(kf, qf[j][s], st[j][kb]);
       }
-      st[kb] = acc;
     }
     // ---- scale, soft-cap, causal / window / length mask, online softmax
-    float tmax = -INFINITY;
+    uint32_t pk[HP][4][2];                         // P^T fragments, 16-bit pairs
 #pragma unroll
-    for (int kb = 0; kb < 4; kb++) {
+    for (int j = 0; j < HP; j++) {
+      float tmax = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int key = kt0 + 16 * kb + 4 * g + i;
-        float v = st[kb][i] * sc;
-        if (a.softcap > 0.f) v = a.softcap * tanhf(v / a.softcap);
-        bool ok = key <= qpos && key < L;
-        if (a.sliding_window > 0 && key <= qpos - a.sliding_window) ok = false;
-        v = ok ? v : -INFINITY;
-        st[kb][i] = v;
-        tmax = fmaxf(tmax, v);
+      for (int kb = 0; kb < 4; kb++) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          float v = st[j][kb][i] * sc;
+          if (a.softcap > 0.f) v = a.softcap * tanhf(v / a.softcap);
+          if (!full) {
+            const int key = kt0 + 16 * kb + 4 * g + i;
+            bool ok = key <= qpos && key < L;
+            if (a.sliding_window > 0 && key <= qpos - a.sliding_window) ok = false;
+            v = ok ? v : -INFINITY;
+          }
+          st[j][kb][i] = v;
+          tmax = fmaxf(tmax, v);
+        }
       }
-    }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(mrow, tmax);
-    const float alpha = mrow == -INFINITY ? 0.f : __expf(mrow - mnew);
-    mrow = mnew;
-    lpart *= alpha;
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(mrow[j], tmax);
+      const float alpha = mrow[j] == -INFINITY ? 0.f : __expf(mrow[j] - mnew);
+      mrow[j] = mnew;
+      lpart[j] *= alpha;
 #pragma unroll
-    for (int d = 0; d < DT; d++) {
-      o[d][0] *= alpha; o[d][1] *= alpha; o[d][2] *= alpha; o[d][3] *= alpha;
-    }
-    uint32_t pk[4][2];                             // P^T fragments, 16-bit pairs
-#pragma unroll
-    for (int kb = 0; kb < 4; kb++) {
-      float p[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        p[i] = st[kb][i] == -INFINITY ? 0.f : __expf(st[kb][i] - mnew);
-        lpart += p[i];
+      for (int d = 0; d < DT; d++) {
+        o[j][d][0] *= alpha; o[j][d][1] *= alpha; o[j][d][2] *= alpha; o[j][d][3] *= alpha;
       }
-      pk[kb][0] = pack2<T>(p[0], p[1]);
-      pk[kb][1] = pack2<T>(p[2], p[3]);
+#pragma unroll
+      for (int kb = 0; kb < 4; kb++) {
+        float p[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          p[i] = st[j][kb][i] == -INFINITY ? 0.f : __expf(st[j][kb][i] - mnew);
+          lpart[j] += p[i];
+        }
+        pk[j][kb][0] = pack2<T>(p[0], p[1]);
+        pk[j][kb][1] = pack2<T>(p[2], p[3]);
+      }
     }
     // ---- O^T += V^T P^T over two 32-key steps (key blocks 2 ks, 2 ks + 1)
 #pragma unroll
     for (int kk = 0; kk < 2; kk++) {
-      const uint4 pb = make_uint4(pk[2 * kk][0], pk[2 * kk][1], pk[2 * kk + 1][0], pk[2 * kk + 1][1]);
       // lane 4q + p of the 16-lane group g addresses row 16 kb + 4 g + q, columns 16 dt + 4 p
       const int qq = r16 >> 2, pp = r16 & 3;
       const int row0 = 16 * (2 * kk) + 4 * g + qq, row1 = row0 + 16;
 #pragma unroll
       for (int d = 0; d < DT; d++) {
         const int col = 16 * d + 4 * pp;                     // element column; chunk col / 8
-        const uint2 v0 = ds_read_tr16(vs + pf_off<D>(row0, col >> 3) + (col & 7));
-        const uint2 v1 = ds_read_tr16(vs + pf_off<D>(row1, col >> 3) + (col & 7));
-        o[d] = mfma16<T>(make_uint4(v0.x, v0.y, v1.x, v1.y), pb, o[d]);
+        const uint2 v0 = ds_read_tr16(vb_ + pf_off<D>(row0, col >> 3) + (col & 7));
+        const uint2 v1 = ds_read_tr16(vb_ + pf_off<D>(row1, col >> 3) + (col & 7));
+        const uint4 va = make_uint4(v0.x, v0.y, v1.x, v1.y);
+#pragma unroll
+        for (int j = 0; j < HP; j++) {
+          const uint4 pb = make_uint4(pk[j][2 * kk][0], pk[j][2 * kk][1], pk[j][2 * kk + 1][0], pk[j][2 * kk + 1][1]);
+          o[j][d] = mfma16<T>(va, pb, o[j][d]);
+        }
       }
     }
+    if (t + 1 < ntile) store_tile(buf ^ 1);       // read last during tile t - 1: free since the barrier
+    __syncthreads();
   }
 
   // ---- normalise and store: lane holds O^T[16 d + 4 g + i][row r16]
-  float l = lpart;
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  if (qrow >= Tq) return;
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  uint16_t* op = a.out + ((size_t)(b * Tq + qrow) * a.Hq + h) * D;
 #pragma unroll
-  for (int d = 0; d < DT; d++) {
-    *(uint2*)(op + 16 * d + 4 * g) = make_uint2(pack2<T>(o[d][0] * inv, o[d][1] * inv),
-                                                pack2<T>(o[d][2] * inv, o[d][3] * inv));
+  for (int j = 0; j < HP; j++) {
+    float l = lpart[j];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (qrow >= Tq) continue;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* op = a.out + ((size_t)(b * Tq + qrow) * a.Hq + h0 + j) * D;
+#pragma unroll
+    for (int d = 0; d < DT; d++) {
+      *(uint2*)(op + 16 * d + 4 * g) = make_uint2(pack2<T>(o[j][d][0] * inv, o[j][d][1] * inv),
+                                                  pack2<T>(o[j][d][2] * inv, o[j][d][3] * inv));
+    }
   }
+}
+
+template <typename T, int D, int HP>
+static void launch_pf_hp(const AttnPrefillArgs& a, hipStream_t st) {
+  dim3 grid((a.Tq + PF_QB - 1) / PF_QB, a.Hq / HP, a.B);
+  if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_prefill_kernel<T, D, 1, HP>), grid, dim3(256), 0, st, a);
+  else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_prefill_kernel<T, D, 2, HP>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_prefill_kernel<T, D, 0, HP>), grid, dim3(256), 0, st, a);
 }
 
 template <typename T, int D>
 static void launch_pf_d(const AttnPrefillArgs& a, hipStream_t st) {
-  dim3 grid((a.Tq + PF_QB - 1) / PF_QB, a.Hq, a.B);
-  if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_prefill_kernel<T, D, 1>), grid, dim3(256), 0, st, a);
-  else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_prefill_kernel<T, D, 2>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_prefill_kernel<T, D, 0>), grid, dim3(256), 0, st, a);
+  // ILLM_PREFILL_HP=2: two query heads per wave sharing the kv head's LDS reads
+  // (even GQA group).  310 registers -> one wave per SIMD: measured slower on
+  // MI355X (T = 1024: 58.4 vs 44.8 us; T = 16384: 7.2 vs 5.0 ms), so opt-in
+  static const int hp_env = getenv("ILLM_PREFILL_HP") ? atoi(getenv("ILLM_PREFILL_HP")) : 1;
+  if (hp_env >= 2 && (a.Hq / a.Hkv) % 2 == 0) launch_pf_hp<T, D, 2>(a, st);
+  else launch_pf_hp<T, D, 1>(a, st);
 }
 
 template <typename T>

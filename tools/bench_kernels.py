@@ -149,7 +149,7 @@ def prefill_attn(dev):
     (contiguous K/V, GQA) at Llama-3-8B head geometry."""
     import torch.nn.functional as F
     Hq, Hkv, D, bs = 32, 8, 128, 64
-    for B, T in ((1, 1024), (1, 4096), (8, 1024)):
+    for B, T in ((1, 1024), (1, 4096), (8, 1024), (1, 16384)):
         nblk = B * (T // bs)
         kc = torch.randn(nblk, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
         vc = torch.randn_like(kc)
