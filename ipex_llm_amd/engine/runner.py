@@ -122,10 +122,12 @@ class DecodeStep:
         self._refresh()
 
     def step(self):
-        if self.graph is not None:
-            self.graph.replay()
-        else:
-            self._body()
+        from ..utils.trace import trace_range
+        with trace_range("decode_step"):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._body()
         return self.next_ids
 
 
@@ -189,6 +191,11 @@ class Engine:
     @torch.no_grad()
     def prefill(self, seq: SequenceState, ids: torch.Tensor, start: int = 0) -> torch.Tensor:
         """Run ids (1-D) for one sequence from position ``start``; returns last logits [1, V]."""
+        from ..utils.trace import trace_range
+        with trace_range(f"prefill[{ids.numel()}]"):
+            return self._prefill(seq, ids, start)
+
+    def _prefill(self, seq: SequenceState, ids: torch.Tensor, start: int = 0) -> torch.Tensor:
         m, c = self.model, self.cache
         dev = m.device
         n = ids.numel()

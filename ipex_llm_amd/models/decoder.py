@@ -482,7 +482,12 @@ class NativeCausalLM(nn.Module):
         rope_in = T <= ROPE_IN_MAX_M and self._rope_in_ok(meta, cache) and self._qkv_native(residual)
         nxt_res = lambda r: res_pp[1] if r is res_pp[0] else res_pp[0]
         zero_next = None                # consumed atomic slab the next accumulating GEMV zeroes
+        from ..utils import trace as _trace
         for li, layer in enumerate(self.layers):
+            if _trace.ENABLED:
+                # per-layer roctx marker (host-side: eager forwards / prefill)
+                with _trace.trace_range(f"layer{li + self.layer_offset}"):
+                    pass
             attn = layer.self_attn
             qp = attn.qkv_proj
             q = torch.empty(T, s.num_heads, s.head_dim, dtype=x.dtype, device=x.device)

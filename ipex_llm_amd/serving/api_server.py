@@ -166,6 +166,12 @@ def build_app(engine: LLMEngine, tokenizer, model_name: str = "ipex-llm-amd", lo
     async def health():
         return {"status": "ok", "running": int(engine.sched.num_running()), "waiting": int(engine.sched.num_waiting())}
 
+    @app.get("/metrics")
+    async def metrics():
+        from fastapi.responses import Response
+        from .metrics import CONTENT_TYPE_LATEST
+        return Response(engine.metrics.render(), media_type=CONTENT_TYPE_LATEST)
+
     @app.get("/v1/models")
     async def models():
         return {"object": "list", "data": [{"id": model_name, "object": "model", "owned_by": "ipex_llm_amd"}]}

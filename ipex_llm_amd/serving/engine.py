@@ -76,6 +76,9 @@ class LLMEngine:
         # padding rows of a captured decode step
         self.cache = model.make_cache(max_model_len, max_batch, block_size, kv_fp8, num_blocks=num_blocks + 1)
         self._scratch = num_blocks
+        self.num_blocks = num_blocks
+        from .metrics import EngineMetrics
+        self.metrics = EngineMetrics()
         self.use_graph = use_graph and model.device.type == "cuda" and ops.native_gpu(self.cache.k[0])
         self._graphs: Dict[tuple, dict] = {}
         model.ensure_rope_cache(max_model_len + 1)
@@ -103,6 +106,7 @@ class LLMEngine:
                         on_token=on_token, generator=g)
             self.requests[rid] = r
             self.sched.add(rid, len(prompt))
+        self.metrics.on_request(len(prompt))
         return rid
 
     def abort(self, rid: int):
@@ -117,6 +121,7 @@ class LLMEngine:
     # ------------------------------------------------------------ step
     def _finish(self, r: Request, reason: str):
         r.finished, r.finish_reason = True, reason
+        self.metrics.on_finish(reason, time.perf_counter() - r.arrival, len(r.generated), r.first_token_time)
         try:
             self.sched.finish(r.rid)
         except RuntimeError:
@@ -129,6 +134,7 @@ class LLMEngine:
         r.generated.append(tok)
         if r.first_token_time is None:
             r.first_token_time = time.perf_counter() - r.arrival
+            self.metrics.on_first_token(r.first_token_time)
         self.sched.grow(r.rid)
         if r.on_token is not None:
             r.on_token(tok, r)
@@ -212,6 +218,12 @@ class LLMEngine:
     def step(self) -> int:
         """One scheduler step: prefill admitted requests, decode all running
         ones.  Returns the number of tokens produced."""
+        from ..utils.trace import trace_range
+        with trace_range("engine_step"):
+            return self._step()
+
+    def _step(self) -> int:
+        t_step = time.perf_counter()
         with self.lock:
             plan = list(self.sched.schedule())
             i1 = plan.index(-1)
@@ -239,6 +251,7 @@ class LLMEngine:
                                       logits_idx=torch.tensor([n - 1], device=dev))
                 self.sched.advance(rid, n)
                 self.stats["prefill_tokens"] += n
+                self.metrics.on_prefill(n)
                 self._emit(r, self._pick(lg, r))
                 produced += 1
             if decode:
@@ -264,6 +277,10 @@ class LLMEngine:
                 produced += B
                 self.stats["decode_tokens"] += B
             self.stats["steps"] += 1
+            self.metrics.on_tokens(produced)
+            self.metrics.on_step(time.perf_counter() - t_step, int(self.sched.num_running()),
+                                 int(self.sched.num_waiting()),
+                                 1.0 - int(self.sched.num_free_blocks()) / max(1, self.num_blocks), len(preempted))
             return produced
 
     def generate(self, prompts: List[List[int]], params: Optional[SamplingParams] = None) -> List[List[int]]:

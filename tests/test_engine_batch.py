@@ -30,3 +30,24 @@ def test_prefill_batch_matches_sequential():
             kb1 = e1.cache.k[li][s1[b].blocks[0]]
             kb2 = e2.cache.k[li][s2[b].blocks[0]]
             assert torch.allclose(kb1[:, :n], kb2[:, :n], atol=1e-5)
+
+
+def test_trace_ranges_recorded_by_torch_profiler():
+    """IPEX_LLM_TRACE ranges (roctx + record_function) around prefill / decode
+    steps and per decoder layer show up in a torch.profiler trace (CPU run)"""
+    import torch
+    from transformers import LlamaConfig
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.utils import trace
+    cfg = LlamaConfig(vocab_size=128, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256)
+    m = random_native_model(cfg, "sym_int8", "cpu", torch.float32, seed=0)
+    trace.enable(True)
+    try:
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+            Engine(m).generate([[1, 2, 3, 4]], max_new_tokens=3, use_graph=False)
+    finally:
+        trace.enable(False)
+    names = {e.name for e in prof.events()}
+    assert "decode_step" in names and "prefill[4]" in names and "layer1" in names

@@ -113,6 +113,12 @@ def test_http_api(native):
                                                          "parameters": {"max_new_tokens": 3}}) as s:
             ev = [json.loads(l[6:]) for l in s.iter_lines() if l]
         assert ev[-1]["details"]["generated_tokens"] == 3
+        # Prometheus metrics: request / token counters, TTFT + TPOT histograms, KV usage
+        m = c.get("/metrics").text
+        assert "ipex_llm_requests_total" in m and "ipex_llm_time_to_first_token_seconds_bucket" in m
+        gen = [l for l in m.splitlines() if l.startswith("ipex_llm_generation_tokens_total")]
+        assert gen and float(gen[0].split()[-1]) >= 5 + 4 + 4 + 5 + 3
+        assert "ipex_llm_kv_cache_usage_ratio" in m and "ipex_llm_time_per_output_token_seconds_count" in m
 
 
 @pytest.mark.gpu
