@@ -43,8 +43,37 @@ def llama3_8b_config():
     )
 
 
+def llama3_70b_config():
+    cfg = llama3_8b_config()
+    cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers = 8192, 28672, 80
+    cfg.num_attention_heads, cfg.num_key_value_heads = 64, 8
+    return cfg
+
+
+def mixtral_8x7b_config():
+    from transformers import MixtralConfig
+    return MixtralConfig(vocab_size=32000, hidden_size=4096, intermediate_size=14336, num_hidden_layers=32,
+                         num_attention_heads=32, num_key_value_heads=8, num_local_experts=8, num_experts_per_tok=2,
+                         max_position_embeddings=32768, rms_norm_eps=1e-5, rope_theta=1e6, sliding_window=None)
+
+
+def qwen25_7b_config():
+    from transformers import Qwen2Config
+    return Qwen2Config(vocab_size=152064, hidden_size=3584, intermediate_size=18944, num_hidden_layers=28,
+                       num_attention_heads=28, num_key_value_heads=4, max_position_embeddings=32768,
+                       rms_norm_eps=1e-6, rope_theta=1000000.0, tie_word_embeddings=False)
+
+
+# --model: the headline is Llama-3-8B (BASELINE.json); the others are the
+# BASELINE configs' models measured on ONE MI355X (70B INT4 fits in 288 GB;
+# Mixtral runs the grouped MoE GEMV) and the reference's serving model
+MODELS = {"llama3-8b": ("Llama-3-8B", llama3_8b_config), "llama3-70b": ("Llama-3-70B", llama3_70b_config),
+          "mixtral-8x7b": ("Mixtral-8x7B", mixtral_8x7b_config), "qwen2.5-7b": ("Qwen2.5-7B", qwen25_7b_config)}
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b", choices=sorted(MODELS))
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=8)
@@ -69,7 +98,8 @@ def main():
     from ipex_llm_amd.engine.runner import Engine, DecodeStep
     from ipex_llm_amd.models.cache import SequenceState
 
-    cfg = llama3_8b_config()
+    mname, mcfg = MODELS[args.model]
+    cfg = mcfg()
     if args.layers:
         cfg.num_hidden_layers = args.layers
     t_build = time.perf_counter()
@@ -128,12 +158,12 @@ def main():
     value = B * world * args.steps / dt
     if rank == 0:
         out = {
-            "metric": "decode tokens/sec + first-token latency, Llama-3-8B INT4 at 1/2/4/8 MI355X",
+            "metric": f"decode tokens/sec + first-token latency, {mname} INT4 at 1/2/4/8 MI355X",
             "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": round(value / BASELINE_TOK_S, 2), "dtype": "bf16",
-            "data": "synthetic (random prompt ids, random-init weights of the Llama-3-8B architecture)",
-            "config": {"model": "Llama-3-8B", "qtype": args.qtype, "global_batch": B * world,
+            "scaling": "weak", "vs_baseline": round(value / BASELINE_TOK_S, 2) if args.model in ("llama3-8b", "qwen2.5-7b") else None, "dtype": "bf16",
+            "data": f"synthetic (random prompt ids, random-init weights of the {mname} architecture)",
+            "config": {"model": mname, "qtype": args.qtype, "global_batch": B * world,
                        "batch_per_gpu": B, "seq_len": P, "parallelism": f"dp{world}",
                        "hipgraph": not args.no_graph, "layers": cfg.num_hidden_layers},
             "first_token_latency_ms": round(ftl_ms, 2),

@@ -120,19 +120,22 @@ def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat
 
     nq, nkv = s.num_heads * s.head_dim, s.num_kv_heads * s.head_dim
     layers = []
-    for _ in range(s.num_layers):
+    for li in range(s.num_layers):
         wqkv = rnd(nq + 2 * nkv, s.hidden_size)
         bqkv = rnd(nq + 2 * nkv) if s.qkv_bias else None
         qkv = lowbit_from_dense(wqkv, qtype, device, bqkv)
         del wqkv
         o = lowbit_from_dense(rnd(s.hidden_size, nq), qtype, device)
-        gu = lowbit_from_dense(interleave_glu_rows(rnd(s.intermediate_size, s.hidden_size),
-                                                   rnd(s.intermediate_size, s.hidden_size)), qtype, device)
-        down = lowbit_from_dense(rnd(s.hidden_size, s.intermediate_size), qtype, device)
+        if s.is_moe_layer(li):
+            mlp = _random_moe(s, qtype, device, rnd)
+        else:
+            gu = lowbit_from_dense(interleave_glu_rows(rnd(s.intermediate_size, s.hidden_size),
+                                                       rnd(s.intermediate_size, s.hidden_size)), qtype, device)
+            down = lowbit_from_dense(rnd(s.hidden_size, s.intermediate_size), qtype, device)
+            mlp = NativeMLP(s, gu, down)
         attn = NativeAttention(s, qkv, o, ones_ish(s.head_dim) if s.qk_norm else None,
                                ones_ish(s.head_dim) if s.qk_norm else None, s.sliding_window)
-        layers.append(NativeLayer(s, attn, NativeMLP(s, gu, down), ones_ish(s.hidden_size),
-                                  ones_ish(s.hidden_size)))
+        layers.append(NativeLayer(s, attn, mlp, ones_ish(s.hidden_size), ones_ish(s.hidden_size)))
         torch.cuda.empty_cache() if torch.device(device).type == "cuda" else None
     embed = rnd(s.vocab_size, s.hidden_size)
     head_w = embed if s.tie_embeddings else rnd(s.vocab_size, s.hidden_size)
@@ -141,6 +144,28 @@ def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat
     s.rope_attention_scaling = att_scale
     model = NativeCausalLM(s, embed, layers, ones_ish(s.hidden_size), lm_head, inv_freq.to(device), dtype)
     return model.eval()
+
+
+@torch.no_grad()
+def _random_moe(s: DecoderSpec, qtype, device, rnd) -> nn.Module:
+    """random-init sparse MoE block (router, E experts quantized one by one on
+    the device, optional shared expert + gate) of ``s``'s geometry"""
+    from .moe import LowBitExperts, NativeMoE, SharedExpertMLP
+    E, I, H = s.num_experts, s.moe_intermediate, s.hidden_size
+    fmt = Q.get_format(qtype).fmt
+    gu = LowBitExperts(E, 2 * I, H, qtype, "meta")
+    dn = LowBitExperts(E, H, I, qtype, "meta")
+    gu.weight = nn.Parameter(torch.stack([ops.quantize(interleave_glu_rows(rnd(I, H), rnd(I, H)), fmt)
+                                          for _ in range(E)]), requires_grad=False)
+    dn.weight = nn.Parameter(torch.stack([ops.quantize(rnd(H, I), fmt) for _ in range(E)]), requires_grad=False)
+    shared, sgate = None, None
+    if s.shared_expert_intermediate:
+        Is = s.shared_expert_intermediate
+        shared = SharedExpertMLP(lowbit_from_dense(interleave_glu_rows(rnd(Is, H), rnd(Is, H)), qtype, device),
+                                 lowbit_from_dense(rnd(H, Is), qtype, device), s.act)
+        sgate = rnd(1, H)
+    renorm = s.norm_topk if s.model_type != "mixtral" else True
+    return NativeMoE(rnd(E, H, scale=0.5), gu, dn, s.top_k, renorm, s.act, shared, sgate, num_experts=E)
 
 
 def _module_weight(m: nn.Module):
