@@ -245,12 +245,21 @@ __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int 
 // VGPRs and the V stream overlaps the QK/softmax of the co-resident wave.
 // Chosen for grids larger than one wave per SIMD (measured on MI355X at
 // batch 8, 1088 waves: 2.564 -> 2.524 ms/step; ILLM_ATTN_LATEV=0/1 forces it)
-template <typename T, int D, int KVF, int RT, bool RQ = false, bool LATEV = false>
+//
+// PVM: P V on the matrix cores as O^T = V^T P^T (the prefill kernel's form):
+// the split's V tile is staged in LDS ([key][D], 16-B XOR swizzle) and read
+// back transposed by ds_read_b64_tr_b16 as the A operand; the B operand is the
+// lane's own softmax numerators (key order of the S^T C layout), so P never
+// leaves registers.  16 MFMAs per 64-key split (D = 128) instead of the
+// per-lane FMA loop and its 2 x RT x DPL cross-lane reductions.
+template <typename T, int D, int KVF, int RT, bool RQ = false, bool LATEV = false, bool PVM = false>
 __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs a) {
   constexpr int EB = KVF == 0 ? 2 : 1;
   constexpr int KSTEP = D / 32;       // MFMA k-steps over the head dim
   constexpr int DPL = D / 16;         // head dims per lane in P.V
   constexpr int VCH = DPL / 8 > 0 ? DPL / 8 : 1;  // 8-element fragments per key per lane
+  constexpr int VU = D / 8;           // PVM staging: 16-B chunks per key = chunks per lane
+  constexpr int KPJ = 64 / VU;        // keys per staging step (lane -> key lane / VU, chunk lane % VU)
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
   const int len = a.seq_lens[b];
@@ -260,7 +269,8 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   const int group = a.Hq / a.Hkv;
   const int R = group * a.Tq;
 
-  __shared__ float ps[SPLIT][RT];
+  __shared__ float ps[PVM ? 1 : SPLIT][RT];
+  __shared__ __attribute__((aligned(16))) uint16_t vl[PVM ? SPLIT * D : 8];
 
   // ---- fused RoPE (rq_part): q/k/v of the new token from the qkv accumulator,
   // rounded exactly like rope_kv_fused (GEMV output in T, cos/sin in T, each
@@ -305,9 +315,16 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     for (int s = 0; s < KSTEP; s++) kf[kt][s] = kv_frag8<T, KVF>(kb + ((size_t)kk * D + 32 * s + 8 * g) * EB);
   }
   const int dg = r16, kg = g;
-  uint4 vf[16][VCH];
+  uint4 vf[PVM ? 1 : 16][VCH];
+  uint4 vm[PVM ? VU : 1];
   auto load_v = [&]() {
-    if constexpr (DPL >= 8) {
+    if constexpr (PVM) {
+#pragma unroll
+      for (int j = 0; j < VU; j++) {
+        const int kk = min(j * KPJ + lane / VU, nk - 1);
+        vm[j] = kv_frag8<T, KVF>(vb + ((size_t)kk * D + 8 * (lane % VU)) * EB);
+      }
+    } else if constexpr (DPL >= 8) {
 #pragma unroll
       for (int i = 0; i < 16; i++) {
         const int kk = min(4 * i + kg, nk - 1);
@@ -409,7 +426,33 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
 #pragma unroll
         for (int s = 0; s < KSTEP; s++) *(uint4*)((uint16_t*)a.k_cache + crow + 32 * s + 8 * g) = kq[s];
       }
-      if constexpr (DPL >= 8) {
+      if constexpr (PVM) {
+        if (lane / VU == kn % KPJ) {
+          const int d0 = 8 * (lane % VU);
+          const float4* p = (const float4*)(a.rq_part + (size_t)b * a.rq_ld + colv + d0);
+          const float4 f0 = p[0], f1 = p[1];
+          const float f[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+          float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          if (a.rq_bias) {
+            const uint4 u = *(const uint4*)(a.rq_bias + colv + d0);
+            const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              bb[2 * e] = to_f32<T>((uint16_t)(w[e] & 0xffff));
+              bb[2 * e + 1] = to_f32<T>((uint16_t)(w[e] >> 16));
+            }
+          }
+          uint32_t w[4];
+#pragma unroll
+          for (int e = 0; e < 4; e++) w[e] = pack2<T>(rnd(bb[2 * e] + f[2 * e]), rnd(bb[2 * e + 1] + f[2 * e + 1]));
+          const uint4 vq = make_uint4(w[0], w[1], w[2], w[3]);
+          vnew[0] = vq;
+#pragma unroll
+          for (int j = 0; j < VU; j++)
+            if (j == kn / KPJ) vm[j] = vq;
+          *(uint4*)((uint16_t*)a.v_cache + crow + d0) = vq;
+        }
+      } else if constexpr (DPL >= 8) {
         if (kg == (kn & 3)) {
 #pragma unroll
           for (int c = 0; c < VCH; c++) {
@@ -466,7 +509,13 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
       // the cache row of the new value was written by this wave above: take it
       // from registers, not from a load that may race the store
       const int kn = nk - 1;
-      if (has_new && kg == (kn & 3)) {
+      if constexpr (PVM) {
+        if (has_new && lane / VU == kn % KPJ) {
+#pragma unroll
+          for (int j = 0; j < VU; j++)
+            if (j == kn / KPJ) vm[j] = vnew[0];
+        }
+      } else if (has_new && kg == (kn & 3)) {
 #pragma unroll
         for (int c = 0; c < VCH; c++)
 #pragma unroll
@@ -500,6 +549,59 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   m = fmaxf(m, __shfl_xor(m, 16, 64));
   m = fmaxf(m, __shfl_xor(m, 32, 64));
   float l = 0.f;
+  const float vs = KVF ? a.v_scale : 1.f;
+  const bool handoff = a.counters != nullptr;
+  if constexpr (PVM) {
+    // P^T fragments (16-bit pairs, key order 16 kt + 4 g + i) and the V tile in LDS
+    uint32_t pk[4][2];
+#pragma unroll
+    for (int kt = 0; kt < 4; kt++) {
+      float p[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        p[i] = m == -INFINITY ? 0.f : __expf(st[kt][i] - m);
+        l += p[i];
+      }
+      pk[kt][0] = pack2<T>(p[0], p[1]);
+      pk[kt][1] = pack2<T>(p[2], p[3]);
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+#pragma unroll
+    for (int j = 0; j < VU; j++) *(uint4*)(vl + pf_off<D>(j * KPJ + lane / VU, lane % VU)) = vm[j];
+    __syncthreads();
+    constexpr int DT = D / 16;
+    f32x4 o[DT];
+#pragma unroll
+    for (int d = 0; d < DT; d++) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int qq = r16 >> 2, pp = r16 & 3;
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+      const int row0 = 32 * kk + 4 * g + qq, row1 = row0 + 16;
+      const uint4 pb = make_uint4(pk[2 * kk][0], pk[2 * kk][1], pk[2 * kk + 1][0], pk[2 * kk + 1][1]);
+#pragma unroll
+      for (int d = 0; d < DT; d++) {
+        const int col = 16 * d + 4 * pp;
+        const uint2 v0 = ds_read_tr16(vl + pf_off<D>(row0, col >> 3) + (col & 7));
+        const uint2 v1 = ds_read_tr16(vl + pf_off<D>(row1, col >> 3) + (col & 7));
+        o[d] = mfma16<T>(make_uint4(v0.x, v0.y, v1.x, v1.y), pb, o[d]);
+      }
+    }
+    // lane holds O^T[16 d + 4 g + i][row r16]
+    if (row < R) {
+      const size_t prow = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit + split;
+      float* po = a.part_o + prow * D + 4 * g;
+#pragma unroll
+      for (int d = 0; d < DT; d++) {
+        if (handoff) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) st_sc1(po + 16 * d + i, o[d][i] * vs);
+        } else {
+          *(float4*)(po + 16 * d) = make_float4(o[d][0] * vs, o[d][1] * vs, o[d][2] * vs, o[d][3] * vs);
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int kt = 0; kt < 4; kt++) {
 #pragma unroll
@@ -554,8 +656,6 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
       x += __shfl_xor(x, 32, 64);
       o[r][d] = x;
     }
-  const float vs = KVF ? a.v_scale : 1.f;
-  const bool handoff = a.counters != nullptr;
   if (kg == 0) {
 #pragma unroll
     for (int r = 0; r < RT; r++) {
@@ -573,6 +673,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
         }
       }
     }
+  }
   }
   if (g == 0 && row < R) {
     const size_t prow = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit + split;
@@ -601,7 +702,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   }
   __syncthreads();
   if (!is_last) return;
-  float* wsh = &ps[0][0];        // SPLIT * RT floats of LDS, reused
+  float* wsh = PVM ? (float*)vl : &ps[0][0];        // LDS scratch of the split, reused
   for (int r = 0; r < R; r++) combine_row<T, true>(a, b, kvh * group + r % group, r / group, wsh);
   if constexpr (rq) {
     // fused-RoPE decode: every split of this (b, kv head) has read its q / k / v
@@ -722,7 +823,7 @@ __global__ void __launch_bounds__(64) attn_combine_kernel(const AttnDecodeArgs a
   }
 }
 
-template <typename T, int D, int RT>
+template <typename T, int D, int RT, bool PVM = false>
 static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
   AttnDecodeArgs a = a0;
   // combine fused into the split kernel when the merge fits its LDS scratch
@@ -739,21 +840,21 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
   const bool latev = latev_env >= 0 ? latev_env == 1 : (long)a.nsplit * a.Hkv * a.B > simds;
   if constexpr (D / 16 >= 8) {
     if (a.rq_part != nullptr) {
-      if (latev) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, true>), grid, dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true>), grid, dim3(64), 0, st, a);
+      if (latev) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, true, PVM>), grid, dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, false, PVM>), grid, dim3(64), 0, st, a);
       if (a.counters == nullptr && !a.no_combine)
         hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
       return;
     }
   }
   if (latev) {
-    if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT, false, true>), grid, dim3(64), 0, st, a);
-    else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT, false, true>), grid, dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, false, true>), grid, dim3(64), 0, st, a);
+    if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT, false, true, PVM>), grid, dim3(64), 0, st, a);
+    else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT, false, true, PVM>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, false, true, PVM>), grid, dim3(64), 0, st, a);
   } else {
-    if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT>), grid, dim3(64), 0, st, a);
-    else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT>), grid, dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT>), grid, dim3(64), 0, st, a);
+    if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 1, RT, false, false, PVM>), grid, dim3(64), 0, st, a);
+    else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 2, RT, false, false, PVM>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, false, false, PVM>), grid, dim3(64), 0, st, a);
   }
   if (a.counters == nullptr && !a.no_combine)
     hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
@@ -762,6 +863,11 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
 template <typename T, int D>
 static void launch_d(const AttnDecodeArgs& a, hipStream_t st) {
   const int R = (a.Hq / a.Hkv) * a.Tq;
+  // P V on MFMA (ILLM_ATTN_PVM=0 keeps the per-lane FMA form, for A/B runs)
+  static const bool pvm = getenv("ILLM_ATTN_PVM") ? atoi(getenv("ILLM_ATTN_PVM")) != 0 : true;
+  if constexpr (D == 64 || D == 128) {
+    if (pvm && R <= 16) return launch_v2<T, D, 16, true>(a, st);
+  }
   if constexpr (D == 64 || D == 128 || D == 256) {
     if (R <= 4) return launch_v2<T, D, 4>(a, st);
     if (R <= 8) return launch_v2<T, D, 8>(a, st);

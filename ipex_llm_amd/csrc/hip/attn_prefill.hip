@@ -35,15 +35,6 @@ namespace illm {
 constexpr int PF_KT = 64;      // keys per tile
 constexpr int PF_QB = 64;      // query rows per workgroup
 
-// 16-byte chunk c of key row r lives at chunk c ^ (r & 15) (D >= 128: 16
-// chunks per row, D = 64: 8 chunks -> r & 7)
-template <int D>
-__device__ __forceinline__ int pf_off(int r, int c) {
-  constexpr int CH = D / 8;            // 16-B chunks per row
-  constexpr int MSK = CH >= 16 ? 15 : CH - 1;
-  return r * D + ((c ^ (r & MSK)) * 8);
-}
-
 template <typename T, int KVF>
 __device__ __forceinline__ uint4 pf_load8(const uint8_t* p, float scale) {
   if constexpr (KVF == 0) {
@@ -63,12 +54,6 @@ __device__ __forceinline__ uint4 pf_load8(const uint8_t* p, float scale) {
     }
     return make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
   }
-}
-
-__device__ __forceinline__ uint2 ds_read_tr16(const uint16_t* p) {
-  typedef short s4 __attribute__((ext_vector_type(4)));
-  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)p);
-  return __builtin_bit_cast(uint2, v);
 }
 
 // HP = query heads per wave that share one kv head (GQA): every K fragment

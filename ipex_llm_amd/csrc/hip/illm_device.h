@@ -64,6 +64,24 @@ __device__ __forceinline__ f32x4 mfma16<F16>(const uint4& a, const uint4& b, f32
                                                 __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
 }
 
+// [row][D] 16-bit tile in LDS with a 16-byte XOR swizzle: chunk c of row r
+// lives at chunk c ^ (r & 15) (D >= 128: 16 chunks per row; D = 64: r & 7),
+// so both row-wise b128 reads and the transposed reads below are conflict-free
+template <int D>
+__device__ __forceinline__ int pf_off(int r, int c) {
+  constexpr int CH = D / 8;            // 16-B chunks per row
+  constexpr int MSK = CH >= 16 ? 15 : CH - 1;
+  return r * D + ((c ^ (r & MSK)) * 8);
+}
+
+// gfx950 ds_read_b64_tr_b16: transposed read of a 16-bit tile (the MFMA A/B
+// fragment of a row-major [k][n] tile read along k)
+__device__ __forceinline__ uint2 ds_read_tr16(const uint16_t* p) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)p);
+  return __builtin_bit_cast(uint2, v);
+}
+
 // wave-level reductions (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -15,6 +15,10 @@ from tools.bench_kernels import timeit  # noqa: E402
 
 SHAPES = [("qkv", 6144, 4096, "part"), ("o", 4096, 4096, "part"), ("glu", 28672, 4096, "glu"),
           ("down", 4096, 14336, "part"), ("lm_head", 128256, 4096, "store")]
+# GEMV_SHAPES=70b: Llama-3-70B projections, the non-GLU ones on the atomic
+# accumulator path the decoder uses (ops.gemv_accum)
+SHAPES_70B = [("qkv", 10240, 8192, "acc"), ("o", 8192, 8192, "acc"), ("glu", 57344, 8192, "glu"),
+              ("down", 8192, 28672, "acc"), ("lm_head", 128256, 8192, "store")]
 
 
 def main():
@@ -23,14 +27,17 @@ def main():
     ops.require()
     f = get_format("sym_int4").fmt
     dev = torch.device("cuda")
-    tag = {"kw": os.environ.get("ILLM_GEMV5_KW", "auto"), "ks": os.environ.get("ILLM_GEMV5_KS", "auto")}
-    for name, n, k, kind in SHAPES:
+    tag = {"kw": os.environ.get("ILLM_GEMV5_KW", "auto"), "ks": os.environ.get("ILLM_GEMV5_KS", "auto"),
+           "nw": os.environ.get("ILLM_GEMV5_NW", "auto")}
+    shapes = SHAPES_70B if os.environ.get("GEMV_SHAPES") == "70b" else SHAPES
+    for name, n, k, kind in shapes:
         if only and name not in only:
             continue
         copies = max(1, int(math.ceil(600e6 / (n * k * 0.5))))
         blobs = [ops.quantize(torch.randn(n, k, device=dev, dtype=torch.bfloat16) * 0.02, f) for _ in range(copies)]
         for M in ms:
             x = torch.randn(M, k, device=dev, dtype=torch.bfloat16)
+            acc = torch.zeros(M, n, device=dev, dtype=torch.float32)
             i = [0]
 
             def run():
@@ -38,6 +45,8 @@ def main():
                 b = blobs[i[0]]
                 if kind == "glu":
                     return ops.gemv_glu(x, b, f, n, k, 0)
+                if kind == "acc":
+                    return ops.gemv_accum(x, b, f, n, k, acc)
                 if kind == "part":
                     return ops.gemv_partials(x, b, f, n, k, 0)
                 return ops.lowbit_matmul(x, b, f, n, k)
