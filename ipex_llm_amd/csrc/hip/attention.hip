@@ -24,18 +24,6 @@ namespace illm {
 constexpr int SPLIT = 64;
 constexpr int RMAX = 16;
 
-// write-through (sc1) stores / L1-bypassing (sc1) loads of the split
-// partials handed to the last-arriving split of a (batch, kv head): the
-// MI355X hand-off form "sc1 stores, s_waitcnt vmcnt(0), one agent-scope
-// atomic add per workgroup, sc1 loads by the workgroup whose add came last"
-// (no __threadfence / L2 write-back on the critical path)
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <typename T, int KVF>
 __device__ __forceinline__ void kv_load8(const uint8_t* p, float scale, float* v) {
   if constexpr (KVF == 0) {

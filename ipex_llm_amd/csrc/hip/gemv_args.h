@@ -60,6 +60,10 @@ struct GemvArgs {
   const int32_t* moe_off;  // [E + 1] pair offsets per expert
   const int32_t* moe_rows; // [P] pair ids sorted by expert
   int moe_xdiv;            // x row of pair p = p / moe_xdiv
+  // grouped EPI_ATOMIC: pair p adds moe_w[p] * y into output row p / moe_odiv
+  // (the routing-weighted combine of the down projection; null = row p)
+  const float* moe_w;
+  int moe_odiv;
   int64_t w_stride;        // bytes between experts' weight blobs
   int waves;               // v4: waves per workgroup (4 or 8; 0 = 4)
   int cpk;                 // v4: chunks per split-K slice (multiple of 4 enables quad scale loads; 0 = derive)

@@ -82,6 +82,18 @@ __device__ __forceinline__ uint2 ds_read_tr16(const uint16_t* p) {
   return __builtin_bit_cast(uint2, v);
 }
 
+// write-through (sc1) stores / L1-bypassing (sc1) loads of data handed to
+// the last-arriving workgroup of a launch: the MI355X hand-off form "sc1
+// stores, s_waitcnt vmcnt(0), one agent-scope atomic add per workgroup, sc1
+// loads by the workgroup whose add came last" (no __threadfence / L2
+// write-back on the critical path)
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // wave-level reductions (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

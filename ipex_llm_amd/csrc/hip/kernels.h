@@ -160,6 +160,20 @@ void launch_moe_group_topk(const float* logits, const float* bias, int T, int E,
                            int renorm, float scale, float* topk_w, int32_t* topk_ids, hipStream_t st);
 
 void launch_moe_align(const int32_t* ids, int P, int e0, int El, int32_t* off, int32_t* rows, hipStream_t st);
+
+// fused decode router: logits, top-k and per-expert pair lists in one launch
+struct MoeRouteArgs {
+  const uint16_t* x;      // [T, H] activations
+  const uint16_t* wr;     // [E, H] router weight (same 16-bit type)
+  int T, H, E, k, renorm, scoring, e0, El;
+  float* logits;          // [T, E] f32 scratch
+  int* counter;           // zero on entry, left zero (last workgroup resets it)
+  float* topk_w;          // [T, k]
+  int32_t* topk_ids;      // [T, k]
+  int32_t* off;           // [El + 1]
+  int32_t* rows;          // [T * k]
+};
+void launch_moe_route(bool bf16, const MoeRouteArgs& a, hipStream_t st);
 void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float* w, const int32_t* ids, int k,
                         int e0, int El, uint16_t* out, int Tn, int H, hipStream_t st);
 

@@ -594,7 +594,16 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
       if (tile0 + t >= NT || n0 >= a.N) continue;
       float o[4] = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
       if constexpr (EPI == EPI_ATOMIC) {
-        float* ws = (float*)a.out + (size_t)m * a.N + n0;
+        int orow = m;
+        if constexpr (MOE) {
+          if (a.moe_w) {            // routing-weighted combine straight into the token's row
+            const float rw = a.moe_w[m];
+#pragma unroll
+            for (int i = 0; i < 4; i++) o[i] *= rw;
+            orow = m / a.moe_odiv;
+          }
+        }
+        float* ws = (float*)a.out + (size_t)orow * a.N + n0;
 #pragma unroll
         for (int i = 0; i < 4; i++)
           if (n0 + i < a.N) __hip_atomic_fetch_add(ws + i, o[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

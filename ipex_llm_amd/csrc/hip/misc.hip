@@ -224,18 +224,20 @@ void launch_reduce_partials(bool bf16, const float* ws, int nsplit, const uint16
 }
 
 // ---- MoE router: softmax / sigmoid + top-k (+renormalise) --------------------
-// one wave per token, E <= 512
-__global__ void __launch_bounds__(64) moe_topk_kernel(const float* logits, int T, int E, int k,
-                                                      int renorm, int scoring, float* topk_w,
-                                                      int32_t* topk_ids) {
-  const int t = blockIdx.x, lane = threadIdx.x;
+// one wave per token row, E <= 512.  SC1: the logits were handed over by other
+// workgroups of the same launch (sc1 loads).  ids_lds (optional) receives the
+// chosen ids for a following in-workgroup align.
+template <bool SC1>
+__device__ __forceinline__ void topk_row(const float* lrow, int E, int k, int renorm, int scoring, float* w_out,
+                                         int32_t* id_out, int* ids_lds) {
+  const int lane = threadIdx.x & 63;
   constexpr int PER = 8;
   float v[PER];
   float mx = -INFINITY;
 #pragma unroll
   for (int j = 0; j < PER; j++) {
     const int e = lane + 64 * j;
-    v[j] = e < E ? logits[(size_t)t * E + e] : -INFINITY;
+    v[j] = e < E ? (SC1 ? ld_sc1(lrow + e) : lrow[e]) : -INFINITY;
     mx = fmaxf(mx, v[j]);
   }
   if (scoring == 0) {
@@ -254,6 +256,7 @@ __global__ void __launch_bounds__(64) moe_topk_kernel(const float* logits, int T
     for (int j = 0; j < PER; j++) v[j] = (lane + 64 * j) < E ? 1.f / (1.f + __expf(-v[j])) : -1.f;
   }
   float tot = 0.f;
+  float wsel = 0.f;                // lane i keeps the i-th chosen weight
   for (int i = 0; i < k; i++) {
     float best = -INFINITY;
     int bi = 0x7fffffff;
@@ -271,15 +274,118 @@ __global__ void __launch_bounds__(64) moe_topk_kernel(const float* logits, int T
 #pragma unroll
     for (int j = 0; j < PER; j++)
       if (lane + 64 * j == bi) v[j] = -INFINITY;
-    if (lane == 0) {
-      topk_w[(size_t)t * k + i] = best;
-      topk_ids[(size_t)t * k + i] = bi;
+    if (lane == i) {
+      wsel = best;
+      id_out[i] = bi;
+      if (ids_lds) ids_lds[i] = bi;
     }
     tot += best;
   }
-  if (renorm && lane == 0) {
-    for (int i = 0; i < k; i++) topk_w[(size_t)t * k + i] /= tot;
+  if (lane < k) w_out[lane] = renorm ? wsel / tot : wsel;
+}
+
+__global__ void __launch_bounds__(64) moe_topk_kernel(const float* logits, int T, int E, int k,
+                                                      int renorm, int scoring, float* topk_w,
+                                                      int32_t* topk_ids) {
+  const int t = blockIdx.x;
+  topk_row<false>(logits + (size_t)t * E, E, k, renorm, scoring, topk_w + (size_t)t * k, topk_ids + (size_t)t * k,
+                  nullptr);
+}
+
+// ---- fused decode router (T <= 16 tokens): logits = x Wr^T in f32, softmax /
+// sigmoid top-k (+renormalise) and the per-expert pair lists of moe_align in
+// ONE launch.  Workgroup = 4 waves, wave = one expert over all T tokens (the
+// router row is read once, x rows from L2); the last workgroup to finish
+// (agent-scope counter, sc1 hand-off) runs top-k per token and the align.
+// Replaces router GEMM + f32 cast + moe_topk + moe_align (4 launches).
+template <typename T>
+__global__ void __launch_bounds__(256) moe_route_kernel(const MoeRouteArgs a) {
+  constexpr int TM = 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int e = blockIdx.x * 4 + wave;
+  if (e < a.E) {
+    float acc[TM];
+#pragma unroll
+    for (int t = 0; t < TM; t++) acc[t] = 0.f;
+    const uint16_t* wrow = a.wr + (size_t)e * a.H;
+    for (int c = lane; c < a.H / 8; c += 64) {
+      const uint4 wv = *(const uint4*)(wrow + 8 * c);
+      const uint32_t ww[4] = {wv.x, wv.y, wv.z, wv.w};
+      float wf[8];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        wf[2 * i] = to_f32<T>((uint16_t)(ww[i] & 0xffff));
+        wf[2 * i + 1] = to_f32<T>((uint16_t)(ww[i] >> 16));
+      }
+#pragma unroll
+      for (int t = 0; t < TM; t++) {
+        if (t < a.T) {
+          const uint4 xv = *(const uint4*)(a.x + (size_t)t * a.H + 8 * c);
+          const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            acc[t] = __builtin_fmaf(wf[2 * i], to_f32<T>((uint16_t)(xw[i] & 0xffff)), acc[t]);
+            acc[t] = __builtin_fmaf(wf[2 * i + 1], to_f32<T>((uint16_t)(xw[i] >> 16)), acc[t]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TM; t++) {
+      if (t < a.T) {
+        const float v = wave_sum(acc[t]);
+        if (lane == 0) st_sc1(a.logits + (size_t)t * a.E + e, v);
+      }
+    }
   }
+  __shared__ int is_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's sc1 stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = prev == (int)gridDim.x - 1;
+    if (is_last) __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!is_last) return;
+
+  // ---- last workgroup: top-k per token, then the per-local-expert pair lists
+  __shared__ int ids_l[16 * 16];
+  __shared__ int cnt[512], start[512];
+  for (int t = wave; t < a.T; t += 4)
+    topk_row<true>(a.logits + (size_t)t * a.E, a.E, a.k, a.renorm, a.scoring, a.topk_w + (size_t)t * a.k,
+                   a.topk_ids + (size_t)t * a.k, ids_l + t * a.k);
+  for (int i = threadIdx.x; i < a.El; i += 256) cnt[i] = 0;
+  __syncthreads();
+  const int P = a.T * a.k;
+  for (int p = threadIdx.x; p < P; p += 256) {
+    const int el = ids_l[p] - a.e0;
+    if (el >= 0 && el < a.El) atomicAdd(&cnt[el], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < a.El; i++) {
+      start[i] = acc;
+      a.off[i] = acc;
+      acc += cnt[i];
+    }
+    a.off[a.El] = acc;
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < P; p += 256) {
+    const int id = ids_l[p], el = id - a.e0;
+    if (el < 0 || el >= a.El) continue;
+    int r = 0;
+    for (int q = 0; q < p; q++) r += ids_l[q] == id;
+    a.rows[start[el] + r] = p;
+  }
+}
+
+void launch_moe_route(bool bf16, const MoeRouteArgs& a, hipStream_t st) {
+  const dim3 grid((unsigned)((a.E + 3) / 4));
+  if (bf16) hipLaunchKernelGGL(moe_route_kernel<BF16>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(moe_route_kernel<F16>, grid, dim3(256), 0, st, a);
 }
 
 // ---- DeepSeek-V3 group-limited router (noaux_tc): sigmoid scores, + the

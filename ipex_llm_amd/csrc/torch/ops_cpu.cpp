@@ -154,6 +154,8 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("embedding_lowbit(Tensor blob, int fmt, int n, int k, Tensor ids, ScalarType dtype) -> Tensor");
   m.def("moe_gemv(Tensor x, Tensor blob, int fmt, int n, int k, Tensor off, Tensor rows, int xdiv, int npairs, int epi, int ksplit, int act) -> Tensor");
   m.def("moe_combine(Tensor part, Tensor w, Tensor ids, int e0, int num_local, ScalarType dtype) -> Tensor");
+  m.def("moe_gemv_accum(Tensor x, Tensor blob, int fmt, int n, int k, Tensor off, Tensor rows, Tensor(a!) acc, Tensor w, int topk, int ksplit) -> ()");
+  m.def("moe_route(Tensor x, Tensor router, int k, bool renorm, int scoring, int e0, int num_local, Tensor(a!) counter) -> (Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {

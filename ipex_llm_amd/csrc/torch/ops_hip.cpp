@@ -910,7 +910,7 @@ std::tuple<Tensor, Tensor> moe_topk(const Tensor& logits, int64_t k, bool renorm
   c10::DeviceGuard g(logits.device());
   Tensor l = logits.to(at::kFloat).contiguous();
   const int64_t E = l.size(-1), T = l.numel() / E;
-  TORCH_CHECK(E <= 512 && k <= E, "moe_topk: E <= 512");
+  TORCH_CHECK(E <= 512 && k <= E && k <= 64, "moe_topk: E <= 512, k <= 64");
   Tensor w = at::empty({T, k}, l.options());
   Tensor ids = at::empty({T, k}, l.options().dtype(at::kInt));
   if (T > 0) illm::launch_moe_topk(l.data_ptr<float>(), (int)T, (int)E, (int)k, renorm, (int)scoring,
@@ -987,6 +987,91 @@ Tensor moe_gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   return ws;
 }
 
+// grouped down projection over expert pairs with the routing-weighted combine
+// in the epilogue: acc[p / topk, :] += w[p] * (x[p] @ W_e^T) by f32 atomics
+// (acc zero on entry; its consumer, add_rms_norm, reads and re-zeroes it)
+void moe_gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, const Tensor& off,
+                    const Tensor& rows, const Tensor& acc, const Tensor& w, int64_t topk, int64_t ksplit) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda() && blob.dim() == 2, "moe_gemv_accum: GPU x and [E, bytes] blob");
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  TORCH_CHECK(xc.dim() == 2 && xc.size(1) == k, "moe_gemv_accum: x must be [pairs, k]");
+  const int64_t P = xc.size(0);
+  TORCH_CHECK(topk >= 1 && P % topk == 0, "moe_gemv_accum: pairs must be tokens * topk");
+  TORCH_CHECK(acc.scalar_type() == at::kFloat && acc.is_contiguous() && acc.numel() == (P / topk) * n,
+              "moe_gemv_accum: acc must be contiguous f32 [tokens, n]");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == P,
+              "moe_gemv_accum: w must be contiguous f32 [tokens, topk]");
+  TORCH_CHECK(blob.size(1) >= illm::dev_total_bytes((int)fmt, n, k), "moe_gemv_accum: expert blob too small");
+  const int64_t E = blob.size(0);
+  TORCH_CHECK(off.numel() == E + 1 && off.scalar_type() == at::kInt && rows.scalar_type() == at::kInt,
+              "moe_gemv_accum: off int32 [E+1], rows int32");
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  const int64_t Mmax = std::min<int64_t>(16, P);
+  illm::GemvArgs a{};
+  a.x = p16(xc);
+  a.M = (int)P;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.KC = (int)KC;
+  a.lut_fmt = (int)fmt;
+  a.moe_off = off.data_ptr<int32_t>();
+  a.moe_rows = rows.data_ptr<int32_t>();
+  a.moe_xdiv = 1;
+  a.moe_w = w.data_ptr<float>();
+  a.moe_odiv = (int)topk;
+  a.w_stride = blob.size(1);
+  a.N = (int)n;
+  a.out = acc.data_ptr();
+  a.ldo = (int)n;
+  const Plan5 p = plan5(Mmax, NT, KC, true, ksplit, true);
+  a.cpk = (int)p.cpk;
+  a.nw = p.nw;
+  TORCH_CHECK(p.shmem <= kMaxLds, "moe_gemv_accum: K slice too large for LDS");
+  launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_ATOMIC, dim3(p.gx, (unsigned)p.ks, (unsigned)E), p.shmem, a);
+}
+
+// fused decode router (<= 16 tokens): logits, top-k and pair lists in one launch
+std::tuple<Tensor, Tensor, Tensor, Tensor> moe_route(const Tensor& x, const Tensor& wr, int64_t k, bool renorm,
+                                                     int64_t scoring, int64_t e0, int64_t num_local,
+                                                     const Tensor& counter) {
+  TORCH_CHECK(x.is_cuda() && wr.is_cuda() && counter.is_cuda(), "moe_route: GPU tensors expected");
+  c10::DeviceGuard g(x.device());
+  Tensor xc = x.contiguous(), wc = wr.contiguous();
+  TORCH_CHECK(xc.dim() == 2 && wc.dim() == 2 && xc.size(1) == wc.size(1), "moe_route: x [T, H], router [E, H]");
+  TORCH_CHECK(xc.scalar_type() == wc.scalar_type() && (is_bf16(xc) || xc.scalar_type() == at::kHalf),
+              "moe_route: x and router must share one 16-bit dtype");
+  const int64_t T = xc.size(0), H = xc.size(1), E = wc.size(0);
+  TORCH_CHECK(T >= 1 && T <= 16, "moe_route: 1..16 tokens");
+  TORCH_CHECK(H % 8 == 0, "moe_route: hidden % 8");
+  TORCH_CHECK(E <= 512 && k >= 1 && k <= 16 && k <= E, "moe_route: E <= 512, 1 <= k <= 16");
+  TORCH_CHECK(num_local >= 1 && num_local <= 512 && e0 >= 0, "moe_route: 1..512 local experts");
+  TORCH_CHECK(counter.scalar_type() == at::kInt && counter.numel() >= 1, "moe_route: int32 counter");
+  auto f32 = xc.options().dtype(at::kFloat);
+  auto i32 = xc.options().dtype(at::kInt);
+  Tensor logits = at::empty({T, E}, f32);
+  Tensor w = at::empty({T, k}, f32);
+  Tensor ids = at::empty({T, k}, i32);
+  Tensor off = at::empty({num_local + 1}, i32);
+  Tensor rows = at::empty({T * k}, i32);
+  illm::MoeRouteArgs a{};
+  a.x = p16(xc);
+  a.wr = p16(wc);
+  a.T = (int)T; a.H = (int)H; a.E = (int)E; a.k = (int)k;
+  a.renorm = renorm ? 1 : 0; a.scoring = (int)scoring; a.e0 = (int)e0; a.El = (int)num_local;
+  a.logits = logits.data_ptr<float>();
+  a.counter = counter.data_ptr<int32_t>();
+  a.topk_w = w.data_ptr<float>();
+  a.topk_ids = ids.data_ptr<int32_t>();
+  a.off = off.data_ptr<int32_t>();
+  a.rows = rows.data_ptr<int32_t>();
+  illm::launch_moe_route(is_bf16(xc), a, cur_stream());
+  return {w, ids, off, rows};
+}
+
 Tensor moe_combine(const Tensor& part, const Tensor& w, const Tensor& ids, int64_t e0, int64_t num_local,
                    at::ScalarType dt) {
   c10::DeviceGuard g(part.device());
@@ -1054,6 +1139,8 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemv", &moe_gemv);
   m.impl("moe_combine", &moe_combine);
+  m.impl("moe_gemv_accum", &moe_gemv_accum);
+  m.impl("moe_route", &moe_route);
   m.impl("quantize_device", &quantize_device);
   m.impl("dequantize_device", &dequantize_device);
   m.impl("gemv", &gemv);

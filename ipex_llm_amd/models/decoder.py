@@ -588,6 +588,16 @@ class NativeCausalLM(nn.Module):
                 pd = ops.gemv_glu_in(pg, dn.weight, dn.fmt, dn.out_features, dn.in_features, s.act, 0, x.dtype)
                 x, _ = ops.add_rms_norm(None, residual, nxt, s.rms_eps, partials=pd, unit_offset=s.norm_unit_offset)
                 continue
+            mlp = layer.mlp
+            if type(mlp).__name__ == "NativeMoE" and layer.post_feedforward_layernorm is None \
+                    and self.tp_group is None and x.shape[0] <= 16 and mlp.acc_ok(x):
+                # MoE decode: routed experts (and a shared expert) add into the
+                # norm's f32 slab; no combine launch, no [T, H] bf16 round trip
+                acc = self._acc(s.hidden_size, x.shape[0], x.device)
+                mlp.forward_acc(x, acc)
+                x, _ = ops.add_rms_norm(None, residual, nxt, s.rms_eps, partials=acc.unsqueeze(0),
+                                        unit_offset=s.norm_unit_offset, zero_partials=True)
+                continue
             act = self._mlp(x, layer.mlp)
             if isinstance(layer.mlp, NativeMLP):
                 x = self._proj_residual_norm(act, layer.mlp.down_proj, residual, nxt,

@@ -11,12 +11,14 @@ MI355X design:
   * one projection of all E experts is ONE uint8 parameter [E, bytes]
     (:class:`LowBitExperts`), tiled for the MFMA GEMV on the GPU and in the
     portable canonical layout on the host / in checkpoints;
-  * decode (<= 16 tokens): router GEMV -> ``moe_topk`` -> ``moe_align``
-    (device-side pair lists per expert) -> grouped GLU GEMV over experts
-    (blockIdx.z = expert, all tokens routed to an expert share one weight
-    stream) -> grouped down GEMV into f32 split-K slabs -> ``moe_combine``
-    (routing weights applied in the reduction).  Five launches for the whole
-    block, no host sync, hipGraph-capturable;
+  * decode (<= 16 tokens): ``moe_route`` (router GEMV, top-k and the
+    device-side per-expert pair lists in ONE launch) -> grouped GLU GEMV over
+    experts (blockIdx.z = expert, all tokens routed to an expert share one
+    weight stream) -> grouped down GEMV whose epilogue applies the routing
+    weight and adds into the token's f32 row by atomics, read (and
+    re-zeroed) by the next residual-add + RMSNorm (:meth:`NativeMoE.forward_acc`,
+    three launches per block).  Standalone forwards end with ``moe_combine``
+    over split-K slabs instead.  No host sync, hipGraph-capturable;
   * prefill / CPU: tokens grouped per expert and run as low-bit GEMMs;
   * expert parallel: rank r owns experts [e0, e0 + El); routing is computed
     everywhere, every rank runs its local experts over all tokens and the
@@ -161,10 +163,60 @@ class NativeMoE(nn.Module):
         logits = F.linear(x, self.router.to(x.dtype))
         return ops.moe_topk(logits.float(), self.top_k, self.renorm, 0)
 
-    def _experts_grouped(self, x, w, ids):
-        """decode: five device-side launches, no host sync"""
+    def _router_w(self, dtype):
+        r = self.__dict__.get("_router_cast")
+        if r is None or r.dtype != dtype or r.device != self.router.device:
+            r = self.router.detach().to(dtype).contiguous()
+            self.__dict__["_router_cast"] = r
+        return r
+
+    def _route_counter(self, device):
+        c = self.__dict__.get("_route_ctr")
+        if c is None or c.device != device:
+            c = torch.zeros(1, dtype=torch.int32, device=device)
+            self.__dict__["_route_ctr"] = c
+        return c
+
+    def fused_route_ok(self, x2: torch.Tensor) -> bool:
+        return (x2.is_cuda and x2.shape[0] <= 16 and ops.native_gpu(x2) and self.num_experts <= 512
+                and self.top_k <= 16 and self.local_experts <= 512 and x2.shape[-1] % 8 == 0
+                and self.gate_up.in_features * 2 * min(16, x2.shape[0]) <= 150 * 1024)
+
+    def _route_fused(self, x2):
+        return ops.moe_route(x2, self._router_w(x2.dtype), self.top_k, self.renorm, 0, self.e0,
+                             self.local_experts, self._route_counter(x2.device))
+
+    def acc_ok(self, x2: torch.Tensor) -> bool:
+        """decode block can accumulate into a residual-norm f32 slab"""
+        sm = self.shared_mlp
+        return (self.ep_group is None and self.fused_route_ok(x2)
+                and (sm is None or (isinstance(sm, SharedExpertMLP) and hasattr(sm.gate_up_proj, "fmt")
+                                    and hasattr(sm.down_proj, "fmt") and getattr(sm.down_proj, "bias", None) is None)))
+
+    @torch.no_grad()
+    def forward_acc(self, x2: torch.Tensor, acc: torch.Tensor) -> torch.Tensor:
+        """decode: acc [T, H] f32 (zero on entry) += MoE(x2), three launches
+        for the routed experts (+ the shared expert's two GEMVs)."""
+        w, ids, off, rows = self._route_fused(x2)
+        gu, dn = self.gate_up, self.down
+        a = ops.moe_gemv_glu(x2, gu.weight, gu.fmt, gu.out_features, gu.in_features, off, rows, self.top_k, self.act)
+        ops.moe_gemv_accum(a, dn.weight, dn.fmt, dn.out_features, dn.in_features, off, rows, acc, w, self.top_k)
+        sm = self.shared_mlp
+        if sm is not None:
+            sg, sd = sm.gate_up_proj, sm.down_proj
+            sa = ops.gemv_glu(x2, sg.weight, sg.fmt, sg.out_features, sg.in_features, sm.act)
+            if self.shared_gate is None:
+                ops.gemv_accum(sa, sd.weight, sd.fmt, sd.out_features, sd.in_features, acc)
+            else:
+                s = sd(sa).float()
+                acc.add_(torch.sigmoid(F.linear(x2, self.shared_gate.to(x2.dtype)).float()) * s)
+        return acc
+
+    def _experts_grouped(self, x, w, ids, off=None, rows=None):
+        """decode: device-side launches only, no host sync"""
         El = self.local_experts
-        off, rows = ops.moe_align(ids, self.e0, El)
+        if off is None:
+            off, rows = ops.moe_align(ids, self.e0, El)
         gu, dn = self.gate_up, self.down
         a = ops.moe_gemv_glu(x, gu.weight, gu.fmt, gu.out_features, gu.in_features, off, rows, self.top_k, self.act)
         part = ops.moe_gemv_partials(a, dn.weight, dn.fmt, dn.out_features, dn.in_features, off, rows)
@@ -190,12 +242,16 @@ class NativeMoE(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).contiguous()
-        w, ids = self.route(x2)
-        if x2.is_cuda and x2.shape[0] <= 16 and ops.native_gpu(x2) and \
-                self.gate_up.in_features * 2 * min(16, x2.shape[0]) <= 150 * 1024:
-            y = self._experts_grouped(x2, w, ids)
+        if self.fused_route_ok(x2):
+            w, ids, off, rows = self._route_fused(x2)
+            y = self._experts_grouped(x2, w, ids, off, rows)
         else:
-            y = self._experts_loop(x2, w, ids)
+            w, ids = self.route(x2)
+            if x2.is_cuda and x2.shape[0] <= 16 and ops.native_gpu(x2) and \
+                    self.gate_up.in_features * 2 * min(16, x2.shape[0]) <= 150 * 1024:
+                y = self._experts_grouped(x2, w, ids)
+            else:
+                y = self._experts_loop(x2, w, ids)
         if self.ep_group is not None:
             from ..parallel.comm import all_reduce_inplace
             y = all_reduce_inplace(y, self.ep_group)

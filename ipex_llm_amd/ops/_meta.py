@@ -100,6 +100,18 @@ def _(part, w, ids, e0, num_local, dtype):
     return part.new_empty((w.numel() // w.shape[-1], part.shape[-1]), dtype=dtype)
 
 
+@register_fake("ipex_llm_amd::moe_gemv_accum")
+def _(x, blob, fmt, n, k, off, rows, acc, w, topk, ksplit):
+    return None
+
+
+@register_fake("ipex_llm_amd::moe_route")
+def _(x, router, k, renorm, scoring, e0, num_local, counter):
+    T = x.shape[0]
+    return (x.new_empty((T, k), dtype=torch.float32), x.new_empty((T, k), dtype=torch.int32),
+            x.new_empty((num_local + 1,), dtype=torch.int32), x.new_empty((T * k,), dtype=torch.int32))
+
+
 @register_fake("ipex_llm_amd::rope_kv_fused")
 def _(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm, norm_eps, q_scale, Hq,
       Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale, pos_offset=None, zero_part=False):

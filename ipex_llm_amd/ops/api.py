@@ -17,7 +17,7 @@ __all__ = [
     "quantize", "dequantize", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
-    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
+    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
     "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope", "attn_prefill", "moe_group_topk",
 ]
 
@@ -245,6 +245,30 @@ def moe_gemv_glu(x, blob, fmt, n, k, off, rows, topk: int, act: int = 0):
 def moe_gemv_partials(x, blob, fmt, n, k, off, rows, ksplit: int = 0):
     """Grouped GEMV over experts on pair rows: x [P, k] -> f32 [ks, P, n]."""
     return _ops().moe_gemv(x, blob, fmt, n, k, off, rows, 1, x.shape[0], 1, ksplit, 0)
+
+
+def moe_gemv_accum(x, blob, fmt, n, k, off, rows, acc, w, topk: int, ksplit: int = 0):
+    """Grouped down projection with the routing-weighted combine in the
+    epilogue: acc[p // topk] += w[p] * x[p] @ W_e^T (f32 atomics; acc [T, n]
+    zero on entry, re-zeroed by its consumer)."""
+    _ops().moe_gemv_accum(x, blob, fmt, n, k, off, rows, acc, w.contiguous(), topk, ksplit)
+    return acc
+
+
+def moe_route(x, router, k: int, renorm: bool, scoring: int, e0: int, num_local: int,
+              counter: Optional[torch.Tensor] = None):
+    """Decode router (<= 16 tokens) in one launch: logits = x router^T (f32),
+    softmax (scoring 0) / sigmoid (1) top-k (+renormalise) and the per-local-
+    expert pair lists -> (w f32 [T, k], ids int32 [T, k], off [El+1], rows [T*k]).
+    ``counter``: int32 device scalar, zero on entry and left zero."""
+    if _native(x) and x.shape[0] <= 16 and router.shape[0] <= 512 and k <= 16 and num_local <= 512:
+        if counter is None:
+            counter = torch.zeros(1, dtype=torch.int32, device=x.device)
+        return _ops().moe_route(x, router.to(x.dtype), k, renorm, scoring, e0, num_local, counter)
+    logits = (x.float() @ router.float().t())
+    w, ids = R.moe_topk(logits, k, renorm, scoring)
+    off, rows = R.moe_align(ids, e0, num_local)
+    return w, ids, off, rows
 
 
 def moe_combine(part, w, ids, e0: int, num_local: int, dtype=torch.bfloat16):
