@@ -166,7 +166,8 @@ struct MoeRouteArgs {
   const uint16_t* x;      // [T, H] activations
   const uint16_t* wr;     // [E, H] router weight (same 16-bit type)
   int T, H, E, k, renorm, scoring, e0, El;
-  float* logits;          // [T, E] f32 scratch
+  int nsp;                // hidden slices (workgroups per expert)
+  float* logits;          // [nsp, T, E] f32 scratch (partial sums)
   int* counter;           // zero on entry, left zero (last workgroup resets it)
   float* topk_w;          // [T, k]
   int32_t* topk_ids;      // [T, k]

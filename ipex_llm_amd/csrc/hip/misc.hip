@@ -227,9 +227,10 @@ void launch_reduce_partials(bool bf16, const float* ws, int nsplit, const uint16
 // one wave per token row, E <= 512.  SC1: the logits were handed over by other
 // workgroups of the same launch (sc1 loads).  ids_lds (optional) receives the
 // chosen ids for a following in-workgroup align.
+// nsp > 1: the logits are nsp partial sums, sp_stride floats apart.
 template <bool SC1>
 __device__ __forceinline__ void topk_row(const float* lrow, int E, int k, int renorm, int scoring, float* w_out,
-                                         int32_t* id_out, int* ids_lds) {
+                                         int32_t* id_out, int* ids_lds, int nsp = 1, size_t sp_stride = 0) {
   const int lane = threadIdx.x & 63;
   constexpr int PER = 8;
   float v[PER];
@@ -237,7 +238,12 @@ __device__ __forceinline__ void topk_row(const float* lrow, int E, int k, int re
 #pragma unroll
   for (int j = 0; j < PER; j++) {
     const int e = lane + 64 * j;
-    v[j] = e < E ? (SC1 ? ld_sc1(lrow + e) : lrow[e]) : -INFINITY;
+    float x = -INFINITY;
+    if (e < E) {
+      x = 0.f;
+      for (int sp = 0; sp < nsp; sp++) x += SC1 ? ld_sc1(lrow + sp * sp_stride + e) : lrow[sp * sp_stride + e];
+    }
+    v[j] = x;
     mx = fmaxf(mx, v[j]);
   }
   if (scoring == 0) {
@@ -294,21 +300,63 @@ __global__ void __launch_bounds__(64) moe_topk_kernel(const float* logits, int T
 
 // ---- fused decode router (T <= 16 tokens): logits = x Wr^T in f32, softmax /
 // sigmoid top-k (+renormalise) and the per-expert pair lists of moe_align in
-// ONE launch.  Workgroup = 4 waves, wave = one expert over all T tokens (the
-// router row is read once, x rows from L2); the last workgroup to finish
+// ONE launch.  The last workgroup to finish
 // (agent-scope counter, sc1 hand-off) runs top-k per token and the align.
+// Workgroup = (expert, hidden slice of 2048): one 16-B chunk of the router
+// row per thread, so every load is in flight at once; the last workgroup sums
+// the slices' partial logits.
 // Replaces router GEMM + f32 cast + moe_topk + moe_align (4 launches).
+// top-k per token (one wave each) + per-local-expert pair lists, run by one
+// workgroup of NT threads over logits lg [T, E] (SC1: handed over by other
+// workgroups of the launch)
+template <bool SC1, int NT>
+__device__ __forceinline__ void route_tail(const MoeRouteArgs& a, const float* lg) {
+  const int wave = threadIdx.x >> 6;
+  __shared__ int ids_l[16 * 16];
+  __shared__ int cnt[512], start[512];
+  for (int t = wave; t < a.T; t += NT / 64)
+    topk_row<SC1>(lg + (size_t)t * a.E, a.E, a.k, a.renorm, a.scoring, a.topk_w + (size_t)t * a.k,
+                  a.topk_ids + (size_t)t * a.k, ids_l + t * a.k, a.nsp, (size_t)a.T * a.E);
+  for (int i = threadIdx.x; i < a.El; i += NT) cnt[i] = 0;
+  __syncthreads();
+  const int P = a.T * a.k;
+  for (int p = threadIdx.x; p < P; p += NT) {
+    const int el = ids_l[p] - a.e0;
+    if (el >= 0 && el < a.El) atomicAdd(&cnt[el], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < a.El; i++) {
+      start[i] = acc;
+      a.off[i] = acc;
+      acc += cnt[i];
+    }
+    a.off[a.El] = acc;
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < P; p += NT) {
+    const int id = ids_l[p], el = id - a.e0;
+    if (el < 0 || el >= a.El) continue;
+    int r = 0;
+    for (int q = 0; q < p; q++) r += ids_l[q] == id;
+    a.rows[start[el] + r] = p;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) moe_route_kernel(const MoeRouteArgs a) {
   constexpr int TM = 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int e = blockIdx.x * 4 + wave;
-  if (e < a.E) {
+  const int e = blockIdx.x, sp = blockIdx.y;
+  __shared__ float red[4][TM];
+  {
     float acc[TM];
 #pragma unroll
     for (int t = 0; t < TM; t++) acc[t] = 0.f;
     const uint16_t* wrow = a.wr + (size_t)e * a.H;
-    for (int c = lane; c < a.H / 8; c += 64) {
+    const int nc = a.H / 8;
+    for (int c = sp * 256 + threadIdx.x; c < nc; c += 256 * a.nsp) {
       const uint4 wv = *(const uint4*)(wrow + 8 * c);
       const uint32_t ww[4] = {wv.x, wv.y, wv.z, wv.w};
       float wf[8];
@@ -334,8 +382,13 @@ __global__ void __launch_bounds__(256) moe_route_kernel(const MoeRouteArgs a) {
     for (int t = 0; t < TM; t++) {
       if (t < a.T) {
         const float v = wave_sum(acc[t]);
-        if (lane == 0) st_sc1(a.logits + (size_t)t * a.E + e, v);
+        if (lane == 0) red[wave][t] = v;
       }
+    }
+    __syncthreads();
+    if (threadIdx.x < a.T) {
+      const int t = threadIdx.x;
+      st_sc1(a.logits + ((size_t)sp * a.T + t) * a.E + e, red[0][t] + red[1][t] + red[2][t] + red[3][t]);
     }
   }
   __shared__ int is_last;
@@ -343,47 +396,18 @@ __global__ void __launch_bounds__(256) moe_route_kernel(const MoeRouteArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const int prev = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = prev == (int)gridDim.x - 1;
+    is_last = prev == (int)(gridDim.x * gridDim.y) - 1;
     if (is_last) __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (!is_last) return;
 
-  // ---- last workgroup: top-k per token, then the per-local-expert pair lists
-  __shared__ int ids_l[16 * 16];
-  __shared__ int cnt[512], start[512];
-  for (int t = wave; t < a.T; t += 4)
-    topk_row<true>(a.logits + (size_t)t * a.E, a.E, a.k, a.renorm, a.scoring, a.topk_w + (size_t)t * a.k,
-                   a.topk_ids + (size_t)t * a.k, ids_l + t * a.k);
-  for (int i = threadIdx.x; i < a.El; i += 256) cnt[i] = 0;
-  __syncthreads();
-  const int P = a.T * a.k;
-  for (int p = threadIdx.x; p < P; p += 256) {
-    const int el = ids_l[p] - a.e0;
-    if (el >= 0 && el < a.El) atomicAdd(&cnt[el], 1);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int i = 0; i < a.El; i++) {
-      start[i] = acc;
-      a.off[i] = acc;
-      acc += cnt[i];
-    }
-    a.off[a.El] = acc;
-  }
-  __syncthreads();
-  for (int p = threadIdx.x; p < P; p += 256) {
-    const int id = ids_l[p], el = id - a.e0;
-    if (el < 0 || el >= a.El) continue;
-    int r = 0;
-    for (int q = 0; q < p; q++) r += ids_l[q] == id;
-    a.rows[start[el] + r] = p;
-  }
+  route_tail<true, 256>(a, a.logits);
 }
 
 void launch_moe_route(bool bf16, const MoeRouteArgs& a, hipStream_t st) {
-  const dim3 grid((unsigned)((a.E + 3) / 4));
+  // (expert, hidden slice) workgroups: one 16-B chunk of the router row per thread
+  const dim3 grid((unsigned)a.E, (unsigned)a.nsp);
   if (bf16) hipLaunchKernelGGL(moe_route_kernel<BF16>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(moe_route_kernel<F16>, grid, dim3(256), 0, st, a);
 }

@@ -1052,7 +1052,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> moe_route(const Tensor& x, const Tens
   TORCH_CHECK(counter.scalar_type() == at::kInt && counter.numel() >= 1, "moe_route: int32 counter");
   auto f32 = xc.options().dtype(at::kFloat);
   auto i32 = xc.options().dtype(at::kInt);
-  Tensor logits = at::empty({T, E}, f32);
+  const int64_t nsp = std::max<int64_t>(1, (H / 8 + 255) / 256);   // 256 16-B chunks per workgroup
+  Tensor logits = at::empty({nsp, T, E}, f32);
   Tensor w = at::empty({T, k}, f32);
   Tensor ids = at::empty({T, k}, i32);
   Tensor off = at::empty({num_local + 1}, i32);
@@ -1062,6 +1063,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> moe_route(const Tensor& x, const Tens
   a.wr = p16(wc);
   a.T = (int)T; a.H = (int)H; a.E = (int)E; a.k = (int)k;
   a.renorm = renorm ? 1 : 0; a.scoring = (int)scoring; a.e0 = (int)e0; a.El = (int)num_local;
+  a.nsp = (int)nsp;
   a.logits = logits.data_ptr<float>();
   a.counter = counter.data_ptr<int32_t>();
   a.topk_w = w.data_ptr<float>();
