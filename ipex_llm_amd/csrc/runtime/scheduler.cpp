@@ -17,6 +17,18 @@
 //   2. WAITING requests are admitted FCFS while the batch has room, the
 //      step's prefill token budget is not exceeded and the pool can hold
 //      prompt + 1 tokens (a request that can never fit is failed).
+//
+// Automatic prefix caching (``enable_prefix_caching()``, the vLLM APC feature
+// of the reference's serving stack, BASELINE "Automatic prefix caching
+// demo"): every FULL block whose K/V are computed is registered under a
+// chained 64-bit content hash (parent hash + its bs token ids, verified
+// against the stored ids on lookup).  Blocks are reference-counted; a block
+// whose last user finishes stays cached on an LRU list and is reclaimed only
+// when the pool runs dry.  An admitted request (or a preempted one coming
+// back) reuses the longest chain of cached blocks of its context (at least
+// its last token is always recomputed, it yields the next-token logits), so
+// only the uncached suffix is prefilled.  Cached blocks are immutable: new
+// tokens always go to blocks past the shared full ones.
 // Exposed to Python as torch.classes.ipex_llm_amd.Scheduler.
 #include <torch/custom_class.h>
 #include <torch/library.h>
@@ -24,12 +36,16 @@
 #include <algorithm>
 #include <cstdint>
 #include <deque>
+#include <set>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 namespace {
 
 enum State : int64_t { WAITING = 0, RUNNING = 1, FINISHED = 2, FAILED = 3 };
+
+constexpr uint64_t kSeed = 0x9e3779b97f4a7c15ull;   // chain hash of the empty prefix
 
 struct Seq {
   int64_t id = 0;
@@ -39,6 +55,26 @@ struct Seq {
   int64_t state = WAITING;
   int64_t preemptions = 0;
   std::vector<int64_t> blocks;
+  std::vector<int64_t> toks;  // prompt + generated ids (prefix caching only)
+  int64_t nhashed = 0;        // leading full blocks already hashed / registered
+  uint64_t last_hash = kSeed; // chain hash after nhashed blocks
+};
+
+uint64_t hash_block(uint64_t parent, const int64_t* t, int64_t n) {
+  uint64_t h = parent ^ 0xcbf29ce484222325ull;
+  for (int64_t i = 0; i < n; i++) {
+    uint64_t v = (uint64_t)t[i] + 0x9e3779b97f4a7c15ull;
+    v = (v ^ (v >> 30)) * 0xbf58476d1ce4e5b9ull;
+    v = (v ^ (v >> 27)) * 0x94d049bb133111ebull;
+    h = (h ^ (v ^ (v >> 31))) * 0x100000001b3ull;
+  }
+  return h ? h : 1;  // 0 marks "no hash"
+}
+
+struct CachedBlock {
+  int64_t block;
+  uint64_t parent;
+  std::vector<int64_t> toks;
 };
 
 class Scheduler : public torch::CustomClassHolder {
@@ -49,6 +85,24 @@ class Scheduler : public torch::CustomClassHolder {
     free_.reserve(num_blocks);
     for (int64_t b = num_blocks - 1; b >= 0; b--) free_.push_back(b);
     total_ = num_blocks;
+    ref_.assign(num_blocks, 0);
+    bhash_.assign(num_blocks, 0);
+    etick_.assign(num_blocks, -1);
+  }
+
+  void enable_prefix_caching(bool on) { apc_ = on; }
+
+  // request with its prompt token ids (prefix caching needs the content)
+  void add_tokens(int64_t id, std::vector<int64_t> prompt) {
+    add(id, (int64_t)prompt.size());
+    if (apc_) seqs_[id].toks = std::move(prompt);
+  }
+
+  // a generated token (fed next step): the context grows by one
+  void append(int64_t id, int64_t tok) {
+    Seq& s = get(id);
+    s.context += 1;
+    if (apc_) s.toks.push_back(tok);
   }
 
   void add(int64_t id, int64_t prompt_len) {
@@ -98,15 +152,27 @@ class Scheduler : public torch::CustomClassHolder {
         waiting_.pop_front();
         continue;
       }
-      if (need > (int64_t)free_.size() || (s.context > budget && !prefill.empty())) break;
+      std::vector<int64_t> hit;
+      uint64_t chain = kSeed;
+      match_prefix(s, hit, chain);
+      int64_t hit_idle = 0;  // cached blocks nobody holds: reusing them does not consume the pool
+      for (int64_t b : hit) hit_idle += ref_[b] == 0;
+      const int64_t fresh = need - (int64_t)hit.size();
+      const int64_t todo = s.context - (int64_t)hit.size() * bs_;
+      if (fresh > available() - hit_idle || (todo > budget && !prefill.empty())) break;
       waiting_.pop_front();
-      for (int64_t i = 0; i < need; i++) s.blocks.push_back(pop_free());
+      for (int64_t b : hit) take(b);
+      s.blocks = hit;
+      for (int64_t i = 0; i < fresh; i++) s.blocks.push_back(pop_free());
       s.state = RUNNING;
-      s.cached = 0;
+      s.cached = (int64_t)hit.size() * bs_;
+      s.nhashed = (int64_t)hit.size();
+      s.last_hash = chain;
+      hit_tokens_ += s.cached;
       s.admitted = ++admit_counter_;
       running_.push_back(s.id);
       prefill.push_back(s.id);
-      budget -= s.context;
+      budget -= todo;
     }
     std::vector<int64_t> out;
     for (auto* v : {&prefill, &decode, &preempted}) {
@@ -123,6 +189,7 @@ class Scheduler : public torch::CustomClassHolder {
     s.cached += n;
     if (s.cached > s.context) s.context = s.cached;
     TORCH_CHECK(s.cached <= (int64_t)s.blocks.size() * bs_, "Scheduler: sequence ", id, " overran its blocks");
+    if (apc_) register_full_blocks(s);
   }
 
   // a token was generated (it will be fed next step): the context grows by one
@@ -141,7 +208,9 @@ class Scheduler : public torch::CustomClassHolder {
   int64_t cached(int64_t id) { return get(id).cached; }
   int64_t context(int64_t id) { return get(id).context; }
   int64_t state(int64_t id) { return get(id).state; }
-  int64_t num_free_blocks() { return (int64_t)free_.size(); }
+  int64_t num_free_blocks() { return available(); }
+  int64_t num_cached_blocks() { return (int64_t)cache_.size(); }
+  int64_t prefix_hit_tokens() { return hit_tokens_; }
   int64_t num_waiting() { return (int64_t)waiting_.size(); }
   int64_t num_running() { return (int64_t)running_.size(); }
   int64_t block_size() { return bs_; }
@@ -149,14 +218,76 @@ class Scheduler : public torch::CustomClassHolder {
  private:
   int64_t blocks_for(int64_t tokens) const { return (tokens + bs_ - 1) / bs_; }
   bool need_block(const Seq& s) const { return s.cached + 1 > (int64_t)s.blocks.size() * bs_; }
+  int64_t available() const { return (int64_t)(free_.size() + evict_.size()); }
+  // a fresh block: the free list first, else the least recently released cached block
   int64_t pop_free() {
-    const int64_t b = free_.back();
-    free_.pop_back();
+    int64_t b;
+    if (!free_.empty()) {
+      b = free_.back();
+      free_.pop_back();
+    } else {
+      TORCH_CHECK(!evict_.empty(), "Scheduler: KV pool exhausted");
+      b = evict_.begin()->second;
+      evict_.erase(evict_.begin());
+      etick_[b] = -1;
+      cache_.erase(bhash_[b]);
+      bhash_[b] = 0;
+    }
+    ref_[b] = 1;
     return b;
   }
+  // one more holder of a cached block
+  void take(int64_t b) {
+    if (ref_[b] == 0 && etick_[b] >= 0) {
+      evict_.erase({etick_[b], b});
+      etick_[b] = -1;
+    }
+    ref_[b]++;
+  }
   void release(Seq& s) {
-    for (auto it = s.blocks.rbegin(); it != s.blocks.rend(); ++it) free_.push_back(*it);
+    for (auto it = s.blocks.rbegin(); it != s.blocks.rend(); ++it) {
+      const int64_t b = *it;
+      if (--ref_[b] > 0) continue;
+      if (bhash_[b] != 0) {          // keep its content for later hits (LRU)
+        etick_[b] = ++tick_;
+        evict_.insert({etick_[b], b});
+      } else {
+        free_.push_back(b);
+      }
+    }
     s.blocks.clear();
+    s.nhashed = 0;
+    s.last_hash = kSeed;
+  }
+  // longest chain of cached full blocks covering the context minus its last token
+  void match_prefix(const Seq& s, std::vector<int64_t>& hit, uint64_t& chain) {
+    chain = kSeed;
+    if (!apc_ || (int64_t)s.toks.size() < s.context) return;
+    const int64_t maxb = (s.context - 1) / bs_;
+    for (int64_t i = 0; i < maxb; i++) {
+      const int64_t* t = s.toks.data() + i * bs_;
+      const uint64_t h = hash_block(chain, t, bs_);
+      auto it = cache_.find(h);
+      if (it == cache_.end() || it->second.parent != chain || !std::equal(t, t + bs_, it->second.toks.begin()))
+        break;
+      hit.push_back(it->second.block);
+      chain = h;
+    }
+  }
+  // full blocks whose K/V are now computed join the content index
+  void register_full_blocks(Seq& s) {
+    while ((s.nhashed + 1) * bs_ <= s.cached && (s.nhashed + 1) * bs_ <= (int64_t)s.toks.size()) {
+      const int64_t i = s.nhashed;
+      const int64_t* t = s.toks.data() + i * bs_;
+      const uint64_t h = hash_block(s.last_hash, t, bs_);
+      const int64_t b = s.blocks[i];
+      if (!cache_.count(h) && bhash_[b] == 0) {
+        cache_[h] = CachedBlock{b, s.last_hash, std::vector<int64_t>(t, t + bs_)};
+        bhash_[b] = h;
+      }
+      s.last_hash = h;
+      s.nhashed++;
+    }
   }
   void preempt(int64_t id) {
     Seq& s = get(id);
@@ -175,6 +306,14 @@ class Scheduler : public torch::CustomClassHolder {
 
   int64_t bs_, max_batch_, max_prefill_, total_ = 0, admit_counter_ = 0;
   std::vector<int64_t> free_;
+  // prefix caching
+  bool apc_ = false;
+  std::unordered_map<uint64_t, CachedBlock> cache_;  // content hash -> block
+  std::vector<int32_t> ref_;                          // holders per block
+  std::vector<uint64_t> bhash_;                       // hash a block is registered under (0: none)
+  std::vector<int64_t> etick_;                        // LRU tick of an idle cached block (-1: not idle)
+  std::set<std::pair<int64_t, int64_t>> evict_;       // idle cached blocks, oldest first
+  int64_t tick_ = 0, hit_tokens_ = 0;
   std::deque<int64_t> waiting_;
   std::vector<int64_t> running_;
   std::unordered_map<int64_t, Seq> seqs_;
@@ -189,6 +328,11 @@ TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
       .def("schedule", &Scheduler::schedule)
       .def("advance", &Scheduler::advance)
       .def("grow", &Scheduler::grow)
+      .def("enable_prefix_caching", &Scheduler::enable_prefix_caching)
+      .def("add_tokens", &Scheduler::add_tokens)
+      .def("append", &Scheduler::append)
+      .def("num_cached_blocks", &Scheduler::num_cached_blocks)
+      .def("prefix_hit_tokens", &Scheduler::prefix_hit_tokens)
       .def("finish", &Scheduler::finish)
       .def("blocks", &Scheduler::blocks)
       .def("cached", &Scheduler::cached)

@@ -59,7 +59,8 @@ class Request:
 class LLMEngine:
     def __init__(self, model: NativeCausalLM, max_batch: int = 64, block_size: int = 64,
                  num_blocks: Optional[int] = None, max_model_len: int = 8192, max_prefill_tokens: int = 8192,
-                 kv_fp8: int = 0, memory_fraction: float = 0.5, eos_token_id=None, use_graph: bool = True):
+                 kv_fp8: int = 0, memory_fraction: float = 0.5, eos_token_id=None, use_graph: bool = True,
+                 enable_prefix_caching: bool = True):
         ops.require() if model.device.type == "cuda" else None
         self.model = model
         s = model.spec
@@ -83,13 +84,18 @@ class LLMEngine:
         self._graphs: Dict[tuple, dict] = {}
         model.ensure_rope_cache(max_model_len + 1)
         self.sched = torch.classes.ipex_llm_amd.Scheduler(num_blocks, block_size, max_batch, max_prefill_tokens)
+        # automatic prefix caching: full KV blocks are shared by content hash
+        # (C++ scheduler); a request prefills only its uncached suffix
+        self.prefix_caching = bool(enable_prefix_caching)
+        self.sched.enable_prefix_caching(self.prefix_caching)
         self.block_size, self.max_model_len = block_size, max_model_len
         eos = eos_token_id if eos_token_id is not None else []
         self.eos = set([eos] if isinstance(eos, int) else eos)
         self.requests: Dict[int, Request] = {}
         self._ids = itertools.count()
         self.lock = threading.Lock()
-        self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "preemptions": 0}
+        self.stats = {"steps": 0, "prefill_tokens": 0, "decode_tokens": 0, "preemptions": 0,
+                      "prefix_hit_tokens": 0}
 
     # ------------------------------------------------------------ API
     def add_request(self, prompt: List[int], params: Optional[SamplingParams] = None,
@@ -105,7 +111,10 @@ class LLMEngine:
             r = Request(rid, list(prompt), params, tokens=list(prompt), arrival=time.perf_counter(),
                         on_token=on_token, generator=g)
             self.requests[rid] = r
-            self.sched.add(rid, len(prompt))
+            if self.prefix_caching:
+                self.sched.add_tokens(rid, [int(t) for t in prompt])
+            else:
+                self.sched.add(rid, len(prompt))
         self.metrics.on_request(len(prompt))
         return rid
 
@@ -135,7 +144,10 @@ class LLMEngine:
         if r.first_token_time is None:
             r.first_token_time = time.perf_counter() - r.arrival
             self.metrics.on_first_token(r.first_token_time)
-        self.sched.grow(r.rid)
+        if self.prefix_caching:
+            self.sched.append(r.rid, int(tok))
+        else:
+            self.sched.grow(r.rid)
         if r.on_token is not None:
             r.on_token(tok, r)
         p = r.params
@@ -242,16 +254,20 @@ class LLMEngine:
                 r = self.requests[rid]
                 toks = r.tokens
                 n = len(toks)
+                start = int(self.sched.cached(rid))        # prefix already in cached KV blocks
+                tq = n - start
                 bt = self._block_table([rid])
-                pos = torch.arange(n, device=dev)
+                pos_h = torch.arange(start, n)
                 blocks = torch.tensor(list(self.sched.blocks(rid)), dtype=torch.long)
-                slots = (blocks[pos.cpu() // bs] * bs + pos.cpu() % bs).to(dev)
-                meta = AttnMeta(1, n, bt, torch.tensor([n], dtype=torch.int32, device=dev), nsplit_for(n), [n])
-                lg = m.forward_tokens(torch.tensor(toks, device=dev), pos, slots, meta, self.cache,
-                                      logits_idx=torch.tensor([n - 1], device=dev))
-                self.sched.advance(rid, n)
-                self.stats["prefill_tokens"] += n
-                self.metrics.on_prefill(n)
+                slots = (blocks[pos_h // bs] * bs + pos_h % bs).to(dev)
+                meta = AttnMeta(1, tq, bt, torch.tensor([n], dtype=torch.int32, device=dev), nsplit_for(n), [n])
+                lg = m.forward_tokens(torch.tensor(toks[start:], device=dev), pos_h.to(dev), slots, meta,
+                                      self.cache, logits_idx=torch.tensor([tq - 1], device=dev))
+                self.sched.advance(rid, tq)
+                self.stats["prefill_tokens"] += tq
+                self.stats["prefix_hit_tokens"] += start
+                self.metrics.on_prefill(tq)
+                self.metrics.on_prefix_hit(start)
                 self._emit(r, self._pick(lg, r))
                 produced += 1
             if decode:

@@ -39,6 +39,8 @@ class EngineMetrics:
         self.finished = Counter("ipex_llm_requests_finished", "requests finished by reason", lab + ["reason"],
                                 registry=r)
         self.prompt_tokens = Counter("ipex_llm_prompt_tokens", "prefilled prompt tokens", lab, registry=r)
+        self.prefix_hits = Counter("ipex_llm_prefix_cache_hit_tokens", "prompt tokens served from cached KV blocks",
+                                   lab, registry=r)
         self.gen_tokens = Counter("ipex_llm_generation_tokens", "generated tokens", lab, registry=r)
         self.preemptions = Counter("ipex_llm_preemptions", "sequences preempted (recompute)", lab, registry=r)
         self.ttft = Histogram("ipex_llm_time_to_first_token_seconds", "time to first token", lab,
@@ -61,6 +63,10 @@ class EngineMetrics:
     def on_prefill(self, n_tokens: int):
         if self.enabled:
             self.prompt_tokens.labels(self.model).inc(n_tokens)
+
+    def on_prefix_hit(self, n_tokens: int):
+        if self.enabled and n_tokens:
+            self.prefix_hits.labels(self.model).inc(n_tokens)
 
     def on_tokens(self, n: int):
         if self.enabled and n:

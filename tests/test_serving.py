@@ -72,6 +72,61 @@ def test_engine_preemption_recompute(native):
     assert [p + o for p, o in zip(prompts, out)] == ref
 
 
+def test_scheduler_prefix_cache_reuse_and_eviction():
+    s = _sched(nb=6, bs=64)
+    s.enable_prefix_caching(True)
+    pa = list(range(1, 150))                    # 149 tokens: 2 full blocks + 21
+    s.add_tokens(1, pa)
+    p, d, pre, f = _split(list(s.schedule()))
+    assert p == [1] and s.cached(1) == 0
+    s.advance(1, len(pa))
+    assert s.num_cached_blocks() == 2           # the two full blocks are indexed
+    # same 128-token prefix, different tail: reuses both full blocks
+    s.add_tokens(2, pa[:128] + [7, 8, 9])
+    p, d, pre, f = _split(list(s.schedule()))
+    assert p == [2] and s.cached(2) == 128
+    assert list(s.blocks(2))[:2] == list(s.blocks(1))[:2]
+    assert s.prefix_hit_tokens() == 128
+    # a prompt that IS exactly the 2 cached blocks recomputes its last token
+    s.add_tokens(3, pa[:128])
+    p, d, pre, f = _split(list(s.schedule()))
+    assert p == [3] and s.cached(3) == 64
+    # finishing keeps content: blocks become idle-but-cached (counted as free)
+    for r in (1, 2, 3):
+        s.finish(r)
+    assert s.num_free_blocks() == 6 and s.num_cached_blocks() == 2
+    s.add_tokens(4, pa[:64] + [1] * 70)          # hits block 0 after all holders left
+    p, d, pre, f = _split(list(s.schedule()))
+    assert p == [4] and s.cached(4) == 64
+    s.finish(4)
+    # a request needing every block evicts the idle cached ones
+    s.add_tokens(5, [3] * 380)
+    p, d, pre, f = _split(list(s.schedule()))
+    assert p == [5] and s.cached(5) == 0 and s.num_free_blocks() == 0
+    s.advance(5, 380)
+    assert s.num_cached_blocks() == 5
+
+
+def test_engine_prefix_cache_matches_uncached(native):
+    """shared system prompt: later requests prefill only their suffix and
+    produce the tokens of the uncached engine"""
+    from ipex_llm_amd.serving.engine import LLMEngine, SamplingParams
+    sys_p = [3 + (i * 7) % 120 for i in range(130)]
+    prompts = [sys_p + [5, 6, 7], sys_p + [9], sys_p + list(range(40, 70)), sys_p[:64] + [1, 2]]
+    ref = LLMEngine(native, max_batch=8, max_model_len=512, enable_prefix_caching=False)
+    want = [ref.generate([p], SamplingParams(max_new_tokens=8))[0] for p in prompts]
+    eng = LLMEngine(native, max_batch=8, max_model_len=512)
+    got = [eng.generate([p], SamplingParams(max_new_tokens=8))[0] for p in prompts]
+    assert got == want
+    # requests 2..4 reuse 128, 128 and 64 cached prompt tokens
+    assert eng.stats["prefix_hit_tokens"] == 128 + 128 + 64
+    # a multi-turn continuation reuses the blocks of the previous turn's answer too
+    turn2 = prompts[2] + got[2] + [11, 12]
+    again = eng.generate([turn2], SamplingParams(max_new_tokens=4))[0]
+    assert again == ref.generate([turn2], SamplingParams(max_new_tokens=4))[0]
+    assert eng.stats["prefix_hit_tokens"] >= 128 + 128 + 64 + 128
+
+
 def _tokenizer():
     from tokenizers import Tokenizer, models, pre_tokenizers
     from transformers import PreTrainedTokenizerFast
@@ -145,3 +200,23 @@ def test_engine_graph_decode_matches_eager_on_gpu(cuda):
     a, b = sum(outs[False], []), sum(outs[True], [])
     assert [len(x) for x in outs[True]] == lens
     assert sum(x == y for x, y in zip(a, b)) >= 0.97 * len(a)
+
+
+@pytest.mark.gpu
+def test_engine_prefix_cache_on_gpu(cuda):
+    """prefix-cached suffix prefill (HIP chunked-prefill attention over cached
+    blocks) + graph decode gives the uncached engine's tokens"""
+    from transformers import LlamaConfig
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.serving.engine import LLMEngine, SamplingParams
+    cfg = LlamaConfig(vocab_size=1024, hidden_size=512, intermediate_size=1024, num_hidden_layers=2,
+                      num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=2048)
+    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=11)
+    table = [(i * 37) % 1000 + 3 for i in range(300)]
+    prompts = [table + [5, 6, 7], table + [9, 10], table[:200] + [4]]
+    ref = LLMEngine(m, max_batch=4, max_model_len=512, enable_prefix_caching=False)
+    want = [ref.generate([p], SamplingParams(max_new_tokens=8))[0] for p in prompts]
+    eng = LLMEngine(m, max_batch=4, max_model_len=512)
+    got = [eng.generate([p], SamplingParams(max_new_tokens=8))[0] for p in prompts]
+    assert got == want
+    assert eng.stats["prefix_hit_tokens"] == 256 + 192
