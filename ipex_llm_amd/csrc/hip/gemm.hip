@@ -15,7 +15,10 @@
 //     memory (the dequantize + hipBLASLt path wrote 2 B per weight);
 //   * activations: the 128 x 128 x-chunk is staged global -> registers ->
 //     LDS as f16 (double buffered, one chunk ahead), padded rows (272 B) so
-//     the B-fragment ds_read_b128 of 16 rows hit distinct banks;
+//     the B-fragment ds_read_b128 of 16 rows hit distinct banks.  bf16
+//     activations are converted to f16 ONCE per call (launch_bf16_to_f16_sat):
+//     converting while staging repeated the work for every n-block and was
+//     ~90 % of the kernel's VALU instructions (rocprofv3 PMC, gate_up M=1024);
 //   * XCD-aware block order: the 8 m-blocks of one n-block run on one XCD
 //     (ids b, b + 8, ...), so a weight chunk comes from HBM once per XCD
 //     and is re-read by the other m-blocks from that XCD's L2.
@@ -104,14 +107,17 @@ __device__ __forceinline__ uint4 gemm_a8(uint32_t lo, uint32_t hi, gh2 d2, gh2 m
 constexpr int GLDX = 128 + 8;     // LDS row stride of the x chunk (halves)
 
 // WN weight tiles (16 rows each) x WM token tiles (16 rows each) per wave; the
-// 4 waves of a block sit side by side along n: block = (4 WN * 16) n x (WM * 16) m.
-//   <2, 8>: 128 n x 128 m, every x fragment read from LDS feeds 2 MFMAs;
-//   <4, 4>: 256 n x 64 m, half the LDS x traffic per MFMA (4 MFMAs per fragment)
-//           and half the x re-reads from L2, at 4 decoded weight tiles per wave.
-template <int DK, typename T, int WN, int WM, int PFW>
+// 4 waves of a block form a WA (along n) x 4/WA (along m) grid:
+// block = (WA WN 16) n x (4/WA WM 16) m.
+//   <2, 8, WA 4>: 128 n x 128 m, every x fragment read from LDS feeds 2 MFMAs;
+//   <4, 4, WA 4>: 256 n x 64 m, 4 MFMAs per x fragment, 4 decoded tiles per wave;
+//   <4, 4, WA 2>: 128 n x 128 m, 4 MFMAs per x fragment (half the LDS reads of
+//                 <2, 8>) at the same accumulator count; each weight tile is
+//                 decoded by the two m-halves' waves (L1 hits for the second).
+template <int DK, typename T, int WN, int WM, int PFW, int WA = 4>
 __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   constexpr int BITS = dk_bits(DK);
-  constexpr int GBM = WM * 16, GBN = 4 * WN * 16;
+  constexpr int GBM = (4 / WA) * WM * 16, GBN = WA * WN * 16;
   __shared__ __attribute__((aligned(16))) uint16_t xs[2][GBM * GLDX];
   __shared__ uint32_t lut2[DK == DK_LUT4 ? 256 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -125,7 +131,8 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   if (nb >= NB) return;
   const int m0 = mb * GBM;
   const int NT = (a.N + 15) / 16;
-  const int tile0 = nb * (4 * WN) + wave * WN;
+  const int wn = wave % WA, wm = wave / WA;           // wave position in the block
+  const int tile0 = nb * (WA * WN) + wn * WN;
   const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
   const uint8_t* tb[WN];
 #pragma unroll
@@ -138,11 +145,12 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   }
 
   // ---- x staging: thread -> rows (tid / 16) + 16 j, 8 columns at (tid % 16) * 8
-  uint4 xr[WM];
+  constexpr int XJ = GBM / 16;
+  uint4 xr[XJ];
   auto stage_load = [&](int c) {
     const int kk = c * 128 + (tid & 15) * 8;
 #pragma unroll
-    for (int j = 0; j < WM; j++) {
+    for (int j = 0; j < XJ; j++) {
       const int m = m0 + (tid >> 4) + 16 * j;
       const bool ok = m < a.M && kk < a.K;
       const uint4 v = *(const uint4*)(a.x + (size_t)(ok ? m : 0) * a.ldx + (ok ? kk : 0));
@@ -151,9 +159,9 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   };
   auto stage_store = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < WM; j++) {
+    for (int j = 0; j < XJ; j++) {
       uint4 v = xr[j];
-      if constexpr (std::is_same<T, BF16>::value) {
+      if (std::is_same<T, BF16>::value && !a.x_f16) {
         uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -206,7 +214,7 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
     return g_as_h2(__builtin_amdgcn_perm(0u, v, blk == 0 ? 0x01000100u : 0x03020302u));
   };
   auto compute = [&](const WChunk& cur, int buf) {
-    const uint16_t* xb = &xs[buf][r16 * GLDX + 8 * g];
+    const uint16_t* xb = &xs[buf][(wm * WM * 16 + r16) * GLDX + 8 * g];
 #pragma unroll
     for (int s = 0; s < 4; s++) {
       const int blk = s >> 1;
@@ -260,7 +268,7 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
       if (n0 >= I) continue;
 #pragma unroll
       for (int mt = 0; mt < WM; mt++) {
-        const int m = m0 + mt * 16 + r16;
+        const int m = m0 + (wm * WM + mt) * 16 + r16;
         if (m >= a.M) continue;
         float o[4];
 #pragma unroll
@@ -287,7 +295,7 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
       for (int i = 0; i < 4; i++) bv[i] = n0 + i < a.N ? to_f32<T>(a.bias[n0 + i]) : 0.f;
 #pragma unroll
     for (int mt = 0; mt < WM; mt++) {
-      const int m = m0 + mt * 16 + r16;
+      const int m = m0 + (wm * WM + mt) * 16 + r16;
       if (m >= a.M) continue;
       const float o[4] = {acc[t][mt][0] + bv[0], acc[t][mt][1] + bv[1], acc[t][mt][2] + bv[2],
                           acc[t][mt][3] + bv[3]};
@@ -298,14 +306,14 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   }
 }
 
-template <int DK, int WN, int WM, int PFW>
+template <int DK, int WN, int WM, int PFW, int WA = 4>
 static void launch_gemm_v(bool bf16, const GemmArgs& a, hipStream_t st) {
-  constexpr int GBM = WM * 16, GBN = 4 * WN * 16;
+  constexpr int GBM = (4 / WA) * WM * 16, GBN = WA * WN * 16;
   const int NB = (a.N + GBN - 1) / GBN, MB = (a.M + GBM - 1) / GBM;
   const int NBp = (NB + 7) / 8 * 8;
   dim3 grid((unsigned)(NBp * MB));
-  if (bf16) hipLaunchKernelGGL((lowbit_gemm_kernel<DK, BF16, WN, WM, PFW>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((lowbit_gemm_kernel<DK, F16, WN, WM, PFW>), grid, dim3(256), 0, st, a);
+  if (bf16) hipLaunchKernelGGL((lowbit_gemm_kernel<DK, BF16, WN, WM, PFW, WA>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((lowbit_gemm_kernel<DK, F16, WN, WM, PFW, WA>), grid, dim3(256), 0, st, a);
 }
 
 template <int DK>
@@ -316,7 +324,30 @@ static void launch_gemm_dk(bool bf16, const GemmArgs& a, hipStream_t st) {
   // gate_up -12 %; M = 8192 -15..18 %
   static const int tile_env = getenv("ILLM_GEMM_TILE") ? atoi(getenv("ILLM_GEMM_TILE")) : 0;
   if (tile_env == 2) launch_gemm_v<DK, 4, 4, 2>(bf16, a, st);
+  else if (tile_env == 3) launch_gemm_v<DK, 4, 4, 2, 2>(bf16, a, st);
+  else if (tile_env == 4) launch_gemm_v<DK, 4, 4, 3, 2>(bf16, a, st);
   else launch_gemm_v<DK, 2, 8, 4>(bf16, a, st);
+}
+
+__global__ void bf16_to_f16_sat_kernel(const uint4* x, uint4* y, int64_t n8) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const uint4 v = x[i];
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const float lo = fminf(fmaxf(bf16_to_f32(w[j] & 0xffff), -65504.f), 65504.f);
+    const float hi = fminf(fmaxf(bf16_to_f32(w[j] >> 16), -65504.f), 65504.f);
+    w[j] = pack2<F16>(lo, hi);
+  }
+  y[i] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+void launch_bf16_to_f16_sat(const uint16_t* x, uint16_t* y, int64_t n, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  if (n8 == 0) return;
+  hipLaunchKernelGGL(bf16_to_f16_sat_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st,
+                     (const uint4*)x, (uint4*)y, n8);
 }
 
 void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st) {

@@ -41,8 +41,11 @@ struct GemmArgs {
   int lut_fmt;
   int glu;                 // 1: tile-interleaved gate/up weight, out = act(gate) * up [M, N / 2]
   int act;                 // 0 = silu, 1 = gelu(tanh)
+  int x_f16;               // 1: x already holds f16 (saturated) copies of the bf16 activations
 };
 void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st);
+// bf16 -> f16 with saturation at +-65504 (the GEMM's MFMA input type), n % 8 == 0
+void launch_bf16_to_f16_sat(const uint16_t* x, uint16_t* y, int64_t n, hipStream_t st);
 
 // ---- norms (norm.hip) ------------------------------------------------------
 struct NormArgs {

@@ -227,7 +227,14 @@ Tensor gemm(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   Tensor out = at::empty(shape, xc.options());
   if (M == 0) return out;
   illm::GemmArgs a{};
-  a.x = p16(xc);
+  // bf16 activations -> f16 once per call (the MFMA input type of the decoded weights)
+  Tensor xh;
+  if (bf16) {
+    xh = at::empty(xc.sizes(), xc.options().dtype(at::kHalf));
+    illm::launch_bf16_to_f16_sat(p16(xc), m16(xh), xc.numel(), cur_stream());
+    a.x_f16 = 1;
+  }
+  a.x = bf16 ? p16(xh) : p16(xc);
   a.M = (int)M;
   a.K = (int)k;
   a.ldx = (int)k;
@@ -257,7 +264,14 @@ Tensor gemm_glu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   Tensor out = at::empty(shape, xc.options());
   if (M == 0) return out;
   illm::GemmArgs a{};
-  a.x = p16(xc);
+  // bf16 activations -> f16 once per call (the MFMA input type of the decoded weights)
+  Tensor xh;
+  if (bf16) {
+    xh = at::empty(xc.sizes(), xc.options().dtype(at::kHalf));
+    illm::launch_bf16_to_f16_sat(p16(xc), m16(xh), xc.numel(), cur_stream());
+    a.x_f16 = 1;
+  }
+  a.x = bf16 ? p16(xh) : p16(xc);
   a.M = (int)M;
   a.K = (int)k;
   a.ldx = (int)k;
