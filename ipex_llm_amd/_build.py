@@ -46,9 +46,24 @@ def _headers_mtime() -> float:
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
+def _deps_mtime(obj: str, fallback: float) -> float:
+    """newest header this object was compiled against (its -MMD depfile);
+    every header under csrc when there is no depfile yet"""
+    try:
+        with open(obj + ".d") as f:
+            txt = f.read().replace("\\\n", " ")
+    except OSError:
+        return fallback
+    deps = [d for d in txt.split(":", 1)[-1].split() if d.endswith((".h", ".cuh", ".hpp"))]
+    try:
+        return max((os.path.getmtime(d) for d in deps), default=0.0)
+    except OSError:                      # a header was renamed or removed
+        return fallback
+
+
 def _cmd(src: str, obj: str):
     tinc, tapi, _ = _torch_paths()
-    common = ["-O3", "-fPIC", "-std=c++17", "-I", CSRC, *_DEFS]
+    common = ["-O3", "-fPIC", "-std=c++17", "-I", CSRC, "-MMD", "-MF", obj + ".d", *_DEFS]
     if src.endswith(".hip"):
         extra = []
         if os.path.basename(src).startswith("gemv_"):
@@ -80,7 +95,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
         obj = os.path.join(OBJ, rel + ".o")
         objs.append(obj)
-        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), _deps_mtime(obj, hdr)):
             todo.append((src, obj))
     jobs = jobs or min(8, max(1, (os.cpu_count() or 4)))
     t0 = time.time()

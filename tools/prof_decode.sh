@@ -12,7 +12,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_b8" -o
 cd "$R"
 for b in b1 b8; do
   db=$(find "gpurun_out/prof_$b" -name "*.db" | head -1)
-  python3 tools/prof_summary.py "$db" 40 --after dequantize_tiled > "gpurun_out/prof_${b}_summary.txt" 2>&1 || python3 tools/prof_summary.py "$db" 40 > "gpurun_out/prof_${b}_summary.txt"
+  python3 tools/prof_summary.py "$db" 40 --after attn_prefill > "gpurun_out/prof_${b}_summary.txt" 2>&1 || python3 tools/prof_summary.py "$db" 40 > "gpurun_out/prof_${b}_summary.txt"
 done
 tail -1 gpurun_out/prof_b1.log | cut -c1-200
 # keep the summaries + rocprofv3 --stats CSVs, drop the (large) trace databases
