@@ -229,6 +229,8 @@ __device__ __forceinline__ uint4 kv_frag8(const uint8_t* p) {
 
 template <typename T, bool SC1 = false>
 __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int h, int t, float* wsh);
+template <typename T, bool SC1, int NR>
+__device__ __forceinline__ bool combine_fast(const AttnDecodeArgs& a, int b, const int* hs, const int* ts, int nr);
 
 // LATEV: issue the V loads after Q K^T (K registers are dead by then): fewer
 // VGPRs and the V stream overlaps the QK/softmax of the co-resident wave.
@@ -692,7 +694,18 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   __syncthreads();
   if (!is_last) return;
   float* wsh = PVM ? (float*)vl : &ps[0][0];        // LDS scratch of the split, reused
-  for (int r = 0; r < R; r++) combine_row<T, true>(a, b, kvh * group + r % group, r / group, wsh);
+  for (int r0 = 0; r0 < R; r0 += 4) {
+    const int nr = min(4, R - r0);
+    int hs[4], ts[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int rr = r0 + min(r, nr - 1);
+      hs[r] = kvh * group + rr % group;
+      ts[r] = rr / group;
+    }
+    if (!combine_fast<T, true, 4>(a, b, hs, ts, nr))
+      for (int r = 0; r < nr; r++) combine_row<T, true>(a, b, hs[r], ts[r], wsh);
+  }
   if constexpr (rq) {
     // fused-RoPE decode: every split of this (b, kv head) has read its q / k / v
     // columns of the qkv accumulator: re-zero them for the next layer's GEMV
@@ -704,6 +717,72 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
       *(float4*)(prow + (a.Hq + a.Hkv + kvh) * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+}
+
+// merge NR (<= 4) rows (b, hs[r], ts[r]) in ONE memory round trip: lane
+// (quad q, phase p) requests its partial quads of splits p, p + P, ... of
+// every row together with the rows' (m, l) pairs before any of them is
+// needed (the split weights only scale what is already in flight); the P
+// phases are summed with shuffles.  A loop over splits waited on one
+// dependent L2 round trip per few splits (5.8 us at 17 splits, B = 1), and
+// merging rows one after another in the fused combine put R such chains in
+// series.  Returns false (nothing done) when the splits do not fit one round.
+template <typename T, bool SC1, int NR>
+__device__ __forceinline__ bool combine_fast(const AttnDecodeArgs& a, int b, const int* hs, const int* ts, int nr) {
+  constexpr int CH = 12;                             // quads in flight per lane per row
+  const int lane = threadIdx.x;
+  const int len = a.seq_lens[b];
+  const int ns = min(a.nsplit, (len + SPLIT - 1) / SPLIT);
+  const int Q = a.D / 4;
+  if (!(Q == 16 || Q == 32 || Q == 64)) return false;
+  const int P = 64 / Q, q = lane % Q, p = lane / Q;
+  if (ns > CH * P) return false;
+  auto ld4 = [](const float* x) -> float4 {
+    if constexpr (SC1) return make_float4(ld_sc1(x), ld_sc1(x + 1), ld_sc1(x + 2), ld_sc1(x + 3));
+    else return *(const float4*)x;
+  };
+  auto ld1 = [](const float* x) -> float {
+    if constexpr (SC1) return ld_sc1(x); else return *x;
+  };
+  float4 pv[NR][CH];
+  float2 ml[NR];
+  size_t row0[NR];
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const int rr = min(r, nr - 1);
+    row0[r] = (((size_t)b * a.Hq + hs[rr]) * a.Tq + ts[rr]) * a.nsplit;
+    const float* po = a.part_o + row0[r] * a.D + 4 * q;
+#pragma unroll
+    for (int j = 0; j < CH; j++) pv[r][j] = ld4(po + (size_t)min(p + j * P, ns - 1) * a.D);
+    ml[r] = make_float2(-INFINITY, 0.f);
+    if (lane < ns) ml[r] = make_float2(ld1(a.part_ml + (row0[r] + lane) * 2), ld1(a.part_ml + (row0[r] + lane) * 2 + 1));
+  }
+#pragma unroll
+  for (int r = 0; r < NR; r++) {
+    const float M = wave_max(ml[r].x);
+    const float w = ml[r].x == -INFINITY ? 0.f : __expf(ml[r].x - M);
+    const float L = wave_sum(w * ml[r].y);
+    const float invL = L > 0.f ? 1.f / L : 0.f;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < CH; j++) {
+      const int s = p + j * P;
+      // an unused split holds unwritten bytes: select, never multiply
+      const float ws = __shfl(w, s & 63, 64);
+      const bool on = s < ns && ws != 0.f;
+      o.x += on ? ws * pv[r][j].x : 0.f; o.y += on ? ws * pv[r][j].y : 0.f;
+      o.z += on ? ws * pv[r][j].z : 0.f; o.w += on ? ws * pv[r][j].w : 0.f;
+    }
+    for (int off = Q; off < 64; off <<= 1) {
+      o.x += __shfl_xor(o.x, off, 64); o.y += __shfl_xor(o.y, off, 64);
+      o.z += __shfl_xor(o.z, off, 64); o.w += __shfl_xor(o.w, off, 64);
+    }
+    if (p == 0 && r < nr) {
+      uint16_t* out = a.out + (((size_t)b * a.Tq + ts[r]) * a.Hq + hs[r]) * a.D + 4 * q;
+      *(uint2*)out = make_uint2(pack2<T>(o.x * invL, o.y * invL), pack2<T>(o.z * invL, o.w * invL));
+    }
+  }
+  return true;
 }
 
 // merge the nsplit partial (o, m, l) of one (b, h, t) row: split weights
@@ -740,54 +819,9 @@ __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int 
     __syncthreads();
     return;
   }
-  const int Q = a.D / 4;                             // float4 quads per partial row
-  if (ns <= 64 && (Q == 16 || Q == 32 || Q == 64)) {
-    // one memory round trip: lane (quad q, phase p) requests its partial quads
-    // of splits p, p + P, ... together with its (m, l) pair BEFORE any of them
-    // is needed (the weights only scale what is already in flight); the P
-    // phases are summed with shuffles.  The per-split loop below waited on
-    // one dependent L2 round trip per 4 splits (5.8 us at 16 splits, B = 1).
-    constexpr int CH = 8;                            // quads in flight per lane per round
-    const int P = 64 / Q, q = lane % Q, p = lane / Q;
-    const float* po = a.part_o + row0 * a.D + 4 * q;
-    auto ld4 = [&](const float* x) -> float4 {
-      if constexpr (SC1) return make_float4(ld_sc1(x), ld_sc1(x + 1), ld_sc1(x + 2), ld_sc1(x + 3));
-      else return *(const float4*)x;
-    };
-    float4 pv[CH];
-#pragma unroll
-    for (int j = 0; j < CH; j++) pv[j] = ld4(po + (size_t)min(p + j * P, ns - 1) * a.D);
-    float2 ml = make_float2(-INFINITY, 0.f);
-    if (lane < ns) ml = make_float2(ld(a.part_ml + (row0 + lane) * 2), ld(a.part_ml + (row0 + lane) * 2 + 1));
-    M = wave_max(ml.x);
-    const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
-    L = wave_sum(w * ml.y);
-    const float invL = L > 0.f ? 1.f / L : 0.f;
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s0 = 0; s0 < ns; s0 += CH * P) {
-      if (s0 > 0) {
-#pragma unroll
-        for (int j = 0; j < CH; j++) pv[j] = ld4(po + (size_t)min(s0 + p + j * P, ns - 1) * a.D);
-      }
-#pragma unroll
-      for (int j = 0; j < CH; j++) {
-        const int s = s0 + p + j * P;
-        // an unused split holds unwritten bytes: select, never multiply
-        const float ws = __shfl(w, s & 63, 64);
-        const bool on = s < ns && ws != 0.f;
-        o.x += on ? ws * pv[j].x : 0.f; o.y += on ? ws * pv[j].y : 0.f;
-        o.z += on ? ws * pv[j].z : 0.f; o.w += on ? ws * pv[j].w : 0.f;
-      }
-    }
-    for (int off = Q; off < 64; off <<= 1) {
-      o.x += __shfl_xor(o.x, off, 64); o.y += __shfl_xor(o.y, off, 64);
-      o.z += __shfl_xor(o.z, off, 64); o.w += __shfl_xor(o.w, off, 64);
-    }
-    if (p == 0) {
-      uint16_t* out = a.out + (((size_t)b * a.Tq + t) * a.Hq + h) * a.D + 4 * q;
-      *(uint2*)out = make_uint2(pack2<T>(o.x * invL, o.y * invL), pack2<T>(o.z * invL, o.w * invL));
-    }
-    return;
+  {
+    const int hs[1] = {h}, ts[1] = {t};
+    if (combine_fast<T, SC1, 1>(a, b, hs, ts, 1)) return;
   }
   if (ns <= 64) {
     // one (m, l) pair per lane, loaded once

@@ -147,6 +147,8 @@ void launch_attn_prefill(bool bf16, const AttnPrefillArgs& a, hipStream_t st);
 // ---- elementwise & misc (misc.hip) ------------------------------------------
 void launch_rwkv4_wkv(const float* decay, const float* first, const float* k, const float* v, float* out,
                       float* num, float* den, float* mx, int B, int T, int C, hipStream_t st);
+void launch_rwkv5_wkv(const float* w, const float* u, const float* r, const float* k, const float* v, float* out,
+                      float* state, int B, int T, int H, int S, hipStream_t st);
 void launch_softmax_rows(bool bf16, uint16_t* x, int64_t rows, int L, hipStream_t st);
 void launch_glu(bool bf16, const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act,
                 hipStream_t st);

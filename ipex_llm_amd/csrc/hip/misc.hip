@@ -738,4 +738,85 @@ void launch_rwkv4_wkv(const float* decay, const float* first, const float* k, co
                      mx, B, T, C);
 }
 
+// RWKV-5 WKV (xe_linear.rwkv_linear_attention_v5, SRC/transformers/models/
+// rwkv5.py:76-119): per (batch, head) an S x S f32 state, for every step
+//   out_t[j] = sum_i r_t[i] (u[i] k_t[i] v_t[j] + s[i][j])
+//   s[i][j]  = k_t[i] v_t[j] + w[i] s[i][j]            (w = exp(-exp(decay)))
+// One workgroup of S threads per (batch, head): thread j owns state column j
+// in registers (coalesced [i][j] rows in memory).  r / k / v of a chunk of
+// RC steps are staged through LDS (coalesced loads, broadcast reads); the
+// per-step scalar sum_i r u k is computed once per step by one lane while
+// staging, so the inner loop is 2 FMAs + 1 MUL per key dim.
+template <int S>
+__global__ void __launch_bounds__(S) rwkv5_wkv_kernel(const float* __restrict__ w, const float* __restrict__ u,
+                                                      const float* __restrict__ r, const float* __restrict__ k,
+                                                      const float* __restrict__ v, float* __restrict__ out,
+                                                      float* __restrict__ state, int T, int H) {
+  constexpr int RC = 32;
+  __shared__ float rs[RC][S], ks[RC][S], vs[RC][S], ws[S], us[S], ruk[RC];
+  const int bh = blockIdx.x, h = bh % H, j = threadIdx.x;
+  const int b = bh / H;
+  float* st = state + (size_t)bh * S * S + j;
+  float s[S];
+#pragma unroll
+  for (int i = 0; i < S; i++) s[i] = st[(size_t)i * S];
+  ws[j] = w[h * S + j];
+  us[j] = u[h * S + j];
+  const size_t ld = (size_t)H * S;
+  const size_t base = (size_t)b * T * ld + (size_t)h * S + j;
+  for (int t0 = 0; t0 < T; t0 += RC) {
+    const int nt = min(RC, T - t0);
+    __syncthreads();
+    for (int tt = 0; tt < nt; tt++) {
+      const size_t o = base + (size_t)(t0 + tt) * ld;
+      rs[tt][j] = r[o];
+      ks[tt][j] = k[o];
+      vs[tt][j] = v[o];
+    }
+    __syncthreads();
+    // sum_i r u k per step: thread j reduces step j % RC over its slice of i
+    // (S / RC threads per step), combined with shuffles
+    {
+      constexpr int PER = S / RC > 0 ? S / RC : 1;
+      const int tt = j % RC, part = j / RC;
+      float acc = 0.f;
+      if (tt < nt)
+        for (int i = part; i < S; i += PER) acc += rs[tt][i] * ks[tt][i] * us[i];
+      for (int off = RC; off < S && off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
+      if constexpr (S > 64) {
+        // two waves: the second wave's partial sums are added through LDS
+        __shared__ float half[RC];
+        if (j >= 64 && j < 64 + RC) half[tt] = acc;
+        __syncthreads();
+        if (j < RC) ruk[tt] = acc + half[tt];
+      } else {
+        if (j < RC) ruk[tt] = acc;
+      }
+    }
+    __syncthreads();
+    for (int tt = 0; tt < nt; tt++) {
+      const float vj = vs[tt][j];
+      float o0 = vj * ruk[tt], o1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < S; i += 2) {
+        o0 = __builtin_fmaf(rs[tt][i], s[i], o0);
+        o1 = __builtin_fmaf(rs[tt][i + 1], s[i + 1], o1);
+        s[i] = __builtin_fmaf(ws[i], s[i], ks[tt][i] * vj);
+        s[i + 1] = __builtin_fmaf(ws[i + 1], s[i + 1], ks[tt][i + 1] * vj);
+      }
+      out[base + (size_t)(t0 + tt) * ld] = o0 + o1;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < S; i++) st[(size_t)i * S] = s[i];
+}
+
+void launch_rwkv5_wkv(const float* w, const float* u, const float* r, const float* k, const float* v, float* out,
+                      float* state, int B, int T, int H, int S, hipStream_t st) {
+  const dim3 grid(B * H);
+  if (S == 32) hipLaunchKernelGGL(rwkv5_wkv_kernel<32>, grid, dim3(32), 0, st, w, u, r, k, v, out, state, T, H);
+  else if (S == 64) hipLaunchKernelGGL(rwkv5_wkv_kernel<64>, grid, dim3(64), 0, st, w, u, r, k, v, out, state, T, H);
+  else hipLaunchKernelGGL(rwkv5_wkv_kernel<128>, grid, dim3(128), 0, st, w, u, r, k, v, out, state, T, H);
+}
+
 }  // namespace illm

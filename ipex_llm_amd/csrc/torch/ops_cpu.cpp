@@ -150,6 +150,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("attn_decode_rope(Tensor part, Tensor? bias, Tensor cos_sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int Hq, int rot_dim, bool interleaved, float q_scale, ScalarType dtype) -> Tensor");
   m.def("gemm_glu(Tensor x, Tensor blob, int fmt, int n, int k, int act) -> Tensor");
   m.def("rwkv_wkv4(Tensor time_decay, Tensor time_first, Tensor k, Tensor v, Tensor(a!) num, Tensor(b!) den, Tensor(c!) mx) -> Tensor");
+  m.def("rwkv_wkv5(Tensor w, Tensor u, Tensor r, Tensor k, Tensor v, Tensor(a!) state) -> Tensor");
   m.def("gemv_norm_in(Tensor acc_in, Tensor residual, Tensor(a!) res_out, Tensor norm_w, float eps, bool unit_offset, Tensor blob, int fmt, int n, int k, int epi, int act, Tensor(b!)? acc_out=None, Tensor(c!)? zero=None) -> Tensor");
   m.def("embedding_lowbit(Tensor blob, int fmt, int n, int k, Tensor ids, ScalarType dtype) -> Tensor");
   m.def("moe_gemv(Tensor x, Tensor blob, int fmt, int n, int k, Tensor off, Tensor rows, int xdiv, int npairs, int epi, int ksplit, int act) -> Tensor");

@@ -308,6 +308,28 @@ Tensor rwkv_wkv4(const Tensor& time_decay, const Tensor& time_first, const Tenso
   return out.to(k.scalar_type());
 }
 
+// RWKV-5 WKV over r/k/v [B, T, H, S] (f32 compute); w = exp(-exp(time_decay)),
+// u = time_first, both [H, S]; state [B, H, S, S] f32 updated in place
+Tensor rwkv_wkv5(const Tensor& w, const Tensor& u, const Tensor& r, const Tensor& k, const Tensor& v, Tensor& state) {
+  TORCH_CHECK(k.is_cuda() && k.dim() == 4 && r.sizes() == k.sizes() && v.sizes() == k.sizes(),
+              "rwkv_wkv5: r, k, v [B, T, H, S] on the GPU");
+  c10::DeviceGuard g(k.device());
+  const int64_t B = k.size(0), T = k.size(1), H = k.size(2), S = k.size(3);
+  TORCH_CHECK(S == 32 || S == 64 || S == 128, "rwkv_wkv5: head size must be 32, 64 or 128");
+  TORCH_CHECK(state.scalar_type() == at::kFloat && state.is_contiguous() && state.dim() == 4 &&
+                  state.size(0) == B && state.size(1) == H && state.size(2) == S && state.size(3) == S,
+              "rwkv_wkv5: state must be contiguous f32 [B, H, S, S]");
+  Tensor rf = r.to(at::kFloat).contiguous(), kf = k.to(at::kFloat).contiguous(), vf = v.to(at::kFloat).contiguous();
+  Tensor wf = w.to(at::kFloat).contiguous(), uf = u.to(at::kFloat).contiguous();
+  TORCH_CHECK(wf.numel() == H * S && uf.numel() == H * S, "rwkv_wkv5: w / u [H, S]");
+  Tensor out = at::empty_like(kf);
+  if (B * H > 0 && T > 0)
+    illm::launch_rwkv5_wkv(wf.data_ptr<float>(), uf.data_ptr<float>(), rf.data_ptr<float>(), kf.data_ptr<float>(),
+                           vf.data_ptr<float>(), out.data_ptr<float>(), state.data_ptr<float>(), (int)B, (int)T,
+                           (int)H, (int)S, cur_stream());
+  return out;
+}
+
 // split-K GEMV accumulated with f32 atomics into acc [M, n] (zero on entry;
 // the consumer -- add_rms_norm / rope_kv_fused with zero_*=True -- reads the
 // single slab and re-zeroes it, so no ks-slab reduction is ever needed)
@@ -1164,6 +1186,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv_norm_in", &gemv_norm_in);
   m.impl("gemm_glu", &gemm_glu);
   m.impl("rwkv_wkv4", &rwkv_wkv4);
+  m.impl("rwkv_wkv5", &rwkv_wkv5);
   m.impl("attn_decode_rope", &attn_decode_rope);
   m.impl("gemm", &gemm);
   m.impl("attn_decode_split", &attn_decode_split);

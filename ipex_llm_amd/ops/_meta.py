@@ -180,3 +180,8 @@ def _(x, blob, fmt, n, k, act):
 @register_fake("ipex_llm_amd::rwkv_wkv4")
 def _(time_decay, time_first, k, v, num, den, mx):
     return torch.empty_like(k)
+
+
+@register_fake("ipex_llm_amd::rwkv_wkv5")
+def _(w, u, r, k, v, state):
+    return torch.empty_like(k, dtype=torch.float32)

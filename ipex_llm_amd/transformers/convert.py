@@ -267,6 +267,9 @@ def _optimize_post(model: nn.Module):
     if mt == "rwkv":
         from ..models.rwkv import patch_rwkv
         patch_rwkv()
+    if mt == "rwkv5":
+        from ..models.rwkv import patch_rwkv5
+        patch_rwkv5(model)
     if (mt in NATIVE_ARCHS or mt in MOE_ARCHS) and getattr(model, "_illm_pre", False):
         from .hf_native import attach_native
         attach_native(model)
