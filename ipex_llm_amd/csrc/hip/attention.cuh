@@ -876,23 +876,112 @@ __device__ __forceinline__ void combine_row(const AttnDecodeArgs& a, int b, int 
   __syncthreads();
 }
 
+// fused-RoPE decode: every split has read the qkv accumulator by now, so the
+// combine re-zeroes it for the next layer's atomic GEMV (block (h, b): q head
+// h and the k/v column blocks dealt over the Hq blocks -- all of them are
+// covered for any Hq / Hkv ratio, MHA included)
+__device__ __forceinline__ void combine_zero_rq(const AttnDecodeArgs& a, int h, int b, int tid, int nthr) {
+  float* row = (float*)a.rq_part + (size_t)b * a.rq_ld;
+  const int D = a.D;
+  for (int d = tid * 4; d < D; d += 4 * nthr) *(float4*)(row + h * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int hh = h; hh < 2 * a.Hkv; hh += a.Hq)
+    for (int d = tid * 4; d < D; d += 4 * nthr)
+      *(float4*)(row + (a.Hq + hh) * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(64) attn_combine_kernel(const AttnDecodeArgs a) {
   __shared__ float wsh[1024];
   combine_row<T>(a, blockIdx.z, blockIdx.x, blockIdx.y, wsh);
-  if (a.rq_part != nullptr && blockIdx.y == 0) {
-    // fused-RoPE decode: every split has read the qkv accumulator by now, so
-    // re-zero it for the next layer's atomic GEMV (block (h, b): q head h and,
-    // for h < 2 Hkv, k/v head h)
-    float* row = (float*)a.rq_part + (size_t)blockIdx.z * a.rq_ld;
-    const int h = blockIdx.x, D = a.D;
-    for (int d = threadIdx.x * 4; d < D; d += 256) *(float4*)(row + h * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
-    // the 2 Hkv k/v column blocks are dealt over the Hq blocks (all of them
-    // are covered for any Hq / Hkv ratio, MHA included)
-    for (int hh = h; hh < 2 * a.Hkv; hh += a.Hq)
-      for (int d = threadIdx.x * 4; d < D; d += 256)
-        *(float4*)(row + (a.Hq + hh) * D + d) = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.rq_part != nullptr && blockIdx.y == 0) combine_zero_rq(a, blockIdx.x, blockIdx.z, threadIdx.x, 64);
+}
+
+// long contexts (more splits than one wave merges in a round trip; 32 K keys
+// = 513 splits): 8 waves per (b, h, t) row.  Split weights for every split go
+// to LDS first; then lane (quad q, phase p) of wave w streams splits
+// w P + p + j (8 P) with 16 partial quads in flight per round, and the
+// (wave, phase) partial sums meet in LDS.  One wave looping over the splits
+// (the kernel above) spent 57.7 us per layer at 32 K keys, longer than the
+// split attention itself (37.2 us).
+constexpr int CW_NW = 8, CW_MAXS = 4096;
+template <typename T>
+__global__ void __launch_bounds__(CW_NW * 64) attn_combine_wide_kernel(const AttnDecodeArgs a) {
+  __shared__ float wsh[CW_MAXS];
+  __shared__ float4 red[CW_NW * 64];
+  __shared__ float rsum[CW_NW];
+  const int h = blockIdx.x, t = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int len = a.seq_lens[b];
+  const int ns = min(a.nsplit, (len + SPLIT - 1) / SPLIT);
+  const size_t row0 = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit;
+  // ---- split weights: block max, exp, block sum of w * l
+  float mx = -INFINITY;
+  for (int s = tid; s < ns; s += CW_NW * 64) mx = fmaxf(mx, a.part_ml[(row0 + s) * 2]);
+  mx = wave_max(mx);
+  if (lane == 0) rsum[wave] = mx;
+  __syncthreads();
+  float M = rsum[0];
+#pragma unroll
+  for (int w = 1; w < CW_NW; w++) M = fmaxf(M, rsum[w]);
+  float L = 0.f;
+  for (int s = tid; s < ns; s += CW_NW * 64) {
+    const float2 ml = *(const float2*)(a.part_ml + (row0 + s) * 2);
+    const float w = ml.x == -INFINITY ? 0.f : __expf(ml.x - M);
+    wsh[s] = w;
+    L += w * ml.y;
   }
+  L = wave_sum(L);
+  __syncthreads();                                  // rsum (max) read by all
+  if (lane == 0) rsum[wave] = L;
+  __syncthreads();
+  L = 0.f;
+#pragma unroll
+  for (int w = 0; w < CW_NW; w++) L += rsum[w];
+  const float invL = L > 0.f ? 1.f / L : 0.f;
+  // ---- weighted sum of the partial rows
+  const int Q = a.D / 4, P = 64 / Q, q = lane % Q, p = lane / Q;
+  const int gp = wave * P + p, GS = CW_NW * P;     // phase of this lane, phase stride
+  float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p < P) {
+    constexpr int U = 16;
+    const float* po = a.part_o + row0 * a.D + 4 * q;
+    for (int s0 = gp; s0 < ns; s0 += U * GS) {
+      float4 pv[U];
+#pragma unroll
+      for (int j = 0; j < U; j++) pv[j] = *(const float4*)(po + (size_t)min(s0 + j * GS, ns - 1) * a.D);
+#pragma unroll
+      for (int j = 0; j < U; j++) {
+        const int s = s0 + j * GS;
+        // an unused split holds unwritten bytes: select, never multiply
+        const float ws = s < ns ? wsh[s] : 0.f;
+        const bool on = ws != 0.f;
+        o.x += on ? ws * pv[j].x : 0.f; o.y += on ? ws * pv[j].y : 0.f;
+        o.z += on ? ws * pv[j].z : 0.f; o.w += on ? ws * pv[j].w : 0.f;
+      }
+    }
+  }
+  red[tid] = o;
+  __syncthreads();
+  if (tid < Q) {
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int w = 0; w < CW_NW; w++)
+      for (int pp = 0; pp < P; pp++) {
+        const float4 v = red[w * 64 + pp * Q + tid];
+        r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+      }
+    uint16_t* out = a.out + (((size_t)b * a.Tq + t) * a.Hq + h) * a.D + 4 * tid;
+    *(uint2*)out = make_uint2(pack2<T>(r.x * invL, r.y * invL), pack2<T>(r.z * invL, r.w * invL));
+  }
+  if (a.rq_part != nullptr && t == 0) combine_zero_rq(a, h, b, tid, CW_NW * 64);
+}
+
+// the combine launch for a.nsplit splits (the max over the batch)
+template <typename T>
+static void launch_combine(const AttnDecodeArgs& a, hipStream_t st) {
+  if (a.nsplit > 24 && a.nsplit <= CW_MAXS && a.D % 4 == 0)
+    hipLaunchKernelGGL((attn_combine_wide_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(CW_NW * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
 }
 
 template <typename T, int D, int RT, bool PVM = false>
@@ -915,7 +1004,7 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
       if (latev) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, true, PVM>), grid, dim3(64), 0, st, a);
       else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, false, PVM>), grid, dim3(64), 0, st, a);
       if (a.counters == nullptr && !a.no_combine)
-        hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
+        launch_combine<T>(a, st);
       return;
     }
   }
@@ -929,7 +1018,7 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
     else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, false, false, PVM>), grid, dim3(64), 0, st, a);
   }
   if (a.counters == nullptr && !a.no_combine)
-    hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
+    launch_combine<T>(a, st);
 }
 
 template <typename T, int D>
@@ -949,7 +1038,7 @@ void launch_d(const AttnDecodeArgs& a, hipStream_t st) {
   if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_decode_kernel<T, D, 1>), grid, dim3(64), 0, st, a);
   else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_decode_kernel<T, D, 2>), grid, dim3(64), 0, st, a);
   else hipLaunchKernelGGL((attn_decode_kernel<T, D, 0>), grid, dim3(64), 0, st, a);
-  if (!a.no_combine) hipLaunchKernelGGL((attn_combine_kernel<T>), dim3(a.Hq, a.Tq, a.B), dim3(64), 0, st, a);
+  if (!a.no_combine) launch_combine<T>(a, st);
 }
 
 }  // namespace illm

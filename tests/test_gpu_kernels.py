@@ -175,6 +175,38 @@ def test_attn_decode_long_context_combine(cuda):
     assert _rel(got[0, 0].float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("D", [64, 80, 128, 256])
+def test_attn_decode_wide_combine(cuda, D):
+    """25..4096 splits: the 8-wave combine (split weights in LDS, partial quads
+    streamed by (wave, phase)) vs an fp32 reference, uneven batch lengths"""
+    torch.manual_seed(6)
+    Hq, Hkv, bs = 4, 2, 64
+    L = [3000, 1700]
+    nblk = sum((x + bs - 1) // bs for x in L)
+    kc = torch.randn(nblk, Hkv, bs, D, device=cuda).bfloat16()
+    vc = torch.randn(nblk, Hkv, bs, D, device=cuda).bfloat16()
+    mb = max((x + bs - 1) // bs for x in L)
+    perm = torch.randperm(nblk, device=cuda).to(torch.int32)
+    bt = torch.zeros(2, mb, dtype=torch.int32, device=cuda)
+    o = 0
+    for b, x in enumerate(L):
+        n = (x + bs - 1) // bs
+        bt[b, :n] = perm[o:o + n]
+        o += n
+    seq_lens = torch.tensor(L, dtype=torch.int32, device=cuda)
+    q = torch.randn(2, 1, Hq, D, device=cuda).bfloat16()
+    ns = (max(L) + 63) // 64
+    assert 24 < ns <= 4096
+    got = ops.attn_decode(q, kc, vc, bt, seq_lens, ns, D ** -0.5)
+    for b, x in enumerate(L):
+        kk = ops.api.gather_kv(kc, bt, b, x).float()
+        vv = ops.api.gather_kv(vc, bt, b, x).float()
+        for h in range(Hq):
+            s = (kk[:, h // 2] @ q[b, 0, h].float()) * D ** -0.5
+            ref = torch.softmax(s, -1) @ vv[:, h // 2]
+            assert _rel(got[b, 0, h].float(), ref) < 1e-2, (b, h)
+
+
 def test_decode_rope_in_mha_multilayer(cuda):
     """multi-layer MHA (Hq == Hkv) decode: fused-RoPE attention path gives the
     same tokens as the rope_kv launch path (the slab re-zeroing covers every
