@@ -12,15 +12,18 @@
 namespace illm {
 
 // ---- GLU: out[m, i] = act(gu[m, i]) * gu[m, I + i] ---------------------------
+// tile > 0: gate / up interleaved in tile-row groups (the fused gate_up weight
+// layout: columns [2 tile j, 2 tile j + tile) gate, the next tile up)
 template <typename T>
-__global__ void glu_kernel(const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act) {
+__global__ void glu_kernel(const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act, int tile) {
   const int64_t n8 = (int64_t)M * I / 8;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n8;
        v += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = v * 8;
     const int m = (int)(e / I), i = (int)(e % I);
-    const uint4 g = *(const uint4*)(gu + (size_t)m * ld + i);
-    const uint4 u = *(const uint4*)(gu + (size_t)m * ld + I + i);
+    const int gc = tile > 0 ? (i / tile) * 2 * tile + i % tile : i;
+    const uint4 g = *(const uint4*)(gu + (size_t)m * ld + gc);
+    const uint4 u = *(const uint4*)(gu + (size_t)m * ld + gc + (tile > 0 ? tile : I));
     const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, uw[4] = {u.x, u.y, u.z, u.w};
     uint32_t o[4];
 #pragma unroll
@@ -36,12 +39,12 @@ __global__ void glu_kernel(const uint16_t* gu, int ld, uint16_t* out, int M, int
   }
 }
 
-void launch_glu(bool bf16, const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act,
+void launch_glu(bool bf16, const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act, int tile,
                 hipStream_t st) {
   const int64_t n8 = (int64_t)M * I / 8;
   const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
-  if (bf16) hipLaunchKernelGGL(glu_kernel<BF16>, dim3(blocks), dim3(256), 0, st, gu, ld, out, M, I, act);
-  else hipLaunchKernelGGL(glu_kernel<F16>, dim3(blocks), dim3(256), 0, st, gu, ld, out, M, I, act);
+  if (bf16) hipLaunchKernelGGL(glu_kernel<BF16>, dim3(blocks), dim3(256), 0, st, gu, ld, out, M, I, act, tile);
+  else hipLaunchKernelGGL(glu_kernel<F16>, dim3(blocks), dim3(256), 0, st, gu, ld, out, M, I, act, tile);
 }
 
 // ---- in-place row softmax (eager attention weights) -------------------------

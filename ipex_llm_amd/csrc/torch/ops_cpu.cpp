@@ -133,7 +133,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("layer_norm(Tensor x, Tensor? w, Tensor? b, float eps) -> Tensor");
   m.def("rope_kv(Tensor qkv, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slots, Tensor pos, Tensor inv_freq, Tensor? q_norm, Tensor? k_norm, float norm_eps, float q_scale, int Hq, int Hkv, int D, int rot_dim, bool interleaved, int kv_fp8, float k_scale, float v_scale) -> ()");
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int kv_fp8, float k_scale, float v_scale, Tensor? alibi) -> Tensor");
-  m.def("glu(Tensor gu, int act) -> Tensor");
+  m.def("glu(Tensor gu, int act, int tile=0) -> Tensor");
   m.def("attn_softmax_(Tensor(a!) x) -> ()");
   m.def("reduce_partials(Tensor ws, Tensor? bias, ScalarType dtype) -> Tensor");
   m.def("moe_topk(Tensor logits, int k, bool renorm, int scoring) -> (Tensor, Tensor)");

@@ -889,16 +889,17 @@ Tensor gemv_attn(const Tensor& po, const Tensor& pml, const Tensor& seq_lens, co
 }
 
 
-Tensor glu(const Tensor& gu, int64_t act) {
+Tensor glu(const Tensor& gu, int64_t act, int64_t tile) {
   c10::DeviceGuard g(gu.device());
   const bool bf16 = is_bf16(gu);
   Tensor x = gu.contiguous();
   const int64_t I2 = x.size(-1), M = x.numel() / I2, I = I2 / 2;
-  TORCH_CHECK(I % 8 == 0, "glu: intermediate size must be a multiple of 8");
+  TORCH_CHECK(I % 8 == 0 && (tile == 0 || (tile % 8 == 0 && I % tile == 0)),
+              "glu: intermediate size must be a multiple of 8 (and of the interleave tile)");
   auto shape = x.sizes().vec();
   shape.back() = I;
   Tensor out = at::empty(shape, x.options());
-  if (M > 0) illm::launch_glu(bf16, p16(x), (int)I2, m16(out), (int)M, (int)I, (int)act, cur_stream());
+  if (M > 0) illm::launch_glu(bf16, p16(x), (int)I2, m16(out), (int)M, (int)I, (int)act, (int)tile, cur_stream());
   return out;
 }
 

@@ -60,7 +60,7 @@ def _(x):
 
 
 @register_fake("ipex_llm_amd::glu")
-def _(gu, act):
+def _(gu, act, tile=0):
     shape = list(gu.shape)
     shape[-1] //= 2
     return gu.new_empty(shape)

@@ -194,9 +194,16 @@ def layer_norm(x, w, b, eps):
     return R.layer_norm(x, w, b, eps)
 
 
-def glu(gu, act=0):
-    if _native(gu) and (gu.shape[-1] // 2) % 8 == 0:
-        return _ops().glu(gu, act)
+def glu(gu, act=0, tile=0):
+    """act(gate) * up; gate / up are the two halves of the last dim, or
+    (tile > 0) interleaved in groups of ``tile`` columns (the fused gate_up
+    weight layout)."""
+    I = gu.shape[-1] // 2
+    if _native(gu) and I % 8 == 0 and (tile == 0 or (tile % 8 == 0 and I % tile == 0)):
+        return _ops().glu(gu, act, tile)
+    if tile:
+        x = gu.reshape(*gu.shape[:-1], I // tile, 2, tile)
+        gu = torch.cat([x[..., 0, :].reshape(*gu.shape[:-1], I), x[..., 1, :].reshape(*gu.shape[:-1], I)], -1)
     return R.glu(gu, act)
 
 

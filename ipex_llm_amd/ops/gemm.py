@@ -1,12 +1,17 @@
 """Prefill-size (M > 64) low-bit GEMM dispatch.
 
-M <= 1536: the MFMA kernel with in-register dequant (``csrc/hip/gemm.hip``:
+Two paths: the MFMA kernel with in-register dequant (``csrc/hip/gemm.hip``:
 f16 MFMA, weights decoded straight from the tiled blob, never
-materialised).  Larger M: dequantize to a transient dense weight + library
-GEMM, which is faster there (measured on MI355X, Llama-3-8B shapes, see
-profiles/prefill_gemm_r1.jsonl: fused 600-680 TF vs library 1.0-1.2 PF at
-M = 4096, parity at M = 1024).  ``ILLM_GEMM_LIB=1`` / ``ILLM_GEMM_FUSED=1``
-force either path (A/B measurements).
+materialised), and dequantize to a transient dense weight + library GEMM
+(hipBLASLt).  Measured on MI355X at Llama-3-8B shapes (sym_int4,
+profiles/prefill_gemm_r2_sweep.jsonl): the library path wins from M = 512 on
+for every projection (M = 1024: qkv 64.7 vs 90.9 us, o 49.5 vs 67.7,
+gate_up 256.6 vs 296.6, down 142.2 vs 205.4) and at M = 256 for the
+N = 4096 projections, whose 128 x 128 fused grid leaves most CUs idle (down
+77 vs 181 us); the fused kernel keeps M <= 128 and the wide-N projections up
+to M = 384 (M = 256: qkv 62 vs 77, gate_up 92 vs 145).  In the model:
+Llama-3-8B first token at 1024 tokens 23.5 -> 21.8 ms.
+``ILLM_GEMM_LIB=1`` / ``ILLM_GEMM_FUSED=1`` force either path (A/B runs).
 """
 from __future__ import annotations
 
@@ -17,13 +22,23 @@ import torch.nn.functional as F
 
 _USE_LIB = os.environ.get("ILLM_GEMM_LIB", "0") == "1"
 _USE_FUSED = os.environ.get("ILLM_GEMM_FUSED", "0") == "1"
-FUSED_MAX_M = 1536
+FUSED_MAX_M = 128          # fused kernel for every shape up to here
+FUSED_WIDE_MAX_M = 384     # ... and for wide projections (N >= FUSED_WIDE_N) up to here
+FUSED_WIDE_N = 6144
+
+
+def use_fused(M: int, n: int) -> bool:
+    if _USE_LIB:
+        return False
+    if _USE_FUSED:
+        return True
+    return M <= FUSED_MAX_M or (M <= FUSED_WIDE_MAX_M and n >= FUSED_WIDE_N)
 
 
 def lowbit_gemm(x, blob, fmt, n, k, bias=None):
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
-    if not _USE_LIB and (M <= FUSED_MAX_M or _USE_FUSED) and hasattr(ops, "gemm"):
+    if use_fused(M, n) and hasattr(ops, "gemm"):
         return ops.gemm(x, blob, fmt, n, k, bias)
     w = ops.dequantize_device(blob, fmt, n, k, x.dtype)
     return F.linear(x, w, bias)
@@ -35,8 +50,7 @@ def lowbit_gemm_glu(x, blob, fmt, n, k, act: int = 0):
     [M, 2I] round trip, no elementwise launches)."""
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
-    if not _USE_LIB and (M <= FUSED_MAX_M or _USE_FUSED) and hasattr(ops, "gemm_glu"):
+    if use_fused(M, n) and hasattr(ops, "gemm_glu"):
         return ops.gemm_glu(x, blob, fmt, n, k, act)
-    from ..models.decoder import deinterleave_glu
-    g, u = deinterleave_glu(lowbit_gemm(x, blob, fmt, n, k))
-    return ((F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")) * u).contiguous()
+    from .api import glu
+    return glu(lowbit_gemm(x, blob, fmt, n, k), act, tile=16)

@@ -136,3 +136,20 @@ def test_hf_eager_family_on_gpu_uses_hip_softmax(cuda, tmp_path):
         api._ops = real
     assert seen and seen[0][-2:] == (16, 16)
     assert ((got - want).norm() / want.norm()).item() < 3e-2
+
+
+@pytest.mark.parametrize("tile", [0, 16])
+def test_glu_kernel_interleaved(cuda, tile):
+    """GLU HIP op over halves (tile 0) and the 16-column gate/up interleave of
+    the fused gate_up weight (the prefill library-GEMM path) vs the reference"""
+    from ipex_llm_amd.models.decoder import deinterleave_glu
+    torch.manual_seed(0)
+    gu = torch.randn(37, 2 * 512, device=cuda).bfloat16()
+    if tile:
+        g, u = deinterleave_glu(gu, tile)
+    else:
+        g, u = gu.chunk(2, -1)
+    want = torch.nn.functional.silu(g.float()).bfloat16().float() * u.float()
+    got = ops.glu(gu, 0, tile=tile)
+    assert torch.ops.ipex_llm_amd.glu is not None
+    assert torch.allclose(got.float(), want, atol=1e-2, rtol=1e-2)
