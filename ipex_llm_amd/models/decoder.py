@@ -449,6 +449,16 @@ class NativeCausalLM(nn.Module):
         a = F.silu(g) if s.act == 0 else F.gelu(g, approximate="tanh")
         return (a * u).contiguous()
 
+    def _prefetch_layer(self, li: int, T: int, dtype, prefetch_dense):
+        L = self.layers[li]
+        mods = [getattr(L.self_attn, "qkv_proj", None), getattr(L.self_attn, "o_proj", None)]
+        if isinstance(L.mlp, NativeMLP):
+            mods += [L.mlp.gate_up_proj, L.mlp.down_proj]
+        items = [(m.weight, m.fmt, m.out_features, m.in_features) for m in mods
+                 if isinstance(m, LowBitLinear) and m.mp_group is None and m.g_idx_map is None
+                 and m.compute_dtype in (None, dtype)]
+        prefetch_dense(items, T, dtype)
+
     # ------------------------------------------------------------------ forward
     def forward_tokens(self, ids: torch.Tensor, pos: torch.Tensor, slots: torch.Tensor, meta: AttnMeta,
                        cache, logits_idx: Optional[torch.Tensor] = None, return_hidden: bool = False,
@@ -483,7 +493,16 @@ class NativeCausalLM(nn.Module):
         nxt_res = lambda r: res_pp[1] if r is res_pp[0] else res_pp[0]
         zero_next = None                # consumed atomic slab the next accumulating GEMV zeroes
         from ..utils import trace as _trace
+        # prefill on the library GEMM path: dense weights of layer li + 1 are
+        # dequantized on a side stream while layer li computes
+        pf = T > ops.GEMV_MAX_M and x.is_cuda and ops.native_gpu(x)
+        if pf:
+            from ..ops.gemm import drop_prefetched, prefetch_dense
+            drop_prefetched()          # entries of an earlier (aborted) forward are keyed by possibly reused pointers
+            self._prefetch_layer(0, T, x.dtype, prefetch_dense)
         for li, layer in enumerate(self.layers):
+            if pf and li + 1 < len(self.layers):
+                self._prefetch_layer(li + 1, T, x.dtype, prefetch_dense)
             if _trace.ENABLED:
                 # per-layer roctx marker (host-side: eager forwards / prefill)
                 with _trace.trace_range(f"layer{li + self.layer_offset}"):
