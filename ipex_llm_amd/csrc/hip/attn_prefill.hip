@@ -58,7 +58,7 @@ __device__ __forceinline__ uint4 pf_load8(const uint8_t* p, float scale) {
 
 // HP = query heads per wave that share one kv head (GQA): every K fragment
 // read from LDS and every transposed V read feeds HP MFMAs.
-template <typename T, int D, int KVF, int HP>
+template <typename T, int D, int KVF, int HP, bool SOFTCAP>
 __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs a) {
   constexpr int EB = KVF == 0 ? 2 : 1;            // cache bytes per element
   constexpr int KSTEP = D / 32;                   // MFMA k-steps over the head dim (QK^T)
@@ -171,23 +171,36 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
     uint32_t pk[HP][4][2];                         // P^T fragments, 16-bit pairs
 #pragma unroll
     for (int j = 0; j < HP; j++) {
-      float tmax = -INFINITY;
+      // soft-cap is a template flag and the mask one uniform branch per tile:
+      // a per-score branch (tanhf's own control flow inlined 16 times) split
+      // the tile loop into ~100 basic blocks, so no MFMA / VALU interleaving
+      // across them (rocprofv3: 3 SALU and 10 VALU per MFMA)
 #pragma unroll
       for (int kb = 0; kb < 4; kb++) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           float v = st[j][kb][i] * sc;
-          if (a.softcap > 0.f) v = a.softcap * tanhf(v / a.softcap);
-          if (!full) {
-            const int key = kt0 + 16 * kb + 4 * g + i;
-            bool ok = key <= qpos && key < L;
-            if (a.sliding_window > 0 && key <= qpos - a.sliding_window) ok = false;
-            v = ok ? v : -INFINITY;
-          }
+          if constexpr (SOFTCAP) v = a.softcap * tanhf(v / a.softcap);
           st[j][kb][i] = v;
-          tmax = fmaxf(tmax, v);
         }
       }
+      if (!full) {
+        const int win = a.sliding_window > 0 ? qpos - a.sliding_window : -1;
+#pragma unroll
+        for (int kb = 0; kb < 4; kb++) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int key = kt0 + 16 * kb + 4 * g + i;
+            const bool ok = key <= qpos && key < L && key > win;
+            st[j][kb][i] = ok ? st[j][kb][i] : -INFINITY;
+          }
+        }
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; kb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) tmax = fmaxf(tmax, st[j][kb][i]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mnew = fmaxf(mrow[j], tmax);
@@ -250,12 +263,18 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
   }
 }
 
+template <typename T, int D, int HP, bool SC>
+static void launch_pf_sc(const AttnPrefillArgs& a, hipStream_t st) {
+  dim3 grid((a.Tq + PF_QB - 1) / PF_QB, a.Hq / HP, a.B);
+  if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_prefill_kernel<T, D, 1, HP, SC>), grid, dim3(256), 0, st, a);
+  else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_prefill_kernel<T, D, 2, HP, SC>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_prefill_kernel<T, D, 0, HP, SC>), grid, dim3(256), 0, st, a);
+}
+
 template <typename T, int D, int HP>
 static void launch_pf_hp(const AttnPrefillArgs& a, hipStream_t st) {
-  dim3 grid((a.Tq + PF_QB - 1) / PF_QB, a.Hq / HP, a.B);
-  if (a.kv_fp8 == 1) hipLaunchKernelGGL((attn_prefill_kernel<T, D, 1, HP>), grid, dim3(256), 0, st, a);
-  else if (a.kv_fp8 == 2) hipLaunchKernelGGL((attn_prefill_kernel<T, D, 2, HP>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_prefill_kernel<T, D, 0, HP>), grid, dim3(256), 0, st, a);
+  if (a.softcap > 0.f) launch_pf_sc<T, D, HP, true>(a, st);
+  else launch_pf_sc<T, D, HP, false>(a, st);
 }
 
 template <typename T, int D>
