@@ -139,6 +139,8 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
 #pragma unroll
   for (int j = 0; j < HP; j++) { mrow[j] = -INFINITY; lpart[j] = 0.f; }
   const float sc = a.scale;
+  constexpr float kLog2e = 1.4426950408889634f;
+  const float sc2 = a.scale * kLog2e;
 
   if (ntile > 0) {
     load_tile(0);
@@ -179,8 +181,10 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
       for (int kb = 0; kb < 4; kb++) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          float v = st[j][kb][i] * sc;
-          if constexpr (SOFTCAP) v = a.softcap * tanhf(v / a.softcap);
+          // scores in the exp2 domain (scale * log2 e folded in): p = exp2(v - m)
+          float v;
+          if constexpr (SOFTCAP) v = a.softcap * tanhf(st[j][kb][i] * sc / a.softcap) * kLog2e;
+          else v = st[j][kb][i] * sc2;
           st[j][kb][i] = v;
         }
       }
@@ -204,7 +208,10 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mnew = fmaxf(mrow[j], tmax);
-      const float alpha = mrow[j] == -INFINITY ? 0.f : __expf(mrow[j] - mnew);
+      // nothing seen yet (mrow = -inf): exp2(-inf) = 0 clears the empty O; a row
+      // still fully masked keeps alpha 1 and a finite max of 0 for the exp2 below
+      const float alpha = mnew == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(mrow[j] - mnew);
+      const float msafe = mnew == -INFINITY ? 0.f : mnew;
       mrow[j] = mnew;
       lpart[j] *= alpha;
 #pragma unroll
@@ -216,7 +223,7 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
         float p[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          p[i] = st[j][kb][i] == -INFINITY ? 0.f : __expf(st[j][kb][i] - mnew);
+          p[i] = __builtin_amdgcn_exp2f(st[j][kb][i] - msafe);      // masked: exp2(-inf) = 0
           lpart[j] += p[i];
         }
         pk[j][kb][0] = pack2<T>(p[0], p[1]);
