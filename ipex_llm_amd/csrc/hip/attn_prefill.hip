@@ -69,9 +69,18 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
   __shared__ __attribute__((aligned(16))) uint16_t ks[2][PF_KT * D];
   __shared__ __attribute__((aligned(16))) uint16_t vs[2][PF_KT * D];
 
-  const int nqb = gridDim.x;
-  const int qb = nqb - 1 - blockIdx.x;            // heaviest (latest) query block first
-  const int h0 = blockIdx.y * HP, b = blockIdx.z;
+  // causal work per query block grows with its index.  Block order: heaviest
+  // query blocks of every (head, batch) first (longest-processing-time first
+  // for the dynamic dispatch); when the whole grid is resident at once (<= 2
+  // workgroups per CU: 64 KiB of LDS each) the second half runs the light
+  // blocks in ascending order instead, so workgroups i and i + grid/2 (one CU)
+  // pair up to the same total (T = 1024: every CU 17 tiles instead of up to 32)
+  const int nqb = gridDim.x, nother = gridDim.y * gridDim.z;
+  const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int rank = lin / nother, other = lin % nother;
+  const int half = (nqb + 1) / 2;
+  const int qb = (nqb * nother <= 512 && rank >= half) ? rank - half : nqb - 1 - rank;
+  const int h0 = (other % gridDim.y) * HP, b = other / gridDim.y;
   const int kvh = h0 / (a.Hq / a.Hkv);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
@@ -213,10 +222,13 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
       const float alpha = mnew == -INFINITY ? 1.f : __builtin_amdgcn_exp2f(mrow[j] - mnew);
       const float msafe = mnew == -INFINITY ? 0.f : mnew;
       mrow[j] = mnew;
-      lpart[j] *= alpha;
+      // O rescale only when some row max of the wave moved (wave-uniform)
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.f) != 0) {
+        lpart[j] *= alpha;
 #pragma unroll
-      for (int d = 0; d < DT; d++) {
-        o[j][d][0] *= alpha; o[j][d][1] *= alpha; o[j][d][2] *= alpha; o[j][d][3] *= alpha;
+        for (int d = 0; d < DT; d++) {
+          o[j][d][0] *= alpha; o[j][d][1] *= alpha; o[j][d][2] *= alpha; o[j][d][3] *= alpha;
+        }
       }
 #pragma unroll
       for (int kb = 0; kb < 4; kb++) {
