@@ -137,59 +137,77 @@ void launch_quantize_device(int fmt, int in_kind, const void* w, int64_t n, int6
 }
 
 // ---- dequantize on device: tiled blob -> dense [n, k] ------------------------
-// One lane per 16-B code vector of the tiled blob (the same lane mapping the
-// GEMV uses), so codes are read with full 1 KiB wave loads and each lane
-// writes 8-element (16-B) row segments.  Used by the M>64 prefill path.
-// The format is a template parameter: the per-element code decode
-// (hd_code_value / nibble position / bits) folds to constants (a runtime
-// switch per element held this kernel to ~1.2 TB/s of output on MI355X).
+// Used by the library-GEMM prefill path (a transient dense weight per call).
+// A workgroup of 4 waves decodes 4 consecutive 128-k chunks of one 16-row
+// tile: each lane decodes its MFMA-fragment codes (row l & 15, k-group l >> 4,
+// the GEMV's lane mapping, full 1 KiB wave loads) into an LDS [16][512] row
+// block, then every wave store writes 1 KiB of ONE output row.  Storing the
+// fragments directly left each wave store as 16 separate 64-B row pieces
+// (~4.2 TB/s of weight bytes in + out on MI355X).  The format is a template
+// parameter so the per-element code decode folds to constants.
+constexpr int DQ_CH = 4;                                  // chunks per workgroup
+constexpr int DQ_LD = DQ_CH * CHUNK_K + 8;                // LDS row stride (elements)
 template <typename T, int FMT>
 __global__ void __launch_bounds__(256) dequantize_tiled_kernel(const uint8_t* blob, int64_t n, int64_t k,
                                                                uint16_t* out) {
   constexpr int fmt = FMT;
   constexpr int bits = fmt_bits(fmt);
+  __shared__ __attribute__((aligned(16))) uint16_t rows[TILE_N * DQ_LD];
   const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
-  const int64_t NT = pad_to(n, TILE_N) / TILE_N;
-  const int64_t vec = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;  // (t, c, [h], lane)
-  const int64_t nvec = NT * KC * (bits == 4 ? 1 : 2) * 64;
-  if (vec >= nvec) return;
-  const int l = (int)(vec & 63);
-  const int64_t tcv = vec >> 6;
-  const int h = bits == 4 ? 0 : (int)(tcv & 1);
-  const int64_t tc = bits == 4 ? tcv : (tcv >> 1);
-  const int64_t t = tc / KC, c = tc % KC;
+  const int64_t ncg = (KC + DQ_CH - 1) / DQ_CH;
+  const int64_t t = blockIdx.x / ncg, cg = blockIdx.x % ncg;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int r = l & 15, g = l >> 4;
-  const int64_t row = t * TILE_N + r;
-  if (row >= n) return;
+  const int64_t c = cg * DQ_CH + w;
   const uint8_t* tile = blob + t * dev_tile_bytes(fmt, KC);
-  const uint8_t* rec = tile + c * dev_code_chunk(fmt);
-  const uint4 q = *(const uint4*)(rec + (h * 64 + l) * 16);
-  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-  // 4-bit: dword s = k-step s (block s/2); 8-bit half h: k-steps 2h, 2h+1 (block h)
-  for (int ss = 0; ss < (bits == 4 ? 4 : 2); ss++) {
-    const int s = bits == 4 ? ss : 2 * h + ss;
-    const int blk = s >> 1;
-    const int64_t kk = c * CHUNK_K + 32 * s + 8 * g;
-    if (kk >= k) continue;
-    const float d = f16_to_f32(((const uint16_t*)(tile + dev_scale_off(fmt, KC, r, c)))[blk]);
-    const float m = fmt_has_min(fmt) ? f16_to_f32(((const uint16_t*)(tile + dev_min_off(fmt, KC, r, c)))[blk]) : 0.f;
-    float v[8];
-    for (int j = 0; j < 8; j++) {
-      int code;
-      if (bits == 4) code = (w[s] >> (4 * dev_nib_pos(fmt, j))) & 15;
-      else code = (w[2 * ss + (j >> 2)] >> (8 * (j & 3))) & 0xff;
-      v[j] = hd_code_value(fmt, code) * d + m;
+  if (c < KC) {
+    const uint8_t* rec = tile + c * dev_code_chunk(fmt);
+    uint32_t wd[bits == 4 ? 4 : 8];
+    {
+      const uint4 q = *(const uint4*)(rec + l * 16);
+      wd[0] = q.x; wd[1] = q.y; wd[2] = q.z; wd[3] = q.w;
+      if constexpr (bits != 4) {
+        const uint4 q1 = *(const uint4*)(rec + (64 + l) * 16);
+        wd[4] = q1.x; wd[5] = q1.y; wd[6] = q1.z; wd[7] = q1.w;
+      }
     }
-    *(uint4*)(out + (size_t)row * k + kk) = make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]),
-                                                       pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
+    const uint16_t* sp = (const uint16_t*)(tile + dev_scale_off(fmt, KC, r, c));
+    const uint16_t* mp = fmt_has_min(fmt) ? (const uint16_t*)(tile + dev_min_off(fmt, KC, r, c)) : nullptr;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {                          // k-step s: elements 32 s + 8 g .. + 7
+      const int blk = s >> 1;
+      const float d = f16_to_f32(sp[blk]);
+      const float m = fmt_has_min(fmt) ? f16_to_f32(mp[blk]) : 0.f;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        int code;
+        // 4-bit: dword s = k-step s; 8-bit: half h = s / 2, dwords 2 (s % 2) .. + 1
+        if (bits == 4) code = (wd[s] >> (4 * dev_nib_pos(fmt, j))) & 15;
+        else code = (wd[4 * (s >> 1) + 2 * (s & 1) + (j >> 2)] >> (8 * (j & 3))) & 0xff;
+        v[j] = hd_code_value(fmt, code) * d + m;
+      }
+      *(uint4*)(rows + r * DQ_LD + w * CHUNK_K + 32 * s + 8 * g) =
+          make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
+    }
+  }
+  __syncthreads();
+  // row segment [cg * 512, cg * 512 + 512) of rows t * 16 .. + 15: 64 x 16-B pieces per row
+  const int64_t k0 = cg * DQ_CH * CHUNK_K;
+#pragma unroll
+  for (int j = 0; j < TILE_N * DQ_CH * CHUNK_K / 8 / 256; j++) {
+    const int v = tid + 256 * j;
+    const int rr = v / (DQ_CH * CHUNK_K / 8), col = (v % (DQ_CH * CHUNK_K / 8)) * 8;
+    const int64_t row = t * TILE_N + rr, kk = k0 + col;
+    if (row < n && kk + 8 <= k) *(uint4*)(out + (size_t)row * k + kk) = *(const uint4*)(rows + rr * DQ_LD + col);
   }
 }
 
 void launch_dequantize_device(bool bf16, int fmt, const uint8_t* blob, int64_t n, int64_t k,
                               uint16_t* out, hipStream_t st) {
-  const int bits = fmt_bits(fmt);
-  const int64_t nvec = (pad_to(n, TILE_N) / TILE_N) * (pad_to(k, CHUNK_K) / CHUNK_K) * (bits == 4 ? 1 : 2) * 64;
-  dim3 grid((unsigned)((nvec + 255) / 256));
+  const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
+  const int64_t nblk = (pad_to(n, TILE_N) / TILE_N) * ((KC + DQ_CH - 1) / DQ_CH);
+  dim3 grid((unsigned)nblk);
 #define DQ_CASE(F)                                                                                       \
   case F:                                                                                                \
     if (bf16) hipLaunchKernelGGL((dequantize_tiled_kernel<BF16, F>), grid, dim3(256), 0, st, blob, n, k, out); \

@@ -477,3 +477,20 @@ def test_attn_decode_fused_combine_opt_in_subprocess(cuda):
                         "fused_combine_repeated or attn_decode_rope_matches or rope_in_mha"],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("name", FMTS)
+@pytest.mark.parametrize("n,k", [(100, 384), (48, 640), (32, 1024)])
+def test_dequantize_device_kernel(cuda, name, n, k):
+    """tiled blob -> dense weight on the GPU (library-GEMM prefill path; LDS
+    row staging over 4 chunks) vs the host dequantizer of the same blob,
+    including partial tiles and chunk groups"""
+    f = get_format(name).fmt
+    torch.manual_seed(2)
+    w = torch.randn(n, k) * 0.05
+    blob = ops.repack_to_device(ops.quantize(w, f), f, n, k)
+    ref = R.dequantize_device_blob(blob, f, n, k)
+    for dt in (torch.bfloat16, torch.float16):
+        got = torch.ops.ipex_llm_amd.dequantize_device(blob.to(cuda), f, n, k, dt)
+        assert got.shape == (n, k)
+        assert torch.allclose(got.float().cpu(), ref.to(dt).float(), atol=1e-3, rtol=1e-2), (name, dt)
