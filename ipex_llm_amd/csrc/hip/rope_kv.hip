@@ -156,7 +156,80 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
   }
 }
 
+// Prefill fast path (projection output in T, full-width NeoX rotary from the
+// cos/sin table, no per-head norm, 16-bit cache): D / 16 lanes per (token,
+// head) row, each rotating 8 consecutive dims of both halves with 16-B loads
+// and stores; 256-thread workgroups.  Same rounding sequence as the general
+// kernel.  The one-wave-per-row kernel with 2-byte accesses took 27.8 us per
+// Llama-3-8B layer at 1024 prompt tokens.
+template <typename T>
+__global__ void __launch_bounds__(256) rope_kv_vec_kernel(const RopeKVArgs a) {
+  const int D = a.D, half = D / 2, LPR = D / 16;
+  const int HT = a.Hq + 2 * a.Hkv;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = gid / LPR;
+  if (row >= (int64_t)a.T * HT) return;
+  const int i0 = (int)(gid % LPR) * 8;
+  const int t = (int)(row / HT), h = (int)(row % HT);
+  const bool is_q = h < a.Hq, is_k = !is_q && h < a.Hq + a.Hkv;
+  const uint16_t* src = a.qkv + (size_t)t * a.ld_qkv + (size_t)h * D;
+  uint16_t* d0p;
+  uint16_t* d1p;
+  if (is_q) {
+    d0p = a.q_out + ((size_t)t * a.Hq + h) * D + i0;
+  } else {
+    int64_t slot;
+    if (a.slots) {
+      slot = a.slots[t];
+    } else {
+      const int64_t pp = a.pos[t] - (a.pos_offset ? a.pos_offset[t / a.tq] : 0);
+      slot = (int64_t)a.block_tables[(size_t)(t / a.tq) * a.max_blocks + pp / a.bs] * a.bs + pp % a.bs;
+    }
+    if (slot < 0) return;                              // padding token
+    const int hk = is_k ? h - a.Hq : h - a.Hq - a.Hkv;
+    d0p = (uint16_t*)(is_k ? a.k_cache : a.v_cache) +
+          (((size_t)(slot / a.bs) * a.Hkv + hk) * a.bs + (size_t)(slot % a.bs)) * D + i0;
+  }
+  d1p = d0p + half;
+  const uint4 x0 = *(const uint4*)(src + i0), x1 = *(const uint4*)(src + i0 + half);
+  if (!is_q && !is_k) {                                // v: copy
+    *(uint4*)d0p = x0;
+    *(uint4*)d1p = x1;
+    return;
+  }
+  const float4* cs = (const float4*)((const float2*)a.cos_sin + (size_t)a.pos[t] * half + i0);
+  const uint32_t w0[4] = {x0.x, x0.y, x0.z, x0.w}, w1[4] = {x1.x, x1.y, x1.z, x1.w};
+  const float osc = is_q ? a.attn_scale_q : 1.f;
+  auto rnd = [](float v) { return to_f32<T>(from_f32<T>(v)); };
+  uint32_t o0[4], o1[4];
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const float4 q = cs[e];                            // (cos, sin) of dims i0 + 2e, i0 + 2e + 1
+    float r0[2], r1[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      // HF casts cos/sin to the activation dtype before the rotation
+      const float c = rnd(u ? q.z : q.x), sn = rnd(u ? q.w : q.y);
+      const float a0 = to_f32<T>((uint16_t)(w0[e] >> (16 * u))), a1 = to_f32<T>((uint16_t)(w1[e] >> (16 * u)));
+      r0[u] = (rnd(a0 * c) - rnd(a1 * sn)) * osc;
+      r1[u] = (rnd(a1 * c) + rnd(a0 * sn)) * osc;
+    }
+    o0[e] = pack2<T>(r0[0], r0[1]);
+    o1[e] = pack2<T>(r1[0], r1[1]);
+  }
+  *(uint4*)d0p = make_uint4(o0[0], o0[1], o0[2], o0[3]);
+  *(uint4*)d1p = make_uint4(o1[0], o1[1], o1[2], o1[3]);
+}
+
 void launch_rope_kv(bool bf16, const RopeKVArgs& a, hipStream_t st) {
+  if (!a.part && !a.q_norm && !a.k_norm && !a.interleaved && a.rot_dim == a.D && a.kv_fp8 == 0 && a.cos_sin &&
+      a.D % 16 == 0 && a.ld_qkv % 8 == 0) {
+    const int64_t n = (int64_t)a.T * (a.Hq + 2 * a.Hkv) * (a.D / 16);
+    dim3 g((unsigned)((n + 255) / 256));
+    if (bf16) hipLaunchKernelGGL(rope_kv_vec_kernel<BF16>, g, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(rope_kv_vec_kernel<F16>, g, dim3(256), 0, st, a);
+    return;
+  }
   dim3 grid(a.Hq + 2 * a.Hkv, a.T);
   if (bf16) hipLaunchKernelGGL(rope_kv_kernel<BF16>, grid, dim3(64), 0, st, a);
   else hipLaunchKernelGGL(rope_kv_kernel<F16>, grid, dim3(64), 0, st, a);

@@ -348,6 +348,30 @@ def test_rope_kv(cuda, interleaved, kv_fp8):
 
 
 @pytest.mark.parametrize("D", [64, 128])
+def test_rope_kv_table_fast_path(cuda, D):
+    """prefill RoPE + KV append from the cos/sin table (the vectorized
+    16-B-per-lane kernel) vs the CPU path; a padding slot (-1) writes nothing"""
+    T, Hq, Hkv, bs = 37, 8, 2, 64
+    torch.manual_seed(1)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=cuda).bfloat16()
+    pos = torch.arange(T, device=cuda) * 3 + 5
+    slots = torch.randperm(4 * bs, device=cuda)[:T]
+    slots[7] = -1
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    fr = torch.arange(512, device=cuda).float()[:, None] * inv[None]
+    tab = torch.stack([fr.cos(), fr.sin()], -1).contiguous()
+    kc = torch.zeros(4, Hkv, bs, D, device=cuda, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    q = torch.empty(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+    ops.rope_kv(qkv, q, kc, vc, slots, pos, tab, Hq, Hkv, D)
+    kc2, vc2 = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q2 = torch.empty(T, Hq, D, dtype=torch.bfloat16)
+    ops.rope_kv(qkv.cpu(), q2, kc2, vc2, slots.cpu(), pos.cpu(), tab.cpu(), Hq, Hkv, D)
+    assert _rel(q.cpu(), q2) < 1e-2
+    assert _rel(kc.cpu(), kc2) < 1e-2 and torch.equal(vc.cpu(), vc2)
+
+
+@pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("Tq", [1, 3])
 @pytest.mark.parametrize("kv_fp8", [0, 1])
 def test_attn_decode(cuda, D, Tq, kv_fp8):
