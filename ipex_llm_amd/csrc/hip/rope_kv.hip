@@ -156,11 +156,11 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
   }
 }
 
-// Prefill fast path (projection output in T, full-width NeoX rotary from the
-// cos/sin table, no per-head norm, 16-bit cache): D / 16 lanes per (token,
-// head) row, each rotating 8 consecutive dims of both halves with 16-B loads
-// and stores; 256-thread workgroups.  Same rounding sequence as the general
-// kernel.  The one-wave-per-row kernel with 2-byte accesses took 27.8 us per
+// Fast path (full-width NeoX rotary from the cos/sin table, no per-head norm,
+// 16-bit cache; input = the projection output in T, or one f32 atomic
+// accumulator slab + bias, re-zeroed here): D / 16 lanes per (token, head)
+// row, each rotating 8 consecutive dims of both halves with 16-B accesses;
+// 256-thread workgroups.  Same rounding sequence as the general kernel.  The one-wave-per-row kernel with 2-byte accesses took 27.8 us per
 // Llama-3-8B layer at 1024 prompt tokens.
 template <typename T>
 __global__ void __launch_bounds__(256) rope_kv_vec_kernel(const RopeKVArgs a) {
@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(256) rope_kv_vec_kernel(const RopeKVArgs a) {
   const int i0 = (int)(gid % LPR) * 8;
   const int t = (int)(row / HT), h = (int)(row % HT);
   const bool is_q = h < a.Hq, is_k = !is_q && h < a.Hq + a.Hkv;
-  const uint16_t* src = a.qkv + (size_t)t * a.ld_qkv + (size_t)h * D;
+  const uint16_t* src = a.part ? nullptr : a.qkv + (size_t)t * a.ld_qkv + (size_t)h * D;
   uint16_t* d0p;
   uint16_t* d1p;
   if (is_q) {
@@ -185,13 +185,50 @@ __global__ void __launch_bounds__(256) rope_kv_vec_kernel(const RopeKVArgs a) {
       const int64_t pp = a.pos[t] - (a.pos_offset ? a.pos_offset[t / a.tq] : 0);
       slot = (int64_t)a.block_tables[(size_t)(t / a.tq) * a.max_blocks + pp / a.bs] * a.bs + pp % a.bs;
     }
-    if (slot < 0) return;                              // padding token
+    if (slot < 0) {                                    // padding token: nothing to write
+      if (a.part && a.zero_part) {
+        float* pp = (float*)a.part + (size_t)t * a.ld_qkv + (size_t)h * D;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        *(float4*)(pp + i0) = z; *(float4*)(pp + i0 + 4) = z;
+        *(float4*)(pp + i0 + half) = z; *(float4*)(pp + i0 + half + 4) = z;
+      }
+      return;
+    }
     const int hk = is_k ? h - a.Hq : h - a.Hq - a.Hkv;
     d0p = (uint16_t*)(is_k ? a.k_cache : a.v_cache) +
           (((size_t)(slot / a.bs) * a.Hkv + hk) * a.bs + (size_t)(slot % a.bs)) * D + i0;
   }
   d1p = d0p + half;
-  const uint4 x0 = *(const uint4*)(src + i0), x1 = *(const uint4*)(src + i0 + half);
+  uint4 x0, x1;
+  if (a.part) {
+    // rnd(bias + acc) like the GEMV output, then the accumulator is re-zeroed
+    float* pp = (float*)a.part + (size_t)t * a.ld_qkv + (size_t)h * D;
+    float4* p0 = (float4*)(pp + i0);
+    float4* p1 = (float4*)(pp + i0 + half);
+    const float4 f[4] = {p0[0], p0[1], p1[0], p1[1]};
+    uint32_t wv[8];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int dd = (e < 2 ? i0 : i0 + half) + 4 * (e & 1);
+      float bb[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.bias) {
+        const uint2 bu = *(const uint2*)(a.bias + (size_t)h * D + dd);
+        bb[0] = to_f32<T>((uint16_t)(bu.x & 0xffff)); bb[1] = to_f32<T>((uint16_t)(bu.x >> 16));
+        bb[2] = to_f32<T>((uint16_t)(bu.y & 0xffff)); bb[3] = to_f32<T>((uint16_t)(bu.y >> 16));
+      }
+      wv[2 * e] = pack2<T>(bb[0] + f[e].x, bb[1] + f[e].y);
+      wv[2 * e + 1] = pack2<T>(bb[2] + f[e].z, bb[3] + f[e].w);
+    }
+    x0 = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    x1 = make_uint4(wv[4], wv[5], wv[6], wv[7]);
+    if (a.zero_part) {
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      p0[0] = z; p0[1] = z; p1[0] = z; p1[1] = z;
+    }
+  } else {
+    x0 = *(const uint4*)(src + i0);
+    x1 = *(const uint4*)(src + i0 + half);
+  }
   if (!is_q && !is_k) {                                // v: copy
     *(uint4*)d0p = x0;
     *(uint4*)d1p = x1;
@@ -222,8 +259,8 @@ __global__ void __launch_bounds__(256) rope_kv_vec_kernel(const RopeKVArgs a) {
 }
 
 void launch_rope_kv(bool bf16, const RopeKVArgs& a, hipStream_t st) {
-  if (!a.part && !a.q_norm && !a.k_norm && !a.interleaved && a.rot_dim == a.D && a.kv_fp8 == 0 && a.cos_sin &&
-      a.D % 16 == 0 && a.ld_qkv % 8 == 0) {
+  if ((!a.part || a.nsplit == 1) && !a.q_norm && !a.k_norm && !a.interleaved && a.rot_dim == a.D &&
+      a.kv_fp8 == 0 && a.cos_sin && a.D % 16 == 0 && a.ld_qkv % 8 == 0) {
     const int64_t n = (int64_t)a.T * (a.Hq + 2 * a.Hkv) * (a.D / 16);
     dim3 g((unsigned)((n + 255) / 256));
     if (bf16) hipLaunchKernelGGL(rope_kv_vec_kernel<BF16>, g, dim3(256), 0, st, a);
