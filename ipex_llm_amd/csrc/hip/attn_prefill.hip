@@ -298,11 +298,18 @@ static void launch_pf_hp(const AttnPrefillArgs& a, hipStream_t st) {
 
 template <typename T, int D>
 static void launch_pf_d(const AttnPrefillArgs& a, hipStream_t st) {
-  // ILLM_PREFILL_HP=2: two query heads per wave sharing the kv head's LDS reads
-  // (even GQA group).  310 registers -> one wave per SIMD: measured slower on
-  // MI355X (T = 1024: 58.4 vs 44.8 us; T = 16384: 7.2 vs 5.0 ms), so opt-in
-  static const int hp_env = getenv("ILLM_PREFILL_HP") ? atoi(getenv("ILLM_PREFILL_HP")) : 1;
-  if (hp_env >= 2 && (a.Hq / a.Hkv) % 2 == 0) launch_pf_hp<T, D, 2>(a, st);
+  // HP = 2: two query heads of one kv head per wave, so every K fragment and
+  // transposed V read from LDS feeds two MFMAs (even GQA group).  It halves
+  // the grid, so it is taken when the halved grid still covers the chip
+  // twice (2 workgroups per CU).  Measured on MI355X (Llama-3-8B heads):
+  // T = 4096 266 -> 212 us, B = 8 x 1024 164 -> 120 us, T = 16 K 3.42 ->
+  // 2.46 ms (895 TFLOP/s); T = 1024 (256 workgroups) 30.3 -> 37.3 us, so HP = 1
+  // there.  ILLM_PREFILL_HP=1/2 forces either.
+  static const int hp_env = getenv("ILLM_PREFILL_HP") ? atoi(getenv("ILLM_PREFILL_HP")) : 0;
+  const bool even = (a.Hq / a.Hkv) % 2 == 0;
+  const long wg2 = (long)((a.Tq + PF_QB - 1) / PF_QB) * (a.Hq / 2) * a.B;
+  const bool hp2 = even && (hp_env == 2 || (hp_env == 0 && wg2 >= 512));
+  if (hp2) launch_pf_hp<T, D, 2>(a, st);
   else launch_pf_hp<T, D, 1>(a, st);
 }
 
