@@ -520,6 +520,45 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   const int h = kvh * group + (row % group);
   const int qpos = len - a.Tq + t;
   const float sc = a.scale * (KVF ? a.k_scale : 1.f);
+#ifndef ILLM_ATTN_SCORE_BF
+#define ILLM_ATTN_SCORE_BF 1
+#endif
+#if ILLM_ATTN_SCORE_BF
+  // the optional soft-cap / ALiBi terms are uniform branches around whole
+  // loops and the mask is branch-free (per-score branches split the score
+  // pass into dozens of basic blocks)
+#pragma unroll
+  for (int kt = 0; kt < 4; kt++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) st[kt][i] *= sc;
+  if (a.softcap > 0.f) {
+#pragma unroll
+    for (int kt = 0; kt < 4; kt++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) st[kt][i] = a.softcap * tanhf(st[kt][i] / a.softcap);
+  }
+  if (a.alibi) {
+    const float slope = row < R ? a.alibi[h] : 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; kt++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) st[kt][i] += slope * (float)(k0 + kt * 16 + 4 * g + i);
+  }
+  const int win = a.sliding_window > 0 ? qpos - a.sliding_window : -1;
+  const int klim = min(nk, qpos - k0 + 1);          // keys kk < klim are visible
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 4; kt++) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int kk = kt * 16 + 4 * g + i;
+      const bool ok = row < R && kk < klim && k0 + kk > win;
+      const float v = ok ? st[kt][i] : -INFINITY;
+      st[kt][i] = v;
+      m = fmaxf(m, v);
+    }
+  }
+#else
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < 4; kt++) {
@@ -537,6 +576,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
       m = fmaxf(m, v);
     }
   }
+#endif
   m = fmaxf(m, __shfl_xor(m, 16, 64));
   m = fmaxf(m, __shfl_xor(m, 32, 64));
   float l = 0.f;
