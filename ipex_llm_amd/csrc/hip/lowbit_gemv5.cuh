@@ -135,10 +135,14 @@ __host__ __device__ constexpr size_t gemv5_attn_shmem(int rows, int cpk, int D, 
   return (size_t)rows * gemv5_attn_heads(cpk, D) * (ns + 1) * 4;
 }
 
-// weight stream loads: read once per decode step by one CU, so the
-// non-temporal policy (ILLM_GEMV_NT=1 at build time) is an option
+// weight stream loads: read once per decode step by one CU (the model's
+// weights are far larger than the 256 MB MALL, nothing survives to the next
+// hipGraph replay), so they take the non-temporal policy.  Same-box A/B on
+// MI355X (Llama-3-8B, 256 steps x 2, profiles/gemv_nt_ab_samebox.txt):
+// B=1 1.780 -> 1.732 ms/token, B=8 2.381 -> 2.356 ms/step.  ILLM_GEMV_NT=0
+// at build time restores default-policy loads.
 #ifndef ILLM_GEMV_NT
-#define ILLM_GEMV_NT 0
+#define ILLM_GEMV_NT 1
 #endif
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
