@@ -156,7 +156,7 @@ __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
 
 template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW>
 __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a) {
-  constexpr int PF = 4;                 // chunks in flight per wave (8 measured slower)
+  constexpr int PF = 4;                 // chunks in flight per wave (6 and 8 measured slower)
   using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;   // MFMA input type
   constexpr int BITS = dk_bits(DK);
   constexpr int TG = NW / KW;          // tile groups per workgroup (NW waves)
