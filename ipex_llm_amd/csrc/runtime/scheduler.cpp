@@ -124,7 +124,9 @@ class Scheduler : public torch::CustomClassHolder {
       Seq& s = seqs_[run[i]];
       if (s.state != RUNNING) continue;
       while (need_block(s)) {
-        if (!free_.empty()) {
+        // the free list first, then idle cached (prefix) blocks: a running
+        // sequence is preempted only when neither is left
+        if (available() > 0) {
           s.blocks.push_back(pop_free());
           continue;
         }

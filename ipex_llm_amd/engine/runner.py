@@ -251,6 +251,8 @@ class Engine:
 
     @torch.no_grad()
     def decode_step_obj(self, seqs: List[SequenceState], max_len: int, greedy: bool, use_graph: bool):
+        gmax = self.model.graph_max_batch() if hasattr(self.model, "graph_max_batch") else 16
+        use_graph = use_graph and len(seqs) <= gmax
         key = (len(seqs), max(len(s.blocks) for s in seqs), greedy, use_graph)
         st = self._steps.get(key)
         bt = make_block_table(seqs, key[1], self.model.device)

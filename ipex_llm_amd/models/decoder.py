@@ -229,6 +229,23 @@ class NativeCausalLM(nn.Module):
     def device(self):
         return self.layers[0].input_layernorm.device
 
+    def graph_max_batch(self) -> int:
+        """Largest one-token-per-sequence decode batch whose ``forward_tokens``
+        is hipGraph-capture safe (no host sync, no data-dependent routing
+        baked in at capture).  0: never capture."""
+        s = self.spec
+        group = s.num_heads // s.num_kv_heads
+        if group > 16 or s.head_dim not in (64, 80, 96, 128, 256):
+            return 0                      # SDPA fallback reads seq_lens on the host
+        lim = 1 << 30
+        for L in self.layers:
+            mlp = L.mlp
+            if type(mlp).__name__ == "NativeMoE":
+                lim = min(lim, mlp.graph_max_tokens())
+            elif not isinstance(mlp, NativeMLP) and not hasattr(mlp, "graph_max_tokens"):
+                lim = min(lim, 16)
+        return lim
+
     # ------------------------------------------------------------------ cache
     def make_cache(self, max_tokens: int, batch: int = 1, block_size: int = 64, kv_fp8: int = 0,
                    num_blocks: Optional[int] = None):

@@ -164,11 +164,15 @@ class NativeMoE(nn.Module):
         return ops.moe_topk(logits.float(), self.top_k, self.renorm, 0)
 
     def _router_w(self, dtype):
-        r = self.__dict__.get("_router_cast")
-        if r is None or r.dtype != dtype or r.device != self.router.device:
-            r = self.router.detach().to(dtype).contiguous()
-            self.__dict__["_router_cast"] = r
-        return r
+        # keyed on the parameter's storage and version counter: load_state_dict /
+        # in-place updates invalidate the cast copy the fused route reads
+        src = self.router
+        key = (src.data_ptr(), src._version, dtype, src.device)
+        c = self.__dict__.get("_router_cast")
+        if c is None or c[0] != key:
+            c = (key, src.detach().to(dtype).contiguous())
+            self.__dict__["_router_cast"] = c
+        return c[1]
 
     def _route_counter(self, device):
         c = self.__dict__.get("_route_ctr")
@@ -176,6 +180,10 @@ class NativeMoE(nn.Module):
             c = torch.zeros(1, dtype=torch.int32, device=device)
             self.__dict__["_route_ctr"] = c
         return c
+
+    def graph_max_tokens(self) -> int:
+        """tokens per forward that stay on device-only launches (capturable)"""
+        return 16
 
     def fused_route_ok(self, x2: torch.Tensor) -> bool:
         return (x2.is_cuda and x2.shape[0] <= 16 and ops.native_gpu(x2) and self.num_experts <= 512

@@ -82,6 +82,11 @@ class LLMEngine:
         self.metrics = EngineMetrics()
         self.use_graph = use_graph and model.device.type == "cuda" and ops.native_gpu(self.cache.k[0])
         self._graphs: Dict[tuple, dict] = {}
+        # every captured (batch, width) bucket allocates from ONE private pool,
+        # and only buckets whose forward is capture-safe are captured (MoE
+        # routing / SDPA fallbacks above the model's limit run eagerly)
+        self._graph_pool = None
+        self._graph_max_b = model.graph_max_batch() if hasattr(model, "graph_max_batch") else 16
         model.ensure_rope_cache(max_model_len + 1)
         self.sched = torch.classes.ipex_llm_amd.Scheduler(num_blocks, block_size, max_batch, max_prefill_tokens)
         # automatic prefix caching: full KV blocks are shared by content hash
@@ -202,7 +207,9 @@ class LLMEngine:
             body()
         torch.cuda.current_stream().wait_stream(s)
         g["graph"] = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g["graph"]):
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g["graph"], pool=self._graph_pool):
             g["logits"] = body()
         self._graphs[(Bb, Wb)] = g
         return g
@@ -274,7 +281,7 @@ class LLMEngine:
                 rs = [self.requests[rid] for rid in decode]
                 B = len(rs)
                 pos_l = [int(self.sched.cached(rid)) for rid in decode]
-                if self.use_graph:
+                if self.use_graph and self._bucket(B) <= self._graph_max_b:
                     lg = self._decode_graph(decode, pos_l)
                 else:
                     bt = self._block_table(decode)

@@ -107,6 +107,30 @@ def test_scheduler_prefix_cache_reuse_and_eviction():
     assert s.num_cached_blocks() == 5
 
 
+def test_scheduler_evicts_idle_cached_before_preempting():
+    """free list empty but idle cached blocks available: a running sequence
+    crossing a block boundary takes an evicted block, nobody is preempted"""
+    s = _sched(nb=4, bs=64)
+    s.enable_prefix_caching(True)
+    s.add_tokens(1, list(range(1, 129)))        # 2 full blocks -> cached after finish
+    _split(list(s.schedule()))
+    s.advance(1, 128)
+    s.finish(1)
+    assert s.num_cached_blocks() == 2 and s.num_free_blocks() == 4
+    s.add_tokens(2, [7] * 64)                   # 1 fresh block + 1 for the next token later
+    s.add_tokens(3, [9] * 63)
+    p, d, pre, f = _split(list(s.schedule()))
+    assert p == [2, 3]
+    s.advance(2, 64); s.grow(2)
+    s.advance(3, 63); s.grow(3)
+    # request 2 needs a 2nd block: the free list holds 0 or 1 blocks, the rest are idle cached
+    for _ in range(3):
+        p, d, pre, f = _split(list(s.schedule()))
+        assert pre == [], "preempted although idle cached blocks were available"
+        for r in d:
+            s.advance(r, 1); s.grow(r)
+
+
 def test_engine_prefix_cache_matches_uncached(native):
     """shared system prompt: later requests prefill only their suffix and
     produce the tokens of the uncached engine"""
