@@ -1,27 +1,31 @@
-// One-shot peer-to-peer all-reduce over xGMI for small tensor-parallel
-// messages (row-parallel o_proj / down_proj outputs during decode).
+// Peer-to-peer all-reduce over xGMI for tensor-parallel messages (row-parallel
+// o_proj / down_proj outputs, including the decoder's f32 split-K
+// accumulators, and MoE expert-parallel partial sums).
 //
 // Reference capability: the patched oneCCL "DG2 LL256" all-reduce
-// (CCL_PATCH:180-830) that exchanges Level-Zero IPC handles
-// and polls flag lines in peer memory.  MI355X design:
-//   * every rank owns one hipMalloc'd buffer = [signal area | data half 0 |
-//     data half 1]; the buffers are exchanged once as hipIpcMemHandles and
-//     mapped into every peer (fully connected xGMI: each GPU reads the 7
-//     peers over 7 separate links at once, which a ring cannot do);
-//   * block b of every rank handles the same contiguous slice of the
-//     message: it copies its slice of the input into its own buffer, then
-//     stores the call's epoch into slot [parity][b][rank] of every peer's
-//     signal area (system-scope release), waits for all ranks' epochs in
-//     its own signal area, and sums the slice from all peers' buffers (f32
-//     accumulation) into the output.  Synchronisation is therefore per block
-//     slice, no grid-wide barrier is needed;
-//   * the data area is double-buffered by epoch parity, so no end-of-call
-//     barrier is needed: a rank can only start call N+2 (which overwrites the
-//     parity of call N) after every peer signalled call N+1, i.e. after every
-//     peer finished reading call N;
-//   * epochs are device-resident per-block counters (all advanced every
-//     call, so all blocks share one parity), so the launch is
-//     hipGraph-capturable (no host-side state changes between replays);
+// (CCL_PATCH:180-830, dg2_ll256_allreduce :624, dg2_allreduce
+// :809) that exchanges Level-Zero IPC handles and polls flag lines in peer
+// memory.  MI355X design:
+//   * every rank owns one hipMalloc'd buffer = [signal area | data p0 | data p1
+//     | result p0 | result p1]; the buffers are exchanged once as
+//     hipIpcMemHandles and mapped into every peer (fully connected xGMI: each
+//     GPU reads its 7 peers over 7 separate links at once, which a ring cannot);
+//   * ONE-SHOT (small messages, decode): block b of every rank copies its
+//     slice of the input into its own data half, publishes the call's epoch
+//     into slot [0][parity][b][rank] of every peer (system-scope release),
+//     waits for all ranks' epochs in its own signal area and sums the slice
+//     from all peers' buffers (f32 accumulation);
+//   * TWO-SHOT (medium messages, prefill chunks / large batches): after the
+//     same publish + wait, rank r reduces only sub-slice r of the block's
+//     slice (W x fewer peer bytes per rank), writes it to its result half,
+//     publishes a phase-2 epoch and gathers the W reduced sub-slices from the
+//     peers' result halves: 2 (W-1)/W of the message crosses the links per
+//     rank instead of (W-1);
+//   * the data/result halves are double-buffered by epoch parity: a rank
+//     starts call N+2 (which overwrites the halves of call N) only after every
+//     peer signalled call N+1, i.e. after every peer's call-N kernel finished;
+//   * epochs are device-resident per-block counters (all advanced every call),
+//     so the launch is hipGraph-capturable;
 //   * every wait loop is bounded: on timeout the kernel raises an error flag
 //     and continues instead of hanging the GPU.
 #include <hip/hip_runtime.h>
@@ -32,39 +36,50 @@
 
 namespace illm {
 
-__device__ __forceinline__ uint32_t* ar_sig(uint8_t* base, int parity, int blk, int src) {
-  return (uint32_t*)base + (parity * AR_MAX_BLOCKS + blk) * AR_MAX_RANKS + src;
+__device__ __forceinline__ uint32_t* ar_sig(uint8_t* base, int phase, int parity, int blk, int src) {
+  return (uint32_t*)base + ((phase * 2 + parity) * AR_MAX_BLOCKS + blk) * AR_MAX_RANKS + src;
 }
 
-template <typename T>
-__device__ __forceinline__ void acc_vec(float (&s)[8], uint4 v) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+// 16-byte vector -> 8 (16-bit) or 4 (f32) accumulator lanes
+template <int DT>
+__device__ __forceinline__ void acc_vec(float (&s)[8], u32x4v v) {
+  if constexpr (DT == AR_F32) {
+    s[0] += __uint_as_float(v.x); s[1] += __uint_as_float(v.y);
+    s[2] += __uint_as_float(v.z); s[3] += __uint_as_float(v.w);
+  } else {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    s[2 * i] += to_f32<T>((uint16_t)(w[i] & 0xffff));
-    s[2 * i + 1] += to_f32<T>((uint16_t)(w[i] >> 16));
+    for (int i = 0; i < 4; i++) {
+      if constexpr (DT == AR_BF16) {
+        s[2 * i] += to_f32<BF16>((uint16_t)(w[i] & 0xffff));
+        s[2 * i + 1] += to_f32<BF16>((uint16_t)(w[i] >> 16));
+      } else {
+        s[2 * i] += to_f32<F16>((uint16_t)(w[i] & 0xffff));
+        s[2 * i + 1] += to_f32<F16>((uint16_t)(w[i] >> 16));
+      }
+    }
   }
 }
+template <int DT>
+__device__ __forceinline__ uint4 pack_vec(const float (&s)[8]) {
+  if constexpr (DT == AR_F32) return make_uint4(__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]),
+                                                __float_as_uint(s[3]));
+  else if constexpr (DT == AR_BF16)
+    return make_uint4(pack2<BF16>(s[0], s[1]), pack2<BF16>(s[2], s[3]), pack2<BF16>(s[4], s[5]), pack2<BF16>(s[6], s[7]));
+  else return make_uint4(pack2<F16>(s[0], s[1]), pack2<F16>(s[2], s[3]), pack2<F16>(s[4], s[5]), pack2<F16>(s[6], s[7]));
+}
 
-template <typename T, int W>
-__global__ void __launch_bounds__(AR_THREADS) one_shot_all_reduce(AllReduceArgs a) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const uint32_t epoch = a.counter[b] + 1;
-  const int parity = epoch & 1;
-  const int64_t per = (a.nvec + gridDim.x - 1) / gridDim.x;
-  const int64_t v0 = b * per, v1 = min(a.nvec, v0 + per);
-
-  // 1. my slice -> my buffer (data half `parity`)
-  uint4* mine = (uint4*)(a.bufs[a.rank] + AR_SIGNAL_BYTES + parity * a.cap);
-  for (int64_t v = v0 + tid; v < v1; v += AR_THREADS) mine[v] = a.in[v];
-  __threadfence_system();
-  __syncthreads();
-
-  // 2. publish the epoch to every rank; 3. wait for every rank's epoch
+// publish `epoch` to every rank's slot (phase, parity, b, rank); wait for all
+// ranks' epochs in the own signal area.  Threads 0..W-1 take part.
+template <int W>
+__device__ __forceinline__ void ar_exchange(const AllReduceArgs& a, int phase, int parity, uint32_t epoch) {
+  const int tid = threadIdx.x, b = blockIdx.x;
   if (tid < W) {
-    __hip_atomic_store(ar_sig(a.bufs[tid], parity, b, a.rank), epoch, __ATOMIC_RELEASE,
+    __hip_atomic_store(ar_sig(a.bufs[tid], phase, parity, b, a.rank), epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t* mysig = ar_sig(a.bufs[a.rank], parity, b, tid);
+    uint32_t* mysig = ar_sig(a.bufs[a.rank], phase, parity, b, tid);
     int64_t spins = 0;
     while (__hip_atomic_load(mysig, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       if (++spins > (1ll << 26)) {  // ~seconds: a peer is gone; report, do not hang
@@ -75,24 +90,59 @@ __global__ void __launch_bounds__(AR_THREADS) one_shot_all_reduce(AllReduceArgs 
     }
   }
   __syncthreads();
+}
 
-  // 4. sum the slice over all ranks (f32), 16 B per thread per step
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4* src[W];
+template <int DT, int W>
+__global__ void __launch_bounds__(AR_THREADS) peer_all_reduce(AllReduceArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t epoch = a.counter[b] + 1;
+  const int parity = epoch & 1;
+  const int64_t per = (a.nvec + gridDim.x - 1) / gridDim.x;
+  const int64_t v0 = b * per, v1 = min(a.nvec, v0 + per);
+
+  // 1. my slice -> my data half `parity`
+  u32x4v* mine = (u32x4v*)(a.bufs[a.rank] + AR_SIGNAL_BYTES + parity * a.cap);
+  const u32x4v* in = (const u32x4v*)a.in;
+  for (int64_t v = v0 + tid; v < v1; v += AR_THREADS) mine[v] = in[v];
+  __threadfence_system();
+  __syncthreads();
+  ar_exchange<W>(a, 0, parity, epoch);
+
+  const u32x4v* src[W];
 #pragma unroll
-  for (int r = 0; r < W; r++) src[r] = (const u32x4*)(a.bufs[r] + AR_SIGNAL_BYTES + parity * a.cap);
-  for (int64_t v = v0 + tid; v < v1; v += AR_THREADS) {
-    uint4 x[W];
+  for (int r = 0; r < W; r++) src[r] = (const u32x4v*)(a.bufs[r] + AR_SIGNAL_BYTES + parity * a.cap);
+  auto reduce_range = [&](int64_t s0, int64_t s1, u32x4v* dst) {
+    for (int64_t v = s0 + tid; v < s1; v += AR_THREADS) {
+      u32x4v x[W];
+#pragma unroll
+      for (int r = 0; r < W; r++) x[r] = __builtin_nontemporal_load(src[r] + v);   // peer data: bypass caches
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < W; r++) acc_vec<DT>(s, x[r]);
+      const uint4 o = pack_vec<DT>(s);
+      dst[v] = u32x4v{o.x, o.y, o.z, o.w};
+    }
+  };
+  if (!a.two_shot) {
+    // 2. sum the slice over all ranks (f32), 16 B per thread per step
+    reduce_range(v0, v1, (u32x4v*)a.out);
+  } else {
+    // 2a. reduce sub-slice `rank` of this block's slice into my result half
+    const int64_t sub = (v1 - v0 + W - 1) / W;
+    const int64_t r0 = min(v1, v0 + a.rank * sub), r1 = min(v1, r0 + sub);
+    u32x4v* res = (u32x4v*)(a.bufs[a.rank] + AR_SIGNAL_BYTES + (2 + parity) * a.cap);
+    reduce_range(r0, r1, res);
+    __threadfence_system();
+    __syncthreads();
+    ar_exchange<W>(a, 1, parity, epoch);
+    // 2b. gather every rank's reduced sub-slice
+    u32x4v* out = (u32x4v*)a.out;
 #pragma unroll
     for (int r = 0; r < W; r++) {
-      const u32x4 t = __builtin_nontemporal_load(src[r] + v);  // peer data: bypass stale cache lines
-      x[r] = make_uint4(t.x, t.y, t.z, t.w);
+      const u32x4v* rr = (const u32x4v*)(a.bufs[r] + AR_SIGNAL_BYTES + (2 + parity) * a.cap);
+      const int64_t g0 = min(v1, v0 + r * sub), g1 = min(v1, g0 + sub);
+      for (int64_t v = g0 + tid; v < g1; v += AR_THREADS) out[v] = __builtin_nontemporal_load(rr + v);
     }
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < W; r++) acc_vec<T>(s, x[r]);
-    a.out[v] = make_uint4(pack2<T>(s[0], s[1]), pack2<T>(s[2], s[3]), pack2<T>(s[4], s[5]),
-                          pack2<T>(s[6], s[7]));
   }
   // all AR_MAX_BLOCKS epochs advance every call (blocks beyond this grid are
   // advanced by block 0), so every block of a call uses the same parity
@@ -105,23 +155,27 @@ int custom_all_reduce_blocks(int64_t nvec) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(nb, AR_MAX_BLOCKS));
 }
 
-void launch_custom_all_reduce(bool bf16, const AllReduceArgs& a, hipStream_t st) {
-  const int nb = custom_all_reduce_blocks(a.nvec);
-#define ARK(TT, WW) hipLaunchKernelGGL((one_shot_all_reduce<TT, WW>), dim3(nb), dim3(AR_THREADS), 0, st, a)
-#define ARW(TT)                       \
-  switch (a.world) {                  \
-    case 1: ARK(TT, 1); break;        \
-    case 2: ARK(TT, 2); break;        \
-    case 3: ARK(TT, 3); break;        \
-    case 4: ARK(TT, 4); break;        \
-    case 5: ARK(TT, 5); break;        \
-    case 6: ARK(TT, 6); break;        \
-    case 7: ARK(TT, 7); break;        \
-    default: ARK(TT, 8); break;       \
+template <int DT>
+static void launch_dt(const AllReduceArgs& a, int nb, hipStream_t st) {
+#define ARK(WW) hipLaunchKernelGGL((peer_all_reduce<DT, WW>), dim3(nb), dim3(AR_THREADS), 0, st, a)
+  switch (a.world) {
+    case 1: ARK(1); break;
+    case 2: ARK(2); break;
+    case 3: ARK(3); break;
+    case 4: ARK(4); break;
+    case 5: ARK(5); break;
+    case 6: ARK(6); break;
+    case 7: ARK(7); break;
+    default: ARK(8); break;
   }
-  if (bf16) { ARW(BF16) } else { ARW(F16) }
-#undef ARW
 #undef ARK
+}
+
+void launch_custom_all_reduce(const AllReduceArgs& a, hipStream_t st) {
+  const int nb = custom_all_reduce_blocks(a.nvec);
+  if (a.dtype == AR_F32) launch_dt<AR_F32>(a, nb, st);
+  else if (a.dtype == AR_BF16) launch_dt<AR_BF16>(a, nb, st);
+  else launch_dt<AR_F16>(a, nb, st);
 }
 
 }  // namespace illm

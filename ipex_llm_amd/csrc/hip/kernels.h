@@ -190,12 +190,15 @@ void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int6
                            int64_t* pos, const int32_t* block_tables, int max_blocks, int bs, int64_t* slots,
                            int32_t* seq_lens, const int64_t* pos_offset, hipStream_t st);
 
-// ---- one-shot xGMI peer all-reduce (allreduce.hip) ------------------------
+// ---- one-shot / two-shot xGMI peer all-reduce (allreduce.hip) -------------
 constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_BLOCKS = 64;
 constexpr int AR_THREADS = 512;
-// signal area: uint32 [2 parity][AR_MAX_BLOCKS][AR_MAX_RANKS], padded to 8 KiB
+// signal area: uint32 [2 phase][2 parity][AR_MAX_BLOCKS][AR_MAX_RANKS] = 8 KiB
 constexpr int64_t AR_SIGNAL_BYTES = 8192;
+// peer buffer: [signal | data parity 0 | data parity 1 | result parity 0 | result parity 1],
+// each data / result half `cap` bytes (the result halves are used by the two-shot form)
+enum ArDtype : int { AR_BF16 = 0, AR_F16 = 1, AR_F32 = 2 };
 
 struct AllReduceArgs {
   uint8_t* bufs[AR_MAX_RANKS];  // every rank's buffer base (mapped), own included
@@ -206,9 +209,11 @@ struct AllReduceArgs {
   int64_t cap;                  // bytes per data half
   uint32_t* counter;            // [AR_MAX_BLOCKS] local epochs
   int* err;
+  int dtype;                    // ArDtype
+  int two_shot;                 // reduce-scatter + all-gather through the result halves
 };
 
-void launch_custom_all_reduce(bool bf16, const AllReduceArgs& a, hipStream_t st);
+void launch_custom_all_reduce(const AllReduceArgs& a, hipStream_t st);
 int custom_all_reduce_blocks(int64_t nvec);
 
 // ---- fused multi-tensor AdamW (optim.hip) ----------------------------------

@@ -3,7 +3,7 @@
 //   ipc_handle(ptr) -> Tensor       64-byte hipIpcMemHandle (CPU uint8)
 //   ipc_open(handle) -> int         peer buffer mapped into this process
 //   ipc_close(ptr) / ipc_free(ptr)
-//   custom_all_reduce(inp, out, bufs, rank, counter, cap, err)
+//   custom_all_reduce(inp, out, bufs, rank, counter, cap, err, two_shot)  bf16 / fp16 / f32
 // The Python side (parallel/comm.py) exchanges handles with
 // torch.distributed.all_gather_object once per process group.
 #include <ATen/ATen.h>
@@ -54,10 +54,12 @@ void ipc_close(int64_t ptr) { HIP_OK(hipIpcCloseMemHandle((void*)(uintptr_t)ptr)
 void ipc_free(int64_t ptr) { HIP_OK(hipFree((void*)(uintptr_t)ptr)); }
 
 void custom_all_reduce(const Tensor& inp, Tensor& out, c10::IntArrayRef bufs, int64_t rank,
-                       Tensor& counter, int64_t cap, Tensor& err) {
+                       Tensor& counter, int64_t cap, Tensor& err, int64_t two_shot) {
   TORCH_CHECK(inp.is_cuda() && out.is_cuda() && inp.is_contiguous() && out.is_contiguous(),
               "custom_all_reduce: contiguous GPU tensors");
-  TORCH_CHECK(inp.scalar_type() == at::kBFloat16 || inp.scalar_type() == at::kHalf, "bf16/fp16 only");
+  const auto dt = inp.scalar_type();
+  TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf || dt == at::kFloat, "custom_all_reduce: bf16/fp16/f32 only");
+  TORCH_CHECK(out.scalar_type() == dt && out.numel() == inp.numel(), "custom_all_reduce: out must match inp");
   const int64_t bytes = inp.numel() * inp.element_size();
   TORCH_CHECK(bytes % 16 == 0 && bytes <= cap, "custom_all_reduce: message must be 16-B aligned and <= cap");
   TORCH_CHECK((int64_t)bufs.size() >= 1 && (int64_t)bufs.size() <= illm::AR_MAX_RANKS, "1..8 ranks");
@@ -73,9 +75,11 @@ void custom_all_reduce(const Tensor& inp, Tensor& out, c10::IntArrayRef bufs, in
   a.cap = cap;
   a.counter = (uint32_t*)counter.data_ptr<int32_t>();
   a.err = err.data_ptr<int32_t>();
-  if (a.nvec > 0)
-    illm::launch_custom_all_reduce(inp.scalar_type() == at::kBFloat16, a,
-                                   at::hip::getCurrentHIPStream().stream());
+  a.dtype = dt == at::kFloat ? illm::AR_F32 : (dt == at::kBFloat16 ? illm::AR_BF16 : illm::AR_F16);
+  // two-shot once every rank reading the whole message from all peers costs
+  // more link time than the extra exchange round (> 256 KiB at W > 2)
+  a.two_shot = two_shot >= 0 ? (int)two_shot : (a.world > 2 && bytes > (256 << 10) ? 1 : 0);
+  if (a.nvec > 0) illm::launch_custom_all_reduce(a, at::hip::getCurrentHIPStream().stream());
 }
 
 // table: int64 [5, T] = (param ptr, grad ptr, exp_avg ptr, exp_avg_sq ptr, numel)
@@ -118,7 +122,7 @@ TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("ipc_open(Tensor handle) -> int", &ipc_open);
   m.def("ipc_close(int ptr) -> ()", &ipc_close);
   m.def("ipc_free(int ptr) -> ()", &ipc_free);
-  m.def("custom_all_reduce(Tensor inp, Tensor(a!) out, int[] bufs, int rank, Tensor(b!) counter, int cap, Tensor(c!) err) -> ()");
+  m.def("custom_all_reduce(Tensor inp, Tensor(a!) out, int[] bufs, int rank, Tensor(b!) counter, int cap, Tensor(c!) err, int two_shot=-1) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {

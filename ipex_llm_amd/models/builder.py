@@ -106,11 +106,29 @@ def lowbit_from_dense(w: torch.Tensor, qtype, device, bias: Optional[torch.Tenso
 
 @torch.no_grad()
 def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat16, seed: int = 0,
-                        lm_head_qtype=None, std: float = 0.02) -> NativeCausalLM:
-    """Random-init model of ``cfg``'s architecture, quantized on ``device``."""
+                        lm_head_qtype=None, std: float = 0.02, tp_group=None, ep_group=None) -> NativeCausalLM:
+    """Random-init model of ``cfg``'s architecture, quantized on ``device``.
+
+    ``tp_group``: tensor parallel (AutoTP layout, SRC example
+    ``Deepspeed-AutoTP/deepspeed_autotp.py:81-106``): every rank draws the SAME
+    full-size random weights (one seed) and keeps/quantizes its shard -- whole
+    query heads and their KV heads (column-parallel qkv), the matching o_proj
+    columns (row-parallel, all-reduced), an I / world slice of gate/up
+    (column) and down (row), a vocab slice of lm_head (logits all-gathered).
+    ``ep_group``: expert parallel -- rank r keeps experts [r E/W, (r+1) E/W).
+    Either way the result equals the single-GPU model of the same seed."""
     spec = spec_from_config(cfg)
     s = spec
     g = torch.Generator(device=device).manual_seed(seed)
+    W = R = 1
+    if tp_group is not None:
+        import torch.distributed as dist
+        W, R = dist.get_world_size(tp_group), dist.get_rank(tp_group)
+    if W > 1:
+        if s.num_heads % W or s.intermediate_size % (16 * W):
+            raise ValueError(f"tensor parallel {W}: heads {s.num_heads} / intermediate {s.intermediate_size}")
+        if s.num_kv_heads % W and W % s.num_kv_heads:
+            raise ValueError(f"tensor parallel {W}: {s.num_kv_heads} KV heads")
 
     def rnd(*shape, scale=std):
         return (torch.randn(*shape, generator=g, device=device, dtype=torch.float32) * scale).to(dtype)
@@ -118,20 +136,42 @@ def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat
     def ones_ish(n):
         return (1.0 + rnd(n, scale=0.02).float()).to(dtype) if not s.norm_unit_offset else rnd(n, scale=0.02)
 
-    nq, nkv = s.num_heads * s.head_dim, s.num_kv_heads * s.head_dim
+    D = s.head_dim
+    nq, nkv = s.num_heads * D, s.num_kv_heads * D
+    hq = s.num_heads // W                                   # local query heads
+    if s.num_kv_heads % W == 0:
+        kv0, hkv = R * (s.num_kv_heads // W), s.num_kv_heads // W
+    else:                                                   # fewer KV heads than ranks: replicate
+        kv0, hkv = (R * hq) // (s.num_heads // s.num_kv_heads), 1
+    Il = s.intermediate_size // W
+    mp = tp_group if W > 1 else None
     layers = []
     for li in range(s.num_layers):
         wqkv = rnd(nq + 2 * nkv, s.hidden_size)
         bqkv = rnd(nq + 2 * nkv) if s.qkv_bias else None
+        if W > 1:
+            rows = torch.cat([torch.arange(R * hq * D, (R + 1) * hq * D),
+                              nq + torch.arange(kv0 * D, (kv0 + hkv) * D),
+                              nq + nkv + torch.arange(kv0 * D, (kv0 + hkv) * D)]).to(wqkv.device)
+            wqkv = wqkv.index_select(0, rows)
+            bqkv = bqkv.index_select(0, rows) if bqkv is not None else None
         qkv = lowbit_from_dense(wqkv, qtype, device, bqkv)
         del wqkv
-        o = lowbit_from_dense(rnd(s.hidden_size, nq), qtype, device)
+        wo = rnd(s.hidden_size, nq)
+        if W > 1:
+            wo = wo[:, R * hq * D:(R + 1) * hq * D]
+        o = lowbit_from_dense(wo.contiguous(), qtype, device)
+        o.mp_group = mp
         if s.is_moe_layer(li):
-            mlp = _random_moe(s, qtype, device, rnd)
+            mlp = _random_moe(s, qtype, device, rnd, ep_group)
         else:
-            gu = lowbit_from_dense(interleave_glu_rows(rnd(s.intermediate_size, s.hidden_size),
-                                                       rnd(s.intermediate_size, s.hidden_size)), qtype, device)
-            down = lowbit_from_dense(rnd(s.hidden_size, s.intermediate_size), qtype, device)
+            wg, wu = rnd(s.intermediate_size, s.hidden_size), rnd(s.intermediate_size, s.hidden_size)
+            wd = rnd(s.hidden_size, s.intermediate_size)
+            if W > 1:
+                wg, wu, wd = wg[R * Il:(R + 1) * Il], wu[R * Il:(R + 1) * Il], wd[:, R * Il:(R + 1) * Il]
+            gu = lowbit_from_dense(interleave_glu_rows(wg.contiguous(), wu.contiguous()), qtype, device)
+            down = lowbit_from_dense(wd.contiguous(), qtype, device)
+            down.mp_group = mp
             mlp = NativeMLP(s, gu, down)
         attn = NativeAttention(s, qkv, o, ones_ish(s.head_dim) if s.qk_norm else None,
                                ones_ish(s.head_dim) if s.qk_norm else None, s.sliding_window)
@@ -139,25 +179,60 @@ def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat
         torch.cuda.empty_cache() if torch.device(device).type == "cuda" else None
     embed = rnd(s.vocab_size, s.hidden_size)
     head_w = embed if s.tie_embeddings else rnd(s.vocab_size, s.hidden_size)
-    lm_head = lowbit_from_dense(head_w, lm_head_qtype or qtype, device)
+    if W > 1:
+        from ..parallel.tp import VocabParallelHead
+        per = (s.vocab_size + W - 1) // W
+        a, b = R * per, min(s.vocab_size, (R + 1) * per)
+        hw = torch.zeros(per, s.hidden_size, dtype=head_w.dtype, device=head_w.device)
+        hw[:b - a] = head_w[a:b]
+        lm_head = VocabParallelHead(lowbit_from_dense(hw, lm_head_qtype or qtype, device), tp_group, s.vocab_size)
+    else:
+        lm_head = lowbit_from_dense(head_w, lm_head_qtype or qtype, device)
     inv_freq, att_scale = compute_inv_freq(cfg, s.head_dim, s.rot_dim or s.head_dim)
     s.rope_attention_scaling = att_scale
-    model = NativeCausalLM(s, embed, layers, ones_ish(s.hidden_size), lm_head, inv_freq.to(device), dtype)
+    if W > 1:
+        import copy
+        s = copy.copy(s)
+        s.num_heads, s.num_kv_heads = hq, hkv
+        for L in layers:
+            L.self_attn.spec = s
+            L.mlp.spec = s
+    model = NativeCausalLM(s, embed, layers, ones_ish(spec.hidden_size), lm_head, inv_freq.to(device), dtype)
+    if W > 1:
+        model.tp_group = tp_group
     return model.eval()
 
 
 @torch.no_grad()
-def _random_moe(s: DecoderSpec, qtype, device, rnd) -> nn.Module:
+def _random_moe(s: DecoderSpec, qtype, device, rnd, ep_group=None) -> nn.Module:
     """random-init sparse MoE block (router, E experts quantized one by one on
-    the device, optional shared expert + gate) of ``s``'s geometry"""
+    the device, optional shared expert + gate) of ``s``'s geometry; with an EP
+    group only this rank's experts are kept (all are drawn: same weights as
+    the single-GPU model)"""
     from .moe import LowBitExperts, NativeMoE, SharedExpertMLP
     E, I, H = s.num_experts, s.moe_intermediate, s.hidden_size
+    e0, El = 0, E
+    if ep_group is not None:
+        import torch.distributed as dist
+        W, R = dist.get_world_size(ep_group), dist.get_rank(ep_group)
+        if E % W:
+            raise ValueError(f"expert parallel {W}: {E} experts")
+        El = E // W
+        e0 = R * El
     fmt = Q.get_format(qtype).fmt
-    gu = LowBitExperts(E, 2 * I, H, qtype, "meta")
-    dn = LowBitExperts(E, H, I, qtype, "meta")
-    gu.weight = nn.Parameter(torch.stack([ops.quantize(interleave_glu_rows(rnd(I, H), rnd(I, H)), fmt)
-                                          for _ in range(E)]), requires_grad=False)
-    dn.weight = nn.Parameter(torch.stack([ops.quantize(rnd(H, I), fmt) for _ in range(E)]), requires_grad=False)
+    gu = LowBitExperts(El, 2 * I, H, qtype, "meta")
+    dn = LowBitExperts(El, H, I, qtype, "meta")
+    gub, dnb = [], []
+    for e in range(E):
+        wg = interleave_glu_rows(rnd(I, H), rnd(I, H))
+        if e0 <= e < e0 + El:
+            gub.append(ops.quantize(wg, fmt))
+    for e in range(E):
+        wd = rnd(H, I)
+        if e0 <= e < e0 + El:
+            dnb.append(ops.quantize(wd, fmt))
+    gu.weight = nn.Parameter(torch.stack(gub), requires_grad=False)
+    dn.weight = nn.Parameter(torch.stack(dnb), requires_grad=False)
     shared, sgate = None, None
     if s.shared_expert_intermediate:
         Is = s.shared_expert_intermediate
@@ -165,7 +240,8 @@ def _random_moe(s: DecoderSpec, qtype, device, rnd) -> nn.Module:
                                  lowbit_from_dense(rnd(H, Is), qtype, device), s.act)
         sgate = rnd(1, H)
     renorm = s.norm_topk if s.model_type != "mixtral" else True
-    return NativeMoE(rnd(E, H, scale=0.5), gu, dn, s.top_k, renorm, s.act, shared, sgate, num_experts=E)
+    return NativeMoE(rnd(E, H, scale=0.5), gu, dn, s.top_k, renorm, s.act, shared, sgate, expert_offset=e0,
+                     num_experts=E, ep_group=ep_group)
 
 
 def _module_weight(m: nn.Module):

@@ -303,6 +303,25 @@ class NativeCausalLM(nn.Module):
         o = outs[0] if len(outs) == 1 else torch.cat(outs, 0)      # (a 1-element cat is a slow strided copy)
         return o.reshape(T, s.num_heads * s.head_dim)
 
+    def _tp_ok(self, mod) -> bool:
+        """row-parallel layer of this model's TP group (or not row-parallel)"""
+        g = getattr(mod, "mp_group", None)
+        return g is None or g is self.tp_group
+
+    @staticmethod
+    def _reduce(acc: torch.Tensor, mod) -> torch.Tensor:
+        """sum a row-parallel layer's f32 split-K accumulator over its TP group
+        in place (custom xGMI all-reduce / RCCL): the fused norm consumers then
+        read the full output exactly as on one GPU"""
+        g = getattr(mod, "mp_group", None)
+        if g is None:
+            return acc
+        from ..parallel.comm import all_reduce_inplace
+        out = all_reduce_inplace(acc, g)
+        if out is not acc:
+            acc.copy_(out)
+        return acc
+
     def _acc(self, n: int, t: int, device, tag: str = "") -> torch.Tensor:
         """Zeroed f32 [t, n] accumulator for the split-K atomic GEMV
         (ops.gemv_accum); its consumer re-zeroes it after reading (or a later
@@ -357,17 +376,21 @@ class NativeCausalLM(nn.Module):
     def _proj_residual_norm(self, x, proj, residual, norm_w, post_norm_w=None):
         """residual += proj(x); return rms_norm(residual) * norm_w."""
         s = self.spec
-        fused = (x.is_cuda and isinstance(proj, LowBitLinear) and proj.bias is None and proj.mp_group is None
-                 and post_norm_w is None and x.shape[0] <= ops.GEMV_MAX_M and self.tp_group is None)
+        fused = (x.is_cuda and isinstance(proj, LowBitLinear) and proj.bias is None and self._tp_ok(proj)
+                 and post_norm_w is None and x.shape[0] <= ops.GEMV_MAX_M)
         if fused and x.shape[0] <= ACC_MAX_M and ops.native_gpu(x):
-            # split-K f32 atomics into one zeroed slab; the norm reads + re-zeroes it
+            # split-K f32 atomics into one zeroed slab (summed over the TP group
+            # for a row-parallel layer); the norm reads + re-zeroes it
             acc = self._acc(proj.out_features, x.shape[0], x.device)
             ops.gemv_accum(x, proj.weight, proj.fmt, proj.out_features, proj.in_features, acc)
+            self._reduce(acc, proj)
             out, _ = ops.add_rms_norm(None, residual, norm_w, s.rms_eps, partials=acc.unsqueeze(0),
                                       unit_offset=s.norm_unit_offset, zero_partials=True)
             return out
         if fused:
             part = ops.gemv_partials(x, proj.weight, proj.fmt, proj.out_features, proj.in_features, 0)
+            if proj.mp_group is not None:
+                part = self._reduce(part.sum(0, keepdim=True), proj)
             out, _ = ops.add_rms_norm(None, residual, norm_w, s.rms_eps, partials=part,
                                       unit_offset=s.norm_unit_offset)
             return out
@@ -386,16 +409,17 @@ class NativeCausalLM(nn.Module):
     _norm_in_env = __import__("os").environ.get("ILLM_NORM_IN", "1") != "0"
 
     def _norm_in_ok(self, ref: torch.Tensor, T: int) -> bool:
-        if not (self._norm_in_env and T <= min(ACC_MAX_M, NORM_IN_MAX_M) and ref.is_cuda and self.tp_group is None
+        if not (self._norm_in_env and T <= min(ACC_MAX_M, NORM_IN_MAX_M) and ref.is_cuda
                 and not self.spec.sandwich_norm and not self._attn_fuse and not self._glu_in_enabled
                 and self.spec.hidden_size % 8 == 0 and ops.native_gpu(ref)):
             return False
         ok = self.__dict__.get("_norm_in_layers")
         if ok is None:
             def lowbit(m, bias_ok=False):
-                return isinstance(m, LowBitLinear) and m.mp_group is None and (bias_ok or m.bias is None)
+                return isinstance(m, LowBitLinear) and self._tp_ok(m) and (bias_ok or m.bias is None)
             ok = all(isinstance(L.mlp, NativeMLP) and lowbit(L.mlp.gate_up_proj) and lowbit(L.mlp.down_proj)
                      and lowbit(L.self_attn.o_proj) and lowbit(L.self_attn.qkv_proj, True)
+                     and L.self_attn.qkv_proj.mp_group is None and L.mlp.gate_up_proj.mp_group is None
                      and (L.self_attn.qkv_proj.bias is None or L.self_attn.qkv_proj.bias.dtype == ref.dtype)
                      and L.post_feedforward_layernorm is None for L in self.layers)
             self.__dict__["_norm_in_layers"] = ok
@@ -423,15 +447,15 @@ class NativeCausalLM(nn.Module):
                      and (L.self_attn.qkv_proj.bias is None or L.self_attn.qkv_proj.bias.dtype == ref.dtype)
                      for L in self.layers)
             self.__dict__["_qkv_native_ok"] = ok
-        return ok and ref.is_cuda and self.tp_group is None and ops.native_gpu(ref)
+        return ok and ref.is_cuda and ops.native_gpu(ref)
 
     def _fused_mlp_ok(self, x, layer, need_env: bool = True) -> bool:
         mlp = layer.mlp
-        if not (x.is_cuda and isinstance(mlp, NativeMLP) and x.shape[0] <= 16 and self.tp_group is None):
+        if not (x.is_cuda and isinstance(mlp, NativeMLP) and x.shape[0] <= 16):
             return False
         gu, dn = mlp.gate_up_proj, mlp.down_proj
         return (isinstance(gu, LowBitLinear) and isinstance(dn, LowBitLinear) and gu.bias is None and dn.bias is None
-                and gu.mp_group is None and dn.mp_group is None and layer.post_feedforward_layernorm is None
+                and gu.mp_group is None and self._tp_ok(dn) and layer.post_feedforward_layernorm is None
                 and dn.in_features % 16 == 0 and (self._glu_in_enabled or not need_env) and ops.native_gpu(x))
 
     def _mlp_acc_ok(self, x, layer) -> bool:
@@ -572,6 +596,7 @@ class NativeCausalLM(nn.Module):
                 H = o.out_features
                 accP, accD = self._acc(H, T, x.device, "P"), self._acc(H, T, x.device, "D")
                 ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
+                self._reduce(accP, o)
                 r2 = nxt_res(residual)
                 gu, dn = mlp.gate_up_proj, mlp.down_proj
                 act = ops.gemv_norm_in(accP, residual, r2, layer.post_attention_layernorm, s.rms_eps,
@@ -579,6 +604,7 @@ class NativeCausalLM(nn.Module):
                                        s.act)
                 residual = r2
                 ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=accP)
+                self._reduce(accD, dn)
                 consumed = None
                 if li + 1 < len(self.layers):
                     pend = accD
@@ -613,6 +639,7 @@ class NativeCausalLM(nn.Module):
                 dacc = self._acc(dn.out_features, x.shape[0], x.device)
                 ops.gemv_glu_in(gacc.unsqueeze(0), dn.weight, dn.fmt, dn.out_features, dn.in_features, s.act, 0,
                                 x.dtype, acc=dacc)
+                self._reduce(dacc, dn)
                 x, _ = ops.add_rms_norm(None, residual, nxt, s.rms_eps, partials=dacc.unsqueeze(0),
                                         unit_offset=s.norm_unit_offset, zero_partials=True)
                 zero_next = gacc
@@ -622,15 +649,24 @@ class NativeCausalLM(nn.Module):
                 gu, dn = layer.mlp.gate_up_proj, layer.mlp.down_proj
                 pg = ops.gemv_partials(x, gu.weight, gu.fmt, gu.out_features, gu.in_features, 0)
                 pd = ops.gemv_glu_in(pg, dn.weight, dn.fmt, dn.out_features, dn.in_features, s.act, 0, x.dtype)
+                if dn.mp_group is not None:
+                    pd = self._reduce(pd.sum(0, keepdim=True), dn)
                 x, _ = ops.add_rms_norm(None, residual, nxt, s.rms_eps, partials=pd, unit_offset=s.norm_unit_offset)
                 continue
             mlp = layer.mlp
             if type(mlp).__name__ == "NativeMoE" and layer.post_feedforward_layernorm is None \
                     and self.tp_group is None and x.shape[0] <= 16 and mlp.acc_ok(x):
                 # MoE decode: routed experts (and a shared expert) add into the
-                # norm's f32 slab; no combine launch, no [T, H] bf16 round trip
+                # norm's f32 slab; no combine launch, no [T, H] bf16 round trip.
+                # Expert parallel: each rank adds its local experts' share, the
+                # slab is summed over the EP group (one all-reduce per block)
                 acc = self._acc(s.hidden_size, x.shape[0], x.device)
                 mlp.forward_acc(x, acc)
+                if mlp.ep_group is not None:
+                    from ..parallel.comm import all_reduce_inplace
+                    r = all_reduce_inplace(acc, mlp.ep_group)
+                    if r is not acc:
+                        acc.copy_(r)
                 x, _ = ops.add_rms_norm(None, residual, nxt, s.rms_eps, partials=acc.unsqueeze(0),
                                         unit_offset=s.norm_unit_offset, zero_partials=True)
                 continue

@@ -197,7 +197,7 @@ class NativeMoE(nn.Module):
     def acc_ok(self, x2: torch.Tensor) -> bool:
         """decode block can accumulate into a residual-norm f32 slab"""
         sm = self.shared_mlp
-        return (self.ep_group is None and self.fused_route_ok(x2)
+        return (self.fused_route_ok(x2)
                 and (sm is None or (isinstance(sm, SharedExpertMLP) and hasattr(sm.gate_up_proj, "fmt")
                                     and hasattr(sm.down_proj, "fmt") and getattr(sm.down_proj, "bias", None) is None)))
 
@@ -210,6 +210,10 @@ class NativeMoE(nn.Module):
         a = ops.moe_gemv_glu(x2, gu.weight, gu.fmt, gu.out_features, gu.in_features, off, rows, self.top_k, self.act)
         ops.moe_gemv_accum(a, dn.weight, dn.fmt, dn.out_features, dn.in_features, off, rows, acc, w, self.top_k)
         sm = self.shared_mlp
+        if sm is not None and self.ep_group is not None:
+            import torch.distributed as dist
+            if dist.get_rank(self.ep_group) != 0:     # the EP all-reduce sums it in once
+                sm = None
         if sm is not None:
             sg, sd = sm.gate_up_proj, sm.down_proj
             sa = ops.gemv_glu(x2, sg.weight, sg.fmt, sg.out_features, sg.in_features, sm.act)

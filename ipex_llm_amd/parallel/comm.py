@@ -84,7 +84,7 @@ def all_reduce_inplace(t: torch.Tensor, group=None) -> torch.Tensor:
         return t
     car = _CUSTOM.get(id(group)) if t.is_cuda else None
     if car is not None and car.eligible(t):
-        return car(t)
+        return car(t, out=t)
     dist.all_reduce(t, group=group)
     return t
 
@@ -110,12 +110,15 @@ class CustomAllReduce:
     """One-shot peer all-reduce for one intra-node process group.
 
     Collective constructor: every rank allocates a peer buffer
-    ([signal | 2 x cap]), the hipIpc handles are all-gathered and opened.
+    ([signal | 2 x data | 2 x result], ``cap`` bytes each), the hipIpc
+    handles are all-gathered and opened.  Messages up to 256 KiB take the
+    one-shot form, larger ones (up to ``cap``) the two-shot form
+    (reduce-scatter + all-gather through the result halves).
     ``__call__`` is capturable in a hipGraph (device-side epochs)."""
 
     SIGNAL = 8192
 
-    def __init__(self, group=None, device=None, max_bytes: int = 1 << 20):
+    def __init__(self, group=None, device=None, max_bytes: int = 8 << 20):
         from .. import ops
         ops.require()
         self.group = group
@@ -131,7 +134,7 @@ class CustomAllReduce:
         self.cap = int(max_bytes)
         A = torch.ops.ipex_llm_amd
         with torch.cuda.device(self.device):
-            self._own = A.ipc_alloc(self.SIGNAL + 2 * self.cap)
+            self._own = A.ipc_alloc(self.SIGNAL + 4 * self.cap)   # signals | data x2 | result x2
             handle = A.ipc_handle(self._own)
         handles = [None] * self.world
         dist.all_gather_object(handles, handle.tolist(), group=group)
@@ -152,12 +155,15 @@ class CustomAllReduce:
 
     def eligible(self, t: torch.Tensor) -> bool:
         nb = t.numel() * t.element_size()
-        return (t.dtype in (torch.bfloat16, torch.float16) and t.is_contiguous() and nb % 16 == 0
+        return (t.dtype in (torch.bfloat16, torch.float16, torch.float32) and t.is_contiguous() and nb % 16 == 0
                 and 0 < nb <= self.cap and t.device == self.device)
 
-    def __call__(self, t: torch.Tensor) -> torch.Tensor:
-        out = torch.empty_like(t)
-        torch.ops.ipex_llm_amd.custom_all_reduce(t, out, self.ptrs, self.rank, self.counter, self.cap, self.err)
+    def __call__(self, t: torch.Tensor, out: Optional[torch.Tensor] = None, two_shot: int = -1) -> torch.Tensor:
+        """sum over the group; ``out`` may alias ``t`` (each block reads its
+        slice before it writes it)"""
+        out = torch.empty_like(t) if out is None else out
+        torch.ops.ipex_llm_amd.custom_all_reduce(t, out, self.ptrs, self.rank, self.counter, self.cap, self.err,
+                                                 two_shot)
         return out
 
     def check(self):
@@ -174,7 +180,7 @@ class CustomAllReduce:
         self._opened = []
 
 
-def setup_custom_all_reduce(group=None, max_bytes: int = 1 << 20) -> Optional[CustomAllReduce]:
+def setup_custom_all_reduce(group=None, max_bytes: int = 8 << 20) -> Optional[CustomAllReduce]:
     """Collective: create (once) the custom all-reduce for ``group`` if the
     group is intra-node, on GPU and the feature is enabled."""
     if not is_dist() or get_world_size(group) == 1 or not torch.cuda.is_available() or not _custom_enabled():

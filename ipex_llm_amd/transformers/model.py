@@ -239,6 +239,13 @@ class _BaseAutoModelClass:
             config = AutoConfig.from_pretrained(path, trust_remote_code=trust)
         meta_path = os.path.join(path, LOW_BIT_META)
         flags = json.load(open(meta_path)) if os.path.exists(meta_path) else {}
+        from .ref_checkpoint import OUR_FORMAT, is_reference_low_bit_dir
+        ref_layout = is_reference_low_bit_dir(path)
+        if flags and flags.get("format", OUR_FORMAT) != OUR_FORMAT:
+            raise ValueError(f"load_low_bit: unknown low-bit layout {flags.get('format')!r} in {meta_path}")
+        if not flags and not ref_layout:
+            raise ValueError(f"load_low_bit: {path} is not a low-bit checkpoint (no {LOW_BIT_META} and no "
+                             "bigdl_transformers_low_bit in config.json)")
         qtype = flags.get("qtype") or getattr(config, "bigdl_transformers_low_bit", "sym_int4")
         dt = torch_dtype if isinstance(torch_dtype, torch.dtype) else \
             getattr(config, "torch_dtype", None) or torch.float16
@@ -250,7 +257,11 @@ class _BaseAutoModelClass:
                              flags.get("modules_to_not_convert"), convert_shape_only=True,
                              mixed_precision=flags.get("mixed_precision", False))
         wfile = os.path.join(path, "model.safetensors")
-        if os.path.exists(wfile):
+        if ref_layout:
+            # reference save_low_bit: ggml CPU-layout blocks, converted (never reinterpreted)
+            from .ref_checkpoint import convert_reference_state_dict, load_reference_state_dict
+            sd = convert_reference_state_dict(load_reference_state_dict(path), model, qtype)
+        elif os.path.exists(wfile):
             sd = load_file(wfile)
         else:
             sd = torch.load(os.path.join(path, "pytorch_model.bin"), map_location="cpu", weights_only=True)

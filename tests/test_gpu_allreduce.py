@@ -30,16 +30,22 @@ def _worker(rank, world, port, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         from ipex_llm_amd.parallel.comm import CustomAllReduce
-        car = CustomAllReduce(None, device="cuda:0", max_bytes=1 << 20)
-        for dt in (torch.bfloat16, torch.float16):
+        car = CustomAllReduce(None, device="cuda:0", max_bytes=1 << 21)
+        for dt in (torch.bfloat16, torch.float16, torch.float32):
             for n in (8, 4096, 8 * 4096, 64 * 4096 + 8):
-                for it in range(3):
-                    g = torch.Generator(device="cuda").manual_seed(1000 * it + n)
-                    base = torch.randn(world, n, generator=g, device="cuda").to(dt)
-                    out = car(base[rank].contiguous())
-                    want = base.float().sum(0)
-                    err = ((out.float() - want).abs().max() / want.abs().max()).item()
-                    assert err < 2e-2, (dt, n, it, err)
+                if n * torch.finfo(dt).bits // 8 > car.cap:
+                    continue
+                for two in (0, 1):
+                    for it in range(3):
+                        g = torch.Generator(device="cuda").manual_seed(1000 * it + n)
+                        base = torch.randn(world, n, generator=g, device="cuda").to(dt)
+                        mine = base[rank].contiguous()
+                        # in place (the decoder reduces its f32 accumulator where it lies)
+                        out = car(mine, out=mine if it == 2 else None, two_shot=two)
+                        want = base.float().sum(0)
+                        err = ((out.float() - want).abs().max() / want.abs().max()).item()
+                        tol = 1e-5 if dt == torch.float32 else 2e-2
+                        assert err < tol, (dt, n, two, it, err)
         # graph capture: the epoch counters live on the device
         x = torch.full((4096,), float(rank + 1), device="cuda", dtype=torch.bfloat16)
         car(x)
@@ -62,11 +68,12 @@ def _worker(rank, world, port, q):
         raise
 
 
-def test_custom_all_reduce_two_procs_one_gpu():
+@pytest.mark.parametrize("world", [2, 4])
+def test_custom_all_reduce_procs_one_gpu(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
@@ -78,4 +85,4 @@ def test_custom_all_reduce_two_procs_one_gpu():
     for p in ps:
         if p.is_alive():
             p.kill()
-    assert res == {0: "ok", 1: "ok"}, res
+    assert res == {r: "ok" for r in range(world)}, res
