@@ -124,11 +124,55 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   const int g = lane >> 4, r16 = lane & 15;
 
   // XCD-aware block order: the MB m-blocks of n-block nb get ids that share id % 8
-  const int NB = (a.N + GBN - 1) / GBN, MB = (a.M + GBM - 1) / GBM;
+  const bool grouped = a.moe_off != nullptr;
+  const int NB = (a.N + GBN - 1) / GBN;
+  const int MB = grouped ? (a.M + GBM - 1) / GBM + a.moe_el : (a.M + GBM - 1) / GBM;
   const int id = blockIdx.x;
   const int grp = id / (8 * MB), rem = id % (8 * MB);
-  const int mb = rem / 8, nb = grp * 8 + rem % 8;
+  int mb = rem / 8;
+  const int nb = grp * 8 + rem % 8;
   if (nb >= NB) return;
+  // grouped: global m-block mb -> (local expert e, its m-block); every thread
+  // scans a slice of the experts (block-uniform result, no host sync)
+  int Mrows = a.M, e_sel = 0, pos0 = 0;
+  const uint8_t* wbase = a.w;
+  if (grouped) {
+    __shared__ int mb_tot[256];
+    __shared__ int sel[3];
+    const int per = (a.moe_el + 255) / 256;            // experts per thread (contiguous)
+    int cnt_blocks = 0;
+    for (int j = 0; j < per; j++) {
+      const int e = tid * per + j;
+      if (e < a.moe_el) cnt_blocks += (a.moe_off[e + 1] - a.moe_off[e] + GBM - 1) / GBM;
+    }
+    mb_tot[tid] = cnt_blocks;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {                 // inclusive scan of m-blocks per thread slice
+      const int v = tid >= o ? mb_tot[tid - o] : 0;
+      __syncthreads();
+      mb_tot[tid] += v;
+      __syncthreads();
+    }
+    if (tid == 0) sel[0] = -1;
+    __syncthreads();
+    const int ex = mb_tot[tid] - cnt_blocks;
+    if (mb >= ex && mb < mb_tot[tid]) {
+      int r = mb - ex;
+      for (int j = 0; j < per; j++) {
+        const int e = tid * per + j;
+        const int c = (a.moe_off[e + 1] - a.moe_off[e] + GBM - 1) / GBM;
+        if (r < c) { sel[0] = e; sel[1] = r; break; }
+        r -= c;
+      }
+    }
+    __syncthreads();
+    if (sel[0] < 0) return;                             // past the last expert's rows
+    e_sel = sel[0];
+    mb = sel[1];
+    pos0 = a.moe_off[e_sel];
+    Mrows = a.moe_off[e_sel + 1] - pos0;
+    wbase = a.w + (size_t)e_sel * a.w_stride;
+  }
   const int m0 = mb * GBM;
   const int NT = (a.N + 15) / 16;
   const int wn = wave % WA, wm = wave / WA;           // wave position in the block
@@ -136,7 +180,7 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
   const uint8_t* tb[WN];
 #pragma unroll
-  for (int t = 0; t < WN; t++) tb[t] = a.w + (size_t)min(tile0 + t, NT - 1) * TB;
+  for (int t = 0; t < WN; t++) tb[t] = wbase + (size_t)min(tile0 + t, NT - 1) * TB;
   const size_t soff = (size_t)a.KC * dk_code_chunk(DK) + (size_t)r16 * 4;   // + c * 64: row r16 of chunk c
   const size_t moff = soff + (size_t)16 * a.KC * 4;
 
@@ -147,13 +191,20 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   // ---- x staging: thread -> rows (tid / 16) + 16 j, 8 columns at (tid % 16) * 8
   constexpr int XJ = GBM / 16;
   uint4 xr[XJ];
+  int xrow[XJ];                                         // source row of staged row j (-1: padding)
+#pragma unroll
+  for (int j = 0; j < XJ; j++) {
+    const int m = m0 + (tid >> 4) + 16 * j;
+    if (m >= Mrows) xrow[j] = -1;
+    else if (!grouped) xrow[j] = m;
+    else xrow[j] = a.moe_x_sorted ? pos0 + m : a.moe_rows[pos0 + m] / a.moe_xdiv;
+  }
   auto stage_load = [&](int c) {
     const int kk = c * 128 + (tid & 15) * 8;
 #pragma unroll
     for (int j = 0; j < XJ; j++) {
-      const int m = m0 + (tid >> 4) + 16 * j;
-      const bool ok = m < a.M && kk < a.K;
-      const uint4 v = *(const uint4*)(a.x + (size_t)(ok ? m : 0) * a.ldx + (ok ? kk : 0));
+      const bool ok = xrow[j] >= 0 && kk < a.K;
+      const uint4 v = *(const uint4*)(a.x + (size_t)(ok ? xrow[j] : 0) * a.ldx + (ok ? kk : 0));
       xr[j] = ok ? v : make_uint4(0, 0, 0, 0);
     }
   };
@@ -268,8 +319,9 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
       if (n0 >= I) continue;
 #pragma unroll
       for (int mt = 0; mt < WM; mt++) {
-        const int m = m0 + (wm * WM + mt) * 16 + r16;
-        if (m >= a.M) continue;
+        const int mm = m0 + (wm * WM + mt) * 16 + r16;
+        if (mm >= Mrows) continue;
+        const int m = !grouped ? mm : (a.moe_out_sorted ? pos0 + mm : a.moe_rows[pos0 + mm]);
         float o[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -295,10 +347,17 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
       for (int i = 0; i < 4; i++) bv[i] = n0 + i < a.N ? to_f32<T>(a.bias[n0 + i]) : 0.f;
 #pragma unroll
     for (int mt = 0; mt < WM; mt++) {
-      const int m = m0 + (wm * WM + mt) * 16 + r16;
-      if (m >= a.M) continue;
+      const int mm = m0 + (wm * WM + mt) * 16 + r16;
+      if (mm >= Mrows) continue;
+      const int m = !grouped ? mm : (a.moe_out_sorted ? pos0 + mm : a.moe_rows[pos0 + mm]);
       const float o[4] = {acc[t][mt][0] + bv[0], acc[t][mt][1] + bv[1], acc[t][mt][2] + bv[2],
                           acc[t][mt][3] + bv[3]};
+      if (a.out_f32) {
+        float* yf = (float*)a.out + (size_t)m * a.ldo + n0;
+        if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) *(float4*)yf = make_float4(o[0], o[1], o[2], o[3]);
+        else for (int i = 0; i < 4 && n0 + i < a.N; i++) yf[i] = o[i];
+        continue;
+      }
       uint16_t* y = a.out + (size_t)m * a.ldo + n0;
       if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
       else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
@@ -309,7 +368,9 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
 template <int DK, int WN, int WM, int PFW, int WA = 4>
 static void launch_gemm_v(bool bf16, const GemmArgs& a, hipStream_t st) {
   constexpr int GBM = (4 / WA) * WM * 16, GBN = WA * WN * 16;
-  const int NB = (a.N + GBN - 1) / GBN, MB = (a.M + GBM - 1) / GBM;
+  const int NB = (a.N + GBN - 1) / GBN;
+  // grouped: every expert may end with a partial m-block
+  const int MB = a.moe_off ? (a.M + GBM - 1) / GBM + a.moe_el : (a.M + GBM - 1) / GBM;
   const int NBp = (NB + 7) / 8 * 8;
   dim3 grid((unsigned)(NBp * MB));
   if (bf16) hipLaunchKernelGGL((lowbit_gemm_kernel<DK, BF16, WN, WM, PFW, WA>), grid, dim3(256), 0, st, a);
@@ -318,6 +379,7 @@ static void launch_gemm_v(bool bf16, const GemmArgs& a, hipStream_t st) {
 
 template <int DK>
 static void launch_gemm_dk(bool bf16, const GemmArgs& a, hipStream_t st) {
+  if (a.moe_off != nullptr) return launch_gemm_v<DK, 2, 8, 4>(bf16, a, st);   // grouped: 128 x 128 blocks
   // default 128 n x 128 m blocks (2 tiles x 8 m-tiles per wave).  ILLM_GEMM_TILE=2 selects
   // 256 n x 64 m: half the LDS x traffic per MFMA but 268 registers -> 1 wave per SIMD;
   // measured on MI355X (Llama-3-8B shapes, sym_int4): M = 1024 qkv/o/down +1..14 %,

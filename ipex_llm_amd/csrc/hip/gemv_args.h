@@ -95,6 +95,7 @@ struct GemvArgs {
   // whose readers all finished before this launch (stream order)
   float* nzero;
   int nzero_n;
+  int pf8;                 // v5: request a <= 8-chunk split-K slice in one go (ILLM_GEMV5_PF8)
 };
 
 }  // namespace illm

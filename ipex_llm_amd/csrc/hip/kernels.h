@@ -42,6 +42,17 @@ struct GemmArgs {
   int glu;                 // 1: tile-interleaved gate/up weight, out = act(gate) * up [M, N / 2]
   int act;                 // 0 = silu, 1 = gelu(tanh)
   int x_f16;               // 1: x already holds f16 (saturated) copies of the bf16 activations
+  // grouped (MoE, "FlashMoE") launch: (token, expert) pairs sorted by expert
+  // (moe_align); blockIdx.x walks (expert, m-block) over every local expert's
+  // pairs, weights of expert e at w + e * w_stride.  M = number of pairs.
+  const int32_t* moe_off;  // [El + 1] pair offsets per local expert (device), null = plain GEMM
+  const int32_t* moe_rows; // [P] pair ids sorted by expert
+  int moe_el;              // local experts
+  int moe_xdiv;            // gathered x row = pair id / moe_xdiv (x_sorted == 0)
+  int moe_x_sorted;        // 1: x row = sorted position (the previous grouped GEMM's output)
+  int moe_out_sorted;      // 1: out row = sorted position; 0: out row = pair id
+  int64_t w_stride;        // bytes between experts' blobs
+  int out_f32;             // 1: out is f32 [rows, ldo] (pre-combine partials)
 };
 void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st);
 // bf16 -> f16 with saturation at +-65504 (the GEMM's MFMA input type), n % 8 == 0

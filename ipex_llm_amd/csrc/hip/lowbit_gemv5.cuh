@@ -154,9 +154,10 @@ __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
 #endif
 }
 
-template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW>
+template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4>
 __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a) {
-  constexpr int PF = 4;                 // chunks in flight per wave (6 and 8 measured slower)
+  // PF: chunks in flight per wave (4; 8 = every chunk of a decode split-K
+  // slice of <= 8 chunks requested before the prologue)
   using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;   // MFMA input type
   constexpr int BITS = dk_bits(DK);
   constexpr int TG = NW / KW;          // tile groups per workgroup (NW waves)
@@ -521,7 +522,7 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
 #pragma unroll
     for (int u = 0; u < PF; u++) {
       if (c + u < c1u) compute_chunk(ring[u], c + u);
-      load_chunk(ring[u], c + u + PF);
+      if (PF < 8 || c + u + PF < c1u) load_chunk(ring[u], c + u + PF);   // PF 8: no clamped re-loads
     }
     c += PF;
 #pragma unroll
@@ -641,10 +642,16 @@ inline void launch5(K kern, dim3 grid, size_t shmem, const GemvArgs& a, hipStrea
 
 template <int DK, typename T, int KW, bool MOE, int NW>
 inline void launch5_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  // all loads of a short split-K slice up front (decode projections: 8 chunks)
+  const bool pf8 = a.pf8 && !MOE && KW == 1 && a.cpk > 0 && a.cpk <= 8;
   if (epi == EPI_STORE) launch5(lowbit_gemv5_kernel<DK, T, EPI_STORE, 1, KW, MOE, NW>, grid, shmem, a, st);
-  else if (epi == EPI_PARTIAL) launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, NW>, grid, shmem, a, st);
-  else if (epi == EPI_ATOMIC) launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, NW>, grid, shmem, a, st);
-  else launch5(lowbit_gemv5_kernel<DK, T, EPI_GLU, 2, KW, MOE, NW>, grid, shmem, a, st);
+  else if (epi == EPI_PARTIAL) {
+    if (pf8) launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, NW, 8>, grid, shmem, a, st);
+    else launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, NW>, grid, shmem, a, st);
+  } else if (epi == EPI_ATOMIC) {
+    if (pf8) launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, NW, 8>, grid, shmem, a, st);
+    else launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, NW>, grid, shmem, a, st);
+  } else launch5(lowbit_gemv5_kernel<DK, T, EPI_GLU, 2, KW, MOE, NW>, grid, shmem, a, st);
 }
 
 template <int DK, typename T, bool MOE>

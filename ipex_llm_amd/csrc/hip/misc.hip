@@ -552,12 +552,12 @@ __global__ void __launch_bounds__(1024) moe_align_kernel(const int32_t* ids, int
     off[El] = acc;
   }
   __syncthreads();
+  // slot within the expert from an LDS cursor: O(P) (the within-expert order
+  // is free -- every consumer indexes rows by pair id)
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
-    const int id = ids[p], e = id - e0;
+    const int e = ids[p] - e0;
     if (e < 0 || e >= El) continue;
-    int r = 0;
-    for (int q = 0; q < p; q++) r += ids[q] == id;
-    rows[start[e] + r] = p;
+    rows[atomicAdd(&start[e], 1)] = p;
   }
 }
 

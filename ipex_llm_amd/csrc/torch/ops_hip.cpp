@@ -69,8 +69,11 @@ void launch_gemv_any(int fmt, bool bf16, int mt, int epi, dim3 grid, const illm:
   hipStream_t st = cur_stream();
   ILLM_DK_SWITCH(fmt, illm::launch_gemv_dk<DKV>(bf16, mt, epi, grid, a, st));
 }
-void launch_gemv5_any(int fmt, bool bf16, int kw, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a) {
+void launch_gemv5_any(int fmt, bool bf16, int kw, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a0) {
   hipStream_t st = cur_stream();
+  static const int pf8 = getenv("ILLM_GEMV5_PF8") ? atoi(getenv("ILLM_GEMV5_PF8")) : 0;
+  illm::GemvArgs a = a0;
+  a.pf8 = pf8;
   ILLM_DK_SWITCH(fmt, illm::launch_gemv5_dk<DKV>(bf16, kw, epi, grid, shmem, a, st));
 }
 
@@ -284,6 +287,65 @@ Tensor gemm_glu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   a.lut_fmt = (int)fmt;
   a.glu = 1;
   a.act = (int)act;
+  illm::launch_lowbit_gemm(bf16, (int)fmt, a, cur_stream());
+  return out;
+}
+
+// grouped ("FlashMoE") prefill GEMM over (token, expert) pairs sorted by
+// expert (moe_align): ONE launch per projection for every local expert, the
+// weights of expert e dequantized in registers from blob[e].  x rows are
+// gathered by pair id / xdiv (x_sorted = false: the tokens) or taken in sorted
+// order (x_sorted: the previous grouped GEMM's output); out rows are the
+// sorted position (out_sorted) or the pair id.  Reference: the vLLM-XPU
+// fused_moe over ipex-llm low-bit experts (vllm_for_multi_arc.patch:5933-6116)
+// and the per-expert loops of models/qwen3_moe.py:70-105.
+Tensor moe_gemm(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, const Tensor& off,
+                const Tensor& rows, int64_t xdiv, bool x_sorted, bool out_sorted, bool glu, int64_t act,
+                bool out_f32) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda() && off.is_cuda() && rows.is_cuda(), "moe_gemm: GPU tensors expected");
+  TORCH_CHECK(blob.dim() == 2 && blob.scalar_type() == at::kByte, "moe_gemm: blob must be uint8 [E, bytes]");
+  TORCH_CHECK(off.scalar_type() == at::kInt && rows.scalar_type() == at::kInt, "moe_gemm: int32 off / rows");
+  TORCH_CHECK(x.size(-1) == k && k % 8 == 0, "moe_gemm: x last dim != in_features");
+  TORCH_CHECK(!glu || n % 32 == 0, "moe_gemm: GLU weights need a multiple of 32 rows");
+  const int64_t El = off.numel() - 1, P = rows.numel();
+  TORCH_CHECK(El >= 1 && El <= 4096 && blob.size(0) == El, "moe_gemm: blob experts != off");
+  TORCH_CHECK(blob.size(1) >= illm::dev_total_bytes((int)fmt, n, k), "moe_gemm: weight blob too small");
+  TORCH_CHECK(xdiv >= 1, "moe_gemm: xdiv >= 1");
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous().view({-1, k});
+  TORCH_CHECK(!x_sorted || xc.size(0) >= P, "moe_gemm: sorted x needs a row per pair");
+  const int64_t nout = glu ? n / 2 : n;
+  Tensor out = at::empty({P, nout}, xc.options().dtype(out_f32 ? at::kFloat : xc.scalar_type()));
+  if (P == 0) return out;
+  illm::GemmArgs a{};
+  Tensor xh;
+  if (bf16) {
+    xh = at::empty(xc.sizes(), xc.options().dtype(at::kHalf));
+    illm::launch_bf16_to_f16_sat(p16(xc), m16(xh), xc.numel(), cur_stream());
+    a.x_f16 = 1;
+  }
+  a.x = bf16 ? p16(xh) : p16(xc);
+  a.M = (int)P;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.N = (int)n;
+  a.KC = (int)(illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K);
+  a.out = (uint16_t*)out.data_ptr();
+  a.ldo = (int)nout;
+  a.lut_fmt = (int)fmt;
+  a.glu = glu ? 1 : 0;
+  a.act = (int)act;
+  a.moe_off = off.data_ptr<int32_t>();
+  a.moe_rows = rows.data_ptr<int32_t>();
+  a.moe_el = (int)El;
+  a.moe_xdiv = (int)xdiv;
+  a.moe_x_sorted = x_sorted ? 1 : 0;
+  a.moe_out_sorted = out_sorted ? 1 : 0;
+  a.w_stride = blob.size(1);
+  a.out_f32 = out_f32 ? 1 : 0;
+  TORCH_CHECK(!(glu && out_f32), "moe_gemm: the GLU epilogue writes activations (no f32 out)");
   illm::launch_lowbit_gemm(bf16, (int)fmt, a, cur_stream());
   return out;
 }
@@ -715,10 +777,10 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, cons
 // token come from the qkv GEMV's atomic accumulator part [B, ld] (+ bias); no
 // rope_kv launch.  The combine launch re-zeroes the accumulator (part is
 // written: zero for the next atomic GEMV).
-Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin,
-                        const Tensor& pos, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
-                        const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
-                        int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt) {
+static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
+    const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin, const Tensor& pos, Tensor& k_cache,
+    Tensor& v_cache, const Tensor& block_tables, const Tensor& seq_lens, int64_t nsplit, double scale, double softcap,
+    int64_t window, int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt, bool no_combine) {
   c10::DeviceGuard g(part.device());
   TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "attn_decode_rope: bf16/fp16 activations");
   TORCH_CHECK(k_cache.scalar_type() == dt && v_cache.scalar_type() == dt, "attn_decode_rope: 16-bit KV cache");
@@ -758,8 +820,11 @@ Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, c
   a.sliding_window = (int)window;
   a.kv_fp8 = 0;
   a.k_scale = a.v_scale = 1.f;
-  // the merging split (fused combine) or the combine launch re-zeroes the accumulator
-  a.counters = fused_combine_on() ? attn_counters(part.device(), B * Hkv) : nullptr;
+  // the merging split (fused combine) or the combine launch re-zeroes the
+  // accumulator; split-only (no_combine): the consumer merges and a later
+  // launch zeroes it
+  a.counters = !no_combine && fused_combine_on() ? attn_counters(part.device(), B * Hkv) : nullptr;
+  a.no_combine = no_combine ? 1 : 0;
   a.rq_part = part.data_ptr<float>();
   a.rq_bias = p16o(bias);
   a.rq_cos_sin = cos_sin.data_ptr<float>();
@@ -769,7 +834,29 @@ Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, c
   a.rq_interleaved = interleaved ? 1 : 0;
   a.rq_qscale = (float)q_scale;
   illm::launch_attn_decode(dt == at::kBFloat16, a, cur_stream());
-  return out;
+  return {out, po, pml};
+}
+
+Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin,
+                        const Tensor& pos, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
+                        const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
+                        int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt) {
+  return std::get<0>(attn_decode_rope_impl(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit,
+                                           scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dt, false));
+}
+
+// fused-RoPE split attention without the combine: (o, m, l) partials for the
+// o_proj GEMV's merging prologue (gemv_attn); the qkv accumulator is NOT
+// re-zeroed here (the caller hands it to a later launch's zeroing)
+std::tuple<Tensor, Tensor> attn_decode_rope_split(const Tensor& part, const c10::optional<Tensor>& bias,
+                                                  const Tensor& cos_sin, const Tensor& pos, Tensor& k_cache,
+                                                  Tensor& v_cache, const Tensor& block_tables, const Tensor& seq_lens,
+                                                  int64_t nsplit, double scale, double softcap, int64_t window,
+                                                  int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale,
+                                                  at::ScalarType dt) {
+  auto r = attn_decode_rope_impl(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
+                                 softcap, window, Hq, rot_dim, interleaved, q_scale, dt, true);
+  return {std::get<1>(r), std::get<2>(r)};
 }
 
 Tensor attn_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
@@ -838,7 +925,8 @@ std::tuple<Tensor, Tensor> attn_decode_split(const Tensor& q, const Tensor& k_ca
 // its prologue.  acc given: f32 atomics into acc [T, n] (returned); else f32
 // split-K slabs [ks, T, n].
 Tensor gemv_attn(const Tensor& po, const Tensor& pml, const Tensor& seq_lens, const Tensor& blob, int64_t fmt,
-                 int64_t n, int64_t k, const c10::optional<Tensor>& acc, int64_t ksplit, at::ScalarType dt) {
+                 int64_t n, int64_t k, const c10::optional<Tensor>& acc, int64_t ksplit, at::ScalarType dt,
+                 const c10::optional<Tensor>& zero, int64_t nw) {
   TORCH_CHECK(po.is_cuda() && po.dim() == 5 && po.scalar_type() == at::kFloat && po.is_contiguous(),
               "gemv_attn: po must be f32 [B, Hq, Tq, ns, D]");
   c10::DeviceGuard g(po.device());
@@ -868,6 +956,10 @@ Tensor gemv_attn(const Tensor& po, const Tensor& pml, const Tensor& seq_lens, co
   a.N = (int)n;
   const bool atomic = acc.has_value() && acc->defined();
   Plan5 p = plan5(M, NT, KC, true, ksplit, atomic);
+  if (nw == 4 || nw == 8) {            // workgroup size: 8 waves halve the per-head re-reads of the partials
+    p.nw = (int)nw;
+    p.gx = (unsigned)((NT + (p.nw / p.kw) - 1) / (p.nw / p.kw));
+  }
   p.shmem += illm::gemv5_attn_shmem_h((int)M, (int)p.cpk, (int)D, (int)ns);
   TORCH_CHECK(p.shmem <= kMaxLds, "gemv_attn: LDS plan too large (too many attention splits)");
   a.cpk = (int)p.cpk;
@@ -881,6 +973,12 @@ Tensor gemv_attn(const Tensor& po, const Tensor& pml, const Tensor& seq_lens, co
   } else {
     out = at::empty({p.ks, M, n}, po.options());
     a.out = out.data_ptr();
+  }
+  if (zero.has_value() && zero->defined()) {
+    TORCH_CHECK(zero->scalar_type() == at::kFloat && zero->is_contiguous() && zero->numel() % 4 == 0,
+                "gemv_attn: zero must be contiguous f32 (numel % 4 == 0)");
+    a.nzero = zero->data_ptr<float>();
+    a.nzero_n = (int)zero->numel();
   }
   a.ldo = (int)n;
   launch_gemv5_any((int)fmt, bf16, p.kw, atomic ? illm::EPI_ATOMIC : illm::EPI_PARTIAL, dim3(p.gx, (unsigned)p.ks),
@@ -1186,9 +1284,11 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv_accum", &gemv_accum);
   m.impl("gemv_norm_in", &gemv_norm_in);
   m.impl("gemm_glu", &gemm_glu);
+  m.impl("moe_gemm", &moe_gemm);
   m.impl("rwkv_wkv4", &rwkv_wkv4);
   m.impl("rwkv_wkv5", &rwkv_wkv5);
   m.impl("attn_decode_rope", &attn_decode_rope);
+  m.impl("attn_decode_rope_split", &attn_decode_rope_split);
   m.impl("gemm", &gemm);
   m.impl("attn_decode_split", &attn_decode_split);
   m.impl("attn_prefill", &attn_prefill);

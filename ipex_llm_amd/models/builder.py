@@ -106,7 +106,8 @@ def lowbit_from_dense(w: torch.Tensor, qtype, device, bias: Optional[torch.Tenso
 
 @torch.no_grad()
 def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat16, seed: int = 0,
-                        lm_head_qtype=None, std: float = 0.02, tp_group=None, ep_group=None) -> NativeCausalLM:
+                        lm_head_qtype=None, std: float = 0.02, tp_group=None, ep_group=None,
+                        tp_shard_lm_head: bool = True) -> NativeCausalLM:
     """Random-init model of ``cfg``'s architecture, quantized on ``device``.
 
     ``tp_group``: tensor parallel (AutoTP layout, SRC example
@@ -179,7 +180,7 @@ def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat
         torch.cuda.empty_cache() if torch.device(device).type == "cuda" else None
     embed = rnd(s.vocab_size, s.hidden_size)
     head_w = embed if s.tie_embeddings else rnd(s.vocab_size, s.hidden_size)
-    if W > 1:
+    if W > 1 and tp_shard_lm_head:
         from ..parallel.tp import VocabParallelHead
         per = (s.vocab_size + W - 1) // W
         a, b = R * per, min(s.vocab_size, (R + 1) * per)

@@ -334,6 +334,13 @@ class NativeCausalLM(nn.Module):
             self._acc_bufs[key] = buf
         return buf
 
+    # decode (norm-in + fused-RoPE path): attention partials merged in the o_proj
+    # GEMV prologue instead of a combine launch (ILLM_OPROJ_COMBINE=1), with
+    # ILLM_OPROJ_KS K slices (32 = one head per workgroup) of ILLM_OPROJ_NW waves
+    _oproj_combine = __import__("os").environ.get("ILLM_OPROJ_COMBINE", "0") == "1"
+    _oproj_ks = int(__import__("os").environ.get("ILLM_OPROJ_KS", "32"))
+    _oproj_nw = int(__import__("os").environ.get("ILLM_OPROJ_NW", "8"))
+
     # ILLM_PREFILL_ATTN=sdpa: torch SDPA over gathered keys instead of the HIP kernel (A/B)
     _prefill_attn_native = __import__("os").environ.get("ILLM_PREFILL_ATTN", "hip") != "sdpa"
 
@@ -575,7 +582,7 @@ class NativeCausalLM(nn.Module):
                                       rope, s.num_heads, s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved,
                                       attn.q_norm, attn.k_norm, s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale,
                                       cache.v_scale, meta.pos_offset, zero_part=T <= ACC_MAX_M)
-                else:
+                elif not (norm_in and self._oproj_combine and attn.o_proj.bias is None):
                     a_rope = ops.attn_decode_rope(qkv_acc, qp.bias, self.rope_cache, pos, cache.k[li], cache.v[li],
                                                   meta.block_tables, meta.seq_lens, meta.nsplit, s.scale,
                                                   s.attn_softcap, attn.sliding_window, s.num_heads, s.rot_dim,
@@ -591,17 +598,31 @@ class NativeCausalLM(nn.Module):
                 # o_proj -> atomic slab P (zeroing the slab the qkv prologue consumed);
                 # the gate/up GEMV adds P to the residual and normalises in its prologue;
                 # down -> atomic slab D (zeroing P), pending for the next layer's qkv
-                a = a_rope if rope_in else self._attention(li, attn, q, meta, cache)
                 o, mlp = attn.o_proj, layer.mlp
                 H = o.out_features
                 accP, accD = self._acc(H, T, x.device, "P"), self._acc(H, T, x.device, "D")
-                ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
+                zero_qkv = None
+                if rope_in and self._oproj_combine and o.bias is None:
+                    # split attention without its combine launch: the o_proj GEMV
+                    # merges each head's partials while staging its K slice (head-
+                    # aligned slices: one head per workgroup), the qkv slab is
+                    # zeroed by the gate/up launch below
+                    po, pml = ops.attn_decode_rope_split(qkv_acc, qp.bias, self.rope_cache, pos, cache.k[li],
+                                                         cache.v[li], meta.block_tables, meta.seq_lens, meta.nsplit,
+                                                         s.scale, s.attn_softcap, attn.sliding_window, s.num_heads,
+                                                         s.rot_dim, s.rope_interleaved, 1.0, x.dtype)
+                    ops.gemv_attn(po, pml, meta.seq_lens, o.weight, o.fmt, H, o.in_features, accP,
+                                  self._oproj_ks, x.dtype, zero=consumed, nw=self._oproj_nw)
+                    zero_qkv = qkv_acc
+                else:
+                    a = a_rope if rope_in else self._attention(li, attn, q, meta, cache)
+                    ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
                 self._reduce(accP, o)
                 r2 = nxt_res(residual)
                 gu, dn = mlp.gate_up_proj, mlp.down_proj
                 act = ops.gemv_norm_in(accP, residual, r2, layer.post_attention_layernorm, s.rms_eps,
                                        s.norm_unit_offset, gu.weight, gu.fmt, gu.out_features, gu.in_features, True,
-                                       s.act)
+                                       s.act, zero=zero_qkv)
                 residual = r2
                 ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=accP)
                 self._reduce(accD, dn)

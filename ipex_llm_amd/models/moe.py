@@ -182,7 +182,11 @@ class NativeMoE(nn.Module):
         return c
 
     def graph_max_tokens(self) -> int:
-        """tokens per forward that stay on device-only launches (capturable)"""
+        """tokens per forward that stay on device-only launches (capturable):
+        the grouped GEMV up to 16 tokens, the grouped GEMM above"""
+        dev = self.gate_up.weight.device
+        if dev.type == "cuda" and ops.native_gpu(self.gate_up.weight) and self.gate_up.out_features % 32 == 0:
+            return 1 << 30
         return 16
 
     def fused_route_ok(self, x2: torch.Tensor) -> bool:
@@ -234,8 +238,27 @@ class NativeMoE(nn.Module):
         part = ops.moe_gemv_partials(a, dn.weight, dn.fmt, dn.out_features, dn.in_features, off, rows)
         return ops.moe_combine(part, w, ids, self.e0, El, x.dtype)
 
+    def _experts_gemm(self, x, w, ids):
+        """prefill ("FlashMoE"): pairs sorted by expert on the device, ONE
+        grouped MFMA GEMM per projection over every local expert (GLU in the
+        gate/up epilogue, f32 per-pair rows from the down GEMM), one combine
+        launch applying the routing weights.  No host sync: capturable."""
+        El = self.local_experts
+        off, rows = ops.moe_align(ids, self.e0, El)
+        gu, dn = self.gate_up, self.down
+        a = ops.moe_gemm(x, gu.weight, gu.fmt, gu.out_features, gu.in_features, off, rows, self.top_k,
+                         False, True, True, self.act)
+        part = ops.moe_gemm(a, dn.weight, dn.fmt, dn.out_features, dn.in_features, off, rows, 1,
+                            True, False, False, 0, True)
+        return ops.moe_combine(part.unsqueeze(0), w, ids, self.e0, El, x.dtype)
+
+    def grouped_gemm_ok(self, x2: torch.Tensor) -> bool:
+        return (x2.is_cuda and ops.native_gpu(x2) and x2.dtype in (torch.bfloat16, torch.float16)
+                and self.gate_up.in_features % 8 == 0 and self.down.in_features % 8 == 0
+                and self.local_experts <= 4096 and self.gate_up.out_features % 32 == 0)
+
     def _experts_loop(self, x, w, ids):
-        """prefill / CPU: per-expert token groups through low-bit GEMMs"""
+        """CPU / fallback: per-expert token groups through low-bit GEMMs"""
         from .decoder import deinterleave_glu
         T, H = x.shape
         y = torch.zeros(T, H, dtype=torch.float32, device=x.device)
@@ -262,6 +285,8 @@ class NativeMoE(nn.Module):
             if x2.is_cuda and x2.shape[0] <= 16 and ops.native_gpu(x2) and \
                     self.gate_up.in_features * 2 * min(16, x2.shape[0]) <= 150 * 1024:
                 y = self._experts_grouped(x2, w, ids)
+            elif self.grouped_gemm_ok(x2):
+                y = self._experts_gemm(x2, w, ids)
             else:
                 y = self._experts_loop(x2, w, ids)
         if self.ep_group is not None:
@@ -323,6 +348,8 @@ class HFLowBitExperts(nn.Module):
         w = top_k_weights.float()
         if x.is_cuda and x.shape[0] <= 16 and ops.native_gpu(x):
             y = NativeMoE._experts_grouped(moe, x, w, ids)
+        elif NativeMoE.grouped_gemm_ok(moe, x):
+            y = NativeMoE._experts_gemm(moe, x, w, ids)
         else:
             y = NativeMoE._experts_loop(moe, x, w, ids)
         if ep is not None:

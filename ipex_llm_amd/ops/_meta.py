@@ -150,7 +150,7 @@ def _(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, windo
 
 
 @register_fake("ipex_llm_amd::gemv_attn")
-def _(po, pml, seq_lens, blob, fmt, n, k, acc, ksplit, dtype):
+def _(po, pml, seq_lens, blob, fmt, n, k, acc, ksplit, dtype, zero=None, nw=0):
     M = po.shape[0] * po.shape[2]
     if acc is not None:
         return torch.empty_like(acc)
@@ -170,11 +170,23 @@ def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit
     return part.new_empty((part.shape[0], 1, Hq, k_cache.shape[3]), dtype=dtype)
 
 
+@register_fake("ipex_llm_amd::attn_decode_rope_split")
+def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, Hq,
+      rot_dim, interleaved, q_scale, dtype):
+    B, D = part.shape[0], k_cache.shape[3]
+    return (part.new_empty((B, Hq, 1, nsplit, D)), part.new_empty((B, Hq, 1, nsplit, 2)))
+
+
 @register_fake("ipex_llm_amd::gemm_glu")
 def _(x, blob, fmt, n, k, act):
     shape = list(x.shape)
     shape[-1] = n // 2
     return x.new_empty(shape)
+
+
+@register_fake("ipex_llm_amd::moe_gemm")
+def _(x, blob, fmt, n, k, off, rows, xdiv, x_sorted, out_sorted, glu, act, out_f32):
+    return x.new_empty((rows.shape[0], n // 2 if glu else n), dtype=torch.float32 if out_f32 else x.dtype)
 
 
 @register_fake("ipex_llm_amd::rwkv_wkv4")

@@ -18,7 +18,7 @@ __all__ = [
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
-    "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope", "attn_prefill", "moe_group_topk",
+    "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope", "attn_decode_rope_split", "attn_prefill", "moe_group_topk",
 ]
 
 
@@ -278,6 +278,16 @@ def moe_route(x, router, k: int, renorm: bool, scoring: int, e0: int, num_local:
     return w, ids, off, rows
 
 
+def moe_gemm(x, blob, fmt, n, k, off, rows, xdiv: int, x_sorted: bool, out_sorted: bool, glu: bool,
+             act: int = 0, out_f32: bool = False):
+    """Grouped low-bit GEMM over (token, expert) pairs sorted by expert
+    (``moe_align``), one launch for every local expert.  blob: uint8 [E, bytes].
+    Rows of the result: sorted position (``out_sorted``) or pair id."""
+    if _native(x):
+        return _ops().moe_gemm(x, blob, fmt, n, k, off, rows, xdiv, x_sorted, out_sorted, glu, act, out_f32)
+    return R.moe_gemm(x, blob, fmt, n, k, off, rows, xdiv, x_sorted, out_sorted, glu, act, out_f32)
+
+
 def moe_combine(part, w, ids, e0: int, num_local: int, dtype=torch.bfloat16):
     """y[t] = sum_j w[t, j] * sum_s part[s, t*k+j] over local experts."""
     if _native(part):
@@ -423,7 +433,19 @@ def attn_decode_split(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale
                                     softcap, window, kv_fp8, k_scale, v_scale, alibi)
 
 
-def gemv_attn(po, pml, seq_lens, blob, fmt, n, k, acc=None, ksplit: int = 0, dtype=torch.bfloat16):
+def gemv_attn(po, pml, seq_lens, blob, fmt, n, k, acc=None, ksplit: int = 0, dtype=torch.bfloat16, zero=None,
+              nw: int = 0):
     """o_proj over the attention partials (combined in the GEMV prologue):
-    atomics into ``acc`` [T, n] when given, else f32 split-K slabs [ks, T, n]."""
-    return _ops().gemv_attn(po, pml, seq_lens, blob, fmt, n, k, acc, ksplit, dtype)
+    atomics into ``acc`` [T, n] when given, else f32 split-K slabs [ks, T, n].
+    ``zero``: an f32 buffer zeroed first (a consumed accumulator); ``nw``:
+    waves per workgroup (8 halves the re-reads of each head's partials)."""
+    return _ops().gemv_attn(po, pml, seq_lens, blob, fmt, n, k, acc, ksplit, dtype, zero, nw)
+
+
+def attn_decode_rope_split(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
+                           softcap, window, Hq: int, rot_dim: int, interleaved: bool, q_scale: float = 1.0,
+                           dtype=torch.bfloat16):
+    """:func:`attn_decode_rope` without the combine: returns the (o, m, l)
+    partials for :func:`gemv_attn`; ``part`` is left for the caller to zero."""
+    return _ops().attn_decode_rope_split(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens,
+                                         nsplit, scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dtype)

@@ -296,3 +296,28 @@ def moe_combine(part, w, ids, e0, num_local, dtype):
     e = ids.reshape(T, k).long() - e0
     valid = ((e >= 0) & (e < num_local)).float()
     return (s * (w.reshape(T, k).float() * valid)[..., None]).sum(1).to(dtype)
+
+
+def moe_gemm(x, blob, fmt, n, k, off, rows, xdiv, x_sorted, out_sorted, glu, act=0, out_f32=False):
+    """fp32 reference of the grouped MoE GEMM (ops.moe_gemm)."""
+    import torch.nn.functional as F
+    P = rows.numel()
+    nout = n // 2 if glu else n
+    out = torch.zeros(P, nout, dtype=torch.float32, device=x.device)
+    offl = off.tolist()
+    rl = rows.tolist()
+    for e in range(len(offl) - 1):
+        s0, s1 = offl[e], offl[e + 1]
+        if s1 <= s0:
+            continue
+        w = (dequantize_device_blob(blob[e], fmt, n, k) if blob.is_cuda else dequantize_canonical(blob[e], fmt, n, k))
+        pos = list(range(s0, s1))
+        xr = [p if x_sorted else rl[p] // xdiv for p in pos]
+        y = x[xr].float() @ w.float().t()
+        if glu:
+            g = y.view(len(pos), n // 32, 2, 16)
+            gate, up = g[:, :, 0].reshape(len(pos), -1), g[:, :, 1].reshape(len(pos), -1)
+            y = (F.silu(gate) if act == 0 else F.gelu(gate, approximate="tanh")) * up
+        orow = pos if out_sorted else [rl[p] for p in pos]
+        out[orow] = y
+    return out if out_f32 else out.to(x.dtype)

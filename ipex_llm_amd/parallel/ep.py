@@ -75,39 +75,61 @@ def shard_experts(model: nn.Module, group=None) -> nn.Module:
 def ep_moe_all_to_all(x: torch.Tensor, moe, group=None) -> torch.Tensor:
     """Token-sharded MoE: x [T_local, H] are THIS rank's tokens; ``moe`` is
     the rank's :class:`NativeMoE` (local experts [e0, e0+El)).  Returns the
-    routed-experts output for the local tokens (shared expert not included)."""
+    routed-experts output for the local tokens (shared expert not included).
+
+    Dropless fixed-capacity dispatch (every rank may send all of its T*k
+    pairs to one peer): pairs are sorted by destination rank on the device
+    (``moe_align`` over rank ids), packed into [world, T*k, H] slots and
+    exchanged with equal-split ``all_to_all_single`` (RCCL alltoall over
+    xGMI); the receiver marks empty slots with expert -1, so the grouped
+    expert GEMMs skip them.  No host synchronisation and no per-expert
+    Python loop: the whole dispatch / compute / combine is capturable."""
+    from .. import ops
     world = get_world_size(group)
     El = moe.local_experts
     T, H = x.shape
     w, ids = moe.route(x)                                     # [T, k]
     k = ids.shape[1]
-    flat = ids.reshape(-1).long()
-    dest = flat // El
-    order = torch.argsort(dest * (T * k) + torch.arange(T * k, device=x.device))
-    send_counts = torch.bincount(dest, minlength=world)
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    sc, rc = send_counts.tolist(), recv_counts.tolist()
-    tok = order // k
-    send_x = x[tok].contiguous()
-    send_e = flat[order].to(torch.int32).contiguous()
-    recv_x = x.new_empty(sum(rc), H)
-    recv_e = send_e.new_empty(sum(rc))
-    dist.all_to_all_single(recv_x, send_x, rc, sc, group=group)
-    dist.all_to_all_single(recv_e, send_e, rc, sc, group=group)
-    # compute the received (token, expert) pairs on the local experts
-    out = torch.zeros(recv_x.shape[0], H, dtype=torch.float32, device=x.device)
-    from ..models.decoder import deinterleave_glu
-    import torch.nn.functional as F
-    le = recv_e.long() - moe.e0
-    for e in torch.unique(le).tolist():
-        sel = (le == e).nonzero(as_tuple=True)[0]
-        h = moe.gate_up.matmul(recv_x[sel], e)
-        g, u = deinterleave_glu(h)
-        a = (F.silu(g.float()) if moe.act == 0 else F.gelu(g.float(), approximate="tanh")) * u.float()
-        out[sel] = moe.down.matmul(a.to(x.dtype), e).float()
-    back = torch.empty(T * k, H, dtype=torch.float32, device=x.device)
-    dist.all_to_all_single(back, out, sc, rc, group=group)
-    y = torch.zeros(T, H, dtype=torch.float32, device=x.device)
-    y.index_add_(0, tok, back * w.reshape(-1)[order].float()[:, None])
+    P = T * k
+    dev = x.device
+    ids32 = ids.reshape(-1).to(torch.int32).contiguous()
+    dest = torch.div(ids32, El, rounding_mode="floor").to(torch.int32)
+    off, rows = ops.moe_align(dest, 0, world)                  # pairs sorted by destination rank
+    rows_l = rows.long()
+    dst_sorted = dest.long()[rows_l]
+    slot = torch.arange(P, device=dev) - off.long()[dst_sorted]   # position inside the destination's slots
+    flat = dst_sorted * P + slot
+    send_x = x.new_zeros(world * P, H)
+    send_x.index_copy_(0, flat, x[rows_l // k])
+    send_e = torch.full((world * P,), -1, dtype=torch.int32, device=dev)
+    send_e.index_copy_(0, flat, ids32[rows_l])
+    recv_x = torch.empty_like(send_x)
+    recv_e = torch.empty_like(send_e)
+    dist.all_to_all_single(recv_x, send_x, group=group)
+    dist.all_to_all_single(recv_e, send_e, group=group)
+    # expert id -1 (empty slot) and other ranks' experts fall outside [e0, e0 + El)
+    if x.is_cuda and ops.native_gpu(x) and moe.grouped_gemm_ok(x):
+        off2, rows2 = ops.moe_align(recv_e, moe.e0, El)
+        gu, dn = moe.gate_up, moe.down
+        a = ops.moe_gemm(recv_x, gu.weight, gu.fmt, gu.out_features, gu.in_features, off2, rows2, 1,
+                         False, True, True, moe.act)
+        out = ops.moe_gemm(a, dn.weight, dn.fmt, dn.out_features, dn.in_features, off2, rows2, 1,
+                           True, False, False, 0, True)
+        out = torch.where((recv_e >= 0)[:, None], out, out.new_zeros(()))   # unwritten rows of empty slots
+    else:                                                     # CPU / non-native fallback
+        import torch.nn.functional as F
+        from ..models.decoder import deinterleave_glu
+        out = torch.zeros(recv_x.shape[0], H, dtype=torch.float32, device=dev)
+        for e in range(El):
+            sel = (recv_e == moe.e0 + e).nonzero(as_tuple=True)[0]
+            if sel.numel() == 0:
+                continue
+            g, u = deinterleave_glu(moe.gate_up.matmul(recv_x[sel], e))
+            a = (F.silu(g.float()) if moe.act == 0 else F.gelu(g.float(), approximate="tanh")) * u.float()
+            out[sel] = moe.down.matmul(a.to(x.dtype), e).float()
+    back = torch.empty_like(out)
+    dist.all_to_all_single(back, out, group=group)
+    y = torch.zeros(T, H, dtype=torch.float32, device=dev)
+    wf = w.reshape(-1).float()[rows_l]
+    y.index_add_(0, rows_l // k, back[flat] * wf[:, None])
     return y.to(x.dtype)

@@ -183,6 +183,12 @@ class _BaseAutoModelClass:
             # AutoTP on the dense weights; each rank quantizes only its shard
             from ..parallel.tp import auto_tp
             auto_tp(model, tp_group)
+            # decode-sized row-parallel messages take the xGMI peer all-reduce
+            # (RCCL stays the fallback for large / ineligible messages)
+            tp = getattr(model, "_tp", None)
+            if tp is not None:
+                from ..parallel.comm import setup_custom_all_reduce
+                setup_custom_all_reduce(tp["group"])
         if expert_parallel:
             # each rank keeps (and quantizes) only its experts
             from ..parallel.ep import shard_experts

@@ -39,10 +39,10 @@ def _worker(rank, world, port, q):
                     for it in range(3):
                         g = torch.Generator(device="cuda").manual_seed(1000 * it + n)
                         base = torch.randn(world, n, generator=g, device="cuda").to(dt)
-                        mine = base[rank].contiguous()
+                        mine = base[rank].clone()
+                        want = base.float().sum(0)
                         # in place (the decoder reduces its f32 accumulator where it lies)
                         out = car(mine, out=mine if it == 2 else None, two_shot=two)
-                        want = base.float().sum(0)
                         err = ((out.float() - want).abs().max() / want.abs().max()).item()
                         tol = 1e-5 if dt == torch.float32 else 2e-2
                         assert err < tol, (dt, n, two, it, err)

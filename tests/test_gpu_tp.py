@@ -1,0 +1,85 @@
+"""Tensor-parallel native decode on the GPU inside the captured hipGraph.
+
+The 1-GPU test box cannot run a multi-GPU job, so 2 ranks share cuda:0 (gloo
+for the host-side rendezvous, the custom peer all-reduce for every
+row-parallel accumulator -- the same kernels and IPC handle exchange as ranks
+on separate GPUs).  Each rank keeps half the heads / intermediate rows of the
+same random weights; the hipGraph decode must reproduce the single-GPU
+model's greedy tokens.  lm_head stays replicated here (its vocab-parallel
+all-gather is an RCCL collective, not available between two processes on one
+device)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+PROMPTS = [[3, 14, 15, 92, 65, 35, 89, 79], [27, 18, 28, 18, 28, 45, 90, 45, 2]]
+
+
+def _cfg():
+    from transformers import LlamaConfig
+    return LlamaConfig(vocab_size=512, hidden_size=512, intermediate_size=1024, num_hidden_layers=3,
+                       num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=1024)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, want, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from ipex_llm_amd.parallel import comm
+        from ipex_llm_amd.models.builder import random_native_model
+        from ipex_llm_amd.engine.runner import Engine
+        g = dist.group.WORLD
+        comm._CUSTOM[id(g)] = comm.CustomAllReduce(g, device="cuda:0", max_bytes=1 << 20)
+        m = random_native_model(_cfg(), "sym_int4", "cuda:0", torch.bfloat16, seed=0, std=0.05, tp_group=g,
+                                tp_shard_lm_head=False)
+        for use_graph in (False, True):
+            out = Engine(m).generate(PROMPTS, max_new_tokens=8, use_graph=use_graph)
+            assert out == want, (rank, use_graph, out, want)
+        comm._CUSTOM[id(g)].check()
+        torch.cuda.synchronize()
+        comm._CUSTOM.pop(id(g)).close()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+        raise
+
+
+def test_tp_native_graph_decode_two_ranks_one_gpu(cuda):
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.engine.runner import Engine
+    m = random_native_model(_cfg(), "sym_int4", cuda, torch.bfloat16, seed=0, std=0.05)
+    want = Engine(m).generate(PROMPTS, max_new_tokens=8, use_graph=True)
+    del m
+    torch.cuda.empty_cache()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, want, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(240)
+    res = {}
+    while not q.empty():
+        r, msg = q.get()
+        res[r] = msg
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert res == {0: "ok", 1: "ok"}, res
