@@ -58,6 +58,11 @@ void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st);
 // bf16 -> f16 with saturation at +-65504 (the GEMM's MFMA input type), n % 8 == 0
 void launch_bf16_to_f16_sat(const uint16_t* x, uint16_t* y, int64_t n, hipStream_t st);
 
+// ---- k-quant decoders (kquant.hip): GGUF q4_K / q5_K / q6_K / q2_K blocks ---
+void launch_kq_dequant(int fmt, bool bf16, const uint8_t* w, int64_t n, int64_t k, uint16_t* out, hipStream_t st);
+void launch_kq_gemv(int fmt, bool bf16, const uint16_t* x, int M, int64_t K, const uint8_t* w, int64_t N,
+                    uint16_t* out, hipStream_t st);
+
 // ---- norms (norm.hip) ------------------------------------------------------
 struct NormArgs {
   const uint16_t* x;       // [M, H] input (ignored when partials != null)

@@ -97,6 +97,14 @@ def lowbit_from_dense(w: torch.Tensor, qtype, device, bias: Optional[torch.Tenso
         if bias is not None:
             m.bias = nn.Parameter(bias.to(device, dt), requires_grad=False)
         return m
+    f = Q.get_format(qtype)
+    if f is not None and f.kquant:
+        from ..transformers.low_bit_linear import KQuantLinear
+        m = KQuantLinear(w.shape[1], w.shape[0], qtype, bias=False, device="meta")
+        m.load_dense(w, device=device, imatrix=imatrix)
+        if bias is not None:
+            m.bias = nn.Parameter(bias.detach().to(device), requires_grad=False)
+        return m
     m = LowBitLinear(w.shape[1], w.shape[0], qtype, bias=False, device="meta")
     m.load_dense(w, device=device, imatrix=imatrix)
     if bias is not None:

@@ -14,10 +14,10 @@ import torch.nn.functional as F
 from . import reference as R
 
 __all__ = [
-    "quantize", "dequantize", "repack_to_device", "repack_from_device", "lowbit_matmul",
+    "quantize", "dequantize", "kq_quantize", "kq_dequantize", "kq_linear", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
-    "moe_align", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
+    "moe_align", "moe_gemm", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
     "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope", "attn_decode_rope_split", "attn_prefill", "moe_group_topk",
 ]
 
@@ -67,6 +67,25 @@ def repack_from_device(dev: torch.Tensor, fmt: int, n: int, k: int) -> torch.Ten
 
 def to_fp8_bytes(x: torch.Tensor, e5m2: bool) -> torch.Tensor:
     return _ops().to_fp8_bytes(x.cpu(), e5m2)
+
+
+# ------------------------------------------------------------ k-quants
+def kq_quantize(w: torch.Tensor, fmt: int, imatrix: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dense [n, k] -> GGUF k-quant super-blocks (C++ host quantizer)"""
+    return _ops().kq_quantize(w.float().cpu().contiguous(), fmt, imatrix)
+
+
+def kq_dequantize(blob: torch.Tensor, fmt: int, n: int, k: int, dtype=torch.float32) -> torch.Tensor:
+    if blob.is_cuda and not _native(blob):
+        return _ops().kq_dequantize(blob.cpu(), fmt, n, k, torch.float32).to(blob.device, dtype)
+    return _ops().kq_dequantize(blob, fmt, n, k, dtype)
+
+
+def kq_linear(x: torch.Tensor, blob: torch.Tensor, fmt: int, n: int, k: int) -> torch.Tensor:
+    """x @ W^T for a k-quant W (HIP GEMV / dequant + BLAS on the GPU, C++ on the host)"""
+    if x.is_cuda and not _native(x):
+        return F.linear(x, kq_dequantize(blob, fmt, n, k, torch.float32).to(x.dtype))
+    return _ops().kq_linear(x, blob, fmt, n, k)
 
 
 # ------------------------------------------------------------ low-bit GEMM

@@ -68,6 +68,10 @@ gguf_mixed_qtype: Dict[str, int] = {"gguf_q4k_s": GGUF_Q4K_S, "gguf_q4k_m": GGUF
 # representable in e4m3), 3-bit nf3 in the 4-bit LUT container.
 FMT_SYM_INT4, FMT_ASYM_INT4, FMT_NF4, FMT_FP4, FMT_SYM_INT8, FMT_FP8E4, FMT_FP8E5, \
     FMT_SYM_INT5, FMT_ASYM_INT5, FMT_NF3, FMT_FP6 = range(11)
+# GGUF k-quant super-block formats (csrc/common/kquant.h): the block bytes
+# are the storage on host and device (GGUF tensors load as-is)
+FMT_Q4K, FMT_Q5K, FMT_Q6K, FMT_Q2K = 11, 12, 13, 14
+KQ_BLOCK_BYTES = {FMT_Q4K: 144, FMT_Q5K: 176, FMT_Q6K: 210, FMT_Q2K: 84}
 
 NF4_TABLE = [
     -1.0, -0.6961928009986877, -0.5250730514526367, -0.39491748809814453,
@@ -95,6 +99,13 @@ class QFormat:
     has_min: bool = False    # second per-block fp16 plane (asym formats)
     gpu: bool = True         # has a tiled MI355X layout + HIP decoder
     k_align: int = 64        # K must be a multiple of this
+    kquant: bool = False     # GGUF k-quant super-blocks (KQuantLinear, not the tiled layout)
+
+    @property
+    def bits_per_weight(self) -> float:
+        if self.kquant:
+            return KQ_BLOCK_BYTES[self.fmt] * 8 / 256
+        return self.bits + 16 / self.block * (2 if self.has_min else 1)
 
 
 
@@ -111,16 +122,51 @@ _FORMATS: Dict[int, QFormat] = {
     SYM_INT5: QFormat("sym_int5", SYM_INT5, FMT_SYM_INT5, 8, 64),
     ASYM_INT5: QFormat("asym_int5", ASYM_INT5, FMT_ASYM_INT5, 8, 64, has_min=True),
     FP6: QFormat("fp6", FP6, FMT_FP6, 8, 64),
+    Q4_K: QFormat("q4_k", Q4_K, FMT_Q4K, 4, 256, has_min=True, k_align=256, kquant=True),
+    Q5_K: QFormat("q5_k", Q5_K, FMT_Q5K, 5, 256, has_min=True, k_align=256, kquant=True),
+    Q6_K: QFormat("q6_k", Q6_K, FMT_Q6K, 6, 256, k_align=256, kquant=True),
+    Q2_K: QFormat("q2_k", Q2_K, FMT_Q2K, 2, 256, has_min=True, k_align=256, kquant=True),
 }
 # qtypes stored in a format of equal or higher precision.  k-quants and IQ
 # grids (GGUF) are re-quantized on load exactly as the reference's GGUF path
 # does (`transformers/gguf/api.py`), into the nearest device container.
 _ALIAS = {
-    FP6_K: FP6, Q4_K: ASYM_INT4, Q5_K: ASYM_INT5, Q6_K: SYM_INT8, Q2_K: ASYM_INT4,
+    FP6_K: FP6,
     IQ2_XXS: ASYM_INT4, IQ2_XS: ASYM_INT4, IQ1_S: ASYM_INT4, IQ1_M: ASYM_INT4,
     SYM_INT4_RTN: SYM_INT4, ASYM_INT4_RTN: ASYM_INT4, SYM_INT8_RTN: SYM_INT8,
-    GGUF_Q4K_S: ASYM_INT4, GGUF_Q4K_M: ASYM_INT4,
+    # gguf mixed policies resolve per module (mixed_kquant_qtype); q4_k otherwise
+    GGUF_Q4K_S: Q4_K, GGUF_Q4K_M: Q4_K,
 }
+# in_features % 256 != 0: the reference's fallback formats
+# (SRC/transformers/utils.py:380-401, check_hidden_size)
+KQ_FALLBACK = {Q4_K: ASYM_INT4, Q5_K: ASYM_INT5, Q6_K: SYM_INT8, Q2_K: ASYM_INT4}
+
+
+def is_kquant(qtype) -> bool:
+    f = get_format(qtype)
+    return f is not None and f.kquant
+
+
+def mixed_kquant_qtype(qtype, module_name: str, num_layers: Optional[int]) -> int:
+    """Per-module qtype of the gguf_q4k_s / gguf_q4k_m policies (reference
+    SRC/transformers/utils.py:337-352): lm_head q6_k; v / down of the first
+    half (q4k_m: q6_k) or first eighth (q4k_s: q5_k) of the layers.  q/k/v
+    are one merged qkv_proj here, so the v rule applies to qkv_proj."""
+    qtype = resolve_qtype(qtype)
+    if qtype not in (GGUF_Q4K_S, GGUF_Q4K_M):
+        return qtype
+    if module_name.endswith("lm_head"):
+        return Q6_K
+    import re
+    m = re.search(r"layers\.(\d+)\.", module_name)
+    leaf = module_name.rsplit(".", 1)[-1]
+    hot = leaf in ("v_proj", "qkv_proj", "down_proj", "w2")
+    if m is None or not hot or not num_layers:
+        return Q4_K
+    layer = int(m.group(1))
+    if qtype == GGUF_Q4K_M:
+        return Q6_K if layer < num_layers // 2 else Q4_K
+    return Q5_K if layer < num_layers // 8 else Q4_K
 
 
 def resolve_qtype(q) -> int:
@@ -177,6 +223,8 @@ def get_block_size(qtype) -> int:
 def storage_bytes(qtype, n: int, k: int) -> int:
     """Bytes of the canonical planar blob for an [n, k] weight."""
     f = get_format(qtype)
+    if f.kquant:
+        return n * (k // 256) * KQ_BLOCK_BYTES[f.fmt]
     codes = n * k * f.bits // 8
     scales = n * (k // f.block) * 2
     mins = scales if f.has_min else 0

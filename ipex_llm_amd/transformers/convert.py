@@ -173,14 +173,36 @@ def _convert_one(module: nn.Linear, qtype: int, device, imatrix=None, mp_group=N
         dt = torch.bfloat16 if qtype == Q.BF16 else torch.float16
         return DenseLinear.from_linear(module, dt, device, mp_group)
     fmt = Q.get_format(qtype)
+    if fmt.kquant and module.in_features % fmt.k_align:
+        # reference check_hidden_size: the nearest 64-block format instead
+        qtype = Q.KQ_FALLBACK[fmt.qtype]
+        fmt = Q.get_format(qtype)
     if module.in_features % fmt.k_align:
         return None
+    if fmt.kquant:
+        from .low_bit_linear import KQuantLinear
+        if convert_shape_only or module.weight.device.type == "meta":
+            return KQuantLinear(module.in_features, module.out_features, fmt.qtype, module.bias is not None,
+                                device="meta", mp_group=mp_group, optimize_lm_head=lm_head)
+        return KQuantLinear.from_linear(module, fmt.qtype, device=device, imatrix=imatrix, mp_group=mp_group,
+                                        optimize_lm_head=lm_head)
     if convert_shape_only or module.weight.device.type == "meta":
         m = LowBitLinear(module.in_features, module.out_features, qtype, module.bias is not None,
                          device="meta", mp_group=mp_group, optimize_lm_head=lm_head)
         return m
     return LowBitLinear.from_linear(module, qtype, device=device, imatrix=imatrix, mp_group=mp_group,
                                     optimize_lm_head=lm_head, enable_scale_search=enable_scale_search)
+
+
+_ROOT_CFG = [None]
+
+
+def model_root_cfg():
+    return _ROOT_CFG[0]
+
+
+def _num_layers(cfg):
+    return getattr(cfg, "num_hidden_layers", None) if cfg is not None else None
 
 
 def _replace_with_low_bit_linear(model: nn.Module, qtype: int, modules_to_not_convert=None, prefix="",
@@ -203,7 +225,7 @@ def _replace_with_low_bit_linear(model: nn.Module, qtype: int, modules_to_not_co
                 not (name == "lm_head" or full.endswith("lm_head")):
             continue                                  # tiny gates stay dense
         if _is_linear(child):
-            q = qtype
+            q = Q.mixed_kquant_qtype(qtype, full, _num_layers(model_root_cfg()))
             is_head = name == "lm_head" or full.endswith("lm_head")
             if is_head and mixed_precision and qtype in (Q.SYM_INT4, Q.ASYM_INT4, Q.WOQ_INT4, Q.NF4, Q.FP4):
                 q = Q.SYM_INT8
@@ -297,8 +319,12 @@ def ggml_convert_low_bit(model: nn.Module, qtype="sym_int4", optimize_model: boo
         qtype = Q.FP8E4 if qtype == Q.TORCH_FP8E4 else Q.FP8E5
     if qtype in (Q.MOFQ4, Q.MOFQ8):
         qtype = _pick_mixed_format(model, qtype)
-    n = _replace_with_low_bit_linear(model, qtype, modules_to_not_convert, "", device, imatrix_data,
-                                     mixed_precision, convert_shape_only, enable_scale_search)
+    _ROOT_CFG[0] = getattr(model, "config", None)     # layer count for the gguf_q4k_s/m policies
+    try:
+        n = _replace_with_low_bit_linear(model, qtype, modules_to_not_convert, "", device, imatrix_data,
+                                         mixed_precision, convert_shape_only, enable_scale_search)
+    finally:
+        _ROOT_CFG[0] = None
     if n == 0:
         logger.warning("ggml_convert_low_bit: no linear layer converted")
     if embedding_qtype is not None or cpu_embedding or disk_embedding:

@@ -308,3 +308,164 @@ def lowbit_row_concat(mods, interleave_glu: bool = False) -> "LowBitLinear":
     if m0.g_idx_map is not None:
         new.g_idx_map = m0.g_idx_map
     return new
+
+
+# ---------------------------------------------------------------- k-quants
+class _KQMatMul(torch.autograd.Function):
+    """y = x W^T with a frozen k-quant W (QLoRA-style base weight): grad_x only"""
+
+    @staticmethod
+    def forward(ctx, x, blob, fmt, n, k):
+        ctx.fmt, ctx.n, ctx.k = fmt, n, k
+        ctx.save_for_backward(blob)
+        ctx.xdtype = x.dtype
+        return ops.kq_linear(x, blob, fmt, n, k)
+
+    @staticmethod
+    def backward(ctx, grad_y):
+        (blob,) = ctx.saved_tensors
+        gx = None
+        if ctx.needs_input_grad[0]:
+            dt = grad_y.dtype if grad_y.dtype in (torch.bfloat16, torch.float16) else torch.float32
+            w = ops.kq_dequantize(blob, ctx.fmt, ctx.n, ctx.k, dt)
+            gx = torch.matmul(grad_y.to(w.dtype), w).to(ctx.xdtype)
+        return gx, None, None, None, None
+
+
+class KQuantLinear(nn.Module):
+    """Linear over a GGUF k-quant weight (q4_k / q5_k / q6_k / q2_k).
+
+    Reference: the k-quant qtypes of ``SRC/ggml/quantize.py:28-60`` held by
+    ``FP4Params`` / ``LowBitLinear`` (``low_bit_linear.py:106-190``) and the
+    gguf_q4k_s/m mixed policies (``transformers/utils.py:286-401``).  The
+    GGUF super-block bytes are the storage on the host, on the device and in
+    checkpoints (``csrc/common/kquant.h``), so GGUF k-quant tensors are used
+    without re-quantization and the bits per weight are the reference's
+    (4.5 / 5.5 / 6.5625 / 2.625).  Decode GEMV and dequantize are HIP kernels
+    (``csrc/hip/kquant.hip``); the CPU path is the C++ kernel library."""
+
+    def __init__(self, in_features: int, out_features: int, qtype="q4_k", bias: bool = True, device=None,
+                 dtype=None, mp_group=None, optimize_lm_head=False):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.qtype = Q.resolve_qtype(qtype)
+        f = Q.get_format(self.qtype)
+        if f is None or not f.kquant:
+            raise ValueError(f"{Q.qtype_name(self.qtype)} is not a k-quant format")
+        if in_features % 256:
+            raise ValueError(f"k-quant formats need in_features % 256 == 0, got {in_features}")
+        self.kq_fmt = f.fmt
+        device = torch.device(device) if device is not None else torch.device("cpu")
+        self.weight = nn.Parameter(torch.zeros(Q.storage_bytes(self.qtype, out_features, in_features),
+                                               dtype=torch.uint8, device=device), requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(out_features, dtype=dtype or torch.float32, device=device)) \
+            if bias else None
+        self.mp_group = mp_group
+        self.optimize_lm_head = optimize_lm_head
+
+    @classmethod
+    @torch.no_grad()
+    def from_linear(cls, linear: nn.Module, qtype="q4_k", device=None, imatrix=None, mp_group=None,
+                    optimize_lm_head=False):
+        w = linear.weight.data
+        dev = torch.device(device) if device is not None else w.device
+        m = cls(w.shape[1], w.shape[0], qtype, bias=getattr(linear, "bias", None) is not None, device="meta",
+                mp_group=mp_group, optimize_lm_head=optimize_lm_head)
+        m.load_dense(w, dev, imatrix)
+        if linear.bias is not None:
+            m.bias = nn.Parameter(linear.bias.data.detach().to(dev).clone(), requires_grad=False)
+        return m
+
+    @torch.no_grad()
+    def load_dense(self, w: torch.Tensor, device=None, imatrix=None):
+        """quantize a dense [out, in] weight (C++ host quantizer, imatrix-aware)"""
+        dev = torch.device(device) if device is not None else w.device
+        blob = ops.kq_quantize(w.float().cpu(), self.kq_fmt, imatrix)
+        self.weight = nn.Parameter(blob.to(dev), requires_grad=False)
+
+    @classmethod
+    def from_blocks(cls, blob: torch.Tensor, qtype, n: int, k: int, device=None, bias=None):
+        """wrap GGUF super-block bytes of an [n, k] weight as they are"""
+        m = cls(k, n, qtype, bias=bias is not None, device="meta")
+        if blob.numel() != Q.storage_bytes(m.qtype, n, k):
+            raise ValueError(f"k-quant blob has {blob.numel()} bytes, expected {Q.storage_bytes(m.qtype, n, k)}")
+        m.weight = nn.Parameter(blob.reshape(-1).to(torch.uint8).to(device or blob.device), requires_grad=False)
+        if bias is not None:
+            m.bias = nn.Parameter(bias.detach().to(m.weight.device), requires_grad=False)
+        return m
+
+    def dequantize(self, dtype=torch.float32) -> torch.Tensor:
+        return ops.kq_dequantize(self.weight, self.kq_fmt, self.out_features, self.in_features, dtype)
+
+    def canonical_blob(self) -> torch.Tensor:
+        return self.weight.data
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        key = prefix + "weight"
+        if key in state_dict:
+            blob = state_dict[key]
+            n, k = self.out_features, self.in_features
+            dev = self.weight.device if self.weight.device.type != "meta" else torch.device("cpu")
+            if blob.dtype != torch.uint8:
+                self.load_dense(blob.view(n, k), dev)
+            elif blob.numel() != Q.storage_bytes(self.qtype, n, k):
+                error_msgs.append(f"{key}: k-quant blob has {blob.numel()} bytes, expected "
+                                  f"{Q.storage_bytes(self.qtype, n, k)}")
+                return
+            else:
+                self.weight = nn.Parameter(blob.reshape(-1).to(dev).clone(), requires_grad=False)
+        elif strict:
+            missing_keys.append(key)
+        bkey = prefix + "bias"
+        if self.bias is not None:
+            if bkey in state_dict:
+                dev = self.bias.device if self.bias.device.type != "meta" else self.weight.device
+                self.bias = nn.Parameter(state_dict[bkey].detach().to(dev).clone(), requires_grad=False)
+            elif strict:
+                missing_keys.append(bkey)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.optimize_lm_head and x.dim() == 3 and x.shape[1] > 10 and not self.training:
+            x = x[:, -1:, :]
+        in_dtype = x.dtype
+        if x.is_cuda and x.dtype not in (torch.bfloat16, torch.float16):
+            x = x.to(torch.float16)
+        if self.training and torch.is_grad_enabled() and x.requires_grad:
+            y = _KQMatMul.apply(x, self.weight, self.kq_fmt, self.out_features, self.in_features)
+        else:
+            y = ops.kq_linear(x, self.weight, self.kq_fmt, self.out_features, self.in_features)
+        if self.mp_group is not None:
+            from ..parallel.comm import all_reduce_inplace
+            y = all_reduce_inplace(y, self.mp_group)
+        if self.bias is not None:
+            y = y + self.bias.to(y.dtype)
+        return y.to(in_dtype) if y.dtype != in_dtype else y
+
+    def extra_repr(self):
+        return (f"in_features={self.in_features}, out_features={self.out_features}, "
+                f"qtype={Q.qtype_name(self.qtype)}, bias={self.bias is not None}")
+
+
+class RowConcatLinear(nn.Module):
+    """Output rows of several linears (e.g. a merged qkv / gate_up whose
+    parts keep different GGUF k-quant types); ``interleave_glu``: 16-row
+    tile interleave of (gate, up) -- the layout of a merged gate_up_proj."""
+
+    def __init__(self, parts, interleave_glu: bool = False):
+        super().__init__()
+        self.parts = nn.ModuleList(parts)
+        self.interleave_glu = interleave_glu
+        self.in_features = parts[0].in_features
+        self.out_features = sum(p.out_features for p in parts)
+        self.bias = None
+        self.mp_group = None
+
+    def forward(self, x):
+        ys = [p(x) for p in self.parts]
+        if self.interleave_glu:
+            g, u = ys
+            I = g.shape[-1]
+            return torch.stack([g.reshape(*g.shape[:-1], I // 16, 16), u.reshape(*u.shape[:-1], I // 16, 16)],
+                               -2).reshape(*g.shape[:-1], 2 * I)
+        return torch.cat(ys, -1)

@@ -33,7 +33,9 @@ def test_qtype_registry_matches_reference_ids():
     assert resolve_qtype("sym_int4") == 2 and resolve_qtype("asym_int4") == 3
     assert resolve_qtype("nf4") == 10 and resolve_qtype("fp8") == 19 and resolve_qtype("woq_int4") == 34
     assert resolve_qtype("gguf_q4k_m") == 102
-    assert get_format("q4_k").name == "asym_int4"
+    # k-quants are native GGUF super-block formats now (test_kquant.py)
+    assert get_format("q4_k").name == "q4_k" and get_format("q4_k").kquant
+    assert get_format("gguf_q4k_m").name == "q4_k"
 
 
 def test_sym_int4_q4_0_convention():
