@@ -14,6 +14,10 @@ using at::Tensor;
 
 namespace {
 
+// decode combine scratch: the wide combine holds up to 4096 split weights in
+// LDS (attention.cuh CW_MAXS), the one-wave combine 1024 (used for D % 4 != 0)
+constexpr int64_t kMaxDecodeSplits = 4096;
+
 inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
 inline bool is_bf16(const Tensor& t) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf,
@@ -759,6 +763,8 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, cons
   a.Hkv = (int)Hkv;
   a.D = (int)D;
   a.bs = (int)bs;
+  TORCH_CHECK(nsplit >= 1 && nsplit <= kMaxDecodeSplits && (nsplit <= 1024 || D % 4 == 0),
+              "attn_decode: nsplit must be 1..", kMaxDecodeSplits, " (1..1024 when D % 4 != 0; combine LDS), got ", nsplit);
   a.nsplit = (int)nsplit;
   a.scale = (float)scale;
   a.softcap = (float)softcap;
@@ -814,6 +820,8 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
   a.Hkv = (int)Hkv;
   a.D = (int)D;
   a.bs = (int)bs;
+  TORCH_CHECK(nsplit >= 1 && nsplit <= kMaxDecodeSplits && (nsplit <= 1024 || D % 4 == 0),
+              "attn_decode: nsplit must be 1..", kMaxDecodeSplits, " (1..1024 when D % 4 != 0; combine LDS), got ", nsplit);
   a.nsplit = (int)nsplit;
   a.scale = (float)scale;
   a.softcap = (float)softcap;

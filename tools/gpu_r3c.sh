@@ -1,7 +1,7 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_tp.py tests/test_gpu_moe_gemm.py tests/test_gpu_moe.py -x -v --timeout 200 --timeout-method thread > gpurun_out/pt_r3c.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kquant.py tests/test_gpu_allreduce.py tests/test_gpu_tp.py tests/test_gpu_moe_gemm.py tests/test_gpu_moe.py -x -v --timeout 200 --timeout-method thread > gpurun_out/pt_r3c.log 2>&1
 rc=$?
 tail -4 gpurun_out/pt_r3c.log
 [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ] && exit $rc
