@@ -772,6 +772,9 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, cons
   a.kv_fp8 = (int)kv_fp8;
   a.k_scale = (float)k_scale;
   a.v_scale = (float)v_scale;
+  if (alibi.has_value() && alibi->defined())
+    TORCH_CHECK(alibi->is_cuda() && alibi->is_contiguous() && alibi->numel() == Hq,
+                "attn_decode: alibi must be a contiguous f32 [Hq] device tensor");
   a.alibi = (alibi.has_value() && alibi->defined()) ? alibi->data_ptr<float>() : nullptr;
   a.counters = fused_combine_on() ? attn_counters(q.device(), B * Hkv) : nullptr;
   a.no_combine = no_combine ? 1 : 0;

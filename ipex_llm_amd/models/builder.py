@@ -25,7 +25,7 @@ from .decoder import (DecoderSpec, NativeAttention, NativeCausalLM, NativeLayer,
 # model types executed by the native decoder (others fall back to the HF
 # forward with low-bit linears, like the reference does for e.g. mixtral)
 NATIVE_DENSE = {"llama", "mistral", "qwen2", "qwen3", "gemma", "gemma2", "phi3", "internlm2", "yi",
-                "aquila", "olmo2", "deepseek", "minicpm", "baichuan", "yuan"}
+                "aquila", "olmo2", "deepseek", "minicpm", "baichuan", "yuan", "glm", "glm4"}
 NATIVE_MOE = {"mixtral", "qwen2_moe", "qwen3_moe"}
 
 
@@ -43,7 +43,9 @@ def spec_from_config(cfg) -> DecoderSpec:
     nh = cfg.num_attention_heads
     nkv = _get(cfg, "num_key_value_heads", default=nh)
     hd = _get(cfg, "head_dim", default=H // nh) or H // nh
-    prf = _get(cfg, "partial_rotary_factor", default=1.0)
+    rp = _get(cfg, "rope_parameters", default=None)
+    prf = _get(cfg, "partial_rotary_factor", default=None) or \
+        (rp.get("partial_rotary_factor") if isinstance(rp, dict) else None) or 1.0
     act_name = _get(cfg, "hidden_act", "hidden_activation", default="silu")
     spec = DecoderSpec(
         model_type=mt, hidden_size=H, num_layers=cfg.num_hidden_layers, num_heads=nh, num_kv_heads=nkv,
@@ -58,6 +60,12 @@ def spec_from_config(cfg) -> DecoderSpec:
     )
     if mt in ("qwen2", "qwen2_moe"):
         spec.qkv_bias = True
+    if mt in ("glm", "glm4"):
+        # GLM / ChatGLM-4: RoPE on the first half of each head, rotating
+        # interleaved pairs (SRC/transformers/models/chatglm4.py:163-205)
+        spec.rope_interleaved = True
+    if mt == "glm4":
+        spec.sandwich_norm = True         # post_self_attn / post_mlp norms
     if mt in ("gemma", "gemma2", "gemma3_text"):
         spec.embed_scale = math.sqrt(H)
         spec.norm_unit_offset = True
@@ -282,6 +290,9 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
     ``_optimize_pre``, linears already low-bit) into a NativeCausalLM that
     shares its parameters.  Returns None for unsupported layouts."""
     cfg = hf_model.config
+    from .generic import GENERIC_ARCHS, generic_from_hf
+    if getattr(cfg, "model_type", None) in GENERIC_ARCHS:
+        return generic_from_hf(hf_model, dtype)
     spec = spec_from_config(cfg)
     tp = getattr(hf_model, "_tp", None)
     if tp is not None:                      # tensor-parallel shard: local heads
@@ -314,8 +325,11 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
             return None
         pre_ff = getattr(L, "pre_feedforward_layernorm", None)
         post_ff = getattr(L, "post_feedforward_layernorm", None)
+        ln2 = L.post_attention_layernorm
+        if spec.model_type == "glm4":     # same sandwich as gemma2 under other names
+            ln2, pre_ff, post_ff = L.post_self_attn_layernorm, L.post_attention_layernorm, L.post_mlp_layernorm
         layers.append(NativeLayer(spec, attn, mlp, L.input_layernorm.weight.data,
-                                  L.post_attention_layernorm.weight.data,
+                                  ln2.weight.data,
                                   pre_ff.weight.data if pre_ff is not None else None,
                                   post_ff.weight.data if post_ff is not None else None))
     first = pp is None or pp["rank"] == 0

@@ -63,6 +63,12 @@ class DecoderSpec:
     sandwich_norm: bool = False
     query_scale: Optional[float] = None
     rope_attention_scaling: float = 1.0
+    # block layout knobs of the non-llama families (models/generic.py)
+    norm_type: str = "rms"            # "rms" | "layer"
+    pos_type: str = "rope"            # "rope" | "alibi" | "learned"
+    parallel_residual: str = "none"   # "none" | "shared" (one norm) | "two" (two norms)
+    glu: bool = True
+    act_fn: str = "silu"
     # MoE
     num_experts: int = 0
     top_k: int = 0
@@ -204,6 +210,7 @@ class NativeCausalLM(nn.Module):
         self.register_buffer("inv_freq", inv_freq.float(), persistent=False)
         self.rope_cache: Optional[torch.Tensor] = None
         self.tp_group = None
+        self.alibi = None                   # [Hq] f32 ALiBi slopes (generic families)
         # pipeline-parallel stage flags (parallel/pipeline.py): a stage owns a
         # contiguous layer range; only the first embeds, only the last has
         # the final norm + lm_head
@@ -267,9 +274,9 @@ class NativeCausalLM(nn.Module):
         if meta.Tq * group <= 16 and (s.head_dim in (64, 80, 96, 128, 256) or not q.is_cuda):
             o = ops.attn_decode(q.view(meta.B, meta.Tq, s.num_heads, s.head_dim), kc, vc, meta.block_tables,
                                 meta.seq_lens, meta.nsplit, s.scale, softcap, window, cache.kv_fp8,
-                                cache.k_scale, cache.v_scale, None, meta.seq_lens_host)
+                                cache.k_scale, cache.v_scale, self.alibi, meta.seq_lens_host)
             return o.view(T, s.num_heads * s.head_dim)
-        if q.is_cuda and s.head_dim in (64, 128) and cache.bs % 64 == 0 and self._prefill_attn_native \
+        if q.is_cuda and self.alibi is None and s.head_dim in (64, 128) and cache.bs % 64 == 0 and self._prefill_attn_native \
                 and ops.native_gpu(q):
             # prefill / long query chunk: flash-attention HIP kernel over the paged cache
             o = ops.attn_prefill(q.view(T, s.num_heads, s.head_dim), kc, vc, meta.block_tables, meta.seq_lens,
@@ -283,8 +290,9 @@ class NativeCausalLM(nn.Module):
             L = int(lens[b])
             kk = ops.api.gather_kv(kc, meta.block_tables, b, L, cache.kv_fp8, cache.k_scale, q.dtype)
             vv = ops.api.gather_kv(vc, meta.block_tables, b, L, cache.kv_fp8, cache.v_scale, q.dtype)
-            if softcap or not q.is_cuda:
-                outs.append(R.attention(qv[b:b + 1], kk[None], vv[None], True, s.scale, softcap, window))
+            if softcap or not q.is_cuda or self.alibi is not None:
+                outs.append(R.attention(qv[b:b + 1], kk[None], vv[None], True, s.scale, softcap, window, None,
+                                        self.alibi))
                 continue
             qq = qv[b].transpose(0, 1)[None]                 # [1, Hq, Tq, D]
             k4 = kk.transpose(0, 1)[None]

@@ -34,7 +34,7 @@ logger = logging.getLogger("ipex_llm_amd")
 
 # architectures whose decoder runs on the native engine
 NATIVE_ARCHS = {"llama", "mistral", "qwen2", "qwen3", "gemma", "gemma2", "phi3", "internlm2", "yi",
-                "aquila", "olmo2", "minicpm"}
+                "aquila", "olmo2", "minicpm", "glm", "glm4"}
 # granite (embedding/residual/logit multipliers), stablelm (partial rotary + LayerNorm) and
 # starcoder2 (biased LayerNorm MLP, no q_proj split) take the HF forward over low-bit linears.
 MOE_ARCHS = {"mixtral", "qwen2_moe", "qwen3_moe"}
@@ -120,6 +120,11 @@ def _optimize_pre(model: nn.Module, qtype: int):
     if mt == "rwkv":
         from ..models.rwkv import prescale_rwkv
         prescale_rwkv(model)
+        return model
+    from ..models.generic import GENERIC_ARCHS, generic_pre
+    if mt in GENERIC_ARCHS:
+        if generic_pre(model):
+            model._illm_pre = True
         return model
     if mt not in NATIVE_ARCHS and mt not in MOE_ARCHS:
         return model
@@ -292,13 +297,18 @@ def _optimize_post(model: nn.Module):
     if mt == "rwkv5":
         from ..models.rwkv import patch_rwkv5
         patch_rwkv5(model)
-    if (mt in NATIVE_ARCHS or mt in MOE_ARCHS) and getattr(model, "_illm_pre", False):
+    from ..models.generic import GENERIC_ARCHS
+    if (mt in NATIVE_ARCHS or mt in MOE_ARCHS or mt in GENERIC_ARCHS) and getattr(model, "_illm_pre", False):
         from .hf_native import attach_native
         attach_native(model)
         if not getattr(model, "_illm_native_attached", False):
             # variant the native decoder cannot run: HF forward over the merged weights
-            from .hf_views import restore_hf_views
-            restore_hf_views(model)
+            if mt in GENERIC_ARCHS:
+                from ..models.generic import restore_generic_views
+                restore_generic_views(model)
+            else:
+                from .hf_views import restore_hf_views
+                restore_hf_views(model)
     return model
 
 

@@ -75,7 +75,7 @@ def restore_hf_views(model: nn.Module) -> nn.Module:
                 or isinstance(mlp.gate_up_proj, FusedGLUView) or hasattr(mlp, "gate_proj"):
             continue
         g, u = glu_rows(mlp.gate_up_proj.out_features // 2)
-        if type(mlp).__name__.startswith("Phi3"):           # its forward calls the fused projection
+        if type(mlp).__name__.startswith(("Phi3", "Glm")):           # its forward calls the fused projection
             mlp.gate_up_proj = FusedGLUView(mlp.gate_up_proj, g + u)
         else:
             mlp.gate_proj = ProjView(mlp, "gate_up_proj", g, False)

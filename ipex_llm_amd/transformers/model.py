@@ -272,7 +272,11 @@ class _BaseAutoModelClass:
         else:
             sd = torch.load(os.path.join(path, "pytorch_model.bin"), map_location="cpu", weights_only=True)
         missing, unexpected = model.load_state_dict(sd, strict=False, assign=True)
-        if getattr(config, "tie_word_embeddings", False) and hasattr(model, "tie_weights"):
+        out_emb = model.get_output_embeddings() if hasattr(model, "get_output_embeddings") else None
+        head_saved = out_emb is not None and getattr(out_emb, "weight", None) is not None and \
+            out_emb.weight.device.type != "meta" and not out_emb.weight.is_floating_point()
+        # (a tied head quantized on its own -- low-bit blob in the checkpoint -- stays untied)
+        if getattr(config, "tie_word_embeddings", False) and hasattr(model, "tie_weights") and not head_saved:
             try:
                 model.tie_weights()
             except Exception:  # pragma: no cover

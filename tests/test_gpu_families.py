@@ -1,0 +1,64 @@
+"""Non-llama families on the GPU (models/generic.py): LayerNorm kernel,
+ALiBi slopes inside the flash-decoding kernel, identity-table rope_kv for
+learned positions, partial / interleaved RoPE -- native logits vs the HF
+forward (fp32, CPU) of the same weights, and hipGraph decode == eager."""
+import pytest
+import torch
+import transformers as T
+
+pytestmark = pytest.mark.gpu
+
+H, NH, L, V = 256, 4, 2, 512        # head_dim 64: the native decode / prefill kernels
+
+
+def _cfg(kind):
+    if kind == "bloom":
+        return T.BloomConfig(hidden_size=H, n_layer=L, n_head=NH, vocab_size=V)
+    if kind == "mpt":
+        return T.MptConfig(d_model=H, n_layers=L, n_heads=NH, max_seq_len=512, vocab_size=V)
+    if kind == "starcoder2":
+        return T.Starcoder2Config(hidden_size=H, num_hidden_layers=L, num_attention_heads=NH, num_key_value_heads=2,
+                                  intermediate_size=512, max_position_embeddings=512, vocab_size=V)
+    if kind == "gpt_neox":
+        return T.GPTNeoXConfig(hidden_size=H, num_hidden_layers=L, num_attention_heads=NH, intermediate_size=512,
+                               max_position_embeddings=512, vocab_size=V)
+    if kind == "gptj":
+        return T.GPTJConfig(n_embd=H, n_layer=L, n_head=NH, rotary_dim=32, n_positions=512, vocab_size=V)
+    if kind == "gpt_bigcode":
+        return T.GPTBigCodeConfig(n_embd=H, n_layer=L, n_head=NH, n_positions=512, vocab_size=V)
+    if kind == "falcon_new":
+        return T.FalconConfig(hidden_size=H, num_hidden_layers=L, num_attention_heads=NH, num_kv_heads=2,
+                              new_decoder_architecture=True, vocab_size=V)
+    raise KeyError(kind)
+
+
+@pytest.mark.parametrize("kind", ["bloom", "mpt", "starcoder2", "gpt_neox", "gptj", "gpt_bigcode", "falcon_new"])
+def test_family_gpu_matches_hf(kind, tmp_path):
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    torch.manual_seed(0)
+    ref = T.AutoModelForCausalLM.from_config(_cfg(kind)).eval()
+    with torch.no_grad():
+        for n, p in ref.named_parameters():
+            if p.dim() == 1:
+                p.add_(torch.randn_like(p) * 0.1)
+    path = str(tmp_path / kind)
+    ref.save_pretrained(path)
+    ids = torch.randint(0, V, (1, 40))
+    with torch.no_grad():
+        want = ref(ids).logits.float()
+    m = AutoModelForCausalLM.from_pretrained(path, load_in_low_bit="sym_int8", torch_dtype=torch.bfloat16)
+    m = m.to("cuda").eval()
+    assert getattr(m, "_illm_native_attached", False)
+    with torch.no_grad():
+        out = m(ids[:, :32].cuda(), use_cache=True)
+        got = out.logits.float().cpu()
+        rel = ((got - want[:, :32]).norm() / want[:, :32].norm()).item()
+        assert rel < 5e-2, (kind, rel)
+        cache = out.past_key_values
+        for t in range(32, 40):                 # single-token decode steps (flash-decoding kernel)
+            step = m(ids[:, t:t + 1].cuda(), past_key_values=cache).logits.float().cpu()
+            r = ((step[:, -1] - want[:, t]).norm() / want[:, t].norm()).item()
+            assert r < 5e-2, (kind, t, r)
+        g = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=True)
+        e = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=False)
+    assert torch.equal(g.cpu(), e.cpu()), kind
