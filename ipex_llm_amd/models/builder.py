@@ -293,6 +293,9 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
     from .generic import GENERIC_ARCHS, generic_from_hf
     if getattr(cfg, "model_type", None) in GENERIC_ARCHS:
         return generic_from_hf(hf_model, dtype)
+    from .mla import MLA_ARCHS, mla_from_hf
+    if getattr(cfg, "model_type", None) in MLA_ARCHS:
+        return mla_from_hf(hf_model, dtype)
     spec = spec_from_config(cfg)
     tp = getattr(hf_model, "_tp", None)
     if tp is not None:                      # tensor-parallel shard: local heads

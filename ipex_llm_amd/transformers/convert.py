@@ -126,6 +126,10 @@ def _optimize_pre(model: nn.Module, qtype: int):
         if generic_pre(model):
             model._illm_pre = True
         return model
+    from ..models.mla import MLA_ARCHS
+    if mt in MLA_ARCHS:
+        model._illm_pre = True          # MLA: weights used as converted (kv_b absorbed at attach)
+        return model
     if mt not in NATIVE_ARCHS and mt not in MOE_ARCHS:
         return model
     base = getattr(model, "model", None)
@@ -298,7 +302,9 @@ def _optimize_post(model: nn.Module):
         from ..models.rwkv import patch_rwkv5
         patch_rwkv5(model)
     from ..models.generic import GENERIC_ARCHS
-    if (mt in NATIVE_ARCHS or mt in MOE_ARCHS or mt in GENERIC_ARCHS) and getattr(model, "_illm_pre", False):
+    from ..models.mla import MLA_ARCHS
+    if (mt in NATIVE_ARCHS or mt in MOE_ARCHS or mt in GENERIC_ARCHS or mt in MLA_ARCHS) and \
+            getattr(model, "_illm_pre", False):
         from .hf_native import attach_native
         attach_native(model)
         if not getattr(model, "_illm_native_attached", False):
@@ -306,7 +312,7 @@ def _optimize_post(model: nn.Module):
             if mt in GENERIC_ARCHS:
                 from ..models.generic import restore_generic_views
                 restore_generic_views(model)
-            else:
+            elif mt not in MLA_ARCHS:
                 from .hf_views import restore_hf_views
                 restore_hf_views(model)
     return model

@@ -193,3 +193,66 @@ def test_glm_native_matches_hf(kind, tmp_path):
             step = m(ids[:, t:t + 1], past_key_values=cache).logits.float()
             r = ((step[:, -1] - want[:, t]).norm() / want[:, t].norm()).item()
             assert r < 3e-2, (t, r)
+
+
+def _mla_cfg(kind):
+    if kind == "deepseek_v3":
+        return T.AutoConfig.for_model("deepseek_v3", hidden_size=128, intermediate_size=256, moe_intermediate_size=64,
+                                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=4,
+                                      vocab_size=V, max_position_embeddings=256, n_routed_experts=8,
+                                      num_experts_per_tok=2, n_group=2, topk_group=1, n_shared_experts=1,
+                                      first_k_dense_replace=1, q_lora_rank=64, kv_lora_rank=64, qk_rope_head_dim=16,
+                                      qk_nope_head_dim=32, v_head_dim=32)
+    if kind == "deepseek_v3_noq":            # q_lora_rank None (V2-Lite style q_proj)
+        return T.AutoConfig.for_model("deepseek_v3", hidden_size=128, intermediate_size=256, moe_intermediate_size=64,
+                                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=4,
+                                      vocab_size=V, max_position_embeddings=256, n_routed_experts=8,
+                                      num_experts_per_tok=2, n_group=2, topk_group=1, n_shared_experts=1,
+                                      first_k_dense_replace=1, q_lora_rank=None, kv_lora_rank=64,
+                                      qk_rope_head_dim=16, qk_nope_head_dim=32, v_head_dim=32, rope_interleave=False)
+    if kind == "minicpm3":
+        return T.AutoConfig.for_model("minicpm3", hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                                      num_attention_heads=4, num_key_value_heads=4, vocab_size=V,
+                                      max_position_embeddings=256, q_lora_rank=64, kv_lora_rank=64,
+                                      qk_rope_head_dim=16, qk_nope_head_dim=32, v_head_dim=32)
+    raise KeyError(kind)
+
+
+@pytest.mark.parametrize("kind", ["deepseek_v3", "deepseek_v3_noq", "minicpm3"])
+def test_mla_native_matches_hf(kind, tmp_path):
+    """absorbed-weight MLA over the paged latent cache vs the HF forward"""
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    from ipex_llm_amd.models.builder import native_from_hf
+    torch.manual_seed(0)
+    ref = T.AutoModelForCausalLM.from_config(_mla_cfg(kind)).eval()
+    with torch.no_grad():
+        for n, p_ in ref.named_parameters():
+            if p_.dim() == 1 and "norm" in n:
+                p_.add_(torch.randn_like(p_) * 0.1)
+            if n.endswith("mlp.gate.weight"):
+                p_.normal_(0, 1.0)
+    p = str(tmp_path / kind)
+    ref.save_pretrained(p)
+    ids = torch.randint(0, V, (1, 12))
+    with torch.no_grad():
+        want = ref(ids).logits.float()
+    m = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32).eval()
+    assert getattr(m, "_illm_native_attached", False)
+    nm = native_from_hf(m)
+    assert type(nm).__name__ == "MLACausalLM"
+    with torch.no_grad():
+        out = m(ids[:, :8], use_cache=True)
+        rel = ((out.logits.float() - want[:, :8]).norm() / want[:, :8].norm()).item()
+        assert rel < 3e-2, rel
+        cache = out.past_key_values
+        # the paged cache holds the latent rows only: [c_kv | k_pe]
+        assert cache.engine.cache.k[0].shape[-1] == 64 + 16 and cache.engine.cache.k[0].shape[1] == 1
+        for t in range(8, 12):
+            step = m(ids[:, t:t + 1], past_key_values=cache).logits.float()
+            r = ((step[:, -1] - want[:, t]).norm() / want[:, t].norm()).item()
+            assert r < 3e-2, (t, r)
+        g = m.generate(ids[:, :6], max_new_tokens=5, do_sample=False)
+    # greedy continuation agrees with the HF argmax of the same prefix
+    with torch.no_grad():
+        lg = ref(g[:, :-1]).logits
+    assert (lg[0, 5:].argmax(-1) == g[0, 6:]).float().mean() >= 0.8

@@ -62,3 +62,40 @@ def test_family_gpu_matches_hf(kind, tmp_path):
         g = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=True)
         e = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=False)
     assert torch.equal(g.cpu(), e.cpu()), kind
+
+
+def test_mla_deepseek_v3_gpu(tmp_path):
+    """absorbed MLA over the paged latent cache on the GPU (bf16): prompt
+    logits and decode steps vs the HF fp32 forward, hipGraph decode == eager"""
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    cfg = T.AutoConfig.for_model("deepseek_v3", hidden_size=256, intermediate_size=512, moe_intermediate_size=128,
+                                 num_hidden_layers=2, num_attention_heads=8, num_key_value_heads=8, vocab_size=V,
+                                 max_position_embeddings=512, n_routed_experts=8, num_experts_per_tok=2, n_group=2,
+                                 topk_group=1, n_shared_experts=1, first_k_dense_replace=1, q_lora_rank=128,
+                                 kv_lora_rank=128, qk_rope_head_dim=32, qk_nope_head_dim=64, v_head_dim=64)
+    torch.manual_seed(0)
+    ref = T.AutoModelForCausalLM.from_config(cfg).eval()
+    with torch.no_grad():
+        for n, p in ref.named_parameters():
+            if n.endswith("mlp.gate.weight"):
+                p.normal_(0, 1.0)
+    path = str(tmp_path / "ds3")
+    ref.save_pretrained(path)
+    ids = torch.randint(0, V, (1, 40))
+    with torch.no_grad():
+        want = ref(ids).logits.float()
+    m = AutoModelForCausalLM.from_pretrained(path, load_in_low_bit="sym_int8", torch_dtype=torch.bfloat16)
+    m = m.to("cuda").eval()
+    assert getattr(m, "_illm_native_attached", False)
+    with torch.no_grad():
+        out = m(ids[:, :32].cuda(), use_cache=True)
+        rel = ((out.logits.float().cpu() - want[:, :32]).norm() / want[:, :32].norm()).item()
+        assert rel < 6e-2, rel
+        cache = out.past_key_values
+        for t in range(32, 40):
+            step = m(ids[:, t:t + 1].cuda(), past_key_values=cache).logits.float().cpu()
+            r = ((step[:, -1] - want[:, t]).norm() / want[:, t].norm()).item()
+            assert r < 6e-2, (t, r)
+        g = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=True)
+        e = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=False)
+    assert torch.equal(g.cpu(), e.cpu())
