@@ -63,6 +63,27 @@ void launch_kq_dequant(int fmt, bool bf16, const uint8_t* w, int64_t n, int64_t 
 void launch_kq_gemv(int fmt, bool bf16, const uint16_t* x, int M, int64_t K, const uint8_t* w, int64_t N,
                     uint16_t* out, hipStream_t st);
 
+// ---- fp8 linear (fp8_gemm.hip): torch_fp8 qtypes on the f8f6f4 MFMA --------
+struct Fp8GemmArgs {
+  const uint8_t* xq;       // [M, K] e4m3 activations (GEMM)
+  const float* sx;         // [M] activation scales (GEMM)
+  const uint16_t* x;       // [M, K] bf16/f16 activations (GEMV)
+  const uint8_t* w;        // [N, K] fp8 weight
+  const float* sw;         // [1] or [N] weight scale
+  int sw_per_channel;
+  const uint16_t* bias;    // [N] or null
+  uint16_t* out;           // [M, N]
+  int M, N;
+  int64_t K;
+};
+// per-token e4m3 quantization: xq = sat(x / sx), sx = amax / 448 (K % 8 == 0)
+void launch_fp8_act_quant(bool bf16, const uint16_t* x, int64_t M, int64_t K, uint8_t* xq, float* sx,
+                          hipStream_t st);
+// N % 128 == 0, K % 128 == 0
+void launch_fp8_gemm(bool bf16, bool e5m2, const Fp8GemmArgs& a, hipStream_t st);
+// M <= 16, K % 16 == 0
+void launch_fp8_gemv(bool bf16, bool e5m2, const Fp8GemmArgs& a, hipStream_t st);
+
 // ---- norms (norm.hip) ------------------------------------------------------
 struct NormArgs {
   const uint16_t* x;       // [M, H] input (ignored when partials != null)

@@ -105,6 +105,13 @@ def lowbit_from_dense(w: torch.Tensor, qtype, device, bias: Optional[torch.Tenso
         if bias is not None:
             m.bias = nn.Parameter(bias.to(device, dt), requires_grad=False)
         return m
+    if qtype in (Q.TORCH_FP8E4, Q.TORCH_FP8E5):
+        from ..transformers.low_bit_linear import TorchFp8Linear
+        lin = nn.Linear(w.shape[1], w.shape[0], bias=bias is not None, device="meta")
+        lin.weight = nn.Parameter(w, requires_grad=False)
+        if bias is not None:
+            lin.bias = nn.Parameter(bias, requires_grad=False)
+        return TorchFp8Linear.from_linear(lin, qtype, device=device)
     f = Q.get_format(qtype)
     if f is not None and f.kquant:
         from ..transformers.low_bit_linear import KQuantLinear

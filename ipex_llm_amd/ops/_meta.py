@@ -197,3 +197,14 @@ def _(time_decay, time_first, k, v, num, den, mx):
 @register_fake("ipex_llm_amd::rwkv_wkv5")
 def _(w, u, r, k, v, state):
     return torch.empty_like(k, dtype=torch.float32)
+
+
+@register_fake("ipex_llm_amd::fp8_act_quant")
+def _(x):
+    x2 = x.reshape(-1, x.shape[-1])
+    return x2.new_empty(x2.shape, dtype=torch.uint8), x2.new_empty(x2.shape[0], dtype=torch.float32)
+
+
+@register_fake("ipex_llm_amd::fp8_linear")
+def _(x, w, w_scale, bias, e5m2):
+    return x.new_empty(*x.shape[:-1], w.shape[0])

@@ -14,7 +14,8 @@ import torch.nn.functional as F
 from . import reference as R
 
 __all__ = [
-    "quantize", "dequantize", "kq_quantize", "kq_dequantize", "kq_linear", "repack_to_device", "repack_from_device", "lowbit_matmul",
+    "quantize", "dequantize", "kq_quantize", "kq_dequantize", "kq_linear", "fp8_linear", "fp8_act_quant",
+    "fp8_quantize_weight", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemm", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
@@ -86,6 +87,36 @@ def kq_linear(x: torch.Tensor, blob: torch.Tensor, fmt: int, n: int, k: int) -> 
     if x.is_cuda and not _native(x):
         return F.linear(x, kq_dequantize(blob, fmt, n, k, torch.float32).to(x.dtype))
     return _ops().kq_linear(x, blob, fmt, n, k)
+
+
+# ------------------------------------------------------------ torch_fp8
+FP8_MAX = {False: 448.0, True: 57344.0}
+
+
+def fp8_quantize_weight(w: torch.Tensor, e5m2: bool = False, per_channel: bool = False):
+    """dense [n, k] -> (uint8 fp8 codes [n, k], f32 scale [1] or [n]): the
+    reference's dynamic_scaled_fp8_quant of a weight (per-tensor amax)"""
+    wf = w.float()
+    amax = wf.abs().amax(dim=1, keepdim=True) if per_channel else wf.abs().amax().reshape(1, 1)
+    s = torch.where(amax > 0, amax / FP8_MAX[e5m2], torch.ones_like(amax))
+    q = (wf / s).clamp(-FP8_MAX[e5m2], FP8_MAX[e5m2]).to(torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn)
+    return q.view(torch.uint8), s.reshape(-1).float()
+
+
+def fp8_act_quant(x: torch.Tensor):
+    """per-token e4m3 quantization -> (codes uint8 [M, K], scales f32 [M])"""
+    return _ops().fp8_act_quant(x)
+
+
+def fp8_linear(x: torch.Tensor, w: torch.Tensor, w_scale: torch.Tensor, bias: Optional[torch.Tensor] = None,
+               e5m2: bool = False) -> torch.Tensor:
+    """y = x @ (w * w_scale)^T (+ bias): GEMV for <= 16 rows, else per-token
+    fp8 activations on the block-scaled f8f6f4 MFMA GEMM (run_linear_fp8)"""
+    if x.is_cuda and not _native(x):
+        wd = w.view(torch.float8_e5m2 if e5m2 else torch.float8_e4m3fn).float() * w_scale.float().view(-1, 1)
+        y = F.linear(x.float(), wd, None if bias is None else bias.float())
+        return y.to(x.dtype)
+    return _ops().fp8_linear(x, w, w_scale, bias, e5m2)
 
 
 # ------------------------------------------------------------ low-bit GEMM

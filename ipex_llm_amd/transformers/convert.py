@@ -181,6 +181,12 @@ def _convert_one(module: nn.Linear, qtype: int, device, imatrix=None, mp_group=N
     if Q.is_dense(qtype):
         dt = torch.bfloat16 if qtype == Q.BF16 else torch.float16
         return DenseLinear.from_linear(module, dt, device, mp_group)
+    if qtype in (Q.TORCH_FP8E4, Q.TORCH_FP8E5):
+        from .low_bit_linear import TorchFp8Linear
+        if convert_shape_only or module.weight.device.type == "meta":
+            return TorchFp8Linear(module.in_features, module.out_features, qtype, module.bias is not None,
+                                  device="meta", mp_group=mp_group, optimize_lm_head=lm_head)
+        return TorchFp8Linear.from_linear(module, qtype, device=device, mp_group=mp_group, optimize_lm_head=lm_head)
     fmt = Q.get_format(qtype)
     if fmt.kquant and module.in_features % fmt.k_align:
         # reference check_hidden_size: the nearest 64-block format instead
@@ -331,8 +337,6 @@ def ggml_convert_low_bit(model: nn.Module, qtype="sym_int4", optimize_model: boo
     modules_to_not_convert = list(modules_to_not_convert or [])
     if optimize_model:
         _optimize_pre(model, qtype)
-    if qtype in (Q.TORCH_FP8E4, Q.TORCH_FP8E5):
-        qtype = Q.FP8E4 if qtype == Q.TORCH_FP8E4 else Q.FP8E5
     if qtype in (Q.MOFQ4, Q.MOFQ8):
         qtype = _pick_mixed_format(model, qtype)
     _ROOT_CFG[0] = getattr(model, "config", None)     # layer count for the gguf_q4k_s/m policies

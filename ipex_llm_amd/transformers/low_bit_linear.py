@@ -469,3 +469,67 @@ class RowConcatLinear(nn.Module):
             return torch.stack([g.reshape(*g.shape[:-1], I // 16, 16), u.reshape(*u.shape[:-1], I // 16, 16)],
                                -2).reshape(*g.shape[:-1], 2 * I)
         return torch.cat(ys, -1)
+
+
+class TorchFp8Linear(nn.Module):
+    """torch_fp8_e4m3 / torch_fp8_e5m2 linear (reference FP8 path:
+    ``ggml_convert_qtype`` -> fp8 weight + f32 scale, forward
+    ``xe_linear.run_linear_fp8``; SRC/transformers/low_bit_linear.py:110-113,
+    168-178, 692-696).  Weight: fp8 codes [out, in] (uint8) + a per-tensor
+    scale (``per_channel``: one per output row); forward on the GPU is the
+    fp8 GEMV (decode) or per-token e4m3 activations on the block-scaled
+    f8f6f4 MFMA GEMM (ops.fp8_linear)."""
+
+    def __init__(self, in_features: int, out_features: int, qtype="torch_fp8_e4m3", bias: bool = True, device=None,
+                 mp_group=None, optimize_lm_head: bool = False, per_channel: bool = False):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.qtype = Q.resolve_qtype(qtype)
+        self.e5m2 = self.qtype == Q.TORCH_FP8E5
+        self.weight = nn.Parameter(torch.empty(out_features, in_features, dtype=torch.uint8, device=device),
+                                   requires_grad=False)
+        self.w_scale = nn.Parameter(torch.ones(out_features if per_channel else 1, dtype=torch.float32,
+                                               device=device), requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(out_features, dtype=torch.float32, device=device), requires_grad=False) \
+            if bias else None
+        self.mp_group = mp_group
+        self.optimize_lm_head = optimize_lm_head
+
+    @classmethod
+    def from_linear(cls, linear, qtype, device=None, mp_group=None, optimize_lm_head=False, per_channel=False):
+        w = linear.weight.data
+        m = cls(w.shape[1], w.shape[0], qtype, bias=getattr(linear, "bias", None) is not None, device="meta",
+                mp_group=mp_group, optimize_lm_head=optimize_lm_head, per_channel=per_channel)
+        dev = device or w.device
+        q, s = ops.fp8_quantize_weight(w, m.e5m2, per_channel)
+        m.weight = nn.Parameter(q.to(dev), requires_grad=False)
+        m.w_scale = nn.Parameter(s.to(dev), requires_grad=False)
+        if linear.bias is not None:
+            m.bias = nn.Parameter(linear.bias.data.detach().to(dev).clone(), requires_grad=False)
+        return m
+
+    def dequantize(self, dtype=torch.float32) -> torch.Tensor:
+        f8 = torch.float8_e5m2 if self.e5m2 else torch.float8_e4m3fn
+        return (self.weight.view(f8).float() * self.w_scale.float().view(-1, 1)).to(dtype)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.optimize_lm_head and x.dim() == 3 and x.shape[1] > 10 and not self.training:
+            x = x[:, -1:, :]
+        in_dtype = x.dtype
+        if x.is_cuda and x.dtype not in (torch.bfloat16, torch.float16):
+            x = x.to(torch.bfloat16)
+        if self.training and torch.is_grad_enabled() and x.requires_grad:
+            y = F.linear(x, self.dequantize(x.dtype))             # (reference: fp8 training unsupported)
+        else:
+            bias = self.bias if self.mp_group is None else None
+            y = ops.fp8_linear(x, self.weight, self.w_scale, None if bias is None else bias.to(x.dtype), self.e5m2)
+        if self.mp_group is not None:
+            from ..parallel.comm import all_reduce_inplace
+            y = all_reduce_inplace(y, self.mp_group)
+            if self.bias is not None:
+                y = y + self.bias.to(y.dtype)
+        return y.to(in_dtype) if y.dtype != in_dtype else y
+
+    def extra_repr(self):
+        return (f"in_features={self.in_features}, out_features={self.out_features}, "
+                f"qtype={Q.qtype_name(self.qtype)}, bias={self.bias is not None}")
