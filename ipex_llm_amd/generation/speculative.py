@@ -58,11 +58,28 @@ class _AutoThreshold:
 @torch.no_grad()
 def speculative_generate(model, prompts: Sequence[Sequence[int]], max_new_tokens: int = 32, eos_token_id=None,
                          timing=None, streamer=None, max_step_draft: int = 8, th_stop_draft: float = 0.6,
-                         auto_th_stop_draft: bool = True, min_new_tokens: int = 0, **_) -> List[List[int]]:
+                         auto_th_stop_draft: bool = True, min_new_tokens: int = 0, use_graph: bool = True,
+                         **_) -> List[List[int]]:
     from ..transformers.hf_native import get_native
     _, tgt = get_native(model)
     _, dft = get_native(model.draft_model)
     eos = set([eos_token_id] if isinstance(eos_token_id, int) else (eos_token_id or []))
+    if tgt.model.device.type == "cuda" and use_graph:
+        # device-resident rounds captured as hipGraphs (generation/spec_graph.py)
+        from .spec_graph import GraphSpeculator, max_graph_draft
+        kmax = max(1, min(max_step_draft, max_graph_draft(tgt.model)))
+        outs = []
+        for p in prompts:
+            max_len = len(p) + max_new_tokens + 2 * kmax + 4
+            sp = model.__dict__.get("_illm_spec_graph")
+            if sp is None or sp.max_len < max_len or sp.k_max != kmax:
+                sp = GraphSpeculator(tgt, dft, min(4, kmax), max(max_len, 1024), k_max=kmax,
+                                     adaptive=auto_th_stop_draft)
+                model.__dict__["_illm_spec_graph"] = sp
+            outs.append(sp.generate(p, max_new_tokens, eos, timing=timing, streamer=streamer))
+            model.n_drafted += sp.drafted
+            model.n_matched += int(sp.n_match)
+        return outs
     sync = torch.cuda.synchronize if tgt.model.device.type == "cuda" else (lambda: None)
     thr = _AutoThreshold(th_stop_draft)
     outs = []

@@ -361,3 +361,27 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
     if pp is not None:
         model.layer_offset = pp["start"]
     return model.eval()
+
+
+@torch.no_grad()
+def dense_copy(model: NativeCausalLM) -> NativeCausalLM:
+    """The same decoder with every low-bit linear replaced by a bf16
+    DenseLinear holding its dequantized weight: a target model that agrees
+    with its INT4 draft like a real checkpoint and its INT4 copy (self-
+    speculative benchmarks / tests on random weights)."""
+    def dense(m):
+        d = DenseLinear(m.in_features, m.out_features, m.bias is not None, torch.bfloat16, "meta")
+        d.weight = nn.Parameter(m.dequantize(torch.bfloat16).contiguous(), requires_grad=False)
+        if m.bias is not None:
+            d.bias = nn.Parameter(m.bias.detach().to(torch.bfloat16), requires_grad=False)
+        return d
+
+    s = model.spec
+    layers = []
+    for L in model.layers:
+        a = L.self_attn
+        attn = NativeAttention(s, dense(a.qkv_proj), dense(a.o_proj), a.q_norm, a.k_norm, a.sliding_window)
+        mlp = NativeMLP(s, dense(L.mlp.gate_up_proj), dense(L.mlp.down_proj))
+        layers.append(NativeLayer(s, attn, mlp, L.input_layernorm.data, L.post_attention_layernorm.data))
+    return NativeCausalLM(s, model.embed_tokens.data, layers, model.norm.data, dense(model.lm_head),
+                          model.inv_freq, torch.bfloat16).eval()

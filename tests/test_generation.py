@@ -48,3 +48,25 @@ def test_self_speculative_matches_target_greedy(tmp_path):
     out = spec.generate(ids, max_new_tokens=24)
     assert torch.equal(out, ref)
     assert spec.n_drafted > 0 and spec.n_matched > 0
+
+
+def test_graph_speculator_eager_matches_target_greedy(tmp_path):
+    """the device-resident round (generation/spec_graph.py) run eagerly on the
+    host: same tokens as the target's plain greedy decoding, for several
+    draft lengths, adaptive or not"""
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    from ipex_llm_amd.transformers.hf_native import get_native
+    from ipex_llm_amd.generation.spec_graph import GraphSpeculator
+    p = _tiny(tmp_path)
+    tgt = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="bf16", torch_dtype=torch.float32)
+    dft = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="sym_int4", torch_dtype=torch.float32)
+    ids = torch.randint(0, 64, (1, 9), generator=torch.Generator().manual_seed(2))
+    ref = tgt.generate(ids, max_new_tokens=24)[0].tolist()
+    te, de = get_native(tgt)[1], get_native(dft)[1]
+    for k, adaptive in ((1, False), (3, False), (2, True)):
+        sp = GraphSpeculator(te, de, k, 128, use_graph=False, k_max=5 if adaptive else k, adaptive=adaptive)
+        out = sp.generate(ids[0].tolist(), 24)
+        assert out == ref, (k, adaptive)
+        assert sp.rounds > 0 and 0.0 <= sp.acceptance <= 1.0
+        # a second call reuses the speculator (graph keys / buffers)
+        assert sp.generate(ids[0].tolist(), 10) == ref[:9 + 10]

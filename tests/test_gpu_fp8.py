@@ -20,9 +20,13 @@ def test_fp8_gemm_matches_emulation(e5m2, M, N, K, per_channel):
     b = torch.randn(N).to(torch.bfloat16)
     w8, ws = ops.fp8_quantize_weight(w, e5m2, per_channel)
     want = ops.fp8_linear(x.float(), w8, ws, b.float(), e5m2)          # host: f32 emulation
-    got = ops.fp8_linear(x.cuda(), w8.cuda(), ws.cuda(), b.cuda(), e5m2).float().cpu()
+    xd, wd_, sd, bd = x.cuda(), w8.cuda(), ws.cuda(), b.cuda()
+    got = torch.ops.ipex_llm_amd.fp8_linear(xd, wd_, sd, bd, e5m2).float().cpu()     # hand-written MFMA GEMM
     rel = ((got - want).norm() / want.norm()).item()
     assert rel < 1e-2, rel
+    got2 = ops.fp8_linear(xd, wd_, sd, bd, e5m2).float().cpu()                        # dispatch (library >= 128 rows)
+    rel2 = ((got2 - want).norm() / want.norm()).item()
+    assert rel2 < 1e-2, rel2
 
 
 def test_fp8_act_quant_matches_host():

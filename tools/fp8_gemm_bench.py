@@ -32,7 +32,8 @@ def main():
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             w8, ws = ops.fp8_quantize_weight(w, False)
             wb = w.to(torch.bfloat16)
-            t_ours = timeit(lambda: ops.fp8_linear(x, w8, ws, None, False))
+            t_ours = timeit(lambda: torch.ops.ipex_llm_amd.fp8_linear(x, w8, ws, None, False))
+            t_disp = timeit(lambda: ops.fp8_linear(x, w8, ws, None, False))
             t_bf16 = timeit(lambda: torch.matmul(x, wb.t()))
             t_sm = None
             try:
@@ -45,7 +46,8 @@ def main():
                 t_sm = f"n/a: {type(ex).__name__}"
             fl = 2.0 * M * N * K
             rec = {"M": M, "proj": name, "N": N, "K": K, "fp8_ours_us": round(t_ours, 1),
-                   "fp8_ours_tflops": round(fl / t_ours / 1e6, 1), "bf16_hipblaslt_us": round(t_bf16, 1),
+                   "fp8_ours_tflops": round(fl / t_ours / 1e6, 1), "fp8_dispatch_us": round(t_disp, 1),
+                   "fp8_dispatch_tflops": round(fl / t_disp / 1e6, 1), "bf16_hipblaslt_us": round(t_bf16, 1),
                    "bf16_tflops": round(fl / t_bf16 / 1e6, 1),
                    "fp8_scaled_mm_us": round(t_sm, 1) if isinstance(t_sm, float) else t_sm}
             print(json.dumps(rec), flush=True)
