@@ -48,7 +48,7 @@ def _permute(w: np.ndarray, n_head: int) -> np.ndarray:
 
 def export_gguf(model, outfile: str, qtype: str = "f16", tokenizer=None) -> str:
     """Write a llama-family HF model (path or module) as GGUF."""
-    from .gguf.reader import F16, F32, Q4_0, Q8_0, GGUFWriter
+    from .gguf.reader import F16, F32, Q2_K, Q4_0, Q4_K, Q5_K, Q6_K, Q8_0, GGUFWriter
     if isinstance(model, str):
         from transformers import AutoModelForCausalLM as HF, AutoTokenizer
         src = model
@@ -63,7 +63,21 @@ def export_gguf(model, outfile: str, qtype: str = "f16", tokenizer=None) -> str:
     arch = {"llama": "llama", "mistral": "llama", "qwen2": "qwen2", "qwen3": "qwen3"}.get(mt)
     if arch is None:
         raise NotImplementedError(f"GGUF export supports llama/mistral/qwen2/qwen3, not {mt}")
-    tq = {"f32": F32, "f16": F16, "q8_0": Q8_0, "q4_0": Q4_0}[qtype]
+    kq = {"q4_k": Q4_K, "q5_k": Q5_K, "q6_k": Q6_K, "q2_k": Q2_K, "q4_k_m": Q4_K, "q4_k_s": Q4_K}
+    tq = {"f32": F32, "f16": F16, "q8_0": Q8_0, "q4_0": Q4_0, **kq}[qtype]
+
+    def mat_type(hf_name, v):
+        """k-quants: only rows of 256-multiples; q4_k_m / q4_k_s: llama.cpp's
+        mixed policy (quantize/qtypes.mixed_kquant_qtype)"""
+        if tq not in kq.values():
+            return tq
+        if v.shape[-1] % 256:
+            return Q8_0 if v.shape[-1] % 32 == 0 else F32
+        if qtype in ("q4_k_m", "q4_k_s"):
+            from .quantize import qtypes as Qt
+            q = Qt.mixed_kquant_qtype("gguf_" + qtype.replace("_k_", "k_"), hf_name, cfg.num_hidden_layers)
+            return {Qt.Q6_K: Q6_K, Qt.Q5_K: Q5_K}.get(q, Q4_K)
+        return tq
     w = GGUFWriter(outfile, arch)
     nh, nkv = cfg.num_attention_heads, getattr(cfg, "num_key_value_heads", cfg.num_attention_heads)
     w.add(f"{arch}.context_length", int(cfg.max_position_embeddings))
@@ -91,12 +105,12 @@ def export_gguf(model, outfile: str, qtype: str = "f16", tokenizer=None) -> str:
              "mlp.up_proj": "ffn_up", "mlp.down_proj": "ffn_down"}
     for k, v in sd.items():
         if k == "model.embed_tokens.weight":
-            w.add_tensor("token_embd.weight", v, tq if v.shape[1] % 32 == 0 else F32)
+            w.add_tensor("token_embd.weight", v, (Q8_0 if tq in kq.values() else tq) if v.shape[1] % 32 == 0 else F32)
         elif k == "model.norm.weight":
             w.add_tensor("output_norm.weight", v, F32)
         elif k == "lm_head.weight":
             if not getattr(cfg, "tie_word_embeddings", False):
-                w.add_tensor("output.weight", v, tq)
+                w.add_tensor("output.weight", v, mat_type("lm_head", v))
         else:
             parts = k.split(".")
             if len(parts) < 5 or parts[1] != "layers":
@@ -109,7 +123,7 @@ def export_gguf(model, outfile: str, qtype: str = "f16", tokenizer=None) -> str:
                 v = _permute(v if v.ndim == 2 else v[:, None], nh if g == "attn_q" else nkv)
                 v = v if wb == "weight" else v[:, 0]
             is_mat = v.ndim == 2 and v.shape[1] % 32 == 0 and "norm" not in g
-            w.add_tensor(f"blk.{i}.{g}.{wb}", v, tq if is_mat else F32)
+            w.add_tensor(f"blk.{i}.{g}.{wb}", v, mat_type(f"model.layers.{i}.{rest}", v) if is_mat else F32)
     w.write()
     return outfile
 

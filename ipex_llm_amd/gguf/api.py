@@ -8,7 +8,12 @@ tensor).  Here one table-driven builder covers the llama-layout families
 (llama / mistral / qwen2 / qwen3 and the MoE variants mixtral / qwen2moe /
 qwen3moe); the tokenizer is rebuilt with transformers' GGUF converters.
 Tensors are dequantized one at a time from the memory-mapped file and then
-re-quantized by ``ggml_convert_low_bit`` into the MI355X formats.
+re-quantized by ``ggml_convert_low_bit`` into the MI355X formats -- except
+the k-quant projections (Q2_K / Q4_K / Q5_K / Q6_K): with ``keep_kquant``
+their super-block bytes become :class:`KQuantLinear` weights as they are
+(the device layout IS the GGUF layout), no dequantize / re-quantize round
+trip, bits per weight and numerics exactly those of the file.  llama.cpp's
+q/k row permutation is undone on whole block rows.
 """
 from __future__ import annotations
 
@@ -105,8 +110,34 @@ def _tokenizer(r: GGUFReader):
     return PreTrainedTokenizerFast(tokenizer_object=fast, **extra)
 
 
-def load_gguf_model(fpath: str, dtype=torch.float16, low_bit: Optional[str] = None) -> Tuple[torch.nn.Module, object]:
-    """GGUF file -> (HF CausalLM with dense ``dtype`` weights, tokenizer)."""
+def _kquant_linear_targets(r: GGUFReader):
+    """GGUF linear tensors stored as k-quants -> (HF module path, qtype)"""
+    from .reader import KQUANT_QTYPE
+    out = {}
+    for name, ti in r.tensors.items():
+        if ti.ggml_type not in KQUANT_QTYPE or len(ti.shape) != 2:
+            continue
+        if name == "output.weight":
+            out[name] = ("lm_head", KQUANT_QTYPE[ti.ggml_type])
+            continue
+        m = re.match(r"blk\.(\d+)\.(\w+?)\.weight$", name)
+        if m and m.group(2) in _LAYER and not _LAYER[m.group(2)].endswith(".weight"):
+            out[name] = (f"model.layers.{m.group(1)}.{_LAYER[m.group(2)]}", KQUANT_QTYPE[ti.ggml_type])
+    return out
+
+
+def _unpermute_rows(raw: np.ndarray, n_rows: int, n_head: int) -> np.ndarray:
+    """llama.cpp q/k permutation undone on whole (block-encoded) rows"""
+    rows = raw.reshape(n_rows, -1)
+    idx = _unpermute(np.arange(n_rows), n_head)
+    return np.ascontiguousarray(rows[idx]).reshape(-1)
+
+
+def load_gguf_model(fpath: str, dtype=torch.float16, low_bit: Optional[str] = None,
+                    keep_kquant: bool = False) -> Tuple[torch.nn.Module, object]:
+    """GGUF file -> (HF CausalLM with dense ``dtype`` weights, tokenizer).
+    ``keep_kquant``: k-quant projections become KQuantLinear modules over the
+    file's blocks (everything else stays dense for ``ggml_convert_low_bit``)."""
     from accelerate import init_empty_weights
     from transformers import AutoModelForCausalLM
     r = GGUFReader(fpath)
@@ -116,7 +147,19 @@ def load_gguf_model(fpath: str, dtype=torch.float16, low_bit: Optional[str] = No
     n_head, n_kv = cfg.num_attention_heads, getattr(cfg, "num_key_value_heads", cfg.num_attention_heads)
     sd: Dict[str, torch.Tensor] = {}
     experts: Dict[int, Dict[str, np.ndarray]] = {}
+    kq_targets = _kquant_linear_targets(r) if keep_kquant else {}
+    kq_blocks = {}
     for name in r.tensors:
+        if name in kq_targets:
+            path, qt = kq_targets[name]
+            ti = r.tensors[name]
+            k, n = ti.shape                                  # GGUF order: ne0 = in_features
+            raw = np.asarray(r.raw(name))
+            kind = name.split(".")[2] if name.startswith("blk.") else ""
+            if kind in ("attn_q", "attn_k") and r.architecture == "llama":
+                raw = _unpermute_rows(raw, n, n_head if kind == "attn_q" else n_kv)
+            kq_blocks[path] = (torch.from_numpy(np.array(raw, dtype=np.uint8)), qt, n, k)
+            continue
         w = r.tensor(name)
         if name == "token_embd.weight":
             sd["model.embed_tokens.weight"] = torch.from_numpy(w)
@@ -155,6 +198,14 @@ def load_gguf_model(fpath: str, dtype=torch.float16, low_bit: Optional[str] = No
     model.load_state_dict(sd, strict=False, assign=True)
     if cfg.tie_word_embeddings:
         model.tie_weights()
+    if kq_blocks:
+        from ..transformers.low_bit_linear import KQuantLinear
+        for path, (blob, qt, n, k) in kq_blocks.items():
+            parent_path, leaf = path.rsplit(".", 1) if "." in path else ("", path)
+            parent = model.get_submodule(parent_path) if parent_path else model
+            old = getattr(parent, leaf)
+            bias = old.bias if getattr(old, "bias", None) is not None and old.bias.device.type != "meta" else None
+            setattr(parent, leaf, KQuantLinear.from_blocks(blob, qt, n, k, device="cpu", bias=bias))
     from ..transformers.model import _reinit_meta_buffers
     _reinit_meta_buffers(model, cfg)
     missing = [n for n, p in model.named_parameters() if p.device.type == "meta"]

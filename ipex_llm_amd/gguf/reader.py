@@ -22,9 +22,9 @@ Q2_K, Q3_K, Q4_K, Q5_K, Q6_K, Q8_K = 10, 11, 12, 13, 14, 15
 BF16 = 30
 # (elements per block, bytes per block)
 BLOCK = {F32: (1, 4), F16: (1, 2), BF16: (1, 2), Q4_0: (32, 18), Q4_1: (32, 20), Q5_0: (32, 22), Q5_1: (32, 24),
-         Q8_0: (32, 34), Q4_K: (256, 144), Q5_K: (256, 176), Q6_K: (256, 210)}
+         Q8_0: (32, 34), Q2_K: (256, 84), Q4_K: (256, 144), Q5_K: (256, 176), Q6_K: (256, 210)}
 TYPE_NAMES = {F32: "F32", F16: "F16", BF16: "BF16", Q4_0: "Q4_0", Q4_1: "Q4_1", Q5_0: "Q5_0", Q5_1: "Q5_1",
-              Q8_0: "Q8_0", Q4_K: "Q4_K", Q5_K: "Q5_K", Q6_K: "Q6_K"}
+              Q8_0: "Q8_0", Q2_K: "Q2_K", Q4_K: "Q4_K", Q5_K: "Q5_K", Q6_K: "Q6_K"}
 
 # key/value types
 (T_U8, T_I8, T_U16, T_I16, T_U32, T_I32, T_F32, T_BOOL, T_STR, T_ARR, T_U64, T_I64, T_F64) = range(13)
@@ -201,7 +201,18 @@ def dequantize(raw: np.ndarray, t: int, n: int) -> np.ndarray:
                 isc = s[:, 2 * qi + idx // 16]                             # scale per 16 elements
                 out[:, base + 32 * qi:base + 32 * qi + 32] = d * isc * q
         return out.reshape(-1)
+    if t == Q2_K:                       # C++ decoder (csrc/cpu/kquant.cpp), same block layout
+        import torch
+        from .. import ops
+        from ..quantize import qtypes as Qt
+        nb = blk.shape[0]
+        return ops.kq_dequantize(torch.from_numpy(np.ascontiguousarray(blk).reshape(-1)), Qt.FMT_Q2K, nb,
+                                 256).numpy().reshape(-1)
     raise NotImplementedError(f"GGUF tensor type {TYPE_NAMES.get(t, t)} is not supported")
+
+
+# GGUF k-quant type -> our native qtype name (blocks used as-is, quantize/qtypes.py)
+KQUANT_QTYPE = {Q2_K: "q2_k", Q4_K: "q4_k", Q5_K: "q5_k", Q6_K: "q6_k"}
 
 
 def _k_scales(s: np.ndarray):
@@ -245,7 +256,8 @@ def quantize_q4_0(x: np.ndarray) -> bytes:
 
 
 class GGUFWriter:
-    """Minimal GGUF v3 writer (metadata + F32/F16/Q8_0/Q4_0 tensors)."""
+    """Minimal GGUF v3 writer (metadata + F32/F16/Q8_0/Q4_0 and the
+    Q2_K/Q4_K/Q5_K/Q6_K k-quant tensors, the latter by the C++ quantizer)."""
 
     def __init__(self, path: str, arch: str = "llama"):
         self.path, self.kv, self.tensors = path, {"general.architecture": (T_STR, arch)}, []
@@ -266,6 +278,12 @@ class GGUFWriter:
             data = quantize_q8_0(arr)
         elif ggml_type == Q4_0:
             data = quantize_q4_0(arr)
+        elif ggml_type in KQUANT_QTYPE:
+            import torch
+            from .. import ops
+            from ..quantize import qtypes as Qt
+            fmt = Qt.get_format(KQUANT_QTYPE[ggml_type]).fmt
+            data = ops.kq_quantize(torch.from_numpy(arr.reshape(-1, arr.shape[-1])), fmt).numpy().tobytes()
         else:
             raise NotImplementedError(TYPE_NAMES.get(ggml_type, ggml_type))
         self.tensors.append((name, tuple(reversed(arr.shape)), ggml_type, data))

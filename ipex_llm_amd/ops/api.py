@@ -139,7 +139,7 @@ def _fp8_linear_lib(x, w, w_scale, bias, e5m2):
         _FP8_LIB[0] = False
         return None
     K, N = x.shape[-1], w.shape[0]
-    if K % 16 or N % 16:
+    if K % 16 or N % 16 or e5m2:          # (rowwise-scaled e4m3 x e5m2 is not a library combination)
         return None
     x2 = x.reshape(-1, K)
     try:
@@ -149,7 +149,7 @@ def _fp8_linear_lib(x, w, w_scale, bias, e5m2):
         y = torch._scaled_mm(xq.view(torch.float8_e4m3fn), wt, scale_a=sx.view(-1, 1), scale_b=sw,
                              bias=None, out_dtype=x.dtype)
         _FP8_LIB[0] = True
-    except (RuntimeError, TypeError):
+    except (RuntimeError, TypeError, ValueError):
         _FP8_LIB[0] = False
         return None
     if bias is not None:

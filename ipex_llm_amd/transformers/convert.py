@@ -75,6 +75,15 @@ def _merge_qkv(attn: nn.Module):
         attn._illm_qkv_split = tuple(m.out_features for m in mods)
         del attn.q_proj, attn.k_proj, attn.v_proj
         return
+    from .low_bit_linear import KQuantLinear, kquant_row_concat
+    if any(isinstance(m, KQuantLinear) for m in mods) and \
+            all(isinstance(m, (KQuantLinear, nn.Linear)) for m in mods):
+        # GGUF k-quant checkpoints (kept in their blocks); dense parts are
+        # converted later inside the RowConcatLinear
+        attn.qkv_proj = kquant_row_concat(mods)
+        attn._illm_qkv_split = tuple(m.out_features for m in mods)
+        del attn.q_proj, attn.k_proj, attn.v_proj
+        return
     if not all(isinstance(m, nn.Linear) for m in mods):
         return
     attn.qkv_proj = _merge_linears([attn.q_proj, attn.k_proj, attn.v_proj])
@@ -101,6 +110,9 @@ def _merge_gate_up(mlp: nn.Module):
                 return
         from .low_bit_linear import lowbit_row_concat
         mlp.gate_up_proj = lowbit_row_concat([mlp.gate_proj, mlp.up_proj], interleave_glu=True)
+    elif type(mlp.gate_proj).__name__ == "KQuantLinear" or type(mlp.up_proj).__name__ == "KQuantLinear":
+        from .low_bit_linear import kquant_row_concat
+        mlp.gate_up_proj = kquant_row_concat([mlp.gate_proj, mlp.up_proj], interleave_glu=True)
     elif isinstance(mlp.gate_proj, nn.Linear) and isinstance(mlp.up_proj, nn.Linear):
         mlp.gate_up_proj = _merge_linears([mlp.gate_proj, mlp.up_proj], interleave_glu=True)
     else:
@@ -146,8 +158,9 @@ def _optimize_pre(model: nn.Module, qtype: int):
         if mlp is not None:
             I = getattr(getattr(mlp, "gate_proj", None), "out_features", None) or \
                 (getattr(getattr(mlp, "gate_up_proj", None), "out_features", 0) // 2)
-            if I and I % 16 == 0 and isinstance(getattr(mlp, "gate_up_proj", getattr(mlp, "gate_proj", None)),
-                                                (nn.Linear, LowBitLinear)):
+            if I and I % 16 == 0 and (isinstance(getattr(mlp, "gate_up_proj", getattr(mlp, "gate_proj", None)),
+                                                 (nn.Linear, LowBitLinear)) or
+                                      type(getattr(mlp, "gate_proj", None)).__name__ == "KQuantLinear"):
                 _merge_gate_up(mlp)
     model._illm_pre = True
     return model

@@ -471,6 +471,29 @@ class RowConcatLinear(nn.Module):
         return torch.cat(ys, -1)
 
 
+def kquant_row_concat(mods, interleave_glu: bool = False) -> nn.Module:
+    """Merge q/k/v (or gate/up with the 16-row tile interleave) whose parts
+    are GGUF k-quant linears: one KQuantLinear over the concatenated block
+    rows when the parts share a type (rows are independent block runs), else
+    a RowConcatLinear keeping each part's type (gguf_q4k_m: v in q6_k)."""
+    if all(isinstance(m, KQuantLinear) for m in mods) and len({m.qtype for m in mods}) == 1 and \
+            len({m.in_features for m in mods}) == 1:
+        k = mods[0].in_features
+        rows = [m.weight.data.view(m.out_features, -1) for m in mods]
+        if interleave_glu:
+            from ..models.decoder import interleave_glu_rows
+            blob = interleave_glu_rows(rows[0], rows[1])
+        else:
+            blob = torch.cat(rows, 0)
+        bias = None
+        if any(m.bias is not None for m in mods) and not interleave_glu:
+            bias = torch.cat([m.bias.data if m.bias is not None else
+                              torch.zeros(m.out_features, dtype=torch.float32) for m in mods])
+        return KQuantLinear.from_blocks(blob.reshape(-1), mods[0].qtype, sum(m.out_features for m in mods), k,
+                                        bias=bias)
+    return RowConcatLinear(mods, interleave_glu)
+
+
 class TorchFp8Linear(nn.Module):
     """torch_fp8_e4m3 / torch_fp8_e5m2 linear (reference FP8 path:
     ``ggml_convert_qtype`` -> fp8 weight + f32 scale, forward

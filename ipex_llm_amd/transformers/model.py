@@ -215,10 +215,12 @@ class _BaseAutoModelClass:
 
     @classmethod
     def from_gguf(cls, fpath: str, optimize_model: bool = True, cpu_embedding: bool = False,
-                  low_bit: str = "sym_int4"):
-        """Load a GGUF file (reference model.py:391-408 / gguf/api.py)."""
+                  low_bit: str = "sym_int4", keep_kquant: bool = True, torch_dtype=torch.float16):
+        """Load a GGUF file (reference model.py:391-408 / gguf/api.py).
+        ``keep_kquant``: Q2_K/Q4_K/Q5_K/Q6_K projections keep their GGUF
+        blocks (native k-quant kernels); other tensors go to ``low_bit``."""
         from ..gguf.api import load_gguf_model
-        model, tokenizer = load_gguf_model(fpath, dtype=torch.float16)
+        model, tokenizer = load_gguf_model(fpath, dtype=torch_dtype, keep_kquant=keep_kquant)
         ggml_convert_low_bit(model, low_bit, optimize_model, cpu_embedding=cpu_embedding)
         _attach(model, low_bit, {})
         return model, tokenizer

@@ -130,3 +130,34 @@ def test_legacy_quant_roundtrip(t):
     raw = np.frombuffer(G.quantize_q4_0(x) if t == G.Q4_0 else G.quantize_q8_0(x), np.uint8)
     y = G.dequantize(raw, t, 256)
     assert np.abs(y - x).max() < (0.5 if t == G.Q4_0 else 0.03)
+
+
+@pytest.mark.parametrize("qt", ["q4_k", "q4_k_m", "q6_k", "q2_k"])
+def test_from_gguf_keeps_kquant_blocks(tmp_path, qt):
+    """k-quant GGUF tensors load as KQuantLinear over the file's own blocks
+    (no dequantize / re-quantize): bits per weight and numerics equal the
+    file's -- logits match a dense model built from the dequantized tensors"""
+    from ipex_llm_amd.convert_model import export_gguf
+    from ipex_llm_amd.gguf.api import load_gguf_model
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    from ipex_llm_amd.transformers.low_bit_linear import KQuantLinear, RowConcatLinear
+    from transformers import LlamaConfig, LlamaForCausalLM
+    torch.manual_seed(0)
+    cfg = LlamaConfig(vocab_size=256, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=512)
+    ref = LlamaForCausalLM(cfg).eval()
+    f = export_gguf(ref, str(tmp_path / f"m-{qt}.gguf"), qt)
+    r = G.GGUFReader(f)
+    kinds = {r.tensors[n].ggml_type for n in r.tensors if n.endswith("attn_v.weight") or n.endswith("ffn_up.weight")}
+    assert kinds & {G.Q2_K, G.Q4_K, G.Q5_K, G.Q6_K}
+    dense, _ = load_gguf_model(f, dtype=torch.float32)                 # dequantized reference
+    m, _ = AutoModelForCausalLM.from_gguf(f, low_bit="sym_int8", keep_kquant=True, torch_dtype=torch.float32)
+    kq = [x for x in m.modules() if isinstance(x, (KQuantLinear, RowConcatLinear))]
+    assert kq, "no k-quant module kept"
+    if qt == "q4_k_m":       # v rows in q6_k, q/k in q4_k: the merged qkv keeps both types
+        assert any(isinstance(x, RowConcatLinear) for x in kq)
+    ids = torch.randint(0, 256, (1, 9))
+    with torch.no_grad():
+        a = dense(ids).logits
+        b = m(ids).logits.float()
+    assert ((a - b).norm() / a.norm()).item() < 1e-3
