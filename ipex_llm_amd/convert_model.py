@@ -61,8 +61,8 @@ def export_gguf(model, outfile: str, qtype: str = "f16", tokenizer=None) -> str:
     cfg = model.config
     mt = cfg.model_type
     arch = {"llama": "llama", "mistral": "llama", "qwen2": "qwen2", "qwen3": "qwen3"}.get(mt)
-    if arch is None:
-        raise NotImplementedError(f"GGUF export supports llama/mistral/qwen2/qwen3, not {mt}")
+    if arch is None and mt not in ("bloom", "falcon", "mpt"):
+        raise NotImplementedError(f"GGUF export supports llama/mistral/qwen2/qwen3/bloom/falcon/mpt, not {mt}")
     kq = {"q4_k": Q4_K, "q5_k": Q5_K, "q6_k": Q6_K, "q2_k": Q2_K, "q4_k_m": Q4_K, "q4_k_s": Q4_K}
     tq = {"f32": F32, "f16": F16, "q8_0": Q8_0, "q4_0": Q4_0, **kq}[qtype]
 
@@ -78,6 +78,10 @@ def export_gguf(model, outfile: str, qtype: str = "f16", tokenizer=None) -> str:
             q = Qt.mixed_kquant_qtype("gguf_" + qtype.replace("_k_", "k_"), hf_name, cfg.num_hidden_layers)
             return {Qt.Q6_K: Q6_K, Qt.Q5_K: Q5_K}.get(q, Q4_K)
         return tq
+    if arch is None:
+        from .gguf.families import export_family_gguf
+        emb_t = Q8_0 if tq in kq.values() else tq
+        return export_family_gguf(model, outfile, emb_t, mat_type)
     w = GGUFWriter(outfile, arch)
     nh, nkv = cfg.num_attention_heads, getattr(cfg, "num_key_value_heads", cfg.num_attention_heads)
     w.add(f"{arch}.context_length", int(cfg.max_position_embeddings))

@@ -27,6 +27,7 @@ from .reader import GGUFReader
 
 ARCH_TO_HF = {"llama": "llama", "mistral": "mistral", "qwen2": "qwen2", "qwen3": "qwen3",
               "qwen2moe": "qwen2_moe", "qwen3moe": "qwen3_moe"}
+# bloom / falcon / mpt / baichuan: gguf/families.py
 
 _LAYER = {
     "attn_norm": "input_layernorm.weight",
@@ -110,12 +111,20 @@ def _tokenizer(r: GGUFReader):
     return PreTrainedTokenizerFast(tokenizer_object=fast, **extra)
 
 
-def _kquant_linear_targets(r: GGUFReader):
+def _kquant_linear_targets(r: GGUFReader, arch: str = "llama", cfg=None):
     """GGUF linear tensors stored as k-quants -> (HF module path, qtype)"""
+    from .families import TABLES, hf_name
     from .reader import KQUANT_QTYPE
     out = {}
     for name, ti in r.tensors.items():
         if ti.ggml_type not in KQUANT_QTYPE or len(ti.shape) != 2:
+            continue
+        if arch in TABLES:
+            if name == "token_embd.weight":
+                continue
+            key = hf_name(arch, name, cfg)
+            if key is not None and key.endswith(".weight"):
+                out[name] = (key[:-len(".weight")], KQUANT_QTYPE[ti.ggml_type])
             continue
         if name == "output.weight":
             out[name] = ("lm_head", KQUANT_QTYPE[ti.ggml_type])
@@ -140,24 +149,40 @@ def load_gguf_model(fpath: str, dtype=torch.float16, low_bit: Optional[str] = No
     file's blocks (everything else stays dense for ``ggml_convert_low_bit``)."""
     from accelerate import init_empty_weights
     from transformers import AutoModelForCausalLM
+    from .families import TABLES, family_config, hf_name, qkv_gguf_to_hf
     r = GGUFReader(fpath)
-    cfg, mt = _config(r)
+    arch = r.architecture
+    fam = family_config(r) if arch in ("bloom", "falcon", "mpt", "baichuan") else None
+    cfg, mt = (fam, fam.model_type) if fam is not None else _config(r)
+    permuted = arch in ("llama", "baichuan")          # llama.cpp's q/k row permutation
     with init_empty_weights():
         model = AutoModelForCausalLM.from_config(cfg, torch_dtype=dtype)
     n_head, n_kv = cfg.num_attention_heads, getattr(cfg, "num_key_value_heads", cfg.num_attention_heads)
     sd: Dict[str, torch.Tensor] = {}
     experts: Dict[int, Dict[str, np.ndarray]] = {}
-    kq_targets = _kquant_linear_targets(r) if keep_kquant else {}
+    kq_targets = _kquant_linear_targets(r, arch, cfg) if keep_kquant else {}
     kq_blocks = {}
     for name in r.tensors:
+        if arch in TABLES and name not in kq_targets:
+            key = hf_name(arch, name, cfg)
+            if key is None:
+                continue
+            w = r.tensor(name)
+            if ".attn_qkv." in name:
+                w = qkv_gguf_to_hf(arch, w, cfg)
+            sd[key] = torch.from_numpy(np.ascontiguousarray(w))
+            continue
         if name in kq_targets:
             path, qt = kq_targets[name]
             ti = r.tensors[name]
             k, n = ti.shape                                  # GGUF order: ne0 = in_features
             raw = np.asarray(r.raw(name))
             kind = name.split(".")[2] if name.startswith("blk.") else ""
-            if kind in ("attn_q", "attn_k") and r.architecture == "llama":
+            if kind in ("attn_q", "attn_k") and permuted:
                 raw = _unpermute_rows(raw, n, n_head if kind == "attn_q" else n_kv)
+            if kind == "attn_qkv":                       # fused families: HF row order, whole block rows
+                rows = qkv_gguf_to_hf(arch, np.arange(n), cfg)
+                raw = np.ascontiguousarray(raw.reshape(n, -1)[rows]).reshape(-1)
             kq_blocks[path] = (torch.from_numpy(np.array(raw, dtype=np.uint8)), qt, n, k)
             continue
         w = r.tensor(name)
@@ -180,9 +205,9 @@ def load_gguf_model(fpath: str, dtype=torch.float16, low_bit: Optional[str] = No
         target = _LAYER.get(kind)
         if target is None:
             continue
-        if kind in ("attn_q", "attn_k") and r.architecture == "llama" and wb == "weight":
+        if kind in ("attn_q", "attn_k") and permuted and wb == "weight":
             w = _unpermute(w, n_head if kind == "attn_q" else n_kv)
-        elif kind in ("attn_q", "attn_k") and r.architecture == "llama" and wb == "bias":
+        elif kind in ("attn_q", "attn_k") and permuted and wb == "bias":
             w = _unpermute(w[:, None], n_head if kind == "attn_q" else n_kv)[:, 0]
         key = f"model.layers.{i}.{target}"
         if not key.endswith((".weight", ".bias")):

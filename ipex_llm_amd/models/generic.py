@@ -269,9 +269,24 @@ def generic_pre(model: nn.Module) -> bool:
             _merge_qkv(attn)
         else:
             fused = getattr(attn, src)
+            perm = _qkv_perm(mt, cfg, s.num_heads, s.num_kv_heads, s.head_dim)
+            if type(fused).__name__ == "KQuantLinear":
+                # GGUF k-quant blocks (gguf/api.py keep_kquant): permute whole block rows
+                from ..transformers.low_bit_linear import KQuantLinear
+                n = fused.out_features
+                rows = fused.weight.data.view(n, -1)
+                idx = torch.tensor(perm if perm is not None else list(range(n)), dtype=torch.long)
+                b = fused.bias.data.index_select(0, idx) if fused.bias is not None else None
+                attn.qkv_proj = KQuantLinear.from_blocks(rows.index_select(0, idx).reshape(-1), fused.qtype, n,
+                                                         fused.in_features, bias=b)
+                inv = [0] * n
+                for i, r in enumerate(idx.tolist()):
+                    inv[r] = i
+                attn._illm_fused_src = (src, inv)
+                delattr(attn, src)
+                continue
             if not isinstance(fused, nn.Linear):
                 return False
-            perm = _qkv_perm(mt, cfg, s.num_heads, s.num_kv_heads, s.head_dim)
             w, b = fused.weight.data, fused.bias.data if fused.bias is not None else None
             if perm is not None:
                 idx = torch.tensor(perm, dtype=torch.long, device=w.device)

@@ -161,3 +161,41 @@ def test_from_gguf_keeps_kquant_blocks(tmp_path, qt):
         a = dense(ids).logits
         b = m(ids).logits.float()
     assert ((a - b).norm() / a.norm()).item() < 1e-3
+
+
+def _family(kind):
+    import transformers as T
+    if kind == "bloom":
+        return T.BloomConfig(vocab_size=256, hidden_size=256, n_layer=2, n_head=4)
+    if kind == "falcon":
+        return T.FalconConfig(vocab_size=256, hidden_size=256, num_hidden_layers=2, num_attention_heads=4)
+    if kind == "falcon_new":
+        return T.FalconConfig(vocab_size=256, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+                              num_kv_heads=2, new_decoder_architecture=True)
+    return T.MptConfig(vocab_size=256, d_model=256, n_layers=2, n_heads=4, max_seq_len=256)
+
+
+@pytest.mark.parametrize("kind", ["bloom", "falcon", "falcon_new", "mpt"])
+@pytest.mark.parametrize("qt", ["f16", "q4_k"])
+def test_gguf_family_round_trip(tmp_path, kind, qt):
+    """bloom / falcon / mpt through llama.cpp's tensor names and [q; k; v]
+    fused-QKV order (reference gguf/models/{bloom,falcon,mpt}.py), then the
+    native generic decoder (k-quant blocks kept for q4_k)"""
+    import transformers as T
+    from ipex_llm_amd.convert_model import export_gguf
+    from ipex_llm_amd.gguf.api import load_gguf_model
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    torch.manual_seed(0)
+    ref = T.AutoModelForCausalLM.from_config(_family(kind)).eval()
+    f = export_gguf(ref, str(tmp_path / f"{kind}-{qt}.gguf"), qt)
+    assert G.GGUFReader(f).architecture == ("falcon" if kind.startswith("falcon") else kind)
+    dense, _ = load_gguf_model(f, dtype=torch.float32)
+    ids = torch.randint(0, 256, (1, 9))
+    with torch.no_grad():
+        a, b = ref(ids).logits, dense(ids).logits
+    assert ((a - b).norm() / a.norm()).item() < (1e-3 if qt == "f16" else 0.15)
+    m, _ = AutoModelForCausalLM.from_gguf(f, low_bit="sym_int8", torch_dtype=torch.float32)
+    assert getattr(m, "_illm_native_attached", False)
+    with torch.no_grad():
+        c = m(ids).logits.float()
+    assert ((c - b).norm() / b.norm()).item() < 3e-2
