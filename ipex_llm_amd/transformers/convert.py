@@ -223,6 +223,7 @@ def _convert_one(module: nn.Linear, qtype: int, device, imatrix=None, mp_group=N
 
 
 _ROOT_CFG = [None]
+_MIXED_PLAN = [None]      # {module name: qtype name} of a saved mixed_fp4 / mixed_fp8 model
 
 
 def model_root_cfg():
@@ -254,6 +255,15 @@ def _replace_with_low_bit_linear(model: nn.Module, qtype: int, modules_to_not_co
             continue                                  # tiny gates stay dense
         if _is_linear(child):
             q = Q.mixed_kquant_qtype(qtype, full, _num_layers(model_root_cfg()))
+            if q in (Q.MOFQ4, Q.MOFQ8):
+                # per tensor; shape-only rebuilds (load_low_bit) follow the saved plan
+                plan = _MIXED_PLAN[0] or {}
+                if full in plan:
+                    q = Q.resolve_qtype(plan[full])
+                elif convert_shape_only or child.weight.device.type == "meta":
+                    q = Q.SYM_INT4 if q == Q.MOFQ4 else Q.SYM_INT8
+                else:
+                    q = _pick_tensor_format(child.weight, q)
             is_head = name == "lm_head" or full.endswith("lm_head")
             if is_head and mixed_precision and qtype in (Q.SYM_INT4, Q.ASYM_INT4, Q.WOQ_INT4, Q.NF4, Q.FP4):
                 q = Q.SYM_INT8
@@ -350,8 +360,6 @@ def ggml_convert_low_bit(model: nn.Module, qtype="sym_int4", optimize_model: boo
     modules_to_not_convert = list(modules_to_not_convert or [])
     if optimize_model:
         _optimize_pre(model, qtype)
-    if qtype in (Q.MOFQ4, Q.MOFQ8):
-        qtype = _pick_mixed_format(model, qtype)
     _ROOT_CFG[0] = getattr(model, "config", None)     # layer count for the gguf_q4k_s/m policies
     try:
         n = _replace_with_low_bit_linear(model, qtype, modules_to_not_convert, "", device, imatrix_data,
@@ -382,20 +390,19 @@ def _cast_non_linear(model, dtype):
                 p.data = p.data.to(dtype)
 
 
-def _pick_mixed_format(model, qtype):
-    """mixed_fp4 / mixed_fp8: choose per model the lower-MSE of (sym_int4, fp4)
-    or (sym_int8, fp8_e4m3) on a sample of linear weights (reference
-    low_bit_linear.py:373-408 does it per tensor)."""
+def _pick_tensor_format(w: torch.Tensor, qtype):
+    """mixed_fp4 / mixed_fp8: the lower-MSE of (sym_int4, fp4) or (sym_int8,
+    fp8_e4m3) for THIS tensor (reference low_bit_linear.py:370-408,
+    FP4Params.quantize)"""
     from .. import ops
     cands = (Q.SYM_INT4, Q.FP4) if qtype == Q.MOFQ4 else (Q.SYM_INT8, Q.FP8E4)
-    err = {c: 0.0 for c in cands}
-    lin = [m for m in model.modules() if isinstance(m, nn.Linear)][:8]
-    for m in lin:
-        w = m.weight.data.float().cpu()
-        if w.shape[1] % 64:
-            continue
-        for c in cands:
-            f = Q.get_format(c).fmt
-            dq = ops.dequantize(ops.quantize(w, f), f, w.shape[0], w.shape[1])
-            err[c] += (dq - w).pow(2).mean().item()
-    return min(cands, key=lambda c: err[c])
+    wf = w.detach().float().cpu()
+    if wf.dim() != 2 or wf.shape[1] % 64:
+        return cands[0]
+    best, best_err = cands[0], None
+    for c in cands:
+        f = Q.get_format(c).fmt
+        err = (ops.dequantize(ops.quantize(wf, f), f, wf.shape[0], wf.shape[1]) - wf).pow(2).mean().item()
+        if best_err is None or err < best_err:
+            best, best_err = c, err
+    return best

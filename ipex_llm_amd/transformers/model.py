@@ -102,6 +102,11 @@ def save_low_bit(self, save_dir: str, *args, **kwargs):
             "modules_to_not_convert": getattr(self, "_illm_skip", []),
             "mixed_precision": bool(getattr(self, "_illm_mixed", False)),
             "format": "ipex_llm_amd/canonical-planar-v1"}
+    if getattr(self, "_illm_qtype", None) in (Q.MOFQ4, Q.MOFQ8):
+        # mixed_fp4 / mixed_fp8 pick a format per tensor: record the plan
+        from .low_bit_linear import LowBitLinear
+        meta["module_qtypes"] = {n: Q.qtype_name(m.qtype) for n, m in self.named_modules()
+                                 if isinstance(m, LowBitLinear)}
     with open(os.path.join(save_dir, LOW_BIT_META), "w") as f:
         json.dump(meta, f, indent=2)
     gc = getattr(self, "generation_config", None)
@@ -261,9 +266,14 @@ class _BaseAutoModelClass:
             dt = getattr(torch, dt)
         with init_empty_weights():
             model = cls.HF_Model.from_config(config, torch_dtype=dt, trust_remote_code=trust)
-        ggml_convert_low_bit(model, qtype, flags.get("optimize_model", True), None,
-                             flags.get("modules_to_not_convert"), convert_shape_only=True,
-                             mixed_precision=flags.get("mixed_precision", False))
+        from . import convert as _cv
+        _cv._MIXED_PLAN[0] = flags.get("module_qtypes")
+        try:
+            ggml_convert_low_bit(model, qtype, flags.get("optimize_model", True), None,
+                                 flags.get("modules_to_not_convert"), convert_shape_only=True,
+                                 mixed_precision=flags.get("mixed_precision", False))
+        finally:
+            _cv._MIXED_PLAN[0] = None
         wfile = os.path.join(path, "model.safetensors")
         if ref_layout:
             # reference save_low_bit: ggml CPU-layout blocks, converted (never reinterpreted)

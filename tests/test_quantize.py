@@ -126,7 +126,7 @@ def test_attn_softmax_fully_masked_row_is_zero():
     assert torch.isfinite(x.float()).all()
 
 
-@pytest.mark.parametrize("mt", ["phi", "gpt_neox"])
+@pytest.mark.parametrize("mt", ["granite", "olmo"])   # (families still on the HF forward)
 def test_hf_eager_attention_uses_illm_softmax(mt, tmp_path, monkeypatch):
     """an eager-configured HF-forward family is routed through illm_eager
     (ops.attn_softmax_) and keeps the dense model's logits"""
@@ -209,3 +209,35 @@ print("ok", rel)
     env = dict(__import__("os").environ, ILLM_CPU_ISA=isa)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_mixed_fp4_picks_per_tensor_and_round_trips(tmp_path):
+    """mixed_fp4: lower-MSE of sym_int4 / fp4 chosen per tensor (reference
+    FP4Params.quantize), and the per-module plan survives save/load"""
+    from transformers import LlamaConfig, LlamaForCausalLM
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    torch.manual_seed(0)
+    cfg = LlamaConfig(vocab_size=256, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=2)
+    ref = LlamaForCausalLM(cfg).eval()
+    with torch.no_grad():       # heavy-tailed weights in layer 1 (fp4's log grid wins there)
+        for n, p_ in ref.named_parameters():
+            if "layers.1." in n and p_.dim() == 2:
+                p_.copy_(torch.distributions.StudentT(1.5).sample(p_.shape).clamp(-50, 50) * 0.01)
+    p = str(tmp_path / "m")
+    ref.save_pretrained(p)
+    m = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="mixed_fp4", torch_dtype=torch.float32).eval()
+    kinds = {mod.qtype for mod in m.modules() if isinstance(mod, LowBitLinear)}
+    assert kinds == {Q.SYM_INT4, Q.FP4}, kinds
+    ids = torch.randint(0, 256, (1, 8))
+    with torch.no_grad():
+        a = m(ids).logits
+    sd = str(tmp_path / "s")
+    m.save_low_bit(sd)
+    m2 = AutoModelForCausalLM.load_low_bit(sd, torch_dtype=torch.float32).eval()
+    k2 = {n: mod.qtype for n, mod in m2.named_modules() if isinstance(mod, LowBitLinear)}
+    k1 = {n: mod.qtype for n, mod in m.named_modules() if isinstance(mod, LowBitLinear)}
+    assert k1 == k2
+    with torch.no_grad():
+        assert torch.allclose(m2(ids).logits, a, atol=1e-5)
