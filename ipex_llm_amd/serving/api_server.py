@@ -164,6 +164,10 @@ def build_app(engine: LLMEngine, tokenizer, model_name: str = "ipex-llm-amd", lo
 
     @app.get("/health")
     async def health():
+        from fastapi.responses import JSONResponse
+        err = runner.error if runner is not None else None
+        if err is not None:           # the engine loop died (device fault / dead rank): not ready
+            return JSONResponse({"status": "error", "error": repr(err)}, status_code=503)
         return {"status": "ok", "running": int(engine.sched.num_running()), "waiting": int(engine.sched.num_waiting())}
 
     @app.get("/metrics")

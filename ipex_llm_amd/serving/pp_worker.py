@@ -93,6 +93,37 @@ class PPModelWorker:
         self._lock = threading.Lock()
         self._stopped = False
         self.stats = {"ticks": 0, "bubbles": 0, "prefill_tokens": 0, "decode_tokens": 0}
+        self.monitor = None                          # parallel.health.RankMonitor (rank 0)
+        self.heartbeat = None
+        self.failed: Optional[str] = None
+
+    def enable_failure_detection(self, timeout: float = 5.0, interval: float = 0.5):
+        """heartbeats on every rank, a monitor on rank 0 (parallel/health.py)"""
+        from ..parallel.health import Heartbeat, RankMonitor, default_store
+        store = default_store()
+        if store is None or self.world == 1:
+            return self
+        self.heartbeat = Heartbeat(store, self._g(self.rank), interval).start()
+        if self.is_head:
+            self.monitor = RankMonitor(store, [self._g(r) for r in range(1, self.world)], timeout,
+                                       poll=interval)
+        return self
+
+    def fail_all(self, reason: str):
+        """finish every in-flight request with an error (streams woken)"""
+        self.failed = reason
+        for sq in list(self.seqs.values()):
+            if not sq.done:
+                sq.done, sq.finish_reason = True, f"error: {reason}"
+                if self.is_head and sq.rid in self.streamer:
+                    self.streamer[sq.rid].put(-1)
+        while self.waiting:
+            rid = self.waiting.popleft()
+            sq = self.seqs.get(rid)
+            if sq is not None and not sq.done:
+                sq.done, sq.finish_reason = True, f"error: {reason}"
+                if rid in self.streamer:
+                    self.streamer[rid].put(-1)
 
     # ----------------------------------------------------------------- helpers
     @property
@@ -291,9 +322,26 @@ class PPModelWorker:
     # ----------------------------------------------------------------- drivers
     @torch.no_grad()
     def process_step(self) -> None:
-        """Rank 0: one pipeline tick (schedule, broadcast, execute)."""
-        ctrl = self._bcast(self._schedule(), 0)
-        self._tick(ctrl)
+        """Rank 0: one pipeline tick (schedule, broadcast, execute).  A dead
+        peer (heartbeat monitor) or a failed collective fails every in-flight
+        request and raises RankFailureError instead of blocking."""
+        from ..parallel.health import RankFailureError, abort_process_group
+        if self.failed:
+            raise RankFailureError(self.failed)
+        try:
+            if self.monitor is not None:
+                self.monitor.check()
+            ctrl = self._bcast(self._schedule(), 0)
+            self._tick(ctrl)
+        except RankFailureError as e:
+            abort_process_group(self.group)
+            self.fail_all(str(e))
+            raise
+        except RuntimeError as e:                   # collective error: a peer vanished mid-tick
+            if self.world == 1:
+                raise
+            self.fail_all(f"collective failed: {e}")
+            raise RankFailureError(self.failed) from e
 
     @torch.no_grad()
     def serve_forever(self) -> None:
@@ -313,17 +361,27 @@ class PPModelWorker:
         self._sends = []
 
     def stop(self) -> None:
-        if self.is_head and not self._stopped:
+        if self.heartbeat is not None:
+            self.heartbeat.stop()
+        if self.is_head and not self._stopped and not self.failed:
             self._stopped = True
             self._bcast({"stop": True}, 0)
             self._drain()
+
+    def health(self) -> dict:
+        """/health payload: ok, or the failure (dead ranks) that stopped serving"""
+        if self.failed:
+            return {"status": "error", "error": self.failed}
+        if self.monitor is not None and not self.monitor.healthy:
+            return {"status": "error", "error": self.monitor.reason}
+        return {"status": "ok", "ticks": self.stats["ticks"]}
 
     def generate(self, prompts, params: Optional[SamplingParams] = None) -> List[List[int]]:
         """Rank 0 offline batch: submit everything, tick until done; returns
         the generated tokens of each prompt."""
         rids = [self.add_request(p, params) for p in prompts]
         while any(r not in self.seqs or not self.seqs[r].done for r in rids):
-            self.process_step()
+            self.process_step()                     # (raises RankFailureError on a dead peer)
         out = [list(self.seqs[r].generated) for r in rids]
         for r in rids:
             self.seqs.pop(r, None)
@@ -366,8 +424,10 @@ class PPEngineLoop:
                     last = time.perf_counter()
                 else:
                     time.sleep(self.idle)
-        except BaseException as e:      # surfaced to the caller through .error
+        except BaseException as e:      # surfaced to the caller through .error / worker.health()
             self.error = e
+            if not self.worker.failed:
+                self.worker.fail_all(repr(e))
 
     def stop(self):
         self._stop.set()

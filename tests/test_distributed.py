@@ -223,3 +223,69 @@ def test_expert_parallel_matches_single(tmp_path):
     with torch.no_grad():
         logits = m(ids).logits.float()
     _run(_ep_worker, 2, p, {"ids": ids.tolist(), "logits": logits.tolist()})
+
+
+def _ppw_fail_worker(rank, world, port, path):
+    _init(rank, world, port)
+    import time
+    from ipex_llm_amd.parallel.health import RankFailureError
+    from ipex_llm_amd.serving.engine import SamplingParams
+    from ipex_llm_amd.serving.pp_worker import PPModelWorker
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    m = AutoModelForCausalLM.from_pretrained(path, load_in_low_bit="sym_int8", torch_dtype=torch.float32,
+                                             pipeline_parallel_stages=world)
+    w = PPModelWorker(m, max_num_seqs=2, max_model_len=128).enable_failure_detection(timeout=3.0, interval=0.2)
+    if rank == 1:
+        n = [0]
+        orig = w._tick
+
+        def dying_tick(ctrl):
+            n[0] += 1
+            if n[0] == 4:
+                os._exit(0)                      # the stage process vanishes mid-generation
+            return orig(ctrl)
+        w._tick = dying_tick
+        w.serve_forever()
+        os._exit(0)
+    t0 = time.time()
+    try:
+        w.generate([list(range(3, 20)), [5, 6, 7]], SamplingParams(max_new_tokens=60))
+        raise AssertionError("generation finished although stage 1 died")
+    except RankFailureError as e:
+        assert "rank" in str(e) or "collective" in str(e), e
+    assert time.time() - t0 < 60
+    assert all(sq.done and sq.finish_reason.startswith("error") for sq in w.seqs.values())
+    assert w.health()["status"] == "error"
+    os._exit(0)                                  # (no teardown collective with a dead peer)
+
+
+def test_pp_serving_detects_dead_rank(tmp_path):
+    """§5.3 failure detection: a pipeline stage dying mid-generation fails the
+    in-flight requests with an error on rank 0 (heartbeats + collective
+    error), instead of blocking until the process-group timeout"""
+    p = str(tmp_path / "m")
+    _tiny_llama(p)
+    _run(_ppw_fail_worker, 2, p)
+
+
+def test_rank_monitor_heartbeats(tmp_path):
+    import time
+    import torch.distributed as dist
+    from ipex_llm_amd.parallel.health import Heartbeat, RankFailureError, RankMonitor
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    hb = Heartbeat(store, 1, interval=0.05).start()
+    mon = RankMonitor(store, [1, 2], timeout=0.5, poll=0.0)
+    time.sleep(0.6)
+    assert mon.poll_now() == [2]                 # rank 2 never beat
+    mon.ranks = [1]
+    mon.check()                                  # rank 1 alive
+    hb._stop.set()                               # rank 1 freezes (no clean stop)
+    time.sleep(0.7)
+    try:
+        mon.check()
+        raise AssertionError("stale heartbeat not detected")
+    except RankFailureError as e:
+        assert "[1]" in str(e)
+    hb2 = Heartbeat(store, 3, interval=0.05).start()
+    hb2.stop()                                   # clean stop is not a failure
+    assert RankMonitor(store, [3], timeout=0.1, poll=0.0).poll_now() == []
