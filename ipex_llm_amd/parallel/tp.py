@@ -140,8 +140,11 @@ def auto_tp(model: nn.Module, group=None, rank: Optional[int] = None, world: Opt
             local = _slice_linear(head, 0, a, b)
             if b - a < per:                      # pad the last shard so all_gather sizes match
                 pad = nn.Linear(local.in_features, per, bias=False, device="meta", dtype=local.weight.dtype)
-                w = torch.zeros(per, local.in_features, dtype=local.weight.dtype)
-                w[:b - a] = local.weight.data
+                if local.weight.device.type == "meta":      # shape-only rebuild (load_low_bit of a TP save)
+                    w = torch.empty(per, local.in_features, dtype=local.weight.dtype, device="meta")
+                else:
+                    w = torch.zeros(per, local.in_features, dtype=local.weight.dtype)
+                    w[:b - a] = local.weight.data
                 pad.weight = nn.Parameter(w, requires_grad=False)
                 local = pad
             model.set_output_embeddings(VocabParallelHead(local, group, V))

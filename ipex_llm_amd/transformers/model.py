@@ -92,7 +92,17 @@ def save_low_bit(self, save_dir: str, *args, **kwargs):
         if key in seen and sd[k].numel() > 0:
             sd[k] = sd[k].clone()
         seen[key] = k
-    save_file(sd, os.path.join(save_dir, "model.safetensors"), metadata={"format": "pt"})
+    tp = getattr(self, "_tp", None)
+    if tp is not None and tp["world"] > 1:
+        # per-rank shard (reference: DeepSpeed AutoTP saves per rank); config + meta from rank 0
+        save_file(sd, os.path.join(save_dir, f"model-tp{tp['rank']:02d}-of-{tp['world']:02d}.safetensors"),
+                  metadata={"format": "pt"})
+        if tp["rank"] != 0:
+            import torch.distributed as dist
+            dist.barrier(group=tp["group"])
+            return
+    else:
+        save_file(sd, os.path.join(save_dir, "model.safetensors"), metadata={"format": "pt"})
     cfg = getattr(self, "config", None)
     if cfg is not None:
         cfg.bigdl_transformers_low_bit = Q.qtype_name(getattr(self, "_illm_qtype", Q.SYM_INT4))
@@ -102,6 +112,8 @@ def save_low_bit(self, save_dir: str, *args, **kwargs):
             "modules_to_not_convert": getattr(self, "_illm_skip", []),
             "mixed_precision": bool(getattr(self, "_illm_mixed", False)),
             "format": "ipex_llm_amd/canonical-planar-v1"}
+    if tp is not None and tp["world"] > 1:
+        meta["tensor_parallel"] = int(tp["world"])
     if getattr(self, "_illm_qtype", None) in (Q.MOFQ4, Q.MOFQ8):
         # mixed_fp4 / mixed_fp8 pick a format per tensor: record the plan
         from .low_bit_linear import LowBitLinear
@@ -115,6 +127,9 @@ def save_low_bit(self, save_dir: str, *args, **kwargs):
             gc.save_pretrained(save_dir)
         except Exception:  # pragma: no cover
             pass
+    if tp is not None and tp["world"] > 1:
+        import torch.distributed as dist
+        dist.barrier(group=tp["group"])
 
 
 def _attach(model, qtype, flags):
@@ -266,6 +281,20 @@ class _BaseAutoModelClass:
             dt = getattr(torch, dt)
         with init_empty_weights():
             model = cls.HF_Model.from_config(config, torch_dtype=dt, trust_remote_code=trust)
+        tp_world = int(flags.get("tensor_parallel", 1) or 1)
+        tp_group = kwargs.pop("tp_group", None)
+        want_tp = kwargs.pop("tensor_parallel", False) or tp_group is not None
+        if tp_world > 1:
+            # per-rank TP checkpoint: shard the empty module tree exactly like
+            # from_pretrained(tensor_parallel=True) did, then load this rank's file
+            from ..parallel.comm import get_rank, get_world_size
+            from ..parallel.tp import auto_tp
+            if get_world_size(tp_group) != tp_world:
+                raise ValueError(f"load_low_bit: checkpoint was saved with tensor_parallel={tp_world}, "
+                                 f"running with {get_world_size(tp_group)} ranks")
+            auto_tp(model, tp_group)
+        elif want_tp:
+            raise ValueError("load_low_bit: tensor_parallel needs a checkpoint saved under tensor parallelism")
         from . import convert as _cv
         _cv._MIXED_PLAN[0] = flags.get("module_qtypes")
         try:
@@ -275,6 +304,8 @@ class _BaseAutoModelClass:
         finally:
             _cv._MIXED_PLAN[0] = None
         wfile = os.path.join(path, "model.safetensors")
+        if tp_world > 1:
+            wfile = os.path.join(path, f"model-tp{get_rank(tp_group):02d}-of-{tp_world:02d}.safetensors")
         if ref_layout:
             # reference save_low_bit: ggml CPU-layout blocks, converted (never reinterpreted)
             from .ref_checkpoint import convert_reference_state_dict, load_reference_state_dict
@@ -298,6 +329,9 @@ class _BaseAutoModelClass:
         if still_meta:
             raise RuntimeError(f"load_low_bit: parameters left uninitialised: {still_meta[:5]}")
         _attach(model, qtype, flags)
+        if tp_world > 1 and getattr(model, "_tp", None) is not None:
+            from ..parallel.comm import setup_custom_all_reduce
+            setup_custom_all_reduce(model._tp["group"])
         from .convert import _optimize_post
         if flags.get("optimize_model", True):
             _optimize_post(model)

@@ -289,3 +289,33 @@ def test_rank_monitor_heartbeats(tmp_path):
     hb2 = Heartbeat(store, 3, interval=0.05).start()
     hb2.stop()                                   # clean stop is not a failure
     assert RankMonitor(store, [3], timeout=0.1, poll=0.0).poll_now() == []
+
+
+def _tp_save_worker(rank, world, port, path, out_dir):
+    _init(rank, world, port)
+    import torch.distributed as dist
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    ids = torch.randint(0, 320, (1, 9), generator=torch.Generator().manual_seed(1))
+    m = AutoModelForCausalLM.from_pretrained(path, load_in_low_bit="sym_int4", torch_dtype=torch.float32,
+                                             tensor_parallel=True)
+    with torch.no_grad():
+        a = m(ids).logits
+    m.save_low_bit(out_dir)
+    assert os.path.exists(os.path.join(out_dir, f"model-tp{rank:02d}-of-{world:02d}.safetensors"))
+    m2 = AutoModelForCausalLM.load_low_bit(out_dir, torch_dtype=torch.float32, tensor_parallel=True)
+    assert m2._tp["world"] == world and m2._tp["rank"] == rank
+    with torch.no_grad():
+        b = m2(ids).logits
+    assert torch.allclose(a, b, atol=1e-5), (a - b).abs().max()
+    dist.destroy_process_group()
+
+
+def test_tp_per_rank_save_and_load(tmp_path):
+    """§5.4: a tensor-parallel model saves one shard per rank and loads back
+    on the same world size without re-sharding the dense checkpoint"""
+    p = str(tmp_path / "m")
+    _tiny_llama(p)
+    _run(_tp_save_worker, 2, p, str(tmp_path / "tp_saved"))
+    import json
+    meta = json.load(open(tmp_path / "tp_saved" / "illm_low_bit.json"))
+    assert meta["tensor_parallel"] == 2

@@ -80,16 +80,20 @@ def test_llama_api_native(llama_dir):
     assert llm.n_vocab() == 320 and llm.n_ctx() == 128
 
 
-def test_llama_api_hf_fallback(tmp_path):
+@pytest.mark.parametrize("native", [False, True])
+def test_llama_api_hf_fallback(tmp_path, native):
+    """gpt2 runs on the native generic decoder; a variant it does not cover
+    (scale_attn_by_inverse_layer_idx) keeps the HF forward + its KV cache"""
     from transformers import GPT2Config, GPT2LMHeadModel
     from ipex_llm_amd.ggml import AutoModelForCausalLM as GgmlAuto
     p = str(tmp_path / "gpt2")
     torch.manual_seed(0)
     GPT2LMHeadModel(GPT2Config(n_embd=64, n_layer=2, n_head=4, vocab_size=320, n_positions=128,
-                               eos_token_id=2, bos_token_id=1)).save_pretrained(p)
+                               eos_token_id=2, bos_token_id=1,
+                               scale_attn_by_inverse_layer_idx=not native)).save_pretrained(p)
     _tokenizer().save_pretrained(p)
     llm = GgmlAuto.from_pretrained(p, model_family="starcoder", n_ctx=64, low_bit="sym_int8", device="cpu")
-    assert llm.ctx._eng is None                           # HF forward + its KV cache
+    assert (llm.ctx._eng is not None) == native
     toks = llm.tokenize("w5 w6 w7")
     with torch.no_grad():
         hf = llm.model.generate(torch.tensor([toks]), max_new_tokens=6, do_sample=False, eos_token_id=None,

@@ -24,6 +24,7 @@ def timeit(fn, iters=20):
 
 
 def main():
+    ops.require()                       # load the extension (torch.ops.ipex_llm_amd.*)
     dev = torch.device("cuda")
     shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
     for M in (1024, 2048, 4096, 8192):
