@@ -1,0 +1,89 @@
+// Skinny GEMM (M <= 16 rows) over dense bf16 / fp16 weights: the decode
+// projections of fp16 / bf16 models (FP16Linear / BF16Linear of the
+// reference, SRC/transformers/low_bit_linear.py:758-948, whose XPU decode
+// runs ESIMD skinny kernels) and the verify forward of self-speculative
+// decoding (k + 1 rows).
+//
+// Pure weight streaming: W [N, K] is read exactly once.  A workgroup of 4
+// waves owns 4 consecutive rows (one per wave); a lane loads 2 x 16 B of its
+// row per step (2 loads in flight per lane, 2 KB per wave-step) and
+// multiplies them against every activation row (L1/L2 resident); the row
+// sums are wave reductions.  The bias is added in the epilogue.
+#include <hip/hip_runtime.h>
+
+#include "illm_device.h"
+#include "kernels.h"
+
+namespace illm {
+
+template <typename T>
+__device__ __forceinline__ float dot8(const uint4& w, const uint4& x) {
+  const uint32_t ws[4] = {w.x, w.y, w.z, w.w}, xs[4] = {x.x, x.y, x.z, x.w};
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    s += to_f32<T>(ws[i] & 0xffff) * to_f32<T>(xs[i] & 0xffff) + to_f32<T>(ws[i] >> 16) * to_f32<T>(xs[i] >> 16);
+  return s;
+}
+
+template <typename T, int MM>
+__global__ void __launch_bounds__(256) dense_gemv_kernel(const uint16_t* __restrict__ x, int M, int64_t K,
+                                                         const uint16_t* __restrict__ w, int64_t N,
+                                                         const uint16_t* __restrict__ bias,
+                                                         uint16_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const uint16_t* wr = w + n * K;
+  float acc[MM];
+#pragma unroll
+  for (int m = 0; m < MM; m++) acc[m] = 0.f;
+  int64_t k = (int64_t)lane * 8;
+  // main loop: two 16-B weight loads per lane in flight
+  for (; k + 64 * 8 < K; k += 2 * 64 * 8) {
+    const uint4 w0 = *(const uint4*)(wr + k);
+    const uint4 w1 = *(const uint4*)(wr + k + 64 * 8);
+#pragma unroll
+    for (int m = 0; m < MM; m++) {
+      if (m < M) {
+        const uint16_t* xr = x + (int64_t)m * K;
+        acc[m] += dot8<T>(w0, *(const uint4*)(xr + k)) + dot8<T>(w1, *(const uint4*)(xr + k + 64 * 8));
+      }
+    }
+  }
+  for (; k < K; k += 64 * 8) {
+    const uint4 w0 = *(const uint4*)(wr + k);
+#pragma unroll
+    for (int m = 0; m < MM; m++)
+      if (m < M) acc[m] += dot8<T>(w0, *(const uint4*)(x + (int64_t)m * K + k));
+  }
+  const float b = bias != nullptr ? to_f32<T>(bias[n]) : 0.f;
+#pragma unroll
+  for (int m = 0; m < MM; m++) {
+    if (m < M) {
+      const float s = wave_sum(acc[m]);
+      if (lane == 0) out[(int64_t)m * N + n] = from_f32<T>(s + b);
+    }
+  }
+}
+
+template <typename T>
+static void dg_t(const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t N, const uint16_t* bias,
+                 uint16_t* out, hipStream_t st) {
+  const dim3 grid((unsigned)((N + 3) / 4));
+#define DG(MMV) hipLaunchKernelGGL((dense_gemv_kernel<T, MMV>), grid, dim3(256), 0, st, x, M, K, w, N, bias, out)
+  if (M <= 1) DG(1);
+  else if (M <= 2) DG(2);
+  else if (M <= 4) DG(4);
+  else if (M <= 8) DG(8);
+  else DG(16);
+#undef DG
+}
+
+void launch_dense_gemv(bool bf16, const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t N,
+                       const uint16_t* bias, uint16_t* out, hipStream_t st) {
+  if (bf16) dg_t<BF16>(x, M, K, w, N, bias, out, st);
+  else dg_t<F16>(x, M, K, w, N, bias, out, st);
+}
+
+}  // namespace illm

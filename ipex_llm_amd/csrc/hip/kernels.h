@@ -63,6 +63,10 @@ void launch_kq_dequant(int fmt, bool bf16, const uint8_t* w, int64_t n, int64_t 
 void launch_kq_gemv(int fmt, bool bf16, const uint16_t* x, int M, int64_t K, const uint8_t* w, int64_t N,
                     uint16_t* out, hipStream_t st);
 
+// ---- dense bf16/f16 skinny GEMM (dense_gemv.hip): M <= 16, K % 8 == 0 ----
+void launch_dense_gemv(bool bf16, const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t N,
+                       const uint16_t* bias, uint16_t* out, hipStream_t st);
+
 // ---- fp8 linear (fp8_gemm.hip): torch_fp8 qtypes on the f8f6f4 MFMA --------
 struct Fp8GemmArgs {
   const uint8_t* xq;       // [M, K] e4m3 activations (GEMM)

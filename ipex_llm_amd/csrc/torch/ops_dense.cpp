@@ -1,0 +1,53 @@
+// dense_linear(x, w, bias?): decode-size (<= 16 rows) projections over dense
+// bf16 / fp16 weights on the streaming skinny-GEMM kernel (dense_gemv.hip);
+// larger M and the host go to the library GEMM.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+#include "../hip/kernels.h"
+
+using at::Tensor;
+
+namespace {
+
+Tensor dense_linear_cpu(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias) {
+  return at::linear(x, w.to(x.scalar_type()), bias.has_value() && bias->defined()
+                                                  ? c10::optional<Tensor>(bias->to(x.scalar_type())) : c10::nullopt);
+}
+
+Tensor dense_linear_hip(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias) {
+  c10::DeviceGuard g(x.device());
+  const int64_t K = x.size(-1), N = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K, "dense_linear: w must be [N, K]");
+  const int64_t M = x.numel() / K;
+  const bool ok = (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) &&
+                  w.scalar_type() == x.scalar_type() && K % 8 == 0 && M <= 16 && w.is_contiguous();
+  if (!ok) return dense_linear_cpu(x, w, bias);        // at::linear on the device (hipBLASLt)
+  Tensor xc = x.contiguous();
+  Tensor b;
+  if (bias.has_value() && bias->defined()) b = bias->to(x.scalar_type()).contiguous();
+  auto shape = x.sizes().vec();
+  shape.back() = N;
+  Tensor y = at::empty(shape, xc.options());
+  if (M > 0)
+    illm::launch_dense_gemv(x.scalar_type() == at::kBFloat16, (const uint16_t*)xc.data_ptr(), (int)M, K,
+                            (const uint16_t*)w.data_ptr(), N, b.defined() ? (const uint16_t*)b.data_ptr() : nullptr,
+                            (uint16_t*)y.data_ptr(), at::hip::getCurrentHIPStream().stream());
+  return y;
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
+  m.def("dense_linear(Tensor x, Tensor w, Tensor? bias) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
+  m.impl("dense_linear", &dense_linear_cpu);
+}
+
+TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
+  m.impl("dense_linear", &dense_linear_hip);
+}

@@ -7,9 +7,9 @@ threshold reads the draft probability) and again for acceptance.
 
 MI355X design: the whole iteration lives on the device and is captured once:
 
-    draft   k + 1 single-token forwards of the INT4 model (feeding ``last``,
-            d1 .. dk; the extra step leaves the draft cache valid through
-            d_k so a fully accepted round needs no catch-up forward)
+    draft   k forwards of the INT4 model: [token at p - 1, last], then
+            d1 .. d(k-1) -- re-feeding position p - 1 writes d_k's KV when
+            the previous round accepted everything, so no catch-up forward
     verify  one target forward over [last, d1 .. dk] (k + 1 query rows:
             skinny GEMV projections, flash-decoding / prefill attention
             reading the paged cache, device-side slots)
@@ -56,6 +56,9 @@ class GraphSpeculator:
         self.warm = set()
         self.p = torch.zeros(1, dtype=torch.long, device=dev)          # position of `last`
         self.last = torch.zeros(1, dtype=torch.long, device=dev)
+        self.prev = torch.zeros(1, dtype=torch.long, device=dev)      # token at position p - 1
+        self.ar1 = torch.arange(2, device=dev)
+        self.one = torch.ones(1, dtype=torch.long, device=dev)
         self.n_out = torch.zeros((), dtype=torch.long, device=dev)
         self.n_match = torch.zeros((), dtype=torch.long, device=dev)
         self.rounds = 0
@@ -69,15 +72,23 @@ class GraphSpeculator:
     def _iter(self, k: int):
         bs_t, bs_d = self.te.cache.bs, self.de.cache.bs
         ar = self.ars[k]
-        tok = self.last
-        drafts = []
-        for j in range(k + 1):
+        # draft step 0 feeds [token at p - 1, last]: re-writing p - 1 is a no-op
+        # unless the previous round accepted every draft (then d_k's KV was
+        # never written) -- so k draft forwards suffice, no catch-up step
+        ids0 = torch.cat([self.prev, self.last])
+        pos0 = self.p - 1 + self.ar1
+        meta = AttnMeta(1, 2, self.bt_d, (self.p + 1).to(torch.int32), self.ns)
+        lg = self.dm.forward_tokens(ids0, pos0, self._slots(self.bt_d, pos0, bs_d), meta, self.de.cache,
+                                    logits_idx=self.one)
+        tok = torch.argmax(lg, dim=-1)
+        drafts = [tok]
+        for j in range(1, k):
             pos = self.p + j
             meta = AttnMeta(1, 1, self.bt_d, (pos + 1).to(torch.int32), self.ns)
             lg = self.dm.forward_tokens(tok, pos, self._slots(self.bt_d, pos, bs_d), meta, self.de.cache)
             tok = torch.argmax(lg, dim=-1)
             drafts.append(tok)
-        d = torch.cat(drafts[:k])                                    # d1 .. dk
+        d = torch.cat(drafts)                                         # d1 .. dk
         ids = torch.cat([self.last, d])
         pos = self.p + ar
         meta = AttnMeta(1, k + 1, self.bt_t, (self.p + k + 1).to(torch.int32), self.ns)
@@ -88,6 +99,7 @@ class GraphSpeculator:
         self.n_out.add_(m + 1)
         self.n_match.add_(m)
         self.p.add_(m + 1)
+        self.prev.copy_(ids.gather(0, m.view(1)))                    # token now at p - 1
         self.last.copy_(pred.gather(0, m.view(1)))
 
     @torch.no_grad()
@@ -115,6 +127,7 @@ class GraphSpeculator:
         first = torch.argmax(te.forward_chunk(st, p, 0)[-1])
         de.forward_chunk(sd, p, 0)
         self.p.fill_(len(p))
+        self.prev.fill_(p[-1])
         self.last.copy_(first.view(1))
         self.n_out.zero_()
         self.n_match.zero_()

@@ -208,3 +208,8 @@ def _(x):
 @register_fake("ipex_llm_amd::fp8_linear")
 def _(x, w, w_scale, bias, e5m2):
     return x.new_empty(*x.shape[:-1], w.shape[0])
+
+
+@register_fake("ipex_llm_amd::dense_linear")
+def _(x, w, bias):
+    return x.new_empty(*x.shape[:-1], w.shape[0])

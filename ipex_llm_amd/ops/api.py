@@ -15,7 +15,7 @@ from . import reference as R
 
 __all__ = [
     "quantize", "dequantize", "kq_quantize", "kq_dequantize", "kq_linear", "fp8_linear", "fp8_act_quant",
-    "fp8_quantize_weight", "repack_to_device", "repack_from_device", "lowbit_matmul",
+    "fp8_quantize_weight", "dense_linear", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemm", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
@@ -87,6 +87,15 @@ def kq_linear(x: torch.Tensor, blob: torch.Tensor, fmt: int, n: int, k: int) -> 
     if x.is_cuda and not _native(x):
         return F.linear(x, kq_dequantize(blob, fmt, n, k, torch.float32).to(x.dtype))
     return _ops().kq_linear(x, blob, fmt, n, k)
+
+
+# ------------------------------------------------------------ dense skinny GEMM
+def dense_linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x @ w^T (+ bias) for dense bf16/fp16 weights: the streaming skinny
+    kernel for <= 16 rows on the GPU, the library GEMM otherwise"""
+    if x.is_cuda and _native(x) and x.numel() // x.shape[-1] <= 16:
+        return _ops().dense_linear(x, w, bias)
+    return F.linear(x, w, bias)
 
 
 # ------------------------------------------------------------ torch_fp8

@@ -246,7 +246,13 @@ class DenseLinear(nn.Module):
         return m
 
     def forward(self, x):
-        y = F.linear(x.to(self.weight.dtype), self.weight, None if self.mp_group else self.bias)
+        xx = x.to(self.weight.dtype)
+        b = None if self.mp_group else self.bias
+        if xx.is_cuda and xx.numel() // xx.shape[-1] <= 16 and \
+                not (torch.is_grad_enabled() and (xx.requires_grad or self.weight.requires_grad)):
+            y = ops.dense_linear(xx, self.weight, b)          # decode: streaming skinny kernel
+        else:
+            y = F.linear(xx, self.weight, b)
         if self.mp_group is not None:
             from ..parallel.comm import all_reduce_inplace
             y = all_reduce_inplace(y, self.mp_group)

@@ -1,0 +1,33 @@
+"""Dense bf16 / fp16 skinny GEMM (csrc/hip/dense_gemv.hip) vs an fp32
+PyTorch reference, and DenseLinear routing decode rows through it."""
+import pytest
+import torch
+
+from ipex_llm_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M", [1, 2, 3, 5, 8, 13, 16])
+@pytest.mark.parametrize("N,K", [(300, 1024), (4096, 4104), (64, 520)])
+def test_dense_gemv_matches_fp32(dt, M, N, K):
+    torch.manual_seed(M * 7 + N)
+    w = (torch.randn(N, K) * 0.05).to(dt)
+    x = torch.randn(M, K).to(dt)
+    b = torch.randn(N).to(dt)
+    want = x.float() @ w.float().t() + b.float()
+    got = torch.ops.ipex_llm_amd.dense_linear(x.cuda(), w.cuda(), b.cuda()).float().cpu()
+    rel = ((got - want).norm() / want.norm()).item()
+    assert rel < 1e-2, rel
+
+
+def test_dense_linear_module_uses_kernel():
+    from ipex_llm_amd.transformers.low_bit_linear import DenseLinear
+    lin = torch.nn.Linear(512, 384)
+    m = DenseLinear.from_linear(lin, torch.bfloat16, torch.device("cuda"))
+    x = torch.randn(3, 512, device="cuda", dtype=torch.bfloat16)
+    with torch.no_grad():
+        got = m(x).float()
+    want = torch.nn.functional.linear(x.float(), m.weight.float(), m.bias.float())
+    assert ((got - want).norm() / want.norm()).item() < 1e-2
