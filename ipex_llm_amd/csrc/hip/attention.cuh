@@ -81,6 +81,10 @@ __global__ void __launch_bounds__(64) attn_decode_kernel(const AttnDecodeArgs a)
   __syncthreads();
 
   const int blk = a.block_tables[(size_t)b * a.max_blocks + k0 / a.bs];
+  if (bad_block(blk, a.num_blocks)) {
+    if (lane == 0) kerr(a.err, ERR_BLOCK_ID);
+    return;
+  }
   const size_t base = (((size_t)blk * a.Hkv + kvh) * a.bs + (k0 % a.bs)) * D;
   const uint8_t* kb = a.k_cache + base * EB;
   const uint8_t* vb = a.v_cache + base * EB;
@@ -293,6 +297,10 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   const int colk = (a.Hq + kvh) * D, colv = (a.Hq + a.Hkv + kvh) * D;
 
   const int blk = a.block_tables[(size_t)b * a.max_blocks + k0 / a.bs];
+  if (bad_block(blk, a.num_blocks)) {                // wave-uniform: the whole split leaves
+    if (threadIdx.x == 0) kerr(a.err, ERR_BLOCK_ID);
+    return;
+  }
   const size_t base = (((size_t)blk * a.Hkv + kvh) * a.bs + (k0 % a.bs)) * D;
   const uint8_t* kb = a.k_cache + base * EB;
   const uint8_t* vb = a.v_cache + base * EB;
@@ -406,7 +414,9 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
       const int kn = nk - 1, pos = len - 1;
       const int nb = a.block_tables[(size_t)b * a.max_blocks + pos / a.bs];
       const size_t crow = (((size_t)nb * a.Hkv + kvh) * a.bs + (size_t)(pos % a.bs)) * D;
-      if (r16 == (kn & 15)) {
+      if (bad_block(nb, a.num_blocks)) {
+        if (threadIdx.x == 0) kerr(a.err, ERR_BLOCK_ID);
+      } else if (r16 == (kn & 15)) {
         uint4 kq[KSTEP];
         lane_rot(colk, 1.f, kq);
 #pragma unroll
@@ -441,7 +451,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
 #pragma unroll
           for (int j = 0; j < VU; j++)
             if (j == kn / KPJ) vm[j] = vq;
-          *(uint4*)((uint16_t*)a.v_cache + crow + d0) = vq;
+          if (!bad_block(nb, a.num_blocks)) *(uint4*)((uint16_t*)a.v_cache + crow + d0) = vq;
         }
       } else if constexpr (DPL >= 8) {
         if (kg == (kn & 3)) {
@@ -469,7 +479,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
 #pragma unroll
             for (int i = 0; i < 16; i++)
               if (i == (kn >> 2)) vf[i][c] = vq;
-            *(uint4*)((uint16_t*)a.v_cache + crow + d0) = vq;
+            if (!bad_block(nb, a.num_blocks)) *(uint4*)((uint16_t*)a.v_cache + crow + d0) = vq;
           }
         }
       }

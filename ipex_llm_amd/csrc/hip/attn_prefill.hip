@@ -110,7 +110,11 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const AttnPrefillArgs
   // staging: unit u = tid + 256 j covers key u / (D / 8), chunk u % (D / 8)
   auto tile_src = [&](int t, const uint8_t* cache) -> const uint8_t* {
     const int k0 = kbeg + t * PF_KT;
-    const int blk = a.block_tables[(size_t)b * a.max_blocks + k0 / a.bs];
+    int blk = a.block_tables[(size_t)b * a.max_blocks + k0 / a.bs];
+    if (bad_block(blk, a.num_blocks)) {                  // read block 0 instead, report
+      kerr(a.err, ERR_BLOCK_ID);
+      blk = 0;
+    }
     return cache + (((size_t)blk * a.Hkv + kvh) * a.bs + (k0 % a.bs)) * D * EB;
   };
   uint4 kreg[UPT], vreg[UPT];

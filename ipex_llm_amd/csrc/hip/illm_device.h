@@ -94,6 +94,19 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Kernel error word (SURVEY §5.2 bounds checks): a kernel that finds an
+// out-of-range index from device data (block table entry, cache slot, expert
+// id) skips the access and ORs a code here; the host reads it with
+// ops.check_kernel_errors() (ILLM_CHECK_KERNELS=1: after every engine step).
+// The bad access never happens, so a corrupt table is an error, not a fault.
+enum KernelErr : int { ERR_BLOCK_ID = 1, ERR_SLOT = 2, ERR_EXPERT = 4, ERR_SEQ_LEN = 8 };
+__device__ __forceinline__ void kerr(int* err, int code) {
+  if (err != nullptr) atomicOr(err, code);
+}
+__device__ __forceinline__ bool bad_block(int blk, int num_blocks) {
+  return num_blocks > 0 && (unsigned)blk >= (unsigned)num_blocks;
+}
+
 // wave-level reductions (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

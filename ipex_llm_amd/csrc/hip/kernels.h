@@ -134,6 +134,8 @@ struct RopeKVArgs {
   const int32_t* block_tables;
   int max_blocks, tq;
   const int64_t* pos_offset;   // [B] (cache index = pos - offset) or null
+  int num_blocks;              // cache blocks (bounds check of slots / block ids)
+  int* err;                    // kernel error word (illm_device.h kerr) or null
 };
 void launch_rope_kv(bool bf16, const RopeKVArgs& a, hipStream_t st);
 
@@ -166,6 +168,8 @@ struct AttnDecodeArgs {
   const int64_t* rq_pos;    // [B] rotary positions
   int rq_ld, rq_rot, rq_interleaved;
   float rq_qscale;
+  int num_blocks;           // cache blocks: block-table entries are bounds-checked
+  int* err;                 // kernel error word or null
 };
 void launch_attn_decode(bool bf16, const AttnDecodeArgs& a, hipStream_t st);
 
@@ -182,6 +186,8 @@ struct AttnPrefillArgs {
   int sliding_window;
   int kv_fp8;                   // 0 = 16-bit cache, 1 = e5m2, 2 = e4m3
   float k_scale, v_scale;
+  int num_blocks;
+  int* err;
 };
 void launch_attn_prefill(bool bf16, const AttnPrefillArgs& a, hipStream_t st);
 

@@ -96,7 +96,9 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
       const int64_t pp = a.pos[t] - (a.pos_offset ? a.pos_offset[t / a.tq] : 0);
       slot = (int64_t)a.block_tables[(size_t)(t / a.tq) * a.max_blocks + pp / a.bs] * a.bs + pp % a.bs;
     }
-    if (slot < 0) {   // padding token: nothing to write, but keep the accumulator zeroed
+    const bool oob = a.num_blocks > 0 && slot >= (int64_t)a.num_blocks * a.bs;
+    if (oob && lane == 0) kerr(a.err, ERR_SLOT);
+    if (slot < 0 || oob) {   // padding token (or a bad slot): nothing to write, keep the accumulator zeroed
       if (a.part && a.zero_part)
         for (int d = lane; d < D; d += 64) ((float*)a.part)[(size_t)t * a.ld_qkv + col0 + d] = 0.f;
       return;
@@ -185,7 +187,9 @@ __global__ void __launch_bounds__(256) rope_kv_vec_kernel(const RopeKVArgs a) {
       const int64_t pp = a.pos[t] - (a.pos_offset ? a.pos_offset[t / a.tq] : 0);
       slot = (int64_t)a.block_tables[(size_t)(t / a.tq) * a.max_blocks + pp / a.bs] * a.bs + pp % a.bs;
     }
-    if (slot < 0) {                                    // padding token: nothing to write
+    const bool oob = a.num_blocks > 0 && slot >= (int64_t)a.num_blocks * a.bs;
+    if (oob) kerr(a.err, ERR_SLOT);
+    if (slot < 0 || oob) {                             // padding token (or a bad slot): nothing to write
       if (a.part && a.zero_part) {
         float* pp = (float*)a.part + (size_t)t * a.ld_qkv + (size_t)h * D;
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);

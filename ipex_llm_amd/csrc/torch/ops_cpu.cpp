@@ -131,6 +131,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("gemv(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias, int epi, int ksplit, int act) -> Tensor");
   m.def("add_rms_norm(Tensor? x, Tensor(b!)? partials, Tensor(a!)? residual, Tensor w, float eps, bool unit_offset, bool store_residual, bool zero_partials=False) -> Tensor");
   m.def("layer_norm(Tensor x, Tensor? w, Tensor? b, float eps) -> Tensor");
+  m.def("kernel_errors(Tensor like, bool reset) -> Tensor");
   m.def("rope_kv(Tensor qkv, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slots, Tensor pos, Tensor inv_freq, Tensor? q_norm, Tensor? k_norm, float norm_eps, float q_scale, int Hq, int Hkv, int D, int rot_dim, bool interleaved, int kv_fp8, float k_scale, float v_scale) -> ()");
   m.def("attn_decode(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int kv_fp8, float k_scale, float v_scale, Tensor? alibi) -> Tensor");
   m.def("glu(Tensor gu, int act, int tile=0) -> Tensor");
@@ -161,7 +162,12 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("moe_route(Tensor x, Tensor router, int k, bool renorm, int scoring, int e0, int num_local, Tensor(a!) counter) -> (Tensor, Tensor, Tensor, Tensor)");
 }
 
+at::Tensor kernel_errors_cpu(const at::Tensor& like, bool reset) {
+  return at::zeros({4}, like.options().dtype(at::kInt));     // host kernels check shapes up front
+}
+
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
+  m.impl("kernel_errors", &kernel_errors_cpu);
   m.impl("quantize_cpu", &quantize_cpu);
   m.impl("dequantize_cpu", &dequantize_cpu);
   m.impl("repack_to_device", &repack_to_device);

@@ -6,6 +6,8 @@
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
+#include <map>
+
 #include "../common/formats.h"
 #include "../hip/kernels.h"
 #include "../hip/gemv_args.h"
@@ -13,6 +15,8 @@
 using at::Tensor;
 
 namespace {
+
+int* kernel_err(const c10::Device& dev);       // per-device kernel error word (defined below)
 
 // decode combine scratch: the wide combine holds up to 4096 split weights in
 // LDS (attention.cuh CW_MAXS), the one-wave combine 1024 (used for D % 4 != 0)
@@ -651,6 +655,8 @@ void rope_kv(const Tensor& qkv, Tensor& q_out, Tensor& k_cache, Tensor& v_cache,
   a.kv_fp8 = (int)kv_fp8;
   a.k_scale = (float)k_scale;
   a.v_scale = (float)v_scale;
+  a.num_blocks = (int)k_cache.size(0);
+  a.err = kernel_err(qkv.device());
   if (T > 0) illm::launch_rope_kv(bf16, a, cur_stream());
 }
 
@@ -670,6 +676,26 @@ static bool fused_combine_on() {
     return e != nullptr && atoi(e) != 0;
   }();
   return on;
+}
+
+// Per-device kernel error word (illm_device.h kerr): allocated on first use
+// (outside graph capture, like the combine counters), read and reset by the
+// kernel_errors op (ops.check_kernel_errors).
+static at::Tensor& kernel_err_buf(const c10::Device& dev) {
+  static std::map<int, at::Tensor> bufs;
+  auto it = bufs.find(dev.index());
+  if (it == bufs.end())
+    it = bufs.emplace(dev.index(), at::zeros({4}, at::TensorOptions().dtype(at::kInt).device(dev))).first;
+  return it->second;
+}
+int* kernel_err(const c10::Device& dev) { return kernel_err_buf(dev).data_ptr<int>(); }
+
+Tensor kernel_errors(const Tensor& like, bool reset) {
+  c10::DeviceGuard g(like.device());
+  at::Tensor& b = kernel_err_buf(like.device());
+  Tensor out = b.clone();
+  if (reset) b.zero_();
+  return out;
 }
 
 int* attn_counters(const c10::Device& dev, int64_t n) {
@@ -728,6 +754,8 @@ void rope_kv_fused(const Tensor& part, const c10::optional<Tensor>& bias, Tensor
   a.kv_fp8 = (int)kv_fp8;
   a.k_scale = (float)k_scale;
   a.v_scale = (float)v_scale;
+  a.num_blocks = (int)k_cache.size(0);
+  a.err = kernel_err(part.device());
   if (a.T > 0) illm::launch_rope_kv(bf16, a, cur_stream());
 }
 
@@ -754,6 +782,8 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, cons
   a.block_tables = block_tables.data_ptr<int32_t>();
   a.seq_lens = seq_lens.data_ptr<int32_t>();
   a.max_blocks = (int)block_tables.size(1);
+  a.num_blocks = (int)k_cache.size(0);
+  a.err = kernel_err(k_cache.device());
   a.part_o = po.data_ptr<float>();
   a.part_ml = pml.data_ptr<float>();
   a.out = m16(out);
@@ -814,6 +844,8 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
   a.block_tables = block_tables.data_ptr<int32_t>();
   a.seq_lens = seq_lens.data_ptr<int32_t>();
   a.max_blocks = (int)block_tables.size(1);
+  a.num_blocks = (int)k_cache.size(0);
+  a.err = kernel_err(k_cache.device());
   a.part_o = po.data_ptr<float>();
   a.part_ml = pml.data_ptr<float>();
   a.out = m16(out);
@@ -911,6 +943,8 @@ Tensor attn_prefill(const Tensor& q, const Tensor& k_cache, const Tensor& v_cach
   a.D = (int)D;
   a.bs = (int)bs;
   a.max_blocks = (int)block_tables.size(1);
+  a.num_blocks = (int)k_cache.size(0);
+  a.err = kernel_err(k_cache.device());
   a.scale = (float)scale;
   a.softcap = (float)softcap;
   a.sliding_window = (int)window;
@@ -1307,6 +1341,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv_attn", &gemv_attn);
   m.impl("add_rms_norm", &add_rms_norm);
   m.impl("layer_norm", &layer_norm);
+  m.impl("kernel_errors", &kernel_errors);
   m.impl("rope_kv", &rope_kv);
   m.impl("attn_decode", &attn_decode);
   m.impl("glu", &glu);

@@ -128,6 +128,9 @@ class DecodeStep:
                 self.graph.replay()
             else:
                 self._body()
+        from .. import ops
+        if ops.api.CHECK_KERNELS and self.native_glue:
+            ops.check_kernel_errors(self.ids.device)          # debug: surface skipped bad indices
         return self.next_ids
 
 

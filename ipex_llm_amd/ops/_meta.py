@@ -213,3 +213,8 @@ def _(x, w, w_scale, bias, e5m2):
 @register_fake("ipex_llm_amd::dense_linear")
 def _(x, w, bias):
     return x.new_empty(*x.shape[:-1], w.shape[0])
+
+
+@register_fake("ipex_llm_amd::kernel_errors")
+def _(like, reset):
+    return like.new_empty(4, dtype=torch.int32)

@@ -15,7 +15,7 @@ from . import reference as R
 
 __all__ = [
     "quantize", "dequantize", "kq_quantize", "kq_dequantize", "kq_linear", "fp8_linear", "fp8_act_quant",
-    "fp8_quantize_weight", "dense_linear", "repack_to_device", "repack_from_device", "lowbit_matmul",
+    "fp8_quantize_weight", "dense_linear", "check_kernel_errors", "KernelError", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
     "moe_align", "moe_gemm", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
@@ -87,6 +87,36 @@ def kq_linear(x: torch.Tensor, blob: torch.Tensor, fmt: int, n: int, k: int) -> 
     if x.is_cuda and not _native(x):
         return F.linear(x, kq_dequantize(blob, fmt, n, k, torch.float32).to(x.dtype))
     return _ops().kq_linear(x, blob, fmt, n, k)
+
+
+# ------------------------------------------------------------ kernel error word
+class KernelError(RuntimeError):
+    pass
+
+
+_KERR_NAMES = {1: "block-table entry outside the KV cache", 2: "cache slot outside the KV cache",
+               4: "expert id out of range", 8: "sequence length out of range"}
+
+
+def check_kernel_errors(device=None, reset: bool = True):
+    """Raise KernelError if a HIP kernel skipped an out-of-range index since
+    the last check (device-side bounds checks).  Synchronises.
+    ILLM_CHECK_KERNELS=1 makes the engines call this after every step."""
+    if device is None:
+        if not torch.cuda.is_available():
+            return 0
+        device = torch.device("cuda", torch.cuda.current_device())
+    like = torch.empty(0, device=device)
+    if like.is_cuda and not _native(like):
+        return 0
+    code = int(_ops().kernel_errors(like, reset)[0])
+    if code:
+        what = [v for k, v in _KERR_NAMES.items() if code & k]
+        raise KernelError(f"HIP kernel bounds check failed (code {code}): {', '.join(what)}")
+    return 0
+
+
+CHECK_KERNELS = __import__("os").environ.get("ILLM_CHECK_KERNELS", "0") == "1"
 
 
 # ------------------------------------------------------------ dense skinny GEMM

@@ -1,14 +1,24 @@
-"""Structured (JSON) output as a logits processor.
+"""Structured (JSON / JSON-schema) output as a logits processor.
 
 Reference: ``SRC/transformers/xgrammar.py`` (wraps the ``xgrammar`` package:
 ``create_json_logits_processor(tokenizer, vocab_size, schema)`` /
-``reset_json_logits_processor``).  ``xgrammar`` is not available in this
-image, so the processor is native: an incremental JSON pushdown recognizer
-over the decoded text; each step the highest-scoring candidates (top
-``max_candidates``) are checked in order and every token that would make the
-output an invalid JSON prefix is masked.  ``schema`` only constrains the
-top-level type (object/array); full JSON-schema validation is parity
-unpinned.
+``reset_json_logits_processor``; xgrammar compiles the schema to a grammar
+and masks tokens with a bitmask every step).  ``xgrammar`` is not available
+in this image, so the processor is native:
+
+* no schema: an incremental JSON pushdown recognizer (any JSON value);
+* a JSON schema: compiled to a regular expression over the output text
+  (objects with declared properties in declared order, required / optional
+  properties, arrays with min/maxItems, string length / pattern, enum,
+  const, integer / number / boolean / null, anyOf / oneOf, type lists,
+  local ``$ref``), matched incrementally with partial matching
+  (``regex.fullmatch(..., partial=True)``): a token is allowed iff the
+  output extended by it can still complete to a schema-valid document, EOS
+  iff the document is complete.
+
+Each step the highest-scoring candidates are checked first and the search
+widens until at least one token passes.  Parity with xgrammar's exact
+whitespace rules is unpinned (here: at most one space between tokens).
 """
 from __future__ import annotations
 
@@ -146,14 +156,141 @@ def _num_prefix(s: str) -> bool:
         return False
 
 
+# ----------------------------------------------------------------- schema -> regex
+_WSP = r" ?"
+_STR_CHAR = r'(?:[^"\\\x00-\x1f]|\\["\\/bfnrt]|\\u[0-9a-fA-F]{4})'
+_INT = r"-?(?:0|[1-9][0-9]{0,15})"
+_NUM = _INT + r"(?:\.[0-9]{1,16})?(?:[eE][+-]?[0-9]{1,3})?"
+
+
+def _lit(v) -> str:
+    import json
+    import regex
+    return regex.escape(json.dumps(v, separators=(", ", ": ")))
+
+
+def _generic(depth: int) -> str:
+    """any JSON value, nesting limited to ``depth`` (regular)"""
+    scalar = "(?:" + "|".join(['"' + _STR_CHAR + '*"', _NUM, "true", "false", "null"]) + ")"
+    if depth <= 0:
+        return scalar
+    inner = _generic(depth - 1)
+    obj = r"\{" + _WSP + "(?:" + '"' + _STR_CHAR + '*"' + _WSP + ":" + _WSP + inner + "(?:" + _WSP + "," + _WSP + \
+        '"' + _STR_CHAR + '*"' + _WSP + ":" + _WSP + inner + ")*)?" + _WSP + r"\}"
+    arr = r"\[" + _WSP + "(?:" + inner + "(?:" + _WSP + "," + _WSP + inner + ")*)?" + _WSP + r"\]"
+    return "(?:" + "|".join([scalar, obj, arr]) + ")"
+
+
+def schema_to_regex(schema, root=None, depth: int = 0) -> str:
+    """JSON schema -> regular expression of its valid documents (compact:
+    at most one space around ``:`` / ``,`` / brackets)"""
+    import regex
+    root = schema if root is None else root
+    if depth > 24:
+        raise ValueError("JSON schema nests too deeply (recursive $ref?)")
+    if schema is True or schema == {}:
+        return _generic(3)
+    if "$ref" in schema:
+        ref = schema["$ref"]
+        if not ref.startswith("#/"):
+            raise ValueError(f"only local $ref is supported, got {ref}")
+        node = root
+        for part in ref[2:].split("/"):
+            node = node[part]
+        return schema_to_regex(node, root, depth + 1)
+    if "const" in schema:
+        return _lit(schema["const"])
+    if "enum" in schema:
+        return "(?:" + "|".join(_lit(v) for v in schema["enum"]) + ")"
+    for key in ("anyOf", "oneOf"):
+        if key in schema:
+            return "(?:" + "|".join(schema_to_regex(s, root, depth + 1) for s in schema[key]) + ")"
+    if "allOf" in schema and len(schema["allOf"]) == 1:
+        return schema_to_regex(schema["allOf"][0], root, depth + 1)
+    t = schema.get("type")
+    if isinstance(t, list):
+        return "(?:" + "|".join(schema_to_regex({**schema, "type": x}, root, depth + 1) for x in t) + ")"
+    if t == "object" or (t is None and "properties" in schema):
+        props = schema.get("properties", {})
+        if not props:
+            return _generic(3) if t is None else r"\{" + _WSP + "(?:" + '"' + _STR_CHAR + '*"' + _WSP + ":" + \
+                _WSP + _generic(2) + "(?:" + _WSP + "," + _WSP + '"' + _STR_CHAR + '*"' + _WSP + ":" + _WSP + \
+                _generic(2) + ")*)?" + _WSP + r"\}"
+        req = set(schema.get("required", []))
+        names = list(props)
+        items = [regex.escape('"' + n + '"') + _WSP + ":" + _WSP + schema_to_regex(props[n], root, depth + 1)
+                 for n in names]
+        sep = _WSP + "," + _WSP
+        alts = []
+        for f in range(len(names)):
+            if any(n in req for n in names[:f]):
+                break                            # a required property cannot be skipped
+            pat = items[f]
+            for j in range(f + 1, len(names)):
+                pat += (sep + items[j]) if names[j] in req else "(?:" + sep + items[j] + ")?"
+            alts.append(pat)
+        body = "(?:" + "|".join(alts) + ")"
+        if not req:
+            body += "?"
+        return r"\{" + _WSP + body + _WSP + r"\}"
+    if t == "array":
+        item = schema_to_regex(schema.get("items", {}), root, depth + 1)
+        lo, hi = int(schema.get("minItems", 0)), schema.get("maxItems")
+        sep = _WSP + "," + _WSP
+        if hi is not None and int(hi) == 0:
+            return r"\[" + _WSP + r"\]"
+        rest = "{%d,%s}" % (max(lo - 1, 0), "" if hi is None else int(hi) - 1)
+        body = item + "(?:" + sep + item + ")" + rest
+        if lo == 0:
+            body = "(?:" + body + ")?"
+        return r"\[" + _WSP + body + _WSP + r"\]"
+    if t == "string":
+        if "pattern" in schema:
+            p = schema["pattern"]
+            p = p[1:] if p.startswith("^") else p
+            p = p[:-1] if p.endswith("$") else p
+            return '"' + "(?:" + p + ")" + '"'
+        lo, hi = int(schema.get("minLength", 0)), schema.get("maxLength")
+        return '"' + _STR_CHAR + "{%d,%s}" % (lo, "" if hi is None else int(hi)) + '"'
+    if t == "integer":
+        return _INT
+    if t == "number":
+        return _NUM
+    if t == "boolean":
+        return "(?:true|false)"
+    if t == "null":
+        return "null"
+    return _generic(3)
+
+
+class _RegexState:
+    """incremental matcher over the decoded output (prefix check = partial match)"""
+
+    def __init__(self, pattern):
+        self.pat = pattern
+
+    def viable(self, text: str) -> bool:
+        return self.pat.fullmatch(text, partial=True) is not None
+
+    def complete(self, text: str) -> bool:
+        return self.pat.fullmatch(text) is not None
+
+
 class JsonLogitsProcessor:
     def __init__(self, tokenizer, vocab_size: int, schema=None, max_candidates: int = 64):
         self.tok, self.V = tokenizer, vocab_size
+        if isinstance(schema, str):
+            import json
+            schema = json.loads(schema)
         self.top = (schema or {}).get("type") if isinstance(schema, dict) else None
         self.max_candidates = max_candidates
         self.schema = schema
         self.prompt_len: Optional[int] = None
         self.states: List[_JsonState] = []
+        self.rx = None
+        if isinstance(schema, dict) and schema:
+            import regex
+            self.rx = _RegexState(regex.compile(schema_to_regex(schema)))
 
     def _state_for(self, b: int, gen: List[int]) -> _JsonState:
         st = _JsonState(self.top)
@@ -161,11 +298,35 @@ class JsonLogitsProcessor:
             st.feed(ch)
         return st
 
+    def _allowed_schema(self, gen: List[int], row: torch.Tensor, eos) -> List[int]:
+        text = self.tok.decode(gen, skip_special_tokens=True)
+        order = torch.argsort(row, descending=True).tolist()
+        allowed, lo = [], 0
+        width = self.max_candidates
+        while not allowed and lo < len(order):
+            for t in order[lo:lo + width]:
+                if t == eos:
+                    if self.rx.complete(text):
+                        allowed.append(t)
+                    continue
+                ext = self.tok.decode(gen + [t], skip_special_tokens=True)
+                if ext != text and self.rx.viable(ext):
+                    allowed.append(t)
+            lo += width
+            width *= 4                                  # widen until some token fits
+        return allowed
+
     def __call__(self, input_ids: torch.Tensor, scores: torch.Tensor) -> torch.Tensor:
         if self.prompt_len is None:
             self.prompt_len = input_ids.shape[1]
         out = torch.full_like(scores, float("-inf"))
         eos = getattr(self.tok, "eos_token_id", None)
+        if self.rx is not None:
+            for b in range(scores.shape[0]):
+                gen = input_ids[b, self.prompt_len:].tolist()
+                allowed = self._allowed_schema(gen, scores[b], eos) or ([eos] if eos is not None else [])
+                out[b, allowed] = scores[b, allowed]
+            return out
         for b in range(scores.shape[0]):
             gen = input_ids[b, self.prompt_len:].tolist()
             st = self._state_for(b, gen)

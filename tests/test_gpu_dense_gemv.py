@@ -12,6 +12,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("M", [1, 2, 3, 5, 8, 13, 16])
 @pytest.mark.parametrize("N,K", [(300, 1024), (4096, 4104), (64, 520)])
 def test_dense_gemv_matches_fp32(dt, M, N, K):
+    ops.require()
     torch.manual_seed(M * 7 + N)
     w = (torch.randn(N, K) * 0.05).to(dt)
     x = torch.randn(M, K).to(dt)

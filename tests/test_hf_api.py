@@ -89,3 +89,45 @@ def test_remote_code_flash_attn_import_filter(tmp_path):
     assert "flash_attn" not in patch_flash_attn_import(str(f))
     with remote_code_patches():
         assert "flash_attn" not in dmu.get_imports(str(f)) and "einops" in dmu.get_imports(str(f))
+
+
+class _CharTok:
+    """character-level tokenizer (ids = printable chars + EOS) for the schema tests"""
+    chars = [chr(c) for c in range(32, 127)]
+
+    def __init__(self):
+        self.eos_token_id = len(self.chars)
+
+    def decode(self, ids, skip_special_tokens=True):
+        return "".join(self.chars[i] for i in ids if i < len(self.chars))
+
+
+def test_json_schema_logits_processor_enforces_schema():
+    """schema-constrained decoding (reference xgrammar.create_json_logits_processor
+    with a JSON schema): random logits, every finished document is valid"""
+    import json
+    from ipex_llm_amd.transformers.xgrammar import create_json_logits_processor
+    schema = {"type": "object",
+              "properties": {"name": {"type": "string", "maxLength": 6}, "age": {"type": "integer"},
+                             "kind": {"enum": ["cat", "dog"]},
+                             "tags": {"type": "array", "items": {"type": "boolean"}, "maxItems": 2}},
+              "required": ["name", "age", "kind"]}
+    tok = _CharTok()
+    V = tok.eos_token_id + 1
+    for seed in range(4):
+        g = torch.Generator().manual_seed(seed)
+        proc = create_json_logits_processor(tok, V, schema)
+        ids = torch.tensor([[0, 1]])                     # "prompt"
+        for _ in range(200):
+            scores = torch.randn(1, V, generator=g)
+            scores[0, tok.eos_token_id] -= 2.0
+            nxt = int(torch.argmax(proc(ids, scores)[0]))
+            ids = torch.cat([ids, torch.tensor([[nxt]])], 1)
+            if nxt == tok.eos_token_id:
+                break
+        text = tok.decode(ids[0, 2:].tolist())
+        assert ids[0, -1].item() == tok.eos_token_id, text
+        doc = json.loads(text)
+        assert set(doc) >= {"name", "age", "kind"} and doc["kind"] in ("cat", "dog"), doc
+        assert isinstance(doc["age"], int) and len(doc["name"]) <= 6
+        assert all(isinstance(x, bool) for x in doc.get("tags", []))
