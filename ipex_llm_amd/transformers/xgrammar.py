@@ -175,9 +175,9 @@ def _generic(depth: int) -> str:
     if depth <= 0:
         return scalar
     inner = _generic(depth - 1)
-    obj = r"\{" + _WSP + "(?:" + '"' + _STR_CHAR + '*"' + _WSP + ":" + _WSP + inner + "(?:" + _WSP + "," + _WSP + \
+    obj = r"\{(?:" + _WSP + '"' + _STR_CHAR + '*"' + _WSP + ":" + _WSP + inner + "(?:" + _WSP + "," + _WSP + \
         '"' + _STR_CHAR + '*"' + _WSP + ":" + _WSP + inner + ")*)?" + _WSP + r"\}"
-    arr = r"\[" + _WSP + "(?:" + inner + "(?:" + _WSP + "," + _WSP + inner + ")*)?" + _WSP + r"\]"
+    arr = r"\[(?:" + _WSP + inner + "(?:" + _WSP + "," + _WSP + inner + ")*)?" + _WSP + r"\]"
     return "(?:" + "|".join([scalar, obj, arr]) + ")"
 
 
@@ -213,7 +213,7 @@ def schema_to_regex(schema, root=None, depth: int = 0) -> str:
     if t == "object" or (t is None and "properties" in schema):
         props = schema.get("properties", {})
         if not props:
-            return _generic(3) if t is None else r"\{" + _WSP + "(?:" + '"' + _STR_CHAR + '*"' + _WSP + ":" + \
+            return _generic(3) if t is None else r"\{(?:" + _WSP + '"' + _STR_CHAR + '*"' + _WSP + ":" + \
                 _WSP + _generic(2) + "(?:" + _WSP + "," + _WSP + '"' + _STR_CHAR + '*"' + _WSP + ":" + _WSP + \
                 _generic(2) + ")*)?" + _WSP + r"\}"
         req = set(schema.get("required", []))
@@ -229,10 +229,10 @@ def schema_to_regex(schema, root=None, depth: int = 0) -> str:
             for j in range(f + 1, len(names)):
                 pat += (sep + items[j]) if names[j] in req else "(?:" + sep + items[j] + ")?"
             alts.append(pat)
-        body = "(?:" + "|".join(alts) + ")"
+        body = "(?:" + _WSP + "(?:" + "|".join(alts) + "))"
         if not req:
             body += "?"
-        return r"\{" + _WSP + body + _WSP + r"\}"
+        return r"\{" + body + _WSP + r"\}"
     if t == "array":
         item = schema_to_regex(schema.get("items", {}), root, depth + 1)
         lo, hi = int(schema.get("minItems", 0)), schema.get("maxItems")
@@ -240,10 +240,10 @@ def schema_to_regex(schema, root=None, depth: int = 0) -> str:
         if hi is not None and int(hi) == 0:
             return r"\[" + _WSP + r"\]"
         rest = "{%d,%s}" % (max(lo - 1, 0), "" if hi is None else int(hi) - 1)
-        body = item + "(?:" + sep + item + ")" + rest
+        body = "(?:" + _WSP + item + "(?:" + sep + item + ")" + rest + ")"
         if lo == 0:
-            body = "(?:" + body + ")?"
-        return r"\[" + _WSP + body + _WSP + r"\]"
+            body += "?"
+        return r"\[" + body + _WSP + r"\]"
     if t == "string":
         if "pattern" in schema:
             p = schema["pattern"]
