@@ -6,8 +6,12 @@ binaries; ``llm-convert`` CLI).  MI355X version, no external binaries:
   * ``outtype`` = any low-bit qtype name (``"int4"`` = sym_int4, ``"nf4"``,
     ``"fp8"`` ...) -> a ``save_low_bit`` directory (safetensors, portable
     canonical layout) loadable with ``AutoModelForCausalLM.load_low_bit``;
-  * ``outtype`` = ``"gguf_f16" | "gguf_q8_0" | "gguf_q4_0" | "gguf_f32"`` -> a
-    GGUF file (llama-layout families) readable by ``from_gguf`` and llama.cpp.
+  * ``outtype`` = ``"gguf_f16" | "gguf_q8_0" | "gguf_q4_0" | "gguf_f32"`` or
+    the k-quants ``"gguf_q4_k" | "gguf_q5_k" | "gguf_q6_k" | "gguf_q2_k" |
+    "gguf_q4_k_m" | "gguf_q4_k_s"`` -> a GGUF file readable by ``from_gguf``
+    and llama.cpp, for the llama-layout families and bloom / falcon / mpt
+    (the reference's per-family ``.bin`` conversions: llama, bloom, gptneox,
+    starcoder; k-quant blocks are the device layout of ``KQuantLinear``).
 """
 from __future__ import annotations
 
@@ -26,6 +30,8 @@ def llm_convert(model: str, outfile: str, outtype: str = "int4", model_family: s
     outtype = outtype.lower()
     if outtype.startswith("gguf"):
         return export_gguf(model, outfile, outtype.split("_", 1)[1] if "_" in outtype else "f16")
+    if outtype in ("q4_k", "q5_k", "q6_k", "q2_k", "q4_k_m", "q4_k_s") and str(outfile).endswith(".gguf"):
+        return export_gguf(model, outfile, outtype)
     from .transformers import AutoModelForCausalLM
     qtype = _OUT_ALIASES.get(outtype, outtype)
     m = AutoModelForCausalLM.from_pretrained(model, load_in_low_bit=qtype,

@@ -199,3 +199,22 @@ def test_gguf_family_round_trip(tmp_path, kind, qt):
     with torch.no_grad():
         c = m(ids).logits.float()
     assert ((c - b).norm() / b.norm()).item() < 3e-2
+
+
+def test_llm_convert_family_kquant(tmp_path):
+    """llm_convert of a non-llama family (bloom) straight to a q4_k_m GGUF"""
+    import transformers as T
+    from ipex_llm_amd.convert_model import llm_convert
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    torch.manual_seed(0)
+    ref = T.AutoModelForCausalLM.from_config(T.BloomConfig(vocab_size=256, hidden_size=256, n_layer=2,
+                                                            n_head=4)).eval()
+    p = str(tmp_path / "hf")
+    ref.save_pretrained(p)
+    f = llm_convert(p, str(tmp_path / "b.gguf"), "gguf_q4_k_m", model_family="bloom")
+    assert G.GGUFReader(f).architecture == "bloom"
+    m, _ = AutoModelForCausalLM.from_gguf(f, torch_dtype=torch.float32)
+    ids = torch.randint(0, 256, (1, 8))
+    with torch.no_grad():
+        a, b = ref(ids).logits, m(ids).logits.float()
+    assert ((a - b).norm() / a.norm()).item() < 0.15
