@@ -303,6 +303,13 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
     from .mla import MLA_ARCHS, mla_from_hf
     if getattr(cfg, "model_type", None) in MLA_ARCHS:
         return mla_from_hf(hf_model, dtype)
+    from .vl import VL_ARCHS, vl_native
+    if getattr(cfg, "model_type", None) in VL_ARCHS:
+        nm = vl_native(hf_model)
+        if nm is not None:
+            rp = getattr(cfg.text_config, "rope_parameters", None) or getattr(cfg.text_config, "rope_scaling", {})
+            nm._mrope_section = list(rp.get("mrope_section", []))
+        return nm
     spec = spec_from_config(cfg)
     tp = getattr(hf_model, "_tp", None)
     if tp is not None:                      # tensor-parallel shard: local heads

@@ -142,6 +142,11 @@ def _optimize_pre(model: nn.Module, qtype: int):
     if mt in MLA_ARCHS:
         model._illm_pre = True          # MLA: weights used as converted (kv_b absorbed at attach)
         return model
+    from ..models.vl import VL_ARCHS, vl_pre
+    if mt in VL_ARCHS:
+        vl_pre(model)
+        model._illm_pre = True
+        return model
     if mt not in NATIVE_ARCHS and mt not in MOE_ARCHS:
         return model
     base = getattr(model, "model", None)
@@ -332,6 +337,9 @@ def _optimize_post(model: nn.Module):
         patch_rwkv5(model)
     from ..models.generic import GENERIC_ARCHS
     from ..models.mla import MLA_ARCHS
+    from ..models.vl import VL_ARCHS, attach_vl
+    if mt in VL_ARCHS and getattr(model, "_illm_pre", False):
+        return attach_vl(model)
     if (mt in NATIVE_ARCHS or mt in MOE_ARCHS or mt in GENERIC_ARCHS or mt in MLA_ARCHS) and \
             getattr(model, "_illm_pre", False):
         from .hf_native import attach_native

@@ -256,3 +256,72 @@ def test_mla_native_matches_hf(kind, tmp_path):
     with torch.no_grad():
         lg = ref(g[:, :-1]).logits
     assert (lg[0, 5:].argmax(-1) == g[0, 6:]).float().mean() >= 0.8
+
+
+def _qwen2vl(tmp_path):
+    vc = dict(depth=1, embed_dim=64, hidden_size=128, num_heads=4, in_channels=3, patch_size=4, spatial_merge_size=2,
+              temporal_patch_size=2, mlp_ratio=2)
+    tc = dict(vocab_size=V, hidden_size=H, intermediate_size=256, num_hidden_layers=L, num_attention_heads=NH,
+              num_key_value_heads=2, max_position_embeddings=512,
+              rope_parameters={"rope_type": "default", "rope_theta": 10000.0, "mrope_section": [4, 6, 6]})
+    cfg = T.Qwen2VLConfig(vision_config=vc, text_config=tc, image_token_id=250, video_token_id=251,
+                          vision_start_token_id=252, vision_end_token_id=253)
+    torch.manual_seed(0)
+    m = T.Qwen2VLForConditionalGeneration(cfg).eval()
+    p = str(tmp_path / "qwen2vl")
+    m.save_pretrained(p)
+    ids = torch.tensor([[5, 6, 252] + [250] * 4 + [253, 7, 8, 9]])
+    pix = torch.randn(16, 3 * 2 * 4 * 4)
+    thw = torch.tensor([[1, 4, 4]])
+    return m, p, ids, pix, thw
+
+
+def test_qwen2_vl_native_mrope_matches_hf(tmp_path):
+    """Qwen2-VL: HF vision tower + native language model with M-RoPE rows;
+    prompt logits match HF, and decoding continues at cache_len + rope_delta"""
+    from ipex_llm_amd.transformers import AutoModelForVision2Seq
+    ref, p, ids, pix, thw = _qwen2vl(tmp_path)
+    mm = (ids == 250).int()
+    with torch.no_grad():
+        want = ref(input_ids=ids, pixel_values=pix, image_grid_thw=thw, mm_token_type_ids=mm).logits.float()
+    m = AutoModelForVision2Seq.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32).eval()
+    assert getattr(m, "_illm_native_attached", False)
+    got = m.vl_forward(input_ids=ids, pixel_values=pix, image_grid_thw=thw, mm_token_type_ids=mm).logits.float()
+    rel = ((got - want).norm() / want.norm()).item()
+    assert rel < 3e-2, rel
+    out = m.generate(input_ids=ids, pixel_values=pix, image_grid_thw=thw, mm_token_type_ids=mm, max_new_tokens=6)
+    # each generated token is the argmax of the HF model over the growing sequence
+    seq = out[0].tolist()
+    for t in range(ids.shape[1], len(seq)):
+        x = torch.tensor([seq[:t]])
+        with torch.no_grad():
+            lg = ref(input_ids=x, pixel_values=pix, image_grid_thw=thw,
+                     mm_token_type_ids=(x == 250).int()).logits[0, -1]
+        top2 = lg.topk(2).values
+        assert seq[t] == int(lg.argmax()) or (top2[0] - top2[1]).abs() < 1e-2, t
+    # text-only prompts: plain native generate (M-RoPE == RoPE)
+    txt = torch.tensor([[5, 6, 7, 8]])
+    assert m.generate(txt, max_new_tokens=3).shape == (1, 7)
+
+
+def test_qwen2_5_vl_native_matches_hf(tmp_path):
+    from ipex_llm_amd.transformers import AutoModelForVision2Seq
+    vc = dict(depth=2, hidden_size=64, intermediate_size=128, num_heads=4, in_channels=3, patch_size=4,
+              spatial_merge_size=2, temporal_patch_size=2, window_size=16, out_hidden_size=H,
+              fullatt_block_indexes=[1])
+    tc = dict(vocab_size=V, hidden_size=H, intermediate_size=256, num_hidden_layers=L, num_attention_heads=NH,
+              num_key_value_heads=2, max_position_embeddings=512,
+              rope_parameters={"rope_type": "default", "rope_theta": 10000.0, "mrope_section": [4, 6, 6]})
+    cfg = T.Qwen2_5_VLConfig(vision_config=vc, text_config=tc, image_token_id=250, video_token_id=251,
+                             vision_start_token_id=252, vision_end_token_id=253)
+    torch.manual_seed(0)
+    ref = T.Qwen2_5_VLForConditionalGeneration(cfg).eval()
+    p = str(tmp_path / "q25vl")
+    ref.save_pretrained(p)
+    ids = torch.tensor([[5, 6, 252] + [250] * 4 + [253, 7, 8, 9]])
+    pix, thw, mm = torch.randn(16, 3 * 2 * 4 * 4), torch.tensor([[1, 4, 4]]), (ids == 250).int()
+    with torch.no_grad():
+        want = ref(input_ids=ids, pixel_values=pix, image_grid_thw=thw, mm_token_type_ids=mm).logits.float()
+    m = AutoModelForVision2Seq.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32).eval()
+    got = m.vl_forward(input_ids=ids, pixel_values=pix, image_grid_thw=thw, mm_token_type_ids=mm).logits.float()
+    assert ((got - want).norm() / want.norm()).item() < 3e-2

@@ -99,3 +99,35 @@ def test_mla_deepseek_v3_gpu(tmp_path):
         g = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=True)
         e = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=False)
     assert torch.equal(g.cpu(), e.cpu())
+
+
+def test_qwen2_vl_gpu(tmp_path):
+    """Qwen2-VL on the GPU: native language model (bf16, head_dim 64) with
+    M-RoPE rows for the image prompt, hipGraph decode at cache_len + delta"""
+    from ipex_llm_amd.transformers import AutoModelForVision2Seq
+    vc = dict(depth=1, embed_dim=64, hidden_size=256, num_heads=4, in_channels=3, patch_size=4, spatial_merge_size=2,
+              temporal_patch_size=2, mlp_ratio=2)
+    tc = dict(vocab_size=V, hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+              num_key_value_heads=2, max_position_embeddings=1024,
+              rope_parameters={"rope_type": "default", "rope_theta": 10000.0, "mrope_section": [8, 12, 12]})
+    cfg = T.Qwen2VLConfig(vision_config=vc, text_config=tc, image_token_id=500, video_token_id=501,
+                          vision_start_token_id=502, vision_end_token_id=503)
+    torch.manual_seed(0)
+    ref = T.Qwen2VLForConditionalGeneration(cfg).eval()
+    path = str(tmp_path / "qvl")
+    ref.save_pretrained(path)
+    ids = torch.tensor([[5, 6, 502] + [500] * 16 + [503] + list(range(10, 40))])
+    pix, thw = torch.randn(64, 3 * 2 * 4 * 4), torch.tensor([[1, 8, 8]])
+    mm = (ids == 500).int()
+    with torch.no_grad():
+        want = ref(input_ids=ids, pixel_values=pix, image_grid_thw=thw, mm_token_type_ids=mm).logits.float()
+    m = AutoModelForVision2Seq.from_pretrained(path, load_in_low_bit="sym_int8", torch_dtype=torch.bfloat16)
+    m = m.to("cuda").eval()
+    got = m.vl_forward(input_ids=ids.cuda(), pixel_values=pix.cuda(), image_grid_thw=thw.cuda(),
+                       mm_token_type_ids=mm.cuda()).logits.float().cpu()
+    assert ((got - want).norm() / want.norm()).item() < 5e-2
+    g = m.generate(input_ids=ids.cuda(), pixel_values=pix.cuda(), image_grid_thw=thw.cuda(), mm_token_type_ids=mm.cuda(),
+                   max_new_tokens=8, use_graph=True)
+    e = m.generate(input_ids=ids.cuda(), pixel_values=pix.cuda(), image_grid_thw=thw.cuda(), mm_token_type_ids=mm.cuda(),
+                   max_new_tokens=8, use_graph=False)
+    assert torch.equal(g.cpu(), e.cpu())
