@@ -1,7 +1,5 @@
 """Library-GEMM formulations for the prefill projections (M = 1024-8192,
-Llama-3-8B shapes, bf16): y = x W^T as F.linear, as (W x^T)^T, and as a
-K-split batched GEMM (bmm over S K-slices + sum) -- the N = 4096 / 6144
-shapes leave hipBLASLt's 256 x 256 tiles with fewer tiles than CUs.  Also
+Llama-3-8B shapes, bf16): y = x W^T as F.linear, as (W x^T)^T,   Also
 the dequantize-to-bf16 cost of each weight (sym_int4).  JSON lines."""
 import json
 import sys
@@ -38,11 +36,8 @@ def main():
             rec = {"M": M, "proj": name, "N": N, "K": K}
             rec["linear_us"] = round(timeit(lambda: torch.nn.functional.linear(x, w)), 1)
             rec["wxT_us"] = round(timeit(lambda: torch.mm(w, x.t()).t()), 1)
-            for S in (2, 4):
-                if K % S == 0:
-                    xs = x.view(M, S, K // S).transpose(0, 1)            # [S, M, K/S]
-                    ws = w.view(N, S, K // S).transpose(0, 1)            # [S, N, K/S]
-                    rec[f"splitk{S}_us"] = round(timeit(lambda: torch.bmm(xs, ws.transpose(1, 2)).sum(0)), 1)
+            # (a strided-batched bmm over overlapping K-slice views of x / W faulted the
+            # library GEMM on MI355X -- illegal address at N = 4096; K splits are not tried)
             blob = torch.ops.ipex_llm_amd.quantize_device(w, fmt, False) if hasattr(torch.ops.ipex_llm_amd,
                                                                                      "quantize_device") else None
             if blob is not None:
