@@ -275,6 +275,9 @@ struct AdamWArgs {
   int chunk;                   // elements per chunk
   float lr, beta1, beta2, eps, weight_decay, bias_corr1, bias_corr2, grad_scale;
   int param_dtype, grad_dtype; // 0 = f32, 1 = bf16
+  // capturable form: f32 {step, lr} read on the device (bias corrections
+  // derived in-kernel), so a hipGraph-replayed optimizer step advances them
+  const float* step_lr;        // nullptr: use lr / bias_corr1 / bias_corr2 above
 };
 void launch_fused_adamw(const AdamWArgs& a, int nchunks, hipStream_t st);
 

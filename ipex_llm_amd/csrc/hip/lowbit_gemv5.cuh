@@ -145,6 +145,12 @@ __host__ __device__ constexpr size_t gemv5_attn_shmem(int rows, int cpk, int D, 
 #define ILLM_GEMV_NT 1
 #endif
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// ablation knobs for tools/probe/gemv5_probe.hip (timing only; results are
+// wrong when set): bit 0 = no dequant/MFMA (loads are xor-folded), bit 1 =
+// no norm/x-staging prologue, bit 2 = no epilogue stores/atomics
+#ifndef ILLM_GEMV5_ABL
+#define ILLM_GEMV5_ABL 0
+#endif
 __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
 #if ILLM_GEMV_NT
   const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
@@ -154,8 +160,12 @@ __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
 #endif
 }
 
+// minimum waves per SIMD the register allocation must allow (1 = unconstrained)
+#ifndef ILLM_GEMV5_MINW
+#define ILLM_GEMV5_MINW 1
+#endif
 template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4>
-__global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a) {
+__global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(const GemvArgs a) {
   // PF: chunks in flight per wave (4; 8 = every chunk of a decode split-K
   // slice of <= 8 chunks requested before the prologue)
   using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;   // MFMA input type
@@ -297,7 +307,7 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
       h[2 * i + 1] = rnd(rnd(av[2 * i + 1]) + to_f32<T>((uint16_t)(rw[i] >> 16)));
     }
   };
-  if (a.nacc) {
+  if (a.nacc && !(ILLM_GEMV5_ABL & 2)) {
     if (threadIdx.x < 16) ninv[threadIdx.x] = 0.f;
     __syncthreads();
     const bool wres = a.nres_out != nullptr && blockIdx.x == 0 && blockIdx.y == 0;
@@ -329,7 +339,7 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
   }
 
   // ---- stage x[0:Mloc, kbase:kbase+kw] -> LDS in C
-  {
+  if (!(ILLM_GEMV5_ABL & 2)) {
     const int vpr = kw / 8;
     for (int v = threadIdx.x; v < Mloc * vpr; v += NW * 64) {
       const int m = v / vpr, kk = (v % vpr) * 8;
@@ -468,6 +478,12 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
     const uint32_t mask_s = a.nib_mask, magic_v = a.nib_magic;
 
     auto compute_chunk = [&](const Chunk& ch, int c) {
+      if constexpr ((ILLM_GEMV5_ABL & 1) != 0) {
+#pragma unroll
+        for (int t = 0; t < TPW; t++)
+          acc[t][0] += __uint_as_float((ch.q[t][0].x ^ ch.q[t][0].y ^ ch.q[t][0].z ^ ch.q[t][0].w ^ ch.sc[t].x) & 0x3fffffu);
+        return;
+      }
       const uint16_t* xc = xrow + (c - c0) * 128;
       uint4 B[4];
 #pragma unroll
@@ -530,6 +546,10 @@ __global__ void __launch_bounds__(NW * 64) lowbit_gemv5_kernel(const GemvArgs a)
       if (c + u < c1u) compute_chunk(ring[u], c + u);
   }
 
+  if constexpr ((ILLM_GEMV5_ABL & 4) != 0) {
+    if (acc[0][0] == 1234.5f) ((float*)a.out)[threadIdx.x] = acc[0][1];
+    return;
+  }
   // ---- reduce the KW k-parts of each tile group through LDS
   constexpr bool ATOMIC_T = EPI == EPI_ATOMIC && !MOE;   // block-transposed atomic epilogue
   if constexpr (KW > 1) {

@@ -35,16 +35,23 @@ __global__ void __launch_bounds__(ADAM_THREADS) fused_adamw_kernel(AdamWArgs a) 
   float* m = (float*)a.exp_avg[t];
   float* v = (float*)a.exp_avg_sq[t];
   const int64_t end = min(n, start + (int64_t)a.chunk);
+  float lr = a.lr, bc1 = a.bias_corr1, bc2 = a.bias_corr2;
+  if (a.step_lr) {
+    const float stp = a.step_lr[0];
+    lr = a.step_lr[1];
+    bc1 = 1.f - powf(a.beta1, stp);
+    bc2 = 1.f - powf(a.beta2, stp);
+  }
   for (int64_t i = start + threadIdx.x; i < end; i += ADAM_THREADS) {
     float gi = ld(g, i, a.grad_dtype) * a.grad_scale;
     float pi = ld(p, i, a.param_dtype);
-    pi *= 1.f - a.lr * a.weight_decay;                  // decoupled weight decay
+    pi *= 1.f - lr * a.weight_decay;                  // decoupled weight decay
     const float mi = a.beta1 * m[i] + (1.f - a.beta1) * gi;
     const float vi = a.beta2 * v[i] + (1.f - a.beta2) * gi * gi;
     m[i] = mi;
     v[i] = vi;
-    const float denom = sqrtf(vi / a.bias_corr2) + a.eps;
-    pi -= a.lr * (mi / a.bias_corr1) / denom;
+    const float denom = sqrtf(vi / bc2) + a.eps;
+    pi -= lr * (mi / bc1) / denom;
     st(p, i, a.param_dtype, pi);
   }
 }

@@ -85,7 +85,8 @@ void custom_all_reduce(const Tensor& inp, Tensor& out, c10::IntArrayRef bufs, in
 // table: int64 [5, T] = (param ptr, grad ptr, exp_avg ptr, exp_avg_sq ptr, numel)
 void fused_adamw(const Tensor& table, const Tensor& chunk_tensor, const Tensor& chunk_start, int64_t chunk,
                  double lr, double beta1, double beta2, double eps, double weight_decay, double bc1, double bc2,
-                 double grad_scale, int64_t param_dtype, int64_t grad_dtype) {
+                 double grad_scale, int64_t param_dtype, int64_t grad_dtype,
+                 const c10::optional<Tensor>& step_lr) {
   TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.dim() == 2 && table.size(0) == 5,
               "fused_adamw: table must be int64 [5, T] on the GPU");
   c10::DeviceGuard g(table.device());
@@ -110,13 +111,19 @@ void fused_adamw(const Tensor& table, const Tensor& chunk_tensor, const Tensor& 
   a.grad_scale = (float)grad_scale;
   a.param_dtype = (int)param_dtype;
   a.grad_dtype = (int)grad_dtype;
+  a.step_lr = nullptr;
+  if (step_lr.has_value()) {
+    TORCH_CHECK(step_lr->is_cuda() && step_lr->scalar_type() == at::kFloat && step_lr->numel() == 2,
+                "fused_adamw: step_lr must be f32 [2] (step, lr) on the GPU");
+    a.step_lr = step_lr->data_ptr<float>();
+  }
   illm::launch_fused_adamw(a, (int)chunk_tensor.numel(), at::hip::getCurrentHIPStream().stream());
 }
 
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
-  m.def("fused_adamw(Tensor table, Tensor chunk_tensor, Tensor chunk_start, int chunk, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, int param_dtype, int grad_dtype) -> ()");
+  m.def("fused_adamw(Tensor table, Tensor chunk_tensor, Tensor chunk_start, int chunk, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, int param_dtype, int grad_dtype, Tensor? step_lr=None) -> ()");
   m.def("ipc_alloc(int nbytes) -> int", &ipc_alloc);
   m.def("ipc_handle(int ptr) -> Tensor", &ipc_handle);
   m.def("ipc_open(Tensor handle) -> int", &ipc_open);

@@ -5,4 +5,4 @@ from .lora import (LoraConfig, LoraLinear, PeftModel, cast_lora_weight, get_peft
 from .optim import FusedAdamW  # noqa: F401
 from .relora import ReLoRAScheduler, relora_restart, reset_optimizer  # noqa: F401
 from .lisa import LayerActivation, find_layers  # noqa: F401
-from .ddp import wrap_ddp  # noqa: F401
+from .ddp import GradBucketSync, wrap_ddp  # noqa: F401

@@ -7,6 +7,12 @@ params/moments in ONE kernel (``csrc/hip/optim.hip``: chunk table ->
 workgroups, f32 moments, bf16 or f32 params).  On CPU it runs the same
 math with torch ``_foreach`` ops.  Semantics = ``torch.optim.AdamW``
 (decoupled weight decay, bias correction).
+
+``capturable=True`` keeps the step count and learning rate of each group in a
+device tensor and the pointer/chunk tables cached, so ``step()`` issues no
+host-to-device copy and can be captured in a hipGraph together with the
+forward and backward (tools/bench_qlora.py --graph).  After changing
+``group["lr"]`` call :meth:`sync_lr` (outside capture).
 """
 from __future__ import annotations
 
@@ -22,9 +28,26 @@ CHUNK = 16384
 
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params: Iterable, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 1e-2):
+                 weight_decay: float = 1e-2, capturable: bool = False):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
+        self.capturable = capturable
+        self._tables = {}          # (device, dtype, ptrs) -> (table, chunk_tensor, chunk_start)
+        self._step_lr = {}         # group index -> f32 [2] (step, lr) on the device
+
+    def sync_lr(self):
+        """copy each group's current ``lr`` into its device (step, lr) pair"""
+        for gi, group in enumerate(self.param_groups):
+            sl = self._step_lr.get(gi)
+            if sl is not None:
+                sl[1].fill_(float(group["lr"]))
+
+    def _dev_step_lr(self, gi, group, dev):
+        sl = self._step_lr.get(gi)
+        if sl is None or sl.device != dev:
+            sl = torch.tensor([0.0, float(group["lr"])], dtype=torch.float32, device=dev)
+            self._step_lr[gi] = sl
+        return sl
 
     def _state(self, p):
         st = self.state[p]
@@ -37,12 +60,17 @@ class FusedAdamW(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
             b1, b2 = group["betas"]
             sts = [self._state(p) for p in ps]
+            if self.capturable and all(p.is_cuda for p in ps) and ops.native_gpu(ps[0]):
+                sl = self._dev_step_lr(gi, group, ps[0].device)
+                sl[0:1].add_(1.0)               # device-side step count (captured with the update)
+                self._fused(group, ps, sts, 0.0, 0.0, step_lr=sl)
+                continue
             for s in sts:
                 s["step"] += 1
             step = sts[0]["step"]
@@ -58,7 +86,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 self._ref(group, ps[i], sts[i], bc1, bc2)
         return loss
 
-    def _fused(self, group, ps, sts, bc1, bc2):
+    def _fused(self, group, ps, sts, bc1, bc2, step_lr=None):
         b1, b2 = group["betas"]
         by_dtype = {}
         for p, s in zip(ps, sts):
@@ -67,17 +95,24 @@ class FusedAdamW(torch.optim.Optimizer):
             rows = [[p.data_ptr() for p, _ in items], [p.grad.data_ptr() for p, _ in items],
                     [s["exp_avg"].data_ptr() for _, s in items], [s["exp_avg_sq"].data_ptr() for _, s in items],
                     [p.numel() for p, _ in items]]
-            table = torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=True)
-            ct, cs = [], []
-            for ti, (p, _) in enumerate(items):
-                for st in range(0, p.numel(), CHUNK):
-                    ct.append(ti)
-                    cs.append(st)
-            chunk_tensor = torch.tensor(ct, dtype=torch.int32).to(dev, non_blocking=True)
-            chunk_start = torch.tensor(cs, dtype=torch.int64).to(dev, non_blocking=True)
+            key = (dev, dt, tuple(tuple(r) for r in rows))
+            cached = self._tables.get(key) if step_lr is not None else None
+            if cached is None:
+                table = torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=True)
+                ct, cs = [], []
+                for ti, (p, _) in enumerate(items):
+                    for st in range(0, p.numel(), CHUNK):
+                        ct.append(ti)
+                        cs.append(st)
+                chunk_tensor = torch.tensor(ct, dtype=torch.int32).to(dev, non_blocking=True)
+                chunk_start = torch.tensor(cs, dtype=torch.int64).to(dev, non_blocking=True)
+                cached = (table, chunk_tensor, chunk_start)
+                if step_lr is not None:
+                    self._tables[key] = cached
+            table, chunk_tensor, chunk_start = cached
             pd = 0 if dt == torch.float32 else 1
             torch.ops.ipex_llm_amd.fused_adamw(table, chunk_tensor, chunk_start, CHUNK, group["lr"], b1, b2,
-                                               group["eps"], group["weight_decay"], bc1, bc2, 1.0, pd, pd)
+                                               group["eps"], group["weight_decay"], bc1, bc2, 1.0, pd, pd, step_lr)
 
     @staticmethod
     def _ref(group, p, s, bc1, bc2):

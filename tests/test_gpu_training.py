@@ -26,6 +26,42 @@ def test_fused_adamw_kernel(cuda, dtype):
         assert torch.allclose(a.float(), b, atol=tol, rtol=tol)
 
 
+def test_fused_adamw_capturable_graph(cuda):
+    """capturable FusedAdamW (device step / lr) replayed from a hipGraph tracks
+    torch.optim.AdamW step for step, lr changes applied through sync_lr"""
+    from ipex_llm_amd.training import FusedAdamW
+    torch.manual_seed(0)
+    shapes = [(37, 5), (3, 40000)]
+    p1 = [torch.nn.Parameter(torch.randn(s, device=cuda)) for s in shapes]
+    p2 = [torch.nn.Parameter(p.detach().clone()) for p in p1]
+    o1 = FusedAdamW(p1, lr=1e-2, weight_decay=0.1, capturable=True)
+    o2 = torch.optim.AdamW(p2, lr=1e-2, weight_decay=0.1)
+    grads = [torch.randn(s, device=cuda) for s in shapes]
+    for a, g in zip(p1, grads):
+        a.grad = g.clone()
+    o1.step()                                   # eager step builds the cached tables
+    for b, g in zip(p2, grads):
+        b.grad = g.clone()
+    o2.step()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        o1.step()
+    for it in range(4):
+        if it == 2:
+            for grp in (o1.param_groups[0], o2.param_groups[0]):
+                grp["lr"] = 3e-3
+            o1.sync_lr()
+        gs = [torch.randn(s, device=cuda) for s in shapes]
+        for a, b, g in zip(p1, p2, gs):
+            a.grad.copy_(g)
+            b.grad = g.clone()
+        graph.replay()
+        o2.step()
+    torch.cuda.synchronize()
+    for a, b in zip(p1, p2):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-5)
+
+
 def test_qlora_step_on_gpu(cuda, tmp_path):
     from transformers import LlamaConfig, LlamaForCausalLM
     from ipex_llm_amd.transformers import AutoModelForCausalLM

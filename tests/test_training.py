@@ -157,3 +157,63 @@ def test_ddp_lora_replicas_stay_identical(tmp_path):
     for p in ps:
         p.join(300)
     assert [p.exitcode for p in ps] == [0, 0]
+
+
+def _bucket_worker(rank, world, port):
+    import os as _os
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import copy
+    import torch.distributed as dist
+    import torch.nn as nn
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ipex_llm_amd.training import FusedAdamW
+    from ipex_llm_amd.training.ddp import GradBucketSync
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(16, 32), nn.Tanh(), nn.Linear(32, 32), nn.Tanh(), nn.Linear(32, 4))
+    model[2].weight.requires_grad_(False)               # a frozen base weight, like QLoRA
+    ref = copy.deepcopy(model)
+    if rank == 1:                                       # different init: broadcast must fix it
+        with torch.no_grad():
+            for p in model.parameters():
+                if p.requires_grad:
+                    p.add_(1.0)
+    sync = GradBucketSync(model, bucket_cap_mb=0.0002)  # ~200 B buckets: several per step
+    assert len(sync.buckets) > 2
+    sync.broadcast_parameters()
+    opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=1e-2)
+    ropt = torch.optim.AdamW([p for p in ref.parameters() if p.requires_grad], lr=1e-2, weight_decay=1e-2)
+    g = torch.Generator().manual_seed(0)
+    xs = [torch.randn(world, 5, 16, generator=g) for _ in range(3)]
+    for it in range(3):
+        x = xs[it]
+        model(x[rank]).pow(2).mean().backward()
+        sync.finish()
+        # reference: the full batch on one replica (mean over ranks of the per-rank means)
+        sum(ref(x[r]).pow(2).mean() for r in range(world)).div(world).backward()
+        for p, q in zip(model.parameters(), ref.parameters()):
+            if p.requires_grad:
+                assert torch.allclose(p.grad, q.grad, atol=1e-6), it
+        opt.step()
+        ropt.step()
+        sync.zero_grad()
+        ropt.zero_grad()
+    v = torch.cat([p.detach().flatten() for p in model.parameters() if p.requires_grad])
+    vs = [torch.empty_like(v) for _ in range(world)]
+    dist.all_gather(vs, v)
+    assert torch.allclose(vs[0], vs[1]), "replicas diverged"
+    dist.destroy_process_group()
+
+
+def test_grad_bucket_sync_matches_full_batch():
+    """GradBucketSync (flat gradient buffer, per-bucket async all-reduce fired
+    from post-accumulate hooks) == full-batch gradients; replicas identical"""
+    from tests.test_distributed import _free_port
+    import torch.multiprocessing as mp
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_bucket_worker, args=(r, 2, port)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    assert [p.exitcode for p in ps] == [0, 0]

@@ -82,6 +82,9 @@ def main():
     ap.add_argument("--rank", type=int, default=8)
     ap.add_argument("--grad-ckpt", action="store_true")
     ap.add_argument("--layers", type=int, default=None, help="debug only: fewer layers")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole training step (zero_grad, forward, backward, fused AdamW) in one "
+                         "hipGraph and replay it")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -103,20 +106,45 @@ def main():
     pm.train()
     params = [p for p in pm.parameters() if p.requires_grad]
     n_train = sum(p.numel() for p in params)
-    opt = FusedAdamW(params, lr=2e-4, weight_decay=0.0)
+    opt = FusedAdamW(params, lr=2e-4, weight_decay=0.0, capturable=args.graph)
     gen = torch.Generator(device=dev).manual_seed(1)
     ids = torch.randint(0, cfg.vocab_size, (args.batch, args.seq), device=dev, generator=gen)
 
     def step():
+        if args.graph:
+            # gradients stay allocated (stable addresses for the captured
+            # optimizer's pointer table) and are zeroed inside the step
+            opt.zero_grad(set_to_none=False)
         loss = pm(input_ids=ids, labels=ids).loss
         loss.backward()
         opt.step()
-        opt.zero_grad(set_to_none=True)
+        if not args.graph:
+            opt.zero_grad(set_to_none=True)
         return loss
 
     losses = []
-    for _ in range(args.warmup):
-        losses.append(step().item())
+    if args.graph:
+        # warm up on a side stream (lazy library / autograd state), then
+        # capture one step; every timed step is one graph replay
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(2, args.warmup)):
+                losses.append(step().item())
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static_loss = step()
+        graph.replay()
+        losses.append(static_loss.item())
+
+        def step():  # noqa: F811
+            graph.replay()
+            return static_loss
+    else:
+        for _ in range(args.warmup):
+            losses.append(step().item())
     torch.cuda.synchronize()
     torch.cuda.reset_peak_memory_stats()
     t0 = time.perf_counter()
@@ -133,7 +161,8 @@ def main():
         "data": "synthetic token batches, random-init Llama-3-8B architecture",
         "config": {"model": "Llama-3-8B" if not args.layers else f"Llama-3-8B[{args.layers} layers]",
                    "batch": args.batch, "seq_len": args.seq, "lora_r": args.rank,
-                   "targets": "q,k,v,o,gate,up,down", "grad_ckpt": args.grad_ckpt, "optimizer": "FusedAdamW"},
+                   "targets": "q,k,v,o,gate,up,down", "grad_ckpt": args.grad_ckpt, "optimizer": "FusedAdamW",
+                   "hipgraph": args.graph},
         "trainable_params": n_train, "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
         "build_s": round(build_s, 1), "loss_first": round(losses[0], 4), "loss_last": round(losses[-1], 4),
     }), flush=True)

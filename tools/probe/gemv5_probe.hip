@@ -1,0 +1,155 @@
+// Decode GEMV time breakdown on MI355X: the production v5 kernel
+// (csrc/hip/lowbit_gemv5.cuh) at the Llama-3-8B decode shapes, launched with
+// the geometry ops_hip.cpp's plan5 picks, hipGraph-replayed over rotating
+// weight copies (cold in the MALL), next to a pure weight-streaming kernel
+// of the same bytes.  Build with -DILLM_GEMV5_ABL=<bits> to drop parts of
+// the kernel (lowbit_gemv5.cuh: 1 dequant/MFMA, 2 prologue, 4 epilogue).
+// Weights are random bytes: timing only.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../ipex_llm_amd/csrc/hip/lowbit_gemv5.cuh"
+
+using namespace illm;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+static size_t shmem5(int rows, int cpk) { return gemv5_shmem(rows, cpk); }
+
+struct Shape { const char* name; int N, K; bool glu; };
+
+int main(int argc, char** argv) {
+  const Shape shapes[] = {{"qkv", 6144, 4096, false}, {"o", 4096, 4096, false},
+                          {"gate_up", 28672, 4096, true}, {"down", 4096, 14336, false}};
+  const int Ms[] = {1, 8};
+  float *nacc, *accout;
+  uint16_t *x, *res, *res2, *nw, *yout;
+  CK(hipMalloc(&nacc, 16 * 16384 * 4));
+  CK(hipMalloc(&accout, 16 * 32768 * 4));
+  CK(hipMalloc(&x, 16 * 16384 * 2));
+  CK(hipMalloc(&res, 16 * 16384 * 2));
+  CK(hipMalloc(&res2, 16 * 16384 * 2));
+  CK(hipMalloc(&nw, 16384 * 2));
+  CK(hipMalloc(&yout, 16 * 32768 * 2));
+  CK(hipMemset(nacc, 0, 16 * 16384 * 4));
+  CK(hipMemset(accout, 0, 16 * 32768 * 4));
+  CK(hipMemset(x, 0x3c, 16 * 16384 * 2));
+  CK(hipMemset(res, 0x3c, 16 * 16384 * 2));
+  CK(hipMemset(nw, 0x3f, 16384 * 2));
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  // sweep: (shape, M, normin, kw, nw, ks); 0 = the production plan5 value
+  struct Cfg { int shape, M, normin, kw, nw, ks; };
+  std::vector<Cfg> cfgs;
+  for (int M : Ms) {
+    cfgs.push_back({0, M, 0, 0, 0, 0});
+    cfgs.push_back({0, M, 1, 0, 0, 0});
+    for (int ks : {2, 4, 8}) for (int nwv : {4, 8}) cfgs.push_back({0, M, 0, 1, nwv, ks});
+    cfgs.push_back({1, M, 0, 0, 0, 0});
+    for (int ks : {2, 4, 8}) for (int nwv : {4, 8}) cfgs.push_back({1, M, 0, 1, nwv, ks});
+    cfgs.push_back({2, M, 0, 0, 0, 0});
+    cfgs.push_back({2, M, 1, 0, 0, 0});
+    for (int kwv : {1, 2, 4}) for (int nwv : {4, 8}) cfgs.push_back({2, M, 0, kwv, nwv, 0});
+    cfgs.push_back({3, M, 0, 0, 0, 0});
+    for (int ks : {4, 7, 8, 14, 16}) for (int nwv : {4, 8}) cfgs.push_back({3, M, 0, 1, nwv, ks});
+  }
+  int cur_shape = -1;
+  uint8_t* wbuf = nullptr;
+  size_t wb = 0;
+  int copies = 0;
+  for (const Cfg& c : cfgs) {
+    const Shape& s = shapes[c.shape];
+    if (c.shape != cur_shape) {
+      if (wbuf) CK(hipFree(wbuf));
+      wb = (size_t)dev_total_bytes(FMT_SYM_INT4, s.N, s.K);
+      copies = std::max(2, (int)(700e6 / wb));
+      CK(hipMalloc(&wbuf, wb * copies));
+      CK(hipMemset(wbuf, 0x5a, wb * copies));
+      cur_shape = c.shape;
+    }
+    const int NT = (s.N + 15) / 16, KC = (s.K + 127) / 128;
+    const int M = c.M, normin = c.normin;
+    if (normin && s.K != 4096) continue;
+    {
+      {
+        GemvArgs a{};
+        a.M = M; a.K = s.K; a.ldx = s.K; a.KC = KC; a.lut_fmt = FMT_SYM_INT4;
+        int kw, nwv, epi;
+        unsigned gx, gy;
+        size_t sh;
+        if (s.glu) {
+          kw = M <= 2 ? 4 : 2;
+          nwv = M <= 2 ? 4 : 8;
+          while (kw > 1 && KC / kw < 4) kw /= 2;
+          if (c.kw) kw = c.kw;
+          if (c.nw) nwv = c.nw;
+          const int groups = NT / 2;
+          gx = (groups + nwv / kw - 1) / (nwv / kw);
+          gy = 1;
+          sh = shmem5(M, KC);
+          a.N = s.N / 2; a.out = yout; a.ldo = s.N / 2; epi = EPI_GLU;
+        } else {
+          kw = 1;
+          nwv = M >= 4 ? 8 : 4;
+          const int target = M <= 2 ? 8 : 4;
+          int ks = std::min(32, std::max(1, (KC + target - 1) / target));
+          while (ks > 1 && NT * ks > 4096) ks /= 2;
+          while (shmem5(M, (KC + ks - 1) / ks) > 65536 && ks < KC) ks *= 2;
+          if (c.ks) ks = c.ks;
+          if (c.nw) nwv = c.nw;
+          const int cpk = (KC + ks - 1) / ks;
+          ks = (KC + cpk - 1) / cpk;
+          a.cpk = cpk;
+          gx = (NT + nwv - 1) / nwv;
+          gy = ks;
+          sh = shmem5(M, cpk);
+          a.N = s.N; a.out = accout; a.ldo = s.N; epi = EPI_ATOMIC;
+        }
+        a.nw = nwv;
+        if (normin) {
+          a.nacc = nacc; a.nres = res; a.nres_out = res2; a.nweight = nw; a.neps = 1e-5f;
+        } else {
+          a.x = x;
+        }
+        auto launch = [&](int i) {
+          GemvArgs b = a;
+          b.w = wbuf + (size_t)(i % copies) * wb;
+          launch_gemv5_dk<DK_INT4S>(true, kw, epi, dim3(gx, gy), sh, b, st);
+        };
+        for (int i = 0; i < copies; i++) launch(i);
+        CK(hipStreamSynchronize(st));
+        const int reps = 4 * copies;
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+        for (int i = 0; i < reps; i++) launch(i);
+        CK(hipStreamEndCapture(st, &g));
+        CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        CK(hipGraphLaunch(ge, st));
+        CK(hipStreamSynchronize(st));
+        CK(hipEventRecord(e0, st));
+        CK(hipGraphLaunch(ge, st));
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const double us = ms * 1e3 / reps;
+        printf("{\"abl\":%d,\"minw\":%d,\"op\":\"%s\",\"M\":%d,\"normin\":%d,\"grid\":[%u,%u],\"nw\":%d,\"kw\":%d,"
+               "\"us\":%.2f,\"TBps\":%.2f}\n", ILLM_GEMV5_ABL, ILLM_GEMV5_MINW, s.name, M, normin, gx, gy, nwv, kw, us,
+               wb / us / 1e6);
+        fflush(stdout);
+        CK(hipGraphExecDestroy(ge));
+        CK(hipGraphDestroy(g));
+      }
+    }
+  }
+  if (wbuf) CK(hipFree(wbuf));
+  return 0;
+}
