@@ -274,9 +274,11 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   constexpr bool RQ_OK = RQ && KVF == 0 && D / 16 >= 8;
   constexpr bool rq = RQ_OK;
   auto rnd = [](float v) { return to_f32<T>(from_f32<T>(v)); };
+  // deferred RMSNorm of the qkv GEMV input (lowbit_gemv5.cuh ndefer): one scale per sequence row
+  const float rq_rs = (rq && a.rq_ss) ? rsqrtf(a.rq_ss[b] / (float)a.rq_ss_n + a.rq_ss_eps) : 1.f;
   auto rq_raw = [&](int col) -> float {
     float s = a.rq_bias ? to_f32<T>(a.rq_bias[col]) : 0.f;
-    s += a.rq_part[(size_t)b * a.rq_ld + col];
+    s += rq_rs * a.rq_part[(size_t)b * a.rq_ld + col];
     return rnd(s);
   };
   const int64_t rpos = rq ? a.rq_pos[b] : 0;
@@ -355,7 +357,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
         }
         const float f[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
 #pragma unroll
-        for (int j = 0; j < 8; j++) v[s][j] = rnd(bb[j] + f[j]);
+        for (int j = 0; j < 8; j++) v[s][j] = rnd(bb[j] + rq_rs * f[j]);
       }
     };
     auto lane_rot = [&](int col0, float scale_out, uint4* outf) {
@@ -445,7 +447,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
           }
           uint32_t w[4];
 #pragma unroll
-          for (int e = 0; e < 4; e++) w[e] = pack2<T>(rnd(bb[2 * e] + f[2 * e]), rnd(bb[2 * e + 1] + f[2 * e + 1]));
+          for (int e = 0; e < 4; e++) w[e] = pack2<T>(rnd(bb[2 * e] + rq_rs * f[2 * e]), rnd(bb[2 * e + 1] + rq_rs * f[2 * e + 1]));
           const uint4 vq = make_uint4(w[0], w[1], w[2], w[3]);
           vnew[0] = vq;
 #pragma unroll
@@ -473,7 +475,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
             }
             uint32_t w[4];
 #pragma unroll
-            for (int e = 0; e < 4; e++) w[e] = pack2<T>(rnd(bb[2 * e] + f[2 * e]), rnd(bb[2 * e + 1] + f[2 * e + 1]));
+            for (int e = 0; e < 4; e++) w[e] = pack2<T>(rnd(bb[2 * e] + rq_rs * f[2 * e]), rnd(bb[2 * e + 1] + rq_rs * f[2 * e + 1]));
             const uint4 vq = make_uint4(w[0], w[1], w[2], w[3]);
             vnew[c] = vq;
 #pragma unroll

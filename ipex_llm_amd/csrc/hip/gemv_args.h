@@ -96,6 +96,19 @@ struct GemvArgs {
   float* nzero;
   int nzero_n;
   int pf8;                 // v5: request a <= 8-chunk split-K slice in one go (ILLM_GEMV5_PF8)
+  // deferred RMSNorm (ndefer = 1, with the nacc/nres/nweight inputs above):
+  // each workgroup stages x' = w * h for its own K slice only (no full-row
+  // pass); the per-row sum of squares of h goes to nss [M] (split-K: the
+  // workgroups of grid column 0 add their slice with one atomic per row) and
+  // the consumer applies rsqrt(ss / K + eps), which commutes with the
+  // projection.  GLU launches (full K per workgroup) apply it themselves.
+  int ndefer;
+  float* nss;
+  // glu-in prologue of a deferred-norm gate/up accumulator: its rows are
+  // scaled by rsqrt(xpss[m] / xpss_n + xpss_eps) before the activation
+  const float* xpss;
+  int xpss_n;
+  float xpss_eps;
 };
 
 }  // namespace illm

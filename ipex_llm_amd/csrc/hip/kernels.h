@@ -136,6 +136,11 @@ struct RopeKVArgs {
   const int64_t* pos_offset;   // [B] (cache index = pos - offset) or null
   int num_blocks;              // cache blocks (bounds check of slots / block ids)
   int* err;                    // kernel error word (illm_device.h kerr) or null
+  // deferred RMSNorm of the projection input (lowbit_gemv5.cuh ndefer): the
+  // accumulator row t is scaled by rsqrt(pss[t] / pss_n + pss_eps) before the bias
+  const float* pss;
+  int pss_n;
+  float pss_eps;
 };
 void launch_rope_kv(bool bf16, const RopeKVArgs& a, hipStream_t st);
 
@@ -163,6 +168,9 @@ struct AttnDecodeArgs {
   // (+ rq_bias), q/k rotated in registers; the split holding the new key
   // uses it from registers and writes it to the cache (no rope_kv launch)
   const float* rq_part;
+  const float* rq_ss;       // deferred RMSNorm: row b of rq_part scaled by rsqrt(rq_ss[b] / rq_ss_n + rq_ss_eps)
+  int rq_ss_n;
+  float rq_ss_eps;
   const uint16_t* rq_bias;
   const float* rq_cos_sin;  // [max_pos, rot / 2, 2]
   const int64_t* rq_pos;    // [B] rotary positions

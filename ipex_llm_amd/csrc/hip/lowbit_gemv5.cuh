@@ -307,7 +307,12 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
       h[2 * i + 1] = rnd(rnd(av[2 * i + 1]) + to_f32<T>((uint16_t)(rw[i] >> 16)));
     }
   };
-  if (a.nacc && !(ILLM_GEMV5_ABL & 2)) {
+  const bool defer = a.nacc != nullptr && a.ndefer != 0;
+  if (defer) {                    // per-row sum of squares of this workgroup's K slice (staging below)
+    if (threadIdx.x < 16) ninv[threadIdx.x] = 0.f;
+    __syncthreads();
+  }
+  if (a.nacc && !defer && !(ILLM_GEMV5_ABL & 2)) {
     if (threadIdx.x < 16) ninv[threadIdx.x] = 0.f;
     __syncthreads();
     const bool wres = a.nres_out != nullptr && blockIdx.x == 0 && blockIdx.y == 0;
@@ -390,6 +395,11 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
           uv[0] += u0.x; uv[1] += u0.y; uv[2] += u0.z; uv[3] += u0.w;
           uv[4] += u1.x; uv[5] += u1.y; uv[6] += u1.z; uv[7] += u1.w;
         }
+        if (a.xpss) {              // deferred RMSNorm of the gate/up input: one scale per row
+          const float sc = rsqrtf(a.xpss[xrow_of(m)] / (float)a.xpss_n + a.xpss_eps);
+#pragma unroll
+          for (int i = 0; i < 8; i++) { gv[i] *= sc; uv[i] *= sc; }
+        }
         uint32_t w[4];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -405,6 +415,36 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
           w[i] = pack2<C>(o2[0], o2[1]);
         }
         val = make_uint4(w[0], w[1], w[2], w[3]);
+      } else if (kbase + kk < a.K && defer) {
+        // deferred RMSNorm: h = rnd(rnd(acc) + res) of this slice, x' = rnd(w * h);
+        // sum of squares per row -> ninv[m] (LDS), grid column 0 writes the residual out
+        float h[8];
+        ni_h(m, kbase + kk, h);
+        float ssq = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; i++) ssq += h[i] * h[i];
+        ssq += __shfl_xor(ssq, 1, 8);
+        ssq += __shfl_xor(ssq, 2, 8);
+        ssq += __shfl_xor(ssq, 4, 8);
+        if ((v & 7) == 0) atomicAdd(&ninv[m], ssq);
+        if (a.nres_out && blockIdx.x == 0)
+          *(uint4*)(a.nres_out + (size_t)m * a.K + kbase + kk) =
+              make_uint4(pack2<T>(h[0], h[1]), pack2<T>(h[2], h[3]), pack2<T>(h[4], h[5]), pack2<T>(h[6], h[7]));
+        const uint4 wq = *(const uint4*)(a.nweight + kbase + kk);
+        const uint32_t wv[4] = {wq.x, wq.y, wq.z, wq.w};
+        uint32_t o4[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          float w0 = to_f32<T>((uint16_t)(wv[i] & 0xffff)), w1 = to_f32<T>((uint16_t)(wv[i] >> 16));
+          if (a.nunit) { w0 = rnd(1.f + w0); w1 = rnd(1.f + w1); }
+          float v0 = rnd(w0 * h[2 * i]), v1 = rnd(w1 * h[2 * i + 1]);
+          if constexpr (!std::is_same<C, T>::value) {
+            v0 = fminf(fmaxf(v0, -65504.f), 65504.f);
+            v1 = fminf(fmaxf(v1, -65504.f), 65504.f);
+          }
+          o4[i] = pack2<C>(v0, v1);
+        }
+        val = make_uint4(o4[0], o4[1], o4[2], o4[3]);
       } else if (kbase + kk < a.K && a.nacc) {
         // normalised residual stream: w * rnd(h * inv), rounded to T like the norm kernel's output
         float h[8];
@@ -466,6 +506,16 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
     }
   }
   __syncthreads();
+  if (defer) {
+    if constexpr (EPI == EPI_GLU) {
+      // full K staged here: the row scale is known locally (applied before the activation)
+      __syncthreads();
+      if (threadIdx.x < Mloc) ninv[threadIdx.x] = rsqrtf(ninv[threadIdx.x] / (float)a.K + a.neps);
+      __syncthreads();
+    } else if (blockIdx.x == 0 && threadIdx.x < Mloc && a.nss) {
+      __hip_atomic_fetch_add(a.nss + threadIdx.x, ninv[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 
   f32x4 acc[TPW];
 #pragma unroll
@@ -601,9 +651,10 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
   const int m = orow_of(r16);
   if constexpr (EPI == EPI_GLU) {
     float o[4];
+    const float rs = defer ? ninv[r16] : 1.f;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const float gv = acc[0][i], uv = acc[TPW - 1][i];
+      const float gv = acc[0][i] * rs, uv = acc[TPW - 1][i] * rs;
       o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
     }
     const int n0 = (tile0 / 2) * 16 + 4 * g;

@@ -37,11 +37,14 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
   constexpr bool BF = std::is_same<T, BF16>::value;
   // projection output element d of this head (split-K partials summed here,
   // rounded to T like the standalone GEMV output)
+  const float rs = a.pss ? rsqrtf(a.pss[t] / (float)a.pss_n + a.pss_eps) : 1.f;   // deferred input norm
   auto raw = [&](int d) -> float {
     if (!a.part) return to_f32<T>(src[d]);
-    float s = a.bias ? to_f32<T>(a.bias[col0 + d]) : 0.f;
+    float s = 0.f;
 #pragma unroll 4
     for (int k = 0; k < a.nsplit; k++) s += a.part[((size_t)k * a.T + t) * a.ld_qkv + col0 + d];
+    s *= rs;
+    if (a.bias) s += to_f32<T>(a.bias[col0 + d]);
     return to_f32<T>(from_f32<T>(s));
   };
   // two elements at once: both columns' split-K loads are in flight together
@@ -52,8 +55,7 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
       r1 = to_f32<T>(src[d1]);
       return;
     }
-    float s0 = a.bias ? to_f32<T>(a.bias[col0 + d0]) : 0.f;
-    float s1 = a.bias ? to_f32<T>(a.bias[col0 + d1]) : 0.f;
+    float s0 = 0.f, s1 = 0.f;
     const float* pk = a.part + (size_t)t * a.ld_qkv + col0;
     const size_t kstride = (size_t)a.T * a.ld_qkv;
 #pragma unroll 4
@@ -61,6 +63,12 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const RopeKVArgs a) {
       s0 += pk[d0];
       s1 += pk[d1];
       pk += kstride;
+    }
+    s0 *= rs;
+    s1 *= rs;
+    if (a.bias) {
+      s0 += to_f32<T>(a.bias[col0 + d0]);
+      s1 += to_f32<T>(a.bias[col0 + d1]);
     }
     r0 = to_f32<T>(from_f32<T>(s0));
     r1 = to_f32<T>(from_f32<T>(s1));
@@ -209,7 +217,12 @@ __global__ void __launch_bounds__(256) rope_kv_vec_kernel(const RopeKVArgs a) {
     float* pp = (float*)a.part + (size_t)t * a.ld_qkv + (size_t)h * D;
     float4* p0 = (float4*)(pp + i0);
     float4* p1 = (float4*)(pp + i0 + half);
-    const float4 f[4] = {p0[0], p0[1], p1[0], p1[1]};
+    float4 f[4] = {p0[0], p0[1], p1[0], p1[1]};
+    if (a.pss) {                                       // deferred input norm: one scale per token row
+      const float rs = rsqrtf(a.pss[t] / (float)a.pss_n + a.pss_eps);
+#pragma unroll
+      for (int e = 0; e < 4; e++) { f[e].x *= rs; f[e].y *= rs; f[e].z *= rs; f[e].w *= rs; }
+    }
     uint32_t wv[8];
 #pragma unroll
     for (int e = 0; e < 4; e++) {

@@ -115,16 +115,24 @@ Plan5 plan5(int64_t rows, int64_t groups, int64_t KC, bool can_split, int64_t ks
   static const int nw_env = getenv("ILLM_GEMV5_NW") ? atoi(getenv("ILLM_GEMV5_NW")) : 0;
   Plan5 p{1, 1, KC, 0, 0, 4};  // kw, ks, cpk, shmem, gx, nw
   if (!can_split) {
-    // GLU: M <= 2 -> 4-wave groups, 4-way K split (1 tile pair each);
-    // larger M -> 8-wave groups, 2-way K split (x staged once per 4 pairs)
-    p.kw = rows <= 2 ? 4 : 2;
+    // GLU: 2-way K split inside the workgroup; M <= 2 -> 4-wave groups (2 tile
+    // pairs), larger M -> 8-wave groups (x staged once per 4 pairs).  MI355X
+    // (profiles/gemv5_geometry_sweep_r3.jsonl, Llama-3-8B gate/up, M = 1):
+    // 448 x 4-wave groups 17.1 us vs 896 x (4-way split, 1 pair) 20.7 us --
+    // the 896-group grid needed two residency rounds at 2 waves per SIMD
+    p.kw = 2;
     p.nw = rows <= 2 ? 4 : 8;
     while (p.kw > 1 && KC / p.kw < 4) p.kw /= 2;
   } else if (ks_req > 0) {
     p.ks = ks_req;
   } else {
-    p.nw = rows >= 4 ? 8 : 4;     // 8-wave groups: x slice shared by 8 tiles (down M=16: 10.8 vs 15.7 us)
-    const int64_t target = rows <= 2 ? 8 : 4;
+    // 8-wave groups: x slice shared by 8 tiles (down M=16: 10.8 vs 15.7 us);
+    // also for the narrow (<= 256-tile) outputs at M = 1 (o 4.85 vs 4.92 us)
+    p.nw = (rows >= 4 || groups <= 256) ? 8 : 4;
+    // ~4-chunk slices for K <= 8K, ~7 for the wide-K down projection: qkv
+    // M = 1 5.75 vs 6.16 us (8 x 4 chunks vs 4 x 8), down M = 1 7.6 vs 10.9 us
+    // (16 x 7 vs 14 x 8), M = 8 9.6 vs 11.1 us (same sweep)
+    const int64_t target = KC >= 64 ? 7 : 4;
     p.ks = std::min<int64_t>(atomic ? 32 : 16, std::max<int64_t>(1, (KC + target - 1) / target));
     // wide outputs (lm_head: 8016 tiles) already fill the chip: slabs only cost
     while (p.ks > 1 && groups * p.ks > 4096) p.ks /= 2;
@@ -420,7 +428,8 @@ static void set_zero(illm::GemvArgs& a, const c10::optional<Tensor>& zero) {
 // EPI_GLU (returns act(gate) * up [M, n / 2] in dt).
 Tensor gemv_norm_in(const Tensor& acc_in, const Tensor& residual, Tensor& res_out, const Tensor& norm_w, double eps,
                     bool unit_offset, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t epi,
-                    int64_t act, const c10::optional<Tensor>& acc_out, const c10::optional<Tensor>& zero) {
+                    int64_t act, const c10::optional<Tensor>& acc_out, const c10::optional<Tensor>& zero,
+                    const c10::optional<Tensor>& ss) {
   TORCH_CHECK(acc_in.is_cuda() && blob.is_cuda() && residual.is_cuda(), "gemv_norm_in: GPU tensors expected");
   c10::DeviceGuard g(acc_in.device());
   const bool bf16 = is_bf16(residual);
@@ -452,6 +461,15 @@ Tensor gemv_norm_in(const Tensor& acc_in, const Tensor& residual, Tensor& res_ou
   a.neps = (float)eps;
   a.nunit = unit_offset ? 1 : 0;
   set_zero(a, zero);
+  if (ss.has_value() && ss->defined()) {
+    // deferred norm: the row scales are applied by the consumer (split-K
+    // atomic output: ss [M] f32 zeroed on entry gets the sum of squares) or
+    // by the GLU epilogue itself
+    TORCH_CHECK(ss->is_cuda() && ss->scalar_type() == at::kFloat && ss->is_contiguous() && ss->numel() >= M,
+                "gemv_norm_in: ss must be contiguous f32 [>= M]");
+    a.ndefer = 1;
+    a.nss = ss->data_ptr<float>();
+  }
   if (epi == illm::EPI_GLU) {
     TORCH_CHECK(n % 32 == 0, "GLU weights must have a multiple of 32 rows");
     Tensor out = at::empty({M, n / 2}, residual.options());
@@ -516,7 +534,8 @@ void gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
 // partial slabs [ks, M, n], or accumulates atomically into ``acc`` [M, n].
 Tensor gemv_glu_in(const Tensor& part, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t act,
                    int64_t ksplit, at::ScalarType dt, const c10::optional<Tensor>& acc,
-                   const c10::optional<Tensor>& zero) {
+                   const c10::optional<Tensor>& zero, const c10::optional<Tensor>& xss, int64_t xss_n,
+                   double xss_eps) {
   TORCH_CHECK(part.is_cuda() && blob.is_cuda() && part.dim() == 3 && part.scalar_type() == at::kFloat &&
               part.is_contiguous(), "gemv_glu_in: part must be contiguous f32 [ns, M, 2k] on the GPU");
   TORCH_CHECK(part.size(2) == 2 * k && k % 16 == 0, "gemv_glu_in: part width must be 2 * k");
@@ -532,6 +551,13 @@ Tensor gemv_glu_in(const Tensor& part, const Tensor& blob, int64_t fmt, int64_t 
   a.x = nullptr;
   a.xpart = part.data_ptr<float>();
   a.xpart_ns = (int)part.size(0);
+  if (xss.has_value() && xss->defined()) {
+    TORCH_CHECK(xss->is_cuda() && xss->scalar_type() == at::kFloat && xss_n > 0,
+                "gemv_glu_in: xss must be f32 [M] with xss_n > 0");
+    a.xpss = xss->data_ptr<float>();
+    a.xpss_n = (int)xss_n;
+    a.xpss_eps = (float)xss_eps;
+  }
   a.M = (int)M;
   a.K = (int)k;
   a.ldx = (int)k;
@@ -714,7 +740,7 @@ void rope_kv_fused(const Tensor& part, const c10::optional<Tensor>& bias, Tensor
                    const c10::optional<Tensor>& q_norm, const c10::optional<Tensor>& k_norm, double norm_eps,
                    double q_scale, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot_dim, bool interleaved,
                    int64_t kv_fp8, double k_scale, double v_scale, const c10::optional<Tensor>& pos_offset,
-                   bool zero_part) {
+                   bool zero_part, const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps) {
   c10::DeviceGuard g(part.device());
   const bool bf16 = is_bf16(q_out);
   TORCH_CHECK(part.dim() == 3 && part.scalar_type() == at::kFloat && part.is_contiguous(),
@@ -756,6 +782,13 @@ void rope_kv_fused(const Tensor& part, const c10::optional<Tensor>& bias, Tensor
   a.v_scale = (float)v_scale;
   a.num_blocks = (int)k_cache.size(0);
   a.err = kernel_err(part.device());
+  if (pss.has_value() && pss->defined()) {
+    TORCH_CHECK(pss->is_cuda() && pss->scalar_type() == at::kFloat && pss->numel() >= a.T && pss_n > 0,
+                "rope_kv_fused: pss must be f32 [T] with pss_n > 0");
+    a.pss = pss->data_ptr<float>();
+    a.pss_n = (int)pss_n;
+    a.pss_eps = (float)pss_eps;
+  }
   if (a.T > 0) illm::launch_rope_kv(bf16, a, cur_stream());
 }
 
@@ -819,7 +852,8 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, cons
 static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
     const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin, const Tensor& pos, Tensor& k_cache,
     Tensor& v_cache, const Tensor& block_tables, const Tensor& seq_lens, int64_t nsplit, double scale, double softcap,
-    int64_t window, int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt, bool no_combine) {
+    int64_t window, int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt, bool no_combine,
+    const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps) {
   c10::DeviceGuard g(part.device());
   TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "attn_decode_rope: bf16/fp16 activations");
   TORCH_CHECK(k_cache.scalar_type() == dt && v_cache.scalar_type() == dt, "attn_decode_rope: 16-bit KV cache");
@@ -876,6 +910,13 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
   a.rq_rot = (int)rot_dim;
   a.rq_interleaved = interleaved ? 1 : 0;
   a.rq_qscale = (float)q_scale;
+  if (pss.has_value() && pss->defined()) {
+    TORCH_CHECK(pss->is_cuda() && pss->scalar_type() == at::kFloat && pss->numel() >= B && pss_n > 0,
+                "attn_decode_rope: pss must be f32 [B] with pss_n > 0");
+    a.rq_ss = pss->data_ptr<float>();
+    a.rq_ss_n = (int)pss_n;
+    a.rq_ss_eps = (float)pss_eps;
+  }
   illm::launch_attn_decode(dt == at::kBFloat16, a, cur_stream());
   return {out, po, pml};
 }
@@ -883,9 +924,11 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
 Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin,
                         const Tensor& pos, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
                         const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
-                        int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt) {
+                        int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt,
+                        const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps) {
   return std::get<0>(attn_decode_rope_impl(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit,
-                                           scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dt, false));
+                                           scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dt, false, pss,
+                                           pss_n, pss_eps));
 }
 
 // fused-RoPE split attention without the combine: (o, m, l) partials for the
@@ -896,9 +939,10 @@ std::tuple<Tensor, Tensor> attn_decode_rope_split(const Tensor& part, const c10:
                                                   Tensor& v_cache, const Tensor& block_tables, const Tensor& seq_lens,
                                                   int64_t nsplit, double scale, double softcap, int64_t window,
                                                   int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale,
-                                                  at::ScalarType dt) {
+                                                  at::ScalarType dt, const c10::optional<Tensor>& pss,
+                                                  int64_t pss_n, double pss_eps) {
   auto r = attn_decode_rope_impl(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
-                                 softcap, window, Hq, rot_dim, interleaved, q_scale, dt, true);
+                                 softcap, window, Hq, rot_dim, interleaved, q_scale, dt, true, pss, pss_n, pss_eps);
   return {std::get<1>(r), std::get<2>(r)};
 }
 

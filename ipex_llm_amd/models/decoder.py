@@ -149,6 +149,13 @@ ACC_MAX_M = int(__import__("os").environ.get("ILLM_ACC_MAX_M", "8"))
 # workgroup re-derives the full-row norm, fine for 1-2 rows, far too much
 # redundant slab traffic at 4-8 (batch 8: 2.38 -> 3.08 ms/step)
 NORM_IN_MAX_M = int(__import__("os").environ.get("ILLM_NORM_IN_MAX_M", "2"))
+# deferred RMSNorm (lowbit_gemv5.cuh ndefer): the consuming GEMV stages
+# w * (residual + acc) for its own K slice only and the 1/rms row scale is
+# applied by the qkv consumer (RoPE / fused-RoPE attention) or in the gate/up
+# GLU epilogue -- no full-row pass per workgroup, so the norm-in path extends
+# to larger decode batches (ILLM_DEFER_NORM=0 restores the full-row prologue)
+DEFER_NORM = __import__("os").environ.get("ILLM_DEFER_NORM", "1") != "0"
+DEFER_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_MAX_M", "4"))
 # decode batches up to this size take the fused-RoPE attention (qkv accumulated
 # atomically into one slab read by the attention, re-zeroed by its combine).
 # Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token,
@@ -423,8 +430,12 @@ class NativeCausalLM(nn.Module):
     # launches per layer fewer.  ILLM_NORM_IN=0 restores the standalone norms.
     _norm_in_env = __import__("os").environ.get("ILLM_NORM_IN", "1") != "0"
 
+    def _defer_ok(self, ref: torch.Tensor, T: int) -> bool:
+        return DEFER_NORM and T <= min(ACC_MAX_M, DEFER_MAX_M) and not self._oproj_combine
+
     def _norm_in_ok(self, ref: torch.Tensor, T: int) -> bool:
-        if not (self._norm_in_env and T <= min(ACC_MAX_M, NORM_IN_MAX_M) and ref.is_cuda
+        lim = max(NORM_IN_MAX_M, DEFER_MAX_M if self._defer_ok(ref, T) else 0)
+        if not (self._norm_in_env and T <= min(ACC_MAX_M, lim) and ref.is_cuda
                 and not self.spec.sandwich_norm and not self._attn_fuse and not self._glu_in_enabled
                 and self.spec.hidden_size % 8 == 0 and ops.native_gpu(ref)):
             return False
@@ -542,6 +553,13 @@ class NativeCausalLM(nn.Module):
         pend = None                     # accumulator awaiting residual-add + norm
         consumed = None                 # accumulator read by the last launch: zeroed by the next GEMV
         res_pp = (residual, torch.empty_like(residual)) if norm_in else None
+        # deferred norm: per-(layer, norm) row sums of squares, zeroed once per step
+        defer = norm_in and self._defer_ok(residual, T)
+        ss_all = None
+        if defer:
+            ss_all = self._acc(T, 2 * len(self.layers), x.device, "SS")
+            ss_all.zero_()
+        ss_q = None                     # sums of squares of the current layer's qkv input (deferred)
         # fused-RoPE decode attention (batch <= ROPE_IN_MAX_M, one token each): the qkv
         # GEMV accumulates into one atomic slab that the attention reads and the
         # combine launch re-zeroes
@@ -565,6 +583,7 @@ class NativeCausalLM(nn.Module):
                     pass
             attn = layer.self_attn
             qp = attn.qkv_proj
+            ss_q = None
             q = torch.empty(T, s.num_heads, s.head_dim, dtype=x.dtype, device=x.device)
             if x.is_cuda and isinstance(qp, LowBitLinear) and qp.mp_group is None and T <= ops.GEMV_MAX_M \
                     and (qp.bias is None or qp.bias.dtype == x.dtype) and ops.native_gpu(x):
@@ -572,10 +591,13 @@ class NativeCausalLM(nn.Module):
                 # T <= 16 accumulates with atomics into one zeroed slab (re-zeroed by the kernel)
                 if T <= ACC_MAX_M or rope_in:
                     part = self._acc(qp.out_features, T, x.device)
+                    ss_q = None
                     if pend is not None:
                         r2 = nxt_res(residual)
+                        ss_q = ss_all[2 * li] if defer else None
                         ops.gemv_norm_in(pend, residual, r2, layer.input_layernorm, s.rms_eps, s.norm_unit_offset,
-                                         qp.weight, qp.fmt, qp.out_features, qp.in_features, False, acc_out=part)
+                                         qp.weight, qp.fmt, qp.out_features, qp.in_features, False, acc_out=part,
+                                         ss=ss_q)
                         residual, consumed, pend = r2, pend, None
                     else:
                         ops.gemv_accum(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, part,
@@ -589,12 +611,14 @@ class NativeCausalLM(nn.Module):
                     ops.rope_kv_fused(part, qp.bias, q, cache.k[li], cache.v[li], pos, meta.block_tables, meta.Tq,
                                       rope, s.num_heads, s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved,
                                       attn.q_norm, attn.k_norm, s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale,
-                                      cache.v_scale, meta.pos_offset, zero_part=T <= ACC_MAX_M)
+                                      cache.v_scale, meta.pos_offset, zero_part=T <= ACC_MAX_M,
+                                      pss=ss_q, pss_n=s.hidden_size, pss_eps=s.rms_eps)
                 elif not (norm_in and self._oproj_combine and attn.o_proj.bias is None):
                     a_rope = ops.attn_decode_rope(qkv_acc, qp.bias, self.rope_cache, pos, cache.k[li], cache.v[li],
                                                   meta.block_tables, meta.seq_lens, meta.nsplit, s.scale,
                                                   s.attn_softcap, attn.sliding_window, s.num_heads, s.rot_dim,
-                                                  s.rope_interleaved, 1.0, x.dtype).view(T, -1)
+                                                  s.rope_interleaved, 1.0, x.dtype, pss=ss_q,
+                                                  pss_n=s.hidden_size, pss_eps=s.rms_eps).view(T, -1)
             else:
                 qkv = qp(x)
                 ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,
@@ -630,7 +654,7 @@ class NativeCausalLM(nn.Module):
                 gu, dn = mlp.gate_up_proj, mlp.down_proj
                 act = ops.gemv_norm_in(accP, residual, r2, layer.post_attention_layernorm, s.rms_eps,
                                        s.norm_unit_offset, gu.weight, gu.fmt, gu.out_features, gu.in_features, True,
-                                       s.act, zero=zero_qkv)
+                                       s.act, zero=zero_qkv, ss=ss_all[2 * li + 1] if defer else None)
                 residual = r2
                 ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=accP)
                 self._reduce(accD, dn)

@@ -114,7 +114,8 @@ def _(x, router, k, renorm, scoring, e0, num_local, counter):
 
 @register_fake("ipex_llm_amd::rope_kv_fused")
 def _(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm, norm_eps, q_scale, Hq,
-      Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale, pos_offset=None, zero_part=False):
+      Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale, pos_offset=None, zero_part=False, pss=None, pss_n=0,
+      pss_eps=0.0):
     return None
 
 
@@ -124,14 +125,15 @@ def _(x, blob, fmt, n, k, acc, ksplit, zero=None):
 
 
 @register_fake("ipex_llm_amd::gemv_norm_in")
-def _(acc_in, residual, res_out, norm_w, eps, unit_offset, blob, fmt, n, k, epi, act, acc_out=None, zero=None):
+def _(acc_in, residual, res_out, norm_w, eps, unit_offset, blob, fmt, n, k, epi, act, acc_out=None, zero=None,
+      ss=None):
     if epi == 2:
         return residual.new_empty((residual.numel() // k, n // 2))
     return torch.empty_like(acc_out)
 
 
 @register_fake("ipex_llm_amd::gemv_glu_in")
-def _(part, blob, fmt, n, k, act, ksplit, dtype, acc=None, zero=None):
+def _(part, blob, fmt, n, k, act, ksplit, dtype, acc=None, zero=None, xss=None, xss_n=0, xss_eps=0.0):
     if acc is not None:
         return acc
     return part.new_empty((max(ksplit, 1), part.shape[1], n), dtype=torch.float32)
@@ -166,13 +168,13 @@ def _(x, blob, fmt, n, k, bias):
 
 @register_fake("ipex_llm_amd::attn_decode_rope")
 def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, Hq,
-      rot_dim, interleaved, q_scale, dtype):
+      rot_dim, interleaved, q_scale, dtype, pss=None, pss_n=0, pss_eps=0.0):
     return part.new_empty((part.shape[0], 1, Hq, k_cache.shape[3]), dtype=dtype)
 
 
 @register_fake("ipex_llm_amd::attn_decode_rope_split")
 def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, Hq,
-      rot_dim, interleaved, q_scale, dtype):
+      rot_dim, interleaved, q_scale, dtype, pss=None, pss_n=0, pss_eps=0.0):
     B, D = part.shape[0], k_cache.shape[3]
     return (part.new_empty((B, Hq, 1, nsplit, D)), part.new_empty((B, Hq, 1, nsplit, 2)))
 

@@ -239,17 +239,39 @@ def gemv_accum(x, blob, fmt, n, k, acc: torch.Tensor, ksplit: int = 0,
 
 def gemv_norm_in(acc_in: torch.Tensor, residual: torch.Tensor, res_out: torch.Tensor, norm_w: torch.Tensor,
                  eps: float, unit_offset: bool, blob, fmt, n, k, glu: bool, act: int = 0,
-                 acc_out: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 acc_out: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None,
+                 ss: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Decode projection of rms_norm(residual + acc_in) * norm_w with the
     residual add and the norm done in the GEMV prologue (no norm launch):
     res_out = residual + acc_in; returns act(gate)*up (``glu``) or acc_out
-    += x @ W^T (atomics).  acc_in is only read; ``zero`` is zeroed first."""
+    += x @ W^T (atomics).  acc_in is only read; ``zero`` is zeroed first.
+
+    ``ss`` (f32 [M], zero on entry): deferred norm -- the atomic output is
+    W (w * h) without the 1/rms row scale, ss receives the per-row sum of
+    squares of h and the consumer (rope_kv_fused / attn_decode_rope /
+    gemv_glu_in with pss/xss) applies rsqrt(ss / k + eps); a GLU launch
+    applies it itself before the activation."""
     if _native(residual):
         return _ops().gemv_norm_in(acc_in, residual, res_out, norm_w, eps, unit_offset, blob, fmt, n, k,
-                                   2 if glu else 3, act, acc_out, zero)
+                                   2 if glu else 3, act, acc_out, zero, ss)
     if zero is not None:
         zero.zero_()
     x = acc_in.to(residual.dtype).view_as(residual)
+    if ss is not None:
+        h = (x + residual).to(residual.dtype)
+        res_out.copy_(h)
+        w = norm_w.float() + 1.0 if unit_offset else norm_w.float()
+        xp = (w.to(residual.dtype).float() * h.float()).to(residual.dtype)
+        sq = h.float().pow(2).sum(-1)
+        if glu:
+            from ..models.decoder import deinterleave_glu
+            inv = torch.rsqrt(sq / k + eps)[:, None]
+            g, u = deinterleave_glu(lowbit_matmul(xp, blob, fmt, n, k).float())
+            g, u = g * inv, u * inv
+            return ((F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")) * u).to(residual.dtype).contiguous()
+        ss[:sq.numel()] += sq
+        acc_out += lowbit_matmul(xp, blob, fmt, n, k).float().view_as(acc_out)
+        return acc_out
     normed, new_res = R.add_rms_norm(x, residual, norm_w, eps, unit_offset)
     res_out.copy_(new_res)
     if glu:
@@ -266,15 +288,21 @@ def gemv_glu(x, blob, fmt, n, k, act: int = 0) -> torch.Tensor:
 
 
 def gemv_glu_in(part, blob, fmt, n, k, act: int = 0, ksplit: int = 0, dtype=torch.bfloat16,
-                acc: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None) -> torch.Tensor:
+                acc: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None,
+                xss: Optional[torch.Tensor] = None, xss_n: int = 0, xss_eps: float = 0.0) -> torch.Tensor:
     """down-projection over act(gate)*up taken straight from the gate/up
     GEMV's split-K slabs (or atomic accumulator) ``part`` [ns, M, 2k];
     returns f32 slabs [ks, M, n], or ``acc`` [M, n] += the product (atomics).
-    ``zero`` (a buffer whose readers are done) is zeroed by the launch."""
+    ``zero`` (a buffer whose readers are done) is zeroed by the launch.
+    ``xss``: deferred-norm sums of squares of the gate/up input (rows scaled by
+    rsqrt(xss / xss_n + xss_eps) before the activation)."""
     if _native(part):
-        return _ops().gemv_glu_in(part, blob, fmt, n, k, act, ksplit, dtype, acc, zero)
+        return _ops().gemv_glu_in(part, blob, fmt, n, k, act, ksplit, dtype, acc, zero, xss, xss_n, xss_eps)
     from ..models.decoder import deinterleave_glu
-    g, u = deinterleave_glu(part.sum(0))
+    ps = part.sum(0)
+    if xss is not None:
+        ps = ps * torch.rsqrt(xss[:ps.shape[0]] / xss_n + xss_eps)[:, None]
+    g, u = deinterleave_glu(ps)
     a = ((F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")) * u).to(dtype)
     if zero is not None:
         zero.zero_()
@@ -467,16 +495,20 @@ def rope_kv(qkv, q_out, k_cache, v_cache, slots, pos, inv_freq, Hq, Hkv, D, rot_
 
 def rope_kv_fused(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, Hq, Hkv, D, rot_dim=None,
                   interleaved=False, q_norm=None, k_norm=None, norm_eps=1e-6, q_scale=1.0, kv_fp8=0,
-                  k_scale=1.0, v_scale=1.0, pos_offset=None, zero_part=False):
+                  k_scale=1.0, v_scale=1.0, pos_offset=None, zero_part=False, pss=None, pss_n=0, pss_eps=0.0):
     """rope_kv over the split-K partials of the QKV GEMV ([ks, T, N] f32,
-    summed + bias in the kernel) with device-side slots from the block table."""
+    summed + bias in the kernel) with device-side slots from the block table.
+    ``pss``: deferred-norm sums of squares of the qkv input (row t scaled by
+    rsqrt(pss[t] / pss_n + pss_eps) before the bias)."""
     rot_dim = rot_dim or D
     if _native(part):
         _ops().rope_kv_fused(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_norm, k_norm,
                              norm_eps, q_scale, Hq, Hkv, D, rot_dim, interleaved, kv_fp8, k_scale, v_scale,
-                             pos_offset, zero_part)
+                             pos_offset, zero_part, pss, pss_n, pss_eps)
         return q_out
     qkv = part.sum(0)
+    if pss is not None:
+        qkv = qkv * torch.rsqrt(pss[:qkv.shape[0]] / pss_n + pss_eps)[:, None]
     if zero_part:
         part.zero_()
     if bias is not None:
@@ -544,12 +576,14 @@ def attn_prefill(q, k_cache, v_cache, block_tables, seq_lens, Tq: int, scale: fl
 
 def attn_decode_rope(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
                      softcap, window, Hq: int, rot_dim: int, interleaved: bool, q_scale: float = 1.0,
-                     dtype=torch.bfloat16):
+                     dtype=torch.bfloat16, pss=None, pss_n: int = 0, pss_eps: float = 0.0):
     """Decode attention (one new token per sequence) with the RoPE of q/k and
     the KV append fused in, reading q/k/v from the qkv GEMV's f32
-    accumulator ``part`` [B, (Hq + 2 Hkv) * D].  Returns [B, 1, Hq, D]."""
+    accumulator ``part`` [B, (Hq + 2 Hkv) * D].  Returns [B, 1, Hq, D].
+    ``pss``: deferred-norm row sums of squares (see gemv_norm_in)."""
     return _ops().attn_decode_rope(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit,
-                                   scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dtype)
+                                   scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dtype, pss, pss_n,
+                                   pss_eps)
 
 
 def attn_decode_split(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap=0.0, window=0,

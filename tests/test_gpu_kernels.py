@@ -118,6 +118,74 @@ def test_gemv_norm_in(cuda, name, M):
     assert torch.equal(res_out2, res_ref)
 
 
+@pytest.mark.parametrize("name", ["sym_int4", "nf4"])
+@pytest.mark.parametrize("M", [1, 4, 8])
+def test_gemv_norm_in_deferred(cuda, name, M):
+    """deferred RMSNorm: the GEMV stages w * h of its K slice only and reports
+    the row sums of squares; the consumer-side row scale (rope_kv_fused pss,
+    gemv_glu_in xss) or the GLU epilogue reproduces the normalised path"""
+    from ipex_llm_amd.models.decoder import interleave_glu_rows
+    f = get_format(name).fmt
+    torch.manual_seed(3)
+    H, n, I = 1024, 768, 256
+    acc_in = torch.randn(M, H, device=cuda) * 0.5
+    res = torch.randn(M, H, device=cuda).bfloat16()
+    wn = (torch.rand(H, device=cuda) + 0.5).bfloat16()
+    blob = ops.quantize(torch.randn(n, H, device=cuda) * 0.05, f)
+    res_ref = res.clone()
+    normed, _ = ops.add_rms_norm(None, res_ref, wn, 1e-5, partials=acc_in.unsqueeze(0))
+    h = (acc_in.bfloat16() + res).float()
+    acc_out, res_out = torch.zeros(M, n, device=cuda), torch.empty_like(res)
+    ss = torch.zeros(M, device=cuda)
+    ops.gemv_norm_in(acc_in, res, res_out, wn, 1e-5, False, blob, f, n, H, False, acc_out=acc_out, ss=ss)
+    assert torch.equal(res_out, res_ref)
+    assert torch.allclose(ss, h.bfloat16().float().pow(2).sum(-1), rtol=1e-4)
+    inv = torch.rsqrt(ss / H + 1e-5)[:, None]
+    ref = ops.gemv_partials(normed, blob, f, n, H, 1)[0]
+    assert _rel(acc_out * inv, ref) < 1e-2, (name, M)
+    # GLU: the epilogue applies the scale itself
+    gu = ops.quantize(interleave_glu_rows(torch.randn(I, H, device=cuda) * 0.05,
+                                          torch.randn(I, H, device=cuda) * 0.05), f)
+    y = ops.gemv_norm_in(acc_in, res, torch.empty_like(res), wn, 1e-5, False, gu, f, 2 * I, H, True, 0,
+                         ss=torch.zeros(M, device=cuda))
+    assert _rel(y, ops.gemv_glu(normed, gu, f, 2 * I, H, 0)) < 1.5e-2, (name, M)
+    # gate/up accumulated unscaled -> down GEMV scales before the activation
+    gacc = torch.zeros(M, 2 * I, device=cuda)
+    gss = torch.zeros(M, device=cuda)
+    ops.gemv_norm_in(acc_in, res, torch.empty_like(res), wn, 1e-5, False, gu, f, 2 * I, H, False, acc_out=gacc,
+                     ss=gss)
+    dn = ops.quantize(torch.randn(H, I, device=cuda) * 0.05, f)
+    d_def = ops.gemv_glu_in(gacc.unsqueeze(0), dn, f, H, I, 0, 0, torch.bfloat16, xss=gss, xss_n=H, xss_eps=1e-5)
+    d_ref = ops.gemv_glu_in((gacc * torch.rsqrt(gss / H + 1e-5)[:, None]).unsqueeze(0), dn, f, H, I, 0, 0,
+                            torch.bfloat16)
+    assert _rel(d_def.sum(0), d_ref.sum(0)) < 1e-3
+
+
+def test_rope_kv_fused_deferred_scale(cuda):
+    """rope_kv_fused with pss == rope_kv_fused over the pre-scaled accumulator"""
+    torch.manual_seed(5)
+    T, Hq, Hkv, D, bs = 4, 8, 2, 128, 16
+    N = (Hq + 2 * Hkv) * D
+    part = torch.randn(T, N, device=cuda) * 3
+    ss = torch.rand(T, device=cuda) * 4096 + 100
+    bias = (torch.randn(N, device=cuda) * 0.1).bfloat16()
+    inv = torch.rsqrt(ss / 1024 + 1e-5)[:, None]
+    pos = torch.tensor([3, 9, 17, 30], device=cuda)
+    bt = torch.arange(8, device=cuda, dtype=torch.int32).view(4, 2)
+    table = torch.randn(64, D // 2, 2, device=cuda)
+    outs = []
+    for scaled in (False, True):
+        kc = torch.zeros(8, Hkv, bs, D, device=cuda, dtype=torch.bfloat16)
+        vc = torch.zeros_like(kc)
+        q = torch.empty(T, Hq, D, device=cuda, dtype=torch.bfloat16)
+        p = (part * inv if scaled else part.clone()).unsqueeze(0).contiguous()
+        ops.rope_kv_fused(p, bias, q, kc, vc, pos, bt, 1, table, Hq, Hkv, D,
+                          pss=None if scaled else ss, pss_n=1024, pss_eps=1e-5)
+        outs.append((q, kc, vc))
+    for a, b in zip(*outs):
+        assert _rel(a.float(), b.float()) < 5e-3
+
+
 @pytest.mark.parametrize("B,interleaved,Hq,Hkv", [(1, False, 8, 2), (2, False, 8, 2), (2, True, 8, 2),
                                                    (2, False, 8, 8), (1, False, 4, 4), (2, False, 4, 2)])
 def test_attn_decode_rope_matches_rope_kv(cuda, B, interleaved, Hq, Hkv):

@@ -24,11 +24,14 @@ struct Shape { const char* name; int N, K; bool glu; };
 
 int main(int argc, char** argv) {
   const Shape shapes[] = {{"qkv", 6144, 4096, false}, {"o", 4096, 4096, false},
-                          {"gate_up", 28672, 4096, true}, {"down", 4096, 14336, false}};
+                          {"gate_up", 28672, 4096, true}, {"down", 4096, 14336, false},
+                          {"gate_up_acc", 28672, 4096, false}};
   const int Ms[] = {1, 8};
-  float *nacc, *accout;
+  float *nacc, *accout, *ssbuf;
   uint16_t *x, *res, *res2, *nw, *yout;
   CK(hipMalloc(&nacc, 16 * 16384 * 4));
+  CK(hipMalloc(&ssbuf, 64 * 4));
+  CK(hipMemset(ssbuf, 0, 64 * 4));
   CK(hipMalloc(&accout, 16 * 32768 * 4));
   CK(hipMalloc(&x, 16 * 16384 * 2));
   CK(hipMalloc(&res, 16 * 16384 * 2));
@@ -48,6 +51,19 @@ int main(int argc, char** argv) {
   // sweep: (shape, M, normin, kw, nw, ks); 0 = the production plan5 value
   struct Cfg { int shape, M, normin, kw, nw, ks; };
   std::vector<Cfg> cfgs;
+  const char* mode = getenv("PROBE_MODE");
+  if (mode && mode[0] == 'd') {
+    // deferred vs full-row norm-in vs plain input, production geometry
+    for (int M : {1, 2, 4, 8}) {
+      for (int ni = 0; ni < 3; ni++) {
+        cfgs.push_back({0, M, ni, 0, 0, 0});
+        cfgs.push_back({2, M, ni, 0, 0, 0});
+        cfgs.push_back({4, M, ni, 0, 0, 0});
+      }
+      cfgs.push_back({1, M, 0, 0, 0, 0});
+      cfgs.push_back({3, M, 0, 0, 0, 0});
+    }
+  } else {
   for (int M : Ms) {
     cfgs.push_back({0, M, 0, 0, 0, 0});
     cfgs.push_back({0, M, 1, 0, 0, 0});
@@ -59,6 +75,7 @@ int main(int argc, char** argv) {
     for (int kwv : {1, 2, 4}) for (int nwv : {4, 8}) cfgs.push_back({2, M, 0, kwv, nwv, 0});
     cfgs.push_back({3, M, 0, 0, 0, 0});
     for (int ks : {4, 7, 8, 14, 16}) for (int nwv : {4, 8}) cfgs.push_back({3, M, 0, 1, nwv, ks});
+  }
   }
   int cur_shape = -1;
   uint8_t* wbuf = nullptr;
@@ -85,7 +102,7 @@ int main(int argc, char** argv) {
         unsigned gx, gy;
         size_t sh;
         if (s.glu) {
-          kw = M <= 2 ? 4 : 2;
+          kw = 2;
           nwv = M <= 2 ? 4 : 8;
           while (kw > 1 && KC / kw < 4) kw /= 2;
           if (c.kw) kw = c.kw;
@@ -97,8 +114,8 @@ int main(int argc, char** argv) {
           a.N = s.N / 2; a.out = yout; a.ldo = s.N / 2; epi = EPI_GLU;
         } else {
           kw = 1;
-          nwv = M >= 4 ? 8 : 4;
-          const int target = M <= 2 ? 8 : 4;
+          nwv = (M >= 4 || NT <= 256) ? 8 : 4;
+          const int target = KC >= 64 ? 7 : 4;
           int ks = std::min(32, std::max(1, (KC + target - 1) / target));
           while (ks > 1 && NT * ks > 4096) ks /= 2;
           while (shmem5(M, (KC + ks - 1) / ks) > 65536 && ks < KC) ks *= 2;
@@ -115,6 +132,7 @@ int main(int argc, char** argv) {
         a.nw = nwv;
         if (normin) {
           a.nacc = nacc; a.nres = res; a.nres_out = res2; a.nweight = nw; a.neps = 1e-5f;
+          if (normin == 2) { a.ndefer = 1; a.nss = ssbuf; }
         } else {
           a.x = x;
         }
