@@ -363,7 +363,16 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     auto lane_rot = [&](int col0, float scale_out, uint4* outf) {
       float v[KSTEP][8];
       lane_raw(col0, v);
-      if (a.rq_rot == D && !a.rq_interleaved) {
+      if (a.rq_prerot) {
+        // the qkv GEMV rotated its partial sums: round, scale, pack
+#pragma unroll
+        for (int s = 0; s < KSTEP; s++) {
+          uint32_t w[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) w[j] = pack2<T>(v[s][2 * j] * scale_out, v[s][2 * j + 1] * scale_out);
+          outf[s] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      } else if (a.rq_rot == D && !a.rq_interleaved) {
         constexpr int HS = KSTEP / 2;
         const float4* csp = (const float4*)a.rq_cos_sin + (size_t)rpos * (D / 4);   // float2 pairs, 2 per float4
 #pragma unroll

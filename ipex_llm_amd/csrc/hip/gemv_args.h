@@ -109,6 +109,14 @@ struct GemvArgs {
   const float* xpss;
   int xpss_n;
   float xpss_eps;
+  // NeoX RoPE applied to the split-K partial sums before the atomic add
+  // (rotation is linear, so the accumulator ends up holding rotated q / k):
+  // output columns [0, rcols) are heads of rD dims, rotated at position
+  // rpos[m] with the f32 (cos, sin) table rcs [max_pos][rD / 2][2]; needs
+  // head-aligned workgroup column blocks (TG * TPW * 16 a multiple of rD)
+  const float* rcs;
+  const int64_t* rpos;
+  int rcols, rD;
 };
 
 }  // namespace illm

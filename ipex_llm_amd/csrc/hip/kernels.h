@@ -176,6 +176,7 @@ struct AttnDecodeArgs {
   const int64_t* rq_pos;    // [B] rotary positions
   int rq_ld, rq_rot, rq_interleaved;
   float rq_qscale;
+  int rq_prerot;            // rq_part already holds rotated q / k (RoPE in the qkv GEMV epilogue)
   int num_blocks;           // cache blocks: block-table entries are bounds-checked
   int* err;                 // kernel error word or null
 };

@@ -164,7 +164,12 @@ __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
 #ifndef ILLM_GEMV5_MINW
 #define ILLM_GEMV5_MINW 1
 #endif
-template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4>
+// scale words shared across lanes (SCL above); ILLM_GEMV5_SCL=0 at build time
+// restores the per-lane scale loads in the chunk ring
+#ifndef ILLM_GEMV5_SCL
+#define ILLM_GEMV5_SCL 0
+#endif
+template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4, bool SCL = ILLM_GEMV5_SCL != 0>
 __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(const GemvArgs a) {
   // PF: chunks in flight per wave (4; 8 = every chunk of a decode split-K
   // slice of <= 8 chunks requested before the prologue)
@@ -229,10 +234,15 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
 #pragma unroll
   for (int t = 0; t < TPW; t++) tb[t] = wbase + (size_t)min(tile0 + t, NT - 1) * TB;
 
+  // SCL: the 16 lanes that share a k-group g hold the scale words of 16
+  // consecutive chunks (lane 16 g + j: chunk sw0 + j, rows 4g..4g+3) instead of
+  // each lane re-loading its chunk's word into the ring: a chunk in flight
+  // costs 4 VGPRs (codes) instead of 8, so twice the chunks fit in flight;
+  // the word is fetched with a ds_bpermute when the chunk is computed
   struct Chunk {
     uint4 q[TPW][BITS / 4];
-    uint4 sc[TPW];
-    uint4 mn[TPW];
+    uint4 sc[SCL ? 1 : TPW];
+    uint4 mn[(SCL || !HASMIN) ? 1 : TPW];
   };
   auto load_chunk = [&](Chunk& ch, int c) {
     c = min(c, wc1 - 1);
@@ -241,12 +251,25 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
       const uint8_t* rec = tb[t] + (size_t)c * dk_code_chunk(DK);
       ch.q[t][0] = ldw16(rec + lane * 16);
       if constexpr (BITS == 8) ch.q[t][1] = ldw16(rec + 1024 + lane * 16);
-      ch.sc[t] = ldw16(tb[t] + soff + (size_t)c * 64);
-      if constexpr (HASMIN) ch.mn[t] = ldw16(tb[t] + moff + (size_t)c * 64);
+      if constexpr (!SCL) {
+        ch.sc[t] = ldw16(tb[t] + soff + (size_t)c * 64);
+        if constexpr (HASMIN) ch.mn[t] = ldw16(tb[t] + moff + (size_t)c * 64);
+      }
+    }
+  };
+  uint4 scl[TPW], mnl[TPW];
+  const int sw0 = wc0;
+  auto load_scl = [&](int cb) {
+    const int cc = min(cb + r16, wc1 - 1);
+#pragma unroll
+    for (int t = 0; t < TPW; t++) {
+      scl[t] = ldw16(tb[t] + soff + (size_t)cc * 64);
+      if constexpr (HASMIN) mnl[t] = ldw16(tb[t] + moff + (size_t)cc * 64);
     }
   };
   Chunk ring[PF];
   if (wave_on) {
+    if constexpr (SCL) load_scl(wc0);
 #pragma unroll
     for (int u = 0; u < PF; u++) load_chunk(ring[u], wc0 + u);
   }
@@ -530,8 +553,9 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
     auto compute_chunk = [&](const Chunk& ch, int c) {
       if constexpr ((ILLM_GEMV5_ABL & 1) != 0) {
 #pragma unroll
-        for (int t = 0; t < TPW; t++)
-          acc[t][0] += __uint_as_float((ch.q[t][0].x ^ ch.q[t][0].y ^ ch.q[t][0].z ^ ch.q[t][0].w ^ ch.sc[t].x) & 0x3fffffu);
+        for (int t = 0; t < TPW; t++)        // every tile folds into acc[0]: no load is dead
+          acc[0][0] += __uint_as_float((ch.q[t][0].x ^ ch.q[t][0].y ^ ch.q[t][0].z ^ ch.q[t][0].w ^
+                                        (SCL ? scl[t].x : ch.sc[t].x)) & 0x3fffffu);
         return;
       }
       const uint16_t* xc = xrow + (c - c0) * 128;
@@ -539,6 +563,26 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
 #pragma unroll
       for (int s = 0; s < 4; s++) B[s] = *(const uint4*)(xc + 32 * s);
       const float4 sx = srow[c - c0];
+      uint4 scv[TPW], mnv[TPW];
+      if constexpr (SCL) {
+        // one window covers the wave's chunk range (launch guarantees <= 16 chunks:
+        // a reload here would make hipcc wait for every load in flight)
+        const int src = (16 * g + (c - sw0)) * 4;
+#pragma unroll
+        for (int t = 0; t < TPW; t++) {
+          scv[t] = make_uint4(__builtin_amdgcn_ds_bpermute(src, scl[t].x), __builtin_amdgcn_ds_bpermute(src, scl[t].y),
+                              __builtin_amdgcn_ds_bpermute(src, scl[t].z), __builtin_amdgcn_ds_bpermute(src, scl[t].w));
+          if constexpr (HASMIN)
+            mnv[t] = make_uint4(__builtin_amdgcn_ds_bpermute(src, mnl[t].x), __builtin_amdgcn_ds_bpermute(src, mnl[t].y),
+                                __builtin_amdgcn_ds_bpermute(src, mnl[t].z), __builtin_amdgcn_ds_bpermute(src, mnl[t].w));
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < TPW; t++) {
+          scv[t] = ch.sc[t];
+          if constexpr (HASMIN) mnv[t] = ch.mn[t];
+        }
+      }
 #pragma unroll
       for (int t = 0; t < TPW; t++) {
 #pragma unroll
@@ -560,14 +604,14 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
           }
           const float nsx = blk == 0 ? sx.x : sx.y;
           const float sxv = blk == 0 ? sx.z : sx.w;
-          const uint32_t scw[4] = {ch.sc[t].x, ch.sc[t].y, ch.sc[t].z, ch.sc[t].w};
+          const uint32_t scw[4] = {scv[t].x, scv[t].y, scv[t].z, scv[t].w};
 #pragma unroll
           for (int i = 0; i < 4; i++) {
             const float d = f16_to_f32((uint16_t)(scw[i] >> (16 * blk)));
             if constexpr (OFF != 0.f) acc[t][i] = __builtin_fmaf(d, P[i] + nsx, acc[t][i]);
             else acc[t][i] = __builtin_fmaf(d, P[i], acc[t][i]);
             if constexpr (HASMIN) {
-              const uint32_t mnw[4] = {ch.mn[t].x, ch.mn[t].y, ch.mn[t].z, ch.mn[t].w};
+              const uint32_t mnw[4] = {mnv[t].x, mnv[t].y, mnv[t].z, mnv[t].w};
               acc[t][i] = __builtin_fmaf(f16_to_f32((uint16_t)(mnw[i] >> (16 * blk))), sxv, acc[t][i]);
             }
           }
@@ -640,7 +684,19 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
     float* ws = (float*)a.out;
     for (int v = threadIdx.x; v < Mloc * NC; v += NW * 64) {
       const int m = v / NC, n = nb + v % NC;
-      if (n < a.N) __hip_atomic_fetch_add(ws + (size_t)m * a.N + n, tbuf[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (n < a.N) {
+        float val = tbuf[v];
+        if (a.rcs != nullptr && n < a.rcols) {
+          // rotate_half RoPE of this workgroup's partial (partner column in the
+          // same head, same LDS row); cos/sin rounded to T as HF casts them
+          const int half = a.rD >> 1, d = n % a.rD, i = d % half;
+          const float2 cs = ((const float2*)a.rcs)[(size_t)a.rpos[m] * half + i];
+          const float c = to_f32<T>(from_f32<T>(cs.x)), sn = to_f32<T>(from_f32<T>(cs.y));
+          const float pv = tbuf[d < half ? v + half : v - half];
+          val = d < half ? val * c - pv * sn : val * c + pv * sn;
+        }
+        __hip_atomic_fetch_add(ws + (size_t)m * a.N + n, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     return;
   }
@@ -711,18 +767,33 @@ inline void launch5(K kern, dim3 grid, size_t shmem, const GemvArgs& a, hipStrea
   hipLaunchKernelGGL(kern, grid, dim3(64 * (a.nw == 8 ? 8 : 4)), shmem, st, a);
 }
 
-template <int DK, typename T, int KW, bool MOE, int NW>
-inline void launch5_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+// chunks in flight per wave: 8 with the shared scale window (same ring VGPRs
+// as 4 with per-lane scale words); ILLM_GEMV5_PFD overrides at build time
+#ifndef ILLM_GEMV5_PFD
+#define ILLM_GEMV5_PFD (ILLM_GEMV5_SCL ? 8 : 4)
+#endif
+template <int DK, typename T, int KW, bool MOE, int NW, bool S>
+inline void launch5_epi_s(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  constexpr int PFD = S ? ILLM_GEMV5_PFD : 4;
   // all loads of a short split-K slice up front (decode projections: 8 chunks)
   const bool pf8 = a.pf8 && !MOE && KW == 1 && a.cpk > 0 && a.cpk <= 8;
-  if (epi == EPI_STORE) launch5(lowbit_gemv5_kernel<DK, T, EPI_STORE, 1, KW, MOE, NW>, grid, shmem, a, st);
+  if (epi == EPI_STORE) launch5(lowbit_gemv5_kernel<DK, T, EPI_STORE, 1, KW, MOE, NW, PFD, S>, grid, shmem, a, st);
   else if (epi == EPI_PARTIAL) {
-    if (pf8) launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, NW, 8>, grid, shmem, a, st);
-    else launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, NW>, grid, shmem, a, st);
+    if (pf8) launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, NW, 8, S>, grid, shmem, a, st);
+    else launch5(lowbit_gemv5_kernel<DK, T, EPI_PARTIAL, 1, KW, MOE, NW, PFD, S>, grid, shmem, a, st);
   } else if (epi == EPI_ATOMIC) {
-    if (pf8) launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, NW, 8>, grid, shmem, a, st);
-    else launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, NW>, grid, shmem, a, st);
-  } else launch5(lowbit_gemv5_kernel<DK, T, EPI_GLU, 2, KW, MOE, NW>, grid, shmem, a, st);
+    if (pf8) launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, NW, 8, S>, grid, shmem, a, st);
+    else launch5(lowbit_gemv5_kernel<DK, T, EPI_ATOMIC, 1, KW, MOE, NW, PFD, S>, grid, shmem, a, st);
+  } else launch5(lowbit_gemv5_kernel<DK, T, EPI_GLU, 2, KW, MOE, NW, PFD, S>, grid, shmem, a, st);
+}
+
+template <int DK, typename T, int KW, bool MOE, int NW>
+inline void launch5_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  // the shared scale window holds 16 chunks: longer per-wave ranges keep the
+  // per-lane scale words
+  const int cpk = a.cpk > 0 ? a.cpk : (a.KC + (int)grid.y - 1) / (int)grid.y;
+  if (ILLM_GEMV5_SCL && (cpk + KW - 1) / KW > 16) return launch5_epi_s<DK, T, KW, MOE, NW, false>(epi, grid, shmem, a, st);
+  return launch5_epi_s<DK, T, KW, MOE, NW, ILLM_GEMV5_SCL != 0>(epi, grid, shmem, a, st);
 }
 
 template <int DK, typename T, bool MOE>

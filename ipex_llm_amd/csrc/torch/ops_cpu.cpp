@@ -147,14 +147,14 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("attn_decode_split(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int kv_fp8, float k_scale, float v_scale, Tensor? alibi) -> (Tensor, Tensor)");
   m.def("gemv_attn(Tensor po, Tensor pml, Tensor seq_lens, Tensor blob, int fmt, int n, int k, Tensor(a!)? acc, int ksplit, ScalarType dtype, Tensor(b!)? zero=None, int nw=0) -> Tensor");
   m.def("gemm(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias) -> Tensor");
-  m.def("gemv_accum(Tensor x, Tensor blob, int fmt, int n, int k, Tensor(a!) acc, int ksplit, Tensor(b!)? zero=None) -> ()");
-  m.def("attn_decode_rope(Tensor part, Tensor? bias, Tensor cos_sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int Hq, int rot_dim, bool interleaved, float q_scale, ScalarType dtype, Tensor? pss=None, int pss_n=0, float pss_eps=0.0) -> Tensor");
+  m.def("gemv_accum(Tensor x, Tensor blob, int fmt, int n, int k, Tensor(a!) acc, int ksplit, Tensor(b!)? zero=None, Tensor? rope_cs=None, Tensor? rope_pos=None, int rope_cols=0, int rope_d=0) -> ()");
+  m.def("attn_decode_rope(Tensor part, Tensor? bias, Tensor cos_sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int Hq, int rot_dim, bool interleaved, float q_scale, ScalarType dtype, Tensor? pss=None, int pss_n=0, float pss_eps=0.0, bool prerot=False) -> Tensor");
   m.def("attn_decode_rope_split(Tensor part, Tensor? bias, Tensor cos_sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int Hq, int rot_dim, bool interleaved, float q_scale, ScalarType dtype, Tensor? pss=None, int pss_n=0, float pss_eps=0.0) -> (Tensor, Tensor)");
   m.def("gemm_glu(Tensor x, Tensor blob, int fmt, int n, int k, int act) -> Tensor");
   m.def("moe_gemm(Tensor x, Tensor blob, int fmt, int n, int k, Tensor off, Tensor rows, int xdiv, bool x_sorted, bool out_sorted, bool glu, int act, bool out_f32) -> Tensor");
   m.def("rwkv_wkv4(Tensor time_decay, Tensor time_first, Tensor k, Tensor v, Tensor(a!) num, Tensor(b!) den, Tensor(c!) mx) -> Tensor");
   m.def("rwkv_wkv5(Tensor w, Tensor u, Tensor r, Tensor k, Tensor v, Tensor(a!) state) -> Tensor");
-  m.def("gemv_norm_in(Tensor acc_in, Tensor residual, Tensor(a!) res_out, Tensor norm_w, float eps, bool unit_offset, Tensor blob, int fmt, int n, int k, int epi, int act, Tensor(b!)? acc_out=None, Tensor(c!)? zero=None, Tensor(d!)? ss=None) -> Tensor");
+  m.def("gemv_norm_in(Tensor acc_in, Tensor residual, Tensor(a!) res_out, Tensor norm_w, float eps, bool unit_offset, Tensor blob, int fmt, int n, int k, int epi, int act, Tensor(b!)? acc_out=None, Tensor(c!)? zero=None, Tensor(d!)? ss=None, Tensor? rope_cs=None, Tensor? rope_pos=None, int rope_cols=0, int rope_d=0) -> Tensor");
   m.def("embedding_lowbit(Tensor blob, int fmt, int n, int k, Tensor ids, ScalarType dtype) -> Tensor");
   m.def("moe_gemv(Tensor x, Tensor blob, int fmt, int n, int k, Tensor off, Tensor rows, int xdiv, int npairs, int epi, int ksplit, int act) -> Tensor");
   m.def("moe_combine(Tensor part, Tensor w, Tensor ids, int e0, int num_local, ScalarType dtype) -> Tensor");

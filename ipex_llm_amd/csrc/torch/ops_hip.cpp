@@ -150,6 +150,14 @@ Plan5 plan5(int64_t rows, int64_t groups, int64_t KC, bool can_split, int64_t ks
   return p;
 }
 
+// RoPE epilogue: 8-wave groups of one tile each = 128-column, head-aligned blocks
+Plan5 plan5_rope(Plan5 p, int64_t NT, int64_t rows) {
+  p.kw = 1;
+  p.nw = 8;
+  p.gx = (unsigned)((NT + 7) / 8);
+  return p;
+}
+
 Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k,
             const c10::optional<Tensor>& bias, int64_t epi, int64_t ksplit, int64_t act) {
   TORCH_CHECK(x.is_cuda() && blob.is_cuda(), "gemv: GPU tensors expected");
@@ -411,6 +419,25 @@ Tensor rwkv_wkv5(const Tensor& w, const Tensor& u, const Tensor& r, const Tensor
 // split-K GEMV accumulated with f32 atomics into acc [M, n] (zero on entry;
 // the consumer -- add_rms_norm / rope_kv_fused with zero_*=True -- reads the
 // single slab and re-zeroes it, so no ks-slab reduction is ever needed)
+// RoPE in the atomic GEMV epilogue (GemvArgs rcs): cos/sin table f32
+// [max_pos, D / 2, 2], positions int64 [M]; the plan must give head-aligned
+// 8-wave column blocks (128 columns: D in {64, 128})
+static bool set_rope(illm::GemvArgs& a, const c10::optional<Tensor>& cs, const c10::optional<Tensor>& pos,
+                     int64_t cols, int64_t D, int64_t M) {
+  if (!cs.has_value() || !cs->defined()) return false;
+  TORCH_CHECK(cs->is_cuda() && cs->scalar_type() == at::kFloat && cs->is_contiguous() && cs->dim() == 3 &&
+                  cs->size(1) * 2 == D && (D == 64 || D == 128),
+              "gemv rope: f32 cos/sin table [max_pos, D/2, 2] with D in {64, 128}");
+  TORCH_CHECK(pos.has_value() && pos->defined() && pos->scalar_type() == at::kLong && pos->numel() >= M,
+              "gemv rope: int64 positions [M]");
+  TORCH_CHECK(cols % D == 0 && cols <= a.N, "gemv rope: rotated columns must be whole heads");
+  a.rcs = cs->data_ptr<float>();
+  a.rpos = pos->data_ptr<int64_t>();
+  a.rcols = (int)cols;
+  a.rD = (int)D;
+  return true;
+}
+
 static void set_zero(illm::GemvArgs& a, const c10::optional<Tensor>& zero) {
   if (zero.has_value() && zero->defined()) {
     TORCH_CHECK(zero->is_cuda() && zero->scalar_type() == at::kFloat && zero->is_contiguous() &&
@@ -429,7 +456,8 @@ static void set_zero(illm::GemvArgs& a, const c10::optional<Tensor>& zero) {
 Tensor gemv_norm_in(const Tensor& acc_in, const Tensor& residual, Tensor& res_out, const Tensor& norm_w, double eps,
                     bool unit_offset, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t epi,
                     int64_t act, const c10::optional<Tensor>& acc_out, const c10::optional<Tensor>& zero,
-                    const c10::optional<Tensor>& ss) {
+                    const c10::optional<Tensor>& ss, const c10::optional<Tensor>& rope_cs,
+                    const c10::optional<Tensor>& rope_pos, int64_t rope_cols, int64_t rope_d) {
   TORCH_CHECK(acc_in.is_cuda() && blob.is_cuda() && residual.is_cuda(), "gemv_norm_in: GPU tensors expected");
   c10::DeviceGuard g(acc_in.device());
   const bool bf16 = is_bf16(residual);
@@ -488,7 +516,9 @@ Tensor gemv_norm_in(const Tensor& acc_in, const Tensor& residual, Tensor& res_ou
   a.N = (int)n;
   a.out = acc_out->data_ptr();
   a.ldo = (int)n;
-  const Plan5 p = plan5(M, NT, KC, true, 0, true);
+  const bool rope = set_rope(a, rope_cs, rope_pos, rope_cols, rope_d, M);
+  Plan5 p = plan5(M, NT, KC, true, 0, true);
+  if (rope) p = plan5_rope(p, NT, M);
   TORCH_CHECK(p.shmem <= kMaxLds, "gemv_norm_in: K slice too large for LDS");
   a.cpk = (int)p.cpk;
   a.nw = p.nw;
@@ -497,7 +527,8 @@ Tensor gemv_norm_in(const Tensor& acc_in, const Tensor& residual, Tensor& res_ou
 }
 
 void gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, Tensor& acc,
-                int64_t ksplit, const c10::optional<Tensor>& zero) {
+                int64_t ksplit, const c10::optional<Tensor>& zero, const c10::optional<Tensor>& rope_cs,
+                const c10::optional<Tensor>& rope_pos, int64_t rope_cols, int64_t rope_d) {
   TORCH_CHECK(x.is_cuda() && blob.is_cuda() && acc.is_cuda(), "gemv_accum: GPU tensors expected");
   c10::DeviceGuard g(x.device());
   const bool bf16 = is_bf16(x);
@@ -520,7 +551,9 @@ void gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   a.N = (int)n;
   a.out = acc.data_ptr();
   a.ldo = (int)n;
-  const Plan5 p = plan5(M, NT, KC, true, ksplit, true);
+  const bool rope = set_rope(a, rope_cs, rope_pos, rope_cols, rope_d, M);
+  Plan5 p = plan5(M, NT, KC, true, ksplit, true);
+  if (rope) p = plan5_rope(p, NT, M);
   a.cpk = (int)p.cpk;
   a.nw = p.nw;
   set_zero(a, zero);
@@ -853,7 +886,7 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
     const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin, const Tensor& pos, Tensor& k_cache,
     Tensor& v_cache, const Tensor& block_tables, const Tensor& seq_lens, int64_t nsplit, double scale, double softcap,
     int64_t window, int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt, bool no_combine,
-    const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps) {
+    const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps, bool prerot) {
   c10::DeviceGuard g(part.device());
   TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "attn_decode_rope: bf16/fp16 activations");
   TORCH_CHECK(k_cache.scalar_type() == dt && v_cache.scalar_type() == dt, "attn_decode_rope: 16-bit KV cache");
@@ -910,6 +943,8 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
   a.rq_rot = (int)rot_dim;
   a.rq_interleaved = interleaved ? 1 : 0;
   a.rq_qscale = (float)q_scale;
+  a.rq_prerot = prerot ? 1 : 0;
+  TORCH_CHECK(!prerot || (rot_dim == D && !interleaved), "attn_decode_rope: prerot needs full-width NeoX RoPE");
   if (pss.has_value() && pss->defined()) {
     TORCH_CHECK(pss->is_cuda() && pss->scalar_type() == at::kFloat && pss->numel() >= B && pss_n > 0,
                 "attn_decode_rope: pss must be f32 [B] with pss_n > 0");
@@ -925,10 +960,10 @@ Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, c
                         const Tensor& pos, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
                         const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
                         int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt,
-                        const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps) {
+                        const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps, bool prerot) {
   return std::get<0>(attn_decode_rope_impl(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit,
                                            scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dt, false, pss,
-                                           pss_n, pss_eps));
+                                           pss_n, pss_eps, prerot));
 }
 
 // fused-RoPE split attention without the combine: (o, m, l) partials for the
@@ -942,7 +977,8 @@ std::tuple<Tensor, Tensor> attn_decode_rope_split(const Tensor& part, const c10:
                                                   at::ScalarType dt, const c10::optional<Tensor>& pss,
                                                   int64_t pss_n, double pss_eps) {
   auto r = attn_decode_rope_impl(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
-                                 softcap, window, Hq, rot_dim, interleaved, q_scale, dt, true, pss, pss_n, pss_eps);
+                                 softcap, window, Hq, rot_dim, interleaved, q_scale, dt, true, pss, pss_n, pss_eps,
+                                 false);
   return {std::get<1>(r), std::get<2>(r)};
 }
 

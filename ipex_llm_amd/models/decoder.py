@@ -155,13 +155,24 @@ NORM_IN_MAX_M = int(__import__("os").environ.get("ILLM_NORM_IN_MAX_M", "2"))
 # GLU epilogue -- no full-row pass per workgroup, so the norm-in path extends
 # to larger decode batches (ILLM_DEFER_NORM=0 restores the full-row prologue)
 DEFER_NORM = __import__("os").environ.get("ILLM_DEFER_NORM", "1") != "0"
-DEFER_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_MAX_M", "4"))
+DEFER_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_MAX_M", "8"))
+# ... and up to this batch for the gate/up GLU launch too (every GLU workgroup
+# stages the full K of acc + residual: at batch 8 that replicated row read
+# costs more than the standalone norm launch, MI355X probe
+# profiles/gemv5_defer_r3.jsonl: GLU 24.7 us deferred vs 19.7 us on a normed x)
+DEFER_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_GLU_MAX_M", "4"))
 # decode batches up to this size take the fused-RoPE attention (qkv accumulated
 # atomically into one slab read by the attention, re-zeroed by its combine).
 # Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token,
 # batch 4 2.128 -> 2.109 ms/step; at batch 8 every split wave re-rotating q
 # costs more than the rope launch it saves (2.382 -> 2.527)
 ROPE_IN_MAX_M = int(__import__("os").environ.get("ILLM_ROPE_IN_MAX_M", "4"))
+# ... unless the qkv GEMV rotates q / k itself: RoPE is linear, so each
+# split-K workgroup rotates its partial before the atomic add (epilogue in
+# lowbit_gemv5.cuh) and the attention reads rotated q / k -- no per-split
+# re-rotation, no rope launch, at every decode batch up to ACC_MAX_M
+# (ILLM_GEMV_ROPE=0 keeps the rotation in the attention / rope kernels)
+GEMV_ROPE = __import__("os").environ.get("ILLM_GEMV_ROPE", "1") != "0"
 
 
 class NativeAttention(nn.Module):
@@ -465,6 +476,13 @@ class NativeCausalLM(nn.Module):
                 and ((s.head_dim == 128 and group <= 16) or (s.head_dim == 256 and group <= 8))
                 and all(L.self_attn.q_norm is None and L.self_attn.k_norm is None for L in self.layers))
 
+    def _qkv_bias_free(self) -> bool:
+        ok = self.__dict__.get("_qkv_nobias")
+        if ok is None:
+            ok = all(getattr(L.self_attn.qkv_proj, "bias", None) is None for L in self.layers)
+            self.__dict__["_qkv_nobias"] = ok
+        return ok
+
     def _qkv_native(self, ref: torch.Tensor) -> bool:
         """every layer's qkv projection runs the native atomic GEMV"""
         ok = self.__dict__.get("_qkv_native_ok")
@@ -563,7 +581,11 @@ class NativeCausalLM(nn.Module):
         # fused-RoPE decode attention (batch <= ROPE_IN_MAX_M, one token each): the qkv
         # GEMV accumulates into one atomic slab that the attention reads and the
         # combine launch re-zeroes
-        rope_in = T <= ROPE_IN_MAX_M and self._rope_in_ok(meta, cache) and self._qkv_native(residual)
+        rope_ok = self._rope_in_ok(meta, cache) and self._qkv_native(residual)
+        prerot = (GEMV_ROPE and rope_ok and T <= ACC_MAX_M and s.rot_dim == s.head_dim and not s.rope_interleaved
+                  and s.head_dim in (64, 128) and self._qkv_bias_free())
+        rope_in = rope_ok and (T <= ROPE_IN_MAX_M or prerot)
+        qrope = (self.rope_cache, pos, (s.num_heads + s.num_kv_heads) * s.head_dim, s.head_dim) if prerot else None
         nxt_res = lambda r: res_pp[1] if r is res_pp[0] else res_pp[0]
         zero_next = None                # consumed atomic slab the next accumulating GEMV zeroes
         from ..utils import trace as _trace
@@ -597,11 +619,11 @@ class NativeCausalLM(nn.Module):
                         ss_q = ss_all[2 * li] if defer else None
                         ops.gemv_norm_in(pend, residual, r2, layer.input_layernorm, s.rms_eps, s.norm_unit_offset,
                                          qp.weight, qp.fmt, qp.out_features, qp.in_features, False, acc_out=part,
-                                         ss=ss_q)
+                                         ss=ss_q, rope=qrope)
                         residual, consumed, pend = r2, pend, None
                     else:
                         ops.gemv_accum(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, part,
-                                       zero=zero_next)
+                                       zero=zero_next, rope=qrope)
                         zero_next = None
                     qkv_acc = part
                     part = part.unsqueeze(0)
@@ -618,7 +640,8 @@ class NativeCausalLM(nn.Module):
                                                   meta.block_tables, meta.seq_lens, meta.nsplit, s.scale,
                                                   s.attn_softcap, attn.sliding_window, s.num_heads, s.rot_dim,
                                                   s.rope_interleaved, 1.0, x.dtype, pss=ss_q,
-                                                  pss_n=s.hidden_size, pss_eps=s.rms_eps).view(T, -1)
+                                                  pss_n=s.hidden_size, pss_eps=s.rms_eps,
+                                                  prerot=prerot).view(T, -1)
             else:
                 qkv = qp(x)
                 ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,
@@ -650,13 +673,21 @@ class NativeCausalLM(nn.Module):
                     a = a_rope if rope_in else self._attention(li, attn, q, meta, cache)
                     ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
                 self._reduce(accP, o)
-                r2 = nxt_res(residual)
                 gu, dn = mlp.gate_up_proj, mlp.down_proj
-                act = ops.gemv_norm_in(accP, residual, r2, layer.post_attention_layernorm, s.rms_eps,
-                                       s.norm_unit_offset, gu.weight, gu.fmt, gu.out_features, gu.in_features, True,
-                                       s.act, zero=zero_qkv, ss=ss_all[2 * li + 1] if defer else None)
-                residual = r2
-                ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=accP)
+                if defer and T > DEFER_GLU_MAX_M:
+                    # standalone residual-add + norm (re-zeroes P), plain GLU GEMV
+                    xn, _ = ops.add_rms_norm(None, residual, layer.post_attention_layernorm, s.rms_eps,
+                                             partials=accP.unsqueeze(0), unit_offset=s.norm_unit_offset,
+                                             zero_partials=True)
+                    act = ops.gemv_glu(xn, gu.weight, gu.fmt, gu.out_features, gu.in_features, s.act)
+                    ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=zero_qkv)
+                else:
+                    r2 = nxt_res(residual)
+                    act = ops.gemv_norm_in(accP, residual, r2, layer.post_attention_layernorm, s.rms_eps,
+                                           s.norm_unit_offset, gu.weight, gu.fmt, gu.out_features, gu.in_features,
+                                           True, s.act, zero=zero_qkv, ss=ss_all[2 * li + 1] if defer else None)
+                    residual = r2
+                    ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=accP)
                 self._reduce(accD, dn)
                 consumed = None
                 if li + 1 < len(self.layers):

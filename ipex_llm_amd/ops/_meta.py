@@ -120,13 +120,13 @@ def _(part, bias, q_out, k_cache, v_cache, pos, block_tables, tq, inv_freq, q_no
 
 
 @register_fake("ipex_llm_amd::gemv_accum")
-def _(x, blob, fmt, n, k, acc, ksplit, zero=None):
+def _(x, blob, fmt, n, k, acc, ksplit, zero=None, rope_cs=None, rope_pos=None, rope_cols=0, rope_d=0):
     return None
 
 
 @register_fake("ipex_llm_amd::gemv_norm_in")
 def _(acc_in, residual, res_out, norm_w, eps, unit_offset, blob, fmt, n, k, epi, act, acc_out=None, zero=None,
-      ss=None):
+      ss=None, rope_cs=None, rope_pos=None, rope_cols=0, rope_d=0):
     if epi == 2:
         return residual.new_empty((residual.numel() // k, n // 2))
     return torch.empty_like(acc_out)
@@ -168,7 +168,7 @@ def _(x, blob, fmt, n, k, bias):
 
 @register_fake("ipex_llm_amd::attn_decode_rope")
 def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, Hq,
-      rot_dim, interleaved, q_scale, dtype, pss=None, pss_n=0, pss_eps=0.0):
+      rot_dim, interleaved, q_scale, dtype, pss=None, pss_n=0, pss_eps=0.0, prerot=False):
     return part.new_empty((part.shape[0], 1, Hq, k_cache.shape[3]), dtype=dtype)
 
 

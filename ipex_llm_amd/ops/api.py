@@ -224,23 +224,44 @@ def gemv_partials(x, blob, fmt, n, k, ksplit: int) -> torch.Tensor:
 
 
 def gemv_accum(x, blob, fmt, n, k, acc: torch.Tensor, ksplit: int = 0,
-               zero: Optional[torch.Tensor] = None) -> torch.Tensor:
+               zero: Optional[torch.Tensor] = None, rope=None) -> torch.Tensor:
     """acc [M, n] f32 (zero on entry) += x @ W^T via split-K f32 atomics; the
     consumer (add_rms_norm / rope_kv_fused with zero_*=True) re-zeroes it, or
-    a later launch does through ``zero`` (a buffer whose readers are done)."""
+    a later launch does through ``zero`` (a buffer whose readers are done).
+    ``rope`` = (cos_sin [max_pos, D/2, 2], pos [M], rotated columns, D): NeoX
+    RoPE applied to each split's partial before its atomic add (rotation is
+    linear), so ``acc`` ends up holding rotated q / k."""
     if _native(x):
-        _ops().gemv_accum(x, blob, fmt, n, k, acc, ksplit, zero)
+        rc, rp, rn, rd = rope if rope is not None else (None, None, 0, 0)
+        _ops().gemv_accum(x, blob, fmt, n, k, acc, ksplit, zero, rc, rp, rn, rd)
         return acc
     if zero is not None:
         zero.zero_()
-    acc += lowbit_matmul(x, blob, fmt, n, k).float().view_as(acc)
+    acc += _rope_cols(lowbit_matmul(x, blob, fmt, n, k).float(), rope, x.dtype).view_as(acc)
     return acc
+
+
+def _rope_cols(y: torch.Tensor, rope, dtype) -> torch.Tensor:
+    """fallback of the GEMV RoPE epilogue: rotate_half RoPE of the first
+    ``cols`` columns of y [M, n] (heads of D dims) at positions ``pos``"""
+    if rope is None:
+        return y
+    cs, pos, cols, D = rope
+    half = D // 2
+    tab = cs[pos.long()].to(dtype).float()                    # [M, half, 2], cos/sin rounded like HF
+    c = torch.cat([tab[..., 0], tab[..., 0]], -1)[:, None, :]
+    sn = torch.cat([tab[..., 1], tab[..., 1]], -1)[:, None, :]
+    h = y[:, :cols].reshape(y.shape[0], cols // D, D)
+    rot = torch.cat([-h[..., half:], h[..., :half]], -1)
+    y = y.clone()
+    y[:, :cols] = (h * c + rot * sn).reshape(y.shape[0], cols)
+    return y
 
 
 def gemv_norm_in(acc_in: torch.Tensor, residual: torch.Tensor, res_out: torch.Tensor, norm_w: torch.Tensor,
                  eps: float, unit_offset: bool, blob, fmt, n, k, glu: bool, act: int = 0,
                  acc_out: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None,
-                 ss: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 ss: Optional[torch.Tensor] = None, rope=None) -> torch.Tensor:
     """Decode projection of rms_norm(residual + acc_in) * norm_w with the
     residual add and the norm done in the GEMV prologue (no norm launch):
     res_out = residual + acc_in; returns act(gate)*up (``glu``) or acc_out
@@ -252,8 +273,9 @@ def gemv_norm_in(acc_in: torch.Tensor, residual: torch.Tensor, res_out: torch.Te
     gemv_glu_in with pss/xss) applies rsqrt(ss / k + eps); a GLU launch
     applies it itself before the activation."""
     if _native(residual):
+        rc, rp, rn, rd = rope if rope is not None else (None, None, 0, 0)
         return _ops().gemv_norm_in(acc_in, residual, res_out, norm_w, eps, unit_offset, blob, fmt, n, k,
-                                   2 if glu else 3, act, acc_out, zero, ss)
+                                   2 if glu else 3, act, acc_out, zero, ss, rc, rp, rn, rd)
     if zero is not None:
         zero.zero_()
     x = acc_in.to(residual.dtype).view_as(residual)
@@ -270,7 +292,7 @@ def gemv_norm_in(acc_in: torch.Tensor, residual: torch.Tensor, res_out: torch.Te
             g, u = g * inv, u * inv
             return ((F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")) * u).to(residual.dtype).contiguous()
         ss[:sq.numel()] += sq
-        acc_out += lowbit_matmul(xp, blob, fmt, n, k).float().view_as(acc_out)
+        acc_out += _rope_cols(lowbit_matmul(xp, blob, fmt, n, k).float(), rope, residual.dtype).view_as(acc_out)
         return acc_out
     normed, new_res = R.add_rms_norm(x, residual, norm_w, eps, unit_offset)
     res_out.copy_(new_res)
@@ -278,7 +300,7 @@ def gemv_norm_in(acc_in: torch.Tensor, residual: torch.Tensor, res_out: torch.Te
         from ..models.decoder import deinterleave_glu
         g, u = deinterleave_glu(lowbit_matmul(normed, blob, fmt, n, k))
         return ((F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")) * u).contiguous()
-    acc_out += lowbit_matmul(normed, blob, fmt, n, k).float().view_as(acc_out)
+    acc_out += _rope_cols(lowbit_matmul(normed, blob, fmt, n, k).float(), rope, residual.dtype).view_as(acc_out)
     return acc_out
 
 
@@ -576,14 +598,14 @@ def attn_prefill(q, k_cache, v_cache, block_tables, seq_lens, Tq: int, scale: fl
 
 def attn_decode_rope(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
                      softcap, window, Hq: int, rot_dim: int, interleaved: bool, q_scale: float = 1.0,
-                     dtype=torch.bfloat16, pss=None, pss_n: int = 0, pss_eps: float = 0.0):
+                     dtype=torch.bfloat16, pss=None, pss_n: int = 0, pss_eps: float = 0.0, prerot: bool = False):
     """Decode attention (one new token per sequence) with the RoPE of q/k and
     the KV append fused in, reading q/k/v from the qkv GEMV's f32
     accumulator ``part`` [B, (Hq + 2 Hkv) * D].  Returns [B, 1, Hq, D].
     ``pss``: deferred-norm row sums of squares (see gemv_norm_in)."""
     return _ops().attn_decode_rope(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit,
                                    scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dtype, pss, pss_n,
-                                   pss_eps)
+                                   pss_eps, prerot)
 
 
 def attn_decode_split(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap=0.0, window=0,

@@ -77,7 +77,37 @@ def prefetch_dense(items, M: int, dtype) -> None:
         _ready[key] = (w, ev)
 
 
+# ---- resident dense shadow of the low-bit weights for prefill -------------
+# Decode streams the low-bit blob (bandwidth-bound); prefill at M >= 512 is
+# compute-bound and runs the library GEMM on a dequantized copy that the path
+# above re-creates on every call (2 B/weight written and re-read: ~20 % of a
+# 1024-token prefill GEMM).  With 288 GB of HBM3E per MI355X the dequantized
+# copy can simply stay resident: ILLM_PREFILL_DENSE_GB=<budget> keeps up to
+# that many GB of bf16/f16 shadows (first use dequantizes, later prefills
+# reuse it; numerics identical to the dequantize-per-call path).  Default 0:
+# nothing kept (the low-bit footprint only).
+_DENSE_BUDGET = float(os.environ.get("ILLM_PREFILL_DENSE_GB", "0")) * 2 ** 30
+_dense_cache = {}            # (blob ptr, version, n, k, dtype) -> dense weight
+_dense_bytes = [0]
+
+
+def dense_cache_clear() -> None:
+    _dense_cache.clear()
+    _dense_bytes[0] = 0
+
+
 def _dense_weight(blob, fmt, n, k, dtype):
+    if _DENSE_BUDGET > 0 and not torch.cuda.is_current_stream_capturing():
+        key = (blob.data_ptr(), blob._version, n, k, dtype)
+        w = _dense_cache.get(key)
+        if w is not None:
+            return w
+        w = torch.ops.ipex_llm_amd.dequantize_device(blob, fmt, n, k, dtype)
+        nb = w.numel() * w.element_size()
+        if _dense_bytes[0] + nb <= _DENSE_BUDGET:
+            _dense_cache[key] = w
+            _dense_bytes[0] += nb
+        return w
     hit = _ready.pop(_key(blob, n, k, dtype), None) if _ready else None
     if hit is None:
         return torch.ops.ipex_llm_amd.dequantize_device(blob, fmt, n, k, dtype)

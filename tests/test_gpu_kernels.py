@@ -222,6 +222,87 @@ def test_attn_decode_rope_matches_rope_kv(cuda, B, interleaved, Hq, Hkv):
     assert int((part2 != 0).sum()) == 0, "qkv accumulator not re-zeroed"
 
 
+@pytest.mark.parametrize("B,Hq,Hkv,D", [(1, 8, 2, 128), (4, 8, 2, 128), (8, 8, 2, 128), (2, 8, 4, 64)])
+def test_gemv_rope_epilogue_and_prerot_attention(cuda, B, Hq, Hkv, D):
+    """RoPE applied to each split-K partial in the qkv GEMV epilogue (rotation is
+    linear) == rotating the finished accumulator; the attention over the
+    pre-rotated accumulator (prerot) == the attention that rotates itself;
+    the norm-in variant (deferred scale) rotates too"""
+    from ipex_llm_amd.engine.runner import nsplit_for
+    from ipex_llm_amd.ops.api import _rope_cols
+    torch.manual_seed(11)
+    f = get_format("sym_int4").fmt
+    H, bs = 1024, 64
+    N = (Hq + 2 * Hkv) * D
+    blob = ops.quantize(torch.randn(N, H, device=cuda) * 0.05, f)
+    x = torch.randn(B, H, device=cuda).bfloat16()
+    L = [40 + 37 * i for i in range(B)]
+    seq_lens = torch.tensor(L, dtype=torch.int32, device=cuda)
+    pos = (seq_lens - 1).long()
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
+    fr = torch.arange(512, device=cuda).float()[:, None] * inv[None]
+    cs = torch.stack([fr.cos(), fr.sin()], -1).contiguous()
+    rope = (cs, pos, (Hq + Hkv) * D, D)
+    a_rot = torch.zeros(B, N, device=cuda)
+    a_raw = torch.zeros(B, N, device=cuda)
+    ops.gemv_accum(x, blob, f, N, H, a_rot, rope=rope)
+    ops.gemv_accum(x, blob, f, N, H, a_raw)
+    assert _rel(a_rot, _rope_cols(a_raw, rope, torch.bfloat16)) < 1e-5
+    # norm-in (deferred) variant
+    acc_in = torch.randn(B, H, device=cuda) * 0.5
+    res = torch.randn(B, H, device=cuda).bfloat16()
+    wn = (torch.rand(H, device=cuda) + 0.5).bfloat16()
+    n_rot, n_raw = torch.zeros(B, N, device=cuda), torch.zeros(B, N, device=cuda)
+    ss1, ss2 = torch.zeros(B, device=cuda), torch.zeros(B, device=cuda)
+    ops.gemv_norm_in(acc_in, res, torch.empty_like(res), wn, 1e-5, False, blob, f, N, H, False, acc_out=n_rot,
+                     ss=ss1, rope=rope)
+    ops.gemv_norm_in(acc_in, res, torch.empty_like(res), wn, 1e-5, False, blob, f, N, H, False, acc_out=n_raw,
+                     ss=ss2)
+    assert _rel(n_rot, _rope_cols(n_raw, rope, torch.bfloat16)) < 1e-5
+    if D != 128:
+        return                                   # fused-RoPE decode attention: head_dim 128 / 256
+    # attention: pre-rotated accumulator vs rotation inside the attention
+    kc = torch.randn(4 * B, Hkv, bs, D, device=cuda).bfloat16()
+    vc = torch.randn(4 * B, Hkv, bs, D, device=cuda).bfloat16()
+    bt = torch.arange(4 * B, dtype=torch.int32, device=cuda).view(B, 4).contiguous()
+    ns = nsplit_for(max(L))
+    kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    p1, p2 = a_rot * 8, a_raw * 8
+    got = ops.attn_decode_rope(p1, None, cs, pos, kc1, vc1, bt, seq_lens, ns, D ** -0.5, 0.0, 0, Hq, D, False, 1.0,
+                               torch.bfloat16, prerot=True)
+    ref = ops.attn_decode_rope(p2, None, cs, pos, kc2, vc2, bt, seq_lens, ns, D ** -0.5, 0.0, 0, Hq, D, False, 1.0,
+                               torch.bfloat16)
+    assert _rel(got, ref) < 2e-2
+    assert _rel(kc1.float(), kc2.float()) < 1e-2 and _rel(vc1.float(), vc2.float()) < 1e-2
+    torch.cuda.synchronize()
+    assert int((p1 != 0).sum()) == 0, "qkv accumulator not re-zeroed"
+
+
+def test_decode_gemv_rope_matches_attention_rope(cuda):
+    """whole-model decode (graph): RoPE in the qkv GEMV epilogue vs in the
+    attention / rope kernels -- greedy tokens agree up to rare last-bit ties"""
+    from transformers import LlamaConfig
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models import decoder as dec
+    from ipex_llm_amd.models.builder import random_native_model
+    cfg = LlamaConfig(vocab_size=512, hidden_size=512, intermediate_size=1024, num_hidden_layers=3,
+                      num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=1024)
+    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=6)
+    prompts = [list(range(1, 50)), list(range(7, 70)), list(range(3, 40)), [5] * 30, list(range(9, 29)),
+               list(range(2, 60, 2))]
+    outs = {}
+    try:
+        for flag in (False, True):
+            dec.GEMV_ROPE = flag
+            outs[flag] = Engine(m).generate(prompts, max_new_tokens=10, use_graph=True)
+        eager = Engine(m).generate(prompts, max_new_tokens=10, use_graph=False)
+    finally:
+        dec.GEMV_ROPE = True
+    assert eager == outs[True]
+    a, b = sum(outs[False], []), sum(outs[True], [])
+    assert sum(x == y for x, y in zip(a, b)) >= 0.95 * len(a)
+
+
 def test_attn_decode_long_context_combine(cuda):
     """> 1024 splits (> 64 Ki keys): the combine takes its no-LDS path"""
     torch.manual_seed(5)

@@ -52,7 +52,12 @@ int main(int argc, char** argv) {
   struct Cfg { int shape, M, normin, kw, nw, ks; };
   std::vector<Cfg> cfgs;
   const char* mode = getenv("PROBE_MODE");
-  if (mode && mode[0] == 'd') {
+  if (mode && mode[0] == 'a') {
+    // ablation builds: production geometry, plain / deferred input
+    for (int M : {1, 8})
+      for (int sh : {0, 1, 2, 3, 4})
+        for (int ni = 0; ni < 3; ni += 2) cfgs.push_back({sh, M, ni, 0, 0, 0});
+  } else if (mode && mode[0] == 'd') {
     // deferred vs full-row norm-in vs plain input, production geometry
     for (int M : {1, 2, 4, 8}) {
       for (int ni = 0; ni < 3; ni++) {
