@@ -247,8 +247,15 @@ __device__ __forceinline__ bool combine_fast(const AttnDecodeArgs& a, int b, con
 // lane's own softmax numerators (key order of the S^T C layout), so P never
 // leaves registers.  16 MFMAs per 64-key split (D = 128) instead of the
 // per-lane FMA loop and its 2 x RT x DPL cross-lane reductions.
-template <typename T, int D, int KVF, int RT, bool RQ = false, bool LATEV = false, bool PVM = false>
-__global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs a) {
+//
+// NWV = 2 (PVM only): two waves per 64-key split, each owning 32 keys (half
+// the K/V loads, QK^T and P V work of the one-wave form, so half its serial
+// instruction chain); the split's softmax max / sum meet in LDS and wave 1's
+// P V accumulator is added by wave 0, which writes the split partial.
+template <typename T, int D, int KVF, int RT, bool RQ = false, bool LATEV = false, bool PVM = false, int NWV = 1>
+__global__ void __launch_bounds__(64 * NWV) attn_decode_v2_kernel(const AttnDecodeArgs a) {
+  static_assert(NWV == 1 || PVM, "two-wave splits need the MFMA P V form");
+  constexpr int KTW = 4 / NWV;        // 16-key tiles per wave
   constexpr int EB = KVF == 0 ? 2 : 1;
   constexpr int KSTEP = D / 32;       // MFMA k-steps over the head dim
   constexpr int DPL = D / 16;         // head dims per lane in P.V
@@ -256,7 +263,8 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   constexpr int VU = D / 8;           // PVM staging: 16-B chunks per key = chunks per lane
   constexpr int KPJ = 64 / VU;        // keys per staging step (lane -> key lane / VU, chunk lane % VU)
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, r16 = lane & 15, g = lane >> 4;
+  const int wv = NWV > 1 ? (int)(threadIdx.x >> 6) : 0;
   const int len = a.seq_lens[b];
   const int k0 = split * SPLIT;
   if (k0 >= len) return;
@@ -265,6 +273,7 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   const int R = group * a.Tq;
 
   __shared__ float ps[PVM ? 1 : SPLIT][RT];
+  __shared__ float mx[NWV > 1 ? 2 * NWV : 1][16];      // NWV > 1: per-wave row max / sum
   __shared__ __attribute__((aligned(16))) uint16_t vl[PVM ? SPLIT * D : 8];
 
   // ---- fused RoPE (rq_part): q/k/v of the new token from the qkv accumulator,
@@ -308,21 +317,22 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   const uint8_t* vb = a.v_cache + base * EB;
 
   // ---- issue every load of the split
-  uint4 kf[4][KSTEP];
+  uint4 kf[KTW][KSTEP];
 #pragma unroll
-  for (int kt = 0; kt < 4; kt++) {
-    const int kk = min(kt * 16 + r16, nk - 1);
+  for (int kt = 0; kt < KTW; kt++) {
+    const int kk = min((wv * KTW + kt) * 16 + r16, nk - 1);
 #pragma unroll
     for (int s = 0; s < KSTEP; s++) kf[kt][s] = kv_frag8<T, KVF>(kb + ((size_t)kk * D + 32 * s + 8 * g) * EB);
   }
   const int dg = r16, kg = g;
   uint4 vf[PVM ? 1 : 16][VCH];
-  uint4 vm[PVM ? VU : 1];
+  constexpr int VUW = PVM ? VU / NWV : 1;           // staging steps of this wave's keys
+  uint4 vm[VUW];
   auto load_v = [&]() {
     if constexpr (PVM) {
 #pragma unroll
-      for (int j = 0; j < VU; j++) {
-        const int kk = min(j * KPJ + lane / VU, nk - 1);
+      for (int j = 0; j < VUW; j++) {
+        const int kk = min((wv * VUW + j) * KPJ + lane / VU, nk - 1);
         vm[j] = kv_frag8<T, KVF>(vb + ((size_t)kk * D + 8 * (lane % VU)) * EB);
       }
     } else if constexpr (DPL >= 8) {
@@ -427,19 +437,19 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
       const size_t crow = (((size_t)nb * a.Hkv + kvh) * a.bs + (size_t)(pos % a.bs)) * D;
       if (bad_block(nb, a.num_blocks)) {
         if (threadIdx.x == 0) kerr(a.err, ERR_BLOCK_ID);
-      } else if (r16 == (kn & 15)) {
+      } else if (r16 == (kn & 15) && (kn >> 4) / KTW == wv) {
         uint4 kq[KSTEP];
         lane_rot(colk, 1.f, kq);
 #pragma unroll
-        for (int kt = 0; kt < 4; kt++)
-          if (kt == (kn >> 4))
+        for (int kt = 0; kt < KTW; kt++)
+          if (wv * KTW + kt == (kn >> 4))
 #pragma unroll
             for (int s = 0; s < KSTEP; s++) kf[kt][s] = kq[s];
 #pragma unroll
         for (int s = 0; s < KSTEP; s++) *(uint4*)((uint16_t*)a.k_cache + crow + 32 * s + 8 * g) = kq[s];
       }
       if constexpr (PVM) {
-        if (lane / VU == kn % KPJ) {
+        if (lane / VU == kn % KPJ && (kn / KPJ) / VUW == wv) {
           const int d0 = 8 * (lane % VU);
           const float4* p = (const float4*)(a.rq_part + (size_t)b * a.rq_ld + colv + d0);
           const float4 f0 = p[0], f1 = p[1];
@@ -460,8 +470,8 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
           const uint4 vq = make_uint4(w[0], w[1], w[2], w[3]);
           vnew[0] = vq;
 #pragma unroll
-          for (int j = 0; j < VU; j++)
-            if (j == kn / KPJ) vm[j] = vq;
+          for (int j = 0; j < VUW; j++)
+            if (wv * VUW + j == kn / KPJ) vm[j] = vq;
           if (!bad_block(nb, a.num_blocks)) *(uint4*)((uint16_t*)a.v_cache + crow + d0) = vq;
         }
       } else if constexpr (DPL >= 8) {
@@ -507,9 +517,9 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   }
 
   // ---- S^T tiles: lane holds (key = 16 kt + 4 g + i, row = r16)
-  f32x4 st[4];
+  f32x4 st[KTW];
 #pragma unroll
-  for (int kt = 0; kt < 4; kt++) {
+  for (int kt = 0; kt < KTW; kt++) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KSTEP; s++) acc = mfma16<T>(kf[kt][s], qf[s], acc);
@@ -522,10 +532,10 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
       // from registers, not from a load that may race the store
       const int kn = nk - 1;
       if constexpr (PVM) {
-        if (has_new && lane / VU == kn % KPJ) {
+        if (has_new && lane / VU == kn % KPJ && (kn / KPJ) / VUW == wv) {
 #pragma unroll
-          for (int j = 0; j < VU; j++)
-            if (j == kn / KPJ) vm[j] = vnew[0];
+          for (int j = 0; j < VUW; j++)
+            if (wv * VUW + j == kn / KPJ) vm[j] = vnew[0];
         }
       } else if (has_new && kg == (kn & 3)) {
 #pragma unroll
@@ -549,30 +559,30 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
   // loops and the mask is branch-free (per-score branches split the score
   // pass into dozens of basic blocks)
 #pragma unroll
-  for (int kt = 0; kt < 4; kt++)
+  for (int kt = 0; kt < KTW; kt++)
 #pragma unroll
     for (int i = 0; i < 4; i++) st[kt][i] *= sc;
   if (a.softcap > 0.f) {
 #pragma unroll
-    for (int kt = 0; kt < 4; kt++)
+    for (int kt = 0; kt < KTW; kt++)
 #pragma unroll
       for (int i = 0; i < 4; i++) st[kt][i] = a.softcap * tanhf(st[kt][i] / a.softcap);
   }
   if (a.alibi) {
     const float slope = row < R ? a.alibi[h] : 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 4; kt++)
+    for (int kt = 0; kt < KTW; kt++)
 #pragma unroll
-      for (int i = 0; i < 4; i++) st[kt][i] += slope * (float)(k0 + kt * 16 + 4 * g + i);
+      for (int i = 0; i < 4; i++) st[kt][i] += slope * (float)(k0 + (wv * KTW + kt) * 16 + 4 * g + i);
   }
   const int win = a.sliding_window > 0 ? qpos - a.sliding_window : -1;
   const int klim = min(nk, qpos - k0 + 1);          // keys kk < klim are visible
   float m = -INFINITY;
 #pragma unroll
-  for (int kt = 0; kt < 4; kt++) {
+  for (int kt = 0; kt < KTW; kt++) {
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const int kk = kt * 16 + 4 * g + i;
+      const int kk = (wv * KTW + kt) * 16 + 4 * g + i;
       const bool ok = row < R && kk < klim && k0 + kk > win;
       const float v = ok ? st[kt][i] : -INFINITY;
       st[kt][i] = v;
@@ -582,10 +592,10 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
 #else
   float m = -INFINITY;
 #pragma unroll
-  for (int kt = 0; kt < 4; kt++) {
+  for (int kt = 0; kt < KTW; kt++) {
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const int kk = kt * 16 + 4 * g + i;
+      const int kk = (wv * KTW + kt) * 16 + 4 * g + i;
       const int key = k0 + kk;
       float v = st[kt][i] * sc;
       if (a.softcap > 0.f) v = a.softcap * tanhf(v / a.softcap);
@@ -600,14 +610,20 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
 #endif
   m = fmaxf(m, __shfl_xor(m, 16, 64));
   m = fmaxf(m, __shfl_xor(m, 32, 64));
+  if constexpr (NWV > 1) {                         // split-wide row max
+    if (g == 0) mx[wv][r16] = m;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NWV; w++) m = fmaxf(m, mx[w][r16]);
+  }
   float l = 0.f;
   const float vs = KVF ? a.v_scale : 1.f;
   const bool handoff = a.counters != nullptr;
   if constexpr (PVM) {
     // P^T fragments (16-bit pairs, key order 16 kt + 4 g + i) and the V tile in LDS
-    uint32_t pk[4][2];
+    uint32_t pk[KTW][2];
 #pragma unroll
-    for (int kt = 0; kt < 4; kt++) {
+    for (int kt = 0; kt < KTW; kt++) {
       float p[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) {
@@ -620,16 +636,24 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
 #pragma unroll
-    for (int j = 0; j < VU; j++) *(uint4*)(vl + pf_off<D>(j * KPJ + lane / VU, lane % VU)) = vm[j];
+    for (int j = 0; j < VUW; j++) *(uint4*)(vl + pf_off<D>((wv * VUW + j) * KPJ + lane / VU, lane % VU)) = vm[j];
+    if constexpr (NWV > 1) {
+      if (g == 0) mx[NWV + wv][r16] = l;
+    }
     __syncthreads();
+    if constexpr (NWV > 1) {
+      l = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; w++) l += mx[NWV + w][r16];
+    }
     constexpr int DT = D / 16;
     f32x4 o[DT];
 #pragma unroll
     for (int d = 0; d < DT; d++) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int qq = r16 >> 2, pp = r16 & 3;
 #pragma unroll
-    for (int kk = 0; kk < 2; kk++) {
-      const int row0 = 32 * kk + 4 * g + qq, row1 = row0 + 16;
+    for (int kk = 0; kk < 2 / NWV; kk++) {
+      const int row0 = 32 * (wv * (2 / NWV) + kk) + 4 * g + qq, row1 = row0 + 16;
       const uint4 pb = make_uint4(pk[2 * kk][0], pk[2 * kk][1], pk[2 * kk + 1][0], pk[2 * kk + 1][1]);
 #pragma unroll
       for (int d = 0; d < DT; d++) {
@@ -639,15 +663,32 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
         o[d] = mfma16<T>(make_uint4(v0.x, v0.y, v1.x, v1.y), pb, o[d]);
       }
     }
+    if constexpr (NWV > 1) {
+      // wave 1's P V sums join wave 0's through LDS (the V tile is dead now)
+      float* ob = (float*)vl;
+      __syncthreads();
+      if (wv == 1) {
+#pragma unroll
+        for (int d = 0; d < DT; d++) *(float4*)(ob + (d * 64 + lane) * 4) = make_float4(o[d][0], o[d][1], o[d][2], o[d][3]);
+      }
+      __syncthreads();
+      if (wv == 0) {
+#pragma unroll
+        for (int d = 0; d < DT; d++) {
+          const float4 u = *(const float4*)(ob + (d * 64 + lane) * 4);
+          o[d][0] += u.x; o[d][1] += u.y; o[d][2] += u.z; o[d][3] += u.w;
+        }
+      }
+    }
     // lane holds O^T[16 d + 4 g + i][row r16]
-    if (row < R) {
+    if (row < R && wv == 0) {
       const size_t prow = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit + split;
       float* po = a.part_o + prow * D + 4 * g;
 #pragma unroll
       for (int d = 0; d < DT; d++) {
         if (handoff) {
-#pragma unroll
-          for (int i = 0; i < 4; i++) st_sc1(po + 16 * d + i, o[d][i] * vs);
+          st16_sc1(a.part_o, (size_t)(po - a.part_o) + 16 * d,
+                   make_float4(o[d][0] * vs, o[d][1] * vs, o[d][2] * vs, o[d][3] * vs));
         } else {
           *(float4*)(po + 16 * d) = make_float4(o[d][0] * vs, o[d][1] * vs, o[d][2] * vs, o[d][3] * vs);
         }
@@ -717,7 +758,9 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
         float* po = a.part_o + prow * D + DPL * dg;
         if (handoff) {
 #pragma unroll
-          for (int d = 0; d < DPL; d++) st_sc1(po + d, o[r][d] * vs);
+          for (int d = 0; d < DPL; d += 4)
+            st16_sc1(a.part_o, (size_t)(po - a.part_o) + d,
+                     make_float4(o[r][d] * vs, o[r][d + 1] * vs, o[r][d + 2] * vs, o[r][d + 3] * vs));
         } else {
 #pragma unroll
           for (int d = 0; d < DPL; d += 4)
@@ -727,11 +770,10 @@ __global__ void __launch_bounds__(64) attn_decode_v2_kernel(const AttnDecodeArgs
     }
   }
   }
-  if (g == 0 && row < R) {
+  if (g == 0 && row < R && wv == 0) {
     const size_t prow = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit + split;
     if (handoff) {
-      st_sc1(a.part_ml + prow * 2, m);
-      st_sc1(a.part_ml + prow * 2 + 1, l);
+      st8_sc1(a.part_ml + prow * 2, m, l);
     } else {
       a.part_ml[prow * 2] = m;
       a.part_ml[prow * 2 + 1] = l;
@@ -798,8 +840,8 @@ __device__ __forceinline__ bool combine_fast(const AttnDecodeArgs& a, int b, con
   if (!(Q == 16 || Q == 32 || Q == 64)) return false;
   const int P = 64 / Q, q = lane % Q, p = lane / Q;
   if (ns > CH * P) return false;
-  auto ld4 = [](const float* x) -> float4 {
-    if constexpr (SC1) return make_float4(ld_sc1(x), ld_sc1(x + 1), ld_sc1(x + 2), ld_sc1(x + 3));
+  auto ld4 = [&](const float* x) -> float4 {
+    if constexpr (SC1) return ld16_sc1(a.part_o, (size_t)(x - a.part_o));
     else return *(const float4*)x;
   };
   auto ld1 = [](const float* x) -> float {
@@ -816,7 +858,10 @@ __device__ __forceinline__ bool combine_fast(const AttnDecodeArgs& a, int b, con
 #pragma unroll
     for (int j = 0; j < CH; j++) pv[r][j] = ld4(po + (size_t)min(p + j * P, ns - 1) * a.D);
     ml[r] = make_float2(-INFINITY, 0.f);
-    if (lane < ns) ml[r] = make_float2(ld1(a.part_ml + (row0[r] + lane) * 2), ld1(a.part_ml + (row0[r] + lane) * 2 + 1));
+    if (lane < ns) {
+      if constexpr (SC1) ml[r] = ld8_sc1(a.part_ml + (row0[r] + lane) * 2);
+      else ml[r] = make_float2(ld1(a.part_ml + (row0[r] + lane) * 2), ld1(a.part_ml + (row0[r] + lane) * 2 + 1));
+    }
   }
 #pragma unroll
   for (int r = 0; r < NR; r++) {
@@ -1060,12 +1105,31 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
   }
   static const int latev_env = getenv("ILLM_ATTN_LATEV") ? atoi(getenv("ILLM_ATTN_LATEV")) : -1;
   const bool latev = latev_env >= 0 ? latev_env == 1 : (long)a.nsplit * a.Hkv * a.B > simds;
+  // two waves per split (PVM, 16-bit KV, no in-kernel combine): ILLM_ATTN_NWV=1 keeps one
+  static const int nwv_env = getenv("ILLM_ATTN_NWV") ? atoi(getenv("ILLM_ATTN_NWV")) : 2;
+  const bool two = PVM && nwv_env == 2 && a.counters == nullptr && a.kv_fp8 == 0;
   if constexpr (D / 16 >= 8) {
     if (a.rq_part != nullptr) {
+      if constexpr (PVM) {
+        if (two) {
+          if (latev) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, true, PVM, 2>), grid, dim3(128), 0, st, a);
+          else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, false, PVM, 2>), grid, dim3(128), 0, st, a);
+          if (!a.no_combine) launch_combine<T>(a, st);
+          return;
+        }
+      }
       if (latev) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, true, PVM>), grid, dim3(64), 0, st, a);
       else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, true, false, PVM>), grid, dim3(64), 0, st, a);
       if (a.counters == nullptr && !a.no_combine)
         launch_combine<T>(a, st);
+      return;
+    }
+  }
+  if constexpr (PVM) {
+    if (two) {
+      if (latev) hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, false, true, PVM, 2>), grid, dim3(128), 0, st, a);
+      else hipLaunchKernelGGL((attn_decode_v2_kernel<T, D, 0, RT, false, false, PVM, 2>), grid, dim3(128), 0, st, a);
+      if (!a.no_combine) launch_combine<T>(a, st);
       return;
     }
   }

@@ -93,6 +93,27 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
 __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 16-B / 8-B forms of the same hand-off (a scalarised 4-B sc1 store per
+// element is several times slower per byte): buffer_store/load_dwordx4 with
+// the sc1 bit (aux 16) through a raw buffer descriptor on `base`
+// (gfx9 word 3 = 0x00020000), and 8-B agent-scope atomic stores / loads
+typedef unsigned int illm_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_sc1(float* base, size_t elem, float4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(illm_u32x4, v), r, (int)(elem * 4), 0, 16);
+}
+__device__ __forceinline__ float4 ld16_sc1(const float* base, size_t elem) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(elem * 4), 0, 16));
+}
+__device__ __forceinline__ void st8_sc1(float* p, float a, float b) {
+  const unsigned long long v = (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
+  __hip_atomic_store((unsigned long long*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 ld8_sc1(const float* p) {
+  const unsigned long long v = __hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_float2(__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)));
+}
 
 // Kernel error word (SURVEY §5.2 bounds checks): a kernel that finds an
 // out-of-range index from device data (block table entry, cache slot, expert

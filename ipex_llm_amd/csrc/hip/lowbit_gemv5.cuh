@@ -167,7 +167,7 @@ __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
 // scale words shared across lanes (SCL above); ILLM_GEMV5_SCL=0 at build time
 // restores the per-lane scale loads in the chunk ring
 #ifndef ILLM_GEMV5_SCL
-#define ILLM_GEMV5_SCL 0
+#define ILLM_GEMV5_SCL 1
 #endif
 template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4, bool SCL = ILLM_GEMV5_SCL != 0>
 __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(const GemvArgs a) {
@@ -767,10 +767,13 @@ inline void launch5(K kern, dim3 grid, size_t shmem, const GemvArgs& a, hipStrea
   hipLaunchKernelGGL(kern, grid, dim3(64 * (a.nw == 8 ? 8 : 4)), shmem, st, a);
 }
 
-// chunks in flight per wave: 8 with the shared scale window (same ring VGPRs
-// as 4 with per-lane scale words); ILLM_GEMV5_PFD overrides at build time
+// chunks in flight per wave.  The shared scale window would fit 8 in the
+// ring VGPRs of 4, but 8 measured slower on MI355X at every decode shape
+// (profiles/gemv5_scl_r3.jsonl: qkv M=1 8.9 vs 6.1 us, GLU 23.0 vs 17.6);
+// with 4 the window only pays for the two-tile GLU launch (M=1 17.1 vs 17.6,
+// deferred-norm 18.0 vs 19.0 us), so that is the one launch that takes it
 #ifndef ILLM_GEMV5_PFD
-#define ILLM_GEMV5_PFD (ILLM_GEMV5_SCL ? 8 : 4)
+#define ILLM_GEMV5_PFD 4
 #endif
 template <int DK, typename T, int KW, bool MOE, int NW, bool S>
 inline void launch5_epi_s(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
@@ -792,8 +795,9 @@ inline void launch5_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hip
   // the shared scale window holds 16 chunks: longer per-wave ranges keep the
   // per-lane scale words
   const int cpk = a.cpk > 0 ? a.cpk : (a.KC + (int)grid.y - 1) / (int)grid.y;
-  if (ILLM_GEMV5_SCL && (cpk + KW - 1) / KW > 16) return launch5_epi_s<DK, T, KW, MOE, NW, false>(epi, grid, shmem, a, st);
-  return launch5_epi_s<DK, T, KW, MOE, NW, ILLM_GEMV5_SCL != 0>(epi, grid, shmem, a, st);
+  if (ILLM_GEMV5_SCL && epi == EPI_GLU && (cpk + KW - 1) / KW <= 16)
+    return launch5(lowbit_gemv5_kernel<DK, T, EPI_GLU, 2, KW, MOE, NW, ILLM_GEMV5_PFD, true>, grid, shmem, a, st);
+  return launch5_epi_s<DK, T, KW, MOE, NW, false>(epi, grid, shmem, a, st);
 }
 
 template <int DK, typename T, bool MOE>
