@@ -1105,9 +1105,14 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
   }
   static const int latev_env = getenv("ILLM_ATTN_LATEV") ? atoi(getenv("ILLM_ATTN_LATEV")) : -1;
   const bool latev = latev_env >= 0 ? latev_env == 1 : (long)a.nsplit * a.Hkv * a.B > simds;
-  // two waves per split (PVM, 16-bit KV, no in-kernel combine): ILLM_ATTN_NWV=1 keeps one
-  static const int nwv_env = getenv("ILLM_ATTN_NWV") ? atoi(getenv("ILLM_ATTN_NWV")) : 2;
-  const bool two = PVM && nwv_env == 2 && a.counters == nullptr && a.kv_fp8 == 0;
+  // two waves per split (PVM, 16-bit KV, no in-kernel combine) while the doubled
+  // grid still has at most one wave per SIMD: MI355X, Llama-3-8B at 1K keys
+  // (same-box A/B, profiles/bench_b*_r3_nwv*.json): B=1 1.654 -> 1.646 ms/token,
+  // but B=8 (1024 split waves) 2.366 -> 2.419 ms/step, so larger grids keep one.
+  // ILLM_ATTN_NWV=1 / 2 forces either form
+  static const int nwv_env = getenv("ILLM_ATTN_NWV") ? atoi(getenv("ILLM_ATTN_NWV")) : 0;
+  const bool small_grid = 2L * a.nsplit * a.Hkv * a.B <= simds;
+  const bool two = PVM && a.counters == nullptr && a.kv_fp8 == 0 && (nwv_env == 2 || (nwv_env == 0 && small_grid));
   if constexpr (D / 16 >= 8) {
     if (a.rq_part != nullptr) {
       if constexpr (PVM) {

@@ -60,7 +60,13 @@ class MatMulLowBit(torch.autograd.Function):
         grad_x = None
         if ctx.needs_input_grad[0]:
             dt = grad_y.dtype if grad_y.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16
-            w = ops.dequantize(blob, ctx.fmt, ctx.n, ctx.k, dtype=dt)
+            if blob.is_cuda and ops.native_gpu(blob):
+                # same dense weight as the forward's library GEMM: the resident
+                # shadow when ILLM_PREFILL_DENSE_GB allows it, else a transient dequant
+                from ..ops.gemm import _dense_weight
+                w = _dense_weight(blob, ctx.fmt, ctx.n, ctx.k, dt)
+            else:
+                w = ops.dequantize(blob, ctx.fmt, ctx.n, ctx.k, dtype=dt)
             grad_x = torch.matmul(grad_y.to(w.dtype), w).to(ctx.xdtype)
         return grad_x, None, None, None, None, None
 
