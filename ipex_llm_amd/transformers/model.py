@@ -158,6 +158,15 @@ def _reinit_meta_buffers(model: nn.Module, config):
         setattr(parent, name.rsplit(".", 1)[-1], new)
 
 
+def _remote_family(path, kwargs) -> bool:
+    """chatglm / qwen v1 checkpoint loaded through the native mapping (the
+    default; ILLM_REMOTE_CODE=1 runs the checkpoint's own remote code instead)"""
+    if os.environ.get("ILLM_REMOTE_CODE", "0") == "1":
+        return False
+    from .remote_families import family_of
+    return family_of(path) is not None
+
+
 class _BaseAutoModelClass:
     HF_Model = None
 
@@ -194,6 +203,11 @@ class _BaseAutoModelClass:
         if prequant is not None:
             from ..gptq import load_gptq_model
             model = load_gptq_model(cls.HF_Model, path, prequant, torch_dtype=torch_dtype, **kwargs)
+        elif _remote_family(path, kwargs):
+            # chatglm / qwen v1: the checkpoint re-expressed as the in-library
+            # Glm / Qwen2 model (remote_families.py), then the normal path
+            from .remote_families import load_remote_family
+            model = load_remote_family(path, torch_dtype)
         else:
             from .patches import remote_code_patches
             with remote_code_patches():        # remote code importing flash_attn stays loadable

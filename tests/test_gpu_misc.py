@@ -104,11 +104,12 @@ def test_hf_eager_family_on_gpu_uses_hip_softmax(cuda, tmp_path):
     the in-place HIP softmax; logits stay close to the dense fp32 model"""
     from transformers import AutoConfig, AutoModelForCausalLM as HFAuto
     from ipex_llm_amd.transformers import AutoModelForCausalLM
-    cfg = AutoConfig.for_model("phi", hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+    # (an architecture the native decoder does not run, so the HF eager attention executes)
+    cfg = AutoConfig.for_model("opt", hidden_size=128, ffn_dim=256, num_hidden_layers=2, word_embed_proj_dim=128,
                                num_attention_heads=4, vocab_size=256, max_position_embeddings=128)
     torch.manual_seed(0)
     ref = HFAuto.from_config(cfg, attn_implementation="eager").eval()
-    p = str(tmp_path / "phi")
+    p = str(tmp_path / "opt")
     ref.save_pretrained(p)
     ids = torch.randint(3, 256, (2, 16), generator=torch.Generator().manual_seed(1))
     with torch.no_grad():
