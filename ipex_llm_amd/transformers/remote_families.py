@@ -16,6 +16,8 @@ normal path (low-bit conversion + the native decoder):
   ``dense_h_to_4h`` = [gate; up] = Glm's ``gate_up_proj``, rotary on the first
   half of each head in interleaved pairs (``partial_rotary_factor`` 0.5,
   base 10000 * ``rope_ratio``), RMSNorm, untied ``output_layer``.
+* internlm (v1) -> ``LlamaForCausalLM`` with ``attention_bias`` (q/k/v/o
+  biases, llama tensor names; reference ``SRC/transformers/models/internlm.py``).
 * qwen -> ``Qwen2ForCausalLM``: ``c_attn`` (q|k|v with bias) split, ``c_proj``
   -> o_proj, MLP ``c_proj(w1(x) * silu(w2(x)))`` -> gate = w2, up = w1,
   down = c_proj, full-width NeoX rotary (``rotary_emb_base``).  Qwen v1's
@@ -35,7 +37,7 @@ from typing import Dict, Optional
 
 import torch
 
-FAMILIES = ("chatglm", "qwen")
+FAMILIES = ("chatglm", "qwen", "internlm")
 
 
 def family_of(path) -> Optional[str]:
@@ -160,6 +162,19 @@ def qwen_to_qwen2_weights(sd: Dict[str, torch.Tensor], c: dict) -> Dict[str, tor
     return out
 
 
+# ---------------------------------------------------------------- internlm v1
+def internlm_to_llama_config(c: dict):
+    from transformers import LlamaConfig
+    rot = c.get("rotary") or {}
+    return LlamaConfig(
+        vocab_size=c["vocab_size"], hidden_size=c["hidden_size"], intermediate_size=c["intermediate_size"],
+        num_hidden_layers=c["num_hidden_layers"], num_attention_heads=c["num_attention_heads"],
+        num_key_value_heads=c.get("num_key_value_heads", c["num_attention_heads"]),
+        max_position_embeddings=c.get("max_position_embeddings", 2048), rms_norm_eps=c.get("rms_norm_eps", 1e-6),
+        attention_bias=bool(c.get("bias", True)), tie_word_embeddings=bool(c.get("tie_word_embeddings", False)),
+        rope_parameters={"rope_type": "default", "rope_theta": float(rot.get("base", c.get("rope_theta", 10000.0)))})
+
+
 def load_remote_family(path, torch_dtype="auto"):
     """HF model of the in-library architecture equivalent to a chatglm / qwen
     checkpoint, with the checkpoint's tensors mapped in (CPU)."""
@@ -172,6 +187,9 @@ def load_remote_family(path, torch_dtype="auto"):
     if fam == "chatglm":
         from transformers import GlmForCausalLM
         cfg, mapped, cls = chatglm_to_glm_config(c), chatglm_to_glm_weights(sd, c), GlmForCausalLM
+    elif fam == "internlm":
+        from transformers import LlamaForCausalLM
+        cfg, mapped, cls = internlm_to_llama_config(c), dict(sd), LlamaForCausalLM
     else:
         from transformers import Qwen2ForCausalLM
         cfg, mapped, cls = qwen_to_qwen2_config(c), qwen_to_qwen2_weights(sd, c), Qwen2ForCausalLM

@@ -81,10 +81,35 @@ def _qwen_dir(tmp_path):
     return ref, d
 
 
-@pytest.mark.parametrize("family,mqa", [("chatglm", True), ("chatglm", False), ("qwen", False)])
+def _internlm_dir(tmp_path):
+    from transformers import LlamaConfig, LlamaForCausalLM
+    cfg = LlamaConfig(vocab_size=96, hidden_size=64, intermediate_size=96, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=4, attention_bias=True, max_position_embeddings=256, rms_norm_eps=1e-6,
+                      rope_parameters={"rope_type": "default", "rope_theta": 10000.0})
+    torch.manual_seed(2)
+    ref = LlamaForCausalLM(cfg).eval()
+    conf = {"model_type": "internlm", "architectures": ["InternLMForCausalLM"], "vocab_size": 96, "hidden_size": 64,
+            "intermediate_size": 96, "num_hidden_layers": 2, "num_attention_heads": 4, "bias": True,
+            "max_position_embeddings": 256, "rms_norm_eps": 1e-6, "rotary": {"base": 10000, "type": "dynamic"}}
+    d = tmp_path / "internlm"
+    d.mkdir()
+    from safetensors.torch import save_file
+    save_file({k: v.contiguous() for k, v in ref.state_dict().items()}, str(d / "model.safetensors"))
+    (d / "config.json").write_text(json.dumps(conf))
+    return ref, d
+
+
+def _family_dir(tmp_path, family, mqa=True):
+    if family == "chatglm":
+        return _chatglm_dir(tmp_path, mqa)
+    return _qwen_dir(tmp_path) if family == "qwen" else _internlm_dir(tmp_path)
+
+
+@pytest.mark.parametrize("family,mqa", [("chatglm", True), ("chatglm", False), ("qwen", False),
+                                        ("internlm", False)])
 def test_remote_family_mapping_reproduces_logits(tmp_path, family, mqa):
     from ipex_llm_amd.transformers.remote_families import family_of, load_remote_family
-    ref, d = _chatglm_dir(tmp_path, mqa) if family == "chatglm" else _qwen_dir(tmp_path)
+    ref, d = _family_dir(tmp_path, family, mqa)
     assert family_of(str(d)) == family
     m = load_remote_family(str(d), torch.float32)
     ids = torch.randint(0, 96, (2, 12), generator=torch.Generator().manual_seed(3))
@@ -94,12 +119,12 @@ def test_remote_family_mapping_reproduces_logits(tmp_path, family, mqa):
     assert torch.allclose(got, want, atol=1e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("family", ["chatglm", "qwen"])
+@pytest.mark.parametrize("family", ["chatglm", "qwen", "internlm"])
 def test_remote_family_low_bit_native(tmp_path, family):
     """from_pretrained(load_in_low_bit) on a chatglm / qwen directory: native
     decoder over low-bit weights, logits close to the dense original"""
     from ipex_llm_amd.transformers import AutoModelForCausalLM
-    ref, d = _chatglm_dir(tmp_path) if family == "chatglm" else _qwen_dir(tmp_path)
+    ref, d = _family_dir(tmp_path, family)
     m = AutoModelForCausalLM.from_pretrained(str(d), load_in_low_bit="sym_int8", torch_dtype=torch.float32)
     assert getattr(m.config, "illm_source_model_type", None) == family
     ids = torch.randint(0, 96, (1, 10), generator=torch.Generator().manual_seed(4))
