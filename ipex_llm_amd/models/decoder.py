@@ -161,6 +161,11 @@ DEFER_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_MAX_M", "8"))
 # costs more than the standalone norm launch, MI355X probe
 # profiles/gemv5_defer_r3.jsonl: GLU 24.7 us deferred vs 19.7 us on a normed x)
 DEFER_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_GLU_MAX_M", "4"))
+# above it: gate/up as a split-K atomic GEMV staging only its own K slice
+# (deferred norm), act(g / rms) * (u / rms) applied by the down GEMV while it
+# stages its input -- no norm launch, no full-row read per workgroup
+# (ILLM_DEFER_MLP_ACC=0: standalone norm + GLU GEMV instead)
+DEFER_MLP_ACC = __import__("os").environ.get("ILLM_DEFER_MLP_ACC", "1") != "0"
 # decode batches up to this size take the fused-RoPE attention (qkv accumulated
 # atomically into one slab read by the attention, re-zeroed by its combine).
 # Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token,
@@ -578,6 +583,7 @@ class NativeCausalLM(nn.Module):
             ss_all = self._acc(T, 2 * len(self.layers), x.device, "SS")
             ss_all.zero_()
         ss_q = None                     # sums of squares of the current layer's qkv input (deferred)
+        zero_gu = None                  # consumed gate/up accumulator (batch > DEFER_GLU_MAX_M), zeroed next
         # fused-RoPE decode attention (batch <= ROPE_IN_MAX_M, one token each): the qkv
         # GEMV accumulates into one atomic slab that the attention reads and the
         # combine launch re-zeroes
@@ -619,7 +625,8 @@ class NativeCausalLM(nn.Module):
                         ss_q = ss_all[2 * li] if defer else None
                         ops.gemv_norm_in(pend, residual, r2, layer.input_layernorm, s.rms_eps, s.norm_unit_offset,
                                          qp.weight, qp.fmt, qp.out_features, qp.in_features, False, acc_out=part,
-                                         ss=ss_q, rope=qrope)
+                                         ss=ss_q, rope=qrope, zero=zero_gu)
+                        zero_gu = None
                         residual, consumed, pend = r2, pend, None
                     else:
                         ops.gemv_accum(x, qp.weight, qp.fmt, qp.out_features, qp.in_features, part,
@@ -674,7 +681,18 @@ class NativeCausalLM(nn.Module):
                     ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
                 self._reduce(accP, o)
                 gu, dn = mlp.gate_up_proj, mlp.down_proj
-                if defer and T > DEFER_GLU_MAX_M:
+                if defer and T > DEFER_GLU_MAX_M and DEFER_MLP_ACC:
+                    r2 = nxt_res(residual)
+                    gacc = self._acc(gu.out_features, T, x.device, "GU")
+                    ss2 = ss_all[2 * li + 1]
+                    ops.gemv_norm_in(accP, residual, r2, layer.post_attention_layernorm, s.rms_eps,
+                                     s.norm_unit_offset, gu.weight, gu.fmt, gu.out_features, gu.in_features, False,
+                                     acc_out=gacc, zero=zero_qkv, ss=ss2)
+                    residual = r2
+                    ops.gemv_glu_in(gacc.unsqueeze(0), dn.weight, dn.fmt, dn.out_features, dn.in_features, s.act, 0,
+                                    x.dtype, acc=accD, zero=accP, xss=ss2, xss_n=s.hidden_size, xss_eps=s.rms_eps)
+                    zero_gu = gacc              # zeroed by the next layer's qkv launch (its readers are done)
+                elif defer and T > DEFER_GLU_MAX_M:
                     # standalone residual-add + norm (re-zeroes P), plain GLU GEMV
                     xn, _ = ops.add_rms_norm(None, residual, layer.post_attention_layernorm, s.rms_eps,
                                              partials=accP.unsqueeze(0), unit_offset=s.norm_unit_offset,
@@ -765,6 +783,8 @@ class NativeCausalLM(nn.Module):
                 x, _ = ops.add_rms_norm(y.contiguous(), residual, nxt, s.rms_eps, unit_offset=s.norm_unit_offset)
         if zero_next is not None:
             zero_next.zero_()
+        if zero_gu is not None:
+            zero_gu.zero_()
         if not self.last_stage:
             return residual
         if return_hidden:
