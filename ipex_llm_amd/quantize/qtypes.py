@@ -127,12 +127,16 @@ _FORMATS: Dict[int, QFormat] = {
     Q6_K: QFormat("q6_k", Q6_K, FMT_Q6K, 6, 256, k_align=256, kquant=True),
     Q2_K: QFormat("q2_k", Q2_K, FMT_Q2K, 2, 256, has_min=True, k_align=256, kquant=True),
 }
-# qtypes stored in a format of equal or higher precision.  k-quants and IQ
-# grids (GGUF) are re-quantized on load exactly as the reference's GGUF path
-# does (`transformers/gguf/api.py`), into the nearest device container.
+# qtypes stored in a format of equal or higher precision.  The IQ1 / IQ2
+# lattice codebooks of ggml are not reproduced (their grid tables ship only
+# inside the llama.cpp binaries the reference downloads): gguf_iq2_xxs / xs /
+# iq1_s / iq1_m quantize into the native 2-bit super-block format q2_k
+# (2.625 bits per weight, imatrix-weighted like the IQ quantizers) -- the
+# closest footprint the device kernels decode; IQ-coded GGUF tensors are not
+# loadable.
 _ALIAS = {
     FP6_K: FP6,
-    IQ2_XXS: ASYM_INT4, IQ2_XS: ASYM_INT4, IQ1_S: ASYM_INT4, IQ1_M: ASYM_INT4,
+    IQ2_XXS: Q2_K, IQ2_XS: Q2_K, IQ1_S: Q2_K, IQ1_M: Q2_K,
     SYM_INT4_RTN: SYM_INT4, ASYM_INT4_RTN: ASYM_INT4, SYM_INT8_RTN: SYM_INT8,
     # gguf mixed policies resolve per module (mixed_kquant_qtype); q4_k otherwise
     GGUF_Q4K_S: Q4_K, GGUF_Q4K_M: Q4_K,

@@ -106,3 +106,24 @@ def test_hidden_not_multiple_of_256_falls_back():
     lin = torch.nn.Linear(192, 64)
     m = _convert_one(lin, Q.Q4_K, "cpu")
     assert isinstance(m, LowBitLinear) and m.qtype == Q.ASYM_INT4
+
+
+def test_iq_qtypes_use_native_2bit_super_blocks():
+    """gguf_iq2_xxs / iq2_xs / iq1_s / iq1_m quantize into the native q2_k
+    container (2.625 bpw, imatrix-weighted), not a 4-bit stand-in"""
+    import torch
+    from transformers import LlamaConfig, LlamaForCausalLM
+    from ipex_llm_amd.quantize import qtypes as Q
+    from ipex_llm_amd.transformers.convert import ggml_convert_low_bit
+    for name in ("gguf_iq2_xxs", "gguf_iq2_xs", "gguf_iq1_s", "gguf_iq1_m"):
+        f = Q.get_format(name)
+        assert f.name == "q2_k" and f.bits == 2 and f.kquant
+    cfg = LlamaConfig(vocab_size=64, hidden_size=256, intermediate_size=512, num_hidden_layers=1, num_attention_heads=4)
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(cfg).eval()
+    ggml_convert_low_bit(m, "gguf_iq2_xxs", optimize_model=False)
+    lins = [x for x in m.model.modules() if type(x).__name__ == "KQuantLinear"]
+    assert lins
+    for lin in lins:
+        bpw = 8 * lin.weight.numel() / (lin.in_features * lin.out_features)
+        assert bpw < 3.0, bpw

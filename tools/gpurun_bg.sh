@@ -7,7 +7,7 @@ out=$1; to=$2; cmd=$3
 for i in 1 2 3 4 5 6 7 8; do
   timeout $((to + 900)) /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$out" 2>&1
   rc=$?
-  if grep -q "status=transient\|no free box\|backing off\|stopped responding while being prepared" "$out" && ! grep -q "status=ok\|status=fail" "$out"; then
+  if grep -q "status=transient\|no free box\|backing off\|stopped responding while being prepared\|taken away by the GPU service" "$out" && ! grep -q "status=ok\|status=fail" "$out"; then
     echo "[gpurun_bg] attempt $i: box not acquired, retrying in 60 s" >> "$out.log"
     sleep 60
     continue
