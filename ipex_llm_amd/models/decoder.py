@@ -164,8 +164,11 @@ DEFER_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_GLU_MAX_M", "4"))
 # above it: gate/up as a split-K atomic GEMV staging only its own K slice
 # (deferred norm), act(g / rms) * (u / rms) applied by the down GEMV while it
 # stages its input -- no norm launch, no full-row read per workgroup
-# (ILLM_DEFER_MLP_ACC=0: standalone norm + GLU GEMV instead)
-DEFER_MLP_ACC = __import__("os").environ.get("ILLM_DEFER_MLP_ACC", "1") != "0"
+# Opt-in (ILLM_DEFER_MLP_ACC=1): measured slower on MI355X at batch 8 than the
+# standalone norm + GLU GEMV it replaces (2.49 vs 2.38 ms/step, same box,
+# profiles/bench_b8_r3_mlpacc*.json): the down GEMV's input staging from the
+# [8, 28672] f32 gate/up slab costs more than the norm launch
+DEFER_MLP_ACC = __import__("os").environ.get("ILLM_DEFER_MLP_ACC", "0") == "1"
 # decode batches up to this size take the fused-RoPE attention (qkv accumulated
 # atomically into one slab read by the attention, re-zeroed by its combine).
 # Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token,
