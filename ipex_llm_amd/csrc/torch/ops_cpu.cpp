@@ -149,7 +149,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("gemm(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias) -> Tensor");
   m.def("gemv_accum(Tensor x, Tensor blob, int fmt, int n, int k, Tensor(a!) acc, int ksplit, Tensor(b!)? zero=None, Tensor? rope_cs=None, Tensor? rope_pos=None, int rope_cols=0, int rope_d=0) -> ()");
   m.def("attn_decode_rope(Tensor part, Tensor? bias, Tensor cos_sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int Hq, int rot_dim, bool interleaved, float q_scale, ScalarType dtype, Tensor? pss=None, int pss_n=0, float pss_eps=0.0, bool prerot=False) -> Tensor");
-  m.def("attn_decode_rope_split(Tensor part, Tensor? bias, Tensor cos_sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int Hq, int rot_dim, bool interleaved, float q_scale, ScalarType dtype, Tensor? pss=None, int pss_n=0, float pss_eps=0.0) -> (Tensor, Tensor)");
+  m.def("attn_decode_rope_split(Tensor part, Tensor? bias, Tensor cos_sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int Hq, int rot_dim, bool interleaved, float q_scale, ScalarType dtype, Tensor? pss=None, int pss_n=0, float pss_eps=0.0, bool prerot=False) -> (Tensor, Tensor)");
   m.def("gemm_glu(Tensor x, Tensor blob, int fmt, int n, int k, int act) -> Tensor");
   m.def("moe_gemm(Tensor x, Tensor blob, int fmt, int n, int k, Tensor off, Tensor rows, int xdiv, bool x_sorted, bool out_sorted, bool glu, int act, bool out_f32) -> Tensor");
   m.def("rwkv_wkv4(Tensor time_decay, Tensor time_first, Tensor k, Tensor v, Tensor(a!) num, Tensor(b!) den, Tensor(c!) mx) -> Tensor");

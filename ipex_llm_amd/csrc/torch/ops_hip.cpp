@@ -975,10 +975,10 @@ std::tuple<Tensor, Tensor> attn_decode_rope_split(const Tensor& part, const c10:
                                                   int64_t nsplit, double scale, double softcap, int64_t window,
                                                   int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale,
                                                   at::ScalarType dt, const c10::optional<Tensor>& pss,
-                                                  int64_t pss_n, double pss_eps) {
+                                                  int64_t pss_n, double pss_eps, bool prerot) {
   auto r = attn_decode_rope_impl(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
                                  softcap, window, Hq, rot_dim, interleaved, q_scale, dt, true, pss, pss_n, pss_eps,
-                                 false);
+                                 prerot);
   return {std::get<1>(r), std::get<2>(r)};
 }
 

@@ -450,7 +450,7 @@ class NativeCausalLM(nn.Module):
     _norm_in_env = __import__("os").environ.get("ILLM_NORM_IN", "1") != "0"
 
     def _defer_ok(self, ref: torch.Tensor, T: int) -> bool:
-        return DEFER_NORM and T <= min(ACC_MAX_M, DEFER_MAX_M) and not self._oproj_combine
+        return DEFER_NORM and T <= min(ACC_MAX_M, DEFER_MAX_M)
 
     def _norm_in_ok(self, ref: torch.Tensor, T: int) -> bool:
         lim = max(NORM_IN_MAX_M, DEFER_MAX_M if self._defer_ok(ref, T) else 0)
@@ -675,7 +675,8 @@ class NativeCausalLM(nn.Module):
                     po, pml = ops.attn_decode_rope_split(qkv_acc, qp.bias, self.rope_cache, pos, cache.k[li],
                                                          cache.v[li], meta.block_tables, meta.seq_lens, meta.nsplit,
                                                          s.scale, s.attn_softcap, attn.sliding_window, s.num_heads,
-                                                         s.rot_dim, s.rope_interleaved, 1.0, x.dtype)
+                                                         s.rot_dim, s.rope_interleaved, 1.0, x.dtype, pss=ss_q,
+                                                         pss_n=s.hidden_size, pss_eps=s.rms_eps, prerot=prerot)
                     ops.gemv_attn(po, pml, meta.seq_lens, o.weight, o.fmt, H, o.in_features, accP,
                                   self._oproj_ks, x.dtype, zero=consumed, nw=self._oproj_nw)
                     zero_qkv = qkv_acc

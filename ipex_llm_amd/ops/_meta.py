@@ -174,7 +174,7 @@ def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit
 
 @register_fake("ipex_llm_amd::attn_decode_rope_split")
 def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, Hq,
-      rot_dim, interleaved, q_scale, dtype, pss=None, pss_n=0, pss_eps=0.0):
+      rot_dim, interleaved, q_scale, dtype, pss=None, pss_n=0, pss_eps=0.0, prerot=False):
     B, D = part.shape[0], k_cache.shape[3]
     return (part.new_empty((B, Hq, 1, nsplit, D)), part.new_empty((B, Hq, 1, nsplit, 2)))
 

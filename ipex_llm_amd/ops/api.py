@@ -627,8 +627,10 @@ def gemv_attn(po, pml, seq_lens, blob, fmt, n, k, acc=None, ksplit: int = 0, dty
 
 def attn_decode_rope_split(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
                            softcap, window, Hq: int, rot_dim: int, interleaved: bool, q_scale: float = 1.0,
-                           dtype=torch.bfloat16):
+                           dtype=torch.bfloat16, pss=None, pss_n: int = 0, pss_eps: float = 0.0,
+                           prerot: bool = False):
     """:func:`attn_decode_rope` without the combine: returns the (o, m, l)
     partials for :func:`gemv_attn`; ``part`` is left for the caller to zero."""
     return _ops().attn_decode_rope_split(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens,
-                                         nsplit, scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dtype)
+                                         nsplit, scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dtype,
+                                         pss, pss_n, pss_eps, prerot)

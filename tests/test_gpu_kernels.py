@@ -667,3 +667,28 @@ def test_dequantize_device_kernel(cuda, name, n, k):
         got = torch.ops.ipex_llm_amd.dequantize_device(blob.to(cuda), f, n, k, dt)
         assert got.shape == (n, k)
         assert torch.allclose(got.float().cpu(), ref.to(dt).float(), atol=1e-3, rtol=1e-2), (name, dt)
+
+
+def test_decode_oproj_combine_with_deferred_norm(cuda):
+    """attention partials merged in the o_proj GEMV prologue (opt-in) on top of
+    the deferred norm and the GEMV-epilogue RoPE: same greedy tokens as the
+    combine launch up to rare last-bit ties, graph == eager"""
+    from transformers import LlamaConfig
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.models.decoder import NativeCausalLM
+    cfg = LlamaConfig(vocab_size=512, hidden_size=512, intermediate_size=1024, num_hidden_layers=3,
+                      num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=1024)
+    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=8)
+    prompts = [list(range(1, 50)), list(range(7, 70))]
+    outs = {}
+    try:
+        for flag in (False, True):
+            NativeCausalLM._oproj_combine = flag
+            outs[flag] = Engine(m).generate(prompts, max_new_tokens=10, use_graph=True)
+        eager = Engine(m).generate(prompts, max_new_tokens=10, use_graph=False)
+    finally:
+        NativeCausalLM._oproj_combine = False
+    assert eager == outs[True]
+    a, b = sum(outs[False], []), sum(outs[True], [])
+    assert sum(x == y for x, y in zip(a, b)) >= 0.95 * len(a)
