@@ -23,7 +23,12 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 # A/B builds: ILLM_BUILD_DEFS="-DFOO=1" ILLM_BUILD_TAG=foo -> build/obj_foo, _C_foo.so
-# (loaded with IPEX_LLM_AMD_LIB=_C_foo.so)
+# (loaded with IPEX_LLM_AMD_LIB=_C_foo.so).  ``--debug``: the device-check
+# build (ILLM_DEVICE_DEBUG: launch-geometry / host-contract checks in the hot
+# kernels, csrc/hip/illm_device.h ILLM_DCHECK_FAILS) -> _C_debug.so
+if "--debug" in sys.argv and __name__ == "__main__":
+    os.environ["ILLM_BUILD_DEFS"] = (os.environ.get("ILLM_BUILD_DEFS", "") + " -DILLM_DEVICE_DEBUG=1").strip()
+    os.environ.setdefault("ILLM_BUILD_TAG", "debug")
 _DEFS = os.environ.get("ILLM_BUILD_DEFS", "").split()
 _TAG = os.environ.get("ILLM_BUILD_TAG", "")
 OBJ = os.path.join(ROOT, "build", "obj" + (f"_{_TAG}" if _TAG else ""))

@@ -57,6 +57,14 @@ __device__ __forceinline__ float kv_load1(const uint8_t* base, size_t idx, float
   else return hd_e4m3_to_f32(base[idx]) * scale;
 }
 
+// key count beyond the sequence's block-table row, or more keys than the
+// split grid covers: the sequence's splits leave (reported once, by split 0)
+__device__ __forceinline__ bool bad_len(const AttnDecodeArgs& a, int len, int split) {
+  const bool bad = (int64_t)len > (int64_t)a.max_blocks * a.bs || (int64_t)a.nsplit * SPLIT < len;
+  if (bad && split == 0 && threadIdx.x == 0) kerr(a.err, ERR_SEQ_LEN);
+  return bad;
+}
+
 template <typename T, int D, int KVF>
 __global__ void __launch_bounds__(64) attn_decode_kernel(const AttnDecodeArgs a) {
   constexpr int EB = KVF == 0 ? 2 : 1;  // bytes per cached element
@@ -65,7 +73,7 @@ __global__ void __launch_bounds__(64) attn_decode_kernel(const AttnDecodeArgs a)
   const int lane = threadIdx.x;
   const int len = a.seq_lens[b];
   const int k0 = split * SPLIT;
-  if (k0 >= len) return;
+  if (k0 >= len || bad_len(a, len, split)) return;
   const int group = a.Hq / a.Hkv;
   const int R = group * a.Tq;  // rows: r = t * group + gi
 
@@ -267,7 +275,7 @@ __global__ void __launch_bounds__(64 * NWV) attn_decode_v2_kernel(const AttnDeco
   const int wv = NWV > 1 ? (int)(threadIdx.x >> 6) : 0;
   const int len = a.seq_lens[b];
   const int k0 = split * SPLIT;
-  if (k0 >= len) return;
+  if (k0 >= len || bad_len(a, len, split)) return;
   const int nk = min(SPLIT, len - k0);
   const int group = a.Hq / a.Hkv;
   const int R = group * a.Tq;

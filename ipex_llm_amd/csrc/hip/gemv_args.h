@@ -117,6 +117,7 @@ struct GemvArgs {
   const float* rcs;
   const int64_t* rpos;
   int rcols, rD;
+  int* err;                // kernel error word: set by the dispatcher in ILLM_DEVICE_DEBUG builds
 };
 
 }  // namespace illm

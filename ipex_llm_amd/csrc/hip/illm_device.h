@@ -120,10 +120,35 @@ __device__ __forceinline__ float2 ld8_sc1(const float* p) {
 // id) skips the access and ORs a code here; the host reads it with
 // ops.check_kernel_errors() (ILLM_CHECK_KERNELS=1: after every engine step).
 // The bad access never happens, so a corrupt table is an error, not a fault.
-enum KernelErr : int { ERR_BLOCK_ID = 1, ERR_SLOT = 2, ERR_EXPERT = 4, ERR_SEQ_LEN = 8 };
+enum KernelErr : int { ERR_BLOCK_ID = 1, ERR_SLOT = 2, ERR_EXPERT = 4, ERR_SEQ_LEN = 8, ERR_TOKEN = 16,
+                       ERR_GEOMETRY = 32 };
 __device__ __forceinline__ void kerr(int* err, int code) {
   if (err != nullptr) atomicOr(err, code);
 }
+
+// Debug build (python -m ipex_llm_amd._build --debug -> _C_debug.so, loaded
+// with IPEX_LLM_AMD_LIB=_C_debug.so): ILLM_DCHECK adds launch-geometry and
+// host-contract checks to the hot kernels (grid covers every output tile and
+// K chunk, MoE pair offsets monotonic, ...).  A failed check prints the kernel
+// site once per workgroup, ORs the code into the error word and makes the
+// caller skip the work; the release build compiles the checks out entirely.
+#ifndef ILLM_DEVICE_DEBUG
+#define ILLM_DEVICE_DEBUG 0
+#endif
+#if ILLM_DEVICE_DEBUG
+#define ILLM_DCHECK_FAILS(ok, err, code)                                                              \
+  ([&]() -> bool {                                                                                    \
+    if (ok) return false;                                                                             \
+    if (threadIdx.x == 0) {                                                                           \
+      printf("[illm device check] %s:%d: %s failed (block %u,%u,%u)\n", __FILE__, __LINE__, #ok,       \
+             blockIdx.x, blockIdx.y, blockIdx.z);                                                     \
+      kerr((err), (code));                                                                            \
+    }                                                                                                 \
+    return true;                                                                                      \
+  }())
+#else
+#define ILLM_DCHECK_FAILS(ok, err, code) false
+#endif
 __device__ __forceinline__ bool bad_block(int blk, int num_blocks) {
   return num_blocks > 0 && (unsigned)blk >= (unsigned)num_blocks;
 }

@@ -240,11 +240,11 @@ void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float
                         int e0, int El, uint16_t* out, int Tn, int H, hipStream_t st);
 
 void launch_embedding_rows(bool bf16, const uint8_t* blob, int fmt, const int64_t* ids, int T, int64_t n, int64_t k,
-                           uint16_t* out, hipStream_t st);
+                           uint16_t* out, int* err, hipStream_t st);
 
 void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int64_t* ids, int64_t* next_ids,
                            int64_t* pos, const int32_t* block_tables, int max_blocks, int bs, int64_t* slots,
-                           int32_t* seq_lens, const int64_t* pos_offset, hipStream_t st);
+                           int32_t* seq_lens, const int64_t* pos_offset, int* err, hipStream_t st);
 
 // ---- one-shot / two-shot xGMI peer all-reduce (allreduce.hip) -------------
 constexpr int AR_MAX_RANKS = 8;

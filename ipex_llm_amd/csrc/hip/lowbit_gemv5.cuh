@@ -227,6 +227,10 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
   const int wc0 = c0 + kp * per;
   const int wc1 = min(c1, wc0 + per);
   const bool wave_on = tile0 < NT && wc0 < wc1;
+  // debug build: the host geometry must cover every output tile and K chunk
+  if (ILLM_DCHECK_FAILS((int64_t)gridDim.x * TG * TPW >= NT && (int64_t)nks * cpk >= a.KC && Mloc <= 16, a.err,
+                        ERR_GEOMETRY))
+    return;
   const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
   const size_t soff = (size_t)a.KC * dk_code_chunk(DK) + (size_t)g * 16;   // + c * 64: rows 4g..4g+3
   const size_t moff = soff + (size_t)16 * a.KC * 4;

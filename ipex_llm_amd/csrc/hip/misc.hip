@@ -598,12 +598,15 @@ void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float
 // (reference xe_linear.dequantize_rows, SRC/transformers/embedding.py:213-224)
 template <typename T>
 __global__ void embedding_rows_kernel(const uint8_t* blob, int fmt, const int64_t* ids, int64_t n, int64_t k,
-                                      uint16_t* out) {
+                                      uint16_t* out, int* err) {
   const int t = blockIdx.y;
   const int64_t kk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (kk >= k) return;
   int64_t row = ids[t];
-  row = row < 0 ? 0 : (row >= n ? n - 1 : row);
+  if (row < 0 || row >= n) {                       // out-of-vocabulary id: clamped, reported
+    if (kk == 0) kerr(err, ERR_TOKEN);
+    row = row < 0 ? 0 : n - 1;
+  }
   const int bits = fmt_bits(fmt);
   const int64_t nb = k / QBLOCK;
   const uint8_t* codes = blob + row * (k * bits / 8);
@@ -629,10 +632,10 @@ __global__ void embedding_rows_kernel(const uint8_t* blob, int fmt, const int64_
 }
 
 void launch_embedding_rows(bool bf16, const uint8_t* blob, int fmt, const int64_t* ids, int T, int64_t n, int64_t k,
-                           uint16_t* out, hipStream_t st) {
+                           uint16_t* out, int* err, hipStream_t st) {
   dim3 grid((unsigned)((k / 2 + 255) / 256), (unsigned)T);
-  if (bf16) hipLaunchKernelGGL(embedding_rows_kernel<BF16>, grid, dim3(256), 0, st, blob, fmt, ids, n, k, out);
-  else hipLaunchKernelGGL(embedding_rows_kernel<F16>, grid, dim3(256), 0, st, blob, fmt, ids, n, k, out);
+  if (bf16) hipLaunchKernelGGL(embedding_rows_kernel<BF16>, grid, dim3(256), 0, st, blob, fmt, ids, n, k, out, err);
+  else hipLaunchKernelGGL(embedding_rows_kernel<F16>, grid, dim3(256), 0, st, blob, fmt, ids, n, k, out, err);
 }
 
 // ---- decode-step glue: greedy argmax + position / slot advance -------------------
@@ -645,7 +648,7 @@ __global__ void __launch_bounds__(1024) decode_advance_kernel(const uint16_t* lo
                                                               int64_t* next_ids, int64_t* pos,
                                                               const int32_t* block_tables, int max_blocks, int bs,
                                                               int64_t* slots, int32_t* seq_lens,
-                                                              const int64_t* pos_offset) {
+                                                              const int64_t* pos_offset, int* err) {
   const int b = blockIdx.x, tid = threadIdx.x;
   if (logits) {
     const uint16_t* row = logits + (size_t)b * V;
@@ -706,18 +709,24 @@ __global__ void __launch_bounds__(1024) decode_advance_kernel(const uint16_t* lo
     const int64_t p = pos[b] + 1;
     pos[b] = p;
     const int64_t ci = p - (pos_offset ? pos_offset[b] : 0);      // cache index
-    if (slots) slots[b] = (int64_t)block_tables[(size_t)b * max_blocks + ci / bs] * bs + ci % bs;
+    if (ci < 0 || ci / bs >= max_blocks) {
+      // past the sequence's block-table row: no slot (the KV append skips -1)
+      kerr(err, ERR_SEQ_LEN);
+      if (slots) slots[b] = -1;
+    } else if (slots) {
+      slots[b] = (int64_t)block_tables[(size_t)b * max_blocks + ci / bs] * bs + ci % bs;
+    }
     if (seq_lens) seq_lens[b] = (int32_t)(ci + 1);
   }
 }
 
 void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int64_t* ids, int64_t* next_ids,
                            int64_t* pos, const int32_t* block_tables, int max_blocks, int bs, int64_t* slots,
-                           int32_t* seq_lens, const int64_t* pos_offset, hipStream_t st) {
+                           int32_t* seq_lens, const int64_t* pos_offset, int* err, hipStream_t st) {
   if (bf16) hipLaunchKernelGGL(decode_advance_kernel<BF16>, dim3(B), dim3(1024), 0, st, logits, V, ids, next_ids, pos,
-                               block_tables, max_blocks, bs, slots, seq_lens, pos_offset);
+                               block_tables, max_blocks, bs, slots, seq_lens, pos_offset, err);
   else hipLaunchKernelGGL(decode_advance_kernel<F16>, dim3(B), dim3(1024), 0, st, logits, V, ids, next_ids, pos,
-                          block_tables, max_blocks, bs, slots, seq_lens, pos_offset);
+                          block_tables, max_blocks, bs, slots, seq_lens, pos_offset, err);
 }
 
 // ---- RWKV-4 WKV recurrence (reference xe_linear.rwkv_linear_attention_v4,

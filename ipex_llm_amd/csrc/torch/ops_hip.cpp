@@ -77,11 +77,17 @@ void launch_gemv_any(int fmt, bool bf16, int mt, int epi, dim3 grid, const illm:
   hipStream_t st = cur_stream();
   ILLM_DK_SWITCH(fmt, illm::launch_gemv_dk<DKV>(bf16, mt, epi, grid, a, st));
 }
+int* kernel_err(const c10::Device& dev);
 void launch_gemv5_any(int fmt, bool bf16, int kw, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a0) {
   hipStream_t st = cur_stream();
   static const int pf8 = getenv("ILLM_GEMV5_PF8") ? atoi(getenv("ILLM_GEMV5_PF8")) : 0;
   illm::GemvArgs a = a0;
   a.pf8 = pf8;
+#if ILLM_DEVICE_DEBUG
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  a.err = kernel_err(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)dev));
+#endif
   ILLM_DK_SWITCH(fmt, illm::launch_gemv5_dk<DKV>(bf16, kw, epi, grid, shmem, a, st));
 }
 
@@ -1363,7 +1369,7 @@ Tensor embedding_lowbit(const Tensor& blob, int64_t fmt, int64_t n, int64_t k, c
   const int64_t T = idc.numel();
   if (T > 0)
     illm::launch_embedding_rows(dt == at::kBFloat16, blob.data_ptr<uint8_t>(), (int)fmt, idc.data_ptr<int64_t>(),
-                                (int)T, n, k, m16(out), cur_stream());
+                                (int)T, n, k, m16(out), kernel_err(blob.device()), cur_stream());
   return out;
 }
 
@@ -1388,7 +1394,7 @@ void decode_advance(const c10::optional<Tensor>& logits, Tensor& ids, Tensor& ne
                               (int)block_tables.size(1), (int)bs, slots.data_ptr<int64_t>(),
                               seq_lens.data_ptr<int32_t>(),
                               (pos_offset.has_value() && pos_offset->defined()) ? pos_offset->data_ptr<int64_t>() : nullptr,
-                              cur_stream());
+                              kernel_err(pos.device()), cur_stream());
 }
 
 }  // namespace

@@ -95,7 +95,8 @@ class KernelError(RuntimeError):
 
 
 _KERR_NAMES = {1: "block-table entry outside the KV cache", 2: "cache slot outside the KV cache",
-               4: "expert id out of range", 8: "sequence length out of range"}
+               4: "expert id out of range", 8: "sequence length out of range (block-table row / split grid)",
+               16: "token id outside the vocabulary", 32: "launch geometry does not cover the output (debug build)"}
 
 
 def check_kernel_errors(device=None, reset: bool = True):
