@@ -96,7 +96,13 @@ def test_decode_advance_past_block_table_gives_no_slot():
 _DEBUG_LIB = __import__("os").path.join(__import__("os").path.dirname(ops.__file__), "..", "_C_debug.so")
 
 
-@pytest.mark.skipif(not __import__("os").path.exists(_DEBUG_LIB), reason="debug build not present "
+def _debug_lib_current():
+    import os
+    rel = os.path.join(os.path.dirname(_DEBUG_LIB), "_C.so")
+    return os.path.exists(_DEBUG_LIB) and os.path.getmtime(_DEBUG_LIB) >= os.path.getmtime(rel) - 3600
+
+
+@pytest.mark.skipif(not _debug_lib_current(), reason="debug build absent or older than _C.so "
                     "(python -m ipex_llm_amd._build --debug)")
 def test_device_debug_build_runs_model_clean():
     """the ILLM_DEVICE_DEBUG build (launch-geometry checks in the hot
