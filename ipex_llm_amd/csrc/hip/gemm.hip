@@ -388,6 +388,8 @@ static void launch_gemm_dk(bool bf16, const GemmArgs& a, hipStream_t st) {
   if (tile_env == 2) launch_gemm_v<DK, 4, 4, 2>(bf16, a, st);
   else if (tile_env == 3) launch_gemm_v<DK, 4, 4, 2, 2>(bf16, a, st);
   else if (tile_env == 4) launch_gemm_v<DK, 4, 4, 3, 2>(bf16, a, st);
+  else if (tile_env == 5) launch_gemm_v<DK, 2, 4, 4>(bf16, a, st);
+  else if (tile_env == 6) launch_gemm_v<DK, 2, 4, 6>(bf16, a, st);
   else launch_gemm_v<DK, 2, 8, 4>(bf16, a, st);
 }
 
