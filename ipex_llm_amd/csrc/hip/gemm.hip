@@ -379,17 +379,27 @@ static void launch_gemm_v(bool bf16, const GemmArgs& a, hipStream_t st) {
 
 template <int DK>
 static void launch_gemm_dk(bool bf16, const GemmArgs& a, hipStream_t st) {
-  if (a.moe_off != nullptr) return launch_gemm_v<DK, 2, 8, 4>(bf16, a, st);   // grouped: 128 x 128 blocks
-  // default 128 n x 128 m blocks (2 tiles x 8 m-tiles per wave).  ILLM_GEMM_TILE=2 selects
-  // 256 n x 64 m: half the LDS x traffic per MFMA but 268 registers -> 1 wave per SIMD;
-  // measured on MI355X (Llama-3-8B shapes, sym_int4): M = 1024 qkv/o/down +1..14 %,
-  // gate_up -12 %; M = 8192 -15..18 %
-  static const int tile_env = getenv("ILLM_GEMM_TILE") ? atoi(getenv("ILLM_GEMM_TILE")) : 0;
-  if (tile_env == 2) launch_gemm_v<DK, 4, 4, 2>(bf16, a, st);
-  else if (tile_env == 3) launch_gemm_v<DK, 4, 4, 2, 2>(bf16, a, st);
-  else if (tile_env == 4) launch_gemm_v<DK, 4, 4, 3, 2>(bf16, a, st);
-  else if (tile_env == 5) launch_gemm_v<DK, 2, 4, 4>(bf16, a, st);
-  else if (tile_env == 6) launch_gemm_v<DK, 2, 4, 6>(bf16, a, st);
+  // ILLM_GEMM_TILE: 0 = 128 n x 128 m blocks (2 tiles x 8 m-tiles per wave), 2 = 256 n x 64 m
+  // (half the LDS x traffic per MFMA but 268 registers -> 1 wave per SIMD; M = 1024 qkv/o/down
+  // +1..14 %, gate_up -12 %, M = 8192 -15..18 %), 3/4 = 2 x 2 wave grid (slower everywhere),
+  // 6 = 128 n x 64 m with 6 weight chunks in flight.  Unset: 6 up to M = 768 (and to 1024
+  // without the GLU epilogue), 0 above -- MI355X, Llama-3-8B shapes, sym_int4
+  // (profiles/prefill_gemm_r3_*tile*.jsonl): twice the blocks on 256 CUs, M = 128 down 188 ->
+  // 113 us, qkv 62 -> 40, M = 1024 qkv 95 -> 82, down 214 -> 184 (gate_up 318 -> 333: kept 0);
+  // from M = 2048 the 128 x 128 block's x reuse wins (o 97 vs 108, gate_up 580 vs 640)
+  static const int tile_env = getenv("ILLM_GEMM_TILE") ? atoi(getenv("ILLM_GEMM_TILE")) : -1;
+  const int rows = a.moe_off != nullptr ? a.M / max(1, a.moe_el) : a.M;     // grouped: rows per expert
+  const int tile = tile_env >= 0 ? tile_env : ((rows <= 768 || (rows <= 1024 && !a.glu)) ? 6 : 0);
+  if (a.moe_off != nullptr) {                                                 // grouped MoE
+    if (tile == 6) return launch_gemm_v<DK, 2, 4, 6>(bf16, a, st);
+    return launch_gemm_v<DK, 2, 8, 4>(bf16, a, st);
+  }
+  const int tile_env2 = tile;
+  if (tile_env2 == 2) launch_gemm_v<DK, 4, 4, 2>(bf16, a, st);
+  else if (tile_env2 == 3) launch_gemm_v<DK, 4, 4, 2, 2>(bf16, a, st);
+  else if (tile_env2 == 4) launch_gemm_v<DK, 4, 4, 3, 2>(bf16, a, st);
+  else if (tile_env2 == 5) launch_gemm_v<DK, 2, 4, 4>(bf16, a, st);
+  else if (tile_env2 == 6) launch_gemm_v<DK, 2, 4, 6>(bf16, a, st);
   else launch_gemm_v<DK, 2, 8, 4>(bf16, a, st);
 }
 

@@ -3,14 +3,14 @@
 Two paths: the MFMA kernel with in-register dequant (``csrc/hip/gemm.hip``:
 f16 MFMA, weights decoded straight from the tiled blob, never
 materialised), and dequantize to a transient dense weight + library GEMM
-(hipBLASLt).  Measured on MI355X at Llama-3-8B shapes (sym_int4,
-profiles/prefill_gemm_r2_sweep.jsonl): the library path wins from M = 512 on
-for every projection (M = 1024: qkv 64.7 vs 90.9 us, o 49.5 vs 67.7,
-gate_up 256.6 vs 296.6, down 142.2 vs 205.4) and at M = 256 for the
-N = 4096 projections, whose 128 x 128 fused grid leaves most CUs idle (down
-77 vs 181 us); the fused kernel keeps M <= 128 and the wide-N projections up
-to M = 384 (M = 256: qkv 62 vs 77, gate_up 92 vs 145).  In the model:
-Llama-3-8B first token at 1024 tokens 23.5 -> 21.8 ms.
+(hipBLASLt).  Measured on MI355X at Llama-3-8B shapes (sym_int4, the fused
+kernel with its round-3 128 n x 64 m blocks below M = 1024,
+profiles/prefill_gemm_r3_small_tile6.jsonl): the fused kernel wins for the
+wide projections (M = 256: qkv 40 vs 53 us, gate_up 93 vs 129; M = 384:
+gate_up 130 vs 134) and for every shape at M <= 128 except the long-K down
+projection (M = 128: 113 vs 84 us -- its 4096-wide output gives few blocks
+for 14336-deep K); the library path wins above (M = 1024: qkv 64.7 vs 82,
+o 50 vs 62, gate_up 239 vs 318, down 138 vs 184).
 ``ILLM_GEMM_LIB=1`` / ``ILLM_GEMM_FUSED=1`` force either path (A/B runs).
 """
 from __future__ import annotations
@@ -22,17 +22,25 @@ import torch.nn.functional as F
 
 _USE_LIB = os.environ.get("ILLM_GEMM_LIB", "0") == "1"
 _USE_FUSED = os.environ.get("ILLM_GEMM_FUSED", "0") == "1"
-FUSED_MAX_M = 128          # fused kernel for every shape up to here
-FUSED_WIDE_MAX_M = 384     # ... and for wide projections (N >= FUSED_WIDE_N) up to here
-FUSED_WIDE_N = 6144
+FUSED_MAX_M = 128          # fused kernel for every shape up to here (K <= FUSED_LONG_K)
+FUSED_LONG_K = 8192        # deeper K (down projections): library path from M > 64
+FUSED_QKV_MAX_M = 256      # N >= 6144 (fused qkv) up to here
+FUSED_WIDE_MAX_M = 384     # N >= FUSED_WIDE_N (gate/up pairs) up to here
+FUSED_WIDE_N = 12288
 
 
-def use_fused(M: int, n: int) -> bool:
+def use_fused(M: int, n: int, k: int = 0) -> bool:
     if _USE_LIB:
         return False
     if _USE_FUSED:
         return True
-    return M <= FUSED_MAX_M or (M <= FUSED_WIDE_MAX_M and n >= FUSED_WIDE_N)
+    if k > FUSED_LONG_K:
+        return M <= 64
+    if n >= FUSED_WIDE_N:
+        return M <= FUSED_WIDE_MAX_M
+    if n >= 6144:
+        return M <= FUSED_QKV_MAX_M
+    return M <= FUSED_MAX_M
 
 
 # ---- dense-weight prefetch for the library path ---------------------------
@@ -61,7 +69,7 @@ def prefetch_dense(items, M: int, dtype) -> None:
         return
     ops = torch.ops.ipex_llm_amd
     for blob, fmt, n, k in items:
-        if not blob.is_cuda or use_fused(M, n):
+        if not blob.is_cuda or use_fused(M, n, k):
             continue
         key = _key(blob, n, k, dtype)
         if key in _ready:
@@ -126,7 +134,7 @@ def drop_prefetched() -> None:
 def lowbit_gemm(x, blob, fmt, n, k, bias=None):
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
-    if use_fused(M, n) and hasattr(ops, "gemm"):
+    if use_fused(M, n, k) and hasattr(ops, "gemm"):
         return ops.gemm(x, blob, fmt, n, k, bias)
     w = _dense_weight(blob, fmt, n, k, x.dtype)
     return F.linear(x, w, bias)
@@ -138,7 +146,7 @@ def lowbit_gemm_glu(x, blob, fmt, n, k, act: int = 0):
     [M, 2I] round trip, no elementwise launches)."""
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
-    if use_fused(M, n) and hasattr(ops, "gemm_glu"):
+    if use_fused(M, n, k) and hasattr(ops, "gemm_glu"):
         return ops.gemm_glu(x, blob, fmt, n, k, act)
     from .api import glu
     return glu(lowbit_gemm(x, blob, fmt, n, k), act, tile=16)

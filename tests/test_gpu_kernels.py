@@ -422,7 +422,7 @@ def test_gemv_glu(cuda, M):
 
 
 @pytest.mark.parametrize("name", ["sym_int4", "nf4", "fp8_e4m3"])
-@pytest.mark.parametrize("M", [100, 700])
+@pytest.mark.parametrize("M", [100, 700, 900])          # 128 n x 64 m blocks up to 768 rows, 128 x 128 above
 def test_lowbit_gemm_glu_epilogue(cuda, name, M):
     """prefill GEMM with act(gate) * up in the epilogue vs GEMM + torch GLU"""
     from ipex_llm_amd.models.decoder import deinterleave_glu, interleave_glu_rows
@@ -440,9 +440,10 @@ def test_lowbit_gemm_glu_epilogue(cuda, name, M):
         assert y.shape == (M, I) and _rel(y, ref) < 1e-2, (name, M, act)
 
 
-def test_lowbit_gemm_prefill(cuda):
+@pytest.mark.parametrize("M", [200, 1500])             # both block shapes of the auto tile choice
+def test_lowbit_gemm_prefill(cuda, M):
     f = get_format("sym_int4").fmt
-    n, k, M = 384, 512, 200
+    n, k = 384, 512
     w = torch.randn(n, k, device=cuda) * 0.05
     blob = ops.quantize(w, f)
     x = torch.randn(M, k, device=cuda).bfloat16()

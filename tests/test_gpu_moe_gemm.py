@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("qtype", ["sym_int4", "asym_int4", "sym_int8"])
-@pytest.mark.parametrize("T,E,k", [(37, 4, 2), (300, 8, 2), (129, 16, 4)])
+@pytest.mark.parametrize("T,E,k", [(37, 4, 2), (300, 8, 2), (129, 16, 4), (1700, 4, 2)])
 def test_moe_gemm_matches_reference(cuda, qtype, T, E, k):
     from ipex_llm_amd import ops
     from ipex_llm_amd.ops import reference as R
