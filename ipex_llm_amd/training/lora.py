@@ -77,6 +77,60 @@ DEFAULT_TARGETS = ["q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj
                    "qkv_proj", "gate_up_proj", "query_key_value", "dense", "W_pack"]
 
 
+_FUSED = os.environ.get("ILLM_LORA_FUSED", "1") == "1"
+
+
+def _base_dense_weight(base, dt):
+    """the frozen base weight as the backward GEMM operand: the resident dense
+    shadow / a transient dequant on the GPU (as MatMulLowBit), dequant on CPU"""
+    from .. import ops
+    if base.weight.is_cuda and ops.native_gpu(base.weight):
+        from ..ops.gemm import _dense_weight
+        return _dense_weight(base.weight, base.fmt, base.out_features, base.in_features, dt)
+    return ops.dequantize(base.weight, base.fmt, base.out_features, base.in_features, dtype=dt)
+
+
+class _LoraLowBitFn(torch.autograd.Function):
+    """y = x W^T (+ bias) + s (x A^T) B^T over a frozen low-bit W as one
+    autograd node.  The LoRA term accumulates into the base GEMM's output
+    (addmm, beta = 1, alpha = s) and, backward, into grad_x = g W + (s g B) A
+    (one accumulating rank-r GEMM): the scale, the two adds over [M, N] /
+    [M, K] and the cast that the module-by-module graph launches per adapter
+    disappear (reference LoraLowBitLinear.forward, SRC/transformers/qlora.py:114-143)."""
+
+    @staticmethod
+    def forward(ctx, x, A, B, base, s):
+        from .. import ops
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        bias = base.bias
+        if bias is not None and bias.dtype != x2.dtype:
+            bias = bias.to(x2.dtype)
+        with torch.no_grad():
+            y = ops.lowbit_matmul(x2, base.weight, base.fmt, base.out_features, base.in_features, bias)
+            xa = torch.mm(x2, A.t())
+            y.addmm_(xa, B.t(), alpha=s)
+        ctx.save_for_backward(x2, xa, A, B)
+        ctx.base, ctx.s, ctx.shp = base, s, shp
+        return y.view(*shp[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, xa, A, B = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1]).to(x2.dtype)
+        s = ctx.s
+        gxa = torch.mm(g2, B).mul_(s)                     # [M, r]
+        gA = torch.mm(gxa.t(), x2) if ctx.needs_input_grad[1] else None
+        gB = torch.mm(g2.t(), xa).mul_(s) if ctx.needs_input_grad[2] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            w = _base_dense_weight(ctx.base, x2.dtype)
+            gx = torch.mm(g2, w)
+            gx.addmm_(gxa, A)
+            gx = gx.view(ctx.shp)
+        return gx, gA, gB, None, None
+
+
 class LoraLinear(nn.Module):
     """base(x) + B(A(dropout(pool(x)))) * scaling over a frozen base layer
     (LowBitLinear -> QLoRA/QA-LoRA, DenseLinear/nn.Linear -> LoRA)."""
@@ -113,7 +167,16 @@ class LoraLinear(nn.Module):
             return x
         return x.reshape(*x.shape[:-1], self.in_features // self.qa_group, self.qa_group).mean(-1)
 
+    def _fused_ok(self, x) -> bool:
+        b = self.base_layer
+        return (_FUSED and isinstance(b, LowBitLinear) and not self.qa_group and torch.is_grad_enabled()
+                and isinstance(self.lora_dropout, nn.Identity) and b.g_idx_map is None and b.mp_group is None
+                and x.dtype == self.lora_A.weight.dtype and x.dtype in (torch.bfloat16, torch.float16)
+                and x.device == b.weight.device and (x.requires_grad or self.lora_A.weight.requires_grad))
+
     def forward(self, x):
+        if not (self.disable_adapters or self.merged) and self._fused_ok(x):
+            return _LoraLowBitFn.apply(x, self.lora_A.weight, self.lora_B.weight, self.base_layer, self.scaling)
         result = self.base_layer(x)
         if self.disable_adapters or self.merged:
             return result

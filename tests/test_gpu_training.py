@@ -84,3 +84,27 @@ def test_qlora_step_on_gpu(cuda, tmp_path):
         opt.zero_grad()
         losses.append(loss.item())
     assert losses[-1] < losses[0] - 0.05, losses
+
+
+@pytest.mark.parametrize("qtype", ["nf4", "sym_int4"])
+def test_fused_lora_node_on_gpu(cuda, monkeypatch, qtype):
+    """one-node QLoRA linear on the HIP GEMM path (M = 640: library GEMM +
+    accumulating rank-r addmm) == the module-by-module graph"""
+    import ipex_llm_amd.training.lora as L
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    torch.manual_seed(2)
+    base = LowBitLinear.from_linear(torch.nn.Linear(512, 384, bias=False), qtype).to(cuda)
+    lay = L.LoraLinear(base, r=8, alpha=16).to(cuda)
+    torch.nn.init.normal_(lay.lora_B.weight, std=0.05)
+    x0 = torch.randn(4, 160, 512, device=cuda).to(torch.bfloat16)
+    gy = torch.randn(4, 160, 384, device=cuda).to(torch.bfloat16)
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(L, "_FUSED", fused)
+        x = x0.clone().requires_grad_()
+        lay.zero_grad()
+        y = lay(x)
+        y.backward(gy)
+        res[fused] = (y.float(), x.grad.float(), lay.lora_A.weight.grad.float(), lay.lora_B.weight.grad.float())
+    for a, b in zip(res[True], res[False]):
+        assert ((a - b).norm() / b.norm()).item() < 2e-2

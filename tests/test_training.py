@@ -217,3 +217,32 @@ def test_grad_bucket_sync_matches_full_batch():
     for p in ps:
         p.join(300)
     assert [p.exitcode for p in ps] == [0, 0]
+
+
+@pytest.mark.parametrize("bias", [False, True])
+def test_fused_lora_node_matches_module_graph(monkeypatch, bias):
+    """the one-node QLoRA linear (LoRA term accumulated into the base GEMM
+    output and into grad_x) == base + B(A(x)) * s built module by module"""
+    import ipex_llm_amd.training.lora as L
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    torch.manual_seed(1)
+    lin = torch.nn.Linear(256, 192, bias=bias)
+    base = LowBitLinear.from_linear(lin, "sym_int4")
+    if bias:
+        base.bias.data = base.bias.data.to(torch.bfloat16)
+    lay = L.LoraLinear(base, r=8, alpha=16)
+    torch.nn.init.normal_(lay.lora_B.weight, std=0.05)
+    x0 = torch.randn(2, 5, 256).to(torch.bfloat16)
+    gy = torch.randn(2, 5, 192).to(torch.bfloat16)
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(L, "_FUSED", fused)
+        assert lay._fused_ok(x0.clone().requires_grad_()) == fused
+        x = x0.clone().requires_grad_()
+        lay.zero_grad()
+        y = lay(x)
+        y.backward(gy)
+        res[fused] = (y.float(), x.grad.float(), lay.lora_A.weight.grad.float(), lay.lora_B.weight.grad.float())
+    for a, b in zip(res[True], res[False]):
+        assert a.shape == b.shape
+        assert ((a - b).norm() / b.norm()).item() < 2e-2
