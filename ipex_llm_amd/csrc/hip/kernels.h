@@ -103,6 +103,8 @@ struct NormArgs {
   int zero_partials;       // re-zero the (atomic-accumulated) partial slab after reading it
 };
 void launch_add_rms_norm(bool bf16, const NormArgs& a, hipStream_t st);
+void launch_rms_norm_bwd(bool bf16, const uint16_t* x, const uint16_t* g, const uint16_t* w, uint16_t* dx, int M,
+                         int H, float eps, int unit_offset, hipStream_t st);
 void launch_layer_norm(bool bf16, const uint16_t* x, const uint16_t* w, const uint16_t* b,
                        uint16_t* out, int M, int H, float eps, hipStream_t st);
 

@@ -169,6 +169,64 @@ static void launch_add_rms(const NormArgs& a, hipStream_t st) {
 #undef L_RMS
 }
 
+// ---- RMSNorm backward (training: QLoRA base models keep their norms frozen)
+// dL/dx of out = w * rnd(x * r), r = rsqrt(mean(x^2) + eps), for the gradient g
+// of out, matching the autograd graph of LlamaRMSNorm: gh = rnd(g * w) (the
+// bf16 product), then in f32 dx = r gh - x r^3 mean(gh x).  One workgroup per
+// row: x, g and w loaded once, two block reductions, one store.
+template <typename T, int MAXV>
+__global__ void __launch_bounds__(NORM_THREADS)
+    rms_norm_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ g,
+                        const uint16_t* __restrict__ w, uint16_t* __restrict__ dx, int H, float eps,
+                        int unit_offset) {
+  __shared__ float red[NORM_THREADS / 64];
+  const int row = blockIdx.x;
+  float xv[MAXV][8], gh[MAXV][8];
+  float ss = 0.f, dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; j++) {
+    const int c = (threadIdx.x + j * NORM_THREADS) * 8;
+    if (c < H) {
+      float gv[8], wv[8];
+      load8<T>(x + (size_t)row * H + c, xv[j]);
+      load8<T>(g + (size_t)row * H + c, gv);
+      load8<T>(w + c, wv);
+      for (int i = 0; i < 8; i++) {
+        const float ww = unit_offset ? rnd<T>(1.f + wv[i]) : wv[i];
+        gh[j][i] = rnd<T>(gv[i] * ww);
+        ss += xv[j][i] * xv[j][i];
+        dot += gh[j][i] * xv[j][i];
+      }
+    }
+  }
+  ss = block_sum<NORM_THREADS>(ss, red);
+  dot = block_sum<NORM_THREADS>(dot, red);
+  const float r = rsqrtf(ss / (float)H + eps);
+  const float k = r * r * r * dot / (float)H;
+#pragma unroll
+  for (int j = 0; j < MAXV; j++) {
+    const int c = (threadIdx.x + j * NORM_THREADS) * 8;
+    if (c < H) {
+      float o[8];
+      for (int i = 0; i < 8; i++) o[i] = r * gh[j][i] - k * xv[j][i];
+      store8<T>(dx + (size_t)row * H + c, o);
+    }
+  }
+}
+
+void launch_rms_norm_bwd(bool bf16, const uint16_t* x, const uint16_t* g, const uint16_t* w, uint16_t* dx, int M,
+                         int H, float eps, int unit_offset, hipStream_t st) {
+  const int nv = (H / 8 + NORM_THREADS - 1) / NORM_THREADS;
+#define L_BWD(TT, MV) \
+  hipLaunchKernelGGL((rms_norm_bwd_kernel<TT, MV>), dim3(M), dim3(NORM_THREADS), 0, st, x, g, w, dx, H, eps, unit_offset)
+  if (bf16) {
+    if (nv <= 1) L_BWD(BF16, 1); else if (nv <= 2) L_BWD(BF16, 2); else if (nv <= 4) L_BWD(BF16, 4); else L_BWD(BF16, 8);
+  } else {
+    if (nv <= 1) L_BWD(F16, 1); else if (nv <= 2) L_BWD(F16, 2); else if (nv <= 4) L_BWD(F16, 4); else L_BWD(F16, 8);
+  }
+#undef L_BWD
+}
+
 void launch_add_rms_norm(bool bf16, const NormArgs& a, hipStream_t st) {
   if (bf16) launch_add_rms<BF16>(a, st); else launch_add_rms<F16>(a, st);
 }

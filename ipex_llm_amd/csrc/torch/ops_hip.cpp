@@ -668,6 +668,24 @@ Tensor add_rms_norm(const c10::optional<Tensor>& x, const c10::optional<Tensor>&
   return out;
 }
 
+// gradient of rms_norm(x) * w w.r.t. x (frozen w), HF rounding
+Tensor rms_norm_bwd(const Tensor& x, const Tensor& g, const Tensor& w, double eps, bool unit_offset) {
+  c10::DeviceGuard dg(x.device());
+  const int64_t H = w.numel();
+  TORCH_CHECK(x.is_contiguous() && g.is_contiguous() && x.numel() == g.numel() && x.numel() % H == 0,
+              "rms_norm_bwd: contiguous x and grad of one shape");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type() && g.scalar_type() == w.scalar_type() &&
+                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "rms_norm_bwd: bf16/f16 x, grad and weight");
+  TORCH_CHECK(H % 8 == 0 && H <= 8 * 512 * 8, "rms_norm_bwd: hidden size multiple of 8, <= 32768");
+  Tensor dx = at::empty_like(x);
+  const int64_t M = x.numel() / H;
+  if (M > 0)
+    illm::launch_rms_norm_bwd(is_bf16(x), p16(x), p16(g), p16(w), m16(dx), (int)M, (int)H, (float)eps, unit_offset,
+                              cur_stream());
+  return dx;
+}
+
 Tensor layer_norm(const Tensor& x, const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
                   double eps) {
   c10::DeviceGuard g(x.device());
@@ -1426,6 +1444,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("moe_group_topk", &moe_group_topk);
   m.impl("gemv_attn", &gemv_attn);
   m.impl("add_rms_norm", &add_rms_norm);
+  m.impl("rms_norm_bwd", &rms_norm_bwd);
   m.impl("layer_norm", &layer_norm);
   m.impl("kernel_errors", &kernel_errors);
   m.impl("rope_kv", &rope_kv);

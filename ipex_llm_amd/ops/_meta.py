@@ -37,6 +37,11 @@ def _(x, partials, residual, w, eps, unit_offset, store_residual, zero_partials=
     return w.new_empty((partials.shape[1], w.shape[0]))
 
 
+@register_fake("ipex_llm_amd::rms_norm_bwd")
+def _(x, g, w, eps, unit_offset):
+    return torch.empty_like(x)
+
+
 @register_fake("ipex_llm_amd::layer_norm")
 def _(x, w, b, eps):
     return torch.empty_like(x)

@@ -286,11 +286,35 @@ def _replace_with_low_bit_linear(model: nn.Module, qtype: int, modules_to_not_co
 
 
 # ----------------------------------------------------------------- post
+class _RMSNormFn(torch.autograd.Function):
+    """HIP RMSNorm forward + HIP backward for x (frozen weight, the QLoRA
+    case): one kernel each way instead of the ~6 f32 cast / pow / mean /
+    rsqrt / mul kernels per direction of the HF module (reference
+    xe_addons.rms_norm, SRC/transformers/models/common.py:184-200)"""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        from .. import ops
+        ctx.save_for_backward(x, w)
+        ctx.eps = eps
+        return ops.rms_norm(x, w, eps)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        return torch.ops.ipex_llm_amd.rms_norm_bwd(x, g.contiguous(), w, ctx.eps, False), None, None
+
+
 def _rmsnorm_forward(self, hidden_states):
     from .. import ops
     w = self.weight
     eps = getattr(self, "variance_epsilon", None) or getattr(self, "eps", 1e-6)
     if hidden_states.is_cuda and hidden_states.dtype == w.dtype and hidden_states.shape[-1] % 8 == 0:
+        if torch.is_grad_enabled() and (hidden_states.requires_grad or w.requires_grad):
+            if not w.requires_grad and ops.native_gpu(hidden_states):
+                return _RMSNormFn.apply(hidden_states.contiguous(), w, eps)
+            from ..ops import reference as R
+            return R.rms_norm(hidden_states, w, eps)          # differentiable torch graph
         return ops.rms_norm(hidden_states.contiguous(), w, eps)
     from ..ops import reference as R
     return R.rms_norm(hidden_states, w.to(hidden_states.dtype), eps)

@@ -108,3 +108,27 @@ def test_fused_lora_node_on_gpu(cuda, monkeypatch, qtype):
         res[fused] = (y.float(), x.grad.float(), lay.lora_A.weight.grad.float(), lay.lora_B.weight.grad.float())
     for a, b in zip(res[True], res[False]):
         assert ((a - b).norm() / b.norm()).item() < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H", [512, 4096])
+def test_rms_norm_backward_kernel(cuda, dtype, H):
+    """HIP RMSNorm backward (frozen weight) vs autograd through the fp32 torch
+    RMSNorm; the patched module's forward/backward through the autograd node"""
+    import types
+    from ipex_llm_amd.transformers.convert import _rmsnorm_forward
+    torch.manual_seed(3)
+    x = torch.randn(37, H, device=cuda).to(dtype)
+    w = (1 + 0.1 * torch.randn(H, device=cuda)).to(dtype)
+    g = torch.randn(37, H, device=cuda).to(dtype)
+    xr = x.float().requires_grad_()
+    h = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5)
+    (h * w.float()).backward(g.float())
+    dx = torch.ops.ipex_llm_amd.rms_norm_bwd(x, g, w, 1e-5, False)
+    assert ((dx.float() - xr.grad).norm() / xr.grad.norm()).item() < 1e-2
+    mod = types.SimpleNamespace(weight=w, variance_epsilon=1e-5)
+    x2 = x.clone().requires_grad_()
+    y = _rmsnorm_forward(mod, x2)
+    assert y.grad_fn is not None
+    y.backward(g)
+    assert ((x2.grad.float() - xr.grad).norm() / xr.grad.norm()).item() < 1e-2

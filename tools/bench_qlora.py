@@ -95,6 +95,10 @@ def main():
     t0 = time.perf_counter()
     model = random_qlora_base(cfg, args.qtype, dev)
     model.config.use_cache = False
+    if os.environ.get("ILLM_TRAIN_NORM", "1") == "1":
+        # optimize_model's norm patch: HIP RMSNorm forward + backward (frozen weight)
+        from ipex_llm_amd.transformers.convert import _patch_norms
+        _patch_norms(model)
     if args.grad_ckpt:
         model.gradient_checkpointing_enable()
         model.enable_input_require_grads()

@@ -1,0 +1,12 @@
+#!/bin/bash
+# HIP RMSNorm backward for training: tests + QLoRA step A/B (ILLM_TRAIN_NORM=0: HF module norms)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py tests/test_gpu_kernels.py -x -q --timeout 200 --timeout-method thread -k "norm or lora or qlora or adamw" > gpurun_out/pt_r3af.log 2>&1
+rc=$?; tail -2 gpurun_out/pt_r3af.log; [ $rc -ne 0 ] && exit $rc
+for cfg in "1 0" "0 0" "1 40" "1 0"; do
+  set -- $cfg
+  ILLM_TRAIN_NORM=$1 ILLM_PREFILL_DENSE_GB=$2 timeout -k 10 400 python tools/bench_qlora.py --steps 8 --warmup 2 > gpurun_out/qlora_n$1_gb$2.log 2>&1 || exit $?
+  echo "hip_norm=$1 shadow_gb=$2 $(tail -1 gpurun_out/qlora_n$1_gb$2.log | grep -o '"ms_per_step": [0-9.]*\|"loss_last": [0-9.]*' | tr '\n' ' ')"
+done
+ILLM_PREFILL_DENSE_GB=40 bash tools/prof_qlora.sh && head -30 gpurun_out/prof_qlora_summary.txt
