@@ -594,6 +594,61 @@ void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float
   else hipLaunchKernelGGL(moe_combine_kernel<F16>, grid, dim3(256), 0, st, part, ks, P, w, ids, k, e0, El, out, Tn, H);
 }
 
+// ---- rotate-half RoPE on [B, H, T, D] activations (training / HF-forward path)
+// out = x cos + rotate_half(x) sin with HF's bf16 rounding (each product, then
+// the sum), x with any batch / head / token strides (the transposed q / k
+// projection views) and D contiguous; cos / sin [Bc, T, D] (Bc = B or 1).
+// bwd: the transposed rotation for the gradient, dx = g cos - rotate_half(g sin)
+// (reference: the rotary wrappers of SRC/transformers/models/common.py and
+// their xe_addons kernels; here also differentiated for QLoRA).
+template <typename T>
+__global__ void __launch_bounds__(256) rope_half_kernel(const uint16_t* __restrict__ x, int64_t sb, int64_t sh,
+                                                        int64_t st, const uint16_t* __restrict__ cs,
+                                                        const uint16_t* __restrict__ sn, int64_t csb,
+                                                        uint16_t* __restrict__ out, int B, int H, int Tn, int D,
+                                                        int bwd) {
+  const int half = D / 2, per_row = half / 4;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = gid / per_row;
+  if (row >= (int64_t)B * H * Tn) return;
+  const int j = (int)(gid % per_row) * 4;
+  const int t = (int)(row % Tn), h = (int)((row / Tn) % H), b = (int)(row / ((int64_t)Tn * H));
+  const uint16_t* xr = x + b * sb + h * sh + t * st;
+  const size_t co = (size_t)b * csb + (size_t)t * D;
+  auto ld4 = [](const uint16_t* p, float* v) {
+    const uint2 u = *(const uint2*)p;
+    v[0] = to_f32<T>(u.x & 0xffff); v[1] = to_f32<T>(u.x >> 16);
+    v[2] = to_f32<T>(u.y & 0xffff); v[3] = to_f32<T>(u.y >> 16);
+  };
+  float x1[4], x2[4], c1[4], c2[4], s1[4], s2[4], o1[4], o2[4];
+  ld4(xr + j, x1); ld4(xr + half + j, x2);
+  ld4(cs + co + j, c1); ld4(cs + co + half + j, c2);
+  ld4(sn + co + j, s1); ld4(sn + co + half + j, s2);
+  auto r = [](float v) { return to_f32<T>(from_f32<T>(v)); };
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (!bwd) {
+      o1[i] = r(x1[i] * c1[i]) + r(-x2[i] * s1[i]);
+      o2[i] = r(x2[i] * c2[i]) + r(x1[i] * s2[i]);
+    } else {
+      o1[i] = r(x1[i] * c1[i]) + r(x2[i] * s2[i]);
+      o2[i] = r(x2[i] * c2[i]) - r(x1[i] * s1[i]);
+    }
+  }
+  uint16_t* orow = out + (size_t)row * D;
+  *(uint2*)(orow + j) = make_uint2(pack2<T>(o1[0], o1[1]), pack2<T>(o1[2], o1[3]));
+  *(uint2*)(orow + half + j) = make_uint2(pack2<T>(o2[0], o2[1]), pack2<T>(o2[2], o2[3]));
+}
+
+void launch_rope_half(bool bf16, const uint16_t* x, int64_t sb, int64_t sh, int64_t st, const uint16_t* cs,
+                      const uint16_t* sn, int64_t csb, uint16_t* out, int B, int H, int Tn, int D, int bwd,
+                      hipStream_t s) {
+  const int64_t n = (int64_t)B * H * Tn * (D / 8);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (bf16) hipLaunchKernelGGL(rope_half_kernel<BF16>, grid, dim3(256), 0, s, x, sb, sh, st, cs, sn, csb, out, B, H, Tn, D, bwd);
+  else hipLaunchKernelGGL(rope_half_kernel<F16>, grid, dim3(256), 0, s, x, sb, sh, st, cs, sn, csb, out, B, H, Tn, D, bwd);
+}
+
 // ---- low-bit embedding gather: canonical blob rows -> dense [T, k] --------------
 // (reference xe_linear.dequantize_rows, SRC/transformers/embedding.py:213-224)
 template <typename T>

@@ -668,6 +668,27 @@ Tensor add_rms_norm(const c10::optional<Tensor>& x, const c10::optional<Tensor>&
   return out;
 }
 
+// rotate-half RoPE of a [B, H, T, D] view (D contiguous) -> contiguous [B, H, T, D]
+Tensor rope_half(const Tensor& x, const Tensor& cos, const Tensor& sin, bool bwd) {
+  c10::DeviceGuard dg(x.device());
+  TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "rope_half: x [B, H, T, D] with contiguous D");
+  const int64_t B = x.size(0), H = x.size(1), Tn = x.size(2), D = x.size(3);
+  TORCH_CHECK(D % 8 == 0, "rope_half: head dim multiple of 8");
+  TORCH_CHECK(cos.dim() == 3 && cos.is_contiguous() && sin.is_contiguous() && cos.sizes() == sin.sizes() &&
+                  cos.size(1) == Tn && cos.size(2) == D && (cos.size(0) == B || cos.size(0) == 1),
+              "rope_half: cos / sin [B or 1, T, D] contiguous");
+  TORCH_CHECK(x.scalar_type() == cos.scalar_type() && x.scalar_type() == sin.scalar_type() &&
+                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "rope_half: bf16/f16 x, cos, sin");
+  TORCH_CHECK(x.stride(0) % 4 == 0 && x.stride(1) % 4 == 0 && x.stride(2) % 4 == 0, "rope_half: 8-B aligned rows");
+  Tensor out = at::empty({B, H, Tn, D}, x.options());
+  if (out.numel() > 0)
+    illm::launch_rope_half(is_bf16(x), (const uint16_t*)x.data_ptr(), x.stride(0), x.stride(1), x.stride(2),
+                           p16(cos), p16(sin), cos.size(0) == 1 ? 0 : Tn * D, m16(out), (int)B, (int)H, (int)Tn,
+                           (int)D, bwd ? 1 : 0, cur_stream());
+  return out;
+}
+
 // gradient of rms_norm(x) * w w.r.t. x (frozen w), HF rounding
 Tensor rms_norm_bwd(const Tensor& x, const Tensor& g, const Tensor& w, double eps, bool unit_offset) {
   c10::DeviceGuard dg(x.device());
@@ -1445,6 +1466,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv_attn", &gemv_attn);
   m.impl("add_rms_norm", &add_rms_norm);
   m.impl("rms_norm_bwd", &rms_norm_bwd);
+  m.impl("rope_half", &rope_half);
   m.impl("layer_norm", &layer_norm);
   m.impl("kernel_errors", &kernel_errors);
   m.impl("rope_kv", &rope_kv);

@@ -42,6 +42,11 @@ def _(x, g, w, eps, unit_offset):
     return torch.empty_like(x)
 
 
+@register_fake("ipex_llm_amd::rope_half")
+def _(x, cos, sin, bwd):
+    return x.new_empty(x.shape)
+
+
 @register_fake("ipex_llm_amd::layer_norm")
 def _(x, w, b, eps):
     return torch.empty_like(x)

@@ -339,6 +339,68 @@ def _patch_routers(model: nn.Module):
             m.forward = types.MethodType(_ds_router_forward, m)
 
 
+class _RopeHalfFn(torch.autograd.Function):
+    """rotate-half RoPE of the HF forward as one HIP kernel each way (the
+    transposed rotation for the gradient) instead of mul / slice / neg / cat
+    / mul / add per tensor and direction"""
+
+    @staticmethod
+    def forward(ctx, x, cos, sin):
+        ctx.save_for_backward(cos, sin)
+        return torch.ops.ipex_llm_amd.rope_half(x, cos, sin, False)
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin = ctx.saved_tensors
+        return torch.ops.ipex_llm_amd.rope_half(g, cos, sin, True), None, None
+
+
+_ROPE_ORIG = {}
+
+
+def _rope_fusable(q, cos, unsqueeze_dim):
+    from .. import ops
+    return (isinstance(unsqueeze_dim, int) and unsqueeze_dim == 1 and q.dim() == 4 and cos.dim() == 3 and q.is_cuda and ops.native_gpu(q)
+            and q.stride(-1) == 1 and q.shape[-1] % 8 == 0 and cos.shape[-1] == q.shape[-1]
+            and cos.shape[1] == q.shape[2] and cos.dtype == q.dtype and q.dtype in (torch.bfloat16, torch.float16)
+            and cos.shape[0] in (1, q.shape[0]) and all(st % 4 == 0 for st in q.stride()[:3]))
+
+
+def _make_rope(orig):
+    def apply_rotary_pos_emb(q, k, cos, sin, unsqueeze_dim=1, **kw):
+        if not kw and _rope_fusable(q, cos, unsqueeze_dim) and _rope_fusable(k, cos, unsqueeze_dim):
+            cos, sin = cos.contiguous(), sin.contiguous()
+            return _RopeHalfFn.apply(q, cos, sin), _RopeHalfFn.apply(k, cos, sin)
+        return orig(q, k, cos, sin, unsqueeze_dim, **kw)
+    apply_rotary_pos_emb.__wrapped__ = orig
+    return apply_rotary_pos_emb
+
+
+def _patch_rope(model: nn.Module):
+    """the HF modeling module's ``apply_rotary_pos_emb`` (rotate-half form:
+    llama / mistral / qwen2 / qwen3 ...) -> the HIP kernel on GPU tensors,
+    the original elsewhere (model-module global, as the reference's
+    per-arch forward patches)"""
+    import sys
+    mods = {type(m).__module__ for m in model.modules() if type(m).__name__.endswith("Attention")}
+    for name in mods:
+        mod = sys.modules.get(name)
+        f = getattr(mod, "apply_rotary_pos_emb", None)
+        if f is None or getattr(f, "__wrapped__", None) is not None or name in _ROPE_ORIG:
+            continue
+        rh = getattr(mod, "rotate_half", None)
+        if rh is None:
+            continue
+        try:                            # interleaved forms (GLM, ...) keep their own function
+            t = torch.arange(8.0)
+            if not torch.equal(rh(t), torch.cat([-t[4:], t[:4]])):
+                continue
+        except Exception:
+            continue
+        _ROPE_ORIG[name] = f
+        mod.apply_rotary_pos_emb = _make_rope(f)
+
+
 def _patch_norms(model: nn.Module):
     for m in model.modules():
         cls = m.__class__.__name__
@@ -350,6 +412,7 @@ def _optimize_post(model: nn.Module):
     """Swap in the native MI355X decoder for supported architectures."""
     mt = getattr(getattr(model, "config", None), "model_type", None)
     _patch_norms(model)
+    _patch_rope(model)
     _patch_routers(model)
     from .attention import patch_eager_attention
     patch_eager_attention(model)

@@ -132,3 +132,34 @@ def test_rms_norm_backward_kernel(cuda, dtype, H):
     assert y.grad_fn is not None
     y.backward(g)
     assert ((x2.grad.float() - xr.grad).norm() / xr.grad.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,cosb", [(2, 2), (3, 1)])
+def test_rope_half_kernel_matches_hf(cuda, dtype, B, cosb):
+    """patched apply_rotary_pos_emb (HIP rotate-half RoPE, strided q/k views)
+    == HF's, forward bit-for-bit and the gradients through autograd"""
+    from transformers.models.llama import modeling_llama as ML
+    from ipex_llm_amd.transformers.convert import _make_rope
+    torch.manual_seed(5)
+    T, Hq, Hk, D = 19, 4, 2, 64
+    orig = getattr(ML.apply_rotary_pos_emb, "__wrapped__", ML.apply_rotary_pos_emb)
+    fused = _make_rope(orig)
+    qp = torch.randn(B, T, Hq * D, device=cuda).to(dtype)
+    kp = torch.randn(B, T, Hk * D, device=cuda).to(dtype)
+    ang = torch.randn(cosb, T, D // 2, device=cuda)
+    cos = torch.cat([ang.cos(), ang.cos()], -1).to(dtype)
+    sin = torch.cat([ang.sin(), ang.sin()], -1).to(dtype)
+    gq = torch.randn(B, Hq, T, D, device=cuda).to(dtype)
+    gk = torch.randn(B, Hk, T, D, device=cuda).to(dtype)
+    res = []
+    for f in (orig, fused):
+        q0, k0 = qp.clone().requires_grad_(), kp.clone().requires_grad_()
+        q = q0.view(B, T, Hq, D).transpose(1, 2)
+        k = k0.view(B, T, Hk, D).transpose(1, 2)
+        qe, ke = f(q, k, cos, sin)
+        (qe.float() * gq.float()).sum().add((ke.float() * gk.float()).sum()).backward()
+        res.append((qe, ke, q0.grad, k0.grad))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for a, b in zip(res[0][2:], res[1][2:]):
+        assert ((a.float() - b.float()).norm() / b.float().norm()).item() < 1e-2

@@ -99,6 +99,9 @@ def main():
         # optimize_model's norm patch: HIP RMSNorm forward + backward (frozen weight)
         from ipex_llm_amd.transformers.convert import _patch_norms
         _patch_norms(model)
+    if os.environ.get("ILLM_TRAIN_ROPE", "1") == "1":
+        from ipex_llm_amd.transformers.convert import _patch_rope
+        _patch_rope(model)
     if args.grad_ckpt:
         model.gradient_checkpointing_enable()
         model.enable_input_require_grads()
