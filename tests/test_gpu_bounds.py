@@ -97,9 +97,15 @@ _DEBUG_LIB = __import__("os").path.join(__import__("os").path.dirname(ops.__file
 
 
 def _debug_lib_current():
+    """the debug build exists and is newer than every native source"""
+    import glob
     import os
-    rel = os.path.join(os.path.dirname(_DEBUG_LIB), "_C.so")
-    return os.path.exists(_DEBUG_LIB) and os.path.getmtime(_DEBUG_LIB) >= os.path.getmtime(rel) - 3600
+    if not os.path.exists(_DEBUG_LIB):
+        return False
+    csrc = os.path.join(os.path.dirname(_DEBUG_LIB), "csrc")
+    srcs = [f for ext in ("hip", "cpp", "h", "cuh") for f in glob.glob(os.path.join(csrc, "**", "*." + ext),
+                                                                          recursive=True)]
+    return os.path.getmtime(_DEBUG_LIB) >= max(os.path.getmtime(f) for f in srcs)
 
 
 @pytest.mark.skipif(not _debug_lib_current(), reason="debug build absent or older than _C.so "
