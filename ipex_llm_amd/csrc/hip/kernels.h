@@ -241,6 +241,8 @@ void launch_moe_route(bool bf16, const MoeRouteArgs& a, hipStream_t st);
 void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float* w, const int32_t* ids, int k,
                         int e0, int El, uint16_t* out, int Tn, int H, hipStream_t st);
 
+void launch_act_mul(bool bf16, const uint16_t* g, const uint16_t* u, const uint16_t* dy, uint16_t* y, uint16_t* dg,
+                    uint16_t* du, int64_t n, int act, hipStream_t s);
 void launch_rope_half(bool bf16, const uint16_t* x, int64_t sb, int64_t sh, int64_t st, const uint16_t* cs,
                       const uint16_t* sn, int64_t csb, uint16_t* out, int B, int H, int Tn, int D, int bwd,
                       hipStream_t s);

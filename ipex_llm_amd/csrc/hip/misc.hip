@@ -594,6 +594,70 @@ void launch_moe_combine(bool bf16, const float* part, int ks, int P, const float
   else hipLaunchKernelGGL(moe_combine_kernel<F16>, grid, dim3(256), 0, st, part, ks, P, w, ids, k, e0, El, out, Tn, H);
 }
 
+// ---- act(gate) * up for two separate [.., I] tensors (the HF MLP form used in
+// training) and its gradient, with HF's rounding: a = rnd(act(g)), y = rnd(a u);
+// backward du = rnd(dy a), dg = rnd(rnd(dy u) act'(g)).  act: 0 silu, 1 gelu-tanh.
+// 8 elements per thread, 16-B accesses.
+template <typename T>
+__global__ void __launch_bounds__(256) act_mul_kernel(const uint16_t* __restrict__ g, const uint16_t* __restrict__ u,
+                                                      const uint16_t* __restrict__ dy, uint16_t* __restrict__ y,
+                                                      uint16_t* __restrict__ dg, uint16_t* __restrict__ du,
+                                                      int64_t n8, int act) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  auto ld8 = [](const uint16_t* p, int64_t i, float* v) {
+    const uint4 q = ((const uint4*)p)[i];
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int e = 0; e < 4; e++) { v[2 * e] = to_f32<T>(w[e] & 0xffff); v[2 * e + 1] = to_f32<T>(w[e] >> 16); }
+  };
+  auto st8 = [](uint16_t* p, int64_t i, const float* v) {
+    ((uint4*)p)[i] = make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
+  };
+  auto r = [](float v) { return to_f32<T>(from_f32<T>(v)); };
+  float gv[8], uv[8];
+  ld8(g, i, gv);
+  ld8(u, i, uv);
+  if (dy == nullptr) {
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) o[e] = r(act == 0 ? silu_f(gv[e]) : gelu_tanh_f(gv[e])) * uv[e];
+    st8(y, i, o);
+    return;
+  }
+  float d[8], og[8], ou[8];
+  ld8(dy, i, d);
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const float x = gv[e];
+    float a, da;
+    if (act == 0) {
+      const float sg = 1.f / (1.f + __expf(-x));
+      a = x * sg;
+      da = sg * (1.f + x * (1.f - sg));
+    } else {
+      const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+      const float inner = k0 * (x + k1 * x * x * x);
+      const float th = tanhf(inner);
+      a = 0.5f * x * (1.f + th);
+      da = 0.5f * (1.f + th) + 0.5f * x * (1.f - th * th) * k0 * (1.f + 3.f * k1 * x * x);
+    }
+    ou[e] = d[e] * r(a);
+    og[e] = r(d[e] * uv[e]) * da;
+  }
+  st8(dg, i, og);
+  st8(du, i, ou);
+}
+
+void launch_act_mul(bool bf16, const uint16_t* g, const uint16_t* u, const uint16_t* dy, uint16_t* y, uint16_t* dg,
+                    uint16_t* du, int64_t n, int act, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  if (n8 == 0) return;
+  const dim3 grid((unsigned)((n8 + 255) / 256));
+  if (bf16) hipLaunchKernelGGL(act_mul_kernel<BF16>, grid, dim3(256), 0, s, g, u, dy, y, dg, du, n8, act);
+  else hipLaunchKernelGGL(act_mul_kernel<F16>, grid, dim3(256), 0, s, g, u, dy, y, dg, du, n8, act);
+}
+
 // ---- rotate-half RoPE on [B, H, T, D] activations (training / HF-forward path)
 // out = x cos + rotate_half(x) sin with HF's bf16 rounding (each product, then
 // the sum), x with any batch / head / token strides (the transposed q / k

@@ -132,6 +132,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("add_rms_norm(Tensor? x, Tensor(b!)? partials, Tensor(a!)? residual, Tensor w, float eps, bool unit_offset, bool store_residual, bool zero_partials=False) -> Tensor");
   m.def("rms_norm_bwd(Tensor x, Tensor g, Tensor w, float eps, bool unit_offset) -> Tensor");
   m.def("rope_half(Tensor x, Tensor cos, Tensor sin, bool bwd) -> Tensor");
+  m.def("act_mul(Tensor g, Tensor u, Tensor? dy, int act) -> Tensor[]");
   m.def("layer_norm(Tensor x, Tensor? w, Tensor? b, float eps) -> Tensor");
   m.def("kernel_errors(Tensor like, bool reset) -> Tensor");
   m.def("rope_kv(Tensor qkv, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slots, Tensor pos, Tensor inv_freq, Tensor? q_norm, Tensor? k_norm, float norm_eps, float q_scale, int Hq, int Hkv, int D, int rot_dim, bool interleaved, int kv_fp8, float k_scale, float v_scale) -> ()");

@@ -668,6 +668,26 @@ Tensor add_rms_norm(const c10::optional<Tensor>& x, const c10::optional<Tensor>&
   return out;
 }
 
+// act(gate) * up (dy undefined) or its gradient (dgate, dup) for contiguous same-shape tensors
+std::vector<Tensor> act_mul(const Tensor& g, const Tensor& u, const c10::optional<Tensor>& dy, int64_t act) {
+  c10::DeviceGuard dg_(g.device());
+  TORCH_CHECK(g.is_contiguous() && u.is_contiguous() && g.sizes() == u.sizes() && g.scalar_type() == u.scalar_type() &&
+                  (g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kHalf) && g.numel() % 8 == 0,
+              "act_mul: contiguous bf16/f16 gate and up of one shape, numel % 8 == 0");
+  const bool bf16 = is_bf16(g);
+  if (!(dy.has_value() && dy->defined())) {
+    Tensor y = at::empty_like(g);
+    illm::launch_act_mul(bf16, p16(g), p16(u), nullptr, m16(y), nullptr, nullptr, g.numel(), (int)act, cur_stream());
+    return {y};
+  }
+  TORCH_CHECK(dy->is_contiguous() && dy->sizes() == g.sizes() && dy->scalar_type() == g.scalar_type(),
+              "act_mul: dy like gate");
+  Tensor dgt = at::empty_like(g), dut = at::empty_like(u);
+  illm::launch_act_mul(bf16, p16(g), p16(u), p16(*dy), nullptr, m16(dgt), m16(dut), g.numel(), (int)act,
+                       cur_stream());
+  return {dgt, dut};
+}
+
 // rotate-half RoPE of a [B, H, T, D] view (D contiguous) -> contiguous [B, H, T, D]
 Tensor rope_half(const Tensor& x, const Tensor& cos, const Tensor& sin, bool bwd) {
   c10::DeviceGuard dg(x.device());
@@ -1467,6 +1487,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("add_rms_norm", &add_rms_norm);
   m.impl("rms_norm_bwd", &rms_norm_bwd);
   m.impl("rope_half", &rope_half);
+  m.impl("act_mul", &act_mul);
   m.impl("layer_norm", &layer_norm);
   m.impl("kernel_errors", &kernel_errors);
   m.impl("rope_kv", &rope_kv);

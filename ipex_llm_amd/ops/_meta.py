@@ -47,6 +47,13 @@ def _(x, cos, sin, bwd):
     return x.new_empty(x.shape)
 
 
+@register_fake("ipex_llm_amd::act_mul")
+def _(g, u, dy, act):
+    if dy is None:
+        return [torch.empty_like(g)]
+    return [torch.empty_like(g), torch.empty_like(u)]
+
+
 @register_fake("ipex_llm_amd::layer_norm")
 def _(x, w, b, eps):
     return torch.empty_like(x)

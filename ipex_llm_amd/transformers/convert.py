@@ -401,6 +401,58 @@ def _patch_rope(model: nn.Module):
         mod.apply_rotary_pos_emb = _make_rope(f)
 
 
+class _ActMulFn(torch.autograd.Function):
+    """act(gate) * up of the HF MLP as one HIP kernel each way (HF rounding)"""
+
+    @staticmethod
+    def forward(ctx, g, u, act):
+        ctx.save_for_backward(g, u)
+        ctx.act = act
+        return torch.ops.ipex_llm_amd.act_mul(g, u, None, act)[0]
+
+    @staticmethod
+    def backward(ctx, dy):
+        g, u = ctx.saved_tensors
+        dg, du = torch.ops.ipex_llm_amd.act_mul(g, u, dy.contiguous(), ctx.act)
+        return dg, du, None
+
+
+def _mlp_act_code(act_fn):
+    name = type(act_fn).__name__
+    if isinstance(act_fn, nn.SiLU) or name == "SiLUActivation":
+        return 0
+    if name in ("GELUTanh", "PytorchGELUTanh", "NewGELUActivation", "GELUPytorchTanh"):
+        return 1
+    return None
+
+
+def _mlp_forward(self, x):
+    from .. import ops
+    g = self.gate_proj(x)
+    u = self.up_proj(x)
+    if (g.is_cuda and ops.native_gpu(g) and g.dtype in (torch.bfloat16, torch.float16) and g.dtype == u.dtype
+            and g.shape == u.shape and g.numel() % 8 == 0):
+        h = _ActMulFn.apply(g.contiguous(), u.contiguous(), self._illm_act)
+    else:
+        h = self.act_fn(g) * u
+    return self.down_proj(h)
+
+
+def _patch_mlp(model: nn.Module):
+    """gated MLPs (gate_proj / up_proj / down_proj, silu or gelu-tanh) of
+    the HF forward -> the fused act * up kernel and its gradient"""
+    for m in model.modules():
+        if not type(m).__name__.endswith("MLP") or getattr(m, "_illm_act", None) is not None:
+            continue
+        if not all(hasattr(m, a) for a in ("gate_proj", "up_proj", "down_proj", "act_fn")):
+            continue
+        code = _mlp_act_code(m.act_fn)
+        if code is None:
+            continue
+        m._illm_act = code
+        m.forward = types.MethodType(_mlp_forward, m)
+
+
 def _patch_norms(model: nn.Module):
     for m in model.modules():
         cls = m.__class__.__name__
@@ -413,6 +465,7 @@ def _optimize_post(model: nn.Module):
     mt = getattr(getattr(model, "config", None), "model_type", None)
     _patch_norms(model)
     _patch_rope(model)
+    _patch_mlp(model)
     _patch_routers(model)
     from .attention import patch_eager_attention
     patch_eager_attention(model)

@@ -163,3 +163,35 @@ def test_rope_half_kernel_matches_hf(cuda, dtype, B, cosb):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     for a, b in zip(res[0][2:], res[1][2:]):
         assert ((a.float() - b.float()).norm() / b.float().norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu_pytorch_tanh"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_act_mul_kernel_matches_hf_mlp(cuda, act, dtype):
+    """patched gated-MLP forward (HIP act * up and its gradient) == the HF
+    expression act_fn(gate) * up: forward bit-for-bit for silu, gradients close"""
+    import types
+    from transformers.activations import ACT2FN
+    from ipex_llm_amd.transformers.convert import _mlp_act_code, _mlp_forward
+    torch.manual_seed(6)
+    H, I = 128, 352
+    lin = lambda i, o: torch.nn.Linear(i, o, bias=False, device=cuda, dtype=dtype)  # noqa: E731
+    m = types.SimpleNamespace(gate_proj=lin(H, I), up_proj=lin(H, I), down_proj=lin(I, H), act_fn=ACT2FN[act])
+    m._illm_act = _mlp_act_code(m.act_fn)
+    assert m._illm_act is not None
+    x0 = torch.randn(3, 17, H, device=cuda).to(dtype)
+    gy = torch.randn(3, 17, H, device=cuda).to(dtype)
+    res = []
+    for fused in (False, True):
+        x = x0.clone().requires_grad_()
+        for p in (m.gate_proj.weight, m.up_proj.weight):
+            p.grad = None
+        y = _mlp_forward(m, x) if fused else m.down_proj(m.act_fn(m.gate_proj(x)) * m.up_proj(x))
+        y.backward(gy)
+        res.append((y, x.grad, m.gate_proj.weight.grad, m.up_proj.weight.grad))
+    if act == "silu":
+        assert torch.equal(res[0][0], res[1][0])
+    else:                     # tanh evaluated differently: last-ulp differences in f16
+        assert ((res[0][0].float() - res[1][0].float()).norm() / res[1][0].float().norm()).item() < 2e-3
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert ((a.float() - b.float()).norm() / b.float().norm()).item() < 1e-2

@@ -102,6 +102,9 @@ def main():
     if os.environ.get("ILLM_TRAIN_ROPE", "1") == "1":
         from ipex_llm_amd.transformers.convert import _patch_rope
         _patch_rope(model)
+    if os.environ.get("ILLM_TRAIN_MLP", "1") == "1":
+        from ipex_llm_amd.transformers.convert import _patch_mlp
+        _patch_mlp(model)
     if args.grad_ckpt:
         model.gradient_checkpointing_enable()
         model.enable_input_require_grads()
