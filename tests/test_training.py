@@ -246,3 +246,21 @@ def test_fused_lora_node_matches_module_graph(monkeypatch, bias):
     for a, b in zip(res[True], res[False]):
         assert a.shape == b.shape
         assert ((a - b).norm() / b.norm()).item() < 2e-2
+
+
+def test_reference_qlora_class_names():
+    """ipex_llm.transformers.qlora names: LoraLowBitLinear over a low-bit
+    base, LoraBF16Linear over a dense bf16 base, each refusing the other"""
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    from ipex_llm_amd.transformers.qlora import LoraBF16Linear, LoraLowBitLinear
+    lin = torch.nn.Linear(128, 64, bias=False)
+    low = LowBitLinear.from_linear(lin, "nf4")
+    a = LoraLowBitLinear(low, r=4, lora_alpha=8)
+    b = LoraBF16Linear(torch.nn.Linear(128, 64, bias=False), r=4, lora_alpha=8)
+    x = torch.randn(3, 128).to(torch.bfloat16)
+    assert a(x).shape == (3, 64) and b(x).shape == (3, 64)
+    assert b.base_layer.weight.dtype == torch.bfloat16
+    with pytest.raises(TypeError):
+        LoraLowBitLinear(lin)
+    with pytest.raises(TypeError):
+        LoraBF16Linear(low)
