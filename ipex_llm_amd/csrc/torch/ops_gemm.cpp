@@ -1,0 +1,161 @@
+// torch.library ops of the MFMA GEMM engine (csrc/hip/gemm_mfma.hip):
+// prefill / training GEMMs over low-bit tiled blobs or dense 16-bit weights.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+#include "../common/formats.h"
+#include "../hip/kernels.h"
+
+using at::Tensor;
+
+namespace {
+
+inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+// geometry: 256 x 256 blocks while they fill the 256 CUs, else 256 x 128,
+// then split-K over even step counts until ~1 wave of blocks
+struct MfgPlan {
+  int tile, ksplit, sps;
+};
+MfgPlan mfg_plan(int64_t M, int64_t N, int64_t K, int64_t tile_req, int64_t ks_req, bool glu) {
+  static const int tile_env = getenv("ILLM_MFG_TILE") ? atoi(getenv("ILLM_MFG_TILE")) : -1;
+  static const int ks_env = getenv("ILLM_MFG_KSPLIT") ? atoi(getenv("ILLM_MFG_KSPLIT")) : 0;
+  const int T = (int)(K / 64);
+  MfgPlan p{illm::MFG_TILE_256x256, 1, T};
+  auto blocks = [&](int tile) {
+    return ((N + illm::mfg_block_n(tile) - 1) / illm::mfg_block_n(tile)) *
+           ((M + illm::mfg_block_m(tile) - 1) / illm::mfg_block_m(tile));
+  };
+  if (tile_req >= 0) p.tile = (int)tile_req;
+  else if (tile_env >= 0) p.tile = tile_env;
+  else if (blocks(illm::MFG_TILE_256x256) < 256) p.tile = illm::MFG_TILE_256x128;
+  int ks = (int)(ks_req > 0 ? ks_req : ks_env);
+  if (ks <= 0) {
+    ks = 1;
+    if (!glu)
+      while (blocks(p.tile) * ks * 2 <= 320 && T / (ks * 2) >= 8) ks *= 2;
+  }
+  if (glu) ks = 1;
+  p.sps = ((T + ks - 1) / ks + 1) / 2 * 2;
+  p.ksplit = (T + p.sps - 1) / p.sps;
+  return p;
+}
+
+// out[..., N] = x[..., K] . W^T (+ bias).  fmt >= 0: w = tiled low-bit blob
+// (bf16 activations normalised per row to f16 for the f16 MFMA); fmt < 0: w =
+// dense [N, K] bf16 / f16 (x converted to w's dtype if needed).  glu: the
+// tile-interleaved gate/up weight, out = act(gate) * up [..., N / 2].
+Tensor mfgemm(const Tensor& x, const Tensor& w, int64_t fmt, int64_t n, int64_t k, const c10::optional<Tensor>& bias,
+              bool glu, int64_t act, int64_t tile, int64_t ksplit) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda(), "mfgemm: GPU tensors expected");
+  TORCH_CHECK(x.size(-1) == k, "mfgemm: x last dim ", x.size(-1), " != in_features ", k);
+  TORCH_CHECK(k % 128 == 0, "mfgemm: in_features must be a multiple of 128");
+  TORCH_CHECK(n % 16 == 0 && (!glu || n % 32 == 0), "mfgemm: out_features must be a multiple of 16 (32 for glu)");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "mfgemm: bf16/fp16 activations");
+  c10::DeviceGuard g(x.device());
+  const bool out_bf16 = x.scalar_type() == at::kBFloat16;
+  Tensor xc = x.contiguous();
+  const int64_t M = xc.numel() / k;
+  auto shape = xc.sizes().vec();
+  shape.back() = glu ? n / 2 : n;
+  Tensor out = at::empty(shape, xc.options());
+  if (M == 0) return out;
+  const bool dense = fmt < 0;
+  illm::MfgArgs a{};
+  Tensor xm, rs;
+  bool dense_bf16 = false;
+  if (dense) {
+    TORCH_CHECK(w.dim() == 2 && w.size(0) == n && w.size(1) == k && w.is_contiguous(), "mfgemm: dense w [n, k]");
+    TORCH_CHECK(w.scalar_type() == at::kBFloat16 || w.scalar_type() == at::kHalf, "mfgemm: dense w bf16/fp16");
+    dense_bf16 = w.scalar_type() == at::kBFloat16;
+    xm = xc.scalar_type() == w.scalar_type() ? xc : xc.to(w.scalar_type());
+    TORCH_CHECK((n + 256) * k * 2 < (int64_t)UINT32_MAX, "mfgemm: dense weight too large for one buffer descriptor");
+    a.w_bytes = (uint32_t)(n * k * 2);
+    a.ldw = (int)k;
+  } else {
+    TORCH_CHECK(w.scalar_type() == at::kByte, "mfgemm: low-bit blob must be uint8");
+    TORCH_CHECK(w.numel() >= illm::dev_total_bytes((int)fmt, n, k), "mfgemm: weight blob too small");
+    if (out_bf16) {
+      xm = at::empty({M, k}, xc.options().dtype(at::kHalf));
+      rs = at::empty({M}, xc.options().dtype(at::kFloat));
+      illm::launch_x_to_f16_rowscale(true, (const uint16_t*)xc.data_ptr(), M, k, (int)k, (uint16_t*)xm.data_ptr(),
+                                     rs.data_ptr<float>(), cur_stream());
+      a.rs = rs.data_ptr<float>();
+    } else {
+      xm = xc;
+    }
+  }
+  TORCH_CHECK((M + 256) * k * 2 < (int64_t)UINT32_MAX, "mfgemm: activations too large for one buffer descriptor");
+  a.x = (const uint16_t*)xm.data_ptr();
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.x_bytes = (uint32_t)(M * k * 2);
+  a.w = (const uint8_t*)w.data_ptr();
+  a.N = (int)n;
+  a.KC = (int)(illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K);
+  a.glu = glu ? 1 : 0;
+  a.act = (int)act;
+  a.lut_fmt = (int)fmt;
+  a.out_bf16 = out_bf16 ? 1 : 0;
+  const Tensor* bp = (bias.has_value() && bias->defined()) ? &*bias : nullptr;
+  Tensor bconv;
+  if (bp != nullptr) {
+    TORCH_CHECK(!glu, "mfgemm: bias with glu is not supported");
+    TORCH_CHECK(bp->numel() == n, "mfgemm: bias size");
+    bconv = bp->contiguous();
+    if (bconv.scalar_type() != at::kBFloat16 && bconv.scalar_type() != at::kHalf) bconv = bconv.to(xc.scalar_type());
+  }
+  const MfgPlan p = mfg_plan(M, n, k, tile, ksplit, glu);
+  a.sps = p.sps;
+  if (p.ksplit > 1) {
+    Tensor ws = at::empty({p.ksplit, M, n}, xc.options().dtype(at::kFloat));
+    a.out = ws.data_ptr();
+    a.out_f32 = 1;
+    a.ldo = (int)n;
+    a.slab = M * n;
+    illm::launch_mfgemm((int)fmt, dense_bf16, p.tile, a, p.ksplit, cur_stream());
+    Tensor b16;
+    if (bp != nullptr) b16 = bconv.scalar_type() == xc.scalar_type() ? bconv : bconv.to(xc.scalar_type());
+    illm::launch_reduce_partials(out_bf16, ws.data_ptr<float>(), p.ksplit,
+                                 bp != nullptr ? (const uint16_t*)b16.data_ptr() : nullptr, (uint16_t*)out.data_ptr(),
+                                 (int)M, (int)n, (int)n, cur_stream());
+    return out;
+  }
+  a.out = out.data_ptr();
+  a.ldo = (int)(glu ? n / 2 : n);
+  if (bp != nullptr) {
+    a.bias = (const uint16_t*)bconv.data_ptr();
+    a.bias_bf16 = bconv.scalar_type() == at::kBFloat16 ? 1 : 0;
+  }
+  illm::launch_mfgemm((int)fmt, dense_bf16, p.tile, a, 1, cur_stream());
+  return out;
+}
+
+// (x16, rs) = per-row power-of-two normalisation of x to f16 (exposed for tests)
+std::vector<Tensor> x_to_f16_rowscale(const Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.size(1) % 8 == 0, "x_to_f16_rowscale: 2-D GPU x, K % 8 == 0");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "x_to_f16_rowscale: bf16/fp16");
+  c10::DeviceGuard g(x.device());
+  Tensor xc = x.contiguous();
+  Tensor y = at::empty(xc.sizes(), xc.options().dtype(at::kHalf));
+  Tensor rs = at::empty({xc.size(0)}, xc.options().dtype(at::kFloat));
+  illm::launch_x_to_f16_rowscale(xc.scalar_type() == at::kBFloat16, (const uint16_t*)xc.data_ptr(), xc.size(0),
+                                 xc.size(1), (int)xc.size(1), (uint16_t*)y.data_ptr(), rs.data_ptr<float>(),
+                                 cur_stream());
+  return {y, rs};
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
+  m.def("mfgemm(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias=None, bool glu=False, int act=0, int tile=-1, int ksplit=0) -> Tensor");
+  m.def("x_to_f16_rowscale(Tensor x) -> Tensor[]");
+}
+
+TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
+  m.impl("mfgemm", &mfgemm);
+  m.impl("x_to_f16_rowscale", &x_to_f16_rowscale);
+}

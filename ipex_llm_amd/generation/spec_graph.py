@@ -103,7 +103,12 @@ class GraphSpeculator:
         self.last.copy_(pred.gather(0, m.view(1)))
 
     @torch.no_grad()
-    def generate(self, prompt: Sequence[int], max_new_tokens: int, eos=(), timing=None, streamer=None) -> List[int]:
+    def generate(self, prompt: Sequence[int], max_new_tokens: int, eos=(), timing=None, streamer=None,
+                 min_new_tokens: int = 0) -> List[int]:
+        """Greedy speculative generation of one prompt.  Stops like the eager
+        path (generation/speculative.py): at ``max_new_tokens``, or at an EOS
+        once ``min_new_tokens`` tokens exist; only the tokens kept are
+        streamed.  The caller ends the streamer."""
         te, de = self.te, self.de
         te._ensure_cache(1, self.max_len)
         de._ensure_cache(1, self.max_len)
@@ -136,12 +141,13 @@ class GraphSpeculator:
         sync()
         if timing is not None:
             timing.first_cost = time.perf_counter() - t0
-        if streamer is not None:
-            streamer.put(first.view(1).cpu())
         eos = set(eos or ())
         got, emitted = 1, [int(first)]
+        done = max_new_tokens <= 1 or (emitted[-1] in eos and 1 >= min_new_tokens)
+        if streamer is not None:
+            streamer.put(first.view(1).cpu())
         self.rounds = self.drafted = 0
-        while got < max_new_tokens and not (emitted[-1] in eos):
+        while not done:
             t1 = time.perf_counter()
             k = self.k
             g = self.graphs.get(k)
@@ -173,26 +179,22 @@ class GraphSpeculator:
                     self.k = k + 1
                 elif m < k // 2 and k > 1:
                     self.k = k - 1
-            emitted.extend(new)
+            got = n
+            kept = []
+            for t in new:                       # the eager path's stop rule, token by token
+                kept.append(t)
+                if len(emitted) + len(kept) >= max_new_tokens or (t in eos and len(emitted) + len(kept) >= min_new_tokens):
+                    done = True
+                    break
+            emitted.extend(kept)
             if timing is not None:
                 dt = time.perf_counter() - t1
-                timing.rest_costs.extend([dt / max(1, len(new))] * len(new))
-            if streamer is not None and new:
-                streamer.put(torch.tensor(new))
-            got = n
-            if any(t in eos for t in new):
-                break
-        # truncate at max_new_tokens / the first EOS
-        out = []
-        for t in emitted:
-            out.append(t)
-            if len(out) >= max_new_tokens or t in eos:
-                break
+                timing.rest_costs.extend([dt / max(1, len(kept))] * len(kept))
+            if streamer is not None and kept:
+                streamer.put(torch.tensor(kept))
         te.cache.allocator.release(st.blocks)
         de.cache.allocator.release(sd.blocks)
-        if streamer is not None:
-            streamer.end()
-        return p + out
+        return p + emitted
 
     @property
     def acceptance(self) -> float:

@@ -76,9 +76,12 @@ def speculative_generate(model, prompts: Sequence[Sequence[int]], max_new_tokens
                 sp = GraphSpeculator(tgt, dft, min(4, kmax), max(max_len, 1024), k_max=kmax,
                                      adaptive=auto_th_stop_draft)
                 model.__dict__["_illm_spec_graph"] = sp
-            outs.append(sp.generate(p, max_new_tokens, eos, timing=timing, streamer=streamer))
+            outs.append(sp.generate(p, max_new_tokens, eos, timing=timing, streamer=streamer,
+                                    min_new_tokens=min_new_tokens))
             model.n_drafted += sp.drafted
             model.n_matched += int(sp.n_match)
+        if streamer is not None:
+            streamer.end()                      # once per batch, as the eager path
         return outs
     sync = torch.cuda.synchronize if tgt.model.device.type == "cuda" else (lambda: None)
     thr = _AutoThreshold(th_stop_draft)

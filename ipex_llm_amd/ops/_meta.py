@@ -237,3 +237,15 @@ def _(x, w, bias):
 @register_fake("ipex_llm_amd::kernel_errors")
 def _(like, reset):
     return like.new_empty(4, dtype=torch.int32)
+
+
+@register_fake("ipex_llm_amd::mfgemm")
+def _(x, w, fmt, n, k, bias=None, glu=False, act=0, tile=-1, ksplit=0):
+    shape = list(x.shape)
+    shape[-1] = n // 2 if glu else n
+    return x.new_empty(shape)
+
+
+@register_fake("ipex_llm_amd::x_to_f16_rowscale")
+def _(x):
+    return [x.new_empty(x.shape, dtype=torch.float16), x.new_empty((x.shape[0],), dtype=torch.float32)]

@@ -67,6 +67,14 @@ class GradBucketSync:
             loss.backward()                   # buckets reduce as their grads complete
             sync.finish()                     # wait for the last buckets
             opt.step(); sync.zero_grad()
+
+    Gradient accumulation (the reference recipe's
+    ``gradient_accumulation_steps``): run every micro-batch but the last
+    under ``with sync.no_sync():`` -- its gradients accumulate locally in the
+    flat buffer and no collective is issued; the last backward reduces the
+    accumulated sum.  A second backward outside ``no_sync`` before
+    ``finish()`` would add into buffers whose all-reduce is in flight, so it
+    raises instead.
     """
 
     def __init__(self, model: nn.Module, group=None, bucket_cap_mb: float = 32.0, average: bool = True):
@@ -99,6 +107,30 @@ class GradBucketSync:
             if cur:
                 self._add_bucket(flat[start:off], cur)
         self._hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in self.params]
+        self._sync = True
+
+    class _NoSync:
+        def __init__(self, owner):
+            self.owner = owner
+
+        def __enter__(self):
+            self.owner._check_idle("no_sync()")
+            self.owner._sync = False
+            return self.owner
+
+        def __exit__(self, *exc):
+            self.owner._sync = True
+            return False
+
+    def no_sync(self):
+        """Context for accumulation micro-batches: gradients accumulate in the
+        flat buffer, no bucket is reduced (the next synced backward reduces
+        the sum)."""
+        return GradBucketSync._NoSync(self)
+
+    def _check_idle(self, what):
+        if any(b.work is not None or b.pending != len(b.params) for b in self.buckets):
+            raise RuntimeError(f"GradBucketSync: {what} while a synced backward is in flight; call finish() first")
 
     def _add_bucket(self, flat, params):
         b = _Bucket(flat, params)
@@ -108,8 +140,11 @@ class GradBucketSync:
 
     def _ready(self, p: nn.Parameter):
         b = self._of.get(id(p))
-        if b is None:
+        if b is None or not self._sync:
             return
+        if b.pending <= 0 or b.work is not None:
+            raise RuntimeError("GradBucketSync: a second backward reached a bucket whose all-reduce is already "
+                               "issued; wrap accumulation micro-batches in no_sync() and call finish() per step")
         if p.grad is not None and p.grad.data_ptr() != b.flat.data_ptr() and not self._is_view(p, b):
             # autograd replaced the gradient tensor (e.g. set_to_none zero_grad): copy it back in
             self._rebind(p, b)

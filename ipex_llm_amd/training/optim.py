@@ -12,7 +12,10 @@ math with torch ``_foreach`` ops.  Semantics = ``torch.optim.AdamW``
 device tensor and the pointer/chunk tables cached, so ``step()`` issues no
 host-to-device copy and can be captured in a hipGraph together with the
 forward and backward (tools/bench_qlora.py --graph).  After changing
-``group["lr"]`` call :meth:`sync_lr` (outside capture).
+``group["lr"]`` call :meth:`sync_lr` (outside capture).  The device step is
+mirrored into ``state[p]["step"]`` by :meth:`state_dict` and re-seeded from
+it after :meth:`load_state_dict` (checkpoint / resume keeps the bias
+correction), and switching between capturable and eager steps carries it.
 """
 from __future__ import annotations
 
@@ -42,12 +45,31 @@ class FusedAdamW(torch.optim.Optimizer):
             if sl is not None:
                 sl[1].fill_(float(group["lr"]))
 
-    def _dev_step_lr(self, gi, group, dev):
+    def _dev_step_lr(self, gi, group, dev, host_step: int = 0):
         sl = self._step_lr.get(gi)
         if sl is None or sl.device != dev:
-            sl = torch.tensor([0.0, float(group["lr"])], dtype=torch.float32, device=dev)
+            sl = torch.tensor([float(host_step), float(group["lr"])], dtype=torch.float32, device=dev)
             self._step_lr[gi] = sl
         return sl
+
+    def _sync_host_steps(self):
+        """copy every device step count into the per-parameter state (one
+        host read per group; outside capture)"""
+        for gi, sl in self._step_lr.items():
+            step = int(round(float(sl[0].item())))
+            for p in self.param_groups[gi]["params"]:
+                st = self.state.get(p)
+                if st:
+                    st["step"] = step
+
+    def state_dict(self):
+        self._sync_host_steps()
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._step_lr.clear()                  # re-seeded from state["step"] by the next capturable step
+        self._tables.clear()
 
     def _state(self, p):
         st = self.state[p]
@@ -60,6 +82,9 @@ class FusedAdamW(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        if self._step_lr and not self.capturable:
+            self._sync_host_steps()            # switched from capturable steps: continue the count
+            self._step_lr.clear()
         for gi, group in enumerate(self.param_groups):
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
@@ -67,7 +92,7 @@ class FusedAdamW(torch.optim.Optimizer):
             b1, b2 = group["betas"]
             sts = [self._state(p) for p in ps]
             if self.capturable and all(p.is_cuda for p in ps) and ops.native_gpu(ps[0]):
-                sl = self._dev_step_lr(gi, group, ps[0].device)
+                sl = self._dev_step_lr(gi, group, ps[0].device, host_step=int(sts[0]["step"]))
                 sl[0:1].add_(1.0)               # device-side step count (captured with the update)
                 self._fused(group, ps, sts, 0.0, 0.0, step_lr=sl)
                 continue

@@ -140,16 +140,19 @@ def _fp4params_stub():
 
 
 def load_reference_state_dict(path: str) -> Dict[str, torch.Tensor]:
+    # the reference's save_low_bit always writes pytorch_model*.bin
+    # (safe_serialization=False, SRC/transformers/model.py:59-103); a
+    # safetensors-only directory carrying bigdl_transformers_low_bit is one of
+    # OUR checkpoints that lost illm_low_bit.json (canonical planar blobs with
+    # sym_int4 sizes identical to ggml blocks): refuse it instead of
+    # converting planar bytes as ggml blocks
     files = sorted(glob.glob(os.path.join(path, "pytorch_model*.bin")))
     if not files:
-        st = sorted(glob.glob(os.path.join(path, "*.safetensors")))
-        if st:
-            from safetensors.torch import load_file
-            out = {}
-            for f in st:
-                out.update(load_file(f))
-            return out
-        raise FileNotFoundError(f"no pytorch_model*.bin / *.safetensors under {path}")
+        if glob.glob(os.path.join(path, "*.safetensors")):
+            raise ValueError(f"{path}: safetensors shards without illm_low_bit.json -- not a reference "
+                             "save_low_bit checkpoint (those are pytorch_model*.bin); restore illm_low_bit.json "
+                             "or re-save with save_low_bit")
+        raise FileNotFoundError(f"no pytorch_model*.bin under {path}")
     stub = _fp4params_stub()
     out = {}
     for f in files:

@@ -149,3 +149,24 @@ def test_unknown_layout_refused(tmp_path):
     os.remove(tmp_path / "illm_low_bit.json")
     with pytest.raises(ValueError, match="not a low-bit checkpoint"):
         AutoModelForCausalLM.load_low_bit(str(tmp_path))
+
+
+def test_own_safetensors_without_marker_refused(tmp_path):
+    """one of our save_low_bit directories that lost illm_low_bit.json (but
+    kept bigdl_transformers_low_bit in config.json) must not be read as a
+    reference (ggml-block) checkpoint: the reference writes .bin only"""
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    from ipex_llm_amd.transformers.ref_checkpoint import load_reference_state_dict
+    from transformers import LlamaConfig
+    torch.manual_seed(0)
+    cfg = LlamaConfig(vocab_size=64, hidden_size=64, intermediate_size=128, num_hidden_layers=1,
+                      num_attention_heads=2, num_key_value_heads=2)
+    from transformers import LlamaForCausalLM
+    base = tmp_path / "base"
+    LlamaForCausalLM(cfg).save_pretrained(base)
+    m = AutoModelForCausalLM.from_pretrained(str(base), load_in_low_bit="sym_int4")
+    out = tmp_path / "ours"
+    m.save_low_bit(str(out))
+    os.remove(out / "illm_low_bit.json")
+    with pytest.raises(ValueError, match="not a reference"):
+        load_reference_state_dict(str(out))

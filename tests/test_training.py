@@ -197,6 +197,32 @@ def _bucket_worker(rank, world, port):
         ropt.step()
         sync.zero_grad()
         ropt.zero_grad()
+    # gradient accumulation: 2 micro-batches per step, the first under no_sync()
+    for it in range(2):
+        x = xs[it]
+        with sync.no_sync():
+            model(x[rank, :2]).pow(2).mean().div(2).backward()
+        model(x[rank, 2:]).pow(2).mean().div(2).backward()
+        sync.finish()
+        sum(ref(x[r, :2]).pow(2).mean().div(2) + ref(x[r, 2:]).pow(2).mean().div(2)
+            for r in range(world)).div(world).backward()
+        for p, q in zip(model.parameters(), ref.parameters()):
+            if p.requires_grad:
+                assert torch.allclose(p.grad, q.grad, atol=1e-6), ("accum", it)
+        opt.step()
+        ropt.step()
+        sync.zero_grad()
+        ropt.zero_grad()
+    # a second synced backward before finish() must raise, not race
+    model(xs[0][rank]).pow(2).mean().backward()
+    try:
+        model(xs[0][rank]).pow(2).mean().backward()
+        raised = False
+    except RuntimeError:
+        raised = True
+    assert raised
+    sync.finish()
+    sync.zero_grad()
     v = torch.cat([p.detach().flatten() for p in model.parameters() if p.requires_grad])
     vs = [torch.empty_like(v) for _ in range(world)]
     dist.all_gather(vs, v)
@@ -264,3 +290,26 @@ def test_reference_qlora_class_names():
         LoraLowBitLinear(lin)
     with pytest.raises(TypeError):
         LoraBF16Linear(low)
+
+
+def test_fused_adamw_state_dict_round_trip_keeps_step():
+    """state_dict() carries the step count (bias correction) and a resumed
+    optimizer continues exactly where the original one was"""
+    from ipex_llm_amd.training import FusedAdamW
+    torch.manual_seed(0)
+    p = torch.nn.Parameter(torch.randn(64))
+    opt = FusedAdamW([p], lr=1e-2)
+    for _ in range(3):
+        p.grad = torch.randn(64)
+        opt.step()
+    sd = opt.state_dict()
+    assert sd["state"][0]["step"] == 3
+    q = torch.nn.Parameter(p.detach().clone())
+    opt2 = FusedAdamW([q], lr=1e-2)
+    import copy
+    opt2.load_state_dict(copy.deepcopy(sd))     # as from disk (torch keeps the moment tensors otherwise)
+    g = torch.randn(64)
+    p.grad, q.grad = g.clone(), g.clone()
+    opt.step()
+    opt2.step()
+    assert torch.allclose(p, q) and opt2.state[q]["step"] == 4
