@@ -70,10 +70,12 @@ __global__ void __launch_bounds__(512, 1) mfg_nt_kernel(const MfgArgs a) {
   constexpr int WI = BN / 64;              // same, dense weights
   constexpr int XS = BM * 64, WS = BN * 64;
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (XS + WS) + (DK == DK_LUT4 ? 512 : 0)];
-  uint16_t* const X0 = smem;
-  uint16_t* const X1 = smem + XS;
-  uint16_t* const W0 = smem + 2 * XS;
-  uint16_t* const W1 = smem + 2 * XS + WS;
+  // weight stages first: their many per-tile read bases stay below 64 KiB
+  // (ds_read immediates), the two x read bases carry the offset
+  uint16_t* const W0 = smem;
+  uint16_t* const W1 = smem + WS;
+  uint16_t* const X0 = smem + 2 * WS;
+  uint16_t* const X1 = smem + 2 * WS + XS;
   uint32_t* const lut2 = (uint32_t*)(smem + 2 * (XS + WS));
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -274,6 +276,33 @@ __global__ void __launch_bounds__(512, 1) mfg_nt_kernel(const MfgArgs a) {
     }
     return;
   }
+  if (a.lora_x != nullptr) {
+    // LoRA: acc = acc * rs + x_a . B^T as extra bf16 MFMA k-steps over the
+    // (padded) rank -- fragments straight from the small L2-resident operands
+#pragma unroll
+    for (int t = 0; t < WN; t++)
+#pragma unroll
+      for (int mt = 0; mt < WM; mt++) {
+        acc[t][mt] *= rsv[mt];
+      }
+#pragma unroll
+    for (int mt = 0; mt < WM; mt++) rsv[mt] = 1.f;
+    for (int s = 0; s < a.lora_rp / 32; s++) {
+      uint4 Al[WN];
+#pragma unroll
+      for (int t = 0; t < WN; t++) {
+        const int n = min((gt0 + t) * 16 + r16, a.N - 1);
+        Al[t] = *(const uint4*)(a.lora_w + (size_t)n * a.lora_rp + 32 * s + 8 * g);
+      }
+#pragma unroll
+      for (int mt = 0; mt < WM; mt++) {
+        const int m = min(m0 + (wm * WM + mt) * 16 + r16, a.M - 1);
+        const uint4 Bl = *(const uint4*)(a.lora_x + (size_t)m * a.lora_rp + 32 * s + 8 * g);
+#pragma unroll
+        for (int t = 0; t < WN; t++) acc[t][mt] = mfma16<BF16>(Al[t], Bl, acc[t][mt]);
+      }
+    }
+  }
 #pragma unroll
   for (int t = 0; t < WN; t++) {
     const int n = (gt0 + t) * 16 + 4 * g;
@@ -348,6 +377,83 @@ __global__ void __launch_bounds__(256) x_to_f16_rowscale_kernel(const uint16_t* 
   }
 }
 
+// the row normalisation above plus the LoRA down-projection of the same row:
+// xa[row, r] = bf16(alpha * sum_k x[row, k] * la[r, k]) for r < R (zero up to
+// rp = R rounded to 32) -- one pass over x serves the f16 copy, the row scale
+// and the adapter input (RR = compile-time bound on R)
+template <int RR>
+__global__ void __launch_bounds__(256) x_rowscale_lora_kernel(const uint16_t* x, int64_t ldx, int K, int in_bf16,
+                                                               uint16_t* y, float* rs, const uint16_t* la, int R,
+                                                               float alpha, uint16_t* xa, int rp) {
+  __shared__ float red[4];
+  __shared__ float dots[4][RR];
+  const int64_t row = blockIdx.x;
+  const uint16_t* xr = x + row * ldx;
+  uint16_t* yr = y + row * (int64_t)K;
+  float amax = 0.f;
+  float d[RR];
+#pragma unroll
+  for (int r = 0; r < RR; r++) d[r] = 0.f;
+  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+    const uint4 v = *(const uint4*)(xr + k);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    float xv[8];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      xv[2 * j] = in_bf16 ? bf16_to_f32(w[j] & 0xffff) : f16_to_f32(w[j] & 0xffff);
+      xv[2 * j + 1] = in_bf16 ? bf16_to_f32(w[j] >> 16) : f16_to_f32(w[j] >> 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) amax = fmaxf(amax, fabsf(xv[j]));
+#pragma unroll
+    for (int r = 0; r < RR; r++) {
+      if (r < R) {
+        const uint4 av = *(const uint4*)(la + (size_t)r * K + k);
+        const uint32_t aw[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          d[r] += xv[2 * j] * bf16_to_f32(aw[j] & 0xffff) + xv[2 * j + 1] * bf16_to_f32(aw[j] >> 16);
+      }
+    }
+  }
+  amax = wave_max(amax);
+#pragma unroll
+  for (int r = 0; r < RR; r++) d[r] = wave_sum(d[r]);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[wv] = amax;
+#pragma unroll
+    for (int r = 0; r < RR; r++) dots[wv][r] = d[r];
+  }
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  for (int r = threadIdx.x; r < rp; r += 256) {
+    const float s = r < R && r < RR ? (dots[0][r] + dots[1][r] + dots[2][r] + dots[3][r]) * alpha : 0.f;
+    xa[row * rp + r] = f32_to_bf16(s);
+  }
+  int shift = 0;
+  if (amax > 0.f && amax <= 3.0e38f) {
+    int e;
+    frexpf(amax, &e);
+    shift = max(-120, min(120, 15 - e));
+  }
+  const float sc = ldexpf(1.f, shift);
+  if (threadIdx.x == 0) rs[row] = ldexpf(1.f, -shift);
+  if (y == nullptr) return;
+  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+    const uint4 v = *(const uint4*)(xr + k);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const float lo = in_bf16 ? bf16_to_f32(w[j] & 0xffff) : f16_to_f32(w[j] & 0xffff);
+      const float hi = in_bf16 ? bf16_to_f32(w[j] >> 16) : f16_to_f32(w[j] >> 16);
+      o[j] = pack2<F16>(lo * sc, hi * sc);
+    }
+    *(uint4*)(yr + k) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 template <int DK, typename TM, int WN, int WM, int WAVES_N>
 void launch_cfg(const MfgArgs& a, int ksplit, hipStream_t st) {
   constexpr int BN = WAVES_N * WN * 16, BM = (8 / WAVES_N) * WM * 16;
@@ -386,6 +492,17 @@ void launch_mfgemm(int fmt, bool dense_bf16, int tile, const MfgArgs& a, int ksp
     case DK_FP8E4: mfg::launch_tile<DK_FP8E4, F16>(tile, a, ksplit, st); break;
     case DK_FP8E5: mfg::launch_tile<DK_FP8E5, F16>(tile, a, ksplit, st); break;
   }
+}
+
+void launch_x_rowscale_lora(bool bf16, const uint16_t* x, int64_t M, int64_t ldx, int K, uint16_t* y, float* rs,
+                            const uint16_t* la, int R, float alpha, uint16_t* xa, int rp, hipStream_t st) {
+  if (M <= 0) return;
+  const dim3 grid((unsigned)M), blk(256);
+  const int ib = bf16 ? 1 : 0;
+  if (R <= 8) hipLaunchKernelGGL(mfg::x_rowscale_lora_kernel<8>, grid, blk, 0, st, x, ldx, K, ib, y, rs, la, R, alpha, xa, rp);
+  else if (R <= 16) hipLaunchKernelGGL(mfg::x_rowscale_lora_kernel<16>, grid, blk, 0, st, x, ldx, K, ib, y, rs, la, R, alpha, xa, rp);
+  else if (R <= 32) hipLaunchKernelGGL(mfg::x_rowscale_lora_kernel<32>, grid, blk, 0, st, x, ldx, K, ib, y, rs, la, R, alpha, xa, rp);
+  else hipLaunchKernelGGL(mfg::x_rowscale_lora_kernel<64>, grid, blk, 0, st, x, ldx, K, ib, y, rs, la, R, alpha, xa, rp);
 }
 
 void launch_x_to_f16_rowscale(bool bf16, const uint16_t* x, int64_t M, int64_t ldx, int K, uint16_t* y, float* rs,

@@ -80,14 +80,32 @@ struct MfgArgs {
   int64_t slab;            // f32 elements between split-K slabs
   int glu, act, lut_fmt;   // glu: tile-interleaved gate/up weight -> act(gate) * up [M, N / 2]
   int sps;                 // k-steps (64) per split, even
+  // rank-r update folded into the epilogue (LoRA): out += lora_x[M, rp] . lora_w[N, rp]^T,
+  // both bf16, zero-padded to rp % 32 == 0 (null: none; not with glu / split-K)
+  const uint16_t* lora_x;
+  const uint16_t* lora_w;
+  int lora_rp;
 };
 int mfg_block_n(int tile);
 int mfg_block_m(int tile);
 // fmt < 0: dense weights (dense_bf16 selects bf16 / f16 MFMA); else a low-bit fmt (f16 MFMA)
 void launch_mfgemm(int fmt, bool dense_bf16, int tile, const MfgArgs& a, int ksplit, hipStream_t st);
+// transposed-weight form (gemm_mfma_nn.hip): out[M, a.N] = g[M, a.K] . W[a.K, a.N] where W is
+// the blob / dense matrix of a linear with out_features a.K and in_features a.N (grad_x);
+// a.K % 64 == 0, low-bit: a.N % 256 == 0 (a.KC = a.N / 128)
+void launch_mfgemm_nn(int fmt, bool dense_bf16, int tile, const MfgArgs& a, int ksplit, hipStream_t st);
 // per-row power-of-two normalisation to f16: y = x * 2^s_m (row max in [2^14, 2^15)), rs[m] = 2^-s_m
 void launch_x_to_f16_rowscale(bool bf16, const uint16_t* x, int64_t M, int64_t ldx, int K, uint16_t* y, float* rs,
                               hipStream_t st);
+
+// ---- training kernels (train_kernels.hip) ------------------------------------
+// fused CE over logits [rows, ld] (V % 8 == 0): loss[row] = lse - x[label] (0 when
+// ignored); write_grad: logits := (softmax - onehot) * scale in place (0 rows if ignored)
+void launch_ce_fused(bool bf16, uint16_t* logits, int64_t rows, int64_t ld, int V, const int64_t* labels,
+                     int ignore_index, float scale, float* loss, bool write_grad, hipStream_t st);
+// out[r, n] += alpha * sum_m a[m, r] * b[m, n]  (a f32 [M, R], R <= 64; b 16-bit [M, ldb]; N % 8 == 0)
+void launch_skinny_tn(bool bf16, const float* a, int R, const uint16_t* b, int64_t ldb, int M, int N, float alpha,
+                      float* out, hipStream_t st);
 
 // ---- k-quant decoders (kquant.hip): GGUF q4_K / q5_K / q6_K / q2_K blocks ---
 void launch_kq_dequant(int fmt, bool bf16, const uint8_t* w, int64_t n, int64_t k, uint16_t* out, hipStream_t st);

@@ -131,9 +131,25 @@ def drop_prefetched() -> None:
     _ready.clear()
 
 
+# ---- the MFMA GEMM engine (csrc/hip/gemm_mfma.hip) ---------------------------
+# 256 x 256 blocks, LDS-DMA staged activations, per-workgroup decode of the
+# blob into LDS: replaces both paths above from ENGINE_MIN_M rows
+# (ILLM_GEMM_ENGINE=0 disables it for A/B runs).
+_ENGINE = os.environ.get("ILLM_GEMM_ENGINE", "1") == "1"
+ENGINE_MIN_M = int(os.environ.get("ILLM_GEMM_ENGINE_MIN_M", "512"))
+
+
+def use_engine(M: int, n: int, k: int, glu: bool = False) -> bool:
+    return (_ENGINE and not _USE_LIB and not _USE_FUSED and M >= ENGINE_MIN_M and k % 128 == 0
+            and n % (32 if glu else 16) == 0 and _DENSE_BUDGET <= 0
+            and hasattr(torch.ops.ipex_llm_amd, "mfgemm"))
+
+
 def lowbit_gemm(x, blob, fmt, n, k, bias=None):
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
+    if use_engine(M, n, k) and x.dtype in (torch.bfloat16, torch.float16):
+        return ops.mfgemm(x, blob, fmt, n, k, bias)
     if use_fused(M, n, k) and hasattr(ops, "gemm"):
         return ops.gemm(x, blob, fmt, n, k, bias)
     w = _dense_weight(blob, fmt, n, k, x.dtype)
@@ -146,6 +162,8 @@ def lowbit_gemm_glu(x, blob, fmt, n, k, act: int = 0):
     [M, 2I] round trip, no elementwise launches)."""
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
+    if use_engine(M, n, k, glu=True) and x.dtype in (torch.bfloat16, torch.float16):
+        return ops.mfgemm(x, blob, fmt, n, k, None, True, act)
     if use_fused(M, n, k) and hasattr(ops, "gemm_glu"):
         return ops.gemm_glu(x, blob, fmt, n, k, act)
     from .api import glu

@@ -1,0 +1,104 @@
+"""Fused lm_head + cross-entropy for causal-LM fine-tuning.
+
+Reference: the HF causal-LM loss the QLoRA recipe trains with
+(``LlamaForCausalLM.forward`` -> ``logits = lm_head(h)`` -> ``loss_function``
+upcasts the [tokens, vocab] logits to f32, softmax, NLL; backward runs the
+softmax gradient and a dense ``dlogits @ W`` -- SURVEY §3.5).  With
+Llama-3's 128 K vocabulary that is a 2 GB f32 tensor per 4 K-token step and
+three full passes over it.
+
+MI355X design: the tokens are processed in chunks; per chunk the logits are
+one engine GEMM (``mfgemm``, bf16, dense lm_head), ``ce_fused_`` turns them
+into the per-row loss and, IN PLACE, the logits gradient (softmax - onehot)
+in one read for the row statistics and one read + write for the gradient,
+and the hidden-state gradient is the transposed engine GEMM
+(``mfgemm_nn``) of that chunk -- computed during the forward, since the only
+consumer of the loss is a scalar backward.  Nothing of size [tokens, vocab]
+outlives a chunk; backward is one scale of the stored [tokens, hidden]
+gradient.  The lm_head weight is frozen here (QLoRA); a trainable head
+falls back to the unfused path.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+CHUNK = int(os.environ.get("ILLM_CE_CHUNK", "1024"))
+
+
+class _FusedLinearCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, weight, labels, ignore_index: int):
+        ops = torch.ops.ipex_llm_amd
+        T, H = h.shape
+        V = weight.shape[0]
+        loss_rows = torch.empty(T, device=h.device, dtype=torch.float32)
+        grad_h = torch.empty_like(h) if h.requires_grad else None
+        for c0 in range(0, T, CHUNK):
+            c1 = min(T, c0 + CHUNK)
+            logits = ops.mfgemm(h[c0:c1], weight, -1, V, H)
+            loss_rows[c0:c1] = ops.ce_fused_(logits, labels[c0:c1], ignore_index, 1.0 if grad_h is not None else 0.0)
+            if grad_h is not None:
+                grad_h[c0:c1] = ops.mfgemm_nn(logits, weight, -1, V, H)
+            del logits
+        n_valid = (labels != ignore_index).sum().clamp_(min=1).to(torch.float32)
+        ctx.save_for_backward(grad_h, n_valid)
+        return loss_rows.sum() / n_valid
+
+    @staticmethod
+    def backward(ctx, g):
+        grad_h, n_valid = ctx.saved_tensors
+        gh = None
+        if grad_h is not None and ctx.needs_input_grad[0]:
+            gh = grad_h * (g / n_valid).to(grad_h.dtype)
+        return gh, None, None, None
+
+
+def fused_linear_cross_entropy(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor,
+                               ignore_index: int = -100, shift: bool = True) -> torch.Tensor:
+    """mean CE of ``hidden @ weight^T`` against ``labels`` (HF causal-LM
+    semantics: position t predicts label t + 1 when ``shift``)."""
+    H = hidden.shape[-1]
+    if shift:
+        hidden = hidden[..., :-1, :]
+        labels = labels[..., 1:]
+    h2 = hidden.reshape(-1, H)
+    lab = labels.reshape(-1).to(torch.int64)
+    return _FusedLinearCE.apply(h2, weight, lab, ignore_index)
+
+
+def fused_ce_supported(model) -> bool:
+    from .. import ops
+    head = getattr(model, "lm_head", None)
+    w = getattr(head, "weight", None)
+    return (isinstance(head, torch.nn.Linear) and head.bias is None and w is not None and w.is_cuda
+            and not w.requires_grad and w.dtype in (torch.bfloat16, torch.float16)
+            and w.is_contiguous() and w.shape[1] % 128 == 0 and w.shape[0] % 128 == 0 and ops.native_gpu(w))
+
+
+def patch_fused_ce(model):
+    """Route ``model(input_ids, labels=...)`` of an HF causal LM through the
+    fused head + loss while training (logits are not materialised: the
+    output's ``logits`` is None).  Inference and unsupported heads keep the
+    original forward."""
+    if getattr(model, "_illm_fused_ce", False):
+        return model
+    orig = model.forward
+
+    def forward(*args, labels: Optional[torch.Tensor] = None, **kwargs):
+        if (labels is None or not torch.is_grad_enabled() or kwargs.get("return_dict") is False
+                or not fused_ce_supported(model)):
+            return orig(*args, labels=labels, **kwargs)
+        from transformers.modeling_outputs import CausalLMOutputWithPast
+        kwargs.pop("logits_to_keep", None)
+        kwargs.pop("num_items_in_batch", None)
+        out = model.model(*args, **kwargs)
+        loss = fused_linear_cross_entropy(out.last_hidden_state, model.lm_head.weight, labels)
+        return CausalLMOutputWithPast(loss=loss, logits=None, past_key_values=out.past_key_values,
+                                      hidden_states=out.hidden_states, attentions=out.attentions)
+
+    model.forward = forward
+    model._illm_fused_ce = True
+    return model

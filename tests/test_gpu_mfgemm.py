@@ -103,3 +103,43 @@ def test_mfgemm_glu_epilogue(cuda, name):
         ref = (torch.nn.functional.silu(g) if act == 0 else torch.nn.functional.gelu(g, approximate="tanh")) * u
         y = torch.ops.ipex_llm_amd.mfgemm(x, blob, f, 2 * I, k, None, True, act)
         assert y.shape == (M, I) and _rel(y, ref) < 5e-3, (name, act)
+
+
+@pytest.mark.parametrize("name", ["sym_int4", "nf4", "asym_int4", "sym_int8", "fp8_e4m3"])
+@pytest.mark.parametrize("tile", [0, 1])
+def test_mfgemm_nn_lowbit(cuda, name, tile):
+    """grad_x = g . W over the tiled blob (transposed LDS reads) vs fp32 torch"""
+    f = get_format(name).fmt
+    torch.manual_seed(5)
+    M, n, k = 300, 640, 768
+    blob = ops.quantize(torch.randn(n, k, device=cuda) * 0.05, f)
+    g = torch.randn(M, n, device=cuda).bfloat16()
+    dense = R.dequantize_device_blob(blob.cpu(), f, n, k).to(cuda)
+    ref = g.float() @ dense
+    y = torch.ops.ipex_llm_amd.mfgemm_nn(g, blob, f, n, k, tile, 1)
+    assert y.shape == (M, k) and _rel(y, ref) < 5e-3, (name, tile)
+
+
+@pytest.mark.parametrize("M,ksplit", [(64, 1), (1024, 1), (700, 3)])
+def test_mfgemm_nn_shapes_tiny_gradients(cuda, M, ksplit):
+    """gradients of 1e-6 (f16 would flush) and split-K"""
+    f = get_format("nf4").fmt
+    torch.manual_seed(6)
+    n, k = 1024, 1280
+    blob = ops.quantize(torch.randn(n, k, device=cuda) * 0.05, f)
+    g = (torch.randn(M, n, device=cuda) * 1e-6).bfloat16()
+    dense = R.dequantize_device_blob(blob.cpu(), f, n, k).to(cuda)
+    ref = g.float() @ dense
+    y = torch.ops.ipex_llm_amd.mfgemm_nn(g, blob, f, n, k, -1, ksplit)
+    assert _rel(y, ref) < 5e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_mfgemm_nn_dense(cuda, dtype):
+    torch.manual_seed(7)
+    M, n, k = 520, 1152, 640
+    w = (torch.randn(n, k, device=cuda) * 0.05).to(dtype)
+    g = torch.randn(M, n, device=cuda).to(dtype)
+    ref = g.float() @ w.float()
+    y = torch.ops.ipex_llm_amd.mfgemm_nn(g, w, -1, n, k)
+    assert y.dtype == dtype and _rel(y, ref) < 5e-3

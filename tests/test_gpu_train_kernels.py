@@ -1,0 +1,123 @@
+"""Training kernels against fp32 PyTorch references: fused cross-entropy
+(loss + in-place logits gradient), the skinny token-axis reduction of the
+LoRA gradients, the fused lm_head + CE autograd function, and the HIP flash
+attention forward / backward (causal, GQA)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_ce_fused_matches_torch(cuda, dtype):
+    torch.manual_seed(0)
+    R, V = 37, 4096 + 64
+    x = (torch.randn(R, V, device=cuda) * 3).to(dtype)
+    lab = torch.randint(0, V, (R,), device=cuda)
+    lab[3] = -100
+    ref_loss = torch.nn.functional.cross_entropy(x.float(), lab, ignore_index=-100, reduction="none")
+    xr = x.float().requires_grad_(True)
+    torch.nn.functional.cross_entropy(xr, lab, ignore_index=-100, reduction="sum").backward()
+    g = x.clone()
+    loss = torch.ops.ipex_llm_amd.ce_fused_(g, lab, -100, 1.0)
+    assert torch.allclose(loss, ref_loss, atol=2e-3, rtol=1e-3)
+    assert _rel(g, xr.grad) < 1e-2
+    assert torch.count_nonzero(g[3]) == 0
+
+
+@pytest.mark.parametrize("R", [8, 16, 32, 64])
+def test_skinny_tn(cuda, R):
+    torch.manual_seed(1)
+    M, N = 1000, 4096 + 128
+    a = torch.randn(M, R, device=cuda)
+    b = torch.randn(M, N, device=cuda).bfloat16()
+    out = torch.ops.ipex_llm_amd.skinny_tn(a, b, 0.5)
+    ref = 0.5 * a.t() @ b.float()
+    assert _rel(out, ref) < 1e-5
+
+
+def test_fused_linear_ce_matches_hf_loss(cuda):
+    from ipex_llm_amd.training.fused_ce import fused_linear_cross_entropy
+    torch.manual_seed(2)
+    B, T, H, V = 2, 300, 256, 2048
+    h = (torch.randn(B, T, H, device=cuda) * 0.5).bfloat16().requires_grad_(True)
+    w = (torch.randn(V, H, device=cuda) * 0.05).bfloat16()
+    lab = torch.randint(0, V, (B, T), device=cuda)
+    lab[0, :10] = -100
+    loss = fused_linear_cross_entropy(h, w, lab)
+    loss.backward()
+    hr = h.detach().float().requires_grad_(True)
+    logits = hr[:, :-1] @ w.float().t()
+    ref = torch.nn.functional.cross_entropy(logits.reshape(-1, V), lab[:, 1:].reshape(-1), ignore_index=-100)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 2e-3 * max(1.0, ref.item())
+    assert _rel(h.grad, hr.grad) < 2e-2
+
+
+def _ref_attn(q, k, v, scale, causal):
+    G = q.shape[1] // k.shape[1]
+    kk = k.float().repeat_interleave(G, 1)
+    vv = v.float().repeat_interleave(G, 1)
+    s = (q.float() @ kk.transpose(-1, -2)) * scale
+    if causal:
+        T = q.shape[2]
+        s = s.masked_fill(torch.triu(torch.ones(T, T, dtype=torch.bool, device=q.device), 1), float("-inf"))
+    return (torch.softmax(s, -1) @ vv).transpose(1, 2)          # [B, T, H, D]
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,T,D", [(2, 8, 2, 256, 128), (1, 4, 4, 128, 64), (2, 4, 1, 192, 128)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_train_flash_attention_fwd_bwd(cuda, B, Hq, Hkv, T, D, causal):
+    from ipex_llm_amd.training.flash_attn import flash_attention
+    torch.manual_seed(3)
+    # HF layout: [B, T, H, D] projections viewed as [B, H, T, D]
+    q = torch.randn(B, T, Hq, D, device=cuda).bfloat16().transpose(1, 2).requires_grad_(True)
+    k = torch.randn(B, T, Hkv, D, device=cuda).bfloat16().transpose(1, 2).requires_grad_(True)
+    v = torch.randn(B, T, Hkv, D, device=cuda).bfloat16().transpose(1, 2).requires_grad_(True)
+    scale = 1 / math.sqrt(D)
+    out = flash_attention(q, k, v, scale, causal)
+    dout = torch.randn_like(out)
+    out.backward(dout)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = _ref_attn(qr, kr, vr, scale, causal)
+    ref.backward(dout.float())
+    assert _rel(out, ref) < 1e-2
+    assert _rel(q.grad, qr.grad) < 2e-2
+    assert _rel(k.grad, kr.grad) < 2e-2
+    assert _rel(v.grad, vr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("qtype,r", [("nf4", 8), ("sym_int4", 16), ("nf4", 40)])
+def test_lora_engine_node_matches_fp32(cuda, qtype, r):
+    """the all-engine QLoRA linear (LoRA in the GEMM epilogues, skinny adapter
+    gradients) vs fp32 torch over the dequantized base"""
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.ops import reference as R
+    from ipex_llm_amd.quantize import get_format
+    from ipex_llm_amd.training.lora import _LoraEngineFn, _engine_lora_ok
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    torch.manual_seed(4)
+    M, N, K, s = 300, 768, 1024, 2.0
+    base = LowBitLinear(K, N, qtype, bias=False, device="meta")
+    base.load_dense((torch.randn(N, K, device=cuda) * 0.05).bfloat16(), device=cuda)
+    A = (torch.randn(r, K, device=cuda) * 0.05).bfloat16().requires_grad_(True)
+    B = (torch.randn(N, r, device=cuda) * 0.05).bfloat16().requires_grad_(True)
+    x = torch.randn(2, M // 2, K, device=cuda).bfloat16().requires_grad_(True)
+    assert _engine_lora_ok(base, x, A)
+    y = _LoraEngineFn.apply(x, A, B, base, s)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    W = R.dequantize_device_blob(base.weight.cpu(), get_format(qtype).fmt, N, K).to(cuda)
+    xr, Ar, Br = (t.detach().float().requires_grad_(True) for t in (x, A, B))
+    yr = xr @ W.t() + s * (xr @ Ar.t()) @ Br.t()
+    yr.backward(gy.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2
+    assert _rel(A.grad, Ar.grad) < 2e-2
+    assert _rel(B.grad, Br.grad) < 2e-2

@@ -193,9 +193,14 @@ def test_http_api(native):
             ev = [json.loads(l[6:]) for l in s.iter_lines() if l]
         assert ev[-1]["details"]["generated_tokens"] == 3
         # Prometheus metrics: request / token counters, TTFT + TPOT histograms, KV usage
-        m = c.get("/metrics").text
+        import time as _time
+        for _ in range(40):    # the last streamed request's counters land just after its final event
+            m = c.get("/metrics").text
+            gen = [l for l in m.splitlines() if l.startswith("ipex_llm_generation_tokens_total")]
+            if gen and float(gen[0].split()[-1]) >= 5 + 4 + 4 + 5 + 3:
+                break
+            _time.sleep(0.05)
         assert "ipex_llm_requests_total" in m and "ipex_llm_time_to_first_token_seconds_bucket" in m
-        gen = [l for l in m.splitlines() if l.startswith("ipex_llm_generation_tokens_total")]
         assert gen and float(gen[0].split()[-1]) >= 5 + 4 + 4 + 5 + 3
         assert "ipex_llm_kv_cache_usage_ratio" in m and "ipex_llm_time_per_output_token_seconds_count" in m
 

@@ -105,6 +105,9 @@ def main():
     if os.environ.get("ILLM_TRAIN_MLP", "1") == "1":
         from ipex_llm_amd.transformers.convert import _patch_mlp
         _patch_mlp(model)
+    # fused lm_head + CE and HIP flash attention fwd / bwd (ILLM_TRAIN_CE / ILLM_TRAIN_ATTN)
+    from ipex_llm_amd.training.lora import enable_training_kernels
+    enable_training_kernels(model)
     if args.grad_ckpt:
         model.gradient_checkpointing_enable()
         model.enable_input_require_grads()
