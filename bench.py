@@ -8,11 +8,16 @@ model sharded over all ranks (AutoTP, reference
 ``example/GPU/Deepspeed-AutoTP/deepspeed_autotp.py:81-106``), the native
 hipGraph decoder all-reduces every row-parallel projection's f32 accumulator
 over RCCL / the custom xGMI all-reduce (strong scaling: fixed global batch).
-``--ep``: MoE experts sharded over the ranks (Mixtral-8x7B, BASELINE config
-3), one all-reduce of the MoE block output per layer.  Random-init weights of
-the exact architecture are generated and quantized on the GPU (identical on
-every rank for TP/EP), a synthetic prompt batch is prefilled (first-token
-latency), then decode steps are replayed from one captured hipGraph.  W
+``--ep``: expert parallel, token-sharded (Mixtral-8x7B, BASELINE config 3):
+rank r keeps experts [r E/W, (r+1) E/W) and serves ITS OWN batch of
+sequences (attention data-parallel, weak scaling); every MoE block sends each
+(token, expert) pair to its expert's owner and back through the HIP peer
+all-to-all over xGMI (parallel/ep.py EPAllToAll: exactly T*k rows per rank
+per direction, device-side counts, captured in the decode hipGraph).
+Random-init weights of the exact architecture are generated and quantized on
+the GPU (identical on every rank for TP/EP), a synthetic prompt batch is
+prefilled (first-token latency), then decode steps are replayed from one
+captured hipGraph.  W
 untimed warmup steps, then EXACTLY K timed decode steps bracketed by barrier
 + synchronize; the slowest rank's time is reported.  Every timed step runs
 the full model (all layers + lm_head + argmax) for the whole batch.
@@ -120,21 +125,22 @@ def main():
     if args.ep and not getattr(cfg, "num_local_experts", None):
         raise SystemExit("--ep needs an MoE model (e.g. --model mixtral-8x7b)")
     group = dist.group.WORLD if sharded else None
-    if sharded:
+    if sharded and args.tp:
         from ipex_llm_amd.parallel.comm import setup_custom_all_reduce
         setup_custom_all_reduce(group)
+    B, P = args.batch, args.prompt_len
     t_build = time.perf_counter()
     # TP / EP: the same weights on every rank (one seed), each keeps its shard
     model = random_native_model(cfg, args.qtype, dev, torch.bfloat16, seed=1234 + (0 if sharded else rank),
-                                tp_group=group if args.tp else None, ep_group=group if args.ep else None)
+                                tp_group=group if args.tp else None, ep_group=group if args.ep else None,
+                                ep_tokens=bool(args.ep), ep_max_tokens=B * P)
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t_build
-
-    B, P = args.batch, args.prompt_len
     max_len = P + args.warmup + args.steps + 8
     eng = Engine(model)
     eng._ensure_cache(B, max_len)
-    g = torch.Generator().manual_seed(7 + (0 if sharded else rank))
+    same_tokens = sharded and args.tp            # TP: one batch; DP / token-sharded EP: a batch per rank
+    g = torch.Generator().manual_seed(7 + (0 if same_tokens else rank))
     prompts = torch.randint(0, cfg.vocab_size, (B, P), generator=g)
 
     def barrier():
@@ -144,6 +150,7 @@ def main():
     # ---- first-token latency (prefill of the whole batch + first token),
     # 1 warm-up + 3 trials (reference all-in-one harness semantics)
     nblk = (max_len + eng.block_size - 1) // eng.block_size
+    barrier()                                    # EP: the MoE exchanges need every rank in step
     ftl = []
     for trial in range(4):
         eng.cache.allocator = type(eng.cache.allocator)(eng.cache.num_blocks)
@@ -178,20 +185,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, ftl_ms = t.tolist()
     ms_step = dt / args.steps * 1e3
-    replicas = 1 if sharded else world
+    replicas = 1 if same_tokens else world
     value = B * replicas * args.steps / dt
     if rank == 0:
         out = {
             "metric": f"decode tokens/sec + first-token latency, {mname} INT4 at 1/2/4/8 MI355X",
             "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-            "scaling": "strong" if sharded else "weak",
+            "scaling": "strong" if same_tokens else "weak",
             # BASELINE.json publishes no value for this metric/config (its
             # charts are off-repo images): no ratio is claimed
             "vs_baseline": None, "dtype": "bf16",
             "data": f"synthetic (random prompt ids, random-init weights of the {mname} architecture)",
             "config": {"model": mname, "qtype": args.qtype, "global_batch": B * replicas,
-                       "batch_per_gpu": B if not sharded else B / world, "seq_len": P,
+                       "batch_per_gpu": B if not same_tokens else B / world, "seq_len": P,
                        "parallelism": f"tp{world}" if args.tp else (f"ep{world}" if args.ep else f"dp{world}"),
                        "hipgraph": not args.no_graph, "layers": cfg.num_hidden_layers},
             "first_token_latency_ms": round(ftl_ms, 2),

@@ -26,8 +26,10 @@
 //     peer signalled call N+1, i.e. after every peer's call-N kernel finished;
 //   * epochs are device-resident per-block counters (all advanced every call),
 //     so the launch is hipGraph-capturable;
-//   * every wait loop is bounded: on timeout the kernel raises an error flag
-//     and continues instead of hanging the GPU.
+//   * every wait loop is bounded (AR_TIMEOUT_S of wall time): on timeout the
+//     kernel sets the communicator's flag and ERR_PEER in the device error word
+//     (ops.check_kernel_errors raises) and writes NaN instead of a sum of stale
+//     peer data, so a lost peer can never become a silently wrong result.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -73,20 +75,24 @@ __device__ __forceinline__ uint4 pack_vec(const float (&s)[8]) {
 
 // publish `epoch` to every rank's slot (phase, parity, b, rank); wait for all
 // ranks' epochs in the own signal area.  Threads 0..W-1 take part.
+// `ok` (block-shared, 1 on entry) drops to 0 when a peer stays silent.
+constexpr int AR_TIMEOUT_S = 10;
 template <int W>
-__device__ __forceinline__ void ar_exchange(const AllReduceArgs& a, int phase, int parity, uint32_t epoch) {
+__device__ __forceinline__ void ar_exchange(const AllReduceArgs& a, int phase, int parity, uint32_t epoch, int& ok) {
   const int tid = threadIdx.x, b = blockIdx.x;
   if (tid < W) {
     __hip_atomic_store(ar_sig(a.bufs[tid], phase, parity, b, a.rank), epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* mysig = ar_sig(a.bufs[a.rank], phase, parity, b, tid);
-    int64_t spins = 0;
+    const uint64_t t0 = wall_clock64();     // 100 MHz constant clock
     while (__hip_atomic_load(mysig, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-      if (++spins > (1ll << 26)) {  // ~seconds: a peer is gone; report, do not hang
-        atomicExch(a.err, 1);
+      if (wall_clock64() - t0 > (uint64_t)AR_TIMEOUT_S * 100000000ull) {  // a peer is gone
+        ok = 0;
+        kerr(a.err, 1);
+        kerr(a.kerr, ERR_PEER);
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(2);
     }
   }
   __syncthreads();
@@ -99,6 +105,8 @@ __global__ void __launch_bounds__(AR_THREADS) peer_all_reduce(AllReduceArgs a) {
   const int parity = epoch & 1;
   const int64_t per = (a.nvec + gridDim.x - 1) / gridDim.x;
   const int64_t v0 = b * per, v1 = min(a.nvec, v0 + per);
+  __shared__ int ok;
+  if (tid == 0) ok = 1;
 
   // 1. my slice -> my data half `parity`
   u32x4v* mine = (u32x4v*)(a.bufs[a.rank] + AR_SIGNAL_BYTES + parity * a.cap);
@@ -106,7 +114,7 @@ __global__ void __launch_bounds__(AR_THREADS) peer_all_reduce(AllReduceArgs a) {
   for (int64_t v = v0 + tid; v < v1; v += AR_THREADS) mine[v] = in[v];
   __threadfence_system();
   __syncthreads();
-  ar_exchange<W>(a, 0, parity, epoch);
+  ar_exchange<W>(a, 0, parity, epoch, ok);
 
   const u32x4v* src[W];
 #pragma unroll
@@ -119,6 +127,10 @@ __global__ void __launch_bounds__(AR_THREADS) peer_all_reduce(AllReduceArgs a) {
       float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < W; r++) acc_vec<DT>(s, x[r]);
+      if (!ok) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) s[q] = __builtin_nanf("");
+      }
       const uint4 o = pack_vec<DT>(s);
       dst[v] = u32x4v{o.x, o.y, o.z, o.w};
     }
@@ -134,18 +146,53 @@ __global__ void __launch_bounds__(AR_THREADS) peer_all_reduce(AllReduceArgs a) {
     reduce_range(r0, r1, res);
     __threadfence_system();
     __syncthreads();
-    ar_exchange<W>(a, 1, parity, epoch);
+    ar_exchange<W>(a, 1, parity, epoch, ok);
     // 2b. gather every rank's reduced sub-slice
     u32x4v* out = (u32x4v*)a.out;
 #pragma unroll
     for (int r = 0; r < W; r++) {
       const u32x4v* rr = (const u32x4v*)(a.bufs[r] + AR_SIGNAL_BYTES + (2 + parity) * a.cap);
       const int64_t g0 = min(v1, v0 + r * sub), g1 = min(v1, g0 + sub);
-      for (int64_t v = g0 + tid; v < g1; v += AR_THREADS) out[v] = __builtin_nontemporal_load(rr + v);
+      for (int64_t v = g0 + tid; v < g1; v += AR_THREADS)
+        out[v] = ok ? __builtin_nontemporal_load(rr + v) : u32x4v{0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u};
     }
   }
   // all AR_MAX_BLOCKS epochs advance every call (blocks beyond this grid are
   // advanced by block 0), so every block of a call uses the same parity
+  if (tid == 0) a.counter[b] = epoch;
+  if (b == 0 && tid >= (int)gridDim.x && tid < AR_MAX_BLOCKS) a.counter[tid] = epoch;
+}
+
+// all-gather over the same buffers: block b copies its slice of the local
+// message into its data half, exchanges epochs (phase 0) like the all-reduce,
+// then reads every rank's slice and writes it at column block r of the
+// [rows, W * inner] output (last-dim concatenation, no permute afterwards)
+template <int W>
+__global__ void __launch_bounds__(AR_THREADS) peer_all_gather(AllReduceArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t epoch = a.counter[b] + 1;
+  const int parity = epoch & 1;
+  const int64_t per = (a.nvec + gridDim.x - 1) / gridDim.x;
+  const int64_t v0 = b * per, v1 = min(a.nvec, v0 + per);
+  __shared__ int ok;
+  if (tid == 0) ok = 1;
+  u32x4v* mine = (u32x4v*)(a.bufs[a.rank] + AR_SIGNAL_BYTES + parity * a.cap);
+  const u32x4v* in = (const u32x4v*)a.in;
+  for (int64_t v = v0 + tid; v < v1; v += AR_THREADS) mine[v] = in[v];
+  __threadfence_system();
+  __syncthreads();
+  ar_exchange<W>(a, 0, parity, epoch, ok);
+  u32x4v* out = (u32x4v*)a.out;
+  const int64_t inner = a.inner;
+#pragma unroll
+  for (int r = 0; r < W; r++) {
+    const u32x4v* src = (const u32x4v*)(a.bufs[r] + AR_SIGNAL_BYTES + parity * a.cap);
+    for (int64_t v = v0 + tid; v < v1; v += AR_THREADS) {
+      const int64_t row = v / inner, c = v - row * inner;
+      out[(row * W + r) * inner + c] =
+          ok ? __builtin_nontemporal_load(src + v) : u32x4v{0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u};
+    }
+  }
   if (tid == 0) a.counter[b] = epoch;
   if (b == 0 && tid >= (int)gridDim.x && tid < AR_MAX_BLOCKS) a.counter[tid] = epoch;
 }
@@ -176,6 +223,22 @@ void launch_custom_all_reduce(const AllReduceArgs& a, hipStream_t st) {
   if (a.dtype == AR_F32) launch_dt<AR_F32>(a, nb, st);
   else if (a.dtype == AR_BF16) launch_dt<AR_BF16>(a, nb, st);
   else launch_dt<AR_F16>(a, nb, st);
+}
+
+void launch_custom_all_gather(const AllReduceArgs& a, hipStream_t st) {
+  const int nb = custom_all_reduce_blocks(a.nvec);
+#define AGK(WW) hipLaunchKernelGGL((peer_all_gather<WW>), dim3(nb), dim3(AR_THREADS), 0, st, a)
+  switch (a.world) {
+    case 1: AGK(1); break;
+    case 2: AGK(2); break;
+    case 3: AGK(3); break;
+    case 4: AGK(4); break;
+    case 5: AGK(5); break;
+    case 6: AGK(6); break;
+    case 7: AGK(7); break;
+    default: AGK(8); break;
+  }
+#undef AGK
 }
 
 }  // namespace illm

@@ -16,8 +16,11 @@
 //   * activations: the 128 x 128 x-chunk is staged global -> registers ->
 //     LDS as f16 (double buffered, one chunk ahead), padded rows (272 B) so
 //     the B-fragment ds_read_b128 of 16 rows hit distinct banks.  bf16
-//     activations are converted to f16 ONCE per call (launch_bf16_to_f16_sat):
-//     converting while staging repeated the work for every n-block and was
+//     activations are converted to f16 ONCE per call with a per-row
+//     power-of-two normalisation (launch_x_to_f16_rowscale, shared with the
+//     MFMA engine): every bf16 value keeps its f16 mantissa, nothing
+//     saturates at 65504, and the epilogue multiplies the row scale back.
+//     Converting while staging repeated the work for every n-block and was
 //     ~90 % of the kernel's VALU instructions (rocprofv3 PMC, gate_up M=1024);
 //   * XCD-aware block order: the 8 m-blocks of one n-block run on one XCD
 //     (ids b, b + 8, ...), so a weight chunk comes from HBM once per XCD
@@ -237,6 +240,20 @@ __global__ void __launch_bounds__(256) lowbit_gemm_kernel(const GemmArgs a) {
   }
 
   // ---- epilogue: lane holds out[m0 + 16 mt + r16][16 tile + 4 g + i]
+  // undo the per-row activation normalisation first (exact: powers of two)
+  if (a.rs != nullptr) {
+#pragma unroll
+    for (int mt = 0; mt < WM; mt++) {
+      const int mm = m0 + (wm * WM + mt) * 16 + r16;
+      float rsv = 1.f;
+      if (mm < Mrows)
+        rsv = a.rs[!grouped ? mm : (a.moe_x_sorted ? pos0 + mm : a.moe_rows[pos0 + mm] / a.moe_xdiv)];
+#pragma unroll
+      for (int t = 0; t < WN; t++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[t][mt][i] *= rsv;
+    }
+  }
   if (a.glu) {
     // the wave's tiles are gate/up pairs (16-row interleave, tile0 even):
     // act(gate) * up in f32, one rounding (as the decode GLU GEMV epilogue)

@@ -41,7 +41,9 @@ struct GemmArgs {
   int lut_fmt;
   int glu;                 // 1: tile-interleaved gate/up weight, out = act(gate) * up [M, N / 2]
   int act;                 // 0 = silu, 1 = gelu(tanh)
-  int x_f16;               // 1: x already holds f16 (saturated) copies of the bf16 activations
+  int x_f16;               // 1: x already holds f16 copies of the bf16 activations
+  const float* rs;         // per x-row power-of-two scale (launch_x_to_f16_rowscale), null = 1:
+                           // x rows are normalised into f16 range, the epilogue multiplies rs back
   // grouped (MoE, "FlashMoE") launch: (token, expert) pairs sorted by expert
   // (moe_align); blockIdx.x walks (expert, m-block) over every local expert's
   // pairs, weights of expert e at w + e * w_stride.  M = number of pairs.
@@ -320,12 +322,17 @@ struct AllReduceArgs {
   int64_t nvec;                 // 16-B vectors in the message
   int64_t cap;                  // bytes per data half
   uint32_t* counter;            // [AR_MAX_BLOCKS] local epochs
-  int* err;
+  int* err;                     // the communicator's flag (CustomAllReduce.check)
+  int* kerr;                    // the device kernel error word (ERR_PEER)
   int dtype;                    // ArDtype
   int two_shot;                 // reduce-scatter + all-gather through the result halves
+  int64_t inner;                // all-gather: 16-B vectors per row of a rank's slice
 };
 
 void launch_custom_all_reduce(const AllReduceArgs& a, hipStream_t st);
+// out [rows, W * inner] <- every rank's in [rows, inner] (16-B vectors): the
+// vocab-parallel logits gather, same buffers / epochs as the all-reduce
+void launch_custom_all_gather(const AllReduceArgs& a, hipStream_t st);
 int custom_all_reduce_blocks(int64_t nvec);
 
 // ---- fused multi-tensor AdamW (optim.hip) ----------------------------------

@@ -261,11 +261,14 @@ Tensor gemm(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   if (M == 0) return out;
   illm::GemmArgs a{};
   // bf16 activations -> f16 once per call (the MFMA input type of the decoded weights)
-  Tensor xh;
-  if (bf16) {
+  Tensor xh, xrs;
+  if (bf16) {   // per-row power-of-two normalisation into f16 range (no saturation)
+    const int64_t xr = xc.numel() / k;
     xh = at::empty(xc.sizes(), xc.options().dtype(at::kHalf));
-    illm::launch_bf16_to_f16_sat(p16(xc), m16(xh), xc.numel(), cur_stream());
+    xrs = at::empty({xr}, xc.options().dtype(at::kFloat));
+    illm::launch_x_to_f16_rowscale(true, p16(xc), xr, k, (int)k, m16(xh), xrs.data_ptr<float>(), cur_stream());
     a.x_f16 = 1;
+    a.rs = xrs.data_ptr<float>();
   }
   a.x = bf16 ? p16(xh) : p16(xc);
   a.M = (int)M;
@@ -298,11 +301,14 @@ Tensor gemm_glu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   if (M == 0) return out;
   illm::GemmArgs a{};
   // bf16 activations -> f16 once per call (the MFMA input type of the decoded weights)
-  Tensor xh;
-  if (bf16) {
+  Tensor xh, xrs;
+  if (bf16) {   // per-row power-of-two normalisation into f16 range (no saturation)
+    const int64_t xr = xc.numel() / k;
     xh = at::empty(xc.sizes(), xc.options().dtype(at::kHalf));
-    illm::launch_bf16_to_f16_sat(p16(xc), m16(xh), xc.numel(), cur_stream());
+    xrs = at::empty({xr}, xc.options().dtype(at::kFloat));
+    illm::launch_x_to_f16_rowscale(true, p16(xc), xr, k, (int)k, m16(xh), xrs.data_ptr<float>(), cur_stream());
     a.x_f16 = 1;
+    a.rs = xrs.data_ptr<float>();
   }
   a.x = bf16 ? p16(xh) : p16(xc);
   a.M = (int)M;
@@ -349,11 +355,14 @@ Tensor moe_gemm(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   Tensor out = at::empty({P, nout}, xc.options().dtype(out_f32 ? at::kFloat : xc.scalar_type()));
   if (P == 0) return out;
   illm::GemmArgs a{};
-  Tensor xh;
-  if (bf16) {
+  Tensor xh, xrs;
+  if (bf16) {   // per-row power-of-two normalisation into f16 range (no saturation)
+    const int64_t xr = xc.numel() / k;
     xh = at::empty(xc.sizes(), xc.options().dtype(at::kHalf));
-    illm::launch_bf16_to_f16_sat(p16(xc), m16(xh), xc.numel(), cur_stream());
+    xrs = at::empty({xr}, xc.options().dtype(at::kFloat));
+    illm::launch_x_to_f16_rowscale(true, p16(xc), xr, k, (int)k, m16(xh), xrs.data_ptr<float>(), cur_stream());
     a.x_f16 = 1;
+    a.rs = xrs.data_ptr<float>();
   }
   a.x = bf16 ? p16(xh) : p16(xc);
   a.M = (int)P;
@@ -1457,6 +1466,9 @@ void decode_advance(const c10::optional<Tensor>& logits, Tensor& ids, Tensor& ne
 }
 
 }  // namespace
+
+// the device error word for the other binding units (ops_dist.cpp)
+int* illm_kernel_err(const c10::Device& dev) { return kernel_err(dev); }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv_glu_in", &gemv_glu_in);

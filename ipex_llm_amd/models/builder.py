@@ -130,7 +130,8 @@ def lowbit_from_dense(w: torch.Tensor, qtype, device, bias: Optional[torch.Tenso
 @torch.no_grad()
 def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat16, seed: int = 0,
                         lm_head_qtype=None, std: float = 0.02, tp_group=None, ep_group=None,
-                        tp_shard_lm_head: bool = True) -> NativeCausalLM:
+                        tp_shard_lm_head: bool = True, ep_tokens: bool = False,
+                        ep_max_tokens: Optional[int] = None) -> NativeCausalLM:
     """Random-init model of ``cfg``'s architecture, quantized on ``device``.
 
     ``tp_group``: tensor parallel (AutoTP layout, SRC example
@@ -139,7 +140,10 @@ def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat
     query heads and their KV heads (column-parallel qkv), the matching o_proj
     columns (row-parallel, all-reduced), an I / world slice of gate/up
     (column) and down (row), a vocab slice of lm_head (logits all-gathered).
-    ``ep_group``: expert parallel -- rank r keeps experts [r E/W, (r+1) E/W).
+    ``ep_group``: expert parallel -- rank r keeps experts [r E/W, (r+1) E/W);
+    ``ep_tokens``: token-sharded EP (each rank runs its own sequences, MoE
+    pairs travel through ``parallel.ep``'s exact all-to-all; collective) --
+    otherwise every rank sees all tokens and the MoE output is all-reduced.
     Either way the result equals the single-GPU model of the same seed."""
     spec = spec_from_config(cfg)
     s = spec
@@ -224,6 +228,9 @@ def random_native_model(cfg, qtype="sym_int4", device="cuda", dtype=torch.bfloat
     model = NativeCausalLM(s, embed, layers, ones_ish(spec.hidden_size), lm_head, inv_freq.to(device), dtype)
     if W > 1:
         model.tp_group = tp_group
+    if ep_group is not None and ep_tokens:
+        from ..parallel.ep import enable_token_sharded_ep
+        enable_token_sharded_ep(model, ep_max_tokens)
     return model.eval()
 
 

@@ -154,6 +154,9 @@ class NativeMoE(nn.Module):
         self.e0 = expert_offset
         self.num_experts = num_experts or router.shape[0]
         self.ep_group = ep_group
+        # token-sharded expert parallel (parallel.ep.enable_token_sharded_ep):
+        # an exchange object; None = replicated tokens + one EP all-reduce
+        self.ep_a2a = None
 
     @property
     def local_experts(self) -> int:
@@ -184,6 +187,9 @@ class NativeMoE(nn.Module):
     def graph_max_tokens(self) -> int:
         """tokens per forward that stay on device-only launches (capturable):
         the grouped GEMV up to 16 tokens, the grouped GEMM above"""
+        a2a = getattr(self, "ep_a2a", None)
+        if a2a is not None:       # the peer exchange is capturable, the exact-split one is not
+            return a2a.max_tokens if a2a.capturable else 0
         dev = self.gate_up.weight.device
         if dev.type == "cuda" and ops.native_gpu(self.gate_up.weight) and self.gate_up.out_features % 32 == 0:
             return 1 << 30
@@ -201,7 +207,7 @@ class NativeMoE(nn.Module):
     def acc_ok(self, x2: torch.Tensor) -> bool:
         """decode block can accumulate into a residual-norm f32 slab"""
         sm = self.shared_mlp
-        return (self.fused_route_ok(x2)
+        return (getattr(self, "ep_a2a", None) is None and self.fused_route_ok(x2)
                 and (sm is None or (isinstance(sm, SharedExpertMLP) and hasattr(sm.gate_up_proj, "fmt")
                                     and hasattr(sm.down_proj, "fmt") and getattr(sm.down_proj, "bias", None) is None)))
 
@@ -277,7 +283,15 @@ class NativeMoE(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).contiguous()
-        if self.fused_route_ok(x2):
+        a2a = getattr(self, "ep_a2a", None)
+        if a2a is not None:
+            # token-sharded EP: this rank's tokens go to their experts' owners
+            # and come back weighted (exact T*k rows each way)
+            from ..parallel.ep import _local_expert_fn
+            w, ids = self.route(x2)
+            fn = self.__dict__.get("_ep_fn") or self.__dict__.setdefault("_ep_fn", _local_expert_fn(self))
+            y = a2a(x2, w, ids, fn)
+        elif self.fused_route_ok(x2):
             w, ids, off, rows = self._route_fused(x2)
             y = self._experts_grouped(x2, w, ids, off, rows)
         else:
@@ -289,7 +303,7 @@ class NativeMoE(nn.Module):
                 y = self._experts_gemm(x2, w, ids)
             else:
                 y = self._experts_loop(x2, w, ids)
-        if self.ep_group is not None:
+        if self.ep_group is not None and a2a is None:
             from ..parallel.comm import all_reduce_inplace
             y = all_reduce_inplace(y, self.ep_group)
         if self.shared_mlp is not None:

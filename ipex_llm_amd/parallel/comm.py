@@ -91,10 +91,15 @@ def all_reduce_inplace(t: torch.Tensor, group=None) -> torch.Tensor:
 
 def all_gather_last_dim(t: torch.Tensor, group=None) -> torch.Tensor:
     """Concatenate every rank's ``t`` along the last dim (vocab-parallel
-    logits)."""
+    logits).  GPU messages that fit take the capturable peer all-gather of
+    the group's :class:`CustomAllReduce` (written straight into the
+    concatenated layout); the rest go to RCCL / gloo."""
     w = get_world_size(group)
     if w == 1:
         return t
+    car = _CUSTOM.get(id(group)) if t.is_cuda else None
+    if car is not None and car.gather_eligible(t):
+        return car.all_gather_last_dim(t)
     parts = [torch.empty_like(t) for _ in range(w)]
     dist.all_gather(parts, t.contiguous(), group=group)
     return torch.cat(parts, dim=-1)
@@ -158,6 +163,19 @@ class CustomAllReduce:
         return (t.dtype in (torch.bfloat16, torch.float16, torch.float32) and t.is_contiguous() and nb % 16 == 0
                 and 0 < nb <= self.cap and t.device == self.device)
 
+    def gather_eligible(self, t: torch.Tensor) -> bool:
+        return (t.dtype in (torch.bfloat16, torch.float16, torch.float32) and t.dim() >= 1
+                and (t.shape[-1] * t.element_size()) % 16 == 0 and 0 < t.numel() * t.element_size() <= self.cap
+                and t.device == self.device)
+
+    def all_gather_last_dim(self, t: torch.Tensor) -> torch.Tensor:
+        """[..., n] on every rank -> [..., W * n] (rank r's block at columns
+        r*n..), one launch, capturable"""
+        t = t.contiguous()
+        out = t.new_empty(*t.shape[:-1], self.world * t.shape[-1])
+        torch.ops.ipex_llm_amd.custom_all_gather(t, out, self.ptrs, self.rank, self.counter, self.cap, self.err)
+        return out
+
     def __call__(self, t: torch.Tensor, out: Optional[torch.Tensor] = None, two_shot: int = -1) -> torch.Tensor:
         """sum over the group; ``out`` may alias ``t`` (each block reads its
         slice before it writes it)"""
@@ -167,6 +185,8 @@ class CustomAllReduce:
         return out
 
     def check(self):
+        """raise if a call timed out waiting for a peer (the kernels also set
+        ERR_PEER in the device error word: ops.check_kernel_errors raises)"""
         if int(self.err.item()) != 0:
             raise RuntimeError("custom all-reduce timed out waiting for a peer")
 

@@ -186,12 +186,15 @@ def _ep_worker(rank, world, port, path, want):
     ref = torch.tensor(want["logits"])
     assert ((got - ref).norm() / ref.norm()).item() < 1e-4
     # token-sharded prefill: all-to-all dispatch == replicated compute
-    from ipex_llm_amd.parallel.ep import ep_moe_all_to_all
+    from ipex_llm_amd.parallel.ep import ExactSplitAllToAll, ep_moe_all_to_all
     from ipex_llm_amd.transformers.hf_native import get_native
     nm, _ = get_native(m)
     moe = nm.layers[0].mlp
     x = torch.randn(6, 128, generator=torch.Generator().manual_seed(rank))
+    moe.ep_a2a = ExactSplitAllToAll(None, moe.local_experts)
     mine = ep_moe_all_to_all(x, moe)
+    assert moe.ep_a2a.last_sent_rows == 6 * 2       # exactly T * k rows leave the rank
+    moe.ep_a2a = None
     import torch.distributed as dist
     xs = [torch.empty_like(x) for _ in range(world)]
     dist.all_gather(xs, x)                       # replicated-token reference

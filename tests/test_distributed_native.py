@@ -72,10 +72,24 @@ def _worker(rank, world, port, kind, want):
         m = random_native_model(_llama_cfg(), "sym_int8", "cpu", torch.float32, seed=0, std=0.05, tp_group=g)
         assert m.spec.num_heads == 8 // world and m.tp_group is g
         assert m.layers[0].self_attn.o_proj.mp_group is g and m.layers[0].mlp.down_proj.mp_group is g
-    else:
+    elif kind == "ep":
         m = random_native_model(_mixtral_cfg(), "sym_int8", "cpu", torch.float32, seed=0, std=0.05, ep_group=g)
         moe = m.layers[0].mlp
         assert moe.local_experts == 8 // world and moe.e0 == rank * (8 // world)
+    else:
+        # token-sharded EP: rank r serves ONLY prompt r % 2 (attention is not
+        # replicated); its MoE pairs travel through the exact-split exchange
+        from ipex_llm_amd.parallel.ep import ExactSplitAllToAll
+        m = random_native_model(_mixtral_cfg(), "sym_int8", "cpu", torch.float32, seed=0, std=0.05, ep_group=g,
+                                ep_tokens=True)
+        a2a = m.layers[0].mlp.ep_a2a
+        assert isinstance(a2a, ExactSplitAllToAll) and m.layers[1].mlp.ep_a2a is a2a
+        from ipex_llm_amd.engine.runner import Engine
+        out = Engine(m).generate([PROMPTS[rank % 2]], max_new_tokens=6, use_graph=False)
+        assert a2a.last_sent_rows == 1 * 2          # last call: one decode token x top-2, nothing more
+        assert out == [want[rank % 2]], (rank, out, want)
+        dist.destroy_process_group()
+        return
     out = _generate(m)
     assert out == want, (rank, out, want)
     dist.destroy_process_group()
@@ -93,3 +107,10 @@ def test_native_ep_decode_matches_single(world):
     from ipex_llm_amd.models.builder import random_native_model
     single = random_native_model(_mixtral_cfg(), "sym_int8", "cpu", torch.float32, seed=0, std=0.05)
     _run(_worker, world, "ep", _generate(single))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_native_ep_token_sharded_matches_single(world):
+    from ipex_llm_amd.models.builder import random_native_model
+    single = random_native_model(_mixtral_cfg(), "sym_int8", "cpu", torch.float32, seed=0, std=0.05)
+    _run(_worker, world, "ep_a2a", _generate(single))

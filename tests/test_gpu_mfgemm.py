@@ -143,3 +143,31 @@ def test_mfgemm_nn_dense(cuda, dtype):
     ref = g.float() @ w.float()
     y = torch.ops.ipex_llm_amd.mfgemm_nn(g, w, -1, n, k)
     assert y.dtype == dtype and _rel(y, ref) < 5e-3
+
+
+def test_small_m_gemm_and_moe_gemm_large_activations(cuda):
+    """the M < ENGINE_MIN_M prefill GEMM, its GLU form and the grouped MoE
+    GEMM take the same row-normalised f16 activations: |x| > 65504 and tiny
+    rows stay exact instead of saturating"""
+    f = get_format("sym_int4").fmt
+    torch.manual_seed(3)
+    M, n, k = 96, 256, 512
+    blob = ops.quantize(torch.randn(n, k, device=cuda) * 0.05, f)
+    x = torch.randn(M, k, device=cuda)
+    x[:16] *= 3e5
+    x[16:32] *= 1e-7
+    x = x.bfloat16()
+    ref = R.lowbit_linear_ref(x, blob.cpu(), f, n, k).to(cuda)
+    y = torch.ops.ipex_llm_amd.gemm(x, blob, f, n, k, None)
+    assert torch.isfinite(y.float()).all()
+    for lo, hi in ((0, 16), (16, 32), (32, M)):
+        assert _rel(y[lo:hi], ref[lo:hi]) < 5e-3, (lo, hi)
+    # grouped: 2 experts, every token routed to expert (t % 2)
+    blob2 = torch.stack([blob, ops.quantize(torch.randn(n, k, device=cuda) * 0.05, f)])
+    ids = (torch.arange(M, device=cuda) % 2).view(M, 1).to(torch.int32)
+    off, rows = ops.moe_align(ids, 0, 2)
+    out = ops.moe_gemm(x, blob2, f, n, k, off, rows, 1, False, False, False, 0, True)
+    ref2 = torch.stack([R.lowbit_linear_ref(x[t:t + 1], blob2[t % 2].cpu(), f, n, k)[0] for t in range(M)]).to(cuda)
+    assert torch.isfinite(out).all()
+    for lo, hi in ((0, 16), (16, 32), (32, M)):
+        assert _rel(out[lo:hi], ref2[lo:hi]) < 5e-3, (lo, hi)

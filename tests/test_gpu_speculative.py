@@ -1,14 +1,38 @@
 """Self-speculative decoding on the GPU as captured hipGraph rounds
 (generation/spec_graph.py): bf16 target (dequantized INT4 weights) + INT4
-draft; the output follows the target's greedy decoding and the rounds ran
-from captured graphs."""
+draft.  Greedy speculation must reproduce the target's own greedy decoding:
+only the GENERATED tokens are compared (never the prompt), for k = 2, 4, 6
+and adaptive k.  The verify pass scores k + 1 rows at once while the
+reference decode scores one, so the two can only legitimately differ where
+the target's two candidates are a numerical tie; a divergence is accepted
+only when an independent forward of the target over the common prefix shows
+that tie (|logit(a) - logit(b)| within bf16 noise), and it is logged.
+Reference behaviour: SRC/transformers/speculative.py:805-1271 (greedy
+acceptance keeps the target's argmax, :878 / :946)."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
-def test_graph_speculative_matches_target():
+def _first_diff(a, b):
+    for i, (x, y) in enumerate(zip(a, b)):
+        if x != y:
+            return i
+    return None
+
+
+def _tie_gap(te, prefix, a, b):
+    """|logit(a) - logit(b)| at the position after ``prefix`` and the logit
+    scale, from a fresh prefill of the target (a third numerical path)"""
+    st = te.new_sequence(len(prefix) + 8)
+    lg = te.forward_chunk(st, list(prefix), 0)[-1].float()
+    te.cache.allocator.release(st.blocks)
+    return abs(lg[a] - lg[b]).item(), lg.abs().max().item()
+
+
+@pytest.mark.parametrize("k,adaptive", [(2, False), (4, False), (6, False), (4, True)])
+def test_graph_speculative_matches_target(k, adaptive):
     from transformers import LlamaConfig
     from ipex_llm_amd.engine.runner import Engine
     from ipex_llm_amd.generation.spec_graph import GraphSpeculator
@@ -16,16 +40,22 @@ def test_graph_speculative_matches_target():
     cfg = LlamaConfig(vocab_size=2048, hidden_size=512, intermediate_size=1024, num_hidden_layers=2,
                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=2048)
     dev = torch.device("cuda")
-    draft = random_native_model(cfg, "sym_int4", dev, torch.bfloat16, seed=0)
+    draft = random_native_model(cfg, "sym_int4", dev, torch.bfloat16, seed=0, std=0.05)
     target = dense_copy(draft)
     te, de = Engine(target), Engine(draft)
     prompt = list(range(3, 60))
-    ref = te.generate([prompt], max_new_tokens=40, use_graph=True)[0]
-    for k, adaptive in ((2, False), (4, True)):
-        sp = GraphSpeculator(te, de, k, 256, k_max=6 if adaptive else k, adaptive=adaptive)
-        out = sp.generate(prompt, 40)
-        assert len(out) == len(ref)
-        agree = sum(int(a == b) for a, b in zip(out, ref)) / len(ref)
-        assert agree >= 0.9, (k, agree)
-        assert sp.graphs, "no round ran from a captured graph"
-        assert sp.acceptance > 0.3, sp.acceptance
+    n_new = 40
+    ref = te.generate([prompt], max_new_tokens=n_new, use_graph=True)[0][len(prompt):]
+    sp = GraphSpeculator(te, de, k, 256, k_max=6 if adaptive else k, adaptive=adaptive)
+    out = sp.generate(prompt, n_new)[len(prompt):]
+    assert len(out) == len(ref) == n_new
+    i = _first_diff(out, ref)
+    if i is not None:
+        gap, scale = _tie_gap(te, prompt + ref[:i], ref[i], out[i])
+        print(f"k={k} adaptive={adaptive}: first divergence at generated token {i}: "
+              f"target {ref[i]} vs speculative {out[i]}, logit gap {gap:.4g} (scale {scale:.3g})")
+        assert gap <= 2e-2 * max(1.0, scale), (k, adaptive, i, gap, scale)
+    else:
+        print(f"k={k} adaptive={adaptive}: all {n_new} generated tokens equal the target's")
+    assert sp.graphs, "no round ran from a captured graph"
+    assert sp.acceptance > 0.3, sp.acceptance

@@ -5,9 +5,9 @@ for the host-side rendezvous, the custom peer all-reduce for every
 row-parallel accumulator -- the same kernels and IPC handle exchange as ranks
 on separate GPUs).  Each rank keeps half the heads / intermediate rows of the
 same random weights; the hipGraph decode must reproduce the single-GPU
-model's greedy tokens.  lm_head stays replicated here (its vocab-parallel
-all-gather is an RCCL collective, not available between two processes on one
-device)."""
+model's greedy tokens.  lm_head is vocab-parallel: the logits all-gather runs
+through the capturable peer all-gather (csrc/hip/allreduce.hip
+peer_all_gather) inside the captured step."""
 import os
 import socket
 
@@ -68,7 +68,9 @@ def _worker(rank, world, port, forced, want, q):
         g = dist.group.WORLD
         comm._CUSTOM[id(g)] = comm.CustomAllReduce(g, device="cuda:0", max_bytes=1 << 20)
         m = random_native_model(_cfg(), "sym_int4", "cuda:0", torch.bfloat16, seed=0, std=0.05, tp_group=g,
-                                tp_shard_lm_head=False)
+                                tp_shard_lm_head=True)
+        from ipex_llm_amd.parallel.tp import VocabParallelHead
+        assert isinstance(m.lm_head, VocabParallelHead)
         want = want.to("cuda:0")
         for use_graph in (False, True):
             got = _forced_logits(m, forced, use_graph)

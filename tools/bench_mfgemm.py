@@ -41,6 +41,7 @@ def main():
                 if qt == "dense":
                     ours = timeit(lambda: torch.ops.ipex_llm_amd.mfgemm(x, w, -1, n, k, None, False, 0, tile, ks))
                     lib = timeit(lambda: F.linear(x, w))
+                    extra = {}
                     y1 = torch.ops.ipex_llm_amd.mfgemm(x, w, -1, n, k, None, False, 0, tile, ks).float()
                     y2 = F.linear(x, w).float()
                 else:
@@ -48,14 +49,19 @@ def main():
                     blob = ops.quantize(w, f)
                     ours = timeit(lambda: torch.ops.ipex_llm_amd.mfgemm(x, blob, f, n, k, None, False, 0, tile, ks))
                     lib = timeit(lambda: F.linear(x, torch.ops.ipex_llm_amd.dequantize_device(blob, f, n, k, x.dtype)))
+                    wd = torch.ops.ipex_llm_amd.dequantize_device(blob, f, n, k, x.dtype)
+                    blas = timeit(lambda: F.linear(x, wd))          # library GEMM alone (weight pre-dequantized)
+                    old = timeit(lambda: torch.ops.ipex_llm_amd.gemm(x, blob, f, n, k, None))
                     y1 = torch.ops.ipex_llm_amd.mfgemm(x, blob, f, n, k, None, False, 0, tile, ks).float()
-                    y2 = F.linear(x, torch.ops.ipex_llm_amd.dequantize_device(blob, f, n, k, x.dtype)).float()
+                    y2 = F.linear(x, wd).float()
+                    del wd
+                    extra = {"blas_only_us": round(blas, 1), "old_kernel_us": round(old, 1)}
                 rel = ((y1 - y2).norm() / y2.norm()).item()
                 fl = 2 * M * n * k
                 print(json.dumps({"qtype": qt, "M": M, "op": name, "ours_us": round(ours, 1), "lib_us": round(lib, 1),
                                   "ours_TF": round(fl / ours / 1e6, 1), "lib_TF": round(fl / lib / 1e6, 1),
                                   "speedup": round(lib / ours, 3), "rel_diff": round(rel, 5),
-                                  "tile": tile, "ks": ks}), flush=True)
+                                  "tile": tile, "ks": ks, **extra}), flush=True)
                 del w, x
 
 
