@@ -104,8 +104,11 @@ class _Detok:
         return d
 
 
-def build_app(engine: LLMEngine, tokenizer, model_name: str = "ipex-llm-amd", loop_thread: Optional[EngineLoop] = None):
-    from fastapi import FastAPI, HTTPException
+def build_app(engine: LLMEngine, tokenizer, model_name: str = "ipex-llm-amd", loop_thread: Optional[EngineLoop] = None,
+              asr=None):
+    """``asr``: a :class:`serving.asr.WhisperTranscriber` serving
+    ``/v1/audio/transcriptions`` (501 without one)."""
+    from fastapi import FastAPI, HTTPException, Request
     from fastapi.middleware.cors import CORSMiddleware
     from fastapi.responses import JSONResponse, StreamingResponse
 
@@ -271,9 +274,38 @@ def build_app(engine: LLMEngine, tokenizer, model_name: str = "ipex-llm-amd", lo
                          req.repetition_penalty, seed=req.seed, default_max=16)
         return await _openai(ids, params, req.stream, False)
 
-    @app.post("/v1/audio/transcriptions")
-    async def transcriptions():
-        raise HTTPException(status_code=501, detail="speech models are not served by this build")
+    async def transcriptions(request):
+        # reference SRC/serving/fastapi/api_server.py:404-428: multipart upload
+        # (file, model, language, prompt, response_format) -> {"text": ...}
+        if asr is None:
+            raise HTTPException(status_code=501, detail="no speech model loaded (start with --asr-model)")
+        from fastapi.responses import PlainTextResponse
+        from .asr import decode_wav, parse_multipart, srt_or_vtt
+        try:
+            form = parse_multipart(await request.body(), request.headers.get("content-type", ""))
+            f = form.get("file")
+            if not isinstance(f, tuple):
+                raise ValueError("missing 'file' upload")
+            audio, sr = decode_wav(f[1])
+        except ValueError as e:
+            raise HTTPException(status_code=400, detail=str(e))
+        lang = form.get("language") or None
+        fmt = form.get("response_format") or "json"
+        try:
+            text = await asyncio.get_running_loop().run_in_executor(
+                None, lambda: asr.transcribe(audio, sr, lang, form.get("prompt") or None))
+        except ValueError as e:
+            raise HTTPException(status_code=400, detail=str(e))
+        if fmt == "text":
+            return PlainTextResponse(text)
+        if fmt in ("srt", "vtt"):
+            return PlainTextResponse(srt_or_vtt(text, fmt, len(audio) / sr))
+        if fmt == "verbose_json":
+            return {"task": "transcribe", "language": lang, "duration": len(audio) / sr, "text": text}
+        return {"text": text}
+
+    transcriptions.__annotations__["request"] = Request     # (postponed annotations: give FastAPI the class)
+    app.post("/v1/audio/transcriptions")(transcriptions)
 
     app.state.engine = engine
     app.state.runner = state["runner"]
@@ -283,12 +315,13 @@ def build_app(engine: LLMEngine, tokenizer, model_name: str = "ipex-llm-amd", lo
 class FastApp:
     """Reference-compatible wrapper: ``FastApp(model, tokenizer).app``."""
 
-    def __init__(self, model, tokenizer, max_batch: int = 32, max_model_len: int = 4096, **kw):
+    def __init__(self, model, tokenizer, max_batch: int = 32, max_model_len: int = 4096, asr=None, **kw):
         from ..transformers.hf_native import get_native
         native = get_native(model)[0] if not hasattr(model, "forward_tokens") else model
         eos = getattr(tokenizer, "eos_token_id", None)
         self.engine = LLMEngine(native, max_batch=max_batch, max_model_len=max_model_len, eos_token_id=eos, **kw)
-        self.app = build_app(self.engine, tokenizer, getattr(getattr(model, "config", None), "_name_or_path", "model"))
+        self.app = build_app(self.engine, tokenizer, getattr(getattr(model, "config", None), "_name_or_path", "model"),
+                             asr=asr)
 
 
 def main(argv=None):
@@ -301,6 +334,7 @@ def main(argv=None):
     ap.add_argument("--max-batch", type=int, default=64)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--asr-model", default=None, help="Whisper checkpoint served at /v1/audio/transcriptions")
     a = ap.parse_args(argv)
     import torch
     import uvicorn
@@ -312,7 +346,11 @@ def main(argv=None):
         model = AutoModelForCausalLM.from_pretrained(a.model, load_in_low_bit=a.low_bit, torch_dtype=torch.bfloat16)
     model = model.to(a.device)
     tok = AutoTokenizer.from_pretrained(a.model)
-    fa = FastApp(model, tok, max_batch=a.max_batch, max_model_len=a.max_model_len)
+    asr = None
+    if a.asr_model:
+        from .asr import WhisperTranscriber
+        asr = WhisperTranscriber.from_pretrained(a.asr_model, a.low_bit, a.device)
+    fa = FastApp(model, tok, max_batch=a.max_batch, max_model_len=a.max_model_len, asr=asr)
     uvicorn.run(fa.app, host=a.host, port=a.port)
 
 
