@@ -108,9 +108,15 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         def run(so):
             src, obj = so
             cmd = _cmd(src, obj)
+            t_start = time.time()
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+            # stamp the object with the compile START time: a source or header
+            # edited while it compiled is then newer and rebuilds next time
+            # (otherwise a stale object -- possibly with an older struct layout
+            # than its neighbours -- would look up to date)
+            os.utime(obj, (t_start, t_start))
             if verbose:
                 print(f"[build] {os.path.relpath(src, ROOT)}", flush=True)
             return src

@@ -1,0 +1,21 @@
+// Host-callable launcher of the 8-phase 256x256 bf16 GEMM (gemm_8p.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace illm {
+
+struct G8Args {
+  const uint16_t* x;      // [M, ldx] bf16
+  const uint16_t* w;      // [N, ldw] bf16
+  const uint16_t* bias;   // [N] bf16 or null
+  void* out;              // [M, ldo] bf16 or f32
+  int M, N, K;            // K % 64 == 0
+  int ldx, ldw, ldo;
+  int out_f32;
+  uint32_t x_bytes, w_bytes;   // buffer extents (reads past them return 0)
+};
+
+void launch_gemm8p(const G8Args& a, hipStream_t st);
+
+}  // namespace illm

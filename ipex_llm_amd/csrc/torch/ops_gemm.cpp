@@ -8,6 +8,7 @@
 #include "../common/formats.h"
 #include "../hip/kernels.h"
 #include "../hip/kernels_train.h"
+#include "../hip/kernels_g8.h"
 
 using at::Tensor;
 
@@ -335,9 +336,50 @@ std::vector<Tensor> x_to_f16_rowscale(const Tensor& x) {
 
 }  // namespace
 
+// dense bf16 NT GEMM on the 8-phase 256 x 256 kernel (gemm_8p.hip):
+// y[M, N] = x[M, K] @ w[N, K]^T (+ bias), bf16 or f32 out; K % 64 == 0
+Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool out_f32) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
+              "gemm_bf16: bf16 GPU tensors");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1, "gemm_bf16: w must be [N, K] with unit inner stride");
+  const int64_t K = w.size(1), N = w.size(0);
+  TORCH_CHECK(x.size(-1) == K && K % 64 == 0 && K > 0, "gemm_bf16: K must match and be a multiple of 64");
+  c10::DeviceGuard g(x.device());
+  Tensor x2 = x.reshape({-1, K});
+  if (x2.stride(1) != 1 || x2.stride(0) % 8 != 0) x2 = x2.contiguous();
+  const int64_t M = x2.size(0);
+  auto shape = x.sizes().vec();
+  shape.back() = N;
+  Tensor out = at::empty({M, N}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  if (M == 0 || N == 0) return out.view(shape);
+  TORCH_CHECK(w.stride(0) % 8 == 0, "gemm_bf16: w row stride must be a multiple of 8 elements");
+  const int64_t xb = (M - 1) * x2.stride(0) * 2 + K * 2, wb = (N - 1) * w.stride(0) * 2 + K * 2;
+  TORCH_CHECK(xb < (int64_t)UINT32_MAX && wb < (int64_t)UINT32_MAX, "gemm_bf16: operands over 4 GiB");
+  if (bias.has_value())
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 && bias->numel() == N && bias->is_contiguous(),
+                "gemm_bf16: bias bf16 [N]");
+  illm::G8Args a{};
+  a.x = (const uint16_t*)x2.data_ptr();
+  a.w = (const uint16_t*)w.data_ptr();
+  a.bias = bias.has_value() ? (const uint16_t*)bias->data_ptr() : nullptr;
+  a.out = out.data_ptr();
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.ldx = (int)x2.stride(0);
+  a.ldw = (int)w.stride(0);
+  a.ldo = (int)N;
+  a.out_f32 = out_f32 ? 1 : 0;
+  a.x_bytes = (uint32_t)xb;
+  a.w_bytes = (uint32_t)wb;
+  illm::launch_gemm8p(a, at::hip::getCurrentHIPStream().stream());
+  return out.view(shape);
+}
+
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("mfgemm(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias=None, bool glu=False, int act=0, int tile=-1, int ksplit=0) -> Tensor");
   m.def("x_to_f16_rowscale(Tensor x) -> Tensor[]");
+  m.def("gemm_bf16(Tensor x, Tensor w, Tensor? bias=None, bool out_f32=False) -> Tensor");
   m.def("mfgemm_nn(Tensor g, Tensor w, int fmt, int n, int k, int tile=-1, int ksplit=0) -> Tensor");
   m.def("mfgemm_lora(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias, Tensor la, Tensor lb, float s) -> Tensor[]");
   m.def("mfgemm_nn_lora(Tensor g, Tensor w, int fmt, int n, int k, Tensor la, Tensor lb, float s) -> Tensor[]");
@@ -346,6 +388,7 @@ TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("mfgemm", &mfgemm);
   m.impl("x_to_f16_rowscale", &x_to_f16_rowscale);
+  m.impl("gemm_bf16", &gemm_bf16);
   m.impl("mfgemm_nn", &mfgemm_nn);
   m.impl("mfgemm_lora", &mfgemm_lora);
   m.impl("mfgemm_nn_lora", &mfgemm_nn_lora);

@@ -297,3 +297,10 @@ def _(g, w, fmt, n, k, la, lb, s):
     M = g.numel() // n
     rp = (la.shape[0] + 31) // 32 * 32
     return [g.new_empty(shape), g.new_empty((M, rp))]
+
+
+@register_fake("ipex_llm_amd::gemm_bf16")
+def _(x, w, bias=None, out_f32=False):
+    shape = list(x.shape)
+    shape[-1] = w.shape[0]
+    return x.new_empty(shape, dtype=torch.float32 if out_f32 else x.dtype)

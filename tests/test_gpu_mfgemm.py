@@ -41,7 +41,7 @@ def test_mfgemm_shapes_and_split_k(cuda, M, ksplit):
     blob = ops.quantize(torch.randn(n, k, device=cuda) * 0.05, f)
     x = torch.randn(M, k, device=cuda).bfloat16()
     bias = torch.randn(n, device=cuda).bfloat16()
-    ref = R.lowbit_linear_ref(x, blob.cpu(), f, n, k, bias=bias.cpu()).to(cuda)
+    ref = R.lowbit_linear_ref(x, blob.cpu(), f, n, k, bias=bias).to(cuda)
     y = torch.ops.ipex_llm_amd.mfgemm(x, blob, f, n, k, bias, False, 0, -1, ksplit)
     assert _rel(y, ref) < 5e-3, (M, ksplit)
 
