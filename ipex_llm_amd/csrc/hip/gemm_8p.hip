@@ -29,6 +29,10 @@
 //     group land on 16 distinct bank slots;
 //   * out = C^T orientation (w rows are the MFMA A operand), so a lane holds
 //     4 consecutive output columns of one row: 8-byte stores;
+//   * the two wave-rows run STAGGERED by one barrier (wave-row 1 enters the
+//     loop one barrier late): on every SIMD one wave issues its MFMA cluster
+//     while the other reads fragments / issues DMA, so the matrix pipe does
+//     not idle through the read-and-wait half of each phase;
 //   * XCD-aware block order (bijective remap) with 4 m-blocks per group, so
 //     concurrently running blocks of one XCD share x and w panels in its L2.
 // All LDS lives in ONE __shared__ array (a second LDS object can make hipcc
@@ -36,6 +40,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../common/quant_block.h"
+#include "gemv_args.h"
 #include "illm_device.h"
 #include "kernels_g8.h"
 #include "mfg_common.h"
@@ -79,8 +85,47 @@ __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// LDS map.  Dense: [A buf0 | B buf0 | A buf1 | B buf1] (128 KB).  Low-bit:
+// [A buf0 | A buf1 | B (single) | codes ring 2 x 16 KB | scales ring 2 x 1 KB |
+//  LUT 2 KB] (132 KB) -- the B image is decoded just in time, so one buffer.
+template <int DK> struct G8Lds;
+template <> struct G8Lds<-1> {
+  static constexpr int A0 = 0, ASTR = BUFB, B0 = IMG, BSTR = BUFB, BYTES = LDS_BYTES;
+};
+template <int DK> struct G8Lds {
+  static constexpr int A0 = 0, ASTR = IMG, B0 = 2 * IMG, BSTR = 0;
+  static constexpr int CODES = 3 * IMG, SCALES = CODES + 2 * 16384, LUT = SCALES + 2 * 1024, BYTES = LUT + 2048;
+};
+
+// 8 weights of one 4-bit code dword -> 8 bf16 (one ds_write_b128 chunk).
+// INT4S nibble order = the pair order of lowbit_decode.h ((u >> 4 i) & 0x000F000F
+// = elements 2 i, 2 i + 1); (128 + q) from the bf16 exponent trick, then
+// (q - 8) d formed exactly in f32 and rounded once to bf16 -- bit-identical
+// to dequantize-to-bf16.  LUT4: byte j = elements 2 j (low nibble), 2 j + 1.
+template <int DK>
+__device__ __forceinline__ uint4 dec8_bf16(uint32_t u, float d, float md, const float2* lut) {
+  uint32_t o[4];
+  if constexpr (DK == DK_INT4S) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t q = ((u >> (4 * i)) & 0x000F000Fu) | 0x43004300u;
+      o[i] = pack2<BF16>(fmaf(__uint_as_float(q << 16), d, md), fmaf(__uint_as_float(q & 0xffff0000u), d, md));
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const float2 l = lut[(u >> (8 * j)) & 0xff];
+      o[j] = pack2<BF16>(l.x * d, l.y * d);
+    }
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+template <int DK>
 __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[LDS_BYTES];
+  constexpr bool DENSE = DK < 0;
+  using L = G8Lds<DK>;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[L::BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   const int g = lane >> 4, r16 = lane & 15;
@@ -110,20 +155,77 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       ar0[h][i] = a_row(h, q0);
       br0[h][i] = b_row(h, q0);
       xo[h][i] = ((uint32_t)(m0 + ra) * (uint32_t)a.ldx + 8u * (uint32_t)(c ^ ((ra >> 1) & 7))) * 2u;
-      wo[h][i] = ((uint32_t)(n0 + rb) * (uint32_t)a.ldw + 8u * (uint32_t)(c ^ ((rb >> 1) & 7))) * 2u;
+      wo[h][i] = DENSE ? ((uint32_t)(n0 + rb) * (uint32_t)a.ldw + 8u * (uint32_t)(c ^ ((rb >> 1) & 7))) * 2u : 0u;
     }
   const g8_rsrc rx = make_rsrc(a.x, a.x_bytes), rw = make_rsrc(a.w, a.w_bytes);
+  auto a_img = [&](int t) -> uint8_t* { return smem + L::A0 + (t & 1) * L::ASTR; };
+  auto b_img = [&](int t) -> uint8_t* { return smem + L::B0 + (t & 1) * L::BSTR; };
   auto stage_a = [&](int h, int t) {          // half-tile A_h of k-tile t -> buffer t & 1
     const int tt = min(t, T - 1);             // past the end: harmless reload (keeps the vmcnt count)
-    const uint8_t* img = smem + (t & 1) * BUFB;
+    const uint8_t* img = a_img(t);
 #pragma unroll
     for (int i = 0; i < 2; i++) dma16(rx, img + ar0[h][i] * ROWB, xo[h][i], tt * 128);
   };
-  auto stage_b = [&](int h, int t) {
+  auto stage_b = [&](int h, int t) {          // dense only
     const int tt = min(t, T - 1);
-    const uint8_t* img = smem + (t & 1) * BUFB + IMG;
+    const uint8_t* img = b_img(t);
 #pragma unroll
     for (int i = 0; i < 2; i++) dma16(rw, img + br0[h][i] * ROWB, wo[h][i], tt * 128);
+  };
+
+  // ---- low-bit B: codes / scales of 128-k chunk c staged into ring slot
+  // c & 1 (one 16-B DMA per lane each), decoded into the B image half h of
+  // k-tile t just in time (see the schedule at the loop)
+  const int KC = a.K / 128;
+  const int NTt = (a.N + 15) / 16;
+  const uint32_t TB = (uint32_t)(DENSE ? 0 : dk_tile_bytes(DK < 0 ? 0 : DK, KC));
+  // codes: wave w <-> block row-tile j = w of half h: rt = (w >> 1) * 4 + 2 h + (w & 1)
+  uint32_t co[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int rt = (wave >> 1) * 4 + 2 * h + (wave & 1);
+    co[h] = (uint32_t)min(n0 / 16 + rt, NTt - 1) * TB + (uint32_t)lane * 16u;
+  }
+  // scales: lane l <-> block row-tile l >> 2, 16-B piece l & 3 of its 64 B
+  const uint32_t so = (uint32_t)min(n0 / 16 + (lane >> 2), NTt - 1) * TB + (uint32_t)KC * 1024u +
+                      (uint32_t)(lane & 3) * 16u;
+  auto stage_codes = [&](int h, int c) {
+    if constexpr (!DENSE) {
+      const int cc = min(c, KC - 1);
+      dma16(rw, smem + L::CODES + (c & 1) * 16384 + h * 8192 + wave * 1024, co[h], cc * 1024);
+    }
+  };
+  auto stage_scales = [&](int c) {            // every wave loads the same 1 KB (uniform vmcnt)
+    if constexpr (!DENSE) {
+      const int cc = min(c, KC - 1);
+      dma16(rw, smem + L::SCALES + (c & 1) * 1024, so, cc * 64);
+    }
+  };
+  // decode half h of k-tile t: this thread's 16 weights = row (wave, r16) of
+  // the half, k 8 g .. 8 g + 7 and 32 + 8 g .. + 7 of the tile
+  uint2 cw = make_uint2(0u, 0u);
+  uint32_t sd = 0u;
+  auto dec_load = [&](int h, int t) {
+    if constexpr (!DENSE) {
+      const int c = t >> 1, kh = t & 1;
+      cw = *(const uint2*)(smem + L::CODES + (c & 1) * 16384 + h * 8192 + wave * 1024 + lane * 16 + kh * 8);
+      const int nl = (wave >> 1) * 64 + 32 * h + (wave & 1) * 16 + r16;
+      sd = *(const uint32_t*)(smem + L::SCALES + (c & 1) * 1024 + nl * 4);
+    }
+  };
+  auto dec_store = [&](int h, int t) {
+    if constexpr (!DENSE) {
+      const int kh = t & 1;
+      const float d = f16_to_f32((uint16_t)(kh ? (sd >> 16) : (sd & 0xffffu)));
+      const float md = DK == DK_INT4S ? -136.f * d : 0.f;
+      const float2* lut = (const float2*)(smem + (DENSE ? 0 : L::LUT));
+      const uint4 v0 = dec8_bf16<DK>(cw.x, d, md, lut), v1 = dec8_bf16<DK>(cw.y, d, md, lut);
+      const int R = (wave >> 1) * 64 + 32 * h + (wave & 1) * 16 + r16;
+      const int sw = (R >> 1) & 7;
+      uint8_t* row = b_img(0) + R * ROWB;
+      *(uint4*)(row + ((g ^ sw) & 7) * 16) = v0;
+      *(uint4*)(row + (((4 + g) ^ sw) & 7) * 16) = v1;
+    }
   };
 
   // ---- fragment read offsets: image row R + r16, logical chunk 4 s + g at
@@ -131,7 +233,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   const int sw = (r16 >> 1) & 7;
   const uint32_t fo0 = (uint32_t)r16 * ROWB + (uint32_t)((g ^ sw) & 7) * 16;
   const uint32_t fo1 = (uint32_t)r16 * ROWB + (uint32_t)(((4 + g) ^ sw) & 7) * 16;
-  const uint32_t a_base = (uint32_t)(wr * 128) * ROWB, b_base = IMG + (uint32_t)(wc * 64) * ROWB;
+  const uint32_t a_base = (uint32_t)(wr * 128) * ROWB, b_base = (uint32_t)(wc * 64) * ROWB;
 
   f32x4 acc[4][8];                            // [n-tile][m-tile], C^T tiles
 #pragma unroll
@@ -140,18 +242,18 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
     for (int mt = 0; mt < 8; mt++) acc[nt][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint4 fa0[4][2], fa1[4][2], fb[2][2];       // A (m) halves, B (n) half; [tile][k-step]
 
-  auto read_a = [&](uint4 (&f)[4][2], const uint8_t* buf, int mh) {
+  auto read_a = [&](uint4 (&f)[4][2], const uint8_t* img, int mh) {
 #pragma unroll
     for (int mt = 0; mt < 4; mt++) {
-      const uint8_t* p = buf + a_base + (uint32_t)(mh * 64 + mt * 16) * ROWB;
+      const uint8_t* p = img + a_base + (uint32_t)(mh * 64 + mt * 16) * ROWB;
       f[mt][0] = *(const uint4*)(p + fo0);
       f[mt][1] = *(const uint4*)(p + fo1);
     }
   };
-  auto read_b = [&](const uint8_t* buf, int nh) {
+  auto read_b = [&](const uint8_t* img, int nh) {
 #pragma unroll
     for (int nt = 0; nt < 2; nt++) {
-      const uint8_t* p = buf + b_base + (uint32_t)(nh * 32 + nt * 16) * ROWB;
+      const uint8_t* p = img + b_base + (uint32_t)(nh * 32 + nt * 16) * ROWB;
       fb[nt][0] = *(const uint4*)(p + fo0);
       fb[nt][1] = *(const uint4*)(p + fo1);
     }
@@ -168,49 +270,133 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // ---- prologue: tile 0 complete, tile 1's A0 / B0 in flight
-  stage_a(0, 0);
-  stage_b(0, 0);
-  stage_a(1, 0);
-  stage_b(1, 0);
-  stage_a(0, 1);
-  stage_b(0, 1);
-  wait_vm8();                                  // A0(0), B0(0) landed
-  barrier();
-
-  for (int u = 0; u < T; u++) {
-    const uint8_t* buf = smem + (u & 1) * BUFB;
-    // phase 0: (mh0, nh0)
-    read_a(fa0, buf, 0);
-    read_b(buf, 0);
-    stage_a(1, u + 1);
-    wait_vm8();
+  if constexpr (DENSE) {
+    // ---- prologue: tile 0 complete, tile 1's A0 / B0 in flight
+    stage_a(0, 0);
+    stage_b(0, 0);
+    stage_a(1, 0);
+    stage_b(1, 0);
+    stage_a(0, 1);
+    stage_b(0, 1);
+    wait_vm8();                                  // A0(0), B0(0) landed
     barrier();
+    if (wr == 1) barrier();                      // stagger: wave-row 1 runs half a phase behind
+    for (int u = 0; u < T; u++) {
+      const uint8_t* ai = a_img(u);
+      const uint8_t* bi = b_img(u);
+      // phase 0: (mh0, nh0)
+      read_a(fa0, ai, 0);
+      read_b(bi, 0);
+      stage_a(1, u + 1);
+      wait_vm8();
+      barrier();
+      wait_lgkm0();
+      mma(fa0, 0, 0);
+      barrier();
+      // phase 1: (mh1, nh0)
+      read_a(fa1, ai, 1);
+      stage_b(1, u + 1);
+      wait_vm8();
+      barrier();
+      wait_lgkm0();
+      mma(fa1, 1, 0);
+      barrier();
+      // phase 2: (mh0, nh1)
+      read_b(bi, 1);
+      stage_a(0, u + 2);
+      wait_vm8();
+      barrier();
+      wait_lgkm0();
+      mma(fa0, 0, 1);
+      barrier();
+      // phase 3: (mh1, nh1)
+      stage_b(0, u + 2);
+      wait_vm8();
+      barrier();
+      mma(fa1, 1, 1);
+      barrier();
+    }
+    if (wr == 0) barrier();                      // close the stagger
+  } else {
+    // ---- low-bit schedule (global phase P = 4 t + p; chunk c = k-tiles 2c, 2c+1):
+    //   p0: frags A(mh0) B(nh0);               DMA A1(t+1)
+    //   p1: frags A(mh1); decode B0(t+1);      DMA t even: scales(t/2+1) again, t odd: scales((t+3)/2)
+    //   p2: frags B(nh1);                      DMA A0(t+2)
+    //   p3: decode B1(t+1);                    DMA t even: codes0(t/2+2), t odd: codes1((t+3)/2)
+    // -> every 4 consecutive phases issue 6 DMAs per lane: vmcnt(6) each
+    // phase keeps exactly the last 4 phases' stages in flight; every code /
+    // scale stage lands >= 5 phases before its first decode and is re-staged
+    // >= 2 phases after its last.  A decode writes its B-image half after the
+    // phase's first barrier, one phase after that half's last read and two
+    // phases before its next read, so the single B image is race-free even
+    // with the two wave-rows staggered by a barrier.
+    if constexpr (DK == DK_LUT4) {
+      if (tid < 256) {
+        const float2 v = make_float2(hd_lut4(a.lut_fmt, tid & 15), hd_lut4(a.lut_fmt, tid >> 4));
+        *(float2*)(smem + L::LUT + tid * 8) = v;
+      }
+    }
+    stage_codes(0, 0);
+    stage_codes(1, 0);
+    stage_scales(0);
+    stage_a(0, 0);
+    stage_a(1, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier();
+    dec_load(0, 0);
+    dec_store(0, 0);                             // B0, B1 of tile 0
+    dec_load(1, 0);
+    dec_store(1, 0);
+    stage_codes(0, 1);
+    stage_scales(1);
+    stage_a(0, 1);
+    stage_codes(1, 1);
     wait_lgkm0();
-    mma(fa0, 0, 0);
     barrier();
-    // phase 1: (mh1, nh0)
-    read_a(fa1, buf, 1);
-    stage_b(1, u + 1);
-    wait_vm8();
-    barrier();
-    wait_lgkm0();
-    mma(fa1, 1, 0);
-    barrier();
-    // phase 2: (mh0, nh1)
-    read_b(buf, 1);
-    stage_a(0, u + 2);
-    wait_vm8();
-    barrier();
-    wait_lgkm0();
-    mma(fa0, 0, 1);
-    barrier();
-    // phase 3: (mh1, nh1)
-    stage_b(0, u + 2);
-    wait_vm8();
-    barrier();
-    mma(fa1, 1, 1);
-    barrier();
+    if (wr == 1) barrier();                      // stagger: wave-row 1 runs half a phase behind
+    for (int u = 0; u < T; u++) {
+      const uint8_t* ai = a_img(u);
+      const uint8_t* bi = b_img(u);
+      const bool odd = u & 1;
+      // phase 0
+      read_a(fa0, ai, 0);
+      read_b(bi, 0);
+      stage_a(1, u + 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      barrier();
+      wait_lgkm0();
+      mma(fa0, 0, 0);
+      barrier();
+      // phase 1
+      read_a(fa1, ai, 1);
+      dec_load(0, u + 1);
+      stage_scales(odd ? (u + 3) >> 1 : (u >> 1) + 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      barrier();
+      wait_lgkm0();
+      mma(fa1, 1, 0);
+      if (u + 1 < T) dec_store(0, u + 1);
+      barrier();
+      // phase 2
+      read_b(bi, 1);
+      stage_a(0, u + 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      barrier();
+      wait_lgkm0();
+      mma(fa0, 0, 1);
+      barrier();
+      // phase 3
+      dec_load(1, u + 1);
+      if (odd) stage_codes(1, (u + 3) >> 1);
+      else stage_codes(0, (u >> 1) + 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      barrier();
+      wait_lgkm0();
+      mma(fa1, 1, 1);
+      if (u + 1 < T) dec_store(1, u + 1);
+      barrier();
+    }
+    if (wr == 0) barrier();                      // close the stagger
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's reloads
 
@@ -252,7 +438,12 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
 
 void launch_gemm8p(const G8Args& a, hipStream_t st) {
   const int MB = (a.M + 255) / 256, NB = (a.N + 255) / 256;
-  hipLaunchKernelGGL(g8::gemm8p_kernel, dim3((unsigned)(MB * NB)), dim3(512), 0, st, a);
+  const dim3 grid((unsigned)(MB * NB)), blk(512);
+  if (a.w_fmt < 0) hipLaunchKernelGGL(g8::gemm8p_kernel<-1>, grid, blk, 0, st, a);
+  else if (fmt_to_dk(a.w_fmt) == DK_INT4S) hipLaunchKernelGGL(g8::gemm8p_kernel<DK_INT4S>, grid, blk, 0, st, a);
+  else hipLaunchKernelGGL(g8::gemm8p_kernel<DK_LUT4>, grid, blk, 0, st, a);
 }
+
+bool gemm8p_supports(int fmt) { return fmt < 0 || fmt_to_dk(fmt) == DK_INT4S || fmt_to_dk(fmt) == DK_LUT4; }
 
 }  // namespace illm

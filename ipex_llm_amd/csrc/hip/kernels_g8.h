@@ -14,8 +14,11 @@ struct G8Args {
   int ldx, ldw, ldo;
   int out_f32;
   uint32_t x_bytes, w_bytes;   // buffer extents (reads past them return 0)
+  int w_fmt;              // -1: dense bf16 w; else a low-bit device-blob format (gemm8p_supports)
+  int lut_fmt;            // LUT formats: the code table (FMT_NF4 / FMT_NF3)
 };
 
 void launch_gemm8p(const G8Args& a, hipStream_t st);
+bool gemm8p_supports(int fmt);
 
 }  // namespace illm

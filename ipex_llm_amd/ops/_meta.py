@@ -304,3 +304,10 @@ def _(x, w, bias=None, out_f32=False):
     shape = list(x.shape)
     shape[-1] = w.shape[0]
     return x.new_empty(shape, dtype=torch.float32 if out_f32 else x.dtype)
+
+
+@register_fake("ipex_llm_amd::gemm8p_lowbit")
+def _(x, blob, fmt, n, k, bias=None, out_f32=False):
+    shape = list(x.shape)
+    shape[-1] = n
+    return x.new_empty(shape, dtype=torch.float32 if out_f32 else x.dtype)

@@ -36,3 +36,24 @@ def test_gemm_bf16_bias_f32_out_strided(cuda):
     # repeated calls are deterministic (no race in the LDS-DMA pipeline)
     y2 = torch.ops.ipex_llm_amd.gemm_bf16(x, w, b, True)
     assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("qtype", ["sym_int4", "nf4"])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (100, 520, 384), (1024, 4096, 4096), (3000, 1040, 1024)])
+def test_gemm8p_lowbit_matches_dequant_fp32(cuda, qtype, M, N, K):
+    """weights decoded to bf16 inside the GEMM == dequantize + fp32 matmul"""
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.ops import reference as R
+    from ipex_llm_amd.quantize import get_format
+    f = get_format(qtype).fmt
+    torch.manual_seed(M + K)
+    blob = ops.quantize(torch.randn(N, K, device=cuda) * 0.05, f)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    ref = R.lowbit_linear_ref(x, blob.cpu(), f, N, K, bias=b).to(cuda)
+    y = torch.ops.ipex_llm_amd.gemm8p_lowbit(x, blob, f, N, K, b)
+    assert y.shape == (M, N) and torch.isfinite(y.float()).all()
+    assert _rel(y, ref) < 6e-3, (qtype, M, N, K)
+    # bit-identical to dequantize-to-bf16 + the dense kernel (same bf16 weights, same order)
+    wd = torch.ops.ipex_llm_amd.dequantize_device(blob, f, N, K, torch.bfloat16)
+    assert torch.equal(y, torch.ops.ipex_llm_amd.gemm_bf16(x, wd, b))
