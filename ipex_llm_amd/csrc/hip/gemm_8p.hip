@@ -92,6 +92,7 @@ template <int DK> struct G8Lds;
 template <> struct G8Lds<-1> {
   static constexpr int A0 = 0, ASTR = BUFB, B0 = IMG, BSTR = BUFB, BYTES = LDS_BYTES;
 };
+template <> struct G8Lds<-2> : G8Lds<-1> {};     // fp8: the dense layout, 128 k per 128-B row
 template <int DK> struct G8Lds {
   static constexpr int A0 = 0, ASTR = IMG, B0 = 2 * IMG, BSTR = 0;
   static constexpr int CODES = 3 * IMG, SCALES = CODES + 2 * 16384, LUT = SCALES + 2 * 1024, BYTES = LUT + 2048;
@@ -121,9 +122,12 @@ __device__ __forceinline__ uint4 dec8_bf16(uint32_t u, float d, float md, const 
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+typedef int32_t g8_i32x8 __attribute__((ext_vector_type(8)));
+
 template <int DK>
 __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
-  constexpr bool DENSE = DK < 0;
+  constexpr bool DENSE = DK < 0;          // both operands staged by LDS-DMA (bf16 or fp8)
+  constexpr bool FP8 = DK == G8_FP8;      // 128 k per K-tile, 16x16x128 block-scaled fp8 MFMA
   using L = G8Lds<DK>;
   __shared__ __attribute__((aligned(1024))) uint8_t smem[L::BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -140,7 +144,8 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   const int gm = min(GM, MB - grp * GM);
   const int mb = grp * GM + rem % gm, nb = rem / gm;
   const int m0 = mb * 256, n0 = nb * 256;
-  const int T = a.K / 64;
+  const int T = FP8 ? a.K / 128 : a.K / 64;
+  constexpr int ES = FP8 ? 1 : 2;         // element bytes
 
   // ---- per-lane LDS-DMA source offsets (bytes; + k-tile via soff) for the
   // two 16-B pieces of each half-tile, and the wave-uniform LDS row bases
@@ -154,8 +159,8 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       const int ra = a_row(h, q), rb = b_row(h, q);
       ar0[h][i] = a_row(h, q0);
       br0[h][i] = b_row(h, q0);
-      xo[h][i] = ((uint32_t)(m0 + ra) * (uint32_t)a.ldx + 8u * (uint32_t)(c ^ ((ra >> 1) & 7))) * 2u;
-      wo[h][i] = DENSE ? ((uint32_t)(n0 + rb) * (uint32_t)a.ldw + 8u * (uint32_t)(c ^ ((rb >> 1) & 7))) * 2u : 0u;
+      xo[h][i] = (uint32_t)(m0 + ra) * (uint32_t)a.ldx * ES + 16u * (uint32_t)(c ^ ((ra >> 1) & 7));
+      wo[h][i] = DENSE ? (uint32_t)(n0 + rb) * (uint32_t)a.ldw * ES + 16u * (uint32_t)(c ^ ((rb >> 1) & 7)) : 0u;
     }
   const g8_rsrc rx = make_rsrc(a.x, a.x_bytes), rw = make_rsrc(a.w, a.w_bytes);
   auto a_img = [&](int t) -> uint8_t* { return smem + L::A0 + (t & 1) * L::ASTR; };
@@ -231,8 +236,10 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   // ---- fragment read offsets: image row R + r16, logical chunk 4 s + g at
   // physical chunk (4 s + g) ^ ((r16 >> 1) & 7)
   const int sw = (r16 >> 1) & 7;
-  const uint32_t fo0 = (uint32_t)r16 * ROWB + (uint32_t)((g ^ sw) & 7) * 16;
-  const uint32_t fo1 = (uint32_t)r16 * ROWB + (uint32_t)(((4 + g) ^ sw) & 7) * 16;
+  // (fp8: the lane's 32-byte fragment = logical chunks 2 g, 2 g + 1)
+  const int c0 = FP8 ? 2 * g : g, c1 = FP8 ? 2 * g + 1 : 4 + g;
+  const uint32_t fo0 = (uint32_t)r16 * ROWB + (uint32_t)((c0 ^ sw) & 7) * 16;
+  const uint32_t fo1 = (uint32_t)r16 * ROWB + (uint32_t)((c1 ^ sw) & 7) * 16;
   const uint32_t a_base = (uint32_t)(wr * 128) * ROWB, b_base = (uint32_t)(wc * 64) * ROWB;
 
   f32x4 acc[4][8];                            // [n-tile][m-tile], C^T tiles
@@ -260,13 +267,33 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   };
   auto mma = [&](const uint4 (&f)[4][2], int mh, int nh) {
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (FP8) {
 #pragma unroll
-    for (int s = 0; s < 2; s++)
+      for (int nt = 0; nt < 2; nt++) {
+        const g8_i32x8 wb = {(int)fb[nt][0].x, (int)fb[nt][0].y, (int)fb[nt][0].z, (int)fb[nt][0].w,
+                             (int)fb[nt][1].x, (int)fb[nt][1].y, (int)fb[nt][1].z, (int)fb[nt][1].w};
 #pragma unroll
-      for (int nt = 0; nt < 2; nt++)
+        for (int mt = 0; mt < 4; mt++) {
+          const g8_i32x8 xa = {(int)f[mt][0].x, (int)f[mt][0].y, (int)f[mt][0].z, (int)f[mt][0].w,
+                               (int)f[mt][1].x, (int)f[mt][1].y, (int)f[mt][1].z, (int)f[mt][1].w};
+          // unit E8M0 block scales (127): the row / column scales go to the epilogue
+          if (a.w_e5m2)
+            acc[nh * 2 + nt][mh * 4 + mt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                wb, xa, acc[nh * 2 + nt][mh * 4 + mt], 1, 0, 0, 127, 0, 127);
+          else
+            acc[nh * 2 + nt][mh * 4 + mt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                wb, xa, acc[nh * 2 + nt][mh * 4 + mt], 0, 0, 0, 127, 0, 127);
+        }
+      }
+    } else {
 #pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-          acc[nh * 2 + nt][mh * 4 + mt] = mfma16<BF16>(fb[nt][s], f[mt][s], acc[nh * 2 + nt][mh * 4 + mt]);
+      for (int s = 0; s < 2; s++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+          for (int mt = 0; mt < 4; mt++)
+            acc[nh * 2 + nt][mh * 4 + mt] = mfma16<BF16>(fb[nt][s], f[mt][s], acc[nh * 2 + nt][mh * 4 + mt]);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -401,20 +428,60 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's reloads
 
   // ---- epilogue: lane holds out[m][n .. n + 3], m = m-tile row r16, n = 4 g
+  if (a.glu) {
+    // w tiles alternate gate / up every 16 rows (the wave's 64 rows = 2
+    // pairs): act(gate) * up in f32, one rounding, out column = pair * 16 + 4 g + i
+    const int I = a.N / 2;
+#pragma unroll
+    for (int pr = 0; pr < 2; pr++) {
+      const int c0 = ((n0 + wc * 64) / 32 + pr) * 16 + 4 * g;
+      if (c0 >= I) continue;
+#pragma unroll
+      for (int mt = 0; mt < 8; mt++) {
+        const int m = m0 + wr * 128 + mt * 16 + r16;
+        if (m >= a.M) continue;
+        float o[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const float gv = acc[2 * pr][mt][i], uv = acc[2 * pr + 1][mt][i];
+          o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
+        }
+        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + c0;
+        if (c0 + 3 < I && ((a.ldo | c0) & 3) == 0) *(uint2*)y = make_uint2(pack2<BF16>(o[0], o[1]), pack2<BF16>(o[2], o[3]));
+        else for (int i = 0; i < 4 && c0 + i < I; i++) y[i] = from_f32<BF16>(o[i]);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int nt = 0; nt < 4; nt++) {
     const int n = n0 + wc * 64 + nt * 16 + 4 * g;
     if (n >= a.N) continue;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    float bv[4] = {0.f, 0.f, 0.f, 0.f}, cs[4] = {1.f, 1.f, 1.f, 1.f};
     if (a.bias != nullptr)
 #pragma unroll
-      for (int i = 0; i < 4; i++) bv[i] = n + i < a.N ? bf16_to_f32(a.bias[n + i]) : 0.f;
+      for (int i = 0; i < 4; i++)
+        bv[i] = n + i < a.N ? (a.out_f16 ? f16_to_f32(a.bias[n + i]) : bf16_to_f32(a.bias[n + i])) : 0.f;
+    if constexpr (FP8) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) cs[i] = a.sw_per_channel ? (n + i < a.N ? a.sw[n + i] : 0.f) : a.sw[0];
+    }
 #pragma unroll
     for (int mt = 0; mt < 8; mt++) {
       const int m = m0 + wr * 128 + mt * 16 + r16;
       if (m >= a.M) continue;
-      const float o0 = acc[nt][mt][0] + bv[0], o1 = acc[nt][mt][1] + bv[1];
-      const float o2 = acc[nt][mt][2] + bv[2], o3 = acc[nt][mt][3] + bv[3];
+      const float rsx = FP8 ? a.sx[m] : 1.f;
+      const float o0 = acc[nt][mt][0] * rsx * cs[0] + bv[0], o1 = acc[nt][mt][1] * rsx * cs[1] + bv[1];
+      const float o2 = acc[nt][mt][2] * rsx * cs[2] + bv[2], o3 = acc[nt][mt][3] * rsx * cs[3] + bv[3];
+      if (FP8 && a.out_f16) {
+        uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n;
+        if (n + 3 < a.N && ((a.ldo | n) & 3) == 0) *(uint2*)y = make_uint2(pack2<F16>(o0, o1), pack2<F16>(o2, o3));
+        else {
+          const float o[4] = {o0, o1, o2, o3};
+          for (int i = 0; i < 4 && n + i < a.N; i++) y[i] = from_f32<F16>(o[i]);
+        }
+        continue;
+      }
       if (a.out_f32) {
         float* y = (float*)a.out + (size_t)m * a.ldo + n;
         if (n + 3 < a.N && ((a.ldo | n) & 3) == 0) *(float4*)y = make_float4(o0, o1, o2, o3);
@@ -439,11 +506,12 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
 void launch_gemm8p(const G8Args& a, hipStream_t st) {
   const int MB = (a.M + 255) / 256, NB = (a.N + 255) / 256;
   const dim3 grid((unsigned)(MB * NB)), blk(512);
-  if (a.w_fmt < 0) hipLaunchKernelGGL(g8::gemm8p_kernel<-1>, grid, blk, 0, st, a);
+  if (a.w_fmt == G8_FP8) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8>, grid, blk, 0, st, a);
+  else if (a.w_fmt < 0) hipLaunchKernelGGL(g8::gemm8p_kernel<-1>, grid, blk, 0, st, a);
   else if (fmt_to_dk(a.w_fmt) == DK_INT4S) hipLaunchKernelGGL(g8::gemm8p_kernel<DK_INT4S>, grid, blk, 0, st, a);
   else hipLaunchKernelGGL(g8::gemm8p_kernel<DK_LUT4>, grid, blk, 0, st, a);
 }
 
-bool gemm8p_supports(int fmt) { return fmt < 0 || fmt_to_dk(fmt) == DK_INT4S || fmt_to_dk(fmt) == DK_LUT4; }
+bool gemm8p_supports(int fmt) { return fmt == -1 || fmt_to_dk(fmt) == DK_INT4S || fmt_to_dk(fmt) == DK_LUT4; }
 
 }  // namespace illm

@@ -16,7 +16,14 @@ struct G8Args {
   uint32_t x_bytes, w_bytes;   // buffer extents (reads past them return 0)
   int w_fmt;              // -1: dense bf16 w; else a low-bit device-blob format (gemm8p_supports)
   int lut_fmt;            // LUT formats: the code table (FMT_NF4 / FMT_NF3)
+  int glu, act;           // glu: w rows are 16-row gate/up tile pairs, out [M, N/2] = act(gate) * up
+  // fp8 (w_fmt == G8_FP8): x = e4m3 bytes [M, ldx], w = e4m3 / e5m2 bytes [N, ldw],
+  // y = sx[m] * sw[n] * (xq . wq) (+ bias), 16-bit out (bf16, or f16 if out_f16)
+  const float* sx;
+  const float* sw;
+  int sw_per_channel, w_e5m2, out_f16;
 };
+constexpr int G8_FP8 = -2;
 
 void launch_gemm8p(const G8Args& a, hipStream_t st);
 bool gemm8p_supports(int fmt);

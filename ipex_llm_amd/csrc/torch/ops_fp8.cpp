@@ -12,6 +12,7 @@
 #include <torch/library.h>
 
 #include "../hip/kernels.h"
+#include "../hip/kernels_g8.h"
 
 using at::Tensor;
 
@@ -68,6 +69,56 @@ Tensor fp8_linear_cpu(const Tensor& x, const Tensor& w, const Tensor& w_scale, c
   return y.to(x.scalar_type()).view(shape);
 }
 
+// the 8-phase 256 x 256 GEMM (gemm_8p.hip) on fp8 operands: 128 k per K-tile,
+// v_mfma_scale_f32_16x16x128_f8f6f4, row / column scales in the epilogue
+// (ILLM_FP8_8P=0: the older 128 x 128 kernel)
+static bool fp8_8p_on() {
+  static const bool on = [] {
+    const char* e = getenv("ILLM_FP8_8P");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
+static void launch_fp8_8p(const Tensor& xq, const Tensor& sx, const Tensor& w, const Tensor& ws, const Tensor& b,
+                          bool e5m2, Tensor& y) {
+  const int64_t M = xq.size(0), K = xq.size(1), N = w.size(0);
+  TORCH_CHECK(M * K < (int64_t)UINT32_MAX && N * K < (int64_t)UINT32_MAX, "fp8 8p: operands over 4 GiB");
+  illm::G8Args a{};
+  a.x = (const uint16_t*)xq.data_ptr();
+  a.w = (const uint16_t*)w.data_ptr();
+  a.bias = b.defined() ? (const uint16_t*)b.data_ptr() : nullptr;
+  a.out = y.data_ptr();
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.ldx = (int)K;
+  a.ldw = (int)K;
+  a.ldo = (int)N;
+  a.x_bytes = (uint32_t)(M * K);
+  a.w_bytes = (uint32_t)(N * K);
+  a.w_fmt = illm::G8_FP8;
+  a.sx = sx.data_ptr<float>();
+  a.sw = ws.data_ptr<float>();
+  a.sw_per_channel = ws.numel() == N ? 1 : 0;
+  a.w_e5m2 = e5m2 ? 1 : 0;
+  a.out_f16 = y.scalar_type() == at::kHalf ? 1 : 0;
+  illm::launch_gemm8p(a, at::hip::getCurrentHIPStream().stream());
+}
+
+// kernel-only entry for benchmarks: pre-quantized activations
+Tensor fp8_gemm8p(const Tensor& xq, const Tensor& sx, const Tensor& w, const Tensor& ws, bool e5m2) {
+  TORCH_CHECK(xq.is_cuda() && xq.dim() == 2 && xq.is_contiguous() && xq.element_size() == 1, "fp8_gemm8p: xq [M, K] bytes");
+  TORCH_CHECK(w.is_cuda() && w.dim() == 2 && w.is_contiguous() && w.size(1) == xq.size(1) && xq.size(1) % 128 == 0,
+              "fp8_gemm8p: w [N, K] bytes, K % 128 == 0");
+  TORCH_CHECK(sx.scalar_type() == at::kFloat && sx.numel() == xq.size(0) && ws.scalar_type() == at::kFloat,
+              "fp8_gemm8p: f32 scales");
+  c10::DeviceGuard g(xq.device());
+  Tensor y = at::empty({xq.size(0), w.size(0)}, xq.options().dtype(at::kBFloat16));
+  if (xq.size(0) > 0) launch_fp8_8p(xq, sx.contiguous(), w, ws.contiguous(), Tensor(), e5m2, y);
+  return y;
+}
+
 Tensor fp8_linear_hip(const Tensor& x, const Tensor& w, const Tensor& w_scale, const c10::optional<Tensor>& bias,
                       bool e5m2) {
   check_w(x, w, w_scale);
@@ -102,6 +153,11 @@ Tensor fp8_linear_hip(const Tensor& x, const Tensor& w, const Tensor& w_scale, c
     illm::launch_fp8_gemv(bf16, e5m2, a, st);
     return y.view(shape);
   }
+  if (K % 128 == 0 && M >= 256 && fp8_8p_on()) {
+    auto [xq, sx] = fp8_act_quant_hip(x2);
+    launch_fp8_8p(xq, sx, wc, ws, b, e5m2, y);
+    return y.view(shape);
+  }
   if (N % 128 == 0 && K % 128 == 0) {
     auto [xq, sx] = fp8_act_quant_hip(x2);
     a.xq = xq.data_ptr<uint8_t>();
@@ -121,6 +177,7 @@ Tensor fp8_linear_hip(const Tensor& x, const Tensor& w, const Tensor& w_scale, c
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("fp8_act_quant(Tensor x) -> (Tensor, Tensor)");
   m.def("fp8_linear(Tensor x, Tensor w, Tensor w_scale, Tensor? bias, bool e5m2) -> Tensor");
+  m.def("fp8_gemm8p(Tensor xq, Tensor sx, Tensor w, Tensor ws, bool e5m2) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
@@ -131,4 +188,5 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("fp8_act_quant", &fp8_act_quant_hip);
   m.impl("fp8_linear", &fp8_linear_hip);
+  m.impl("fp8_gemm8p", &fp8_gemm8p);
 }

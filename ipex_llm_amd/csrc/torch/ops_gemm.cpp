@@ -380,20 +380,22 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
 // low-bit weights (tiled device blob, sym_int4 / nf4 / nf3) decoded to bf16
 // in LDS inside the same 8-phase GEMM: y = x @ dequant(W)^T (+ bias)
 Tensor gemm8p_lowbit(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k,
-                     const c10::optional<Tensor>& bias, bool out_f32) {
+                     const c10::optional<Tensor>& bias, bool out_f32, bool glu, int64_t act) {
   TORCH_CHECK(x.is_cuda() && blob.is_cuda() && x.scalar_type() == at::kBFloat16, "gemm8p_lowbit: bf16 x on the GPU");
   TORCH_CHECK(illm::gemm8p_supports((int)fmt), "gemm8p_lowbit: unsupported format ", fmt);
   TORCH_CHECK(x.size(-1) == k && k % 128 == 0 && k > 0, "gemm8p_lowbit: in_features must be a multiple of 128");
   TORCH_CHECK(blob.scalar_type() == at::kByte && blob.is_contiguous() &&
               blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemm8p_lowbit: weight blob too small");
   TORCH_CHECK(blob.numel() < (int64_t)UINT32_MAX, "gemm8p_lowbit: blob over 4 GiB");
+  TORCH_CHECK(!glu || (n % 32 == 0 && !out_f32 && !bias.has_value()), "gemm8p_lowbit: GLU needs n % 32, bf16 out, no bias");
   c10::DeviceGuard g(x.device());
   Tensor x2 = x.reshape({-1, k});
   if (x2.stride(1) != 1 || x2.stride(0) % 8 != 0) x2 = x2.contiguous();
   const int64_t M = x2.size(0);
+  const int64_t nout = glu ? n / 2 : n;
   auto shape = x.sizes().vec();
-  shape.back() = n;
-  Tensor out = at::empty({M, n}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  shape.back() = nout;
+  Tensor out = at::empty({M, nout}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   if (M == 0 || n == 0) return out.view(shape);
   const int64_t xb = (M - 1) * x2.stride(0) * 2 + k * 2;
   TORCH_CHECK(xb < (int64_t)UINT32_MAX, "gemm8p_lowbit: x over 4 GiB");
@@ -410,7 +412,9 @@ Tensor gemm8p_lowbit(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n
   a.K = (int)k;
   a.ldx = (int)x2.stride(0);
   a.ldw = 0;
-  a.ldo = (int)n;
+  a.ldo = (int)nout;
+  a.glu = glu ? 1 : 0;
+  a.act = (int)act;
   a.out_f32 = out_f32 ? 1 : 0;
   a.x_bytes = (uint32_t)xb;
   a.w_bytes = (uint32_t)blob.numel();
@@ -424,7 +428,7 @@ TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("mfgemm(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias=None, bool glu=False, int act=0, int tile=-1, int ksplit=0) -> Tensor");
   m.def("x_to_f16_rowscale(Tensor x) -> Tensor[]");
   m.def("gemm_bf16(Tensor x, Tensor w, Tensor? bias=None, bool out_f32=False) -> Tensor");
-  m.def("gemm8p_lowbit(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias=None, bool out_f32=False) -> Tensor");
+  m.def("gemm8p_lowbit(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias=None, bool out_f32=False, bool glu=False, int act=0) -> Tensor");
   m.def("mfgemm_nn(Tensor g, Tensor w, int fmt, int n, int k, int tile=-1, int ksplit=0) -> Tensor");
   m.def("mfgemm_lora(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias, Tensor la, Tensor lb, float s) -> Tensor[]");
   m.def("mfgemm_nn_lora(Tensor g, Tensor w, int fmt, int n, int k, Tensor la, Tensor lb, float s) -> Tensor[]");

@@ -307,7 +307,12 @@ def _(x, w, bias=None, out_f32=False):
 
 
 @register_fake("ipex_llm_amd::gemm8p_lowbit")
-def _(x, blob, fmt, n, k, bias=None, out_f32=False):
+def _(x, blob, fmt, n, k, bias=None, out_f32=False, glu=False, act=0):
     shape = list(x.shape)
-    shape[-1] = n
+    shape[-1] = n // 2 if glu else n
     return x.new_empty(shape, dtype=torch.float32 if out_f32 else x.dtype)
+
+
+@register_fake("ipex_llm_amd::fp8_gemm8p")
+def _(xq, sx, w, ws, e5m2):
+    return xq.new_empty((xq.shape[0], w.shape[0]), dtype=torch.bfloat16)

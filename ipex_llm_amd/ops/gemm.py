@@ -135,7 +135,10 @@ def drop_prefetched() -> None:
 # 256 x 256 blocks, LDS-DMA staged activations, per-workgroup decode of the
 # blob into LDS: replaces both paths above from ENGINE_MIN_M rows
 # (ILLM_GEMM_ENGINE=0 disables it for A/B runs).
-_ENGINE = os.environ.get("ILLM_GEMM_ENGINE", "1") == "1"
+# Off by default: measured 0.63-0.88x dequant + hipBLASLt at M = 1024-4096
+# (profiles/mfgemm_engine_sweep_r4.jsonl) and 242 vs 167 ms per QLoRA step
+# (profiles/qlora_r4_ab_*.json); the 8-phase GEMM above replaced it.
+_ENGINE = os.environ.get("ILLM_GEMM_ENGINE", "0") == "1"
 ENGINE_MIN_M = int(os.environ.get("ILLM_GEMM_ENGINE_MIN_M", "512"))
 
 
@@ -145,9 +148,35 @@ def use_engine(M: int, n: int, k: int, glu: bool = False) -> bool:
             and hasattr(torch.ops.ipex_llm_amd, "mfgemm"))
 
 
+# ---- the 8-phase 256 x 256 GEMM (csrc/hip/gemm_8p.hip): bf16 MFMA, weights
+# decoded to bf16 in LDS just in time (bit-identical to dequantize-to-bf16 +
+# GEMM), LDS-DMA activations, counted-vmcnt pipeline, staggered wave-rows.
+# sym_int4 and the nf4 / nf3 LUT formats; bf16 activations; from G8_MIN_M rows
+# (ILLM_GEMM_8P=0 disables it).
+_G8 = os.environ.get("ILLM_GEMM_8P", "0") == "1"     # opt-in: 0.6-0.7x dequant + hipBLASLt so far (profiles/gemm8p_sweep_r4.jsonl)
+G8_MIN_M = int(os.environ.get("ILLM_GEMM_8P_MIN_M", "1024"))
+_G8_FMTS = None
+
+
+def _g8_fmts():
+    global _G8_FMTS
+    if _G8_FMTS is None:
+        from ..quantize import get_format
+        _G8_FMTS = {get_format(q).fmt for q in ("sym_int4", "nf4", "nf3")}
+    return _G8_FMTS
+
+
+def use_g8(x, M: int, n: int, k: int, fmt: int, glu: bool = False) -> bool:
+    return (_G8 and not _USE_LIB and not _USE_FUSED and x.is_cuda and x.dtype == torch.bfloat16 and M >= G8_MIN_M
+            and k % 128 == 0 and (not glu or n % 32 == 0) and fmt in _g8_fmts() and _DENSE_BUDGET <= 0
+            and hasattr(torch.ops.ipex_llm_amd, "gemm8p_lowbit"))
+
+
 def lowbit_gemm(x, blob, fmt, n, k, bias=None):
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
+    if use_g8(x, M, n, k, fmt) and (bias is None or bias.dtype == torch.bfloat16):
+        return ops.gemm8p_lowbit(x, blob, fmt, n, k, bias)
     if use_engine(M, n, k) and x.dtype in (torch.bfloat16, torch.float16):
         return ops.mfgemm(x, blob, fmt, n, k, bias)
     if use_fused(M, n, k) and hasattr(ops, "gemm"):
@@ -162,6 +191,8 @@ def lowbit_gemm_glu(x, blob, fmt, n, k, act: int = 0):
     [M, 2I] round trip, no elementwise launches)."""
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
+    if use_g8(x, M, n, k, fmt, glu=True):
+        return ops.gemm8p_lowbit(x, blob, fmt, n, k, None, False, True, act)
     if use_engine(M, n, k, glu=True) and x.dtype in (torch.bfloat16, torch.float16):
         return ops.mfgemm(x, blob, fmt, n, k, None, True, act)
     if use_fused(M, n, k) and hasattr(ops, "gemm_glu"):

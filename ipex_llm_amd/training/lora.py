@@ -186,7 +186,9 @@ def _engine_lora_ok(base, x, A) -> bool:
             and A.dtype == torch.bfloat16)
 
 
-_ENGINE_NN = os.environ.get("ILLM_LORA_ENGINE_NN", "1") == "1"
+# off by default: the engine NN GEMM measured slower than dequant + hipBLASLt
+# (profiles/qlora_llama3_8b_r4_engine_rocprof.txt)
+_ENGINE_NN = os.environ.get("ILLM_LORA_ENGINE_NN", "0") == "1"
 
 
 def _engine_nn_ok(base, g2) -> bool:

@@ -11,7 +11,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("e5m2", [False, True])
-@pytest.mark.parametrize("M,N,K", [(17, 128, 128), (64, 256, 512), (200, 384, 1024), (1024, 1024, 4096)])
+@pytest.mark.parametrize("M,N,K", [(17, 128, 128), (64, 256, 512), (200, 384, 1024), (1024, 1024, 4096),
+                                   (300, 520, 384), (2048, 4096, 2048)])
 @pytest.mark.parametrize("per_channel", [False, True])
 def test_fp8_gemm_matches_emulation(e5m2, M, N, K, per_channel):
     torch.manual_seed(M + N)

@@ -57,3 +57,26 @@ def test_gemm8p_lowbit_matches_dequant_fp32(cuda, qtype, M, N, K):
     # bit-identical to dequantize-to-bf16 + the dense kernel (same bf16 weights, same order)
     wd = torch.ops.ipex_llm_amd.dequantize_device(blob, f, N, K, torch.bfloat16)
     assert torch.equal(y, torch.ops.ipex_llm_amd.gemm_bf16(x, wd, b))
+
+
+@pytest.mark.parametrize("qtype", ["sym_int4", "nf4"])
+@pytest.mark.parametrize("act", [0, 1])
+def test_gemm8p_lowbit_glu_epilogue(cuda, qtype, act):
+    """gate/up tile-interleaved weight: act(gate) * up in the epilogue"""
+    import torch.nn.functional as F
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.models.decoder import interleave_glu_rows
+    from ipex_llm_amd.quantize import get_format
+    f = get_format(qtype).fmt
+    torch.manual_seed(act)
+    M, I, K = 700, 768, 1024
+    wg, wu = torch.randn(I, K, device=cuda) * 0.05, torch.randn(I, K, device=cuda) * 0.05
+    blob = ops.quantize(interleave_glu_rows(wg, wu), f)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    h = torch.ops.ipex_llm_amd.gemm8p_lowbit(x, blob, f, 2 * I, K, None, True).float()   # f32, interleaved
+    hg = h.view(M, I // 16, 2, 16)
+    g_, u_ = hg[:, :, 0].reshape(M, I), hg[:, :, 1].reshape(M, I)
+    ref = (F.silu(g_) if act == 0 else F.gelu(g_, approximate="tanh")) * u_
+    y = torch.ops.ipex_llm_amd.gemm8p_lowbit(x, blob, f, 2 * I, K, None, False, True, act)
+    assert y.shape == (M, I)
+    assert _rel(y, ref) < 8e-3

@@ -34,6 +34,8 @@ def main():
             w8, ws = ops.fp8_quantize_weight(w, False)
             wb = w.to(torch.bfloat16)
             t_ours = timeit(lambda: torch.ops.ipex_llm_amd.fp8_linear(x, w8, ws, None, False))
+            xq8, sx8 = torch.ops.ipex_llm_amd.fp8_act_quant(x)
+            t_k8p = timeit(lambda: torch.ops.ipex_llm_amd.fp8_gemm8p(xq8, sx8, w8, ws, False))
             t_disp = timeit(lambda: ops.fp8_linear(x, w8, ws, None, False))
             t_bf16 = timeit(lambda: torch.matmul(x, wb.t()))
             t_sm = None
@@ -47,10 +49,12 @@ def main():
                 t_sm = f"n/a: {type(ex).__name__}"
             fl = 2.0 * M * N * K
             rec = {"M": M, "proj": name, "N": N, "K": K, "fp8_ours_us": round(t_ours, 1),
+                   "fp8_8p_kernel_only_us": round(t_k8p, 1), "fp8_8p_kernel_tflops": round(fl / t_k8p / 1e6, 1),
                    "fp8_ours_tflops": round(fl / t_ours / 1e6, 1), "fp8_dispatch_us": round(t_disp, 1),
                    "fp8_dispatch_tflops": round(fl / t_disp / 1e6, 1), "bf16_hipblaslt_us": round(t_bf16, 1),
                    "bf16_tflops": round(fl / t_bf16 / 1e6, 1),
-                   "fp8_scaled_mm_us": round(t_sm, 1) if isinstance(t_sm, float) else t_sm}
+                   "fp8_scaled_mm_us": round(t_sm, 1) if isinstance(t_sm, float) else t_sm,
+                   "kernel_vs_scaled_mm": round(t_sm / t_k8p, 3) if isinstance(t_sm, float) else None}
             print(json.dumps(rec), flush=True)
             del w, x, w8, wb
             torch.cuda.empty_cache()
