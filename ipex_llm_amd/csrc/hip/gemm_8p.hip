@@ -92,7 +92,8 @@ template <int DK> struct G8Lds;
 template <> struct G8Lds<-1> {
   static constexpr int A0 = 0, ASTR = BUFB, B0 = IMG, BSTR = BUFB, BYTES = LDS_BYTES;
 };
-template <> struct G8Lds<-2> : G8Lds<-1> {};     // fp8: the dense layout, 128 k per 128-B row
+template <> struct G8Lds<-2> : G8Lds<-1> {};     // fp8 (e4m3 w): the dense layout, 128 k per 128-B row
+template <> struct G8Lds<-3> : G8Lds<-1> {};     // fp8 (e5m2 w)
 template <int DK> struct G8Lds {
   static constexpr int A0 = 0, ASTR = IMG, B0 = 2 * IMG, BSTR = 0;
   static constexpr int CODES = 3 * IMG, SCALES = CODES + 2 * 16384, LUT = SCALES + 2 * 1024, BYTES = LUT + 2048;
@@ -127,7 +128,9 @@ typedef int32_t g8_i32x8 __attribute__((ext_vector_type(8)));
 template <int DK>
 __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   constexpr bool DENSE = DK < 0;          // both operands staged by LDS-DMA (bf16 or fp8)
-  constexpr bool FP8 = DK == G8_FP8;      // 128 k per K-tile, 16x16x128 block-scaled fp8 MFMA
+  constexpr bool FP8 = DK <= G8_FP8;      // 128 k per K-tile, 16x16x128 block-scaled fp8 MFMA
+  constexpr int FMTW = DK == G8_FP8 - 1 ? 1 : 0;   // w operand format (0 e4m3, 1 e5m2): a compile-time
+                                                   // constant -- a runtime select made hipcc issue both MFMAs
   using L = G8Lds<DK>;
   __shared__ __attribute__((aligned(1024))) uint8_t smem[L::BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -277,12 +280,8 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
           const g8_i32x8 xa = {(int)f[mt][0].x, (int)f[mt][0].y, (int)f[mt][0].z, (int)f[mt][0].w,
                                (int)f[mt][1].x, (int)f[mt][1].y, (int)f[mt][1].z, (int)f[mt][1].w};
           // unit E8M0 block scales (127): the row / column scales go to the epilogue
-          if (a.w_e5m2)
-            acc[nh * 2 + nt][mh * 4 + mt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                wb, xa, acc[nh * 2 + nt][mh * 4 + mt], 1, 0, 0, 127, 0, 127);
-          else
-            acc[nh * 2 + nt][mh * 4 + mt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                wb, xa, acc[nh * 2 + nt][mh * 4 + mt], 0, 0, 0, 127, 0, 127);
+          acc[nh * 2 + nt][mh * 4 + mt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              wb, xa, acc[nh * 2 + nt][mh * 4 + mt], FMTW, 0, 0, 127, 0, 127);
         }
       }
     } else {
@@ -506,7 +505,8 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
 void launch_gemm8p(const G8Args& a, hipStream_t st) {
   const int MB = (a.M + 255) / 256, NB = (a.N + 255) / 256;
   const dim3 grid((unsigned)(MB * NB)), blk(512);
-  if (a.w_fmt == G8_FP8) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8>, grid, blk, 0, st, a);
+  if (a.w_fmt == G8_FP8 && a.w_e5m2) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8 - 1>, grid, blk, 0, st, a);
+  else if (a.w_fmt == G8_FP8) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8>, grid, blk, 0, st, a);
   else if (a.w_fmt < 0) hipLaunchKernelGGL(g8::gemm8p_kernel<-1>, grid, blk, 0, st, a);
   else if (fmt_to_dk(a.w_fmt) == DK_INT4S) hipLaunchKernelGGL(g8::gemm8p_kernel<DK_INT4S>, grid, blk, 0, st, a);
   else hipLaunchKernelGGL(g8::gemm8p_kernel<DK_LUT4>, grid, blk, 0, st, a);
