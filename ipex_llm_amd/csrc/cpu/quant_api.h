@@ -25,4 +25,10 @@ void illm_kq_dequantize(int fmt, const uint8_t* src, int64_t n, int64_t k, float
 void illm_kq_gemm(int fmt, const float* x, int64_t m, const uint8_t* w, int64_t n, int64_t k, float* y);
 void illm_cpu_gemm_q4(int fmt, const float* x, int64_t m, const uint8_t* codes, const uint16_t* scales,
                       const uint16_t* mins, int64_t n, int64_t k, float* y, int isa);
+int illm_cpu_i8_supported(int fmt);
+int illm_cpu_lut_supported(int fmt);
+void illm_cpu_gemm_i8(int fmt, const float* x, int64_t m, const uint8_t* codes, const uint16_t* scales,
+                      const uint16_t* mins, int64_t n, int64_t k, float* y, int isa);
+void illm_cpu_gemm_lut(int fmt, const float* x, int64_t m, const uint8_t* codes, const uint16_t* scales,
+                       int64_t n, int64_t k, float* y, int isa);
 }

@@ -76,7 +76,16 @@ Tensor repack_from_device(const Tensor& dev, int64_t fmt, int64_t n, int64_t k) 
   return canon;
 }
 
+Tensor linear_cpu_isa(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t isa_req);
+
 Tensor linear_cpu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k) {
+  static const int isa = getenv("ILLM_CPU_ISA") ? atoi(getenv("ILLM_CPU_ISA")) : 0;
+  return linear_cpu_isa(x, blob, fmt, n, k, isa);
+}
+
+// isa: 0 auto, 1 AVX2, 2 AVX-512 (VNNI for the integer formats), -1 the
+// portable per-block dequant-dot loop (tests pin every path)
+Tensor linear_cpu_isa(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t isa_req) {
   check_fmt(fmt);
   TORCH_CHECK(x.size(-1) == k, "x last dim must equal in_features");
   Tensor xf = x.reshape({-1, k}).to(at::kFloat).contiguous();
@@ -90,7 +99,7 @@ Tensor linear_cpu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, i
     if (!e) e = getenv("BIGDL_LLM_LINEAR_THRESHOLD");
     return e ? (int64_t)atoll(e) : (int64_t)128;
   }();
-  static const int isa = getenv("ILLM_CPU_ISA") ? atoi(getenv("ILLM_CPU_ISA")) : 0;
+  const int isa = (int)isa_req;
   if (M > thr) {
     Tensor w = at::empty({n, k}, xf.options());
     illm_dequantize((int)fmt, p.codes, p.scales, p.mins, n, k, w.data_ptr<float>());
@@ -101,6 +110,10 @@ Tensor linear_cpu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, i
   Tensor y = at::empty({M, n}, xf.options());
   if (illm_cpu_q4_supported((int)fmt) && isa >= 0 && k % 64 == 0)
     illm_cpu_gemm_q4((int)fmt, xf.data_ptr<float>(), M, p.codes, p.scales, p.mins, n, k, y.data_ptr<float>(), isa);
+  else if (illm_cpu_i8_supported((int)fmt) && isa >= 0 && k % 64 == 0)
+    illm_cpu_gemm_i8((int)fmt, xf.data_ptr<float>(), M, p.codes, p.scales, p.mins, n, k, y.data_ptr<float>(), isa);
+  else if (illm_cpu_lut_supported((int)fmt) && isa >= 0 && k % 64 == 0)
+    illm_cpu_gemm_lut((int)fmt, xf.data_ptr<float>(), M, p.codes, p.scales, n, k, y.data_ptr<float>(), isa);
   else
     illm_cpu_gemm((int)fmt, xf.data_ptr<float>(), M, p.codes, p.scales, p.mins, n, k, y.data_ptr<float>());
   auto shape = x.sizes().vec();
@@ -124,6 +137,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("repack_to_device(Tensor canon, int fmt, int n, int k) -> Tensor");
   m.def("repack_from_device(Tensor dev, int fmt, int n, int k) -> Tensor");
   m.def("linear_cpu(Tensor x, Tensor blob, int fmt, int n, int k) -> Tensor");
+  m.def("linear_cpu_isa(Tensor x, Tensor blob, int fmt, int n, int k, int isa) -> Tensor");
   m.def("to_fp8_bytes(Tensor x, bool e5m2) -> Tensor");
   // device kernels (ops_hip.cpp)
   m.def("quantize_device(Tensor w, int fmt, bool scale_search) -> Tensor");
@@ -176,5 +190,6 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
   m.impl("repack_to_device", &repack_to_device);
   m.impl("repack_from_device", &repack_from_device);
   m.impl("linear_cpu", &linear_cpu);
+  m.impl("linear_cpu_isa", &linear_cpu_isa);
   m.impl("to_fp8_bytes", &to_fp8_bytes);
 }

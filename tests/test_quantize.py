@@ -241,3 +241,55 @@ def test_mixed_fp4_picks_per_tensor_and_round_trips(tmp_path):
     assert k1 == k2
     with torch.no_grad():
         assert torch.allclose(m2(ids).logits, a, atol=1e-5)
+
+
+_ISAS = [1, 2, -1]
+
+
+@pytest.mark.parametrize("qtype", ["sym_int8", "sym_int5", "asym_int5", "nf4", "fp4", "nf3", "fp8_e4m3",
+                                   "fp8_e5m2", "fp6"])
+@pytest.mark.parametrize("M", [1, 5, 17])
+@pytest.mark.parametrize("isa", _ISAS)
+def test_cpu_lowbit_gemm_paths_match_dequant(qtype, M, isa):
+    """every CPU GEMM path (AVX-512 / VNNI, AVX2, portable) of the 8-bit
+    integer formats (int8-activation integer dot) and the LUT / minifloat
+    formats (in-register code expansion, exact f32 activations) == x @
+    dequant(W)^T; the minifloat decode is checked on every byte value"""
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.quantize import get_format
+    if isa == 2 and torch.backends.cpu.get_cpu_capability() != "AVX512":
+        pytest.skip("no AVX-512 on this host")
+    f = get_format(qtype).fmt
+    torch.manual_seed(M)
+    n, k = 40, 384
+    w = torch.randn(n, k) * 0.05
+    w[0, :64] = torch.linspace(-0.4, 0.4, 64)             # wide block: exercises large codes
+    blob = ops.quantize(w, f)
+    x = torch.randn(M, k)
+    y = torch.ops.ipex_llm_amd.linear_cpu_isa(x, blob, f, n, k, isa)
+    ref = x @ ops.dequantize(blob, f, n, k).T
+    rel = ((y - ref).norm() / ref.norm()).item()
+    integer = qtype in ("sym_int8", "sym_int5", "asym_int5") and isa >= 0
+    assert rel < (1e-2 if integer else 1e-5), (qtype, isa, rel)
+
+
+@pytest.mark.parametrize("qtype", ["fp8_e4m3", "fp8_e5m2"])
+@pytest.mark.parametrize("isa", _ISAS)
+def test_cpu_minifloat_decode_every_code(qtype, isa):
+    """a weight row holding all 256 codes (scale 1) dotted with one-hot rows
+    recovers each code's value exactly (normals, subnormals, signs)"""
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.quantize import get_format
+    if isa == 2 and torch.backends.cpu.get_cpu_capability() != "AVX512":
+        pytest.skip("no AVX-512 on this host")
+    f = get_format(qtype).fmt
+    codes = torch.arange(256, dtype=torch.uint8)
+    vals = torch.tensor([float(v) for v in codes.view(torch.float8_e4m3fn if qtype == "fp8_e4m3"
+                                                     else torch.float8_e5m2).float()])
+    codes[~torch.isfinite(vals)] = 0                      # NaN / inf codes never hold weights
+    vals[~torch.isfinite(vals)] = 0.0
+    scales = torch.ones(256 // 64, dtype=torch.float16)    # canonical blob: codes | f16 block scales
+    blob = torch.cat([codes, scales.view(torch.uint8)])
+    assert torch.equal(ops.dequantize(blob, f, 1, 256)[0], vals)
+    y = torch.ops.ipex_llm_amd.linear_cpu_isa(torch.eye(256), blob, f, 1, 256, isa)[:, 0]
+    assert torch.equal(y, vals)
