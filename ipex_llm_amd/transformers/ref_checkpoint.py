@@ -16,7 +16,17 @@ woq_int4        fp16 d, 32 B nibbles (even/odd interleave)  34
 asym_int4 q4_1  fp16 d, fp16 m, 32 B nibbles               36
 sym_int8 q8_0   f32 d, 64 int8                              68
 fp8 e4m3/e5m2   f32 d, 64 codes                             68
+q5_k / q6_k /   ggml k-quant super-blocks of 256 (standard  176 /
+q2_k            block_q5_K / q6_K / q2_K), kept as is       210 / 84
 ==============  =========================================  =======
+
+The k-quant rows are the reference's ``block_q5_K`` / ``block_q6_K`` /
+``block_q2_K`` (``VLLM_PATCH:4928-4966``): the GGUF layouts our k-quant
+kernels read, so they pass through unchanged (merged projections are
+assembled by whole rows).  Its ``block_q4_K`` is NOT the GGUF one (16 bytes
+of 8-bit scales / mins instead of 12 packed 6-bit ones, ``VLLM_PATCH:4935``),
+and ``q5_0`` / ``q5_1`` (sym_int5 / asym_int5), ``fp6`` and ``fp6_k`` have no
+element order in the reference sources: those checkpoints are refused.
 
 Nibble order inside a q4_0 block (``load_qblocks``, ``VLLM_PATCH:3944-3975``):
 byte j holds element j (low nibble) and element j + 32 (high nibble);
@@ -61,8 +71,12 @@ _GGML = {
 }
 
 
+# k-quants whose reference block is the GGUF one (kept as is)
+_KQ_PASS = (Q.Q5_K, Q.Q6_K, Q.Q2_K)
+
+
 def supported_qtypes():
-    return [Q.qtype_name(q) for q in _GGML]
+    return [Q.qtype_name(q) for q in list(_GGML) + list(_KQ_PASS)]
 
 
 def is_reference_low_bit_dir(path: str) -> bool:
@@ -81,6 +95,19 @@ def is_reference_low_bit_dir(path: str) -> bool:
 def ggml_to_canonical(blob: torch.Tensor, qtype, n: int, k: int) -> torch.Tensor:
     """reference ggml-CPU-layout blob of W[n, k] -> our canonical planar blob"""
     qt = Q.resolve_qtype(qtype)
+    if qt in _KQ_PASS:
+        from .. import ops
+        raw = blob.reshape(-1).contiguous().view(torch.uint8)
+        want = torch.ops.ipex_llm_amd.kq_total_bytes(Q.get_format(qt).fmt, n, k) if hasattr(
+            torch.ops.ipex_llm_amd, "kq_total_bytes") else None
+        if k % 256:
+            raise ValueError(f"reference low-bit checkpoint: k-quant in_features {k} is not a multiple of 256")
+        bb = {Q.Q5_K: 176, Q.Q6_K: 210, Q.Q2_K: 84}[qt]
+        if raw.numel() != n * (k // 256) * bb or (want is not None and raw.numel() != want):
+            raise ValueError(f"reference low-bit blob has {raw.numel()} bytes, expected {n * (k // 256) * bb} "
+                             f"({Q.qtype_name(qt)} [{n}, {k}], {bb}-byte super-blocks)")
+        del ops
+        return raw.clone()
     if qt not in _GGML:
         raise ValueError(f"reference low-bit checkpoint: qtype {Q.qtype_name(qt)} is not supported "
                          f"(supported: {', '.join(supported_qtypes())})")
@@ -114,6 +141,8 @@ def ggml_to_canonical(blob: torch.Tensor, qtype, n: int, k: int) -> torch.Tensor
 def canonical_to_ggml(blob: torch.Tensor, qtype, n: int, k: int) -> torch.Tensor:
     """inverse of :func:`ggml_to_canonical` (tests / export to the reference layout)"""
     qt = Q.resolve_qtype(qtype)
+    if qt in _KQ_PASS:
+        return blob.reshape(-1).view(torch.uint8).clone()
     bb, sk, has_min, order = _GGML[qt]
     nb = n * (k // 64)
     cb = nb * (32 if bb in (34, 36) else 64)
@@ -170,7 +199,7 @@ def convert_reference_state_dict(ref_sd: Dict[str, torch.Tensor], model: torch.n
     meta, shapes only): low-bit blobs -> canonical planar, merged projections
     assembled (q/k/v -> qkv_proj, gate/up -> 16-row tile-interleaved
     gate_up_proj) without re-quantizing."""
-    from .low_bit_linear import LowBitLinear, canon_join, canon_planes
+    from .low_bit_linear import KQuantLinear, LowBitLinear, canon_join, canon_planes
     from ..models.decoder import interleave_glu_rows
     out: Dict[str, torch.Tensor] = {}
     used = set()
@@ -182,13 +211,29 @@ def convert_reference_state_dict(ref_sd: Dict[str, torch.Tensor], model: torch.n
             return ggml_to_canonical(t, qtype, n, k)
         raise ValueError(f"{key}: expected a low-bit uint8 blob, got {t.dtype}")
 
+    kq = Q.resolve_qtype(qtype) in _KQ_PASS
     for name, mod in model.named_modules():
-        if not isinstance(mod, LowBitLinear):
+        if not isinstance(mod, (LowBitLinear, KQuantLinear)):
             continue
-        n, k, fmt = mod.out_features, mod.in_features, mod.fmt
+        n, k, fmt = mod.out_features, mod.in_features, getattr(mod, "fmt", None)
         wk = name + ".weight"
         if wk in ref_sd:
             out[wk] = canon(wk, n, k)
+        elif kq:
+            # super-block rows are self-contained: merge / interleave whole rows
+            parent = name.rsplit(".", 1)[0]
+            leaf = name.rsplit(".", 1)[-1]
+            if leaf == "qkv_proj" and all(f"{parent}.{p}_proj.weight" in ref_sd for p in "qkv"):
+                per = [ref_sd[f"{parent}.{p}_proj.weight"].numel() for p in "qkv"]
+                rows = [n * p // sum(per) for p in per]
+                out[wk] = torch.cat([canon(f"{parent}.{p}_proj.weight", r, k) for p, r in zip("qkv", rows)])
+            elif leaf == "gate_up_proj" and f"{parent}.gate_proj.weight" in ref_sd:
+                half = n // 2
+                g = canon(f"{parent}.gate_proj.weight", half, k).view(half, -1)
+                u = canon(f"{parent}.up_proj.weight", half, k).view(half, -1)
+                out[wk] = interleave_glu_rows(g, u).reshape(-1)
+            else:
+                raise KeyError(f"reference checkpoint has no weight for {name}")
         else:
             parent = name.rsplit(".", 1)[0]
             leaf = name.rsplit(".", 1)[-1]

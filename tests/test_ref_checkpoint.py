@@ -82,11 +82,27 @@ def _split_rows(blob, fmt, n, k, rows):
     return outs
 
 
-@pytest.mark.parametrize("qt", ["sym_int4", "asym_int4"])
+def _kq_split_rows(blob, n, rows):
+    v = blob.view(n, -1)
+    outs, r0 = [], 0
+    for r in rows:
+        outs.append(v[r0:r0 + r].reshape(-1).clone())
+        r0 += r
+    return outs
+
+
+def _kq_split_gate_up(blob, n2):
+    t = blob.view(n2 // 32, 2, 16, -1)
+    return t[:, 0].reshape(-1).clone(), t[:, 1].reshape(-1).clone()
+
+
+@pytest.mark.parametrize("qt", ["sym_int4", "asym_int4", "q6_k", "q5_k", "q2_k"])
 def test_load_reference_checkpoint_logits(tmp_path, qt):
     from transformers import LlamaConfig, LlamaForCausalLM
     from ipex_llm_amd.transformers import AutoModelForCausalLM
-    cfg = LlamaConfig(vocab_size=256, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+    kq = qt.endswith("_k")
+    h = 256 if kq else 128
+    cfg = LlamaConfig(vocab_size=256, hidden_size=h, intermediate_size=2 * h, num_hidden_layers=2,
                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256)
     torch.manual_seed(0)
     dense = LlamaForCausalLM(cfg).eval()
@@ -102,18 +118,19 @@ def test_load_reference_checkpoint_logits(tmp_path, qt):
     sd = {}
     hd = cfg.hidden_size // cfg.num_attention_heads
     for name, mod in ours.named_modules():
-        from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
-        if not isinstance(mod, LowBitLinear):
+        from ipex_llm_amd.transformers.low_bit_linear import KQuantLinear, LowBitLinear
+        if not isinstance(mod, (LowBitLinear, KQuantLinear)):
             continue
         n, k = mod.out_features, mod.in_features
-        blob = mod.canonical_blob()
+        blob = mod.weight.data.reshape(-1).cpu() if kq else mod.canonical_blob()
         parent = name.rsplit(".", 1)[0]
         if name.endswith("qkv_proj"):
             rows = [cfg.num_attention_heads * hd, cfg.num_key_value_heads * hd, cfg.num_key_value_heads * hd]
-            for p, b, r in zip("qkv", _split_rows(blob, fmt, n, k, rows), rows):
+            parts = _kq_split_rows(blob, n, rows) if kq else _split_rows(blob, fmt, n, k, rows)
+            for p, b, r in zip("qkv", parts, rows):
                 sd[f"{parent}.{p}_proj.weight"] = RC.canonical_to_ggml(b, qt, r, k)
         elif name.endswith("gate_up_proj"):
-            g, u = _split_gate_up(blob, fmt, n, k)
+            g, u = _kq_split_gate_up(blob, n) if kq else _split_gate_up(blob, fmt, n, k)
             sd[f"{parent}.gate_proj.weight"] = RC.canonical_to_ggml(g, qt, n // 2, k)
             sd[f"{parent}.up_proj.weight"] = RC.canonical_to_ggml(u, qt, n // 2, k)
         else:
