@@ -26,6 +26,11 @@
 #include "../common/kquant.h"
 #include "../common/quant_block.h"
 
+namespace illm {
+void iq_quantize_block(int fmt, const float* x, const float* im, uint8_t* out);   // iquant.cpp
+void iq_dequant_block(int fmt, const uint8_t* b, float* y);
+}
+
 namespace {
 
 using illm::QK_K;
@@ -288,7 +293,9 @@ void quant_q2k(const float* x, const float* im, uint8_t* out) {
 }
 
 void dequant_block(int fmt, const uint8_t* b, float* y) {
-  if (fmt == illm::FMT_Q4K || fmt == illm::FMT_Q5K) {
+  if (illm::is_iq(fmt)) {
+    illm::iq_dequant_block(fmt, b, y);
+  } else if (fmt == illm::FMT_Q4K || fmt == illm::FMT_Q5K) {
     const float d = f(((const uint16_t*)b)[0]), dmin = f(((const uint16_t*)b)[1]);
     const uint8_t* sc = b + 4;
     const bool five = fmt == illm::FMT_Q5K;
@@ -365,7 +372,8 @@ void illm_kq_quantize(int fmt, const float* src, int64_t n, int64_t k, const flo
       const float* x = src + r * k + b * QK_K;
       const float* im = imatrix ? imatrix + b * QK_K : nullptr;
       uint8_t* o = dst + (r * nb + b) * bb;
-      if (fmt == illm::FMT_Q4K) quant_q4k_q5k(x, im, o, false);
+      if (illm::is_iq(fmt)) illm::iq_quantize_block(fmt, x, im, o);
+      else if (fmt == illm::FMT_Q4K) quant_q4k_q5k(x, im, o, false);
       else if (fmt == illm::FMT_Q5K) quant_q4k_q5k(x, im, o, true);
       else if (fmt == illm::FMT_Q6K) quant_q6k(x, im, o);
       else quant_q2k(x, im, o);

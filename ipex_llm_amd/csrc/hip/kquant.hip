@@ -1,5 +1,6 @@
 // k-quant (q4_K / q5_K / q6_K / q2_K, GGUF super-block layouts, common/kquant.h)
-// decoders on gfx950: dequantize to bf16/f16 (prefill GEMM input, QLoRA
+// and IQ lattice (iq2_xxs / iq2_xs / iq1_s, common/iquant.h; codebooks in
+// constant memory) decoders on gfx950: dequantize to bf16/f16 (prefill GEMM input, QLoRA
 // backward) and the decode GEMV (M <= 8) straight from the GGUF blocks.
 //
 // Reference capability: the k-quant qtypes and the gguf_q4k_s/m mixed
@@ -19,6 +20,11 @@
 
 namespace illm {
 
+// the IQ codebooks (common/iq_grids.h) in constant memory
+__constant__ uint64_t d_iq2xxs_grid[256] = ILLM_IQ2XXS_GRID;
+__constant__ uint64_t d_iq2xs_grid[512] = ILLM_IQ2XS_GRID;
+__constant__ uint64_t d_iq1s_grid[2048] = ILLM_IQ1S_GRID;
+
 __device__ __forceinline__ float kq_h(const uint8_t* p) { return f16_to_f32(*(const uint16_t*)p); }
 // q6_K blocks are 210 B: odd blocks start 2 mod 4, so its 32-bit code reads
 // are assembled from two 16-bit loads (every other format is 4-B aligned)
@@ -29,7 +35,15 @@ __device__ __forceinline__ uint32_t ld32_a2(const uint8_t* p) {
 // 4 consecutive weights e0..e0+3 (e0 % 4 == 0) of one super-block
 template <int FMT>
 __device__ __forceinline__ void kq_dec4(const uint8_t* b, int e0, float* w) {
-  if constexpr (FMT == FMT_Q4K || FMT == FMT_Q5K) {
+  if constexpr (is_iq(FMT)) {
+    // IQ: decode the lane's 8-weight chunk, keep its half
+    float w8[8];
+    const uint64_t* grid = FMT == FMT_IQ2XXS ? d_iq2xxs_grid : (FMT == FMT_IQ2XS ? d_iq2xs_grid : d_iq1s_grid);
+    iq_dec8(FMT, b, e0 >> 3, grid, w8);
+    const int o = e0 & 4;
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = w8[o + i];
+  } else if constexpr (FMT == FMT_Q4K || FMT == FMT_Q5K) {
     const int j = e0 >> 6, hi = (e0 >> 5) & 1, l = e0 & 31, sub = 2 * j + hi;
     int s, m;
     kq_scale_min_k4(sub, b + 4, &s, &m);
@@ -129,6 +143,9 @@ void launch_kq_dequant(int fmt, bool bf16, const uint8_t* w, int64_t n, int64_t 
     case FMT_Q4K: dq_fmt<FMT_Q4K>(bf16, w, n, k, out, st); break;
     case FMT_Q5K: dq_fmt<FMT_Q5K>(bf16, w, n, k, out, st); break;
     case FMT_Q6K: dq_fmt<FMT_Q6K>(bf16, w, n, k, out, st); break;
+    case FMT_IQ2XXS: dq_fmt<FMT_IQ2XXS>(bf16, w, n, k, out, st); break;
+    case FMT_IQ2XS: dq_fmt<FMT_IQ2XS>(bf16, w, n, k, out, st); break;
+    case FMT_IQ1S: dq_fmt<FMT_IQ1S>(bf16, w, n, k, out, st); break;
     default: dq_fmt<FMT_Q2K>(bf16, w, n, k, out, st); break;
   }
 }
@@ -152,6 +169,9 @@ void launch_kq_gemv(int fmt, bool bf16, const uint16_t* x, int M, int64_t K, con
     case FMT_Q4K: gv_fmt<FMT_Q4K>(bf16, x, M, K, w, N, out, st); break;
     case FMT_Q5K: gv_fmt<FMT_Q5K>(bf16, x, M, K, w, N, out, st); break;
     case FMT_Q6K: gv_fmt<FMT_Q6K>(bf16, x, M, K, w, N, out, st); break;
+    case FMT_IQ2XXS: gv_fmt<FMT_IQ2XXS>(bf16, x, M, K, w, N, out, st); break;
+    case FMT_IQ2XS: gv_fmt<FMT_IQ2XS>(bf16, x, M, K, w, N, out, st); break;
+    case FMT_IQ1S: gv_fmt<FMT_IQ1S>(bf16, x, M, K, w, N, out, st); break;
     default: gv_fmt<FMT_Q2K>(bf16, x, M, K, w, N, out, st); break;
   }
 }

@@ -71,7 +71,11 @@ FMT_SYM_INT4, FMT_ASYM_INT4, FMT_NF4, FMT_FP4, FMT_SYM_INT8, FMT_FP8E4, FMT_FP8E
 # GGUF k-quant super-block formats (csrc/common/kquant.h): the block bytes
 # are the storage on host and device (GGUF tensors load as-is)
 FMT_Q4K, FMT_Q5K, FMT_Q6K, FMT_Q2K = 11, 12, 13, 14
-KQ_BLOCK_BYTES = {FMT_Q4K: 144, FMT_Q5K: 176, FMT_Q6K: 210, FMT_Q2K: 84}
+# IQ lattice super-blocks (csrc/common/iquant.h): ggml's layouts and bits
+# per weight, our own codebooks
+FMT_IQ2XXS, FMT_IQ2XS, FMT_IQ1S = 15, 16, 17
+KQ_BLOCK_BYTES = {FMT_Q4K: 144, FMT_Q5K: 176, FMT_Q6K: 210, FMT_Q2K: 84,
+                  FMT_IQ2XXS: 66, FMT_IQ2XS: 74, FMT_IQ1S: 50}
 
 NF4_TABLE = [
     -1.0, -0.6961928009986877, -0.5250730514526367, -0.39491748809814453,
@@ -126,24 +130,27 @@ _FORMATS: Dict[int, QFormat] = {
     Q5_K: QFormat("q5_k", Q5_K, FMT_Q5K, 5, 256, has_min=True, k_align=256, kquant=True),
     Q6_K: QFormat("q6_k", Q6_K, FMT_Q6K, 6, 256, k_align=256, kquant=True),
     Q2_K: QFormat("q2_k", Q2_K, FMT_Q2K, 2, 256, has_min=True, k_align=256, kquant=True),
+    IQ2_XXS: QFormat("gguf_iq2_xxs", IQ2_XXS, FMT_IQ2XXS, 2, 256, k_align=256, kquant=True),
+    IQ2_XS: QFormat("gguf_iq2_xs", IQ2_XS, FMT_IQ2XS, 2, 256, k_align=256, kquant=True),
+    IQ1_S: QFormat("gguf_iq1_s", IQ1_S, FMT_IQ1S, 1, 256, k_align=256, kquant=True),
 }
-# qtypes stored in a format of equal or higher precision.  The IQ1 / IQ2
-# lattice codebooks of ggml are not reproduced (their grid tables ship only
-# inside the llama.cpp binaries the reference downloads): gguf_iq2_xxs / xs /
-# iq1_s / iq1_m quantize into the native 2-bit super-block format q2_k
-# (2.625 bits per weight, imatrix-weighted like the IQ quantizers) -- the
-# closest footprint the device kernels decode; IQ-coded GGUF tensors are not
-# loadable.
+# qtypes stored in a format of equal or higher precision.  gguf_iq2_xxs /
+# gguf_iq2_xs / gguf_iq1_s are native IQ lattice formats with ggml's block
+# layouts and bits per weight (2.0625 / 2.3125 / 1.5625) but OUR codebooks
+# (ggml's grid tables are not in the reference repository; csrc/common/
+# iquant.h): IQ-coded GGUF tensors are therefore not loadable.  gguf_iq1_m
+# (1.75 bpw) quantizes into q2_k (2.625 bpw).
 _ALIAS = {
     FP6_K: FP6,
-    IQ2_XXS: Q2_K, IQ2_XS: Q2_K, IQ1_S: Q2_K, IQ1_M: Q2_K,
+    IQ1_M: Q2_K,
     SYM_INT4_RTN: SYM_INT4, ASYM_INT4_RTN: ASYM_INT4, SYM_INT8_RTN: SYM_INT8,
     # gguf mixed policies resolve per module (mixed_kquant_qtype); q4_k otherwise
     GGUF_Q4K_S: Q4_K, GGUF_Q4K_M: Q4_K,
 }
 # in_features % 256 != 0: the reference's fallback formats
 # (SRC/transformers/utils.py:380-401, check_hidden_size)
-KQ_FALLBACK = {Q4_K: ASYM_INT4, Q5_K: ASYM_INT5, Q6_K: SYM_INT8, Q2_K: ASYM_INT4}
+KQ_FALLBACK = {Q4_K: ASYM_INT4, Q5_K: ASYM_INT5, Q6_K: SYM_INT8, Q2_K: ASYM_INT4,
+               IQ2_XXS: ASYM_INT4, IQ2_XS: ASYM_INT4, IQ1_S: ASYM_INT4}
 
 
 def is_kquant(qtype) -> bool:

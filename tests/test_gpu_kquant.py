@@ -10,7 +10,9 @@ from ipex_llm_amd.quantize import qtypes as Q
 
 pytestmark = pytest.mark.gpu
 
-FMTS = {"q4_k": Q.FMT_Q4K, "q5_k": Q.FMT_Q5K, "q6_k": Q.FMT_Q6K, "q2_k": Q.FMT_Q2K}
+FMTS = {"q4_k": Q.FMT_Q4K, "q5_k": Q.FMT_Q5K, "q6_k": Q.FMT_Q6K, "q2_k": Q.FMT_Q2K,
+        # IQ lattice formats (csrc/common/iquant.h, codebooks in constant memory)
+        "gguf_iq2_xxs": Q.FMT_IQ2XXS, "gguf_iq2_xs": Q.FMT_IQ2XS, "gguf_iq1_s": Q.FMT_IQ1S}
 
 
 @pytest.mark.parametrize("name", list(FMTS))
@@ -43,11 +45,12 @@ def test_kq_linear_matches_fp32(name, m):
     assert rel < 1e-2, rel
 
 
-def test_kquant_linear_module_on_gpu():
+@pytest.mark.parametrize("qt", ["q4_k", "gguf_iq2_xxs"])
+def test_kquant_linear_module_on_gpu(qt):
     from ipex_llm_amd.transformers.low_bit_linear import KQuantLinear
     torch.manual_seed(2)
     lin = torch.nn.Linear(512, 96, bias=True)
-    m = KQuantLinear.from_linear(lin, "q4_k").cuda().to(torch.bfloat16)
+    m = KQuantLinear.from_linear(lin, qt).cuda().to(torch.bfloat16)
     x = torch.randn(2, 3, 512)
     want = torch.nn.functional.linear(x, m.dequantize().float().cpu(), lin.bias.detach())
     got = m(x.cuda().to(torch.bfloat16)).float().cpu()
