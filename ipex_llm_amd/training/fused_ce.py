@@ -8,11 +8,12 @@ Llama-3's 128 K vocabulary that is a 2 GB f32 tensor per 4 K-token step and
 three full passes over it.
 
 MI355X design: the tokens are processed in chunks; per chunk the logits are
-one engine GEMM (``mfgemm``, bf16, dense lm_head), ``ce_fused_`` turns them
-into the per-row loss and, IN PLACE, the logits gradient (softmax - onehot)
-in one read for the row statistics and one read + write for the gradient,
-and the hidden-state gradient is the transposed engine GEMM
-(``mfgemm_nn``) of that chunk -- computed during the forward, since the only
+one bf16 GEMM (the library GEMM: it measured faster than our engine and
+8-phase kernels on this shape, profiles/qlora_llama3_8b_r4_*), ``ce_fused_``
+turns them into the per-row loss and, IN PLACE, the logits gradient
+(softmax - onehot) in one read for the row statistics and one read + write
+for the gradient, and the hidden-state gradient is the second GEMM
+(dlogits @ W) of that chunk -- computed during the forward, since the only
 consumer of the loss is a scalar backward.  Nothing of size [tokens, vocab]
 outlives a chunk; backward is one scale of the stored [tokens, hidden]
 gradient.  The lm_head weight is frozen here (QLoRA); a trainable head
@@ -25,7 +26,7 @@ from typing import Optional
 
 import torch
 
-CHUNK = int(os.environ.get("ILLM_CE_CHUNK", "1024"))
+CHUNK = int(os.environ.get("ILLM_CE_CHUNK", "2048"))
 
 
 class _FusedLinearCE(torch.autograd.Function):
@@ -33,15 +34,16 @@ class _FusedLinearCE(torch.autograd.Function):
     def forward(ctx, h, weight, labels, ignore_index: int):
         ops = torch.ops.ipex_llm_amd
         T, H = h.shape
+        w = weight if weight.dtype == h.dtype else weight.to(h.dtype)
         V = weight.shape[0]
         loss_rows = torch.empty(T, device=h.device, dtype=torch.float32)
         grad_h = torch.empty_like(h) if h.requires_grad else None
         for c0 in range(0, T, CHUNK):
             c1 = min(T, c0 + CHUNK)
-            logits = ops.mfgemm(h[c0:c1], weight, -1, V, H)
+            logits = torch.mm(h[c0:c1], w.t())
             loss_rows[c0:c1] = ops.ce_fused_(logits, labels[c0:c1], ignore_index, 1.0 if grad_h is not None else 0.0)
             if grad_h is not None:
-                grad_h[c0:c1] = ops.mfgemm_nn(logits, weight, -1, V, H)
+                torch.mm(logits, w, out=grad_h[c0:c1])
             del logits
         n_valid = (labels != ignore_index).sum().clamp_(min=1).to(torch.float32)
         ctx.save_for_backward(grad_h, n_valid)
