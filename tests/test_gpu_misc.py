@@ -96,7 +96,9 @@ def test_rwkv_model_on_gpu_matches_cpu(cuda, tmp_path):
     with torch.no_grad():
         want = m(ids).logits
         got = m.to(cuda)(ids.to(cuda)).logits.cpu()
-    assert ((got - want).norm() / want.norm()).item() < 1e-2
+    # the CPU side runs sym_int8 on the int8-activation integer dot (per-64
+    # activation quantization, as ggml's q8_0 path): ~1-2 % from the GPU
+    assert ((got - want).norm() / want.norm()).item() < 3e-2
 
 
 def test_hf_eager_family_on_gpu_uses_hip_softmax(cuda, tmp_path):

@@ -94,9 +94,14 @@ def test_train_flash_attention_fwd_bwd(cuda, B, Hq, Hkv, T, D, causal):
 
 
 @pytest.mark.parametrize("qtype,r", [("nf4", 8), ("sym_int4", 16), ("nf4", 40)])
-def test_lora_engine_node_matches_fp32(cuda, qtype, r):
+def test_lora_engine_node_matches_fp32(cuda, qtype, r, monkeypatch):
     """the all-engine QLoRA linear (LoRA in the GEMM epilogues, skinny adapter
-    gradients) vs fp32 torch over the dequantized base"""
+    gradients) vs fp32 torch over the dequantized base (the engine path is
+    opt-in: ILLM_GEMM_ENGINE=1 ILLM_LORA_ENGINE_NN=1)"""
+    import ipex_llm_amd.ops.gemm as G
+    import ipex_llm_amd.training.lora as L
+    monkeypatch.setattr(G, "_ENGINE", True)
+    monkeypatch.setattr(L, "_ENGINE_NN", True)
     from ipex_llm_amd import ops
     from ipex_llm_amd.ops import reference as R
     from ipex_llm_amd.quantize import get_format
