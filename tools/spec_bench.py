@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--prompt", type=int, default=256)
     ap.add_argument("--new", type=int, default=128)
+    ap.add_argument("--ks", default="1,2,3,4,6,4a", help="draft lengths; 'a' suffix = adaptive")
+    ap.add_argument("--std", type=float, default=0.02, help="random-init weight std")
+    ap.add_argument("--skip-plain", action="store_true", help="(profiling) no plain-decode baselines")
     args = ap.parse_args()
     from transformers import LlamaConfig
     from ipex_llm_amd.engine.runner import Engine, GenTiming
@@ -32,7 +35,7 @@ def main():
                       num_attention_heads=32, num_key_value_heads=8, max_position_embeddings=8192,
                       rope_theta=500000.0)
     dev = torch.device("cuda")
-    draft = random_native_model(cfg, "sym_int4", dev, torch.bfloat16, seed=0)
+    draft = random_native_model(cfg, "sym_int4", dev, torch.bfloat16, seed=0, std=args.std)
     target = dense_copy(draft)
     torch.cuda.synchronize()
     prompt = torch.randint(0, 128256, (args.prompt,), generator=torch.Generator().manual_seed(1)).tolist()
@@ -48,10 +51,15 @@ def main():
               flush=True)
         return out[0], ms
 
-    ref, t_bf16 = plain(te, "plain_bf16_target")
-    _, t_int4 = plain(de, "plain_int4")
+    if args.skip_plain:
+        ref = te.generate([prompt], max_new_tokens=args.new, use_graph=True)[0]
+        t_bf16 = t_int4 = float("nan")
+    else:
+        ref, t_bf16 = plain(te, "plain_bf16_target")
+        _, t_int4 = plain(de, "plain_int4")
     max_len = args.prompt + args.new + 64
-    for k, adaptive in ((1, False), (2, False), (3, False), (4, False), (6, False), (4, True)):
+    cfgs = [(int(v.rstrip("a")), v.endswith("a")) for v in args.ks.split(",")]
+    for k, adaptive in cfgs:
         sp = GraphSpeculator(te, de, k, max_len, k_max=8 if adaptive else k, adaptive=adaptive)
         sp.generate(prompt, args.new)                      # warm-up + capture
         torch.cuda.synchronize()
@@ -62,12 +70,14 @@ def main():
         tm = GenTiming()
         sp.generate(prompt, args.new, timing=tm)
         ms = tm.rest_cost_mean * 1e3
-        agree = sum(int(a == b) for a, b in zip(out, ref)) / len(ref)
+        gen, gref = out[len(prompt):], ref[len(prompt):]          # generated tokens only
+        agree = sum(int(a == b) for a, b in zip(gen, gref)) / max(1, len(gref))
+        first_div = next((i for i, (a, b) in enumerate(zip(gen, gref)) if a != b), None)
         print(json.dumps({"mode": "speculative_graph", "k": k, "adaptive": adaptive, "ms_per_token": round(ms, 3),
                           "acceptance": round(sp.acceptance, 3), "tokens_per_round": round((len(out) - len(prompt) - 1)
                                                                                           / max(1, sp.rounds), 2),
                           "speedup_vs_bf16": round(t_bf16 / ms, 2), "vs_int4": round(t_int4 / ms, 2),
-                          "token_agreement_with_target_greedy": round(agree, 3),
+                          "generated_token_agreement": round(agree, 3), "first_divergence": first_div,
                           "wall_s_total": round(time.perf_counter() - t0, 3)}), flush=True)
 
 
