@@ -26,6 +26,8 @@ struct G8Args {
 constexpr int G8_FP8 = -2;
 
 void launch_gemm8p(const G8Args& a, hipStream_t st);
+// dense bf16 only, bf16 out, no bias / GLU, K % 128 == 0 (gemm_4w.hip)
+void launch_gemm4w(const G8Args& a, hipStream_t st);
 bool gemm8p_supports(int fmt);
 
 }  // namespace illm

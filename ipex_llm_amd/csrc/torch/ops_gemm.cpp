@@ -337,8 +337,10 @@ std::vector<Tensor> x_to_f16_rowscale(const Tensor& x) {
 }  // namespace
 
 // dense bf16 NT GEMM on the 8-phase 256 x 256 kernel (gemm_8p.hip):
-// y[M, N] = x[M, K] @ w[N, K]^T (+ bias), bf16 or f32 out; K % 64 == 0
-Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool out_f32) {
+// y[M, N] = x[M, K] @ w[N, K]^T (+ bias), bf16 or f32 out; K % 64 == 0.
+// kernel = 1: the experimental 4-wave 128 x 128-per-wave kernel
+// (gemm_4w.hip; bf16 out, no bias, K % 128 == 0)
+Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool out_f32, int64_t kernel) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
               "gemm_bf16: bf16 GPU tensors");
   TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1, "gemm_bf16: w must be [N, K] with unit inner stride");
@@ -373,7 +375,12 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   a.x_bytes = (uint32_t)xb;
   a.w_bytes = (uint32_t)wb;
   a.w_fmt = -1;
-  illm::launch_gemm8p(a, at::hip::getCurrentHIPStream().stream());
+  if (kernel == 1) {
+    TORCH_CHECK(!bias.has_value() && !out_f32 && K % 128 == 0, "gemm_bf16(kernel=1): bf16 out, no bias, K % 128 == 0");
+    illm::launch_gemm4w(a, at::hip::getCurrentHIPStream().stream());
+  } else {
+    illm::launch_gemm8p(a, at::hip::getCurrentHIPStream().stream());
+  }
   return out.view(shape);
 }
 
@@ -427,7 +434,7 @@ Tensor gemm8p_lowbit(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("mfgemm(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias=None, bool glu=False, int act=0, int tile=-1, int ksplit=0) -> Tensor");
   m.def("x_to_f16_rowscale(Tensor x) -> Tensor[]");
-  m.def("gemm_bf16(Tensor x, Tensor w, Tensor? bias=None, bool out_f32=False) -> Tensor");
+  m.def("gemm_bf16(Tensor x, Tensor w, Tensor? bias=None, bool out_f32=False, int kernel=0) -> Tensor");
   m.def("gemm8p_lowbit(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias=None, bool out_f32=False, bool glu=False, int act=0) -> Tensor");
   m.def("mfgemm_nn(Tensor g, Tensor w, int fmt, int n, int k, int tile=-1, int ksplit=0) -> Tensor");
   m.def("mfgemm_lora(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias, Tensor la, Tensor lb, float s) -> Tensor[]");

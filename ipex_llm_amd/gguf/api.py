@@ -2,7 +2,8 @@
 
 Reference: ``SRC/transformers/gguf/api.py:21-75`` (``load_gguf_model``
 dispatching to per-family builders: llama, mistral, mixtral, baichuan,
-bloom, falcon, mpt, yuan2) and ``gguf/models/llama.py:28-129`` (config from
+bloom, falcon, mpt, yuan2 -- Yuan 2.0 builds models/yuan.py's in-library
+LFA model) and ``gguf/models/llama.py:28-129`` (config from
 the key/values, q/k row permutation undone, weights loaded tensor by
 tensor).  Here one table-driven builder covers the llama-layout families
 (llama / mistral / qwen2 / qwen3 and the MoE variants mixtral / qwen2moe /
@@ -46,7 +47,34 @@ _LAYER = {
     "ffn_up_shexp": "mlp.shared_expert.up_proj",
     "ffn_down_shexp": "mlp.shared_expert.down_proj",
     "ffn_gate_inp_shexp": "mlp.shared_expert_gate.weight",
+    # Yuan 2.0 localized filtering (reference gguf/models/yuan2.py:88-97)
+    "lf_output_norm": "self_attn.lf_gate.output_layernorm.weight",
+    "conv1": "self_attn.lf_gate.conv1",
+    "conv2": "self_attn.lf_gate.conv2",
 }
+
+
+def is_yuan(r: GGUFReader) -> bool:
+    """Yuan 2.0 GGUF: architecture "llama" + "yuan" in general.name (the
+    reference's dispatch, gguf/api.py:45-56)"""
+    return r.architecture == "llama" and "yuan" in str(r.kv.get("general.name", "")).lower()
+
+
+def _yuan_config(r: GGUFReader):
+    """reference gguf/models/yuan2.py:31-59 (llama.* keys)"""
+    from ..models.yuan import YuanConfig, register
+    register()
+    g = lambda k, d=None: r.kv.get(f"llama.{k}", d)           # noqa: E731
+    toks = r.kv.get("tokenizer.ggml.tokens")
+    return YuanConfig(vocab_size=len(toks) if toks is not None else r.tensors["token_embd.weight"].shape[1],
+                      hidden_size=g("embedding_length"), intermediate_size=g("feed_forward_length"),
+                      num_hidden_layers=g("block_count"), num_attention_heads=g("attention.head_count"),
+                      max_position_embeddings=g("context_length", 4096),
+                      rms_norm_eps=g("attention.layer_norm_rms_epsilon", 1e-6),
+                      tie_word_embeddings="output.weight" not in r.tensors,
+                      pad_token_id=r.kv.get("tokenizer.ggml.padding_token_id"),
+                      bos_token_id=r.kv.get("tokenizer.ggml.bos_token_id"),
+                      eos_token_id=r.kv.get("tokenizer.ggml.eos_token_id"))
 
 
 def _unpermute(w: np.ndarray, n_head: int) -> np.ndarray:
@@ -153,8 +181,14 @@ def load_gguf_model(fpath: str, dtype=torch.float16, low_bit: Optional[str] = No
     r = GGUFReader(fpath)
     arch = r.architecture
     fam = family_config(r) if arch in ("bloom", "falcon", "mpt", "baichuan") else None
-    cfg, mt = (fam, fam.model_type) if fam is not None else _config(r)
-    permuted = arch in ("llama", "baichuan")          # llama.cpp's q/k row permutation
+    yuan = is_yuan(r)
+    if yuan:
+        cfg, mt = _yuan_config(r), "yuan"
+    else:
+        cfg, mt = (fam, fam.model_type) if fam is not None else _config(r)
+    # llama.cpp's q/k row permutation (Yuan files keep the HF order: the
+    # reference's yuan2 loader maps attn_q / attn_k as they are)
+    permuted = arch in ("llama", "baichuan") and not yuan
     with init_empty_weights():
         model = AutoModelForCausalLM.from_config(cfg, torch_dtype=dtype)
     n_head, n_kv = cfg.num_attention_heads, getattr(cfg, "num_key_value_heads", cfg.num_attention_heads)

@@ -330,6 +330,15 @@ def native_from_hf(hf_model, dtype=None) -> Optional[NativeCausalLM]:
         if pp is not None and not (pp["start"] <= i < pp["end"]):
             continue                        # owned by another pipeline stage
         at = L.self_attn
+        if spec.model_type == "yuan":
+            from .yuan import yuan_lf_from_hf
+            lf = yuan_lf_from_hf(at, spec.rms_eps, L.input_layernorm.weight.dtype, L.input_layernorm.weight.device)
+            attn = NativeAttention(spec, None, at.o_proj)
+            attn.lf = lf
+            mlp = NativeMLP(spec, L.mlp.gate_up_proj, L.mlp.down_proj)
+            layers.append(NativeLayer(spec, attn, mlp, L.input_layernorm.weight.data,
+                                      L.post_attention_layernorm.weight.data))
+            continue
         if not hasattr(at, "qkv_proj"):
             return None
         qn = getattr(at, "q_norm", None)

@@ -193,6 +193,7 @@ class NativeAttention(nn.Module):
         self.q_norm = nn.Parameter(q_norm, requires_grad=False) if q_norm is not None else None
         self.k_norm = nn.Parameter(k_norm, requires_grad=False) if k_norm is not None else None
         self.sliding_window = sliding_window
+        self.lf = None                      # Yuan 2.0 localized filtering (models/yuan.py YuanLF)
 
 
 class NativeMLP(nn.Module):
@@ -286,8 +287,15 @@ class NativeCausalLM(nn.Module):
         s = self.spec
         nblk = num_blocks or batch * ((max_tokens + block_size - 1) // block_size)
         self.ensure_rope_cache(max_tokens + 1)
-        return PagedKVCache(len(self.layers), nblk, s.num_kv_heads, s.head_dim, block_size, self.dtype,
-                            self.device, kv_fp8)
+        cache = PagedKVCache(len(self.layers), nblk, s.num_kv_heads, s.head_dim, block_size, self.dtype,
+                             self.device, kv_fp8)
+        if any(L.self_attn.lf is not None for L in self.layers):
+            # Yuan LFA: h and conv1 output of every position, slot-addressed,
+            # plus one zero row standing for position -1
+            H = s.hidden_size
+            cache.lf = [torch.zeros(nblk * block_size + 1, H + H // 2, dtype=self.dtype, device=self.device)
+                        for _ in self.layers]
+        return cache
 
     # ------------------------------------------------------------------ pieces
     def _attention(self, li: int, attn: NativeAttention, q: torch.Tensor, meta: AttnMeta, cache) -> torch.Tensor:
@@ -302,6 +310,24 @@ class NativeCausalLM(nn.Module):
                                 meta.seq_lens, meta.nsplit, s.scale, softcap, window, cache.kv_fp8,
                                 cache.k_scale, cache.v_scale, self.alibi, meta.seq_lens_host)
             return o.view(T, s.num_heads * s.head_dim)
+        if group <= 16 and meta.Tq <= 16 and (s.head_dim in (64, 80, 96, 128, 256) or not q.is_cuda):
+            # short query chunks (speculative verify of k + 1 tokens, tiny
+            # prefills): the decode kernel over <= 16 // group tokens at a
+            # time, the later tokens' keys cut off by a shorter length, so
+            # every query row is reduced exactly as in one-token decoding
+            # (greedy speculative output == plain greedy output)
+            c = 16 // group
+            qv = q.view(meta.B, meta.Tq, s.num_heads, s.head_dim)
+            outs = []
+            for t0 in range(0, meta.Tq, c):
+                n = min(c, meta.Tq - t0)
+                cut = meta.Tq - t0 - n
+                lens = meta.seq_lens - cut if cut else meta.seq_lens
+                lens_h = None if meta.seq_lens_host is None else [int(v) - cut for v in meta.seq_lens_host]
+                outs.append(ops.attn_decode(qv[:, t0:t0 + n].contiguous(), kc, vc, meta.block_tables, lens,
+                                            meta.nsplit, s.scale, softcap, window, cache.kv_fp8, cache.k_scale,
+                                            cache.v_scale, self.alibi, lens_h))
+            return torch.cat(outs, 1).view(T, s.num_heads * s.head_dim)
         if q.is_cuda and self.alibi is None and s.head_dim in (64, 128) and cache.bs % 64 == 0 and self._prefill_attn_native \
                 and ops.native_gpu(q):
             # prefill / long query chunk: flash-attention HIP kernel over the paged cache
@@ -653,7 +679,7 @@ class NativeCausalLM(nn.Module):
                                                   pss_n=s.hidden_size, pss_eps=s.rms_eps,
                                                   prerot=prerot).view(T, -1)
             else:
-                qkv = qp(x)
+                qkv = attn.lf.qkv(x, cache.lf[li], slots, pos, meta, cache.bs) if attn.lf is not None else qp(x)
                 ops.rope_kv(qkv, q, cache.k[li], cache.v[li], slots, pos, rope, s.num_heads,
                             s.num_kv_heads, s.head_dim, s.rot_dim, s.rope_interleaved, attn.q_norm, attn.k_norm,
                             s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale, cache.v_scale)

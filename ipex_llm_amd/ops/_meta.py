@@ -300,7 +300,7 @@ def _(g, w, fmt, n, k, la, lb, s):
 
 
 @register_fake("ipex_llm_amd::gemm_bf16")
-def _(x, w, bias=None, out_f32=False):
+def _(x, w, bias=None, out_f32=False, kernel=0):
     shape = list(x.shape)
     shape[-1] = w.shape[0]
     return x.new_empty(shape, dtype=torch.float32 if out_f32 else x.dtype)

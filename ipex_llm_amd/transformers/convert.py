@@ -34,7 +34,7 @@ logger = logging.getLogger("ipex_llm_amd")
 
 # architectures whose decoder runs on the native engine
 NATIVE_ARCHS = {"llama", "mistral", "qwen2", "qwen3", "gemma", "gemma2", "phi3", "internlm2", "yi",
-                "aquila", "olmo2", "minicpm", "glm", "glm4"}
+                "aquila", "olmo2", "minicpm", "glm", "glm4", "yuan"}
 # granite (embedding/residual/logit multipliers), stablelm (partial rotary + LayerNorm) and
 # starcoder2 (biased LayerNorm MLP, no q_proj split) take the HF forward over low-bit linears.
 MOE_ARCHS = {"mixtral", "qwen2_moe", "qwen3_moe"}
@@ -155,7 +155,12 @@ def _optimize_pre(model: nn.Module, qtype: int):
         return model
     for layer in layers:
         attn = getattr(layer, "self_attn", None) or getattr(layer, "attention", None)
-        if attn is not None:
+        if attn is not None and mt == "yuan":
+            # LFA: q / k read the filtered stream, v the plain one -> [q; k] only
+            if not hasattr(attn, "qk_proj") and isinstance(getattr(attn, "q_proj", None), nn.Linear):
+                attn.qk_proj = _merge_linears([attn.q_proj, attn.k_proj])
+                del attn.q_proj, attn.k_proj
+        elif attn is not None:
             _merge_qkv(attn)
         mlp = getattr(layer, "mlp", None) or getattr(layer, "feed_forward", None)
         if mlp is not None and hasattr(mlp, "experts"):

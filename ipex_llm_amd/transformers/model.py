@@ -31,6 +31,9 @@ import torch.nn as nn
 
 from ..quantize import qtypes as Q
 from .convert import ggml_convert_low_bit
+from ..models.yuan import register as _register_yuan
+
+_register_yuan()                     # model_type "yuan" (Yuan 2.0 LFA) known to the Auto* classes
 
 logger = logging.getLogger("ipex_llm_amd")
 LOW_BIT_META = "illm_low_bit.json"

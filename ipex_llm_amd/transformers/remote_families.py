@@ -37,7 +37,7 @@ from typing import Dict, Optional
 
 import torch
 
-FAMILIES = ("chatglm", "qwen", "internlm")
+FAMILIES = ("chatglm", "qwen", "internlm", "yuan")
 
 
 def family_of(path) -> Optional[str]:
@@ -190,6 +190,11 @@ def load_remote_family(path, torch_dtype="auto"):
     elif fam == "internlm":
         from transformers import LlamaForCausalLM
         cfg, mapped, cls = internlm_to_llama_config(c), dict(sd), LlamaForCausalLM
+    elif fam == "yuan":
+        # Yuan 2.0 (remote code): the in-library LFA model, same tensor names
+        from ..models.yuan import YuanForCausalLM, yuan_config_from_remote
+        cfg, cls = yuan_config_from_remote(c), YuanForCausalLM
+        mapped = {k: v for k, v in sd.items() if not k.endswith("rotary_emb.inv_freq")}
     else:
         from transformers import Qwen2ForCausalLM
         cfg, mapped, cls = qwen_to_qwen2_config(c), qwen_to_qwen2_weights(sd, c), Qwen2ForCausalLM
@@ -205,7 +210,8 @@ def load_remote_family(path, torch_dtype="auto"):
     if missing or unexpected:
         raise ValueError(f"{fam} checkpoint mapping: missing {missing[:5]}, unexpected {unexpected[:5]}")
     # buffers built on meta (rotary inv_freq) are recomputed on the CPU
-    model.model.rotary_emb = type(model.model.rotary_emb)(model.config)
+    if hasattr(model.model, "rotary_emb"):
+        model.model.rotary_emb = type(model.model.rotary_emb)(model.config)
     model = model.to(torch_dtype)
     model.config.illm_source_model_type = fam
     return model.eval()

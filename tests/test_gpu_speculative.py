@@ -31,14 +31,17 @@ def _tie_gap(te, prefix, a, b):
     return abs(lg[a] - lg[b]).item(), lg.abs().max().item()
 
 
-@pytest.mark.parametrize("k,adaptive", [(2, False), (4, False), (6, False), (4, True)])
-def test_graph_speculative_matches_target(k, adaptive):
+@pytest.mark.parametrize("k,adaptive,heads", [(2, False, 4), (4, False, 4), (6, False, 4), (4, True, 4),
+                                              (4, False, 8), (6, False, 8)])
+def test_graph_speculative_matches_target(k, adaptive, heads):
+    """heads = 8 (GQA group 4): k + 1 >= 5 verify rows exceed one 16-row
+    decode-attention launch and run as exact chunks (decoder._attention)"""
     from transformers import LlamaConfig
     from ipex_llm_amd.engine.runner import Engine
     from ipex_llm_amd.generation.spec_graph import GraphSpeculator
     from ipex_llm_amd.models.builder import dense_copy, random_native_model
     cfg = LlamaConfig(vocab_size=2048, hidden_size=512, intermediate_size=1024, num_hidden_layers=2,
-                      num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=2048)
+                      num_attention_heads=heads, num_key_value_heads=2, max_position_embeddings=2048)
     dev = torch.device("cuda")
     draft = random_native_model(cfg, "sym_int4", dev, torch.bfloat16, seed=0, std=0.05)
     target = dense_copy(draft)
