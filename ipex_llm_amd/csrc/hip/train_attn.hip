@@ -48,14 +48,17 @@ __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
   const int kvh = h / (a.Hq / a.Hkv);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int qrow = qb * FA_QB + wave * 16 + r16;                 // < T (T % 64 == 0)
-  const int kend = a.causal ? (qb + 1) * FA_QB : a.T;
-  const int ntile = kend / FA_KT;
+  // the forward also takes ragged T (encoders, inference): rows >= T load
+  // row T - 1 and store nothing, keys >= T are masked (backward: T % 64 == 0)
+  const int qrow = qb * FA_QB + wave * 16 + r16;
+  const int qld = min(qrow, a.T - 1);
+  const int kend = a.causal ? min((qb + 1) * FA_QB, a.T) : a.T;
+  const int ntile = (kend + FA_KT - 1) / FA_KT;
 
   // Q (and dO) fragments: B operands of S^T = K Q^T (dP^T = V dO^T)
   uint4 qf[KSTEP], df[BWD ? KSTEP : 1];
   {
-    const uint16_t* qp = a.q + (size_t)b * a.qsb + (size_t)h * a.qsh + (size_t)qrow * a.qst;
+    const uint16_t* qp = a.q + (size_t)b * a.qsb + (size_t)h * a.qsh + (size_t)qld * a.qst;
 #pragma unroll
     for (int s = 0; s < KSTEP; s++) qf[s] = *(const uint4*)(qp + 32 * s + 8 * g);
     if constexpr (BWD) {
@@ -79,8 +82,9 @@ __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
     for (int j = 0; j < UPT; j++) {
       const int u = tid + 256 * j;
       const int r = u / (D / 8), c = u % (D / 8);
-      kreg[j] = *(const uint4*)(kbase + (size_t)(t * FA_KT + r) * a.kst + c * 8);
-      vreg[j] = *(const uint4*)(vbase + (size_t)(t * FA_KT + r) * a.vst + c * 8);
+      const int kr = min(t * FA_KT + r, a.T - 1);
+      kreg[j] = *(const uint4*)(kbase + (size_t)kr * a.kst + c * 8);
+      vreg[j] = *(const uint4*)(vbase + (size_t)kr * a.vst + c * 8);
     }
   };
   auto store_tile = [&](int buf) {
@@ -109,7 +113,7 @@ __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
     const int kt0 = t * FA_KT;
     const uint16_t* kb_ = ks[buf];
     const uint16_t* vb_ = vs[buf];
-    const bool full = !a.causal || kt0 + FA_KT - 1 <= qb * FA_QB;
+    const bool full = (!a.causal || kt0 + FA_KT - 1 <= qb * FA_QB) && kt0 + FA_KT <= a.T;
 
     // ---- S^T = K Q^T (and dP^T = V dO^T): lane holds keys 16 kb + 4 g + i of query qrow
     f32x4 st[4], dp[BWD ? 4 : 1];
@@ -134,7 +138,8 @@ __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           float v = st[kb][i] * sc2;
-          if (!full && kt0 + 16 * kb + 4 * g + i > qrow) v = -INFINITY;
+          const int key = kt0 + 16 * kb + 4 * g + i;
+          if (!full && ((a.causal && key > qrow) || key >= a.T)) v = -INFINITY;
           st[kb][i] = v;
         }
       float tmax = -INFINITY;
@@ -205,6 +210,7 @@ __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     const float inv = l > 0.f ? 1.f / l : 0.f;
+    if (qrow >= a.T) return;
     uint16_t* op = a.out + ((size_t)(b * a.T + qrow) * a.Hq + h) * D;
 #pragma unroll
     for (int d = 0; d < DT; d++)
@@ -378,7 +384,7 @@ __global__ void __launch_bounds__(256) fa_delta_kernel(const TrainAttnArgs a) {
 
 template <typename T, int D>
 void launch_fwd_d(const TrainAttnArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((fa_q_kernel<T, D, false>), dim3(a.T / FA_QB, a.Hq, a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((fa_q_kernel<T, D, false>), dim3((a.T + FA_QB - 1) / FA_QB, a.Hq, a.B), dim3(256), 0, st, a);
 }
 
 template <typename T, int D>

@@ -54,14 +54,16 @@ void check_bhtd(const Tensor& t, const char* name) {
   TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0, name, ": 16-B aligned rows");
 }
 
-illm::TrainAttnArgs attn_args(const Tensor& q, const Tensor& k, const Tensor& v, double scale, bool causal) {
+illm::TrainAttnArgs attn_args(const Tensor& q, const Tensor& k, const Tensor& v, double scale, bool causal,
+                              bool ragged_ok = false) {
   check_bhtd(q, "q");
   check_bhtd(k, "k");
   check_bhtd(v, "v");
   const int64_t B = q.size(0), Hq = q.size(1), T = q.size(2), D = q.size(3), Hkv = k.size(1);
   TORCH_CHECK(k.size(0) == B && v.size(0) == B && k.size(2) == T && v.size(2) == T && k.size(3) == D &&
               v.size(3) == D && v.size(1) == Hkv && Hq % Hkv == 0, "train attention: shapes");
-  TORCH_CHECK(T % 64 == 0 && (D == 64 || D == 128), "train attention: T % 64 == 0, D in {64, 128}");
+  TORCH_CHECK((ragged_ok ? T > 0 : T % 64 == 0) && (D == 64 || D == 128),
+              "train attention: T % 64 == 0 (backward) / T > 0 (forward), D in {64, 128}");
   TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type(), "train attention: dtypes");
   illm::TrainAttnArgs a{};
   a.q = (const uint16_t*)q.data_ptr();
@@ -79,7 +81,7 @@ illm::TrainAttnArgs attn_args(const Tensor& q, const Tensor& k, const Tensor& v,
 // flash attention forward for training: (out [B, T, Hq, D], lse [B, Hq, T] log2 domain)
 std::vector<Tensor> train_attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, double scale, bool causal) {
   c10::DeviceGuard g(q.device());
-  illm::TrainAttnArgs a = attn_args(q, k, v, scale, causal);
+  illm::TrainAttnArgs a = attn_args(q, k, v, scale, causal, true);
   Tensor out = at::empty({q.size(0), q.size(2), q.size(1), q.size(3)}, q.options());
   Tensor lse = at::empty({q.size(0), q.size(1), q.size(2)}, q.options().dtype(at::kFloat));
   a.out = (uint16_t*)out.data_ptr();

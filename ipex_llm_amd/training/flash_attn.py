@@ -7,8 +7,12 @@ routes causal self-attention (no padding mask) through the hand-written
 gfx950 kernels of ``csrc/hip/train_attn.hip``: a forward that keeps only the
 per-row log-sum-exp, and a deterministic two-kernel backward (dK / dV per
 key block with the group's query heads swept in registers, dQ per query
-block).  Anything else (padding masks, dropout, sliding windows, soft-capping,
-head dims other than 64 / 128, T % 64 != 0) falls back to SDPA.
+block).  Bidirectional self-attention (``is_causal`` False: BERT / ViT /
+Whisper-encoder layers) takes the same forward without the causal mask, for
+any sequence length at inference (ragged tails masked in the kernel).
+Anything else (padding masks, dropout, sliding windows, soft-capping, head
+dims other than 64 / 128, cross-attention, T % 64 != 0 with gradients)
+falls back to SDPA.
 """
 from __future__ import annotations
 
@@ -51,15 +55,20 @@ def supported(q, k, v, attention_mask, dropout, kwargs) -> bool:
     if attention_mask is not None:
         return False
     B, Hq, T, D = q.shape
-    return (D in (64, 128) and T % 64 == 0 and k.shape[2] == T and Hq % k.shape[1] == 0
+    grad = torch.is_grad_enabled() and (q.requires_grad or k.requires_grad or v.requires_grad)
+    # the forward takes ragged T (encoders at inference); the backward needs T % 64 == 0
+    return (D in (64, 128) and (T % 64 == 0 or not grad) and k.shape[2] == T and Hq % k.shape[1] == 0
             and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1)
 
 
 def illm_flash_attention_forward(module, query, key, value, attention_mask, scaling: Optional[float] = None,
                                  dropout: float = 0.0, **kwargs):
-    if getattr(module, "is_causal", True) and supported(query, key, value, attention_mask,
-                                                        dropout if module.training else 0.0, kwargs):
-        return flash_attention(query, key, value, scaling, causal=True), None
+    """causal decoders (training) and bidirectional encoders (bert / vit /
+    whisper-encoder self-attention: ``module.is_causal`` False, no padding)"""
+    causal = kwargs.get("is_causal")
+    causal = bool(getattr(module, "is_causal", True) if causal is None else causal)
+    if supported(query, key, value, attention_mask, dropout if module.training else 0.0, kwargs):
+        return flash_attention(query, key, value, scaling, causal=causal), None
     from transformers.integrations.sdpa_attention import sdpa_attention_forward
     return sdpa_attention_forward(module, query, key, value, attention_mask, scaling=scaling, dropout=dropout,
                                   **kwargs)

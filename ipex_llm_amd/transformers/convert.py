@@ -38,6 +38,10 @@ NATIVE_ARCHS = {"llama", "mistral", "qwen2", "qwen3", "gemma", "gemma2", "phi3",
 # granite (embedding/residual/logit multipliers), stablelm (partial rotary + LayerNorm) and
 # starcoder2 (biased LayerNorm MLP, no q_proj split) take the HF forward over low-bit linears.
 MOE_ARCHS = {"mixtral", "qwen2_moe", "qwen3_moe"}
+# encoder / encoder-decoder families whose HF forward runs (reference
+# models/bert.py, whisper.py, mllama.py, minicpmv.py): attention on the HIP
+# flash kernel where it applies, linears low-bit
+ENCODER_FLASH_ARCHS = {"bert", "roberta", "xlm-roberta", "vit", "whisper", "clip", "siglip", "mllama"}
 
 
 # ----------------------------------------------------------------- pre
@@ -474,6 +478,11 @@ def _optimize_post(model: nn.Module):
     _patch_routers(model)
     from .attention import patch_eager_attention
     patch_eager_attention(model)
+    if mt in ENCODER_FLASH_ARCHS and getattr(model.config, "_attn_implementation", None) in (None, "sdpa"):
+        # bidirectional encoder self-attention on the HIP flash kernel
+        # (training/flash_attn.py; padded batches / cross-attention keep SDPA)
+        from ..training.flash_attn import patch_flash_attention
+        patch_flash_attention(model)
     if mt == "rwkv":
         from ..models.rwkv import patch_rwkv
         patch_rwkv()

@@ -80,3 +80,71 @@ def test_qwen2_vl_image_text_lowbit(tmp_path):
     assert _rel(got, want) < 5e-2
     from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
     assert any(isinstance(x, LowBitLinear) for x in m.modules())
+
+
+def test_mllama_image_text_lowbit():
+    """Llama-3.2-Vision layout: tiled vision encoder (local + global layers),
+    gated cross-attention layers in the text model (reference models/mllama.py)"""
+    import copy
+    import transformers as T
+    from ipex_llm_amd import optimize_model
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    vc = dict(hidden_size=64, num_hidden_layers=2, num_global_layers=1, attention_heads=4, intermediate_size=128,
+              image_size=28, patch_size=14, max_num_tiles=2, vision_output_dim=128, intermediate_layers_indices=[0],
+              supported_aspect_ratios=[[1, 1], [1, 2]])
+    tc = dict(vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+              num_key_value_heads=2, cross_attention_layers=[1], max_position_embeddings=256, pad_token_id=0,
+              bos_token_id=1, eos_token_id=2)
+    cfg = T.MllamaConfig(vision_config=vc, text_config=tc, image_token_index=290)
+    torch.manual_seed(0)
+    ref = T.MllamaForConditionalGeneration(cfg).eval()
+    with torch.no_grad():                   # open the cross-attention / MLP gates (zero at init)
+        for n, p in ref.named_parameters():
+            if "gate" in n and p.numel() == 1:
+                p.fill_(0.7)
+    ids = torch.randint(3, 280, (1, 10))
+    ids[0, 1] = 290
+    cam = torch.zeros(1, 10, 1, 2, dtype=torch.long)
+    cam[:, 1:, 0, :] = 1
+    kw = dict(input_ids=ids, pixel_values=torch.randn(1, 1, 2, 3, 28, 28), aspect_ratio_ids=torch.tensor([[2]]),
+              aspect_ratio_mask=torch.tensor([[[1, 1]]]), cross_attention_mask=cam)
+    with torch.no_grad():
+        want = ref(**kw).logits
+        m = optimize_model(copy.deepcopy(ref), low_bit="sym_int8")
+        got = m(**kw).logits
+    assert any(isinstance(x, LowBitLinear) for x in m.model.vision_model.modules())
+    assert any(isinstance(x, LowBitLinear) for x in m.model.language_model.modules())
+    assert _rel(got, want) < 5e-2
+    # the image matters: a different image changes the text logits
+    kw2 = dict(kw, pixel_values=torch.randn(1, 1, 2, 3, 28, 28))
+    with torch.no_grad():
+        assert _rel(m(**kw2).logits, got) > 1e-3
+
+
+def test_internvl_image_text_lowbit():
+    """InternVL layout: InternViT encoder + pixel-shuffle projector + LLM
+    (reference models/internvl.py)"""
+    import copy
+    import transformers as T
+    from ipex_llm_amd import optimize_model
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    vc = dict(hidden_size=64, num_hidden_layers=2, num_attention_heads=4, intermediate_size=128,
+              image_size=[28, 28], patch_size=[14, 14])
+    tc = dict(model_type="qwen2", vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+              num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256)
+    try:
+        cfg = T.InternVLConfig(vision_config=vc, text_config=tc, image_token_id=290, downsample_ratio=0.5)
+        torch.manual_seed(0)
+        ref = T.InternVLForConditionalGeneration(cfg).eval()
+    except (TypeError, ValueError) as e:               # pragma: no cover - config layout of other versions
+        pytest.skip(f"InternVLConfig layout: {e}")
+    n_img = ((28 // 14) ** 2) // 4                     # pixel shuffle 0.5: tokens per image
+    ids = torch.randint(3, 280, (1, 10))
+    ids[0, 1:1 + n_img] = 290
+    kw = dict(input_ids=ids, pixel_values=torch.randn(1, 3, 28, 28))
+    with torch.no_grad():
+        want = ref(**kw).logits
+        m = optimize_model(copy.deepcopy(ref), low_bit="sym_int8")
+        got = m(**kw).logits
+    assert any(isinstance(x, LowBitLinear) for x in m.modules())
+    assert _rel(got, want) < 5e-2
