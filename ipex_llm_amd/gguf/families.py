@@ -8,7 +8,9 @@ HF parameter names; the fused QKV weights llama.cpp stores as
 back into the HF row order so the regular conversion path (and the native
 generic decoder, models/generic.py) takes over.  baichuan-7B is a llama
 layout (llama.cpp splits ``W_pack`` and permutes q/k like llama); the ALiBi
-baichuan-13B needs remote code and is refused.
+baichuan-13B is refused, as in the reference, whose GGUF baichuan loader
+builds the RoPE model (``gguf/models/model_implement/baichuan/
+modeling_baichuan.py:95,184``).
 """
 from __future__ import annotations
 
