@@ -131,3 +131,40 @@ def test_qwen2_vl_gpu(tmp_path):
     e = m.generate(input_ids=ids.cuda(), pixel_values=pix.cuda(), image_grid_thw=thw.cuda(), mm_token_type_ids=mm.cuda(),
                    max_new_tokens=8, use_graph=False)
     assert torch.equal(g.cpu(), e.cpu())
+
+
+def test_yuan_lfa_gpu(tmp_path):
+    """Yuan 2.0 LFA on the native decoder (models/yuan.py): prefill, cached
+    single-token steps (the filter reads the slot-addressed h / conv cache)
+    and hipGraph decode == eager decode"""
+    from ipex_llm_amd.models.yuan import YuanConfig, YuanForCausalLM
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    torch.manual_seed(0)
+    ref = YuanForCausalLM(YuanConfig(vocab_size=V, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                                     num_attention_heads=4, max_position_embeddings=512)).eval()
+    with torch.no_grad():
+        for n, p in ref.named_parameters():
+            if p.dim() == 1:
+                p.add_(torch.randn_like(p) * 0.1)
+            elif "conv" in n:
+                p.mul_(4.0)
+    path = str(tmp_path / "yuan")
+    ref.save_pretrained(path)
+    ids = torch.randint(0, V, (1, 40))
+    with torch.no_grad():
+        want = ref(ids).logits.float()
+    m = AutoModelForCausalLM.from_pretrained(path, load_in_low_bit="sym_int8", torch_dtype=torch.bfloat16)
+    m = m.to("cuda").eval()
+    assert getattr(m, "_illm_native_attached", False)
+    with torch.no_grad():
+        out = m(ids[:, :32].cuda(), use_cache=True)
+        got = out.logits.float().cpu()
+        assert ((got - want[:, :32]).norm() / want[:, :32].norm()).item() < 5e-2
+        cache = out.past_key_values
+        for t in range(32, 40):
+            step = m(ids[:, t:t + 1].cuda(), past_key_values=cache).logits.float().cpu()
+            r = ((step[:, -1] - want[:, t]).norm() / want[:, t].norm()).item()
+            assert r < 5e-2, (t, r)
+        g = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=True)
+        e = m.generate(ids[:, :16].cuda(), max_new_tokens=12, do_sample=False, use_graph=False)
+    assert torch.equal(g.cpu(), e.cpu())
