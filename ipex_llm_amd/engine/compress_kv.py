@@ -36,6 +36,13 @@ def snapkv_compress(model, cache, seq: SequenceState, L: int, q_window: Dict[int
     Hkv, G, D = s.num_kv_heads, s.num_heads // s.num_kv_heads, s.head_dim
     keep_n = capacity - window
     dst = slots_for(seq, 0, capacity, cache.bs).to(dev)
+    lf = getattr(cache, "lf", None)
+    if lf is not None:
+        # Yuan LFA: the next step's filter reads the previous position's h /
+        # conv rows at cache index L - 1 - offset = capacity - 1
+        src_last = slots_for(seq, L - 1, 1, cache.bs).to(dev)
+        for t in lf:
+            t[dst[-1:]] = t[src_last]
     for li in range(len(model.layers)):
         kk = ops.api.gather_kv(cache.k[li], bt, 0, L, cache.kv_fp8, cache.k_scale, model.dtype)   # [L, Hkv, D]
         vv = ops.api.gather_kv(cache.v[li], bt, 0, L, cache.kv_fp8, cache.v_scale, model.dtype)

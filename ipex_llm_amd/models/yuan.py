@@ -289,7 +289,10 @@ class YuanLF(nn.Module):
         """cache slot of each token's previous position (zero_row at position 0)"""
         T = slots.shape[0]
         b = torch.arange(T, device=slots.device) // meta.Tq
-        pp = (pos.long() - 1).clamp_min(0)
+        pp = pos.long() - 1
+        if meta.pos_offset is not None:              # compressed KV: cache index = position - offset
+            pp = pp - meta.pos_offset.long()[b]
+        pp = pp.clamp_min(0)
         blk = meta.block_tables.long()[b, pp // bs]
         ps = blk * bs + pp % bs
         return torch.where(pos.long() > 0, ps, torch.full_like(ps, zero_row))
