@@ -1,0 +1,27 @@
+#!/bin/bash
+# round-4: training flash-attention timing + PMC passes (one counter group per run)
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+T="timeout -k 10"
+$T 120 python -u tools/attn_train_probe.py 512 > gpurun_out/attn_train_r4o.jsonl 2>&1 && \
+$T 120 python -u tools/attn_train_probe.py 2048 >> gpurun_out/attn_train_r4o.jsonl 2>&1
+rc=$?; grep T gpurun_out/attn_train_r4o.jsonl; [ $rc -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp
+$T 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_attn -o p1 -- python3 $GRAFT_REPO_ROOT/tools/attn_train_probe.py 512 > $GRAFT_REPO_ROOT/gpurun_out/pmc_attn.log 2>&1
+rc=$?; cd $GRAFT_REPO_ROOT; echo "pmc rc=$rc"
+python3 - <<'PY'
+import csv, glob, collections
+fs = glob.glob("gpurun_out/pmc_attn/**/*counter_collection.csv", recursive=True)
+agg = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
+for f in fs:
+    for r in csv.DictReader(open(f)):
+        k = r.get("Kernel_Name", "")[:70]
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        n[(k, r["Counter_Name"])] += 1
+with open("gpurun_out/pmc_attn_summary.txt", "w") as o:
+    for k, d in agg.items():
+        o.write(k + "\n")
+        for c, v in sorted(d.items()):
+            o.write(f"   {c:28s} {v:.4g} (n={n[(k, c)]})\n")
+print(open("gpurun_out/pmc_attn_summary.txt").read())
+PY
+rm -rf gpurun_out/pmc_attn
