@@ -36,10 +36,52 @@ namespace {
 constexpr int FA_KT = 64;   // keys per tile
 constexpr int FA_QB = 64;   // query rows per workgroup (forward / dQ)
 
+// ---- LDS-DMA tile staging ------------------------------------------------------
+// A [64 rows][D] 16-bit tile of a row-strided tensor goes straight to LDS
+// (buffer_load_dwordx4 ... lds: 1 KB per wave instruction, lane-linear
+// destination), swizzled on the SOURCE side into the pf_off layout: the lane
+// writing physical chunk p of row r fetches logical chunk p ^ (r & MSK).  No
+// register staging (the register form spilled to scratch and waited on its
+// own loads), the next tile in flight across the compute of the current one.
+// Issued from inline asm so hipcc does not drain vmcnt before the LDS reads.
+typedef int32_t ta_rsrc __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ ta_rsrc ta_make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t p = (uint64_t)(uintptr_t)base;
+  return ta_rsrc{(int32_t)(uint32_t)p, (int32_t)((uint32_t)(p >> 32) & 0xffffu), (int32_t)bytes, 0x00020000};
+}
+
+__device__ __forceinline__ uint32_t ta_lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p);
+}
+
+// rows row0 .. row0 + 63 (clamped to nrows - 1) of a tensor with row stride
+// `rstride` elements -> LDS tile at byte address `lds` (wave-uniform)
+template <int D>
+__device__ __forceinline__ void ta_stage(const ta_rsrc& rs, uint32_t lds, int row0, int64_t rstride, int nrows,
+                                         int wave, int lane) {
+  constexpr int CH = D / 8, MSK = CH >= 16 ? 15 : CH - 1;
+  constexpr int RPI = 64 / CH;                    // rows per wave instruction
+  constexpr int NI = 64 / RPI / 4;                // instructions per wave (4 waves)
+#pragma unroll
+  for (int i = 0; i < NI; i++) {
+    const int idx = wave * NI + i;
+    const int r = idx * RPI + lane / CH, pch = lane % CH;
+    const int srow = min(row0 + r, nrows - 1);
+    const uint32_t voff = (uint32_t)((int64_t)srow * rstride * 2) + (uint32_t)((pch ^ (r & MSK)) * 16);
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds + (uint32_t)(idx * RPI * D * 2));   // wave-uniform
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(m0), "v"(voff), "s"(rs), "s"(0) : "memory", "m0");
+  }
+}
+
+__device__ __forceinline__ void ta_wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // ---- forward (with_dq = false) and dQ (with_dq = true) --------------------
 template <typename T, int D, bool BWD>
 __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
-  constexpr int KSTEP = D / 32, DT = D / 16, UPT = FA_KT * D / 8 / 256;
+  constexpr int KSTEP = D / 32, DT = D / 16;
   __shared__ __attribute__((aligned(16))) uint16_t ks[2][FA_KT * D];
   __shared__ __attribute__((aligned(16))) uint16_t vs[2][FA_KT * D];
   const int nqb = gridDim.x;
@@ -76,25 +118,13 @@ __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
 
   const uint16_t* kbase = a.k + (size_t)b * a.ksb + (size_t)kvh * a.ksh;
   const uint16_t* vbase = a.v + (size_t)b * a.vsb + (size_t)kvh * a.vsh;
-  uint4 kreg[UPT], vreg[UPT];
-  auto load_tile = [&](int t) {
-#pragma unroll
-    for (int j = 0; j < UPT; j++) {
-      const int u = tid + 256 * j;
-      const int r = u / (D / 8), c = u % (D / 8);
-      const int kr = min(t * FA_KT + r, a.T - 1);
-      kreg[j] = *(const uint4*)(kbase + (size_t)kr * a.kst + c * 8);
-      vreg[j] = *(const uint4*)(vbase + (size_t)kr * a.vst + c * 8);
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < UPT; j++) {
-      const int u = tid + 256 * j;
-      const int r = u / (D / 8), c = u % (D / 8);
-      *(uint4*)(ks[buf] + pf_off<D>(r, c)) = kreg[j];
-      *(uint4*)(vs[buf] + pf_off<D>(r, c)) = vreg[j];
-    }
+  const ta_rsrc rk = ta_make_rsrc(kbase, (uint32_t)(((int64_t)(a.T - 1) * a.kst + D) * 2));
+  const ta_rsrc rv = ta_make_rsrc(vbase, (uint32_t)(((int64_t)(a.T - 1) * a.vst + D) * 2));
+  const uint32_t ks_l = ta_lds_addr(ks), vs_l = ta_lds_addr(vs);
+  constexpr uint32_t TILE_B = FA_KT * D * 2;
+  auto stage = [&](int t, int buf) {
+    ta_stage<D>(rk, ks_l + buf * TILE_B, t * FA_KT, a.kst, a.T, wave, lane);
+    ta_stage<D>(rv, vs_l + buf * TILE_B, t * FA_KT, a.vst, a.T, wave, lane);
   };
 
   f32x4 o[DT];                                 // forward: O^T; backward: dQ^T
@@ -104,12 +134,21 @@ __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
   constexpr float kLog2e = 1.4426950408889634f;
   const float sc2 = a.scale * kLog2e;
 
-  load_tile(0);
-  store_tile(0);
+  stage(0, 0);
+  // the Q / dO fragments (and LSE / delta) are consumed here, so hipcc's own
+  // vmcnt waits for them sit before the loop, not at its head where they
+  // would also drain the next tile's DMA every iteration
+#pragma unroll
+  for (int s2 = 0; s2 < KSTEP; s2++) {
+    asm volatile("" :: "v"(qf[s2].x), "v"(qf[s2].y), "v"(qf[s2].z), "v"(qf[s2].w));
+    if constexpr (BWD) asm volatile("" :: "v"(df[s2].x), "v"(df[s2].y), "v"(df[s2].z), "v"(df[s2].w));
+  }
+  if constexpr (BWD) asm volatile("" :: "v"(lse2), "v"(delta));
+  ta_wait_vm0();
   __syncthreads();
   for (int t = 0; t < ntile; t++) {
     const int buf = t & 1;
-    if (t + 1 < ntile) load_tile(t + 1);
+    if (t + 1 < ntile) stage(t + 1, buf ^ 1);   // buffer last read in iteration t - 1
     const int kt0 = t * FA_KT;
     const uint16_t* kb_ = ks[buf];
     const uint16_t* vb_ = vs[buf];
@@ -200,7 +239,7 @@ __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
         o[d] = mfma16<T>(va, pb, o[d]);
       }
     }
-    if (t + 1 < ntile) store_tile(buf ^ 1);
+    ta_wait_vm0();                               // tile t + 1 landed (this wave's pieces)
     __syncthreads();
   }
 
@@ -230,7 +269,7 @@ __global__ void __launch_bounds__(256) fa_q_kernel(const TrainAttnArgs a) {
 // ---- dK / dV -----------------------------------------------------------------
 template <typename T, int D>
 __global__ void __launch_bounds__(256) fa_dkdv_kernel(const TrainAttnArgs a) {
-  constexpr int KSTEP = D / 32, DT = D / 16, UPT = FA_QB * D / 8 / 256;
+  constexpr int KSTEP = D / 32, DT = D / 16;
   __shared__ __attribute__((aligned(16))) uint16_t qs[2][FA_QB * D];
   __shared__ __attribute__((aligned(16))) uint16_t os[2][FA_QB * D];   // dO tile
   __shared__ float ls[2][2 * FA_QB];                                   // LSE2, delta of the tile's rows
@@ -256,32 +295,23 @@ __global__ void __launch_bounds__(256) fa_dkdv_kernel(const TrainAttnArgs a) {
   const int qb0 = a.causal ? kb : 0;                                   // first query block that sees these keys
   const int nqb = a.T / FA_QB - qb0;
   const int nwork = G * nqb;                                           // (head, query block) pairs
-  uint4 qreg[UPT], oreg[UPT];
   float lreg = 0.f;
-  auto load_tile = [&](int w) {
+  const uint32_t qs_l = ta_lds_addr(qs), os_l = ta_lds_addr(os);
+  constexpr uint32_t TILE_B = FA_QB * D * 2;
+  auto load_tile = [&](int w, int buf) {
     const int hh = kvh * G + w / nqb, qb = qb0 + w % nqb;
     const uint16_t* qp = a.q + (size_t)b * a.qsb + (size_t)hh * a.qsh;
     const uint16_t* dp = a.dout + (size_t)b * a.dsb + (size_t)hh * a.dsh;
-#pragma unroll
-    for (int j = 0; j < UPT; j++) {
-      const int u = tid + 256 * j;
-      const int r = u / (D / 8), c = u % (D / 8);
-      qreg[j] = *(const uint4*)(qp + (size_t)(qb * FA_QB + r) * a.qst + c * 8);
-      oreg[j] = *(const uint4*)(dp + (size_t)(qb * FA_QB + r) * a.dst + c * 8);
-    }
+    ta_stage<D>(ta_make_rsrc(qp, (uint32_t)(((int64_t)(a.T - 1) * a.qst + D) * 2)), qs_l + buf * TILE_B,
+                qb * FA_QB, a.qst, a.T, wave, lane);
+    ta_stage<D>(ta_make_rsrc(dp, (uint32_t)(((int64_t)(a.T - 1) * a.dst + D) * 2)), os_l + buf * TILE_B,
+                qb * FA_QB, a.dst, a.T, wave, lane);
     if (tid < 2 * FA_QB) {
       const size_t ri = ((size_t)b * a.Hq + hh) * a.T + qb * FA_QB + (tid & (FA_QB - 1));
       lreg = tid < FA_QB ? a.lse[ri] : a.delta[ri];
     }
   };
   auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < UPT; j++) {
-      const int u = tid + 256 * j;
-      const int r = u / (D / 8), c = u % (D / 8);
-      *(uint4*)(qs[buf] + pf_off<D>(r, c)) = qreg[j];
-      *(uint4*)(os[buf] + pf_off<D>(r, c)) = oreg[j];
-    }
     if (tid < 2 * FA_QB) ls[buf][tid] = lreg;
   };
 
@@ -292,13 +322,14 @@ __global__ void __launch_bounds__(256) fa_dkdv_kernel(const TrainAttnArgs a) {
   const float sc2 = a.scale * kLog2e;
 
   if (nwork > 0) {
-    load_tile(0);
+    load_tile(0, 0);
+    ta_wait_vm0();
     store_tile(0);
   }
   __syncthreads();
   for (int w = 0; w < nwork; w++) {
     const int buf = w & 1;
-    if (w + 1 < nwork) load_tile(w + 1);
+    if (w + 1 < nwork) load_tile(w + 1, buf ^ 1);
     const int qb = qb0 + w % nqb;
     const bool diag = a.causal && qb == kb;
     const uint16_t* qb_ = qs[buf];
@@ -347,6 +378,7 @@ __global__ void __launch_bounds__(256) fa_dkdv_kernel(const TrainAttnArgs a) {
         dk[d] = mfma16<T>(da, make_uint4(q0.x, q0.y, q1.x, q1.y), dk[d]);
       }
     }
+    ta_wait_vm0();                               // Q / dO tiles and the LSE / delta row of w + 1
     if (w + 1 < nwork) store_tile(buf ^ 1);
     __syncthreads();
   }

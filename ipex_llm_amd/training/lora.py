@@ -119,9 +119,12 @@ class _LoraLowBitFn(torch.autograd.Function):
         x2, xa, A, B = ctx.saved_tensors
         g2 = g.reshape(-1, g.shape[-1]).to(x2.dtype)
         s = ctx.s
-        gxa = torch.mm(g2, B).mul_(s)                     # [M, r]
+        # the LoRA scale rides on the GEMMs' alpha (beta = 0: the 1-element
+        # input is never read) instead of separate [M, r] / [N, r] scale launches
+        z = g2.new_empty(())                               # (no fill launch)
+        gxa = torch.addmm(z, g2, B, beta=0, alpha=s)      # [M, r]
         gA = torch.mm(gxa.t(), x2) if ctx.needs_input_grad[1] else None
-        gB = torch.mm(g2.t(), xa).mul_(s) if ctx.needs_input_grad[2] else None
+        gB = torch.addmm(z, g2.t(), xa, beta=0, alpha=s) if ctx.needs_input_grad[2] else None
         gx = None
         if ctx.needs_input_grad[0]:
             base = ctx.base

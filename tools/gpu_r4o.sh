@@ -2,6 +2,8 @@
 # round-4: training flash-attention timing + PMC passes (one counter group per run)
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 T="timeout -k 10"
+$T 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_train_kernels.py tests/test_gpu_encoders.py > gpurun_out/t_r4o.log 2>&1
+rc=$?; tail -3 gpurun_out/t_r4o.log; [ $rc -eq 0 ] || exit $rc
 $T 120 python -u tools/attn_train_probe.py 512 > gpurun_out/attn_train_r4o.jsonl 2>&1 && \
 $T 120 python -u tools/attn_train_probe.py 2048 >> gpurun_out/attn_train_r4o.jsonl 2>&1
 rc=$?; grep T gpurun_out/attn_train_r4o.jsonl; [ $rc -eq 0 ] || exit $rc
