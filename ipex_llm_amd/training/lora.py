@@ -78,6 +78,9 @@ DEFAULT_TARGETS = ["q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj
 
 
 _FUSED = os.environ.get("ILLM_LORA_FUSED", "1") == "1"
+# sibling adapters over one input (q/k/v, gate/up) as one autograd node
+_GROUP = os.environ.get("ILLM_LORA_GROUP", "1") == "1"
+_GROUPS = (("q_proj", "k_proj", "v_proj"), ("gate_proj", "up_proj"))
 
 
 def _base_dense_weight(base, dt):
@@ -139,6 +142,71 @@ class _LoraLowBitFn(torch.autograd.Function):
             gx.addmm_(gxa, A)
             gx = gx.view(ctx.shp)
         return gx, gA, gB, None, None
+
+
+class _LoraGroupFn(torch.autograd.Function):
+    """q / k / v (or gate / up) adapters over ONE shared input as one
+    autograd node: x A_all^T for all siblings in one pass over x (A_all =
+    [A_q; A_k; A_v]), each base GEMM + its rank-r add as in _LoraLowBitFn;
+    backward reads x once more for every dA (gxa_all^T x), accumulates
+    grad_x = sum_i g_i W_i + gxa_all A_all into one buffer (beta = 1 GEMMs)
+    instead of per-sibling outputs summed by autograd.  Same math as the
+    per-module path, fewer passes over the [tokens, hidden] activations."""
+
+    @staticmethod
+    def forward(ctx, x, s, bases, *AB):
+        from .. import ops
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        As, Bs = AB[0::2], AB[1::2]
+        with torch.no_grad():
+            xa_all = torch.mm(x2, torch.cat(As, 0).t())          # [M, sum r]
+            ys, off = [], 0
+            for base, A, B in zip(bases, As, Bs):
+                r = A.shape[0]
+                bias = base.bias
+                if bias is not None and bias.dtype != x2.dtype:
+                    bias = bias.to(x2.dtype)
+                y = ops.lowbit_matmul(x2, base.weight, base.fmt, base.out_features, base.in_features, bias)
+                y.addmm_(xa_all[:, off:off + r], B.t(), alpha=s)
+                ys.append(y.view(*shp[:-1], y.shape[-1]))
+                off += r
+        ctx.save_for_backward(x2, xa_all, *AB)
+        ctx.s, ctx.shp, ctx.bases = s, shp, bases
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        x2, xa_all, *AB = ctx.saved_tensors
+        As, Bs = AB[0::2], AB[1::2]
+        s = ctx.s
+        z = x2.new_empty(())
+        gxas, grads, gx, off = [], [], None, 0
+        for base, A, B, g in zip(ctx.bases, As, Bs, gs):
+            r = A.shape[0]
+            if g is None:
+                gxas.append(x2.new_zeros(x2.shape[0], r))
+                grads.append((None, torch.zeros_like(B)))
+                off += r
+                continue
+            g2 = g.reshape(-1, g.shape[-1]).to(x2.dtype)
+            gxas.append(torch.addmm(z, g2, B, beta=0, alpha=s))
+            grads.append((None, torch.addmm(z, g2.t(), xa_all[:, off:off + r], beta=0, alpha=s)))
+            if ctx.needs_input_grad[0]:
+                w = _base_dense_weight(base, x2.dtype)
+                gx = torch.mm(g2, w) if gx is None else gx.addmm_(g2, w)
+            off += r
+        gxa_all = torch.cat(gxas, 1)
+        gA_all = torch.mm(gxa_all.t(), x2)                         # [sum r, K]: one pass over x
+        if gx is not None:
+            gx.addmm_(gxa_all, torch.cat(As, 0))
+            gx = gx.view(ctx.shp)
+        out, off = [], 0
+        for (A, (_, gB)) in zip(As, grads):
+            r = A.shape[0]
+            out += [gA_all[off:off + r], gB]
+            off += r
+        return (gx, None, None, *out)
 
 
 class _LoraEngineFn(torch.autograd.Function):
@@ -247,8 +315,37 @@ class LoraLinear(nn.Module):
                 and x.dtype == self.lora_A.weight.dtype and x.dtype in (torch.bfloat16, torch.float16)
                 and x.device == b.weight.device and (x.requires_grad or self.lora_A.weight.requires_grad))
 
+    def _group_forward(self, x):
+        """sibling adapters sharing this input (get_peft_model links q/k/v and
+        gate/up): the first one computes every sibling's output in one
+        _LoraGroupFn node, the others pick theirs up (same input tensor)"""
+        grp = self.__dict__.get("_lora_group")
+        if not grp or not _GROUP:
+            return None
+        key = (id(x), x._version, x.data_ptr())
+        cache = grp["cache"]
+        if cache is not None and cache[0] == key and self in cache[1]:
+            out = cache[1].pop(self)
+            if not cache[1]:
+                grp["cache"] = None
+            return out
+        mods = grp["mods"]
+        if self is not mods[0] or not all(m._fused_ok(x) and not (m.disable_adapters or m.merged) for m in mods) \
+                or len({m.scaling for m in mods}) != 1 or any(_engine_lora_ok(m.base_layer, x, m.lora_A.weight)
+                                                              for m in mods):
+            return None
+        ab = []
+        for m in mods:
+            ab += [m.lora_A.weight, m.lora_B.weight]
+        ys = _LoraGroupFn.apply(x, self.scaling, [m.base_layer for m in mods], *ab)
+        grp["cache"] = (key, {m: y for m, y in zip(mods[1:], ys[1:])})
+        return ys[0]
+
     def forward(self, x):
         if not (self.disable_adapters or self.merged) and self._fused_ok(x):
+            y = self._group_forward(x)
+            if y is not None:
+                return y
             if _engine_lora_ok(self.base_layer, x, self.lora_A.weight):
                 return _LoraEngineFn.apply(x, self.lora_A.weight, self.lora_B.weight, self.base_layer, self.scaling)
             return _LoraLowBitFn.apply(x, self.lora_A.weight, self.lora_B.weight, self.base_layer, self.scaling)
@@ -400,11 +497,28 @@ def get_peft_model(model: nn.Module, config: LoraConfig, adapter_name: str = "de
             n += 1
     if n == 0:
         raise ValueError(f"no module matched target_modules={config.target_modules}")
+    link_lora_groups(model)
     if config.modules_to_save:
         for pn, p in model.named_parameters():
             if any(s in pn for s in config.modules_to_save) and p.is_floating_point():
                 p.requires_grad_(True)
     return PeftModel(model, config)
+
+
+def link_lora_groups(model: nn.Module) -> int:
+    """link sibling LoraLinear modules that read the same input (a parent's
+    q/k/v, gate/up) for the grouped forward; returns the number of groups"""
+    n = 0
+    for mod in model.modules():
+        for names in _GROUPS:
+            mods = [getattr(mod, c, None) for c in names]
+            if all(isinstance(m, LoraLinear) for m in mods) and \
+                    len({m.in_features for m in mods}) == 1:
+                grp = {"mods": mods, "cache": None}
+                for m in mods:
+                    m.__dict__["_lora_group"] = grp
+                n += 1
+    return n
 
 
 def prepare_model_for_kbit_training(model: nn.Module, use_gradient_checkpointing: bool = True) -> nn.Module:

@@ -313,3 +313,55 @@ def test_fused_adamw_state_dict_round_trip_keeps_step():
     opt.step()
     opt2.step()
     assert torch.allclose(p, q) and opt2.state[q]["step"] == 4
+
+
+def test_grouped_lora_siblings_match_per_module(monkeypatch):
+    """q/k/v and gate/up adapters over one input as one _LoraGroupFn node ==
+    the per-module fused nodes: outputs, grad_x and every adapter gradient"""
+    import torch.nn as nn
+    from ipex_llm_amd.training import lora as L
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+
+    class Blk(nn.Module):
+        def __init__(self):
+            super().__init__()
+            for n, o in (("q_proj", 256), ("k_proj", 128), ("v_proj", 128), ("gate_proj", 384), ("up_proj", 384)):
+                m = LowBitLinear(256, o, "sym_int8", bias=False, device="meta")
+                m.load_dense(torch.randn(o, 256) * 0.05, device="cpu")
+                setattr(self, n, m)
+
+        def forward(self, x):
+            return (self.q_proj(x).sum() + 2 * self.k_proj(x).sum() + (self.v_proj(x) ** 2).sum()
+                    + (self.gate_proj(x) * self.up_proj(x)).sum())
+
+    torch.manual_seed(0)
+    blk = Blk()
+    model = L.get_peft_model(blk, L.LoraConfig(r=4, lora_alpha=8, target_modules=["q_proj", "k_proj", "v_proj",
+                                                                                     "gate_proj", "up_proj"]))
+    assert L.link_lora_groups(blk) == 2
+    for m in model.lora_modules().values():
+        m.to(torch.bfloat16)
+        with torch.no_grad():
+            m.lora_B.weight.normal_(0, 0.05)
+    x0 = torch.randn(2, 7, 256, dtype=torch.bfloat16)
+
+    def run(group):
+        monkeypatch.setattr(L, "_GROUP", group)
+        calls = []
+        orig = L._LoraGroupFn.forward
+        monkeypatch.setattr(L._LoraGroupFn, "forward", staticmethod(lambda *a: calls.append(1) or orig(*a)))
+        for p in model.parameters():
+            p.grad = None
+        x = x0.clone().requires_grad_(True)
+        out = blk(x)
+        out.backward()
+        grads = {n: p.grad.float().clone() for n, p in model.named_parameters() if p.requires_grad}
+        return out.float(), x.grad.float(), grads, len(calls)
+    o1, gx1, g1, n1 = run(True)
+    o0, gx0, g0, n0 = run(False)
+    assert n1 == 2 and n0 == 0
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()      # noqa: E731  (bf16 summation order differs)
+    assert rel(o1, o0) < 1e-2
+    assert rel(gx1, gx0) < 2e-2
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 2e-2, k
