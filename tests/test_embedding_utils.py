@@ -21,7 +21,9 @@ def test_embedding_variants_match(tmp_path):
     base = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32)
     with torch.no_grad():
         ref = base(ids).logits
-    for kw, cls, tol in (({"cpu_embedding": True}, CPUEmbedding, 1e-5), ({"disk_embedding": True}, DiskEmbedding, 5e-3),
+    # disk embeddings are fp16: the ~5e-4 input change moves some codes of the
+    # CPU GEMM's per-token int8 activations by one step (csrc/cpu/gemm_q4.cpp)
+    for kw, cls, tol in (({"cpu_embedding": True}, CPUEmbedding, 1e-5), ({"disk_embedding": True}, DiskEmbedding, 3e-2),
                          ({"embedding_qtype": "sym_int8"}, LowBitEmbedding, 5e-2)):
         m = AutoModelForCausalLM.from_pretrained(p, load_in_low_bit="sym_int8", torch_dtype=torch.float32, **kw)
         assert isinstance(m.model.embed_tokens, cls)

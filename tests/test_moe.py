@@ -101,4 +101,6 @@ def test_hf_lowbit_experts_matches_dequantized_bank():
     idx = torch.tensor([[0, 1], [2, 3], [1, 2], [3, 0], [2, 1]])
     w = torch.rand(5, 2)
     with torch.no_grad():
-        assert torch.allclose(q(x, idx, w), ex(x, idx, w), atol=1e-4, rtol=1e-3)
+        # the CPU expert GEMMs quantize activations to int8 per 64-block (sym_int8 x q8 dots)
+        a, b = q(x, idx, w), ex(x, idx, w)
+        assert ((a - b).norm() / b.norm()).item() < 2e-2

@@ -77,8 +77,9 @@ def test_cpu_lowbit_gemm_matches_reference():
         x = torch.randn(5, 256)
         ref = x @ R.dequantize_canonical(blob, f, 96, 256).t()
         y = ops.lowbit_matmul(x, blob, f, 96, 256)
-        if name in ("sym_int4", "asym_int4"):
-            # int8-activation integer-dot path (per-64-block activation scales)
+        if name in ("sym_int4", "asym_int4", "sym_int8"):
+            # int8-activation integer-dot path (per-64-block activation scales;
+            # ggml's q4_0 / q8_0 x q8_0 dots do the same)
             assert ((y - ref).norm() / ref.norm()).item() < 1.5e-2
         else:
             assert torch.allclose(y, ref, rtol=1e-4, atol=1e-4)

@@ -13,7 +13,7 @@ def native():
     from ipex_llm_amd.models.builder import random_native_model
     cfg = LlamaConfig(vocab_size=128, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=1024)
-    return random_native_model(cfg, "sym_int8", "cpu", torch.float32, seed=0, std=0.2)
+    return random_native_model(cfg, "fp8_e4m3", "cpu", torch.float32, seed=0, std=0.2)
 
 
 def _sched(nb=4, bs=64, mb=8, mp=4096):

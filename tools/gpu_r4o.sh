@@ -27,3 +27,9 @@ with open("gpurun_out/pmc_attn_summary.txt", "w") as o:
 print(open("gpurun_out/pmc_attn_summary.txt").read())
 PY
 rm -rf gpurun_out/pmc_attn
+# QLoRA A/B on the same box: default (grouped LoRA, DMA attention), per-module LoRA, dense shadow
+T="timeout -k 10"
+$T 300 python -u tools/bench_qlora.py --steps 6 --warmup 2 > gpurun_out/qlora_r4o_default.json 2>&1 && \
+ILLM_LORA_GROUP=0 $T 300 python -u tools/bench_qlora.py --steps 6 --warmup 2 > gpurun_out/qlora_r4o_nogroup.json 2>&1 && \
+ILLM_PREFILL_DENSE_GB=40 $T 300 python -u tools/bench_qlora.py --steps 6 --warmup 2 > gpurun_out/qlora_r4o_shadow.json 2>&1
+rc=$?; grep -h ms_per_step gpurun_out/qlora_r4o_*.json | cut -c1-200; exit $rc
