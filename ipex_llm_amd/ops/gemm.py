@@ -99,6 +99,15 @@ _dense_cache = {}            # (blob ptr, version, n, k, dtype) -> dense weight
 _dense_bytes = [0]
 
 
+def set_dense_budget(gb: float) -> None:
+    """budget (GiB) of dequantized weights kept resident by ``_dense_weight``
+    (frozen low-bit weights: the cache never goes stale); 0 disables"""
+    global _DENSE_BUDGET
+    _DENSE_BUDGET = float(gb) * 2 ** 30
+    if _DENSE_BUDGET <= 0:
+        dense_cache_clear()
+
+
 def dense_cache_clear() -> None:
     _dense_cache.clear()
     _dense_bytes[0] = 0

@@ -557,6 +557,21 @@ def enable_training_kernels(model: nn.Module) -> nn.Module:
     if os.environ.get("ILLM_TRAIN_ATTN", "1") == "1":
         from .flash_attn import patch_flash_attention
         patch_flash_attention(model)
+    # the frozen low-bit base dequantized once and kept resident for the
+    # forward and grad_x GEMMs (exactly the per-step dequant's values) when
+    # HBM allows: on a 288 GB MI355X a Llama-3-8B base costs 15 GB and saves
+    # the 448 dequant launches of every step.  ILLM_TRAIN_DENSE_GB=<GiB> sets
+    # the budget, 0 keeps the pure low-bit footprint.
+    gb = os.environ.get("ILLM_TRAIN_DENSE_GB", "auto")
+    if gb == "auto":
+        total = torch.cuda.get_device_properties(w.device).total_memory / 2 ** 30
+        gb = min(48.0, 0.25 * total) if total >= 128 else 0.0
+    gb = float(gb)
+    if gb > 0:
+        from ..ops.gemm import _DENSE_BUDGET, set_dense_budget
+        if _DENSE_BUDGET < gb * 2 ** 30:
+            set_dense_budget(gb)
+    model._illm_train_dense_gb = gb
     return model
 
 

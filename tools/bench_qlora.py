@@ -175,7 +175,7 @@ def main():
         "config": {"model": "Llama-3-8B" if not args.layers else f"Llama-3-8B[{args.layers} layers]",
                    "batch": args.batch, "seq_len": args.seq, "lora_r": args.rank,
                    "targets": "q,k,v,o,gate,up,down", "grad_ckpt": args.grad_ckpt, "optimizer": "FusedAdamW",
-                   "hipgraph": args.graph},
+                   "hipgraph": args.graph, "dense_base_cache_gb": getattr(model, "_illm_train_dense_gb", 0.0)},
         "trainable_params": n_train, "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
         "build_s": round(build_s, 1), "loss_first": round(losses[0], 4), "loss_last": round(losses[-1], 4),
     }), flush=True)
