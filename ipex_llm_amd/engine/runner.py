@@ -179,6 +179,7 @@ class Engine:
         self.block_size = block_size
         self.kv_fp8 = kv_fp8
         self._steps: Dict[Tuple[int, int], DecodeStep] = {}
+        self._pf_graphs: Dict[Tuple[int, int, int], tuple] = {}
         self.cache: Optional[PagedKVCache] = None
         self._cache_key = None
 
@@ -187,6 +188,7 @@ class Engine:
         if self.cache is None or self.cache.num_blocks < blocks:
             self.cache = self.model.make_cache(max_len, batch, self.block_size, self.kv_fp8, num_blocks=blocks)
             self._steps.clear()
+            self._pf_graphs.clear()
         else:
             self.cache.allocator = type(self.cache.allocator)(self.cache.num_blocks)
         return self.cache
@@ -213,22 +215,75 @@ class Engine:
         return logits
 
     @torch.no_grad()
-    def prefill_batch(self, seqs: List[SequenceState], ids: torch.Tensor) -> torch.Tensor:
+    def prefill_batch(self, seqs: List[SequenceState], ids: torch.Tensor, use_graph: bool = False) -> torch.Tensor:
         """Prefill B equal-length prompts (ids [B, n]) in ONE forward: the
         projections run as [B*n, K] GEMMs (weights read once for the whole
-        batch), attention per sequence.  Returns last-token logits [B, V]."""
+        batch), attention per sequence.  Returns last-token logits [B, V].
+
+        ``use_graph``: the forward is captured once per (B, n, blocks) shape
+        as a hipGraph and replayed (token ids, cache slots and block table
+        copied into its static inputs): the ~15 launches per layer leave the
+        host path -- the first-token analogue of the decode-step graph.
+        Dense native decoders on one GPU only (no MoE routing / TP / EP)."""
         m, c = self.model, self.cache
         dev = m.device
         B, n = ids.shape
+        nb = max(len(s.blocks) for s in seqs)
+        if use_graph and self._pf_graph_ok():
+            key = (B, n, nb)
+            ent = self._pf_graphs.get(key)
+            fresh = ent is None
+            if fresh:
+                ent = self._prefill_buffers(B, n, nb)
+            graph, ids_s, slots_s, bt_s, out, meta, pos, lidx = ent
+            ids_s.copy_(ids.reshape(-1).to(dev), non_blocking=True)
+            slots_s.copy_(torch.cat([slots_for(s, 0, n, c.bs) for s in seqs]).to(dev), non_blocking=True)
+            bt_s.copy_(make_block_table(seqs, nb, dev))
+            if fresh:
+                # warm-up (lazy library state) writes exactly these sequences'
+                # KV, then the capture (which does not execute)
+                side = torch.cuda.Stream(device=dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):
+                    m.forward_tokens(ids_s, pos, slots_s, meta, c, logits_idx=lidx)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    out = m.forward_tokens(ids_s, pos, slots_s, meta, c, logits_idx=lidx)
+                ent = (graph, ids_s, slots_s, bt_s, out, meta, pos, lidx)
+                self._pf_graphs[key] = ent
+            graph.replay()
+            for s in seqs:
+                s.length = n
+            return out.clone()
         pos = torch.arange(n, device=dev).repeat(B)
         slots = torch.cat([slots_for(s, 0, n, c.bs) for s in seqs]).to(dev)
-        bt = make_block_table(seqs, max(len(s.blocks) for s in seqs), dev)
+        bt = make_block_table(seqs, nb, dev)
         meta = AttnMeta(B, n, bt, torch.full((B,), n, dtype=torch.int32, device=dev), nsplit_for(n), [n] * B)
         logits = m.forward_tokens(ids.reshape(-1).to(dev), pos, slots, meta, c,
                                   logits_idx=torch.arange(B, device=dev) * n + (n - 1))
         for s in seqs:
             s.length = n
         return logits
+
+    def _pf_graph_ok(self) -> bool:
+        m = self.model
+        dev = getattr(m, "device", None)
+        if dev is None or dev.type != "cuda" or getattr(m, "tp_group", None) is not None:
+            return False
+        from ..models.decoder import NativeMLP
+        return all(isinstance(L.mlp, NativeMLP) for L in getattr(m, "layers", [])) and m.graph_max_batch() > 0
+
+    def _prefill_buffers(self, B: int, n: int, nb: int):
+        """static inputs of a captured prefill (graph / output filled on first use)"""
+        dev = self.model.device
+        ids_s = torch.zeros(B * n, dtype=torch.long, device=dev)
+        slots_s = torch.zeros(B * n, dtype=torch.long, device=dev)
+        bt_s = torch.zeros(B, nb, dtype=torch.int32, device=dev)
+        pos = torch.arange(n, device=dev).repeat(B)
+        meta = AttnMeta(B, n, bt_s, torch.full((B,), n, dtype=torch.int32, device=dev), nsplit_for(n), [n] * B)
+        lidx = torch.arange(B, device=dev) * n + (n - 1)
+        return None, ids_s, slots_s, bt_s, None, meta, pos, lidx
 
     @torch.no_grad()
     def forward_chunk(self, seq: SequenceState, tokens: Sequence[int], start: int) -> torch.Tensor:

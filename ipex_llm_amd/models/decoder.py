@@ -626,7 +626,7 @@ class NativeCausalLM(nn.Module):
         from ..utils import trace as _trace
         # prefill on the library GEMM path: dense weights of layer li + 1 are
         # dequantized on a side stream while layer li computes
-        pf = T > ops.GEMV_MAX_M and x.is_cuda and ops.native_gpu(x)
+        pf = T > ops.GEMV_MAX_M and x.is_cuda and ops.native_gpu(x) and not torch.cuda.is_current_stream_capturing()
         if pf:
             from ..ops.gemm import drop_prefetched, prefetch_dense
             drop_prefetched()          # entries of an earlier (aborted) forward are keyed by possibly reused pointers

@@ -57,3 +57,36 @@ def test_compress_kv_graph_decode_on_gpu(cuda):
     graph = Engine(m).generate(prompt, max_new_tokens=12, use_graph=True, compress_kv=True,
                                compress_capacity=192, compress_window=32)
     assert eager == graph and len(graph[0]) == 399 + 12
+
+
+@pytest.mark.parametrize("B,n", [(1, 200), (4, 520)])
+def test_graph_prefill_matches_eager(cuda, B, n):
+    """Engine.prefill_batch(use_graph=True): captured once per shape (first
+    call: warm-up + capture + replay), later calls replay with new prompts /
+    slots / block tables -- logits and the written KV (via the following
+    graph decode) equal the eager prefill's"""
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.models.cache import SequenceState
+    m = random_native_model(_cfg(), "sym_int4", cuda, torch.bfloat16, seed=11)
+    e = Engine(m)
+    max_len = n + 32
+    e._ensure_cache(2 * B, max_len)
+    nblk = (max_len + e.block_size - 1) // e.block_size
+    g = torch.Generator().manual_seed(1)
+    res = {}
+    for trial in range(3):                       # trial 0 captures, 1-2 replay (new prompts on trial 2)
+        prompts = torch.randint(0, 1024, (B, n), generator=g if trial == 2 else torch.Generator().manual_seed(0))
+        for mode in (False, True):
+            e.cache.allocator = type(e.cache.allocator)(e.cache.num_blocks)
+            seqs = [SequenceState(e.cache.allocator.alloc(nblk)) for _ in range(B)]
+            if mode:                             # different blocks than the eager run: the table is an input
+                seqs = [SequenceState(e.cache.allocator.alloc(nblk)) for _ in range(B)]
+            lg = e.prefill_batch(seqs, prompts, use_graph=mode).float()
+            st = e.decode_step_obj(seqs, max_len, greedy=True, use_graph=True)
+            st.set_state(lg.argmax(-1), torch.tensor([s.length for s in seqs], device=cuda))
+            toks = [st.step().clone() for _ in range(6)]
+            res[mode] = (lg, torch.stack(toks).cpu())
+        assert e._pf_graphs, "prefill graph not captured"
+        torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-3, atol=1e-3)
+        assert torch.equal(res[True][1], res[False][1]), trial
