@@ -109,7 +109,42 @@ def main(argv=None):
     sub.add_parser("env-check", help="print the software / GPU environment")
     b = sub.add_parser("bench", help="decode benchmark (bench.py)")
     b.add_argument("rest", nargs=argparse.REMAINDER)
+    ai = sub.add_parser("bench-all", help="all-in-one benchmark: YAML config -> CSV (dev/benchmark/all-in-one)")
+    ai.add_argument("--config", default=None)
+    ai.add_argument("--out", default="all_in_one.csv")
+    ai.add_argument("--baseline", default=None, help="regression check against this CSV")
+    ai.add_argument("--threshold", type=float, default=5.0)
+    pp = sub.add_parser("ppl", help="strided perplexity of a text file (dev/benchmark/perplexity)")
+    pp.add_argument("--model_path", required=True)
+    pp.add_argument("--data_path", required=True)
+    pp.add_argument("--precision", default="sym_int4")
+    pp.add_argument("--chunk_size", type=int, default=512)
+    pp.add_argument("--stride", type=int, default=0)
+    pp.add_argument("--max_tokens", type=int, default=None)
+    pp.add_argument("--device", default="cuda")
     a = ap.parse_args(argv)
+    if a.cmd == "bench-all":
+        from ..utils import all_in_one as A
+        cfg = A.load_config(a.config)
+        A.run(cfg, a.out)
+        missing = A.check_results(a.out, cfg)
+        out = {"csv": a.out, "missing": missing}
+        if a.baseline:
+            out["regressions"] = A.compare(a.baseline, a.out, a.threshold)
+        print(json.dumps(out, indent=2))
+        return 1 if missing or out.get("regressions") else 0
+    if a.cmd == "ppl":
+        import torch
+        from transformers import AutoTokenizer
+        from ..transformers import AutoModelForCausalLM
+        from ..utils.perplexity import strided_perplexity, text_ids
+        tok = AutoTokenizer.from_pretrained(a.model_path)
+        model = AutoModelForCausalLM.from_pretrained(a.model_path, load_in_low_bit=a.precision,
+                                                     torch_dtype=torch.float16 if a.device != "cpu" else torch.float32)
+        model = model.to(a.device).eval()
+        r = strided_perplexity(model, text_ids(tok, a.data_path, a.max_tokens), a.chunk_size, a.stride or None)
+        print(json.dumps({"model": a.model_path, "precision": a.precision, **r}))
+        return r
     if a.cmd == "generate":
         return cmd_generate(a)
     if a.cmd == "chat":
