@@ -38,5 +38,9 @@ void launch_train_attn_fwd(bool bf16, const TrainAttnArgs& a, hipStream_t st);
 void launch_x_rowscale_lora(bool bf16, const uint16_t* x, int64_t M, int64_t ldx, int K, uint16_t* y, float* rs,
                             const uint16_t* la, int R, float alpha, uint16_t* xa, int rp, hipStream_t st);
 void launch_train_attn_bwd(bool bf16, const TrainAttnArgs& a, hipStream_t st);
+// C[M, N] += alpha * A[M, r] B[N, r]^T (lora_update.hip); 16-bit, r % 8 == 0,
+// r <= 64, N % 4 == 0, rows of A / B 16-B aligned
+void launch_lora_update(bool bf16, uint16_t* C, int64_t ldc, const uint16_t* A, int64_t lda, const uint16_t* B,
+                        int64_t ldb, int M, int N, int r, float alpha, hipStream_t st);
 
 }  // namespace illm

@@ -31,6 +31,28 @@ Tensor ce_fused_(Tensor& logits, const Tensor& labels, int64_t ignore_index, dou
   return loss;
 }
 
+// C[M, N] += alpha * A[M, r] @ B[N, r]^T in place (the LoRA rank-r term)
+Tensor lora_update_(Tensor& C, const Tensor& A, const Tensor& B, double alpha) {
+  TORCH_CHECK(C.is_cuda() && A.is_cuda() && B.is_cuda(), "lora_update_: GPU tensors expected");
+  TORCH_CHECK(C.dim() == 2 && A.dim() == 2 && B.dim() == 2 && A.size(0) == C.size(0) && B.size(0) == C.size(1) &&
+              A.size(1) == B.size(1), "lora_update_: C [M, N], A [M, r], B [N, r]");
+  const int64_t r = A.size(1);
+  TORCH_CHECK(r > 0 && r <= 64 && r % 8 == 0, "lora_update_: r % 8 == 0, r <= 64");
+  TORCH_CHECK(C.scalar_type() == A.scalar_type() && C.scalar_type() == B.scalar_type() &&
+              (C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kHalf), "lora_update_: one 16-bit dtype");
+  TORCH_CHECK(C.stride(1) == 1 && C.stride(0) % 4 == 0 && C.size(1) % 4 == 0, "lora_update_: C rows, N % 4 == 0");
+  auto ok16 = [](const Tensor& t) {
+    return t.stride(1) == 1 && t.stride(0) % 8 == 0 && ((uintptr_t)t.data_ptr() & 15) == 0;
+  };
+  TORCH_CHECK(ok16(A) && ok16(B), "lora_update_: A / B rows 16-B aligned with unit inner stride");
+  c10::DeviceGuard g(C.device());
+  if (C.numel() == 0) return C;
+  illm::launch_lora_update(C.scalar_type() == at::kBFloat16, (uint16_t*)C.data_ptr(), C.stride(0),
+                           (const uint16_t*)A.data_ptr(), A.stride(0), (const uint16_t*)B.data_ptr(), B.stride(0),
+                           (int)C.size(0), (int)C.size(1), (int)r, (float)alpha, cur_stream());
+  return C;
+}
+
 // out[r, n] = alpha * sum_m a[m, r] * b[m, n]  (a [M, R] f32, R <= 64; b [M, N] 16-bit) -> f32 [R, N]
 Tensor skinny_tn(const Tensor& a, const Tensor& b, double alpha) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "skinny_tn: GPU tensors expected");
@@ -127,11 +149,13 @@ TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("train_attn_bwd(Tensor q, Tensor k, Tensor v, Tensor out, Tensor lse, Tensor dout, float scale, bool causal=True) -> Tensor[]");
   m.def("ce_fused_(Tensor(a!) logits, Tensor labels, int ignore_index=-100, float grad_scale=0.0) -> Tensor");
   m.def("skinny_tn(Tensor a, Tensor b, float alpha=1.0) -> Tensor");
+  m.def("lora_update_(Tensor(a!) c, Tensor a, Tensor b, float alpha=1.0) -> Tensor(a!)");
 }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("ce_fused_", &ce_fused_);
   m.impl("skinny_tn", &skinny_tn);
+  m.impl("lora_update_", &lora_update_);
   m.impl("train_attn_fwd", &train_attn_fwd);
   m.impl("train_attn_bwd", &train_attn_bwd);
 }

@@ -83,6 +83,26 @@ _GROUP = os.environ.get("ILLM_LORA_GROUP", "1") == "1"
 _GROUPS = (("q_proj", "k_proj", "v_proj"), ("gate_proj", "up_proj"))
 
 
+def _rank_update_(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
+    """C += alpha * A @ B^T in place (A [M, r], B [N, r]): the LoRA rank-r term
+    on the HIP rank-update kernel (csrc/hip/lora_update.hip: a read-modify-
+    write of C at memory speed) where it applies, the library addmm otherwise"""
+    from .. import ops
+    r = A.shape[1]
+    if (_RANK_KERNEL and C.is_cuda and ops.native_gpu(C) and C.dtype in (torch.bfloat16, torch.float16)
+            and A.dtype == C.dtype and B.dtype == C.dtype and r % 8 == 0 and r <= 64 and C.shape[1] % 4 == 0
+            and C.stride(1) == 1 and C.stride(0) % 4 == 0 and A.stride(1) == 1 and A.stride(0) % 8 == 0
+            and A.data_ptr() % 16 == 0):
+        if B.stride(1) != 1 or B.stride(0) % 8 or B.data_ptr() % 16:
+            B = B.contiguous()
+        return torch.ops.ipex_llm_amd.lora_update_(C, A, B, float(alpha))
+    return C.addmm_(A, B.t(), alpha=alpha)
+
+
+# ILLM_LORA_RANK_KERNEL=0: the LoRA adds on the library addmm (A/B)
+_RANK_KERNEL = os.environ.get("ILLM_LORA_RANK_KERNEL", "1") == "1"
+
+
 def _base_dense_weight(base, dt):
     """the frozen base weight as the backward GEMM operand: the resident dense
     shadow / a transient dequant on the GPU (as MatMulLowBit), dequant on CPU"""
@@ -112,7 +132,7 @@ class _LoraLowBitFn(torch.autograd.Function):
         with torch.no_grad():
             y = ops.lowbit_matmul(x2, base.weight, base.fmt, base.out_features, base.in_features, bias)
             xa = torch.mm(x2, A.t())
-            y.addmm_(xa, B.t(), alpha=s)
+            _rank_update_(y, xa, B, s)
         ctx.save_for_backward(x2, xa, A, B)
         ctx.base, ctx.s, ctx.shp = base, s, shp
         return y.view(*shp[:-1], y.shape[-1])
@@ -139,7 +159,7 @@ class _LoraLowBitFn(torch.autograd.Function):
             else:
                 w = _base_dense_weight(base, x2.dtype)
                 gx = torch.mm(g2, w)
-            gx.addmm_(gxa, A)
+            _rank_update_(gx, gxa, A.t())
             gx = gx.view(ctx.shp)
         return gx, gA, gB, None, None
 
@@ -168,7 +188,7 @@ class _LoraGroupFn(torch.autograd.Function):
                 if bias is not None and bias.dtype != x2.dtype:
                     bias = bias.to(x2.dtype)
                 y = ops.lowbit_matmul(x2, base.weight, base.fmt, base.out_features, base.in_features, bias)
-                y.addmm_(xa_all[:, off:off + r], B.t(), alpha=s)
+                _rank_update_(y, xa_all[:, off:off + r], B, s)
                 ys.append(y.view(*shp[:-1], y.shape[-1]))
                 off += r
         ctx.save_for_backward(x2, xa_all, *AB)
@@ -199,7 +219,7 @@ class _LoraGroupFn(torch.autograd.Function):
         gxa_all = torch.cat(gxas, 1)
         gA_all = torch.mm(gxa_all.t(), x2)                         # [sum r, K]: one pass over x
         if gx is not None:
-            gx.addmm_(gxa_all, torch.cat(As, 0))
+            _rank_update_(gx, gxa_all, torch.cat(As, 0).t())
             gx = gx.view(ctx.shp)
         out, off = [], 0
         for (A, (_, gB)) in zip(As, grads):

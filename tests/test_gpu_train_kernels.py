@@ -126,3 +126,18 @@ def test_lora_engine_node_matches_fp32(cuda, qtype, r, monkeypatch):
     assert _rel(x.grad, xr.grad) < 1e-2
     assert _rel(A.grad, Ar.grad) < 2e-2
     assert _rel(B.grad, Br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,r", [(4096, 4096, 8), (300, 1000, 16), (77, 14336, 24), (64, 4100, 64), (1, 8, 8)])
+def test_lora_update_matches_fp32(cuda, M, N, r):
+    """C += alpha * A B^T on the rank-update kernel (csrc/hip/lora_update.hip)
+    == fp32 torch, incl. a strided column slice as A (the grouped LoRA's xa)"""
+    torch.manual_seed(M + r)
+    C = torch.randn(M, N, device=cuda).bfloat16()
+    wide = torch.randn(M, r + 16, device=cuda).bfloat16()
+    A = wide[:, 8:8 + r]                                 # stride r + 16, 16-B aligned start
+    B = (torch.randn(N, r, device=cuda) * 0.1).bfloat16()
+    ref = C.float() + 0.7 * (A.float() @ B.float().t())
+    out = torch.ops.ipex_llm_amd.lora_update_(C.clone(), A, B, 0.7)
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 5e-3
+    assert (out.float() - ref).abs().max().item() < 0.05
