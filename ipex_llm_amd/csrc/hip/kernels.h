@@ -259,6 +259,9 @@ void launch_rwkv4_wkv(const float* decay, const float* first, const float* k, co
 void launch_rwkv5_wkv(const float* w, const float* u, const float* r, const float* k, const float* v, float* out,
                       float* state, int B, int T, int H, int S, hipStream_t st);
 void launch_softmax_rows(bool bf16, uint16_t* x, int64_t rows, int L, hipStream_t st);
+// read nbytes (16-B granules) from p on `wgs` workgroups and drop them: an
+// Infinity-Cache warm-up for the next reader (csrc/hip/prefetch.hip)
+void launch_l3_prefetch(const void* p, size_t nbytes, int wgs, unsigned* sink, hipStream_t st);
 void launch_glu(bool bf16, const uint16_t* gu, int ld, uint16_t* out, int M, int I, int act, int tile,
                 hipStream_t st);
 void launch_quantize_device(int fmt, int in_kind, const void* w, int64_t n, int64_t k,

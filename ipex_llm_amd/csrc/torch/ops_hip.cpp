@@ -1465,6 +1465,28 @@ void decode_advance(const c10::optional<Tensor>& logits, Tensor& ids, Tensor& ne
                               kernel_err(pos.device()), cur_stream());
 }
 
+// stream bytes [offset, offset + nbytes) of t's storage through the caches
+// (Infinity-Cache warm-up for the next reader); nbytes < 0 -> to the end
+void l3_prefetch(const Tensor& t, int64_t offset, int64_t nbytes, int64_t wgs) {
+  TORCH_CHECK(t.is_cuda(), "l3_prefetch: GPU tensor");
+  const int64_t total = (int64_t)(t.numel() * t.element_size());
+  TORCH_CHECK(offset >= 0 && offset <= total, "l3_prefetch: offset out of range");
+  if (nbytes < 0 || offset + nbytes > total) nbytes = total - offset;
+  const char* p = (const char*)t.data_ptr() + offset;
+  // 16-B granules from the first aligned address inside the range
+  const int64_t lead = (int64_t)((16 - ((uintptr_t)p & 15)) & 15);
+  if (nbytes <= lead) return;
+  c10::DeviceGuard g(t.device());
+  // the kernel's write-only sink (its loads must be consumed): one per device,
+  // made on first use outside capture like the error word
+  static std::map<int, at::Tensor> sinks;
+  auto it = sinks.find(t.device().index());
+  if (it == sinks.end())
+    it = sinks.emplace(t.device().index(), at::empty({64}, t.options().dtype(at::kInt))).first;
+  illm::launch_l3_prefetch(p + lead, (size_t)(nbytes - lead), (int)wgs, (unsigned*)it->second.data_ptr<int>(),
+                           cur_stream());
+}
+
 }  // namespace
 
 // the device error word for the other binding units (ops_dist.cpp)
@@ -1473,6 +1495,7 @@ int* illm_kernel_err(const c10::Device& dev) { return kernel_err(dev); }
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv_glu_in", &gemv_glu_in);
   m.impl("decode_advance", &decode_advance);
+  m.impl("l3_prefetch", &l3_prefetch);
   m.impl("rope_kv_fused", &rope_kv_fused);
   m.impl("embedding_lowbit", &embedding_lowbit);
   m.impl("moe_align", &moe_align);

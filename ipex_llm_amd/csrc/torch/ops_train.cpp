@@ -40,7 +40,8 @@ Tensor lora_update_(Tensor& C, const Tensor& A, const Tensor& B, double alpha) {
   TORCH_CHECK(r > 0 && r <= 64 && r % 8 == 0, "lora_update_: r % 8 == 0, r <= 64");
   TORCH_CHECK(C.scalar_type() == A.scalar_type() && C.scalar_type() == B.scalar_type() &&
               (C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kHalf), "lora_update_: one 16-bit dtype");
-  TORCH_CHECK(C.stride(1) == 1 && C.stride(0) % 4 == 0 && C.size(1) % 4 == 0, "lora_update_: C rows, N % 4 == 0");
+  TORCH_CHECK(C.stride(1) == 1 && C.stride(0) % 8 == 0 && C.size(1) % 8 == 0 && ((uintptr_t)C.data_ptr() & 15) == 0,
+              "lora_update_: C rows 16-B aligned, N % 8 == 0");
   auto ok16 = [](const Tensor& t) {
     return t.stride(1) == 1 && t.stride(0) % 8 == 0 && ((uintptr_t)t.data_ptr() & 15) == 0;
   };
@@ -51,6 +52,28 @@ Tensor lora_update_(Tensor& C, const Tensor& A, const Tensor& B, double alpha) {
                            (const uint16_t*)A.data_ptr(), A.stride(0), (const uint16_t*)B.data_ptr(), B.stride(0),
                            (int)C.size(0), (int)C.size(1), (int)r, (float)alpha, cur_stream());
   return C;
+}
+
+// out[r, n] = alpha * sum_m a[m, r] * b[m, n] on the MFMA token-axis reduction
+// (a [M, r], b [M, N] one 16-bit dtype) -> f32 [r, N]
+Tensor lora_tn(const Tensor& a, const Tensor& b, double alpha) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.size(0) == b.size(0),
+              "lora_tn: a [M, r], b [M, N] GPU tensors");
+  const int64_t r = a.size(1), N = b.size(1);
+  TORCH_CHECK(r > 0 && r <= 64 && r % 8 == 0 && N % 8 == 0, "lora_tn: r % 8 == 0, r <= 64, N % 8 == 0");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf),
+              "lora_tn: one 16-bit dtype");
+  auto ok16 = [](const Tensor& t) {
+    return t.stride(1) == 1 && t.stride(0) % 8 == 0 && ((uintptr_t)t.data_ptr() & 15) == 0;
+  };
+  TORCH_CHECK(ok16(a) && ok16(b), "lora_tn: rows 16-B aligned with unit inner stride");
+  c10::DeviceGuard g(a.device());
+  Tensor out = at::zeros({r, N}, a.options().dtype(at::kFloat));
+  if (a.size(0) == 0) return out;
+  illm::launch_lora_tn(a.scalar_type() == at::kBFloat16, (const uint16_t*)a.data_ptr(), a.stride(0), (int)r,
+                       (const uint16_t*)b.data_ptr(), b.stride(0), (int)a.size(0), (int)N, (float)alpha,
+                       out.data_ptr<float>(), cur_stream());
+  return out;
 }
 
 // out[r, n] = alpha * sum_m a[m, r] * b[m, n]  (a [M, R] f32, R <= 64; b [M, N] 16-bit) -> f32 [R, N]
@@ -150,12 +173,14 @@ TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("ce_fused_(Tensor(a!) logits, Tensor labels, int ignore_index=-100, float grad_scale=0.0) -> Tensor");
   m.def("skinny_tn(Tensor a, Tensor b, float alpha=1.0) -> Tensor");
   m.def("lora_update_(Tensor(a!) c, Tensor a, Tensor b, float alpha=1.0) -> Tensor(a!)");
+  m.def("lora_tn(Tensor a, Tensor b, float alpha=1.0) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("ce_fused_", &ce_fused_);
   m.impl("skinny_tn", &skinny_tn);
   m.impl("lora_update_", &lora_update_);
+  m.impl("lora_tn", &lora_tn);
   m.impl("train_attn_fwd", &train_attn_fwd);
   m.impl("train_attn_bwd", &train_attn_bwd);
 }

@@ -90,9 +90,9 @@ def _rank_update_(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, alpha: floa
     from .. import ops
     r = A.shape[1]
     if (_RANK_KERNEL and C.is_cuda and ops.native_gpu(C) and C.dtype in (torch.bfloat16, torch.float16)
-            and A.dtype == C.dtype and B.dtype == C.dtype and r % 8 == 0 and r <= 64 and C.shape[1] % 4 == 0
-            and C.stride(1) == 1 and C.stride(0) % 4 == 0 and A.stride(1) == 1 and A.stride(0) % 8 == 0
-            and A.data_ptr() % 16 == 0):
+            and A.dtype == C.dtype and B.dtype == C.dtype and r % 8 == 0 and r <= 64 and C.shape[1] % 8 == 0
+            and C.stride(1) == 1 and C.stride(0) % 8 == 0 and C.data_ptr() % 16 == 0 and A.stride(1) == 1
+            and A.stride(0) % 8 == 0 and A.data_ptr() % 16 == 0):
         if B.stride(1) != 1 or B.stride(0) % 8 or B.data_ptr() % 16:
             B = B.contiguous()
         return torch.ops.ipex_llm_amd.lora_update_(C, A, B, float(alpha))
@@ -101,6 +101,28 @@ def _rank_update_(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, alpha: floa
 
 # ILLM_LORA_RANK_KERNEL=0: the LoRA adds on the library addmm (A/B)
 _RANK_KERNEL = os.environ.get("ILLM_LORA_RANK_KERNEL", "1") == "1"
+
+
+def _tn(a: torch.Tensor, b: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
+    """alpha * a^T b over the token axis (a [M, r], b [M, N]) -> [r, N] in
+    a's dtype: the LoRA weight gradients.  On the HIP token-axis reduction
+    (csrc/hip/lora_update.hip lora_tn: both operands through transposed LDS
+    reads, f32 atomics over row slices) where it applies -- the library
+    runs these K = tokens, M = r shapes on a 256 x 128 macro-tile at a
+    fraction of HBM speed -- the library GEMM otherwise"""
+    from .. import ops
+    r, N = a.shape[1], b.shape[1]
+    if (_TN_KERNEL and a.is_cuda and ops.native_gpu(a) and a.dtype in (torch.bfloat16, torch.float16)
+            and b.dtype == a.dtype and r % 8 == 0 and r <= 64 and N % 8 == 0
+            and all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in (a, b))):
+        return torch.ops.ipex_llm_amd.lora_tn(a, b, float(alpha)).to(a.dtype)
+    if alpha == 1.0:
+        return torch.mm(a.t(), b)
+    return torch.addmm(a.new_empty(()), a.t(), b, beta=0, alpha=alpha)
+
+
+# ILLM_LORA_TN_KERNEL=0: dA / dB on the library GEMM (A/B)
+_TN_KERNEL = os.environ.get("ILLM_LORA_TN_KERNEL", "1") == "1"
 
 
 def _base_dense_weight(base, dt):
@@ -146,8 +168,8 @@ class _LoraLowBitFn(torch.autograd.Function):
         # input is never read) instead of separate [M, r] / [N, r] scale launches
         z = g2.new_empty(())                               # (no fill launch)
         gxa = torch.addmm(z, g2, B, beta=0, alpha=s)      # [M, r]
-        gA = torch.mm(gxa.t(), x2) if ctx.needs_input_grad[1] else None
-        gB = torch.addmm(z, g2.t(), xa, beta=0, alpha=s) if ctx.needs_input_grad[2] else None
+        gA = _tn(gxa, x2) if ctx.needs_input_grad[1] else None
+        gB = _tn(xa, g2, s).t().contiguous() if ctx.needs_input_grad[2] else None
         gx = None
         if ctx.needs_input_grad[0]:
             base = ctx.base
@@ -211,13 +233,13 @@ class _LoraGroupFn(torch.autograd.Function):
                 continue
             g2 = g.reshape(-1, g.shape[-1]).to(x2.dtype)
             gxas.append(torch.addmm(z, g2, B, beta=0, alpha=s))
-            grads.append((None, torch.addmm(z, g2.t(), xa_all[:, off:off + r], beta=0, alpha=s)))
+            grads.append((None, _tn(xa_all[:, off:off + r], g2, s).t().contiguous()))
             if ctx.needs_input_grad[0]:
                 w = _base_dense_weight(base, x2.dtype)
                 gx = torch.mm(g2, w) if gx is None else gx.addmm_(g2, w)
             off += r
         gxa_all = torch.cat(gxas, 1)
-        gA_all = torch.mm(gxa_all.t(), x2)                         # [sum r, K]: one pass over x
+        gA_all = _tn(gxa_all, x2)                                  # [sum r, K]: one pass over x
         if gx is not None:
             _rank_update_(gx, gxa_all, torch.cat(As, 0).t())
             gx = gx.view(ctx.shp)

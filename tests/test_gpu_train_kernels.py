@@ -128,7 +128,8 @@ def test_lora_engine_node_matches_fp32(cuda, qtype, r, monkeypatch):
     assert _rel(B.grad, Br.grad) < 2e-2
 
 
-@pytest.mark.parametrize("M,N,r", [(4096, 4096, 8), (300, 1000, 16), (77, 14336, 24), (64, 4100, 64), (1, 8, 8)])
+@pytest.mark.parametrize("M,N,r", [(4096, 4096, 8), (300, 1000, 16), (77, 14336, 24), (64, 4104, 64), (1, 8, 8),
+                                   (33, 200, 8)])
 def test_lora_update_matches_fp32(cuda, M, N, r):
     """C += alpha * A B^T on the rank-update kernel (csrc/hip/lora_update.hip)
     == fp32 torch, incl. a strided column slice as A (the grouped LoRA's xa)"""
@@ -141,3 +142,20 @@ def test_lora_update_matches_fp32(cuda, M, N, r):
     out = torch.ops.ipex_llm_amd.lora_update_(C.clone(), A, B, 0.7)
     assert ((out.float() - ref).norm() / ref.norm()).item() < 5e-3
     assert (out.float() - ref).abs().max().item() < 0.05
+
+
+@pytest.mark.parametrize("M,N,r", [(4096, 4096, 24), (300, 1000, 16), (77, 14336, 8), (4100, 4104, 64),
+                                   (1, 8, 8), (8192, 1024, 40)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_lora_tn_matches_fp32(cuda, M, N, r, dt):
+    """out = alpha a^T b over the token axis on the MFMA reduction
+    (csrc/hip/lora_update.hip lora_tn) == fp32 torch, incl. a strided column
+    slice as a (the grouped LoRA's xa_all[:, off:off + r])"""
+    torch.manual_seed(M + r)
+    wide = torch.randn(M, r + 16, device=cuda).to(dt)
+    a = wide[:, 8:8 + r]
+    b = torch.randn(M, N, device=cuda).to(dt)
+    ref = 0.7 * (a.float().t() @ b.float())
+    out = torch.ops.ipex_llm_amd.lora_tn(a, b, 0.7)
+    assert out.dtype == torch.float32 and out.shape == (r, N)
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-4
