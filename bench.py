@@ -205,6 +205,7 @@ def main():
                        "batch_per_gpu": B if not same_tokens else B / world, "seq_len": P,
                        "parallelism": f"tp{world}" if args.tp else (f"ep{world}" if args.ep else f"dp{world}"),
                        "hipgraph": not args.no_graph, "prefill_hipgraph": pf_graph,
+                       "prefill_dense_shadow_gb": eng.prefill_dense_gb,
                        "layers": cfg.num_hidden_layers},
             "first_token_latency_ms": round(ftl_ms, 2),
             "decode_ms_per_token": round(ms_step, 4),

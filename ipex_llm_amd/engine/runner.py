@@ -182,6 +182,15 @@ class Engine:
         self._pf_graphs: Dict[Tuple[int, int, int], tuple] = {}
         self.cache: Optional[PagedKVCache] = None
         self._cache_key = None
+        # prefill GEMMs on a resident dequantized shadow when HBM allows
+        # (ops/gemm.py auto_dense_budget; ILLM_PREFILL_DENSE_GB overrides)
+        self.prefill_dense_gb = 0.0
+        p = next(iter(model.parameters()), None) if hasattr(model, "parameters") else None
+        if p is None and hasattr(model, "buffers"):
+            p = next(iter(model.buffers()), None)
+        if p is not None and p.is_cuda:
+            from ..ops.gemm import auto_dense_budget
+            self.prefill_dense_gb = auto_dense_budget(p.device)
 
     def _ensure_cache(self, batch: int, max_len: int):
         blocks = batch * ((max_len + self.block_size - 1) // self.block_size)

@@ -16,6 +16,7 @@ o 50 vs 62, gate_up 239 vs 318, down 138 vs 184).
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -95,7 +96,7 @@ def prefetch_dense(items, M: int, dtype) -> None:
 # reuse it; numerics identical to the dequantize-per-call path).  Default 0:
 # nothing kept (the low-bit footprint only).
 _DENSE_BUDGET = float(os.environ.get("ILLM_PREFILL_DENSE_GB", "0")) * 2 ** 30
-_dense_cache = {}            # (blob ptr, version, n, k, dtype) -> dense weight
+_dense_cache = {}            # (blob ptr, version, n, k, dtype) -> (weakref to blob, dense weight)
 _dense_bytes = [0]
 
 
@@ -113,16 +114,47 @@ def dense_cache_clear() -> None:
     _dense_bytes[0] = 0
 
 
+def auto_dense_budget(device, cap_gb: float = float("inf")) -> float:
+    """Inference default for the prefill shadow (engine construction): an
+    explicit ILLM_PREFILL_DENSE_GB wins; otherwise on a >= 128 GiB device
+    (MI355X: 288 GB HBM3E) up to min(48 GiB, 1/4 of HBM) of dequantized
+    weights stay resident -- a Llama-3-8B INT4 model adds 15 GB next to its
+    4.5 GB of low-bit weights (``cap_gb`` bounds the automatic choice).
+    Returns the budget in GiB."""
+    env = os.environ.get("ILLM_PREFILL_DENSE_GB")
+    if env is not None:
+        gb = float(env)
+    else:
+        total = torch.cuda.get_device_properties(device).total_memory / 2 ** 30
+        gb = min(48.0, 0.25 * total, cap_gb) if total >= 128 else 0.0
+    if gb * 2 ** 30 > _DENSE_BUDGET:
+        set_dense_budget(gb)
+    return gb
+
+
+def _dense_drop(key):
+    ent = _dense_cache.pop(key, None)
+    if ent is not None:
+        _dense_bytes[0] -= ent[1].numel() * ent[1].element_size()
+
+
 def _dense_weight(blob, fmt, n, k, dtype):
-    if _DENSE_BUDGET > 0 and not torch.cuda.is_current_stream_capturing():
+    if _DENSE_BUDGET > 0:
+        # keyed by address, validated by identity: an entry lives exactly as
+        # long as its blob (weakref callback), so a later model whose blob
+        # reuses the address never sees another model's weights
         key = (blob.data_ptr(), blob._version, n, k, dtype)
-        w = _dense_cache.get(key)
-        if w is not None:
-            return w
+        ent = _dense_cache.get(key)
+        if ent is not None:
+            if ent[0]() is blob:
+                return ent[1]
+            _dense_drop(key)
         w = torch.ops.ipex_llm_amd.dequantize_device(blob, fmt, n, k, dtype)
+        if torch.cuda.is_current_stream_capturing():
+            return w                # captured: a transient of the graph's pool, never cached
         nb = w.numel() * w.element_size()
         if _dense_bytes[0] + nb <= _DENSE_BUDGET:
-            _dense_cache[key] = w
+            _dense_cache[key] = (weakref.ref(blob, lambda _r, key=key: _dense_drop(key)), w)
             _dense_bytes[0] += nb
         return w
     hit = _ready.pop(_key(blob, n, k, dtype), None) if _ready else None

@@ -78,6 +78,13 @@ class LLMEngine:
         self.cache = model.make_cache(max_model_len, max_batch, block_size, kv_fp8, num_blocks=num_blocks + 1)
         self._scratch = num_blocks
         self.num_blocks = num_blocks
+        # prefill GEMMs on a resident dequantized shadow (ops/gemm.py
+        # auto_dense_budget), bounded by half of what the KV pool left free
+        self.prefill_dense_gb = 0.0
+        if model.device.type == "cuda":
+            from ..ops.gemm import auto_dense_budget
+            free, _ = torch.cuda.mem_get_info(model.device)
+            self.prefill_dense_gb = auto_dense_budget(model.device, cap_gb=0.5 * free / 2 ** 30)
         from .metrics import EngineMetrics
         self.metrics = EngineMetrics()
         self.use_graph = use_graph and model.device.type == "cuda" and ops.native_gpu(self.cache.k[0])

@@ -90,3 +90,47 @@ def test_graph_prefill_matches_eager(cuda, B, n):
         assert e._pf_graphs, "prefill graph not captured"
         torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-3, atol=1e-3)
         assert torch.equal(res[True][1], res[False][1]), trial
+
+
+def test_prefill_dense_shadow_matches_transient(cuda):
+    """the resident dequantized prefill shadow (ops/gemm.py _dense_weight,
+    auto-enabled by Engine on a >= 128 GiB device) gives the transient-dequant
+    logits exactly, eager and graph-captured; entries die with their blob, and
+    a new model whose blobs reuse freed addresses never sees stale weights"""
+    import gc
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.models.cache import SequenceState
+    from ipex_llm_amd.ops import gemm as G
+    old = G._DENSE_BUDGET
+
+    def run(seed, budget, mode):
+        G.set_dense_budget(budget)
+        m = random_native_model(_cfg(), "sym_int4", cuda, torch.bfloat16, seed=seed)
+        e = Engine(m)
+        G.set_dense_budget(budget)             # the engine's auto rule must not override the test's choice
+        e._ensure_cache(2, 640)
+        out = []
+        for _ in range(2):                     # 2nd call: cache hit (eager) / graph replay
+            e.cache.allocator = type(e.cache.allocator)(e.cache.num_blocks)
+            seqs = [SequenceState(e.cache.allocator.alloc(10)) for _ in range(2)]
+            ids = torch.randint(0, 1024, (2, 300), generator=torch.Generator().manual_seed(7))
+            out.append(e.prefill_batch(seqs, ids, use_graph=mode).float().cpu())
+        n_cached = len(G._dense_cache)
+        del e, m
+        gc.collect()
+        return out, n_cached
+
+    try:
+        for mode in (False, True):
+            ref, _ = run(1, 0.0, mode)
+            got, n_cached = run(1, 1.0, mode)
+            assert n_cached > 0
+            for a, b in zip(ref, got):
+                assert torch.equal(a, b)
+            assert len(G._dense_cache) == 0        # dropped with the model
+            other, _ = run(2, 1.0, mode)           # same shapes, other weights
+            ref2, _ = run(2, 0.0, mode)
+            assert all(torch.equal(a, b) for a, b in zip(other, ref2))
+    finally:
+        G.set_dense_budget(old / 2 ** 30)
