@@ -21,6 +21,7 @@
 // load of the wave's strip is issued before the first MFMA (one memory
 // latency per wave), k > r lanes feed zeros, fp32 math, one rounding.
 #include <algorithm>
+#include <cstdlib>
 
 #include "illm_device.h"
 #include "kernels.h"
@@ -174,8 +175,11 @@ __global__ void __launch_bounds__(256) lora_tn_kernel(const uint16_t* a, int64_t
 void launch_lora_tn(bool bf16, const uint16_t* a, int64_t lda, int r, const uint16_t* b, int64_t ldb, int M, int N,
                     float alpha, float* out, hipStream_t st) {
   const int nb = (N + 63) / 64;
-  // ~2048 workgroups, >= 2 stages each
-  int splits = std::max(1, std::min((M + 2 * TN_RB - 1) / (2 * TN_RB), 2048 / std::max(1, nb)));
+  // row slices of >= min_rows (every slice ends in r x 64 f32 atomics per
+  // workgroup), up to ~wg_target workgroups; ILLM_LORA_TN_ROWS / _WGS for sweeps
+  static const int min_rows = getenv("ILLM_LORA_TN_ROWS") ? atoi(getenv("ILLM_LORA_TN_ROWS")) : 128;
+  static const int wg_target = getenv("ILLM_LORA_TN_WGS") ? atoi(getenv("ILLM_LORA_TN_WGS")) : 2048;
+  int splits = std::max(1, std::min((M + min_rows - 1) / std::max(TN_RB, min_rows), wg_target / std::max(1, nb)));
   const int rows_per = ((M + splits - 1) / splits + TN_RB - 1) / TN_RB * TN_RB;
   splits = (M + rows_per - 1) / rows_per;
   dim3 grid((unsigned)nb, (unsigned)splits);
