@@ -254,6 +254,10 @@ def _replace_with_low_bit_linear(model: nn.Module, qtype: int, modules_to_not_co
     """Recursively replace nn.Linear (reference convert.py:472-752)."""
     skip = set(modules_to_not_convert or [])
     n_conv = 0
+    if isinstance(model, nn.MultiheadAttention):
+        # torch MHA reads out_proj.weight directly (F.multi_head_attention_forward):
+        # its projections stay dense (e.g. the Gemma-3 / SigLIP multimodal pooler)
+        return 0
     for name, child in list(model.named_children()):
         full = f"{prefix}.{name}" if prefix else name
         if name in skip or full in skip:

@@ -148,3 +148,83 @@ def test_internvl_image_text_lowbit():
         got = m(**kw).logits
     assert any(isinstance(x, LowBitLinear) for x in m.modules())
     assert _rel(got, want) < 5e-2
+
+
+def _mm_parity(ref, kw, tol=5e-2):
+    import copy
+    from ipex_llm_amd import optimize_model
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    with torch.no_grad():
+        want = ref(**kw).logits
+        m = optimize_model(copy.deepcopy(ref), low_bit="sym_int8")
+        got = m(**kw).logits
+    assert sum(isinstance(x, LowBitLinear) for x in m.modules()) > 0
+    assert _rel(got, want) < tol
+    return m
+
+
+_TXT = dict(vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+            num_key_value_heads=2, max_position_embeddings=256)
+
+
+def test_qwen2_audio_lowbit():
+    """Qwen2-Audio: Whisper-style audio encoder + pooled projector + Qwen2
+    (reference serving/fastapi audio path, models/qwen2_audio)"""
+    import transformers as T
+    ac = dict(num_mel_bins=16, encoder_layers=2, encoder_attention_heads=4, encoder_ffn_dim=128, d_model=64,
+              max_source_positions=20)
+    torch.manual_seed(0)
+    ref = T.Qwen2AudioForConditionalGeneration(
+        T.Qwen2AudioConfig(audio_config=ac, text_config=_TXT, audio_token_index=290)).eval()
+    ids = torch.randint(3, 280, (1, 16))
+    ids[0, 1:11] = 290                                  # 40 frames -> 20 (conv) -> 10 (pool)
+    kw = dict(input_ids=ids, input_features=torch.randn(1, 16, 40), attention_mask=torch.ones_like(ids),
+              feature_attention_mask=torch.ones(1, 40, dtype=torch.long))
+    m = _mm_parity(ref, kw)
+    with torch.no_grad():                                # the audio matters
+        assert _rel(m(**dict(kw, input_features=torch.randn(1, 16, 40))).logits, m(**kw).logits) > 1e-3
+
+
+def test_gemma3_image_text_lowbit():
+    """Gemma-3 vision: SigLIP tower + pooled projector; the tower's
+    nn.MultiheadAttention projections stay dense (torch reads their weights)"""
+    import transformers as T
+    vc = dict(hidden_size=64, num_hidden_layers=2, num_attention_heads=4, intermediate_size=128, image_size=28,
+              patch_size=14)
+    torch.manual_seed(0)
+    ref = T.Gemma3ForConditionalGeneration(
+        T.Gemma3Config(vision_config=vc, text_config=dict(_TXT, head_dim=16, sliding_window=64),
+                       mm_tokens_per_image=4, image_token_index=290)).eval()
+    ids = torch.randint(3, 280, (1, 12))
+    ids[0, 1:5] = 290
+    _mm_parity(ref, dict(input_ids=ids, pixel_values=torch.randn(1, 3, 28, 28), token_type_ids=(ids == 290).long()))
+
+
+def test_llava_image_text_lowbit():
+    import transformers as T
+    vc = dict(model_type="clip_vision_model", hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+              intermediate_size=128, image_size=28, patch_size=14, projection_dim=64)
+    torch.manual_seed(0)
+    ref = T.LlavaForConditionalGeneration(
+        T.LlavaConfig(vision_config=vc, text_config=dict(_TXT, model_type="llama"), image_token_index=290,
+                      vision_feature_layer=-1)).eval()
+    ids = torch.randint(3, 280, (1, 12))
+    ids[0, 1:5] = 290
+    _mm_parity(ref, dict(input_ids=ids, pixel_values=torch.randn(1, 3, 28, 28)))
+
+
+def test_janus_image_understanding_lowbit():
+    """Janus: SigLIP-style understanding encoder + aligner + Llama (reference
+    models/janus.py); the VQ-VAE generation head is built but unused here"""
+    import transformers as T
+    vc = dict(hidden_size=64, num_hidden_layers=2, num_attention_heads=4, intermediate_size=128, image_size=28,
+              patch_size=14, projection_dim=64)
+    vq = dict(embed_dim=8, num_embeddings=32, latent_channels=32, base_channels=32, channel_multiplier=[1, 1],
+              num_res_blocks=1, num_patches=2, image_token_embed_dim=64, projection_dim=64)
+    torch.manual_seed(0)
+    ref = T.JanusForConditionalGeneration(
+        T.JanusConfig(vision_config=vc, text_config=dict(_TXT, model_type="llama"), vq_config=vq,
+                      image_token_id=290)).eval()
+    ids = torch.randint(3, 280, (1, 12))
+    ids[0, 1:5] = 290
+    _mm_parity(ref, dict(input_ids=ids, pixel_values=torch.randn(1, 3, 28, 28)))
