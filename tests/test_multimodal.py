@@ -228,3 +228,26 @@ def test_janus_image_understanding_lowbit():
     ids = torch.randint(3, 280, (1, 12))
     ids[0, 1:5] = 290
     _mm_parity(ref, dict(input_ids=ids, pixel_values=torch.randn(1, 3, 28, 28)))
+
+
+def test_qwen2_5_omni_thinker_audio_lowbit():
+    """Qwen2.5-Omni thinker (reference models/qwen2_5_omni.py): audio encoder
+    + M-RoPE Qwen2 text model, converted end to end"""
+    import transformers as T
+    ac = dict(num_mel_bins=16, encoder_layers=2, encoder_attention_heads=4, encoder_ffn_dim=128, d_model=64,
+              max_source_positions=20, n_window=10, output_dim=64)
+    vc = dict(depth=2, hidden_size=64, intermediate_size=128, num_heads=4, out_hidden_size=64, patch_size=14,
+              spatial_merge_size=2, temporal_patch_size=2, fullatt_block_indexes=[1], window_size=56)
+    t = dict(_TXT, rope_parameters={"rope_type": "default", "rope_theta": 10000.0, "mrope_section": [2, 3, 3]})
+    try:
+        cfg = T.Qwen2_5OmniThinkerConfig(audio_config=ac, vision_config=vc, text_config=t, audio_token_index=291,
+                                         image_token_index=290, video_token_index=292, vision_start_token_id=293,
+                                         audio_start_token_id=294, audio_end_token_id=295)
+        torch.manual_seed(0)
+        ref = T.Qwen2_5OmniThinkerForConditionalGeneration(cfg).eval()
+    except (TypeError, ValueError, KeyError) as e:     # pragma: no cover - config layout of other versions
+        pytest.skip(f"Qwen2.5-Omni config layout: {e}")
+    ids = torch.randint(3, 280, (1, 16))
+    ids[0, 1:6] = 291
+    _mm_parity(ref, dict(input_ids=ids, input_features=torch.randn(1, 16, 40), attention_mask=torch.ones_like(ids),
+                         feature_attention_mask=torch.ones(1, 40, dtype=torch.long)))
