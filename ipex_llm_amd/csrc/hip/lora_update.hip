@@ -177,7 +177,7 @@ void launch_lora_tn(bool bf16, const uint16_t* a, int64_t lda, int r, const uint
   const int nb = (N + 63) / 64;
   // row slices of >= min_rows (every slice ends in r x 64 f32 atomics per
   // workgroup), up to ~wg_target workgroups; ILLM_LORA_TN_ROWS / _WGS for sweeps
-  static const int min_rows = getenv("ILLM_LORA_TN_ROWS") ? atoi(getenv("ILLM_LORA_TN_ROWS")) : 128;
+  static const int min_rows = getenv("ILLM_LORA_TN_ROWS") ? atoi(getenv("ILLM_LORA_TN_ROWS")) : 256;
   static const int wg_target = getenv("ILLM_LORA_TN_WGS") ? atoi(getenv("ILLM_LORA_TN_WGS")) : 2048;
   int splits = std::max(1, std::min((M + min_rows - 1) / std::max(TN_RB, min_rows), wg_target / std::max(1, nb)));
   const int rows_per = ((M + splits - 1) / splits + TN_RB - 1) / TN_RB * TN_RB;

@@ -105,3 +105,39 @@ def test_whisper_encoder_flash(cuda, monkeypatch):
         got = m.encoder(feats.to(cuda, torch.bfloat16)).last_hidden_state
     assert n[0] == cfg.encoder_layers, n[0]
     assert _rel(got.float().cpu(), want) < 3e-2
+
+
+@pytest.mark.parametrize("fam", ["qwen2_audio", "llava"])
+def test_multimodal_lowbit_on_gpu(cuda, fam):
+    """audio / image + text models converted to sym_int8 run on the HIP low-bit
+    GEMV/GEMM and match the fp32 CPU model"""
+    from ipex_llm_amd import optimize_model
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    txt = dict(vocab_size=300, hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+               num_key_value_heads=2, max_position_embeddings=256)
+    torch.manual_seed(0)
+    ids = torch.randint(3, 280, (1, 24))
+    if fam == "qwen2_audio":
+        ac = dict(num_mel_bins=16, encoder_layers=2, encoder_attention_heads=4, encoder_ffn_dim=512, d_model=256,
+                  max_source_positions=20)
+        ref = T.Qwen2AudioForConditionalGeneration(
+            T.Qwen2AudioConfig(audio_config=ac, text_config=txt, audio_token_index=290)).eval()
+        ids[0, 1:11] = 290
+        kw = dict(input_ids=ids, input_features=torch.randn(1, 16, 40), attention_mask=torch.ones_like(ids),
+                  feature_attention_mask=torch.ones(1, 40, dtype=torch.long))
+    else:
+        vc = dict(model_type="clip_vision_model", hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+                  intermediate_size=512, image_size=56, patch_size=14, projection_dim=256)
+        ref = T.LlavaForConditionalGeneration(
+            T.LlavaConfig(vision_config=vc, text_config=dict(txt, model_type="llama"), image_token_index=290,
+                          vision_feature_layer=-1)).eval()
+        ids[0, 1:17] = 290
+        kw = dict(input_ids=ids, pixel_values=torch.randn(1, 3, 56, 56))
+    with torch.no_grad():
+        want = ref(**kw).logits
+    m = optimize_model(copy.deepcopy(ref).to(torch.bfloat16), low_bit="sym_int8").to(cuda)
+    assert any(isinstance(x, LowBitLinear) and x.weight.is_cuda for x in m.modules())
+    gkw = {k: (v.to(cuda, torch.bfloat16) if v.is_floating_point() else v.to(cuda)) for k, v in kw.items()}
+    with torch.no_grad():
+        got = m(**gkw).logits
+    assert _rel(got.float().cpu(), want) < 5e-2

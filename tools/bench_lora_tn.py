@@ -8,7 +8,9 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-import ipex_llm_amd  # noqa: E402,F401
+from ipex_llm_amd import ops  # noqa: E402
+
+ops.require()
 
 P = torch.ops.ipex_llm_amd
 M = 4096

@@ -2,7 +2,7 @@
 # round-4: dense prefill shadow test + TTFT; lora_tn split-policy sweep
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 T="timeout -k 10"
-$T 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_model.py tests/test_gpu_train_kernels.py -m gpu > gpurun_out/t_r4y.log 2>&1
+$T 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_model.py tests/test_gpu_encoders.py -m gpu -k "dense_shadow or multimodal" > gpurun_out/t_r4y.log 2>&1
 rc=$?; tail -3 gpurun_out/t_r4y.log; [ $rc -eq 0 ] || exit $rc
 for rw in "128 2048" "256 1024" "512 1024" "256 2048"; do
   set -- $rw
