@@ -42,9 +42,10 @@ void launch_train_attn_bwd(bool bf16, const TrainAttnArgs& a, hipStream_t st);
 // r <= 64, N % 4 == 0, rows of A / B 16-B aligned
 void launch_lora_update(bool bf16, uint16_t* C, int64_t ldc, const uint16_t* A, int64_t lda, const uint16_t* B,
                         int64_t ldb, int M, int N, int r, float alpha, hipStream_t st);
-// out[r, n] += alpha * sum_m a[m, r] b[m, n] (f32 out, zeroed by the caller);
+// out[r, n] += alpha * sum_m a[m, r] b[m, n] (f32 out, zeroed by the caller; trans:
+// out is [N, r]);
 // 16-bit a [M, r] / b [M, N], r <= 64, r % 8 == 0, N % 8 == 0, rows 16-B aligned
 void launch_lora_tn(bool bf16, const uint16_t* a, int64_t lda, int r, const uint16_t* b, int64_t ldb, int M, int N,
-                    float alpha, float* out, hipStream_t st);
+                    float alpha, float* out, bool trans, hipStream_t st);
 
 }  // namespace illm

@@ -108,7 +108,7 @@ constexpr int TN_RB = 64;       // rows per LDS stage
 template <typename T>
 __global__ void __launch_bounds__(256) lora_tn_kernel(const uint16_t* a, int64_t lda, int r, const uint16_t* b,
                                                       int64_t ldb, int M, int N, int rows_per, float alpha,
-                                                      float* out) {
+                                                      float* out, bool trans) {
   __shared__ __attribute__((aligned(16))) uint16_t bt[TN_RB * 64];
   __shared__ __attribute__((aligned(16))) uint16_t at[TN_RB * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -165,7 +165,8 @@ __global__ void __launch_bounds__(256) lora_tn_kernel(const uint16_t* a, int64_t
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const int rr = 16 * rt + 4 * g + i;
-      if (rr < r) atomicAdd(out + (size_t)rr * N + n, alpha * acc[rt][i]);
+      // trans: out is [N, r] (the layout of a LoRA B gradient), else [r, N]
+      if (rr < r) atomicAdd(out + (trans ? (size_t)n * r + rr : (size_t)rr * N + n), alpha * acc[rt][i]);
     }
   }
 }
@@ -173,7 +174,7 @@ __global__ void __launch_bounds__(256) lora_tn_kernel(const uint16_t* a, int64_t
 }  // namespace
 
 void launch_lora_tn(bool bf16, const uint16_t* a, int64_t lda, int r, const uint16_t* b, int64_t ldb, int M, int N,
-                    float alpha, float* out, hipStream_t st) {
+                    float alpha, float* out, bool trans, hipStream_t st) {
   const int nb = (N + 63) / 64;
   // row slices of >= min_rows (every slice ends in r x 64 f32 atomics per
   // workgroup), up to ~wg_target workgroups; ILLM_LORA_TN_ROWS / _WGS for sweeps
@@ -184,9 +185,11 @@ void launch_lora_tn(bool bf16, const uint16_t* a, int64_t lda, int r, const uint
   splits = (M + rows_per - 1) / rows_per;
   dim3 grid((unsigned)nb, (unsigned)splits);
   if (bf16)
-    hipLaunchKernelGGL(lora_tn_kernel<BF16>, grid, dim3(256), 0, st, a, lda, r, b, ldb, M, N, rows_per, alpha, out);
+    hipLaunchKernelGGL(lora_tn_kernel<BF16>, grid, dim3(256), 0, st, a, lda, r, b, ldb, M, N, rows_per, alpha, out,
+                       trans);
   else
-    hipLaunchKernelGGL(lora_tn_kernel<F16>, grid, dim3(256), 0, st, a, lda, r, b, ldb, M, N, rows_per, alpha, out);
+    hipLaunchKernelGGL(lora_tn_kernel<F16>, grid, dim3(256), 0, st, a, lda, r, b, ldb, M, N, rows_per, alpha, out,
+                       trans);
 }
 
 void launch_lora_update(bool bf16, uint16_t* C, int64_t ldc, const uint16_t* A, int64_t lda, const uint16_t* B,

@@ -56,7 +56,7 @@ Tensor lora_update_(Tensor& C, const Tensor& A, const Tensor& B, double alpha) {
 
 // out[r, n] = alpha * sum_m a[m, r] * b[m, n] on the MFMA token-axis reduction
 // (a [M, r], b [M, N] one 16-bit dtype) -> f32 [r, N]
-Tensor lora_tn(const Tensor& a, const Tensor& b, double alpha) {
+static void lora_tn_check(const Tensor& a, const Tensor& b) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.size(0) == b.size(0),
               "lora_tn: a [M, r], b [M, N] GPU tensors");
   const int64_t r = a.size(1), N = b.size(1);
@@ -67,12 +67,32 @@ Tensor lora_tn(const Tensor& a, const Tensor& b, double alpha) {
     return t.stride(1) == 1 && t.stride(0) % 8 == 0 && ((uintptr_t)t.data_ptr() & 15) == 0;
   };
   TORCH_CHECK(ok16(a) && ok16(b), "lora_tn: rows 16-B aligned with unit inner stride");
+}
+
+static void lora_tn_launch(const Tensor& a, const Tensor& b, double alpha, Tensor& out, bool trans) {
+  if (a.size(0) == 0) return;
   c10::DeviceGuard g(a.device());
-  Tensor out = at::zeros({r, N}, a.options().dtype(at::kFloat));
-  if (a.size(0) == 0) return out;
-  illm::launch_lora_tn(a.scalar_type() == at::kBFloat16, (const uint16_t*)a.data_ptr(), a.stride(0), (int)r,
-                       (const uint16_t*)b.data_ptr(), b.stride(0), (int)a.size(0), (int)N, (float)alpha,
-                       out.data_ptr<float>(), cur_stream());
+  illm::launch_lora_tn(a.scalar_type() == at::kBFloat16, (const uint16_t*)a.data_ptr(), a.stride(0), (int)a.size(1),
+                       (const uint16_t*)b.data_ptr(), b.stride(0), (int)a.size(0), (int)b.size(1), (float)alpha,
+                       out.data_ptr<float>(), trans, cur_stream());
+}
+
+Tensor lora_tn(const Tensor& a, const Tensor& b, double alpha) {
+  lora_tn_check(a, b);
+  Tensor out = at::zeros({a.size(1), b.size(1)}, a.options().dtype(at::kFloat));
+  lora_tn_launch(a, b, alpha, out, false);
+  return out;
+}
+
+// accumulate alpha a^T b into a caller-zeroed contiguous f32 region: [r, N],
+// or [N, r] with trans (several gradients share one zero fill and one cast)
+Tensor& lora_tn_acc_(Tensor& out, const Tensor& a, const Tensor& b, double alpha, bool trans) {
+  lora_tn_check(a, b);
+  const int64_t r = a.size(1), N = b.size(1);
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 2 &&
+                  out.size(0) == (trans ? N : r) && out.size(1) == (trans ? r : N),
+              "lora_tn_acc_: out must be a contiguous f32 ", trans ? "[N, r]" : "[r, N]", " tensor");
+  lora_tn_launch(a, b, alpha, out, trans);
   return out;
 }
 
@@ -174,6 +194,7 @@ TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("skinny_tn(Tensor a, Tensor b, float alpha=1.0) -> Tensor");
   m.def("lora_update_(Tensor(a!) c, Tensor a, Tensor b, float alpha=1.0) -> Tensor(a!)");
   m.def("lora_tn(Tensor a, Tensor b, float alpha=1.0) -> Tensor");
+  m.def("lora_tn_acc_(Tensor(a!) out, Tensor a, Tensor b, float alpha=1.0, bool trans=False) -> Tensor(a!)");
 }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
@@ -181,6 +202,7 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("skinny_tn", &skinny_tn);
   m.impl("lora_update_", &lora_update_);
   m.impl("lora_tn", &lora_tn);
+  m.impl("lora_tn_acc_", &lora_tn_acc_);
   m.impl("train_attn_fwd", &train_attn_fwd);
   m.impl("train_attn_bwd", &train_attn_bwd);
 }

@@ -273,6 +273,11 @@ def _(a, b, alpha=1.0):
     return a.new_empty((a.shape[1], b.shape[1]), dtype=torch.float32)
 
 
+@register_fake("ipex_llm_amd::lora_tn_acc_")
+def _(out, a, b, alpha=1.0, trans=False):
+    return out
+
+
 @register_fake("ipex_llm_amd::lora_update_")
 def _(c, a, b, alpha=1.0):
     return c

@@ -103,6 +103,36 @@ def _rank_update_(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, alpha: floa
 _RANK_KERNEL = os.environ.get("ILLM_LORA_RANK_KERNEL", "1") == "1"
 
 
+def _tn_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    from .. import ops
+    r, N = a.shape[1], b.shape[1]
+    return (_TN_KERNEL and a.is_cuda and ops.native_gpu(a) and a.dtype in (torch.bfloat16, torch.float16)
+            and b.dtype == a.dtype and r % 8 == 0 and r <= 64 and N % 8 == 0
+            and all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in (a, b)))
+
+
+def _tn_many(jobs, dtype):
+    """[(a, b, alpha, trans)] -> [alpha a^T b] ([r, N], or [N, r] with trans)
+    in ``dtype``.  On the HIP reduction all of one node's weight gradients
+    accumulate into ONE zeroed f32 slab (the B gradients written transposed
+    by the kernel) and leave through ONE cast: one fill + one cast launch per
+    autograd node instead of a fill, a cast and a transpose copy per gradient"""
+    if not jobs:
+        return []
+    if all(_tn_ok(a, b) for a, b, _, _ in jobs):
+        shapes = [((b.shape[1], a.shape[1]) if tr else (a.shape[1], b.shape[1])) for a, b, _, tr in jobs]
+        slab = torch.zeros(sum(x * y for x, y in shapes), dtype=torch.float32, device=jobs[0][0].device)
+        outs, off = [], 0
+        for (a, b, alpha, tr), (x, y) in zip(jobs, shapes):
+            v = slab[off:off + x * y].view(x, y)
+            torch.ops.ipex_llm_amd.lora_tn_acc_(v, a, b, float(alpha), tr)
+            outs.append((off, x, y))
+            off += x * y
+        cast = slab.to(dtype)
+        return [cast[o:o + x * y].view(x, y) for o, x, y in outs]
+    return [(_tn(a, b, alpha).t().contiguous() if tr else _tn(a, b, alpha)) for a, b, alpha, tr in jobs]
+
+
 def _tn(a: torch.Tensor, b: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
     """alpha * a^T b over the token axis (a [M, r], b [M, N]) -> [r, N] in
     a's dtype: the LoRA weight gradients.  On the HIP token-axis reduction
@@ -110,11 +140,7 @@ def _tn(a: torch.Tensor, b: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
     reads, f32 atomics over row slices) where it applies -- the library
     runs these K = tokens, M = r shapes on a 256 x 128 macro-tile at a
     fraction of HBM speed -- the library GEMM otherwise"""
-    from .. import ops
-    r, N = a.shape[1], b.shape[1]
-    if (_TN_KERNEL and a.is_cuda and ops.native_gpu(a) and a.dtype in (torch.bfloat16, torch.float16)
-            and b.dtype == a.dtype and r % 8 == 0 and r <= 64 and N % 8 == 0
-            and all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 for t in (a, b))):
+    if _tn_ok(a, b):
         return torch.ops.ipex_llm_amd.lora_tn(a, b, float(alpha)).to(a.dtype)
     if alpha == 1.0:
         return torch.mm(a.t(), b)
@@ -168,8 +194,11 @@ class _LoraLowBitFn(torch.autograd.Function):
         # input is never read) instead of separate [M, r] / [N, r] scale launches
         z = g2.new_empty(())                               # (no fill launch)
         gxa = torch.addmm(z, g2, B, beta=0, alpha=s)      # [M, r]
-        gA = _tn(gxa, x2) if ctx.needs_input_grad[1] else None
-        gB = _tn(xa, g2, s).t().contiguous() if ctx.needs_input_grad[2] else None
+        jobs = ([(gxa, x2, 1.0, False)] if ctx.needs_input_grad[1] else []) + \
+            ([(xa, g2, s, True)] if ctx.needs_input_grad[2] else [])
+        res = _tn_many(jobs, A.dtype)
+        gA = res.pop(0) if ctx.needs_input_grad[1] else None
+        gB = res.pop(0) if ctx.needs_input_grad[2] else None
         gx = None
         if ctx.needs_input_grad[0]:
             base = ctx.base
@@ -223,23 +252,25 @@ class _LoraGroupFn(torch.autograd.Function):
         As, Bs = AB[0::2], AB[1::2]
         s = ctx.s
         z = x2.new_empty(())
-        gxas, grads, gx, off = [], [], None, 0
+        jobs, gx, off = [], None, 0
+        # every sibling's s g B lands in its column slice of one [M, sum r]
+        # buffer (strided GEMM output: no concatenation pass)
+        gxa_all = (x2.new_empty if all(g is not None for g in gs) else x2.new_zeros)(xa_all.shape)
         for base, A, B, g in zip(ctx.bases, As, Bs, gs):
             r = A.shape[0]
             if g is None:
-                gxas.append(x2.new_zeros(x2.shape[0], r))
-                grads.append((None, torch.zeros_like(B)))
                 off += r
                 continue
             g2 = g.reshape(-1, g.shape[-1]).to(x2.dtype)
-            gxas.append(torch.addmm(z, g2, B, beta=0, alpha=s))
-            grads.append((None, _tn(xa_all[:, off:off + r], g2, s).t().contiguous()))
+            torch.addmm(z, g2, B, beta=0, alpha=s, out=gxa_all[:, off:off + r])
+            jobs.append((xa_all[:, off:off + r], g2, s, True))         # dB [N, r]
             if ctx.needs_input_grad[0]:
                 w = _base_dense_weight(base, x2.dtype)
                 gx = torch.mm(g2, w) if gx is None else gx.addmm_(g2, w)
             off += r
-        gxa_all = torch.cat(gxas, 1)
-        gA_all = _tn(gxa_all, x2)                                  # [sum r, K]: one pass over x
+        # [sum r, K] (one pass over x) + every dB: one slab, one cast
+        *gBs, gA_all = _tn_many(jobs + [(gxa_all, x2, 1.0, False)], As[0].dtype)
+        grads = [(None, gBs.pop(0) if g is not None else torch.zeros_like(B)) for B, g in zip(Bs, gs)]
         if gx is not None:
             _rank_update_(gx, gxa_all, torch.cat(As, 0).t())
             gx = gx.view(ctx.shp)

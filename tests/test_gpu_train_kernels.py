@@ -159,3 +159,23 @@ def test_lora_tn_matches_fp32(cuda, M, N, r, dt):
     out = torch.ops.ipex_llm_amd.lora_tn(a, b, 0.7)
     assert out.dtype == torch.float32 and out.shape == (r, N)
     assert ((out - ref).norm() / ref.norm()).item() < 1e-4
+
+
+def test_lora_tn_acc_slab_transposed(cuda):
+    """several LoRA gradients accumulated into one zeroed f32 slab, B
+    gradients written transposed ([N, r]) by the kernel (training/lora.py _tn_many)"""
+    from ipex_llm_amd.training.lora import _tn_many
+    torch.manual_seed(5)
+    M = 1000
+    x = torch.randn(M, 512, device=cuda).bfloat16()
+    wide = torch.randn(M, 40, device=cuda).bfloat16()
+    xa = wide[:, 8:32]                                   # 24 = q/k/v r=8 slices, strided
+    gs = [torch.randn(M, n, device=cuda).bfloat16() for n in (512, 128, 128)]
+    gxa = torch.randn(M, 24, device=cuda).bfloat16()
+    jobs = [(xa[:, 8 * i:8 * i + 8], g, 0.5, True) for i, g in enumerate(gs)] + [(gxa, x, 1.0, False)]
+    outs = _tn_many(jobs, torch.bfloat16)
+    for (a, b, al, tr), o in zip(jobs, outs):
+        ref = al * (a.float().t() @ b.float())
+        ref = ref.t() if tr else ref
+        assert o.shape == ref.shape and o.dtype == torch.bfloat16 and o.is_contiguous()
+        assert ((o.float() - ref).norm() / ref.norm()).item() < 1e-2
