@@ -22,6 +22,7 @@ import json
 import math
 import os
 import re
+import weakref
 from dataclasses import asdict, dataclass, field
 from typing import Dict, List, Optional, Union
 
@@ -147,6 +148,8 @@ def _tn(a: torch.Tensor, b: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
     return torch.addmm(a.new_empty(()), a.t(), b, beta=0, alpha=alpha)
 
 
+# ILLM_LORA_GXA_SLICES=0: grouped s g B as separate outputs + concatenation (A/B)
+_GXA_SLICES = os.environ.get("ILLM_LORA_GXA_SLICES", "1") == "1"
 # ILLM_LORA_TN_KERNEL=0: dA / dB on the library GEMM (A/B)
 _TN_KERNEL = os.environ.get("ILLM_LORA_TN_KERNEL", "1") == "1"
 
@@ -215,6 +218,51 @@ class _LoraLowBitFn(torch.autograd.Function):
         return gx, gA, gB, None, None
 
 
+# K-concatenated LoRA for wide siblings (gate / up): y_i = [x | s x A_all^T]
+# [W_i | B_i-block]^T -- the adapter rides as R extra K columns of the base
+# GEMM (R = sum of ranks, <= 0.6 % more MACs) on a resident augmented shadow
+# [N, K + R] whose tail holds B_i in its sibling's column block, instead of a
+# rank-update pass that reads and writes the [M, N] output (235 MB per
+# 14336-wide projection at 4096 tokens).  The backward's g W reads the same
+# shadow through a [:, :K] view.  ILLM_LORA_KCAT=auto (siblings with
+# N >= 2 K, dense shadow budget > 0) / 1 (every group) / 0 (off, A/B).
+_KCAT = os.environ.get("ILLM_LORA_KCAT", "auto")
+_aug_cache = {}                 # (blob ptr, version, R, off, dtype) -> (weakref to blob, [N, K + R] shadow)
+
+
+def _kcat_ok(bases, x2, As) -> bool:
+    from .. import ops
+    from ..ops.gemm import _DENSE_BUDGET
+    if _KCAT == "0" or not (x2.is_cuda and ops.native_gpu(x2) and _DENSE_BUDGET > 0):
+        return False
+    if x2.dtype not in (torch.bfloat16, torch.float16) or x2.shape[0] <= ops.GEMV_MAX_M:
+        return False
+    K, R = x2.shape[1], sum(A.shape[0] for A in As)
+    if (K + R) % 8 or any(b.in_features != K for b in bases):
+        return False
+    return _KCAT == "1" or min(b.out_features for b in bases) >= 2 * K
+
+
+def _aug_weight(base, R: int, off: int, dtype, B=None):
+    """the augmented shadow of ``base`` ([N, K + R], made on first use from the
+    dequantized blob); ``B`` ([N, r], the adapter's current value) is written
+    into columns K + off .. K + off + r"""
+    blob = base.weight
+    key = (blob.data_ptr(), blob._version, R, off, dtype)
+    ent = _aug_cache.get(key)
+    if ent is None or ent[0]() is not blob:
+        N, K = base.out_features, base.in_features
+        w = torch.zeros(N, K + R, dtype=dtype, device=blob.device)
+        w[:, :K].copy_(torch.ops.ipex_llm_amd.dequantize_device(blob, base.fmt, N, K, dtype))
+        ent = (weakref.ref(blob, lambda _r, key=key: _aug_cache.pop(key, None)), w)
+        _aug_cache[key] = ent
+    w = ent[1]
+    if B is not None:
+        K = base.in_features
+        w[:, K + off:K + off + B.shape[1]].copy_(B)
+    return w
+
+
 class _LoraGroupFn(torch.autograd.Function):
     """q / k / v (or gate / up) adapters over ONE shared input as one
     autograd node: x A_all^T for all siblings in one pass over x (A_all =
@@ -230,7 +278,24 @@ class _LoraGroupFn(torch.autograd.Function):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         As, Bs = AB[0::2], AB[1::2]
+        kcat = _kcat_ok(bases, x2, As)
         with torch.no_grad():
+            if kcat:
+                K, R = x2.shape[1], sum(A.shape[0] for A in As)
+                xa_all = torch.addmm(x2.new_empty(()), x2, torch.cat(As, 0).t(), beta=0, alpha=s)   # s x A^T
+                x_ext = torch.cat([x2, xa_all], 1)
+                ys, off = [], 0
+                for base, A, B in zip(bases, As, Bs):
+                    w = _aug_weight(base, R, off, x2.dtype, B)
+                    y = torch.mm(x_ext, w.t())
+                    if base.bias is not None:
+                        y.add_(base.bias.to(y.dtype))
+                    ys.append(y.view(*shp[:-1], y.shape[-1]))
+                    off += A.shape[0]
+                del x_ext
+                ctx.save_for_backward(x2, xa_all, *AB)
+                ctx.s, ctx.shp, ctx.bases, ctx.kcat = s, shp, bases, (R, x2.dtype)
+                return tuple(ys)
             xa_all = torch.mm(x2, torch.cat(As, 0).t())          # [M, sum r]
             ys, off = [], 0
             for base, A, B in zip(bases, As, Bs):
@@ -243,7 +308,7 @@ class _LoraGroupFn(torch.autograd.Function):
                 ys.append(y.view(*shp[:-1], y.shape[-1]))
                 off += r
         ctx.save_for_backward(x2, xa_all, *AB)
-        ctx.s, ctx.shp, ctx.bases = s, shp, bases
+        ctx.s, ctx.shp, ctx.bases, ctx.kcat = s, shp, bases, None
         return tuple(ys)
 
     @staticmethod
@@ -256,18 +321,27 @@ class _LoraGroupFn(torch.autograd.Function):
         # every sibling's s g B lands in its column slice of one [M, sum r]
         # buffer (strided GEMM output: no concatenation pass)
         gxa_all = (x2.new_empty if all(g is not None for g in gs) else x2.new_zeros)(xa_all.shape)
+        gxas = []
         for base, A, B, g in zip(ctx.bases, As, Bs, gs):
             r = A.shape[0]
             if g is None:
+                gxas.append(gxa_all[:, off:off + r])
                 off += r
                 continue
             g2 = g.reshape(-1, g.shape[-1]).to(x2.dtype)
-            torch.addmm(z, g2, B, beta=0, alpha=s, out=gxa_all[:, off:off + r])
-            jobs.append((xa_all[:, off:off + r], g2, s, True))         # dB [N, r]
+            if _GXA_SLICES:
+                torch.addmm(z, g2, B, beta=0, alpha=s, out=gxa_all[:, off:off + r])
+            else:
+                gxas.append(torch.addmm(z, g2, B, beta=0, alpha=s))
+            # dB [N, r] (the K-concat forward saved s x A^T: alpha 1)
+            jobs.append((xa_all[:, off:off + r], g2, 1.0 if ctx.kcat else s, True))
             if ctx.needs_input_grad[0]:
-                w = _base_dense_weight(base, x2.dtype)
+                w = (_aug_weight(base, ctx.kcat[0], off, ctx.kcat[1])[:, :base.in_features] if ctx.kcat
+                     else _base_dense_weight(base, x2.dtype))
                 gx = torch.mm(g2, w) if gx is None else gx.addmm_(g2, w)
             off += r
+        if not _GXA_SLICES:
+            gxa_all = torch.cat(gxas, 1)
         # [sum r, K] (one pass over x) + every dB: one slab, one cast
         *gBs, gA_all = _tn_many(jobs + [(gxa_all, x2, 1.0, False)], As[0].dtype)
         grads = [(None, gBs.pop(0) if g is not None else torch.zeros_like(B)) for B, g in zip(Bs, gs)]

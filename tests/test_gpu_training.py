@@ -195,3 +195,51 @@ def test_act_mul_kernel_matches_hf_mlp(cuda, act, dtype):
         assert ((res[0][0].float() - res[1][0].float()).norm() / res[1][0].float().norm()).item() < 2e-3
     for a, b in zip(res[0][1:], res[1][1:]):
         assert ((a.float() - b.float()).norm() / b.float().norm()).item() < 1e-2
+
+
+def test_lora_group_kcat_matches_rank_update(cuda, monkeypatch):
+    """gate/up-style sibling adapters: the K-concatenated forward ([x | s x A^T]
+    against the augmented [W | B] shadow) == the rank-update forward, values
+    and all gradients; a new adapter value reaches the shadow's tail"""
+    import ipex_llm_amd.training.lora as L
+    from ipex_llm_amd.ops import gemm as G
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    old = G._DENSE_BUDGET
+    G.set_dense_budget(1.0)
+    try:
+        torch.manual_seed(4)
+        bases = [LowBitLinear.from_linear(torch.nn.Linear(256, 1024, bias=False), "nf4").to(cuda) for _ in range(2)]
+        As = [(torch.randn(8, 256, device=cuda) * 0.05).bfloat16().requires_grad_() for _ in range(2)]
+        Bs = [(torch.randn(1024, 8, device=cuda) * 0.05).bfloat16().requires_grad_() for _ in range(2)]
+        x0 = torch.randn(2, 200, 256, device=cuda).bfloat16()
+        gys = [torch.randn(2, 200, 1024, device=cuda).bfloat16() for _ in range(2)]
+        res = {}
+        for mode in ("1", "0", "1"):
+            monkeypatch.setattr(L, "_KCAT", mode)
+            x = x0.clone().requires_grad_()
+            for p in As + Bs:
+                p.grad = None
+            AB = [t for pair in zip(As, Bs) for t in pair]
+            ys = L._LoraGroupFn.apply(x, 2.0, bases, *AB)
+            torch.autograd.backward(ys, gys)
+            res[mode] = [y.float() for y in ys] + [x.grad.float()] + [p.grad.float() for p in As + Bs]
+            with torch.no_grad():                       # the next pass sees a changed adapter
+                Bs[0].add_(0.01)
+        assert L._aug_cache, "augmented shadow not used"
+        # pass 1 (kcat) and pass 2 (rank update) ran on different B values; compare
+        # pass 3 (kcat, B changed twice) with a rank-update rerun on the same values
+        monkeypatch.setattr(L, "_KCAT", "0")
+        with torch.no_grad():
+            Bs[0].sub_(0.01)
+        x = x0.clone().requires_grad_()
+        for p in As + Bs:
+            p.grad = None
+        AB = [t for pair in zip(As, Bs) for t in pair]
+        ys = L._LoraGroupFn.apply(x, 2.0, bases, *AB)
+        torch.autograd.backward(ys, gys)
+        want = [y.float() for y in ys] + [x.grad.float()] + [p.grad.float() for p in As + Bs]
+        for a, b in zip(res["1"], want):
+            assert ((a - b).norm() / b.norm()).item() < 2e-2
+    finally:
+        G.set_dense_budget(old / 2 ** 30)
+        L._aug_cache.clear()
