@@ -224,9 +224,13 @@ class _LoraLowBitFn(torch.autograd.Function):
 # [N, K + R] whose tail holds B_i in its sibling's column block, instead of a
 # rank-update pass that reads and writes the [M, N] output (235 MB per
 # 14336-wide projection at 4096 tokens).  The backward's g W reads the same
-# shadow through a [:, :K] view.  ILLM_LORA_KCAT=auto (siblings with
-# N >= 2 K, dense shadow budget > 0) / 1 (every group) / 0 (off, A/B).
+# shadow through a [:, :K] view.  ILLM_LORA_KCAT=auto (default: siblings with
+# N >= 2 K, dense shadow budget > 0) / 1 (every group) / 0 (off).  Same-box
+# A/B on MI355X, Llama-3-8B QLoRA (profiles/qlora_ab_*kcat*_r4.json): 137.7 vs
+# 140.1 ms/step for the rank-update pass with the extended K padded to 4160;
+# unpadded (K = 4112) it was slower, 142.3 vs 139.9.
 _KCAT = os.environ.get("ILLM_LORA_KCAT", "auto")
+_KCAT_PAD = int(os.environ.get("ILLM_LORA_KCAT_PAD", "64"))
 _aug_cache = {}                 # (blob ptr, version, R, off, dtype) -> (weakref to blob, [N, K + R] shadow)
 
 
@@ -283,7 +287,12 @@ class _LoraGroupFn(torch.autograd.Function):
             if kcat:
                 K, R = x2.shape[1], sum(A.shape[0] for A in As)
                 xa_all = torch.addmm(x2.new_empty(()), x2, torch.cat(As, 0).t(), beta=0, alpha=s)   # s x A^T
-                x_ext = torch.cat([x2, xa_all], 1)
+                # the extended K padded to a multiple of _KCAT_PAD (zero columns):
+                # the library GEMM at K = 4112 picked a slow tile
+                Rp = -(-(K + R) // _KCAT_PAD) * _KCAT_PAD - K
+                parts = [x2, xa_all] + ([x2.new_zeros(x2.shape[0], Rp - R)] if Rp > R else [])
+                x_ext = torch.cat(parts, 1)
+                R = Rp
                 ys, off = [], 0
                 for base, A, B in zip(bases, As, Bs):
                     w = _aug_weight(base, R, off, x2.dtype, B)
