@@ -210,6 +210,16 @@ class _LoraLowBitFn(torch.autograd.Function):
                 # engine GEMM, csrc/hip/gemm_mfma_nn.hip): no dense W
                 gx = torch.ops.ipex_llm_amd.mfgemm_nn(g2, base.weight, base.fmt, base.out_features,
                                                       base.in_features)
+            elif _kcat_rows_ok(base, g2, A):
+                # gx = [g | s g B] [W ; A]: the adapter term as r extra K rows of
+                # the grad_x GEMM (row-augmented shadow) instead of a rank-update
+                # pass over the [M, K] output (the 14336-wide down projection)
+                N, r = base.out_features, A.shape[0]
+                Rp = -(-(N + r) // _KCAT_PAD) * _KCAT_PAD - N
+                w = _aug_rows_weight(base, Rp, x2.dtype, A)
+                parts = [g2, gxa] + ([g2.new_zeros(g2.shape[0], Rp - r)] if Rp > r else [])
+                gx = torch.mm(torch.cat(parts, 1), w).view(ctx.shp)
+                return gx, gA, gB, None, None
             else:
                 w = _base_dense_weight(base, x2.dtype)
                 gx = torch.mm(g2, w)
@@ -231,6 +241,7 @@ class _LoraLowBitFn(torch.autograd.Function):
 # unpadded (K = 4112) it was slower, 142.3 vs 139.9.
 _KCAT = os.environ.get("ILLM_LORA_KCAT", "auto")
 _KCAT_PAD = int(os.environ.get("ILLM_LORA_KCAT_PAD", "64"))
+_KCAT_ROWS = os.environ.get("ILLM_LORA_KCAT_ROWS", "1") == "1"   # the down projection's grad_x form
 _aug_cache = {}                 # (blob ptr, version, R, off, dtype) -> (weakref to blob, [N, K + R] shadow)
 
 
@@ -264,6 +275,37 @@ def _aug_weight(base, R: int, off: int, dtype, B=None):
     if B is not None:
         K = base.in_features
         w[:, K + off:K + off + B.shape[1]].copy_(B)
+    return w
+
+
+def _kcat_rows_ok(base, g2, A) -> bool:
+    """row-augmented grad_x for a single adapter whose input is much wider
+    than its output (down projection: K >= 2 N), same switches as _kcat_ok"""
+    from .. import ops
+    from ..ops.gemm import _DENSE_BUDGET
+    if _KCAT == "0" or not _KCAT_ROWS or not (g2.is_cuda and ops.native_gpu(g2) and _DENSE_BUDGET > 0):
+        return False
+    if g2.dtype not in (torch.bfloat16, torch.float16) or g2.shape[0] <= ops.GEMV_MAX_M or A.dtype != g2.dtype:
+        return False
+    return _KCAT == "1" or base.in_features >= 2 * base.out_features
+
+
+def _aug_rows_weight(base, Rp: int, dtype, A=None):
+    """[N + Rp, K] shadow of ``base``: W on top, ``A`` ([r, K], current value)
+    written into rows N .. N + r, zeros below"""
+    blob = base.weight
+    key = ("rows", blob.data_ptr(), blob._version, Rp, dtype)
+    ent = _aug_cache.get(key)
+    if ent is None or ent[0]() is not blob:
+        N, K = base.out_features, base.in_features
+        w = torch.zeros(N + Rp, K, dtype=dtype, device=blob.device)
+        w[:N].copy_(torch.ops.ipex_llm_amd.dequantize_device(blob, base.fmt, N, K, dtype))
+        ent = (weakref.ref(blob, lambda _r, key=key: _aug_cache.pop(key, None)), w)
+        _aug_cache[key] = ent
+    w = ent[1]
+    if A is not None:
+        N = base.out_features
+        w[N:N + A.shape[0]].copy_(A)
     return w
 
 

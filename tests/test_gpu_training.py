@@ -243,3 +243,34 @@ def test_lora_group_kcat_matches_rank_update(cuda, monkeypatch):
     finally:
         G.set_dense_budget(old / 2 ** 30)
         L._aug_cache.clear()
+
+
+def test_lora_kcat_rows_grad_x_matches(cuda, monkeypatch):
+    """down-projection-style adapter (K >= 2 N): grad_x through the row-
+    augmented [W ; A] shadow == the rank-update grad_x"""
+    import ipex_llm_amd.training.lora as L
+    from ipex_llm_amd.ops import gemm as G
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    old = G._DENSE_BUDGET
+    G.set_dense_budget(1.0)
+    try:
+        torch.manual_seed(6)
+        base = LowBitLinear.from_linear(torch.nn.Linear(1024, 256, bias=False), "nf4").to(cuda)
+        A = (torch.randn(8, 1024, device=cuda) * 0.05).bfloat16().requires_grad_()
+        B = (torch.randn(256, 8, device=cuda) * 0.05).bfloat16().requires_grad_()
+        x0 = torch.randn(2, 200, 1024, device=cuda).bfloat16()
+        gy = torch.randn(2, 200, 256, device=cuda).bfloat16()
+        res = {}
+        for mode in ("1", "0"):
+            monkeypatch.setattr(L, "_KCAT", mode)
+            x = x0.clone().requires_grad_()
+            A.grad = B.grad = None
+            y = L._LoraLowBitFn.apply(x, A, B, base, 2.0)
+            y.backward(gy)
+            res[mode] = [y.float(), x.grad.float(), A.grad.float(), B.grad.float()]
+        assert any(k[0] == "rows" for k in L._aug_cache), "row-augmented shadow not used"
+        for a, b in zip(res["1"], res["0"]):
+            assert ((a - b).norm() / b.norm()).item() < 2e-2
+    finally:
+        G.set_dense_budget(old / 2 ** 30)
+        L._aug_cache.clear()
