@@ -67,6 +67,55 @@ __global__ void __launch_bounds__(256) dense_gemv_kernel(const uint16_t* __restr
   }
 }
 
+// act(x Wg^T) * (x Wu^T) for a gate/up weight in the 16-row tile interleave
+// (rows 32 p .. + 15 gate, 32 p + 16 .. + 31 up: output column 16 p + j): one
+// wave streams the gate and the up row of one output column, so the
+// [M, 2I] projection, the de-interleave copies and the activation / product
+// launches of the unfused path disappear.  Rounding follows that path: g and
+// u rounded to T, act(g) rounded, the product rounded.  act: 0 SiLU, 1 GELU
+// (tanh).
+template <typename T, int MM>
+__global__ void __launch_bounds__(256) dense_glu_kernel(const uint16_t* __restrict__ x, int M, int64_t K,
+                                                        const uint16_t* __restrict__ w, int64_t I, int act,
+                                                        uint16_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= I) return;
+  const int64_t rg = 32 * (i / 16) + (i % 16);
+  const uint16_t* wg = w + rg * K;
+  const uint16_t* wu = wg + 16 * K;
+  float ag[MM], au[MM];
+#pragma unroll
+  for (int m = 0; m < MM; m++) ag[m] = au[m] = 0.f;
+  for (int64_t k = (int64_t)lane * 8; k < K; k += 64 * 8) {
+    const uint4 g0 = *(const uint4*)(wg + k);
+    const uint4 u0 = *(const uint4*)(wu + k);
+#pragma unroll
+    for (int m = 0; m < MM; m++) {
+      if (m < M) {
+        const uint4 xv = *(const uint4*)(x + (int64_t)m * K + k);
+        ag[m] += dot8<T>(g0, xv);
+        au[m] += dot8<T>(u0, xv);
+      }
+    }
+  }
+  auto rnd = [](float v) { return to_f32<T>(from_f32<T>(v)); };
+#pragma unroll
+  for (int m = 0; m < MM; m++) {
+    if (m < M) {
+      const float g = rnd(wave_sum(ag[m])), u = rnd(wave_sum(au[m]));
+      float a;
+      if (act == 0) {
+        a = g / (1.f + __expf(-g));
+      } else {
+        const float c = 0.7978845608028654f * (g + 0.044715f * g * g * g);
+        a = 0.5f * g * (1.f + tanhf(c));
+      }
+      if (lane == 0) out[(int64_t)m * I + i] = from_f32<T>(rnd(a) * u);
+    }
+  }
+}
+
 template <typename T>
 static void dg_t(const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t N, const uint16_t* bias,
                  uint16_t* out, hipStream_t st) {
@@ -78,6 +127,25 @@ static void dg_t(const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t
   else if (M <= 8) DG(8);
   else DG(16);
 #undef DG
+}
+
+template <typename T>
+static void dglu_t(const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t I, int act, uint16_t* out,
+                   hipStream_t st) {
+  const dim3 grid((unsigned)((I + 3) / 4));
+#define DG(MMV) hipLaunchKernelGGL((dense_glu_kernel<T, MMV>), grid, dim3(256), 0, st, x, M, K, w, I, act, out)
+  if (M <= 1) DG(1);
+  else if (M <= 2) DG(2);
+  else if (M <= 4) DG(4);
+  else if (M <= 8) DG(8);
+  else DG(16);
+#undef DG
+}
+
+void launch_dense_glu(bool bf16, const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t I, int act,
+                      uint16_t* out, hipStream_t st) {
+  if (bf16) dglu_t<BF16>(x, M, K, w, I, act, out, st);
+  else dglu_t<F16>(x, M, K, w, I, act, out, st);
 }
 
 void launch_dense_gemv(bool bf16, const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t N,

@@ -115,6 +115,9 @@ void launch_kq_gemv(int fmt, bool bf16, const uint16_t* x, int M, int64_t K, con
                     uint16_t* out, hipStream_t st);
 
 // ---- dense bf16/f16 skinny GEMM (dense_gemv.hip): M <= 16, K % 8 == 0 ----
+// act(x Wg^T) * (x Wu^T), W = 16-row tile-interleaved gate/up [2I, K], M <= 16
+void launch_dense_glu(bool bf16, const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t I, int act,
+                      uint16_t* out, hipStream_t st);
 void launch_dense_gemv(bool bf16, const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t N,
                        const uint16_t* bias, uint16_t* out, hipStream_t st);
 

@@ -38,10 +38,32 @@ Tensor dense_linear_hip(const Tensor& x, const Tensor& w, const c10::optional<Te
   return y;
 }
 
+// act(x Wg^T) * (x Wu^T) over a 16-row tile-interleaved gate/up weight [2I, K]
+Tensor dense_glu_hip(const Tensor& x, const Tensor& w, int64_t act) {
+  c10::DeviceGuard g(x.device());
+  const int64_t K = x.size(-1), I = w.size(0) / 2;
+  const int64_t M = x.numel() / K;
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.size(0) % 32 == 0, "dense_glu: w must be [2I, K], 2I % 32 == 0");
+  TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) &&
+                  w.scalar_type() == x.scalar_type() && K % 8 == 0 && M <= 16 && w.is_contiguous() &&
+                  (act == 0 || act == 1),
+              "dense_glu: one 16-bit dtype, K % 8 == 0, <= 16 rows, contiguous w, act 0/1");
+  Tensor xc = x.contiguous();
+  auto shape = x.sizes().vec();
+  shape.back() = I;
+  Tensor y = at::empty(shape, xc.options());
+  if (M > 0)
+    illm::launch_dense_glu(x.scalar_type() == at::kBFloat16, (const uint16_t*)xc.data_ptr(), (int)M, K,
+                           (const uint16_t*)w.data_ptr(), I, (int)act, (uint16_t*)y.data_ptr(),
+                           at::hip::getCurrentHIPStream().stream());
+  return y;
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("dense_linear(Tensor x, Tensor w, Tensor? bias) -> Tensor");
+  m.def("dense_glu(Tensor x, Tensor w, int act=0) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
@@ -50,4 +72,5 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("dense_linear", &dense_linear_hip);
+  m.impl("dense_glu", &dense_glu_hip);
 }

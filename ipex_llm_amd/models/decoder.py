@@ -124,6 +124,16 @@ def interleave_glu_rows(gate: torch.Tensor, up: torch.Tensor, tile: int = 16) ->
     return torch.stack([gate.view(I // tile, tile, K), up.view(I // tile, tile, K)], 1).reshape(2 * I, K)
 
 
+# decode-size GLU over dense (bf16 / fp16) gate/up weights in one streaming
+# launch (csrc/hip/dense_gemv.hip dense_glu); ILLM_DENSE_GLU=0 for A/B
+_DENSE_GLU = __import__("os").environ.get("ILLM_DENSE_GLU", "1") != "0"
+# rows up to which it runs: MI355X, Llama-3-8B bf16 (profiles/spec_{glu,noglu}_r4.jsonl):
+# one-token decode 3.790 -> 3.527 ms/token, but the 3-4-row speculative verify
+# got slower (k = 2: 3.389 -> 3.551 ms/token), half as many waves each
+# streaming two rows with 4 activation rows of VALU per byte
+DENSE_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DENSE_GLU_MAX_M", "2"))
+
+
 def deinterleave_glu(gu: torch.Tensor, tile: int = 16):
     shp = gu.shape[:-1]
     I = gu.shape[-1] // 2
@@ -563,6 +573,12 @@ class NativeCausalLM(nn.Module):
             # prefill: the activation runs in the GEMM epilogue (no [T, 2I] round trip)
             from ..ops.gemm import lowbit_gemm_glu
             return lowbit_gemm_glu(x.contiguous(), gu.weight, gu.fmt, gu.out_features, gu.in_features, s.act)
+        if _DENSE_GLU and x.is_cuda and isinstance(gu, DenseLinear) and gu.bias is None and gu.mp_group is None \
+                and x.shape[0] <= DENSE_GLU_MAX_M and s.act in (0, 1) and x.dtype == gu.weight.dtype \
+                and ops.native_gpu(x) \
+                and gu.out_features % 32 == 0 and gu.in_features % 8 == 0:
+            # decode / verify rows on dense weights: one streaming launch, GLU in its epilogue
+            return torch.ops.ipex_llm_amd.dense_glu(x, gu.weight, s.act)
         y = gu(x)
         g, u = deinterleave_glu(y)
         a = F.silu(g) if s.act == 0 else F.gelu(g, approximate="tanh")

@@ -273,6 +273,11 @@ def _(a, b, alpha=1.0):
     return a.new_empty((a.shape[1], b.shape[1]), dtype=torch.float32)
 
 
+@register_fake("ipex_llm_amd::dense_glu")
+def _(x, w, act=0):
+    return x.new_empty((*x.shape[:-1], w.shape[0] // 2))
+
+
 @register_fake("ipex_llm_amd::lora_tn_acc_")
 def _(out, a, b, alpha=1.0, trans=False):
     return out

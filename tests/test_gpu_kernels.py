@@ -693,3 +693,28 @@ def test_decode_oproj_combine_with_deferred_norm(cuda):
     assert eager == outs[True]
     a, b = sum(outs[False], []), sum(outs[True], [])
     assert sum(x == y for x, y in zip(a, b)) >= 0.95 * len(a)
+
+
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+@pytest.mark.parametrize("act", [0, 1])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_dense_glu_matches_unfused(cuda, M, act, dt):
+    """dense_glu (csrc/hip/dense_gemv.hip): act(x Wg^T) * (x Wu^T) over the
+    16-row tile-interleaved gate/up weight == the unfused dense path
+    (projection, de-interleave, activation, product) and an fp32 reference"""
+    import torch.nn.functional as F
+    from ipex_llm_amd.models.decoder import deinterleave_glu
+    torch.manual_seed(M + 10 * act)
+    K, I = 512, 384
+    w = (torch.randn(2 * I, K, device=cuda) * 0.05).to(dt)
+    x = torch.randn(M, K, device=cuda).to(dt)
+    got = torch.ops.ipex_llm_amd.dense_glu(x, w, act)
+    y = torch.ops.ipex_llm_amd.dense_linear(x, w, None)
+    g, u = deinterleave_glu(y)
+    a = F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")
+    want = (a * u).float()
+    assert got.shape == (M, I) and got.dtype == dt
+    assert ((got.float() - want).norm() / want.norm()).item() < 1e-2
+    gf, uf = deinterleave_glu(x.float() @ w.float().t())
+    ref = (F.silu(gf) if act == 0 else F.gelu(gf, approximate="tanh")) * uf
+    assert ((got.float() - ref).norm() / ref.norm()).item() < 2e-2
