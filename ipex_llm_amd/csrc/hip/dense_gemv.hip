@@ -87,18 +87,42 @@ __global__ void __launch_bounds__(256) dense_glu_kernel(const uint16_t* __restri
   float ag[MM], au[MM];
 #pragma unroll
   for (int m = 0; m < MM; m++) ag[m] = au[m] = 0.f;
-  for (int64_t k = (int64_t)lane * 8; k < K; k += 64 * 8) {
-    const uint4 g0 = *(const uint4*)(wg + k);
-    const uint4 u0 = *(const uint4*)(wu + k);
+  // each weight / activation element is widened once per step and shared by
+  // the gate and up products of every row (the per-call conversions of two
+  // dot8s per row made the 3-4-row verify VALU-bound)
+  auto step = [&](const uint4& g0, const uint4& u0, int64_t k) {
+    float gf[8], uf[8];
+    const uint32_t gs[4] = {g0.x, g0.y, g0.z, g0.w}, us[4] = {u0.x, u0.y, u0.z, u0.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      gf[2 * j] = to_f32<T>(gs[j] & 0xffff), gf[2 * j + 1] = to_f32<T>(gs[j] >> 16);
+      uf[2 * j] = to_f32<T>(us[j] & 0xffff), uf[2 * j + 1] = to_f32<T>(us[j] >> 16);
+    }
 #pragma unroll
     for (int m = 0; m < MM; m++) {
       if (m < M) {
         const uint4 xv = *(const uint4*)(x + (int64_t)m * K + k);
-        ag[m] += dot8<T>(g0, xv);
-        au[m] += dot8<T>(u0, xv);
+        const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
+        float sg = 0.f, su = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const float x0 = to_f32<T>(xs[j] & 0xffff), x1 = to_f32<T>(xs[j] >> 16);
+          sg += gf[2 * j] * x0 + gf[2 * j + 1] * x1;
+          su += uf[2 * j] * x0 + uf[2 * j + 1] * x1;
+        }
+        ag[m] += sg;
+        au[m] += su;
       }
     }
+  };
+  int64_t k = (int64_t)lane * 8;
+  for (; k + 64 * 8 < K; k += 2 * 64 * 8) {         // two gate + two up loads per lane in flight
+    const uint4 g0 = *(const uint4*)(wg + k), g1 = *(const uint4*)(wg + k + 64 * 8);
+    const uint4 u0 = *(const uint4*)(wu + k), u1 = *(const uint4*)(wu + k + 64 * 8);
+    step(g0, u0, k);
+    step(g1, u1, k + 64 * 8);
   }
+  for (; k < K; k += 64 * 8) step(*(const uint4*)(wg + k), *(const uint4*)(wu + k), k);
   auto rnd = [](float v) { return to_f32<T>(from_f32<T>(v)); };
 #pragma unroll
   for (int m = 0; m < MM; m++) {

@@ -127,11 +127,13 @@ def interleave_glu_rows(gate: torch.Tensor, up: torch.Tensor, tile: int = 16) ->
 # decode-size GLU over dense (bf16 / fp16) gate/up weights in one streaming
 # launch (csrc/hip/dense_gemv.hip dense_glu); ILLM_DENSE_GLU=0 for A/B
 _DENSE_GLU = __import__("os").environ.get("ILLM_DENSE_GLU", "1") != "0"
-# rows up to which it runs: MI355X, Llama-3-8B bf16 (profiles/spec_{glu,noglu}_r4.jsonl):
-# one-token decode 3.790 -> 3.527 ms/token, but the 3-4-row speculative verify
-# got slower (k = 2: 3.389 -> 3.551 ms/token), half as many waves each
-# streaming two rows with 4 activation rows of VALU per byte
-DENSE_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DENSE_GLU_MAX_M", "2"))
+# rows up to which it runs -- every decode / verify size: a row's result must
+# not depend on how many rows share the launch, or the k + 1-row speculative
+# verify stops reproducing one-token greedy decoding (capping it at 2 rows
+# dropped the generated-token agreement to 0.016, profiles/spec_glu2_r4.jsonl).
+# MI355X, Llama-3-8B bf16 (profiles/spec_glu16_r4.jsonl, spec_noglu_r4.jsonl):
+# one-token decode 3.790 -> 3.522 ms/token; speculative k = 2 3.444 ms/token
+DENSE_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DENSE_GLU_MAX_M", "16"))
 
 
 def deinterleave_glu(gu: torch.Tensor, tile: int = 16):
