@@ -57,7 +57,10 @@ def test_graph_speculative_matches_target(k, adaptive, heads):
         gap, scale = _tie_gap(te, prompt + ref[:i], ref[i], out[i])
         print(f"k={k} adaptive={adaptive}: first divergence at generated token {i}: "
               f"target {ref[i]} vs speculative {out[i]}, logit gap {gap:.4g} (scale {scale:.3g})")
-        assert gap <= 2e-2 * max(1.0, scale), (k, adaptive, i, gap, scale)
+        # every verify row is reduced exactly as in one-token decoding (chunked
+        # decode attention, row-count-independent GEMV / GLU kernels): a
+        # divergence is a numerics mismatch, not a tie, and fails
+        assert False, (k, adaptive, i, gap, scale)
     else:
         print(f"k={k} adaptive={adaptive}: all {n_new} generated tokens equal the target's")
     assert sp.graphs, "no round ran from a captured graph"
