@@ -21,6 +21,9 @@ captured hipGraph.  W
 untimed warmup steps, then EXACTLY K timed decode steps bracketed by barrier
 + synchronize; the slowest rank's time is reported.  Every timed step runs
 the full model (all layers + lm_head + argmax) for the whole batch.
+With N > 1 in the default data-parallel mode the same model is also run
+tensor-parallel over all N ranks (fixed global batch) and reported as the
+``tp_side`` field of the one JSON line (``--no-tp-side`` skips it).
 
     python bench.py --gpus 1 --steps 64 --warmup 8
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
@@ -84,74 +87,19 @@ MODELS = {"llama3-8b": ("Llama-3-8B", llama3_8b_config), "llama3-70b": ("Llama-3
           "mixtral-8x7b": ("Mixtral-8x7B", mixtral_8x7b_config), "qwen2.5-7b": ("Qwen2.5-7B", qwen25_7b_config)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="llama3-8b", choices=sorted(MODELS))
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=64)
-    ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "8")))
-    ap.add_argument("--prompt-len", type=int, default=1024)
-    ap.add_argument("--qtype", default="sym_int4")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-prefill-graph", action="store_true",
-                    help="eager prefill (default: the batched prefill is captured once per shape as a hipGraph "
-                         "in the untimed first trial and replayed)")
-    ap.add_argument("--layers", type=int, default=None, help="debug only: fewer layers (invalid for the metric)")
-    ap.add_argument("--tp", action="store_true", help="tensor parallel over all ranks (AutoTP)")
-    ap.add_argument("--ep", action="store_true", help="expert parallel over all ranks (MoE models)")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-        # the collective backend really spans the job: RCCL sum of ones
-        chk = torch.ones(1, device=dev)
-        dist.all_reduce(chk)
-        assert int(chk.item()) == world, f"RCCL world {int(chk.item())} != WORLD_SIZE {world}"
-
-    import ipex_llm_amd.ops as ops
-    ops.require()
-    from ipex_llm_amd.models.builder import random_native_model
-    from ipex_llm_amd.engine.runner import Engine, DecodeStep
+def measure(model, eng, args, prompts, dev, world, rank):
+    """first-token latency (1 warm-up + 3 trials of the batched prefill) and
+    K timed decode steps after W warm-up steps, slowest rank; returns
+    (ms per step, first-token ms, next ids, prefill graph used)"""
     from ipex_llm_amd.models.cache import SequenceState
-
-    mname, mcfg = MODELS[args.model]
-    cfg = mcfg()
-    if args.layers:
-        cfg.num_hidden_layers = args.layers
-    sharded = world > 1 and (args.tp or args.ep)
-    if args.ep and not getattr(cfg, "num_local_experts", None):
-        raise SystemExit("--ep needs an MoE model (e.g. --model mixtral-8x7b)")
-    group = dist.group.WORLD if sharded else None
-    if sharded and args.tp:
-        from ipex_llm_amd.parallel.comm import setup_custom_all_reduce
-        setup_custom_all_reduce(group)
-    B, P = args.batch, args.prompt_len
-    t_build = time.perf_counter()
-    # TP / EP: the same weights on every rank (one seed), each keeps its shard
-    model = random_native_model(cfg, args.qtype, dev, torch.bfloat16, seed=1234 + (0 if sharded else rank),
-                                tp_group=group if args.tp else None, ep_group=group if args.ep else None,
-                                ep_tokens=bool(args.ep), ep_max_tokens=B * P)
-    torch.cuda.synchronize()
-    t_build = time.perf_counter() - t_build
-    max_len = P + args.warmup + args.steps + 8
-    eng = Engine(model)
+    B = prompts.shape[0]
+    max_len = args.prompt_len + args.warmup + args.steps + 8
     eng._ensure_cache(B, max_len)
-    same_tokens = sharded and args.tp            # TP: one batch; DP / token-sharded EP: a batch per rank
-    g = torch.Generator().manual_seed(7 + (0 if same_tokens else rank))
-    prompts = torch.randint(0, cfg.vocab_size, (B, P), generator=g)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    # ---- first-token latency (prefill of the whole batch + first token),
-    # 1 warm-up + 3 trials (reference all-in-one harness semantics)
     nblk = (max_len + eng.block_size - 1) // eng.block_size
     barrier()                                    # EP: the MoE exchanges need every rank in step
     ftl = []
@@ -183,14 +131,111 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     tok = st.next_ids.clone()
-
-    t = torch.tensor([dt, sum(ftl) / len(ftl)], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt, sum(ftl) / len(ftl)], dtype=torch.float64)
     if world > 1:
+        if dist.get_backend() == "nccl":
+            t = t.to(dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt, ftl_ms = t.tolist()
-    ms_step = dt / args.steps * 1e3
+    return dt / args.steps * 1e3, ftl_ms, tok, pf_graph
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b", choices=sorted(MODELS))
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "8")))
+    ap.add_argument("--prompt-len", type=int, default=1024)
+    ap.add_argument("--qtype", default="sym_int4")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-prefill-graph", action="store_true",
+                    help="eager prefill (default: the batched prefill is captured once per shape as a hipGraph "
+                         "in the untimed first trial and replayed)")
+    ap.add_argument("--layers", type=int, default=None, help="debug only: fewer layers (invalid for the metric)")
+    ap.add_argument("--tp", action="store_true", help="tensor parallel over all ranks (AutoTP)")
+    ap.add_argument("--ep", action="store_true", help="expert parallel over all ranks (MoE models)")
+    ap.add_argument("--no-tp-side", action="store_true",
+                    help="N > 1 data-parallel run: skip the tensor-parallel (strong-scaling) side measurement")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # code-path smoke only (tests/test_gpu_bench_dist.py): every rank on cuda:0,
+    # gloo rendezvous, the peer all-reduce / all-to-all forced over it
+    shared = os.environ.get("BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = 0
+        os.environ.setdefault("ILLM_AR_P2P", "force")
+        os.environ.setdefault("ILLM_EP_P2P", "force")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        if shared:
+            dist.init_process_group("gloo")
+            chk = torch.ones(1)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+            chk = torch.ones(1, device=dev)
+        # the collective backend really spans the job: a sum of ones
+        dist.all_reduce(chk)
+        assert int(chk.item()) == world, f"world {int(chk.item())} != WORLD_SIZE {world}"
+
+    import ipex_llm_amd.ops as ops
+    ops.require()
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.engine.runner import Engine
+
+    mname, mcfg = MODELS[args.model]
+    cfg = mcfg()
+    if args.layers:
+        cfg.num_hidden_layers = args.layers
+    sharded = world > 1 and (args.tp or args.ep)
+    if args.ep and not getattr(cfg, "num_local_experts", None):
+        raise SystemExit("--ep needs an MoE model (e.g. --model mixtral-8x7b)")
+    group = dist.group.WORLD if sharded else None
+    if sharded and args.tp:
+        from ipex_llm_amd.parallel.comm import setup_custom_all_reduce
+        setup_custom_all_reduce(group)
+    B, P = args.batch, args.prompt_len
+    t_build = time.perf_counter()
+    # TP / EP: the same weights on every rank (one seed), each keeps its shard
+    model = random_native_model(cfg, args.qtype, dev, torch.bfloat16, seed=1234 + (0 if sharded else rank),
+                                tp_group=group if args.tp else None, ep_group=group if args.ep else None,
+                                ep_tokens=bool(args.ep), ep_max_tokens=B * P)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t_build
+    eng = Engine(model)
+    same_tokens = sharded and args.tp            # TP: one batch; DP / token-sharded EP: a batch per rank
+    g = torch.Generator().manual_seed(7 + (0 if same_tokens else rank))
+    prompts = torch.randint(0, cfg.vocab_size, (B, P), generator=g)
+    ms_step, ftl_ms, tok, pf_graph = measure(model, eng, args, prompts, dev, world, rank)
+    dense_gb = eng.prefill_dense_gb
+
+    # N > 1 data-parallel: the same model tensor-parallel over all ranks as a
+    # side result (strong scaling, fixed global batch B): the replicas above
+    # never cross xGMI, this run all-reduces every row-parallel projection over
+    # the custom peer all-reduce / RCCL inside the captured decode graph
+    tp_side = None
+    if world > 1 and not sharded and not args.no_tp_side and world <= 8 \
+            and cfg.num_attention_heads % world == 0 and cfg.num_key_value_heads % world == 0:
+        del eng, model
+        torch.cuda.empty_cache()
+        from ipex_llm_amd.parallel.comm import setup_custom_all_reduce
+        wg = dist.group.WORLD
+        setup_custom_all_reduce(wg)
+        tp_model = random_native_model(cfg, args.qtype, dev, torch.bfloat16, seed=1234, tp_group=wg)
+        tp_eng = Engine(tp_model)
+        tp_prompts = torch.randint(0, cfg.vocab_size, (B, P), generator=torch.Generator().manual_seed(7))
+        t_ms, t_ftl, _, _ = measure(tp_model, tp_eng, args, tp_prompts, dev, world, rank)
+        tp_side = {"parallelism": f"tp{world}", "scaling": "strong", "global_batch": B,
+                   "value": round(B * 1e3 / t_ms, 2), "unit": "tokens/s", "ms_per_step": round(t_ms, 4),
+                   "first_token_latency_ms": round(t_ftl, 2)}
+
     replicas = 1 if same_tokens else world
-    value = B * replicas * args.steps / dt
+    value = B * replicas * 1e3 / ms_step
     if rank == 0:
         out = {
             "metric": f"decode tokens/sec + first-token latency, {mname} INT4 at 1/2/4/8 MI355X",
@@ -205,7 +250,7 @@ def main():
                        "batch_per_gpu": B if not same_tokens else B / world, "seq_len": P,
                        "parallelism": f"tp{world}" if args.tp else (f"ep{world}" if args.ep else f"dp{world}"),
                        "hipgraph": not args.no_graph, "prefill_hipgraph": pf_graph,
-                       "prefill_dense_shadow_gb": eng.prefill_dense_gb,
+                       "prefill_dense_shadow_gb": dense_gb,
                        "layers": cfg.num_hidden_layers},
             "first_token_latency_ms": round(ftl_ms, 2),
             "decode_ms_per_token": round(ms_step, 4),
@@ -218,10 +263,11 @@ def main():
                                   "ours_per_sequence_tokens_per_s": round(1e3 / ms_step, 2)},
             "build_s": round(t_build, 1), "sample_next_ids": tok[:4].tolist(),
         }
+        if tp_side is not None:
+            out["tp_side"] = tp_side
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
 
 if __name__ == "__main__":
     main()

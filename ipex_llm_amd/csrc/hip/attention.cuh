@@ -1159,9 +1159,21 @@ static void launch_v2(const AttnDecodeArgs& a0, hipStream_t st) {
     launch_combine<T>(a, st);
 }
 
+}  // namespace illm
+#include "attn_dec_v3.cuh"
+namespace illm {
+
 template <typename T, int D>
 void launch_d(const AttnDecodeArgs& a, hipStream_t st) {
   const int R = (a.Hq / a.Hkv) * a.Tq;
+  if constexpr (D == 64 || D == 128) {
+    if (v3_ok(a, D)) {
+      if constexpr (D == 128) {
+        if (a.rq_part != nullptr) return launch_v3<T, D, true>(a, st);
+      }
+      return launch_v3<T, D, false>(a, st);
+    }
+  }
   // P V on MFMA (ILLM_ATTN_PVM=0 keeps the per-lane FMA form, for A/B runs)
   static const bool pvm = getenv("ILLM_ATTN_PVM") ? atoi(getenv("ILLM_ATTN_PVM")) != 0 : true;
   if constexpr (D == 64 || D == 128) {

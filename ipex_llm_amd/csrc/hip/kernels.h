@@ -235,6 +235,9 @@ struct AttnDecodeArgs {
   int rq_prerot;            // rq_part already holds rotated q / k (RoPE in the qkv GEMV epilogue)
   int num_blocks;           // cache blocks: block-table entries are bounds-checked
   int* err;                 // kernel error word or null
+  // v3 (attn_dec_v3.cuh): zeroed [B * Hkv] arrival counters for its in-kernel
+  // combine (null: separate combine launch)
+  int* v3_counters;
 };
 void launch_attn_decode(bool bf16, const AttnDecodeArgs& a, hipStream_t st);
 

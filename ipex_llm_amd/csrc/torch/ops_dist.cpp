@@ -1,5 +1,5 @@
 // Peer-memory (hipIpc) buffers and the one-shot xGMI all-reduce op.
-//   ipc_alloc(nbytes) -> int        device pointer of a zeroed hipMalloc buffer
+//   ipc_alloc(nbytes, uncached) -> int  device pointer of a zeroed (uncached) buffer
 //   ipc_handle(ptr) -> Tensor       64-byte hipIpcMemHandle (CPU uint8)
 //   ipc_open(handle) -> int         peer buffer mapped into this process
 //   ipc_close(ptr) / ipc_free(ptr)
@@ -27,9 +27,17 @@ namespace {
     TORCH_CHECK(e_ == hipSuccess, #x " failed: ", hipGetErrorString(e_));                \
   } while (0)
 
-int64_t ipc_alloc(int64_t nbytes) {
+// uncached: hipDeviceMallocUncached memory (never held in any L2).  Peer
+// buffers are written by OTHER GPUs over xGMI (signal epochs, EP dispatch rows
+// and counts) and polled / read by the owner: a coarse-grained hipMalloc line
+// the owner's L2 still holds would not see a peer's store (remote writes do not
+// invalidate it, and an acquire does not invalidate locally-owned lines), so
+// the flags and every peer-written byte live in uncached memory -- the form
+// the ROCm custom all-reduces use for their signal buffers.
+int64_t ipc_alloc(int64_t nbytes, bool uncached) {
   void* p = nullptr;
-  HIP_OK(hipMalloc(&p, (size_t)nbytes));
+  if (uncached) HIP_OK(hipExtMallocWithFlags(&p, (size_t)nbytes, hipDeviceMallocUncached));
+  else HIP_OK(hipMalloc(&p, (size_t)nbytes));
   HIP_OK(hipMemset(p, 0, (size_t)nbytes));
   HIP_OK(hipDeviceSynchronize());
   return (int64_t)(uintptr_t)p;
@@ -270,7 +278,7 @@ void fused_adamw(const Tensor& table, const Tensor& chunk_tensor, const Tensor& 
 
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("fused_adamw(Tensor table, Tensor chunk_tensor, Tensor chunk_start, int chunk, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, float grad_scale, int param_dtype, int grad_dtype, Tensor? step_lr=None) -> ()");
-  m.def("ipc_alloc(int nbytes) -> int", &ipc_alloc);
+  m.def("ipc_alloc(int nbytes, bool uncached=False) -> int", &ipc_alloc);
   m.def("ipc_handle(int ptr) -> Tensor", &ipc_handle);
   m.def("ipc_open(Tensor handle) -> int", &ipc_open);
   m.def("ipc_close(int ptr) -> ()", &ipc_close);

@@ -831,6 +831,29 @@ Tensor kernel_errors(const Tensor& like, bool reset) {
   return out;
 }
 
+// v3 decode attention (attn_dec_v3.cuh): the last-arriving split workgroup of
+// each (batch, kv head) merges the partials in-kernel (its own counter buffer:
+// the v2 fused combine keeps ILLM_ATTN_FUSED_COMBINE).  Default on: MI355X,
+// Llama-3-8B at 1 K keys, per layer from cold caches (profiles/attn_dec_v3_r5.jsonl):
+// batch 1 9.42 vs 10.29 us with the combine launch, batch 8 18.50 vs 18.57;
+// ILLM_ATTN_V3_FUSE=0 keeps the combine launch
+static bool v3_fuse_on() {
+  static const bool on = [] {
+    const char* e = getenv("ILLM_ATTN_V3_FUSE");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+int* attn_counters(const c10::Device& dev, int64_t n);
+static int* v3_counters(const c10::Device& dev, int64_t n) {
+  static std::vector<Tensor> bufs(64);
+  const int idx = dev.index() < 0 ? 0 : dev.index();
+  constexpr int64_t kCap = 1 << 16;
+  if (n > kCap) return nullptr;
+  if (!bufs[idx].defined()) bufs[idx] = at::zeros({kCap}, at::TensorOptions().device(dev).dtype(at::kInt));
+  return bufs[idx].data_ptr<int>();
+}
+
 int* attn_counters(const c10::Device& dev, int64_t n) {
   static std::vector<Tensor> bufs(64);
   const int idx = dev.index() < 0 ? 0 : dev.index();
@@ -947,6 +970,7 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_impl(const Tensor& q, cons
                 "attn_decode: alibi must be a contiguous f32 [Hq] device tensor");
   a.alibi = (alibi.has_value() && alibi->defined()) ? alibi->data_ptr<float>() : nullptr;
   a.counters = fused_combine_on() ? attn_counters(q.device(), B * Hkv) : nullptr;
+  a.v3_counters = !no_combine && v3_fuse_on() ? v3_counters(q.device(), B * Hkv) : nullptr;
   a.no_combine = no_combine ? 1 : 0;
   illm::launch_attn_decode(bf16, a, cur_stream());
   return {out, po, pml};
@@ -1008,6 +1032,7 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
   // accumulator; split-only (no_combine): the consumer merges and a later
   // launch zeroes it
   a.counters = !no_combine && fused_combine_on() ? attn_counters(part.device(), B * Hkv) : nullptr;
+  a.v3_counters = !no_combine && v3_fuse_on() ? v3_counters(part.device(), B * Hkv) : nullptr;
   a.no_combine = no_combine ? 1 : 0;
   a.rq_part = part.data_ptr<float>();
   a.rq_bias = p16o(bias);

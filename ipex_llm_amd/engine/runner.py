@@ -189,8 +189,10 @@ class Engine:
         if p is None and hasattr(model, "buffers"):
             p = next(iter(model.buffers()), None)
         if p is not None and p.is_cuda:
+            # bounded by half of the free HBM (as serving.engine.LLMEngine does)
             from ..ops.gemm import auto_dense_budget
-            self.prefill_dense_gb = auto_dense_budget(p.device)
+            free, _ = torch.cuda.mem_get_info(p.device)
+            self.prefill_dense_gb = auto_dense_budget(p.device, cap_gb=0.5 * free / 2 ** 30)
 
     def _ensure_cache(self, batch: int, max_len: int):
         blocks = batch * ((max_len + self.block_size - 1) // self.block_size)
@@ -244,7 +246,7 @@ class Engine:
             fresh = ent is None
             if fresh:
                 ent = self._prefill_buffers(B, n, nb)
-            graph, ids_s, slots_s, bt_s, out, meta, pos, lidx = ent
+            graph, ids_s, slots_s, bt_s, out, meta, pos, lidx = ent[:8]
             ids_s.copy_(ids.reshape(-1).to(dev), non_blocking=True)
             slots_s.copy_(torch.cat([slots_for(s, 0, n, c.bs) for s in seqs]).to(dev), non_blocking=True)
             bt_s.copy_(make_block_table(seqs, nb, dev))
@@ -257,9 +259,12 @@ class Engine:
                     m.forward_tokens(ids_s, pos, slots_s, meta, c, logits_idx=lidx)
                 torch.cuda.current_stream(dev).wait_stream(side)
                 graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
+                from ..ops.gemm import pin_dense_shadows
+                # the resident dequantized shadows the graph reads are pinned in its
+                # entry: a later cache drop cannot free memory the replay still reads
+                with pin_dense_shadows() as pins, torch.cuda.graph(graph):
                     out = m.forward_tokens(ids_s, pos, slots_s, meta, c, logits_idx=lidx)
-                ent = (graph, ids_s, slots_s, bt_s, out, meta, pos, lidx)
+                ent = (graph, ids_s, slots_s, bt_s, out, meta, pos, lidx, pins)
                 self._pf_graphs[key] = ent
             graph.replay()
             for s in seqs:

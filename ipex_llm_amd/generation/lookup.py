@@ -30,15 +30,26 @@ def performance_mode_lookahead(prompt_len: int) -> Optional[int]:
 
 
 class PromptLookupCandidates:
-    """n-gram -> earliest position table, updated as tokens are generated."""
+    """n-gram -> earliest position table, updated as tokens are generated, and
+    the reference's adaptive candidate count
+    (``PromptLookupCandidateGenerator.update_candidate_strategy``,
+    SRC/transformers/lookup.py:163-175, 253-270): +1 (capped at
+    ``max_candidates`` = 9) when every candidate was accepted; otherwise -1 with
+    probability that grows with the number of rejected candidates and falls with
+    the running acceptance rate; from 0 candidates (plain decoding) the count is
+    re-enabled at 1 with probability ~ the acceptance rate + 0.15."""
 
     def __init__(self, num_output_tokens: int = 10, max_matching_ngram_size: int = 2, min_candidates: int = 0,
-                 max_candidates: int = 16):
+                 max_candidates: int = 9, seed: Optional[int] = None):
+        import random
         self.num_output_tokens = num_output_tokens
         self.max_n = max(1, max_matching_ngram_size)
         self.min_c, self.max_c = min_candidates, max_candidates
         self.table: Dict[Tuple[int, ...], int] = {}
         self.tokens: List[int] = []
+        self.n_drafted = 0
+        self.n_matched = 0
+        self._rng = random.Random(seed)
 
     def init(self, tokens: Sequence[int]):
         self.tokens = list(tokens)
@@ -54,6 +65,8 @@ class PromptLookupCandidates:
                 self.table.setdefault(tuple(self.tokens[i:i + n]), i)
 
     def candidates(self) -> List[int]:
+        if self.num_output_tokens == 0:
+            return []
         L = len(self.tokens)
         for n in range(min(self.max_n, L - 1), 0, -1):
             key = tuple(self.tokens[L - n:])
@@ -62,12 +75,23 @@ class PromptLookupCandidates:
                 return self.tokens[i + n:i + n + self.num_output_tokens]
         return []
 
-    def update(self, n_cand: int, n_accepted: int):
-        # adaptive count (reference: +2 when all accepted, -1 otherwise)
-        if n_cand and n_accepted == n_cand:
-            self.num_output_tokens = min(self.max_c, self.num_output_tokens + 2)
-        elif n_cand:
-            self.num_output_tokens = max(self.min_c + 1, self.num_output_tokens - 1)
+    @property
+    def accept_rate(self) -> float:
+        return self.n_matched / self.n_drafted if self.n_drafted > 0 else 1.0
+
+    def update(self, n_cand: int, n_accepted: int, accept_rate: Optional[float] = None):
+        """one verify step: ``n_cand`` candidates drafted, ``n_accepted`` matched"""
+        self.n_drafted += n_cand
+        self.n_matched += n_accepted
+        rate = self.accept_rate if accept_rate is None else accept_rate
+        if self.num_output_tokens == 0:
+            if self._rng.random() - 0.15 <= rate:
+                self.num_output_tokens = 1
+        elif n_accepted == self.num_output_tokens:
+            self.num_output_tokens = min(self.num_output_tokens + 1, self.max_c)
+        elif n_cand > n_accepted:
+            if self._rng.random() + 0.1 * (n_cand - n_accepted) > rate:
+                self.num_output_tokens = max(self.num_output_tokens - 1, self.min_c)
 
 
 @torch.no_grad()

@@ -133,7 +133,9 @@ _DENSE_GLU = __import__("os").environ.get("ILLM_DENSE_GLU", "1") != "0"
 # dropped the generated-token agreement to 0.016, profiles/spec_glu2_r4.jsonl).
 # MI355X, Llama-3-8B bf16 (profiles/spec_glu16_r4.jsonl, spec_noglu_r4.jsonl):
 # one-token decode 3.790 -> 3.522 ms/token; speculative k = 2 3.444 ms/token
-DENSE_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DENSE_GLU_MAX_M", "16"))
+# the kernel serves at most 16 rows (TORCH_CHECK in dense_glu_hip): larger
+# settings are clamped so bigger batches take the unfused path
+DENSE_GLU_MAX_M = min(int(__import__("os").environ.get("ILLM_DENSE_GLU_MAX_M", "16")), 16)
 
 
 def deinterleave_glu(gu: torch.Tensor, tile: int = 16):

@@ -15,6 +15,7 @@ o 50 vs 62, gate_up 239 vs 318, down 138 vs 184).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import weakref
 
@@ -96,8 +97,61 @@ def prefetch_dense(items, M: int, dtype) -> None:
 # reuse it; numerics identical to the dequantize-per-call path).  Default 0:
 # nothing kept (the low-bit footprint only).
 _DENSE_BUDGET = float(os.environ.get("ILLM_PREFILL_DENSE_GB", "0")) * 2 ** 30
-_dense_cache = {}            # (blob ptr, version, n, k, dtype) -> (weakref to blob, dense weight)
-_dense_bytes = [0]
+_dense_bytes = [0]           # bytes charged to the budget by every resident shadow (incl. training/lora.py's)
+
+
+class ChargedCache(dict):
+    """key -> (weakref to blob, shadow, charged bytes): removing an entry (pop,
+    del, clear, the blob's weakref callback) refunds its bytes to the budget"""
+
+    def pop(self, key, *default):
+        ent = super().pop(key, None)
+        if ent is None:
+            return default[0] if default else None
+        _dense_bytes[0] -= ent[2]
+        return ent
+
+    def __delitem__(self, key):
+        self.pop(key)
+
+    def clear(self):
+        for k in list(self.keys()):
+            self.pop(k)
+
+    def _pop_if(self, key, ref):
+        ent = self.get(key)
+        if ent is not None and ent[0] is ref:      # a newer entry under a reused address stays
+            self.pop(key)
+
+    def put(self, key, blob, w, charged: int):
+        self.pop(key)
+        super().__setitem__(key, (weakref.ref(blob, lambda r, key=key, c=self: c._pop_if(key, r)), w, charged))
+        _dense_bytes[0] += charged
+
+
+_dense_cache = ChargedCache()  # (blob ptr, version, n, k, dtype) -> (weakref to blob, dense weight, bytes)
+
+
+def dense_fits(nbytes: int) -> bool:
+    """another ``nbytes`` of resident shadow stays within the budget"""
+    return _DENSE_BUDGET > 0 and _dense_bytes[0] + nbytes <= _DENSE_BUDGET
+
+
+# a prefill graph being captured records the addresses of the shadows it reads:
+# they are pinned in the graph's own entry (Engine._pf_graphs), so dropping a
+# cache entry (budget change, dense_cache_clear) can never free memory a
+# captured graph still reads
+_capture_pins = None
+
+
+@contextlib.contextmanager
+def pin_dense_shadows():
+    global _capture_pins
+    prev, _capture_pins = _capture_pins, []
+    try:
+        yield _capture_pins
+    finally:
+        _capture_pins = prev
 
 
 def set_dense_budget(gb: float) -> None:
@@ -111,7 +165,6 @@ def set_dense_budget(gb: float) -> None:
 
 def dense_cache_clear() -> None:
     _dense_cache.clear()
-    _dense_bytes[0] = 0
 
 
 def auto_dense_budget(device, cap_gb: float = float("inf")) -> float:
@@ -133,9 +186,7 @@ def auto_dense_budget(device, cap_gb: float = float("inf")) -> float:
 
 
 def _dense_drop(key):
-    ent = _dense_cache.pop(key, None)
-    if ent is not None:
-        _dense_bytes[0] -= ent[1].numel() * ent[1].element_size()
+    _dense_cache.pop(key, None)
 
 
 def _dense_weight(blob, fmt, n, k, dtype):
@@ -147,15 +198,16 @@ def _dense_weight(blob, fmt, n, k, dtype):
         ent = _dense_cache.get(key)
         if ent is not None:
             if ent[0]() is blob:
+                if _capture_pins is not None and torch.cuda.is_current_stream_capturing():
+                    _capture_pins.append(ent[1])
                 return ent[1]
             _dense_drop(key)
         w = torch.ops.ipex_llm_amd.dequantize_device(blob, fmt, n, k, dtype)
         if torch.cuda.is_current_stream_capturing():
             return w                # captured: a transient of the graph's pool, never cached
         nb = w.numel() * w.element_size()
-        if _dense_bytes[0] + nb <= _DENSE_BUDGET:
-            _dense_cache[key] = (weakref.ref(blob, lambda _r, key=key: _dense_drop(key)), w)
-            _dense_bytes[0] += nb
+        if dense_fits(nb):
+            _dense_cache.put(key, blob, w, nb)
         return w
     hit = _ready.pop(_key(blob, n, k, dtype), None) if _ready else None
     if hit is None:

@@ -24,6 +24,11 @@ from typing import Dict, Optional, Tuple
 import torch
 import torch.distributed as dist
 
+# peer (hipIpc) buffers of the custom all-reduce / EP all-to-all are allocated
+# uncached (ops_dist.cpp ipc_alloc): other GPUs write flags and data into them
+# over xGMI.  ILLM_PEER_CACHED=1 restores plain hipMalloc (A/B only).
+PEER_UNCACHED = os.environ.get("ILLM_PEER_CACHED", "0") != "1"
+
 _CUSTOM: Dict[int, "CustomAllReduce"] = {}
 
 
@@ -139,7 +144,7 @@ class CustomAllReduce:
         self.cap = int(max_bytes)
         A = torch.ops.ipex_llm_amd
         with torch.cuda.device(self.device):
-            self._own = A.ipc_alloc(self.SIGNAL + 4 * self.cap)   # signals | data x2 | result x2
+            self._own = A.ipc_alloc(self.SIGNAL + 4 * self.cap, PEER_UNCACHED)   # signals | data x2 | result x2
             handle = A.ipc_handle(self._own)
         handles = [None] * self.world
         dist.all_gather_object(handles, handle.tolist(), group=group)
@@ -205,8 +210,8 @@ def setup_custom_all_reduce(group=None, max_bytes: int = 8 << 20) -> Optional[Cu
     group is intra-node, on GPU and the feature is enabled."""
     if not is_dist() or get_world_size(group) == 1 or not torch.cuda.is_available() or not _custom_enabled():
         return None
-    if dist.get_backend(group) != "nccl":
-        return None
+    if dist.get_backend(group) != "nccl" and os.environ.get("ILLM_AR_P2P") != "force":
+        return None                 # force: also over a gloo group (ranks sharing one GPU: smoke tests)
     key = id(group)
     if key not in _CUSTOM:
         try:

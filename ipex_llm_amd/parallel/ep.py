@@ -38,7 +38,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from .comm import barrier, get_rank, get_world_size
+from .comm import PEER_UNCACHED, barrier, get_rank, get_world_size
 
 
 def expert_range(num_experts: int, rank: int, world: int):
@@ -200,7 +200,7 @@ class EPAllToAll:
         W, cap, H = self.world, self.cap, hidden
         self.nbytes = A.ep_buffer_bytes(W, cap, H)
         with torch.cuda.device(self.device):
-            self._own = A.ipc_alloc(self.nbytes)
+            self._own = A.ipc_alloc(self.nbytes, PEER_UNCACHED)
             handle = A.ipc_handle(self._own)
         handles = [None] * W
         dist.all_gather_object(handles, handle.tolist(), group=group)

@@ -31,7 +31,7 @@ CHUNK = int(os.environ.get("ILLM_CE_CHUNK", "2048"))
 
 class _FusedLinearCE(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, weight, labels, ignore_index: int):
+    def forward(ctx, h, weight, labels, ignore_index: int, denom):
         ops = torch.ops.ipex_llm_amd
         T, H = h.shape
         w = weight if weight.dtype == h.dtype else weight.to(h.dtype)
@@ -45,7 +45,12 @@ class _FusedLinearCE(torch.autograd.Function):
             if grad_h is not None:
                 torch.mm(logits, w, out=grad_h[c0:c1])
             del logits
-        n_valid = (labels != ignore_index).sum().clamp_(min=1).to(torch.float32)
+        if denom is None:
+            n_valid = (labels != ignore_index).sum().clamp_(min=1).to(torch.float32)
+        else:
+            # HF ``num_items_in_batch``: the summed loss over the items of the
+            # whole (gradient-accumulated) batch, not this micro-batch's mean
+            n_valid = torch.as_tensor(denom, device=h.device).to(torch.float32).reshape(())
         ctx.save_for_backward(grad_h, n_valid)
         return loss_rows.sum() / n_valid
 
@@ -55,26 +60,48 @@ class _FusedLinearCE(torch.autograd.Function):
         gh = None
         if grad_h is not None and ctx.needs_input_grad[0]:
             gh = grad_h * (g / n_valid).to(grad_h.dtype)
-        return gh, None, None, None
+        return gh, None, None, None, None
 
 
 def fused_linear_cross_entropy(hidden: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor,
-                               ignore_index: int = -100, shift: bool = True) -> torch.Tensor:
-    """mean CE of ``hidden @ weight^T`` against ``labels`` (HF causal-LM
-    semantics: position t predicts label t + 1 when ``shift``)."""
+                               ignore_index: int = -100, shift: bool = True,
+                               num_items_in_batch=None) -> torch.Tensor:
+    """CE of ``hidden @ weight^T`` against ``labels`` with HF causal-LM
+    semantics: position t predicts label t + 1 when ``shift``; the mean over
+    the valid labels, or -- when ``num_items_in_batch`` is given (the HF
+    Trainer passes it under gradient accumulation) -- the sum divided by it."""
     H = hidden.shape[-1]
     if shift:
         hidden = hidden[..., :-1, :]
         labels = labels[..., 1:]
     h2 = hidden.reshape(-1, H)
     lab = labels.reshape(-1).to(torch.int64)
-    return _FusedLinearCE.apply(h2, weight, lab, ignore_index)
+    return _FusedLinearCE.apply(h2, weight, lab, ignore_index, num_items_in_batch)
+
+
+def plain_ce_head(config) -> bool:
+    """True when the model's HF loss is plain CE over ``lm_head(h)``: heads that
+    soft-cap (Gemma-2 ``final_logit_softcapping``) or scale their logits (Cohere
+    ``logit_scale``, Granite ``logits_scaling``) keep the HF forward, which
+    applies those terms."""
+    if config is None:
+        return True
+    for name in ("final_logit_softcapping", "output_logit_softcapping"):
+        if getattr(config, name, None):
+            return False
+    for name in ("logit_scale", "logits_scaling", "output_multiplier_scale"):
+        v = getattr(config, name, None)
+        if v is not None and float(v) != 1.0:
+            return False
+    return True
 
 
 def fused_ce_supported(model) -> bool:
     from .. import ops
     head = getattr(model, "lm_head", None)
     w = getattr(head, "weight", None)
+    if not plain_ce_head(getattr(model, "config", None)):
+        return False
     return (isinstance(head, torch.nn.Linear) and head.bias is None and w is not None and w.is_cuda
             and not w.requires_grad and w.dtype in (torch.bfloat16, torch.float16)
             and w.is_contiguous() and w.shape[1] % 128 == 0 and w.shape[0] % 128 == 0 and ops.native_gpu(w))
@@ -95,9 +122,10 @@ def patch_fused_ce(model):
             return orig(*args, labels=labels, **kwargs)
         from transformers.modeling_outputs import CausalLMOutputWithPast
         kwargs.pop("logits_to_keep", None)
-        kwargs.pop("num_items_in_batch", None)
+        n_items = kwargs.pop("num_items_in_batch", None)
         out = model.model(*args, **kwargs)
-        loss = fused_linear_cross_entropy(out.last_hidden_state, model.lm_head.weight, labels)
+        loss = fused_linear_cross_entropy(out.last_hidden_state, model.lm_head.weight, labels,
+                                          num_items_in_batch=n_items)
         return CausalLMOutputWithPast(loss=loss, logits=None, past_key_values=out.past_key_values,
                                       hidden_states=out.hidden_states, attentions=out.attentions)
 

@@ -242,7 +242,16 @@ class _LoraLowBitFn(torch.autograd.Function):
 _KCAT = os.environ.get("ILLM_LORA_KCAT", "auto")
 _KCAT_PAD = int(os.environ.get("ILLM_LORA_KCAT_PAD", "64"))
 _KCAT_ROWS = os.environ.get("ILLM_LORA_KCAT_ROWS", "1") == "1"   # the down projection's grad_x form
-_aug_cache = {}                 # (blob ptr, version, R, off, dtype) -> (weakref to blob, [N, K + R] shadow)
+from ..ops.gemm import ChargedCache as _ChargedCache  # noqa: E402
+
+# (blob ptr, version, R, off, dtype) -> (weakref to blob, [N, K + R] shadow, bytes): charged to the
+# same resident-shadow budget as ops/gemm.py's prefill shadows (ILLM_TRAIN_DENSE_GB / ILLM_PREFILL_DENSE_GB)
+_aug_cache = _ChargedCache()
+
+
+def _aug_fits(key, nbytes: int) -> bool:
+    from ..ops.gemm import dense_fits
+    return key in _aug_cache or dense_fits(nbytes)
 
 
 def _kcat_ok(bases, x2, As) -> bool:
@@ -255,7 +264,17 @@ def _kcat_ok(bases, x2, As) -> bool:
     K, R = x2.shape[1], sum(A.shape[0] for A in As)
     if (K + R) % 8 or any(b.in_features != K for b in bases):
         return False
-    return _KCAT == "1" or min(b.out_features for b in bases) >= 2 * K
+    if not (_KCAT == "1" or min(b.out_features for b in bases) >= 2 * K):
+        return False
+    # every augmented shadow is resident or still fits the budget (else the rank-update path)
+    need, off = 0, 0
+    for b, A in zip(bases, As):
+        key = (b.weight.data_ptr(), b.weight._version, R, off, x2.dtype)
+        if key not in _aug_cache:
+            need += b.out_features * (K + R) * x2.element_size()
+        off += A.shape[0]
+    from ..ops.gemm import dense_fits
+    return need == 0 or dense_fits(need)
 
 
 def _aug_weight(base, R: int, off: int, dtype, B=None):
@@ -269,8 +288,8 @@ def _aug_weight(base, R: int, off: int, dtype, B=None):
         N, K = base.out_features, base.in_features
         w = torch.zeros(N, K + R, dtype=dtype, device=blob.device)
         w[:, :K].copy_(torch.ops.ipex_llm_amd.dequantize_device(blob, base.fmt, N, K, dtype))
-        ent = (weakref.ref(blob, lambda _r, key=key: _aug_cache.pop(key, None)), w)
-        _aug_cache[key] = ent
+        _aug_cache.put(key, blob, w, w.numel() * w.element_size())
+        ent = _aug_cache[key]
     w = ent[1]
     if B is not None:
         K = base.in_features
@@ -287,7 +306,17 @@ def _kcat_rows_ok(base, g2, A) -> bool:
         return False
     if g2.dtype not in (torch.bfloat16, torch.float16) or g2.shape[0] <= ops.GEMV_MAX_M or A.dtype != g2.dtype:
         return False
-    return _KCAT == "1" or base.in_features >= 2 * base.out_features
+    if not (_KCAT == "1" or base.in_features >= 2 * base.out_features):
+        return False
+    N, K = base.out_features, base.in_features
+    Rp = -(-(N + A.shape[0]) // _KCAT_PAD) * _KCAT_PAD - N        # as in _LoraLowBitFn.backward
+    key = ("rows", base.weight.data_ptr(), base.weight._version, Rp, g2.dtype)
+    # the W rows are shared with the prefill / forward shadow (below): only the
+    # adapter rows are new when that shadow is already resident
+    from ..ops.gemm import _dense_cache
+    dkey = (base.weight.data_ptr(), base.weight._version, N, K, g2.dtype)
+    need = (N + Rp) * K * g2.element_size() - (_dense_cache[dkey][2] if dkey in _dense_cache else 0)
+    return _aug_fits(key, need)
 
 
 def _aug_rows_weight(base, Rp: int, dtype, A=None):
@@ -297,11 +326,17 @@ def _aug_rows_weight(base, Rp: int, dtype, A=None):
     key = ("rows", blob.data_ptr(), blob._version, Rp, dtype)
     ent = _aug_cache.get(key)
     if ent is None or ent[0]() is not blob:
+        from ..ops.gemm import _dense_cache
         N, K = base.out_features, base.in_features
         w = torch.zeros(N + Rp, K, dtype=dtype, device=blob.device)
         w[:N].copy_(torch.ops.ipex_llm_amd.dequantize_device(blob, base.fmt, N, K, dtype))
-        ent = (weakref.ref(blob, lambda _r, key=key: _aug_cache.pop(key, None)), w)
-        _aug_cache[key] = ent
+        # one copy of W: the forward's shadow (lowbit_matmul -> _dense_weight) becomes a
+        # view of these rows; its bytes move into this entry
+        dkey = (blob.data_ptr(), blob._version, N, K, dtype)
+        _dense_cache.pop(dkey)
+        _aug_cache.put(key, blob, w, w.numel() * w.element_size())
+        _dense_cache.put(dkey, blob, w[:N], 0)
+        ent = _aug_cache[key]
     w = ent[1]
     if A is not None:
         N = base.out_features
@@ -703,11 +738,23 @@ def get_peft_model(model: nn.Module, config: LoraConfig, adapter_name: str = "de
     return PeftModel(model, config)
 
 
+def _cross_attention(name: str, mod: nn.Module) -> bool:
+    """cross-attention blocks (mllama cross-attention layers, Whisper / T5
+    encoder_attn / EncDecAttention): their k / v project another input than q"""
+    leaf = name.rsplit(".", 1)[-1].lower()
+    if getattr(mod, "is_cross_attention", False) or "cross" in leaf or "encoder_attn" in leaf \
+            or "encdec" in leaf:
+        return True
+    return "crossattention" in type(mod).__name__.lower()
+
+
 def link_lora_groups(model: nn.Module) -> int:
     """link sibling LoraLinear modules that read the same input (a parent's
     q/k/v, gate/up) for the grouped forward; returns the number of groups"""
     n = 0
-    for mod in model.modules():
+    for mname, mod in model.named_modules():
+        if _cross_attention(mname, mod):
+            continue                  # k / v read the encoder states, not q's input
         for names in _GROUPS:
             mods = [getattr(mod, c, None) for c in names]
             if all(isinstance(m, LoraLinear) for m in mods) and \

@@ -37,6 +37,30 @@ def test_candidate_table():
     assert g.candidates() == []
 
 
+def test_candidate_count_policy_matches_reference():
+    """reference update_candidate_strategy (lookup.py:253-270): +1 capped at 9
+    on full acceptance, never below 0, re-enabled from 0 by the acceptance rate"""
+    from ipex_llm_amd.generation.lookup import PromptLookupCandidates
+    g = PromptLookupCandidates(num_output_tokens=8, seed=0)
+    g.update(8, 8)
+    assert g.num_output_tokens == 9
+    g.update(9, 9)
+    assert g.num_output_tokens == 9                  # max_candidates
+    assert g.accept_rate == 1.0
+    # many rejections with a low acceptance rate walk it down to 0 (min_candidates)
+    for _ in range(40):
+        g.update(g.num_output_tokens, 0)
+    assert g.num_output_tokens == 0 and g.candidates() == []
+    assert 0.0 < g.accept_rate < 0.5
+    # at 0 drafts the re-enable probability is accept_rate + 0.15
+    hits = 0
+    for i in range(400):
+        h = PromptLookupCandidates(num_output_tokens=0, seed=i)
+        h.update(0, 0, accept_rate=0.35)
+        hits += h.num_output_tokens == 1
+    assert 0.35 < hits / 400 < 0.65
+
+
 def test_self_speculative_matches_target_greedy(tmp_path):
     from ipex_llm_amd.transformers import AutoModelForCausalLM
     p = _tiny(tmp_path)

@@ -104,3 +104,50 @@ def test_llama_api_hf_fallback(tmp_path, native):
     # prefix reuse through the HF cache (crop) gives the same continuation
     again = llm.generate(toks, max_new_tokens=6, temperature=0, repetition_penalty=1.0)
     assert again == got
+
+
+def test_langchain_native_llm_and_embeddings(llama_dir):
+    """reference langchain/llms/bigdlllm.py + embeddings/bigdlllm.py over the
+    native Llama: _call streams the completion chunks and concatenates them
+    (== the client's own completion), get_num_tokens tokenizes with the client,
+    the family classes pick their ggml class, embeddings are client.embed"""
+    from ipex_llm_amd.langchain import BigdlNativeLLM, LlamaEmbeddings, LlamaLLM, BigdlNativeEmbeddings
+    llm = LlamaLLM(llama_dir, n_ctx=128, low_bit="sym_int8", seed=0, temperature=0.0, max_tokens=6,
+                   repeat_penalty=1.0)
+    assert type(llm.client).__name__ == "Llama" and llm._llm_type == "BigDL"
+    text = llm.invoke("w5 w6 w7")
+    ref = llm.client(prompt="w5 w6 w7", max_tokens=6, temperature=0.0, repeat_penalty=1.0, top_k=40,
+                     top_p=0.95)["choices"][0]["text"]
+    assert text == ref and len(text) > 0
+    chunks = list(llm.stream("w5 w6 w7"))
+    assert "".join(c["choices"][0]["text"] for c in chunks) == ref
+    assert llm.get_num_tokens("w5 w6 w7") == len(llm.client.tokenize(b"w5 w6 w7"))
+    with pytest.raises(ValueError):
+        BigdlNativeLLM(llama_dir, model_family="nosuch")
+    llm.stop = ["w9"]
+    with pytest.raises(ValueError):
+        llm._get_parameters(["x"])
+    emb = LlamaEmbeddings(llama_dir, low_bit="sym_int8", n_ctx=128)
+    q = emb.embed_query("w5 w6")
+    assert q == llm.client.embed("w5 w6") and len(q) == 128
+    assert emb.embed_documents(["w5 w6", "w7"])[0] == q
+    assert BigdlNativeEmbeddings(client=emb.client).embed_query("w5 w6") == q
+
+
+def test_langchain_vllm_wrapper_batches_on_engine(llama_dir):
+    """reference langchain/vllm/vllm.py VLLM: prompts through the continuous-
+    batching engine, greedy == the engine's own generate"""
+    from transformers import AutoTokenizer
+    from ipex_llm_amd.langchain import VLLM
+    from ipex_llm_amd.serving.engine import LLMEngine, SamplingParams
+    from ipex_llm_amd.transformers import AutoModelForCausalLM
+    from ipex_llm_amd.transformers.hf_native import get_native
+    hf = AutoModelForCausalLM.from_pretrained(llama_dir, load_in_low_bit="sym_int8", torch_dtype=torch.float32)
+    tok = AutoTokenizer.from_pretrained(llama_dir)
+    eng = LLMEngine(get_native(hf)[0], max_batch=4)
+    llm = VLLM(client=eng, tokenizer=tok, temperature=0.0, max_new_tokens=5, ignore_eos=True)
+    outs = llm.generate_texts(["w5 w6 w7", "w9 w10"])
+    ids = [tok.encode("w5 w6 w7"), tok.encode("w9 w10")]
+    ref = eng.generate(ids, SamplingParams(max_new_tokens=5))
+    assert outs == [tok.decode(r, skip_special_tokens=True) for r in ref]
+    assert llm.invoke("w5 w6 w7") == outs[0]

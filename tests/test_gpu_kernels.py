@@ -718,3 +718,26 @@ def test_dense_glu_matches_unfused(cuda, M, act, dt):
     gf, uf = deinterleave_glu(x.float() @ w.float().t())
     ref = (F.silu(gf) if act == 0 else F.gelu(gf, approximate="tanh")) * uf
     assert ((got.float() - ref).norm() / ref.norm()).item() < 2e-2
+
+
+@pytest.mark.parametrize("env", [{"ILLM_ATTN_V3_NW": "2"}, {"ILLM_ATTN_V3_NW": "8"},
+                                 {"ILLM_ATTN_V3_NW": "4", "ILLM_ATTN_V3_FUSE": "1"},
+                                 {"ILLM_ATTN_V3_FUSE": "0"}, {"ILLM_ATTN_V3": "0"}])
+def test_attn_decode_v3_variants_subprocess(cuda, env):
+    """v3 decode attention (attn_dec_v3.cuh) at forced split widths (2 / 4 / 8
+    waves of 32 keys), with the in-kernel last-arriver merge, and v2
+    (ILLM_ATTN_V3=0): the fp32-reference attention checks, the fused-RoPE
+    checks (cache contents, accumulator re-zeroed) and the repeated uneven-length
+    launches (counters back to zero) in a child process per setting (the
+    settings are read once per process)"""
+    import os
+    import subprocess
+    import sys
+    if os.environ.get("ILLM_V3_CHILD") == "1":
+        pytest.skip("already the child process")
+    e = dict(os.environ, ILLM_V3_CHILD="1", **env)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", __file__, "-k",
+                        "(test_attn_decode or attn_decode_rope_matches or fused_combine_repeated or rope_in_mha "
+                        "or gemv_rope_epilogue) and not subprocess"],
+                       env=e, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

@@ -60,6 +60,41 @@ def test_fused_linear_ce_matches_hf_loss(cuda):
     assert _rel(h.grad, hr.grad) < 2e-2
 
 
+def test_fused_ce_patch_honours_num_items_in_batch(cuda):
+    """the patched HF forward divides the summed loss by ``num_items_in_batch``
+    like the HF loss does (the Trainer passes it under gradient accumulation
+    and then does NOT divide by the accumulation steps): two micro-batches with
+    the whole batch's item count == one unfused loss over both, gradients too"""
+    from transformers import LlamaConfig, LlamaForCausalLM
+    from ipex_llm_amd.training.fused_ce import patch_fused_ce
+    torch.manual_seed(4)
+    cfg = LlamaConfig(vocab_size=1024, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                      num_attention_heads=4, num_key_value_heads=2)
+    ref = LlamaForCausalLM(cfg).to(cuda, torch.bfloat16)
+    fused = LlamaForCausalLM(cfg).to(cuda, torch.bfloat16)
+    fused.load_state_dict(ref.state_dict())
+    for m in (ref, fused):
+        m.lm_head.weight.requires_grad_(False)
+        m.train()
+    patch_fused_ce(fused)
+    ids = torch.randint(0, 1024, (4, 64), device=cuda)
+    lab = ids.clone()
+    lab[0, :20] = -100
+    n_items = int((lab[:, 1:] != -100).sum())
+    for m in (ref, fused):
+        for mb in (slice(0, 2), slice(2, 4)):
+            out = m(input_ids=ids[mb], labels=lab[mb], num_items_in_batch=torch.tensor(n_items, device=cuda))
+            out.loss.backward()
+    assert fused.forward.__name__ == "forward" and getattr(fused, "_illm_fused_ce", False)
+    gr = ref.model.layers[0].mlp.down_proj.weight.grad
+    gf = fused.model.layers[0].mlp.down_proj.weight.grad
+    assert _rel(gf, gr) < 3e-2
+    with torch.no_grad():
+        lr = ref(input_ids=ids, labels=lab).loss
+    lf = fused(input_ids=ids, labels=lab, num_items_in_batch=n_items).loss
+    assert abs(lf.item() - lr.item()) < 2e-2 * max(1.0, lr.item())
+
+
 def _ref_attn(q, k, v, scale, causal):
     G = q.shape[1] // k.shape[1]
     kk = k.float().repeat_interleave(G, 1)

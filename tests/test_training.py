@@ -365,3 +365,38 @@ def test_grouped_lora_siblings_match_per_module(monkeypatch):
     assert rel(gx1, gx0) < 2e-2
     for k in g0:
         assert rel(g1[k], g0[k]) < 2e-2, k
+
+
+def test_fused_ce_refuses_softcap_and_scaled_heads():
+    """heads whose HF loss soft-caps or scales the logits keep the HF forward
+    (the fused lm_head + CE applies neither)"""
+    from types import SimpleNamespace
+    from ipex_llm_amd.training.fused_ce import plain_ce_head
+    assert plain_ce_head(None)
+    assert plain_ce_head(SimpleNamespace(final_logit_softcapping=None, logit_scale=None))
+    assert not plain_ce_head(SimpleNamespace(final_logit_softcapping=30.0))
+    assert not plain_ce_head(SimpleNamespace(logit_scale=0.0625))
+    assert not plain_ce_head(SimpleNamespace(logits_scaling=8.0))
+    assert plain_ce_head(SimpleNamespace(logits_scaling=1.0))
+
+
+def test_link_lora_groups_skips_cross_attention():
+    """q / k / v of a cross-attention block read different inputs: never grouped"""
+    import torch.nn as nn
+    from ipex_llm_amd.training.lora import LoraConfig, get_peft_model, link_lora_groups
+
+    class Attn(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.q_proj, self.k_proj, self.v_proj = nn.Linear(64, 64), nn.Linear(64, 64), nn.Linear(64, 64)
+
+    class Layer(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.self_attn, self.encoder_attn = Attn(), Attn()
+
+    m = nn.Sequential(Layer())
+    peft = get_peft_model(m, LoraConfig(r=4, target_modules=["q_proj", "k_proj", "v_proj"]))
+    assert link_lora_groups(peft) == 1
+    assert "_lora_group" in m[0].self_attn.q_proj.__dict__
+    assert "_lora_group" not in m[0].encoder_attn.q_proj.__dict__
