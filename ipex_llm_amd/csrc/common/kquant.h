@@ -15,7 +15,7 @@
 #pragma once
 #include <stdint.h>
 
-#include "iquant.h"        // IQ lattice formats (15..17) share the super-block plumbing
+#include "iquant.h"        // IQ lattice formats (15..18) share the super-block plumbing
 #include "quant_block.h"   // ILLM_HD (host / host+device inline)
 
 namespace illm {
@@ -24,7 +24,7 @@ enum KqFmt : int { FMT_Q4K = 11, FMT_Q5K = 12, FMT_Q6K = 13, FMT_Q2K = 14 };
 constexpr int QK_K = 256;
 
 // super-block formats: the k-quants and the IQ lattice formats (iquant.h)
-constexpr bool is_kq(int f) { return f >= FMT_Q4K && f <= FMT_IQ1S; }
+constexpr bool is_kq(int f) { return f >= FMT_Q4K && f <= FMT_IQ1M; }
 constexpr int kq_block_bytes(int f) {
   return f == FMT_Q4K ? 144 : f == FMT_Q5K ? 176 : f == FMT_Q6K ? 210 : f == FMT_Q2K ? 84 : iq_block_bytes(f);
 }

@@ -1,4 +1,4 @@
-// Host quantizers of the IQ lattice formats (iq2_xxs / iq2_xs / iq1_s,
+// Host quantizers of the IQ lattice formats (iq2_xxs / iq2_xs / iq1_s / iq1_m,
 // common/iquant.h): the gguf_iq2_xxs / gguf_iq2_xs / gguf_iq1_s qtypes the
 // reference produces through ggml_quantize_tensor_with_weights with an
 // importance matrix (SRC/transformers/low_bit_linear.py:153-190,
@@ -274,6 +274,74 @@ void quant_iq1s(const float* x, const float* im, uint8_t* out) {
   }
 }
 
+// IQ1_M chunk: the better of the two shift signs (returns the entry, *neg = sign)
+inline int iq1m_chunk(const Neighbors& nb, const float* x, const float* w, float s, int* neg, float* err) {
+  float e0, e1;
+  const int a = iq1_chunk(nb, x, w, s, illm::IQ1M_DELTA, &e0);
+  const int b = iq1_chunk(nb, x, w, s, -illm::IQ1M_DELTA, &e1);
+  *neg = e1 < e0;
+  *err = e1 < e0 ? e1 : e0;
+  return e1 < e0 ? b : a;
+}
+
+// iq1_m: a 3-bit scale per 16 weights and a shift sign per 8 (finer than
+// iq1_s's per-32 scale and shift, 1.75 instead of 1.5625 bpw): per 16-weight
+// sub-block the scale is searched over the same multipliers as iq1_s, every
+// chunk taking its best (entry, shift sign); then d = max scale / 15 is
+// rounded to f16 and the entries re-chosen for the 3-bit quantized scales
+void quant_iq1m(const float* x, const float* im, uint8_t* out) {
+  const Neighbors& nb = neighbors(illm::FMT_IQ1S);
+  float w[256];
+  weights_of(x, im, w);
+  float sc[16];
+  float smax = 0.f;
+  for (int g = 0; g < 16; g++) {
+    const float* xg = x + 16 * g;
+    float amax = 0.f;
+    for (int i = 0; i < 16; i++) amax = std::max(amax, fabsf(xg[i]));
+    float bs = amax, be = 3.4e38f;
+    if (amax > 0.f) {
+      for (float f : SCALE_F) {
+        const float sv = amax / 1.125f * f;
+        float tot = 0.f;
+        for (int c = 0; c < 2; c++) {
+          float er;
+          int ng;
+          iq1m_chunk(nb, xg + 8 * c, w + 16 * g + 8 * c, sv, &ng, &er);
+          tot += er;
+        }
+        if (tot < be) { be = tot; bs = sv; }
+      }
+    }
+    sc[g] = amax > 0.f ? bs : 0.f;
+    smax = std::max(smax, sc[g]);
+  }
+  const float d = smax / 15.f;
+  const uint16_t dh = illm::hd_f32_to_f16(d);
+  const float dq = illm::hd_f16_to_f32(dh);
+  memset(out, 0, illm::iq_block_bytes(illm::FMT_IQ1M));
+  uint16_t sw[4] = {0, 0, 0, 0};
+  for (int g = 0; g < 16; g++) {
+    const int l = dq > 0.f ? (int)lrintf((sc[g] / dq - 1.f) * 0.5f) : 0;
+    const int ls = std::min(7, std::max(0, l));
+    const float sv = dq * (float)(2 * ls + 1);
+    const int ib = g >> 1, hf = g & 1;
+    sw[ib >> 1] |= (uint16_t)(ls << (6 * (ib & 1) + 3 * hf));
+    for (int c2 = 0; c2 < 2; c2++) {
+      const int c = 2 * g + c2;
+      float er;
+      int ng = 0;
+      const int e = sv > 0.f ? iq1m_chunk(nb, x + 8 * c, w + 8 * c, sv, &ng, &er) : 0;
+      out[c] = (uint8_t)(e & 0xff);
+      out[32 + (c >> 1)] |= (uint8_t)((((e >> 8) & 7) | (ng << 3)) << (4 * (c & 1)));
+    }
+  }
+  for (int i = 0; i < 4; i++) {
+    sw[i] |= (uint16_t)(((dh >> (4 * i)) & 15) << 12);
+    memcpy(out + 48 + 2 * i, &sw[i], 2);
+  }
+}
+
 }  // namespace
 
 namespace illm {
@@ -281,11 +349,12 @@ namespace illm {
 // one 256-weight super-block of an IQ format (imatrix slice or null)
 void iq_quantize_block(int fmt, const float* x, const float* im, uint8_t* out) {
   if (fmt == FMT_IQ1S) quant_iq1s(x, im, out);
+  else if (fmt == FMT_IQ1M) quant_iq1m(x, im, out);
   else quant_iq2(fmt, x, im, out);
 }
 
 void iq_dequant_block(int fmt, const uint8_t* b, float* y) {
-  const uint64_t* grid = fmt == FMT_IQ2XXS ? G2XXS : (fmt == FMT_IQ2XS ? G2XS : G1S);
+  const uint64_t* grid = fmt == FMT_IQ2XXS ? G2XXS : (fmt == FMT_IQ2XS ? G2XS : G1S);   // iq1_s / iq1_m: G1S
   for (int c = 0; c < 32; c++) iq_dec8(fmt, b, c, grid, y + 8 * c);
 }
 

@@ -1,5 +1,5 @@
 // k-quant (q4_K / q5_K / q6_K / q2_K, GGUF super-block layouts, common/kquant.h)
-// and IQ lattice (iq2_xxs / iq2_xs / iq1_s, common/iquant.h; codebooks in
+// and IQ lattice (iq2_xxs / iq2_xs / iq1_s / iq1_m, common/iquant.h; codebooks in
 // constant memory) decoders on gfx950: dequantize to bf16/f16 (prefill GEMM input, QLoRA
 // backward) and the decode GEMV (M <= 8) straight from the GGUF blocks.
 //
@@ -38,7 +38,7 @@ __device__ __forceinline__ void kq_dec4(const uint8_t* b, int e0, float* w) {
   if constexpr (is_iq(FMT)) {
     // IQ: decode the lane's 8-weight chunk, keep its half
     float w8[8];
-    const uint64_t* grid = FMT == FMT_IQ2XXS ? d_iq2xxs_grid : (FMT == FMT_IQ2XS ? d_iq2xs_grid : d_iq1s_grid);
+    const uint64_t* grid = FMT == FMT_IQ2XXS ? d_iq2xxs_grid : (FMT == FMT_IQ2XS ? d_iq2xs_grid : d_iq1s_grid);  // iq1_m: iq1_s grid
     iq_dec8(FMT, b, e0 >> 3, grid, w8);
     const int o = e0 & 4;
 #pragma unroll
@@ -146,6 +146,7 @@ void launch_kq_dequant(int fmt, bool bf16, const uint8_t* w, int64_t n, int64_t 
     case FMT_IQ2XXS: dq_fmt<FMT_IQ2XXS>(bf16, w, n, k, out, st); break;
     case FMT_IQ2XS: dq_fmt<FMT_IQ2XS>(bf16, w, n, k, out, st); break;
     case FMT_IQ1S: dq_fmt<FMT_IQ1S>(bf16, w, n, k, out, st); break;
+    case FMT_IQ1M: dq_fmt<FMT_IQ1M>(bf16, w, n, k, out, st); break;
     default: dq_fmt<FMT_Q2K>(bf16, w, n, k, out, st); break;
   }
 }
@@ -172,6 +173,7 @@ void launch_kq_gemv(int fmt, bool bf16, const uint16_t* x, int M, int64_t K, con
     case FMT_IQ2XXS: gv_fmt<FMT_IQ2XXS>(bf16, x, M, K, w, N, out, st); break;
     case FMT_IQ2XS: gv_fmt<FMT_IQ2XS>(bf16, x, M, K, w, N, out, st); break;
     case FMT_IQ1S: gv_fmt<FMT_IQ1S>(bf16, x, M, K, w, N, out, st); break;
+    case FMT_IQ1M: gv_fmt<FMT_IQ1M>(bf16, x, M, K, w, N, out, st); break;
     default: gv_fmt<FMT_Q2K>(bf16, x, M, K, w, N, out, st); break;
   }
 }

@@ -73,9 +73,9 @@ FMT_SYM_INT4, FMT_ASYM_INT4, FMT_NF4, FMT_FP4, FMT_SYM_INT8, FMT_FP8E4, FMT_FP8E
 FMT_Q4K, FMT_Q5K, FMT_Q6K, FMT_Q2K = 11, 12, 13, 14
 # IQ lattice super-blocks (csrc/common/iquant.h): ggml's layouts and bits
 # per weight, our own codebooks
-FMT_IQ2XXS, FMT_IQ2XS, FMT_IQ1S = 15, 16, 17
+FMT_IQ2XXS, FMT_IQ2XS, FMT_IQ1S, FMT_IQ1M = 15, 16, 17, 18
 KQ_BLOCK_BYTES = {FMT_Q4K: 144, FMT_Q5K: 176, FMT_Q6K: 210, FMT_Q2K: 84,
-                  FMT_IQ2XXS: 66, FMT_IQ2XS: 74, FMT_IQ1S: 50}
+                  FMT_IQ2XXS: 66, FMT_IQ2XS: 74, FMT_IQ1S: 50, FMT_IQ1M: 56}
 
 NF4_TABLE = [
     -1.0, -0.6961928009986877, -0.5250730514526367, -0.39491748809814453,
@@ -133,16 +133,15 @@ _FORMATS: Dict[int, QFormat] = {
     IQ2_XXS: QFormat("gguf_iq2_xxs", IQ2_XXS, FMT_IQ2XXS, 2, 256, k_align=256, kquant=True),
     IQ2_XS: QFormat("gguf_iq2_xs", IQ2_XS, FMT_IQ2XS, 2, 256, k_align=256, kquant=True),
     IQ1_S: QFormat("gguf_iq1_s", IQ1_S, FMT_IQ1S, 1, 256, k_align=256, kquant=True),
+    IQ1_M: QFormat("gguf_iq1_m", IQ1_M, FMT_IQ1M, 1, 256, k_align=256, kquant=True),
 }
 # qtypes stored in a format of equal or higher precision.  gguf_iq2_xxs /
-# gguf_iq2_xs / gguf_iq1_s are native IQ lattice formats with ggml's block
-# layouts and bits per weight (2.0625 / 2.3125 / 1.5625) but OUR codebooks
-# (ggml's grid tables are not in the reference repository; csrc/common/
-# iquant.h): IQ-coded GGUF tensors are therefore not loadable.  gguf_iq1_m
-# (1.75 bpw) quantizes into q2_k (2.625 bpw).
+# gguf_iq2_xs / gguf_iq1_s / gguf_iq1_m are native IQ lattice formats with
+# ggml's block layouts and bits per weight (2.0625 / 2.3125 / 1.5625 / 1.75) but
+# OUR codebooks (ggml's grid tables are not in the reference repository;
+# csrc/common/iquant.h): IQ-coded GGUF tensors are therefore not loadable.
 _ALIAS = {
     FP6_K: FP6,
-    IQ1_M: Q2_K,
     SYM_INT4_RTN: SYM_INT4, ASYM_INT4_RTN: ASYM_INT4, SYM_INT8_RTN: SYM_INT8,
     # gguf mixed policies resolve per module (mixed_kquant_qtype); q4_k otherwise
     GGUF_Q4K_S: Q4_K, GGUF_Q4K_M: Q4_K,
@@ -150,7 +149,7 @@ _ALIAS = {
 # in_features % 256 != 0: the reference's fallback formats
 # (SRC/transformers/utils.py:380-401, check_hidden_size)
 KQ_FALLBACK = {Q4_K: ASYM_INT4, Q5_K: ASYM_INT5, Q6_K: SYM_INT8, Q2_K: ASYM_INT4,
-               IQ2_XXS: ASYM_INT4, IQ2_XS: ASYM_INT4, IQ1_S: ASYM_INT4}
+               IQ2_XXS: ASYM_INT4, IQ2_XS: ASYM_INT4, IQ1_S: ASYM_INT4, IQ1_M: ASYM_INT4}
 
 
 def is_kquant(qtype) -> bool:

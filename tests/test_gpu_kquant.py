@@ -12,7 +12,8 @@ pytestmark = pytest.mark.gpu
 
 FMTS = {"q4_k": Q.FMT_Q4K, "q5_k": Q.FMT_Q5K, "q6_k": Q.FMT_Q6K, "q2_k": Q.FMT_Q2K,
         # IQ lattice formats (csrc/common/iquant.h, codebooks in constant memory)
-        "gguf_iq2_xxs": Q.FMT_IQ2XXS, "gguf_iq2_xs": Q.FMT_IQ2XS, "gguf_iq1_s": Q.FMT_IQ1S}
+        "gguf_iq2_xxs": Q.FMT_IQ2XXS, "gguf_iq2_xs": Q.FMT_IQ2XS, "gguf_iq1_s": Q.FMT_IQ1S,
+        "gguf_iq1_m": Q.FMT_IQ1M}
 
 
 @pytest.mark.parametrize("name", list(FMTS))

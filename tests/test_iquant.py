@@ -1,4 +1,4 @@
-"""IQ lattice formats (gguf_iq2_xxs / gguf_iq2_xs / gguf_iq1_s): ggml's block
+"""IQ lattice formats (gguf_iq2_xxs / gguf_iq2_xs / gguf_iq1_s / gguf_iq1_m): ggml's block
 layouts and bits per weight (csrc/common/iquant.h), our own codebooks
 (tools/gen_iq_grids.py) and imatrix-weighted quantizers
 (csrc/cpu/iquant.cpp).  Reference: SRC/ggml/quantize.py:43-47 (qtype ids),
@@ -7,7 +7,7 @@ with ggml's grids is unpinned: the grid tables are not in the reference."""
 import pytest
 import torch
 
-IQ = {"gguf_iq2_xxs": 2.0625, "gguf_iq2_xs": 2.3125, "gguf_iq1_s": 1.5625}
+IQ = {"gguf_iq2_xxs": 2.0625, "gguf_iq2_xs": 2.3125, "gguf_iq1_s": 1.5625, "gguf_iq1_m": 1.75}
 
 
 def _rel(a, b):
@@ -28,7 +28,7 @@ def test_bits_per_weight_and_round_trip(qtype, bpw):
     wd = ops.kq_dequantize(blob, f.fmt, n, k)
     err = _rel(wd, w)
     # Gaussian weights at ~2 / ~1.5 bits: the lattice error budget
-    assert err < (0.62 if qtype == "gguf_iq1_s" else 0.42), err
+    assert err < (0.62 if qtype.startswith("gguf_iq1") else 0.42), err
     # the integer-constrained reconstruction beats a crude 1-level sign code
     sign_code = w.sign() * w.abs().mean()
     assert err < _rel(sign_code, w)
@@ -73,3 +73,29 @@ def test_cpu_linear_and_model(qtype):
     with torch.no_grad():
         out = m(torch.randint(0, 128, (1, 5))).logits
     assert torch.isfinite(out).all()
+
+
+def test_iq1_m_finer_scales_beat_iq1_s():
+    """iq1_m (3-bit scale per 16 weights, shift sign per 8; ggml's 56-byte block,
+    d in the scale words' top nibbles) reconstructs better than iq1_s at 1.75
+    vs 1.5625 bpw; the super-block scale round-trips through the nibbles"""
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.quantize import get_format
+    torch.manual_seed(3)
+    w = torch.randn(32, 1024) * 0.02
+    errs = {}
+    for q in ("gguf_iq1_s", "gguf_iq1_m"):
+        f = get_format(q).fmt
+        errs[q] = _rel(ops.kq_dequantize(ops.kq_quantize(w, f), f, 32, 1024), w)
+    assert errs["gguf_iq1_m"] < errs["gguf_iq1_s"], errs
+    f = get_format("gguf_iq1_m").fmt
+    blob = ops.kq_quantize(w[:1, :256], f).view(torch.uint8)
+    assert blob.numel() == 56
+    sc = blob[48:56].to(torch.int32)
+    words = sc[0::2] | (sc[1::2] << 8)
+    d16 = int(((words[0] >> 12) | ((words[1] >> 8) & 0xF0) | ((words[2] >> 4) & 0xF00) | (words[3] & 0xF000)))
+    d = torch.tensor([d16], dtype=torch.int16).view(torch.float16).float().item()
+    assert 0 < d < 1
+    # every weight is d * odd * (ternary +- 1/8): the block max is within the scale range
+    wd = ops.kq_dequantize(blob, f, 1, 256)
+    assert wd.abs().max().item() <= d * 15 * 1.125 + 1e-6

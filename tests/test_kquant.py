@@ -109,18 +109,16 @@ def test_hidden_not_multiple_of_256_falls_back():
 
 
 def test_iq_qtypes_use_native_2bit_super_blocks():
-    """gguf_iq2_xxs / iq2_xs / iq1_s are native IQ lattice super-blocks
-    (csrc/common/iquant.h); gguf_iq1_m maps to the q2_k container -- never a
-    4-bit stand-in"""
+    """gguf_iq2_xxs / iq2_xs / iq1_s / iq1_m are native IQ lattice
+    super-blocks (csrc/common/iquant.h) -- never a 4-bit stand-in"""
     import torch
     from transformers import LlamaConfig, LlamaForCausalLM
     from ipex_llm_amd.quantize import qtypes as Q
     from ipex_llm_amd.transformers.convert import ggml_convert_low_bit
-    for name in ("gguf_iq2_xxs", "gguf_iq2_xs", "gguf_iq1_s"):
+    for name in ("gguf_iq2_xxs", "gguf_iq2_xs", "gguf_iq1_s", "gguf_iq1_m"):
         f = Q.get_format(name)
         assert f.name == name and f.bits <= 2 and f.kquant
-    f = Q.get_format("gguf_iq1_m")
-    assert f.name == "q2_k" and f.bits == 2 and f.kquant
+    assert Q.get_format("gguf_iq1_m").bits_per_weight == 1.75
     cfg = LlamaConfig(vocab_size=64, hidden_size=256, intermediate_size=512, num_hidden_layers=1, num_attention_heads=4)
     torch.manual_seed(0)
     m = LlamaForCausalLM(cfg).eval()
