@@ -23,6 +23,9 @@ int64_t illm_kq_total_bytes(int fmt, int64_t n, int64_t k);
 void illm_kq_quantize(int fmt, const float* src, int64_t n, int64_t k, const float* imatrix, uint8_t* dst);
 void illm_kq_dequantize(int fmt, const uint8_t* src, int64_t n, int64_t k, float* dst);
 void illm_kq_gemm(int fmt, const float* x, int64_t m, const uint8_t* w, int64_t n, int64_t k, float* y);
+// gemm_kq.cpp: integer-dot GEMV / GEMM straight from the super-blocks (isa: 0 auto, 1 AVX2, 2 AVX-512 VNNI)
+void illm_kq_gemm_int(int fmt, const float* x, int64_t m, const uint8_t* w, int64_t n, int64_t k, float* y,
+                      int isa);
 void illm_cpu_gemm_q4(int fmt, const float* x, int64_t m, const uint8_t* codes, const uint16_t* scales,
                       const uint16_t* mins, int64_t n, int64_t k, float* y, int isa);
 int illm_cpu_i8_supported(int fmt);

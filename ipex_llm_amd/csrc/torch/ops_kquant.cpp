@@ -58,16 +58,30 @@ Tensor kq_dequantize_hip(const Tensor& blob, int64_t fmt, int64_t n, int64_t k, 
   return dt == at::kFloat ? out.to(at::kFloat) : out;
 }
 
-Tensor kq_linear_cpu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k) {
+// isa: 0 = auto (integer dots below 512 rows, dequantize + GEMM above -- the
+// reference's BIGDL_LLM_LINEAR_THRESHOLD split), 1 = integer AVX2, 2 = integer
+// AVX-512 VNNI, 3 = f32 row-dequant reference
+Tensor kq_linear_isa(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t isa) {
   check_kq(fmt, k);
   TORCH_CHECK(x.size(-1) == k && blob.numel() == illm::kq_total_bytes((int)fmt, n, k), "kq_linear: shapes");
   Tensor xc = x.to(at::kFloat).contiguous();
   const int64_t m = xc.numel() / k;
   auto shape = x.sizes().vec();
   shape.back() = n;
+  Tensor bc = blob.contiguous();
+  if (isa == 0 && m >= 512) {
+    Tensor w = at::empty({n, k}, xc.options());
+    illm_kq_dequantize((int)fmt, bc.data_ptr<uint8_t>(), n, k, w.data_ptr<float>());
+    return at::matmul(xc, w.t()).view(shape).to(x.scalar_type());
+  }
   Tensor y = at::empty(shape, xc.options());
-  illm_kq_gemm((int)fmt, xc.data_ptr<float>(), m, blob.contiguous().data_ptr<uint8_t>(), n, k, y.data_ptr<float>());
+  if (isa == 3) illm_kq_gemm((int)fmt, xc.data_ptr<float>(), m, bc.data_ptr<uint8_t>(), n, k, y.data_ptr<float>());
+  else illm_kq_gemm_int((int)fmt, xc.data_ptr<float>(), m, bc.data_ptr<uint8_t>(), n, k, y.data_ptr<float>(), (int)isa);
   return y.to(x.scalar_type());
+}
+
+Tensor kq_linear_cpu(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k) {
+  return kq_linear_isa(x, blob, fmt, n, k, 0);
 }
 
 Tensor kq_linear_hip(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k) {
@@ -98,6 +112,7 @@ TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("kq_quantize(Tensor w, int fmt, Tensor? imatrix) -> Tensor", &kq_quantize);
   m.def("kq_dequantize(Tensor blob, int fmt, int n, int k, ScalarType dtype) -> Tensor");
   m.def("kq_linear(Tensor x, Tensor blob, int fmt, int n, int k) -> Tensor");
+  m.def("kq_linear_isa(Tensor x, Tensor blob, int fmt, int n, int k, int isa) -> Tensor", &kq_linear_isa);
 }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {

@@ -160,7 +160,9 @@ def test_from_gguf_keeps_kquant_blocks(tmp_path, qt):
     with torch.no_grad():
         a = dense(ids).logits
         b = m(ids).logits.float()
-    assert ((a - b).norm() / a.norm()).item() < 1e-3
+        # the CPU k-quant GEMM multiplies int8 activations (per-64 scales) against
+        # the super-block codes, as ggml's q8 x k-quant dot does
+        assert ((a - b).norm() / a.norm()).item() < 3e-2
 
 
 def _family(kind):

@@ -65,7 +65,7 @@ def test_cpu_linear_and_model(qtype):
     x = torch.randn(3, k)
     y = ops.kq_linear(x, blob, f, n, k)
     ref = x @ ops.kq_dequantize(blob, f, n, k).T
-    assert _rel(y, ref) < 1e-5
+    assert _rel(y, ref) < 2e-2                   # int8 activations (csrc/cpu/gemm_kq.cpp)
     cfg = LlamaConfig(vocab_size=128, hidden_size=256, intermediate_size=512, num_hidden_layers=1,
                       num_attention_heads=4, num_key_value_heads=2)
     m = optimize_model(LlamaForCausalLM(cfg).eval(), low_bit=qtype)

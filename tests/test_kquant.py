@@ -53,7 +53,9 @@ def test_kquant_linear_cpu(name):
     x = torch.randn(3, 256)
     want = torch.nn.functional.linear(x, m.dequantize(), lin.bias)
     got = m(x)
-    assert torch.allclose(got, want, atol=1e-4, rtol=1e-4)
+    # int8 activations against the super-block codes (csrc/cpu/gemm_kq.cpp,
+    # ggml's q8 x k-quant form): equal up to the activation rounding
+    assert ((got - want).norm() / want.norm()).item() < 2e-2
 
 
 def _tiny(path):
@@ -128,3 +130,33 @@ def test_iq_qtypes_use_native_2bit_super_blocks():
     for lin in lins:
         bpw = 8 * lin.weight.numel() / (lin.in_features * lin.out_features)
         assert bpw < 3.0, bpw
+
+
+@pytest.mark.parametrize("qtype", ["q4_k", "q5_k", "q6_k", "q2_k", "gguf_iq2_xxs", "gguf_iq2_xs",
+                                   "gguf_iq1_s", "gguf_iq1_m"])
+def test_cpu_integer_gemm_from_super_blocks(qtype):
+    """csrc/cpu/gemm_kq.cpp: int8 activations x unpacked u8 codes straight from
+    the GGUF super-blocks (AVX2 and AVX-512 VNNI) == the f32 GEMM over the
+    dequantized weight up to the int8 activation rounding; the auto path
+    dequantizes + GEMMs at >= 512 rows (the reference's linear threshold)"""
+    import torch
+    from ipex_llm_amd import ops
+    from ipex_llm_amd.quantize import get_format
+    f = get_format(qtype).fmt
+    torch.manual_seed(5)
+    n, k = 72, 768
+    w = torch.randn(n, k) * 0.02
+    blob = ops.kq_quantize(w, f)
+    wd = ops.kq_dequantize(blob, f, n, k)
+    isas = [1, 2] if "avx512_vnni" in open("/proc/cpuinfo").read() else [1]
+    for m in (1, 3, 9):
+        x = torch.randn(m, k)
+        ref = x @ wd.T
+        for isa in isas:
+            y = torch.ops.ipex_llm_amd.kq_linear_isa(x, blob, f, n, k, isa)
+            assert ((y - ref).norm() / ref.norm()).item() < 2e-2, (qtype, m, isa)
+        assert torch.equal(torch.ops.ipex_llm_amd.kq_linear_isa(x, blob, f, n, k, 0),
+                           torch.ops.ipex_llm_amd.kq_linear_isa(x, blob, f, n, k, isas[-1]))
+    x = torch.randn(512, k)
+    y = ops.kq_linear(x, blob, f, n, k)
+    assert torch.allclose(y, x @ wd.T, atol=1e-4, rtol=1e-4)
