@@ -118,6 +118,10 @@ struct GemvArgs {
   const int64_t* rpos;
   int rcols, rD;
   int* err;                // kernel error word: set by the dispatcher in ILLM_DEVICE_DEBUG builds
+  // EPI_STORE (v5, plain): greedy-decode argmax partials of the stored (T-rounded)
+  // outputs: wave (blockIdx.x * TG + tile group) writes {max, index as int bits}
+  // of its columns for every row m to amax[part * M + m] (first index on ties)
+  float2* amax;
 };
 
 }  // namespace illm

@@ -155,6 +155,15 @@ struct NormArgs {
   int unit_offset;         // gemma: x * (1 + w)
   int store_residual;
   int zero_partials;       // re-zero the (atomic-accumulated) partial slab after reading it
+  // embedding gather (decode step entry): row m of the input is x[ids[m]] of
+  // the [vocab, H] table, written unnormalised to gather_out (the residual
+  // stream) next to the normalised out; block 0 also zeroes zero[0:zero_n]
+  const int64_t* ids;
+  int64_t vocab;
+  uint16_t* gather_out;
+  float* zero;
+  int zero_n;
+  int* err;
 };
 void launch_add_rms_norm(bool bf16, const NormArgs& a, hipStream_t st);
 void launch_rms_norm_bwd(bool bf16, const uint16_t* x, const uint16_t* g, const uint16_t* w, uint16_t* dx, int M,
@@ -311,7 +320,8 @@ void launch_embedding_rows(bool bf16, const uint8_t* blob, int fmt, const int64_
 
 void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int64_t* ids, int64_t* next_ids,
                            int64_t* pos, const int32_t* block_tables, int max_blocks, int bs, int64_t* slots,
-                           int32_t* seq_lens, const int64_t* pos_offset, int* err, hipStream_t st);
+                           int32_t* seq_lens, const int64_t* pos_offset, int* err, hipStream_t st,
+                           const float* parts = nullptr, int nparts = 0);
 
 // ---- one-shot / two-shot xGMI peer all-reduce (allreduce.hip) -------------
 constexpr int AR_MAX_RANKS = 8;

@@ -371,8 +371,63 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
   }
 
   // ---- stage x[0:Mloc, kbase:kbase+kw] -> LDS in C
-  if (!(ILLM_GEMV5_ABL & 2)) {
-    const int vpr = kw / 8;
+  const int vpr = kw / 8;
+  // the staged value's LDS store and its per-(row, 64-block) sums: the 8
+  // lanes of a block are 8 consecutive threads (vpr is a multiple of 16),
+  // reduced with shuffles instead of a second LDS pass behind another barrier
+  auto commit_x = [&](int v, uint4 val) {
+    const int m = v / vpr, kk = (v % vpr) * 8;
+    *(uint4*)(xs + m * ldx + kk) = val;
+    const uint32_t sw[4] = {val.x, val.y, val.z, val.w};
+    float bsum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; i++) bsum += to_f32<C>((uint16_t)(sw[i] & 0xffff)) + to_f32<C>((uint16_t)(sw[i] >> 16));
+    bsum += __shfl_xor(bsum, 1, 8);
+    bsum += __shfl_xor(bsum, 2, 8);
+    bsum += __shfl_xor(bsum, 4, 8);
+    if ((v & 7) == 0) {
+      const int blk = kk >> 6, nch = c1 - c0;
+      float* rec = (float*)(sxs + m * nch + (blk >> 1));
+      rec[blk & 1] = -OFF * bsum;
+      rec[2 + (blk & 1)] = bsum;
+    }
+  };
+  auto to_c = [](uint4 val) -> uint4 {
+    if constexpr (!std::is_same<C, T>::value) {   // bf16 activations -> f16 (LUT formats)
+      uint32_t w[4] = {val.x, val.y, val.z, val.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const float lo = fminf(fmaxf(bf16_to_f32(w[i] & 0xffff), -65504.f), 65504.f);
+        const float hi = fminf(fmaxf(bf16_to_f32(w[i] >> 16), -65504.f), 65504.f);
+        w[i] = pack2<F16>(lo, hi);
+      }
+      return make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    return val;
+  };
+  const bool plain_x = !a.apo && !a.xpart && !defer && !a.nacc;
+  if (!(ILLM_GEMV5_ABL & 2) && plain_x) {
+    // plain activations: every load of a thread's (up to XPF) staging slots is
+    // requested before the first LDS store / shuffle reduction -- one L2 round
+    // trip instead of one per slot (the loop form below serialised them:
+    // ~3.8 us of a 19.9 us gate/up GEMV prologue at M = 8, 8 slots per thread,
+    // profiles/gemv5_ablation2_r3.jsonl abl 1 vs 3)
+    constexpr int XPF = 4;
+    const int nthr = NW * 64, total = Mloc * vpr;
+    for (int v0 = threadIdx.x; v0 < total; v0 += XPF * nthr) {
+      uint4 xv[XPF];
+#pragma unroll
+      for (int u = 0; u < XPF; u++) {
+        const int vv = min(v0 + u * nthr, total - 1);
+        const int m = vv / vpr, kk = (vv % vpr) * 8;
+        xv[u] = kbase + kk < a.K ? *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk)
+                                 : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < XPF; u++)
+        if (v0 + u * nthr < total) commit_x(v0 + u * nthr, to_c(xv[u]));
+    }
+  } else if (!(ILLM_GEMV5_ABL & 2)) {
     for (int v = threadIdx.x; v < Mloc * vpr; v += NW * 64) {
       const int m = v / vpr, kk = (v % vpr) * 8;
       uint4 val = make_uint4(0, 0, 0, 0);
@@ -501,35 +556,9 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
         }
         val = make_uint4(o4[0], o4[1], o4[2], o4[3]);
       } else if (kbase + kk < a.K) {
-        val = *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk);
-        if constexpr (!std::is_same<C, T>::value) {   // bf16 activations -> f16 (LUT formats)
-          uint32_t w[4] = {val.x, val.y, val.z, val.w};
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const float lo = fminf(fmaxf(bf16_to_f32(w[i] & 0xffff), -65504.f), 65504.f);
-            const float hi = fminf(fmaxf(bf16_to_f32(w[i] >> 16), -65504.f), 65504.f);
-            w[i] = pack2<F16>(lo, hi);
-          }
-          val = make_uint4(w[0], w[1], w[2], w[3]);
-        }
+        val = to_c(*(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk));
       }
-      *(uint4*)(xs + m * ldx + kk) = val;
-      // per (row, 64-block) sums of the staged activations: the 8 lanes of a
-      // block are 8 consecutive threads (vpr is a multiple of 16), reduced with
-      // shuffles here instead of a second LDS pass behind another barrier
-      const uint32_t sw[4] = {val.x, val.y, val.z, val.w};
-      float bsum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; i++) bsum += to_f32<C>((uint16_t)(sw[i] & 0xffff)) + to_f32<C>((uint16_t)(sw[i] >> 16));
-      bsum += __shfl_xor(bsum, 1, 8);
-      bsum += __shfl_xor(bsum, 2, 8);
-      bsum += __shfl_xor(bsum, 4, 8);
-      if ((v & 7) == 0) {
-        const int blk = kk >> 6, nch = c1 - c0;
-        float* rec = (float*)(sxs + m * nch + (blk >> 1));
-        rec[blk & 1] = -OFF * bsum;
-        rec[2 + (blk & 1)] = bsum;
-      }
+      commit_x(v, val);
     }
   }
   __syncthreads();
@@ -724,6 +753,8 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
       else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
     }
   } else {
+    float abest = -INFINITY;         // argmax partial (EPI_STORE + a.amax)
+    int abi = 0x7fffffff;
 #pragma unroll
     for (int t = 0; t < TPW; t++) {
       const int n0 = (tile0 + t) * 16 + 4 * g;
@@ -755,6 +786,27 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
         uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n0;
         if (n0 + 3 < a.N && ((a.ldo | n0) & 3) == 0) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
         else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
+        if constexpr (EPI == EPI_STORE && !MOE) {
+          if (a.amax) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const float v = to_f32<T>(from_f32<T>(o[i]));   // the stored logit
+              if (n0 + i < a.N && v > abest) { abest = v; abi = n0 + i; }
+            }
+          }
+        }
+      }
+    }
+    if constexpr (EPI == EPI_STORE && !MOE) {
+      if (a.amax) {
+        // the 4 k-groups of this row hold 4 disjoint column sets (first index on ties)
+#pragma unroll
+        for (int off = 16; off < 64; off <<= 1) {
+          const float ov = __shfl_xor(abest, off, 64);
+          const int oi = __shfl_xor(abi, off, 64);
+          if (ov > abest || (ov == abest && oi < abi)) { abest = ov; abi = oi; }
+        }
+        if (g == 0) a.amax[((size_t)blockIdx.x * TG + tg) * a.M + m] = make_float2(abest, __int_as_float(abi));
       }
     }
   }

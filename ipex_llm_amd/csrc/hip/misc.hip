@@ -762,14 +762,59 @@ void launch_embedding_rows(bool bf16, const uint8_t* blob, int fmt, const int64_
 // feeds the token back as the next input, advances the position and
 // precomputes the next step's KV slot and key count -- replacing ~8 small
 // framework kernels per graph-captured decode step.
+//
+// parts (instead of logits): the lm_head GEMV's per-wave argmax partials
+// (lowbit_gemv5.cuh EPI_STORE + amax, {max, index bits} [nparts][B]): the
+// vocabulary scan shrinks from V logits to nparts pairs, same tie rule
 template <typename T>
 __global__ void __launch_bounds__(1024) decode_advance_kernel(const uint16_t* logits, int V, int64_t* ids,
                                                               int64_t* next_ids, int64_t* pos,
                                                               const int32_t* block_tables, int max_blocks, int bs,
                                                               int64_t* slots, int32_t* seq_lens,
-                                                              const int64_t* pos_offset, int* err) {
+                                                              const int64_t* pos_offset, int* err,
+                                                              const float2* parts, int nparts) {
   const int b = blockIdx.x, tid = threadIdx.x;
-  if (logits) {
+  if (parts) {
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    const int B = gridDim.x;
+    for (int p0 = tid; p0 < nparts; p0 += 1024 * 4) {
+      float2 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) q[u] = parts[(size_t)min(p0 + u * 1024, nparts - 1) * B + b];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (p0 + u * 1024 >= nparts) break;
+        const int qi = __float_as_int(q[u].y);
+        if (q[u].x > best || (q[u].x == best && qi < bi)) { best = q[u].x; bi = qi; }
+      }
+    }
+    __shared__ float pv[16];
+    __shared__ int pi[16];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if ((tid & 63) == 0) { pv[tid >> 6] = best; pi[tid >> 6] = bi; }
+    __syncthreads();
+    if (tid < 64) {
+      best = tid < 16 ? pv[tid] : -INFINITY;
+      bi = tid < 16 ? pi[tid] : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+      }
+      if (tid == 0) {
+        if (bi == 0x7fffffff) bi = 0;
+        ids[b] = bi;
+        next_ids[b] = bi;
+      }
+    }
+  } else if (logits) {
     const uint16_t* row = logits + (size_t)b * V;
     float best = -INFINITY;
     int bi = 0x7fffffff;
@@ -841,11 +886,13 @@ __global__ void __launch_bounds__(1024) decode_advance_kernel(const uint16_t* lo
 
 void launch_decode_advance(bool bf16, const uint16_t* logits, int B, int V, int64_t* ids, int64_t* next_ids,
                            int64_t* pos, const int32_t* block_tables, int max_blocks, int bs, int64_t* slots,
-                           int32_t* seq_lens, const int64_t* pos_offset, int* err, hipStream_t st) {
+                           int32_t* seq_lens, const int64_t* pos_offset, int* err, hipStream_t st,
+                           const float* parts, int nparts) {
+  const float2* pp = (const float2*)parts;
   if (bf16) hipLaunchKernelGGL(decode_advance_kernel<BF16>, dim3(B), dim3(1024), 0, st, logits, V, ids, next_ids, pos,
-                               block_tables, max_blocks, bs, slots, seq_lens, pos_offset, err);
+                               block_tables, max_blocks, bs, slots, seq_lens, pos_offset, err, pp, nparts);
   else hipLaunchKernelGGL(decode_advance_kernel<F16>, dim3(B), dim3(1024), 0, st, logits, V, ids, next_ids, pos,
-                          block_tables, max_blocks, bs, slots, seq_lens, pos_offset, err);
+                          block_tables, max_blocks, bs, slots, seq_lens, pos_offset, err, pp, nparts);
 }
 
 // ---- RWKV-4 WKV recurrence (reference xe_linear.rwkv_linear_attention_v4,

@@ -39,10 +39,22 @@ __global__ void __launch_bounds__(NORM_THREADS)
     add_rms_norm_kernel(const uint16_t* __restrict__ x, const float* __restrict__ partials,
                         int nsplit, uint16_t* __restrict__ residual, const uint16_t* __restrict__ w,
                         uint16_t* __restrict__ out, int H, float eps, int unit_offset,
-                        int store_residual, int zero_partials) {
+                        int store_residual, int zero_partials, const int64_t* __restrict__ ids, int64_t vocab,
+                        uint16_t* __restrict__ gather_out, float* zero, int zero_n, int* err) {
   __shared__ float red[NORM_THREADS / 64];
   const int row = blockIdx.x;
   const int M = gridDim.x;
+  int64_t xrow = row;
+  if (ids) {
+    // embedding row of this token (an out-of-vocabulary id reads row 0 and is reported)
+    xrow = ids[row];
+    if ((uint64_t)xrow >= (uint64_t)vocab) {
+      if (threadIdx.x == 0) kerr(err, ERR_TOKEN);
+      xrow = 0;
+    }
+    if (zero && row == 0)
+      for (int i = threadIdx.x; i < zero_n; i += NORM_THREADS) zero[i] = 0.f;
+  }
   // the weight does not depend on the row: load it first so it is not a
   // dependent memory round trip behind the block reduction
   uint4 wraw[MAXV];
@@ -77,7 +89,8 @@ __global__ void __launch_bounds__(NORM_THREADS)
           ((float4*)z)[1] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       } else {
-        load8<T>(x + (size_t)row * H + c, a);
+        load8<T>(x + (size_t)xrow * H + c, a);
+        if (gather_out) store8<T>(gather_out + (size_t)row * H + c, a);
       }
       if (residual) {
         float r[8];
@@ -161,7 +174,8 @@ static void launch_add_rms(const NormArgs& a, hipStream_t st) {
 #define L_RMS(MV)                                                                             \
   hipLaunchKernelGGL((add_rms_norm_kernel<T, MV>), dim3(a.M), dim3(NORM_THREADS), 0, st, a.x, \
                      a.partials, a.nsplit, a.residual, a.w, a.out, a.H, a.eps, a.unit_offset,  \
-                     a.store_residual, a.zero_partials)
+                     a.store_residual, a.zero_partials, a.ids, a.vocab, a.gather_out, a.zero,  \
+                     a.zero_n, a.err)
   if (nv <= 1) L_RMS(1);
   else if (nv <= 2) L_RMS(2);
   else if (nv <= 4) L_RMS(4);

@@ -159,7 +159,9 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("moe_align(Tensor ids, int e0, int num_local) -> (Tensor, Tensor)");
   m.def("gemv_glu_in(Tensor part, Tensor blob, int fmt, int n, int k, int act, int ksplit, ScalarType dtype, Tensor(a!)? acc=None, Tensor(b!)? zero=None, Tensor? xss=None, int xss_n=0, float xss_eps=0.0) -> Tensor");
   m.def("l3_prefetch(Tensor t, int offset=0, int nbytes=-1, int wgs=1024) -> ()");
-  m.def("decode_advance(Tensor? logits, Tensor(a!) ids, Tensor(b!) next_ids, Tensor(c!) pos, Tensor block_tables, int bs, Tensor(d!) slots, Tensor(e!) seq_lens, Tensor? pos_offset=None) -> ()");
+  m.def("decode_advance(Tensor? logits, Tensor(a!) ids, Tensor(b!) next_ids, Tensor(c!) pos, Tensor block_tables, int bs, Tensor(d!) slots, Tensor(e!) seq_lens, Tensor? pos_offset=None, Tensor? parts=None) -> ()");
+  m.def("gemv_argmax(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias=None) -> (Tensor, Tensor)");
+  m.def("embed_rms_norm(Tensor ids, Tensor table, Tensor w, float eps, bool unit_offset=False, Tensor(a!)? zero=None) -> (Tensor, Tensor)");
   m.def("rope_kv_fused(Tensor(d!) part, Tensor? bias, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor pos, Tensor block_tables, int tq, Tensor inv_freq, Tensor? q_norm, Tensor? k_norm, float norm_eps, float q_scale, int Hq, int Hkv, int D, int rot_dim, bool interleaved, int kv_fp8, float k_scale, float v_scale, Tensor? pos_offset=None, bool zero_part=False, Tensor? pss=None, int pss_n=0, float pss_eps=0.0) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_lens, int Tq, float scale, float softcap, int window, int kv_fp8, float k_scale, float v_scale) -> Tensor");
   m.def("attn_decode_split(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int kv_fp8, float k_scale, float v_scale, Tensor? alibi) -> (Tensor, Tensor)");

@@ -245,6 +245,54 @@ Tensor gemv(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t
   return out;
 }
 
+// greedy decode head: the v5 GEMV stores the logits (T) and every wave writes
+// the argmax {max, index} of its columns per row (parts [nparts, M, 2] f32),
+// which decode_advance reduces instead of re-reading the [M, V] logits.
+// Split-K 1 (the stored values are final); M <= 16.
+std::tuple<Tensor, Tensor> gemv_argmax(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k,
+                                       const c10::optional<Tensor>& bias) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda() && x.size(-1) == k, "gemv_argmax: GPU x [M, k]");
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  const int64_t M = xc.numel() / k;
+  TORCH_CHECK(M >= 1 && M <= 16, "gemv_argmax: 1..16 rows");
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemv_argmax: weight blob too small");
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  Plan5 p = plan5(M, NT, KC, true, 1);
+  // the full-K x slice (M x K bf16) is staged once per workgroup: larger M
+  // shares it among 8 tiles (one workgroup per CU fits at M = 8, K = 4096)
+  static const int nw_env = getenv("ILLM_ARGMAX_NW") ? atoi(getenv("ILLM_ARGMAX_NW")) : 0;
+  p.nw = nw_env == 4 || nw_env == 8 ? nw_env : (M > 2 ? 8 : 4);
+  p.gx = (unsigned)((NT + p.nw - 1) / p.nw);
+  TORCH_CHECK(p.shmem <= kMaxLds, "gemv_argmax: x slice exceeds LDS");
+  illm::GemvArgs a{};
+  a.x = p16(xc);
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.KC = (int)KC;
+  a.lut_fmt = (int)fmt;
+  a.N = (int)n;
+  a.cpk = (int)p.cpk;
+  a.nw = p.nw;
+  auto out_shape = xc.sizes().vec();
+  out_shape.back() = n;
+  Tensor out = at::empty(out_shape, xc.options());
+  a.out = out.data_ptr();
+  a.ldo = (int)n;
+  a.bias = p16o(bias);
+  const int64_t tg = p.nw / p.kw;
+  const int64_t nparts = NT;                        // TPW = 1: one part per 16-column tile
+  TORCH_CHECK((int64_t)p.gx * tg >= nparts, "gemv_argmax: geometry");
+  Tensor parts = at::empty({nparts, M, 2}, xc.options().dtype(at::kFloat));
+  a.amax = (float2*)parts.data_ptr<float>();
+  launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_STORE, dim3(p.gx, 1), p.shmem, a);
+  return {out, parts};
+}
+
 // prefill-size low-bit GEMM: MFMA with in-register dequant of the tiled weight
 Tensor gemm(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, const c10::optional<Tensor>& bias) {
   TORCH_CHECK(x.is_cuda() && blob.is_cuda(), "gemm: GPU tensors expected");
@@ -675,6 +723,43 @@ Tensor add_rms_norm(const c10::optional<Tensor>& x, const c10::optional<Tensor>&
   a.zero_partials = zero_partials && a.partials != nullptr;
   if (M > 0) illm::launch_add_rms_norm(bf16, a, cur_stream());
   return out;
+}
+
+// decode-step entry: embedding gather + RMSNorm of the first layer in one
+// launch (the gathered rows are the residual stream), optionally zeroing an
+// f32 buffer (the step's deferred-norm sums of squares): replaces the
+// embedding gather, the Fill and the first norm launch
+std::tuple<Tensor, Tensor> embed_rms_norm(const Tensor& ids, const Tensor& table, const Tensor& w, double eps,
+                                          bool unit_offset, const c10::optional<Tensor>& zero) {
+  c10::DeviceGuard g(w.device());
+  const bool bf16 = is_bf16(w);
+  const int64_t H = w.numel();
+  TORCH_CHECK(H % 8 == 0 && H <= 8 * 256 * 8, "embed_rms_norm: hidden size must be a multiple of 8, <= 16384");
+  TORCH_CHECK(table.dim() == 2 && table.size(1) == H && table.is_contiguous() &&
+                  table.scalar_type() == w.scalar_type(), "embed_rms_norm: table [V, H] in the weight dtype");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.is_cuda(), "embed_rms_norm: int64 ids");
+  const int64_t M = ids.numel();
+  Tensor res = at::empty({M, H}, w.options());
+  Tensor out = at::empty({M, H}, w.options());
+  illm::NormArgs a{};
+  a.x = p16(table);
+  a.w = p16(w);
+  a.out = m16(out);
+  a.M = (int)M;
+  a.H = (int)H;
+  a.eps = (float)eps;
+  a.unit_offset = unit_offset;
+  a.ids = ids.data_ptr<int64_t>();
+  a.vocab = table.size(0);
+  a.gather_out = m16(res);
+  a.err = kernel_err(w.device());
+  if (zero.has_value() && zero->defined()) {
+    TORCH_CHECK(zero->scalar_type() == at::kFloat && zero->is_contiguous() && zero->is_cuda(), "zero: f32");
+    a.zero = zero->data_ptr<float>();
+    a.zero_n = (int)zero->numel();
+  }
+  if (M > 0) illm::launch_add_rms_norm(bf16, a, cur_stream());
+  return {res, out};
 }
 
 // act(gate) * up (dy undefined) or its gradient (dgate, dup) for contiguous same-shape tensors
@@ -1469,12 +1554,16 @@ Tensor embedding_lowbit(const Tensor& blob, int64_t fmt, int64_t n, int64_t k, c
 // logits: [B, V] bf16/f16 or undefined (sampling done by the host: only advance)
 void decode_advance(const c10::optional<Tensor>& logits, Tensor& ids, Tensor& next_ids, Tensor& pos,
                     const Tensor& block_tables, int64_t bs, Tensor& slots, Tensor& seq_lens,
-                    const c10::optional<Tensor>& pos_offset) {
+                    const c10::optional<Tensor>& pos_offset, const c10::optional<Tensor>& parts) {
   c10::DeviceGuard g(pos.device());
   const int64_t B = pos.numel();
   TORCH_CHECK(pos.scalar_type() == at::kLong && ids.scalar_type() == at::kLong && slots.scalar_type() == at::kLong &&
               seq_lens.scalar_type() == at::kInt && block_tables.scalar_type() == at::kInt, "decode_advance dtypes");
   const bool has = logits.has_value() && logits->defined();
+  const bool hp = parts.has_value() && parts->defined();
+  TORCH_CHECK(!hp || (parts->dim() == 3 && parts->size(1) == B && parts->size(2) == 2 &&
+                      parts->scalar_type() == at::kFloat && parts->is_contiguous()),
+              "decode_advance: parts must be f32 [nparts, B, 2]");
   bool bf16 = true;
   int V = 0;
   if (has) {
@@ -1487,7 +1576,8 @@ void decode_advance(const c10::optional<Tensor>& logits, Tensor& ids, Tensor& ne
                               (int)block_tables.size(1), (int)bs, slots.data_ptr<int64_t>(),
                               seq_lens.data_ptr<int32_t>(),
                               (pos_offset.has_value() && pos_offset->defined()) ? pos_offset->data_ptr<int64_t>() : nullptr,
-                              kernel_err(pos.device()), cur_stream());
+                              kernel_err(pos.device()), cur_stream(), hp ? parts->data_ptr<float>() : nullptr,
+                              hp ? (int)parts->size(0) : 0);
 }
 
 // stream bytes [offset, offset + nbytes) of t's storage through the caches
@@ -1520,6 +1610,8 @@ int* illm_kernel_err(const c10::Device& dev) { return kernel_err(dev); }
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("gemv_glu_in", &gemv_glu_in);
   m.impl("decode_advance", &decode_advance);
+  m.impl("gemv_argmax", &gemv_argmax);
+  m.impl("embed_rms_norm", &embed_rms_norm);
   m.impl("l3_prefetch", &l3_prefetch);
   m.impl("rope_kv_fused", &rope_kv_fused);
   m.impl("embedding_lowbit", &embedding_lowbit);

@@ -27,6 +27,23 @@ def nsplit_for(max_len: int) -> int:
     return max(1, (max_len + SPLIT - 1) // SPLIT)
 
 
+_ARGMAX_EPI = __import__("os").environ.get("ILLM_ARGMAX_EPI", "1") != "0"
+
+
+def _argmax_head_ok(head, h: torch.Tensor, spec) -> bool:
+    """greedy decode through the lm_head GEMV's argmax epilogue (ops_hip.cpp
+    gemv_argmax): a plain single-device low-bit head on the v5 GEMV formats"""
+    from ..transformers.low_bit_linear import LowBitLinear
+    from ..quantize import qtypes as Q
+    return (_ARGMAX_EPI and isinstance(head, LowBitLinear) and head.mp_group is None
+            and getattr(head, "g_idx_map", None) is None and getattr(head, "compute_dtype", None) in (None, h.dtype)
+            and not spec.final_softcap and h.dim() == 2 and h.shape[0] <= 16
+            and h.dtype in (torch.bfloat16, torch.float16)
+            and head.fmt in (Q.FMT_SYM_INT4, Q.FMT_ASYM_INT4, Q.FMT_NF4, Q.FMT_NF3, Q.FMT_FP4, Q.FMT_SYM_INT8,
+                             Q.FMT_SYM_INT5, Q.FMT_ASYM_INT5, Q.FMT_FP8E4, Q.FMT_FP8E5, Q.FMT_FP6)
+            and (head.bias is None or head.bias.dtype == h.dtype))
+
+
 class DecodeStep:
     """Static-buffer decode step (B sequences, 1 new token each).
 
@@ -69,7 +86,17 @@ class DecodeStep:
         m = self.model
         if self.native_glue:
             h = m.forward_tokens(self.ids, self.pos, self.slots, meta, self.cache, return_hidden=True)
-            logits = m.lm_head(h.contiguous())
+            head = m.lm_head
+            if self.greedy and _argmax_head_ok(head, h, m.spec):
+                # the lm_head GEMV writes per-wave argmax partials next to the
+                # logits: decode_advance reduces ~V / 16 pairs, not V logits
+                logits, parts = torch.ops.ipex_llm_amd.gemv_argmax(h.contiguous(), head.weight, head.fmt,
+                                                                  head.out_features, head.in_features, head.bias)
+                self.logits = logits
+                torch.ops.ipex_llm_amd.decode_advance(None, self.ids, self.next_ids, self.pos, self.block_tables,
+                                                      self.cache.bs, self.slots, self.seq_lens, self.off, parts)
+                return
+            logits = head(h.contiguous())
             if m.spec.final_softcap:
                 logits = (torch.tanh(logits.float() / m.spec.final_softcap) * m.spec.final_softcap).to(h.dtype)
             self.logits = logits

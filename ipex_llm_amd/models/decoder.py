@@ -489,6 +489,16 @@ class NativeCausalLM(nn.Module):
     # launches per layer fewer.  ILLM_NORM_IN=0 restores the standalone norms.
     _norm_in_env = __import__("os").environ.get("ILLM_NORM_IN", "1") != "0"
 
+    _embed_norm_env = __import__("os").environ.get("ILLM_EMBED_NORM", "1") != "0"
+
+    def _embed_norm_ok(self, ids: torch.Tensor) -> bool:
+        e = self.embed_tokens
+        return (self._embed_norm_env and self.embed_module is None and self.spec.embed_scale == 1.0
+                and isinstance(e, torch.Tensor) and e.is_cuda and ids.is_cuda and e.dim() == 2
+                and e.dtype == self.dtype and e.dtype in (torch.bfloat16, torch.float16) and e.is_contiguous()
+                and self.layers[0].input_layernorm.dtype == e.dtype and self.spec.hidden_size % 8 == 0
+                and ops.native_gpu(ids))
+
     def _defer_ok(self, ref: torch.Tensor, T: int) -> bool:
         return DEFER_NORM and T <= min(ACC_MAX_M, DEFER_MAX_M)
 
@@ -607,16 +617,26 @@ class NativeCausalLM(nn.Module):
         is the previous stage's residual stream [T, H]; a non-last stage
         returns its residual stream instead of logits."""
         s = self.spec
-        if hidden_in is not None:
-            residual = hidden_in.to(self.dtype).contiguous().clone()
-        else:
-            h = self.embed_module(ids).to(self.dtype) if self.embed_module is not None else \
-                F.embedding(ids, self.embed_tokens)
-            if s.embed_scale != 1.0:
-                h = h * torch.tensor(s.embed_scale, dtype=h.dtype, device=h.device)
-            residual = h.contiguous()
-        x = ops.rms_norm(residual, self.layers[0].input_layernorm, s.rms_eps, s.norm_unit_offset)
         T = ids.shape[0]
+        ss_zeroed = None
+        if hidden_in is None and self._embed_norm_ok(ids):
+            # one launch: embedding gather (the residual stream), the first
+            # layer's RMSNorm and the zeroing of the step's deferred-norm sums
+            defer0 = self._norm_in_ok(self.embed_tokens, T) and self._defer_ok(self.embed_tokens, T)
+            ss_zeroed = self._acc(T, 2 * len(self.layers), ids.device, "SS") if defer0 else None
+            residual, x = torch.ops.ipex_llm_amd.embed_rms_norm(ids.contiguous(), self.embed_tokens,
+                                                               self.layers[0].input_layernorm, s.rms_eps,
+                                                               s.norm_unit_offset, ss_zeroed)
+        else:
+            if hidden_in is not None:
+                residual = hidden_in.to(self.dtype).contiguous().clone()
+            else:
+                h = self.embed_module(ids).to(self.dtype) if self.embed_module is not None else \
+                    F.embedding(ids, self.embed_tokens)
+                if s.embed_scale != 1.0:
+                    h = h * torch.tensor(s.embed_scale, dtype=h.dtype, device=h.device)
+                residual = h.contiguous()
+            x = ops.rms_norm(residual, self.layers[0].input_layernorm, s.rms_eps, s.norm_unit_offset)
         rope = self.rope_cache if self.rope_cache is not None else self.inv_freq
         # norm-in decode: the down projection's atomic accumulator stays pending
         # and the next layer's qkv GEMV adds + normalises it in its prologue;
@@ -630,7 +650,8 @@ class NativeCausalLM(nn.Module):
         ss_all = None
         if defer:
             ss_all = self._acc(T, 2 * len(self.layers), x.device, "SS")
-            ss_all.zero_()
+            if ss_zeroed is not ss_all:
+                ss_all.zero_()
         ss_q = None                     # sums of squares of the current layer's qkv input (deferred)
         zero_gu = None                  # consumed gate/up accumulator (batch > DEFER_GLU_MAX_M), zeroed next
         # fused-RoPE decode attention (batch <= ROPE_IN_MAX_M, one token each): the qkv

@@ -336,3 +336,9 @@ def _(x, blob, fmt, n, k, bias=None, out_f32=False, glu=False, act=0):
 @register_fake("ipex_llm_amd::fp8_gemm8p")
 def _(xq, sx, w, ws, e5m2):
     return xq.new_empty((xq.shape[0], w.shape[0]), dtype=torch.bfloat16)
+
+
+@register_fake("ipex_llm_amd::gemv_argmax")
+def _gemv_argmax(x, blob, fmt, n, k, bias=None):
+    M = x.numel() // k
+    return x.new_empty(*x.shape[:-1], n), x.new_empty(((n + 15) // 16, M, 2), dtype=torch.float32)

@@ -741,3 +741,81 @@ def test_attn_decode_v3_variants_subprocess(cuda, env):
                         "or gemv_rope_epilogue) and not subprocess"],
                        env=e, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+@pytest.mark.parametrize("name", ["sym_int4", "asym_int4", "nf4", "fp8_e4m3"])
+def test_gemv_argmax_epilogue(cuda, M, name):
+    """lm_head GEMV with the argmax epilogue: the stored logits equal the plain
+    GEMV's, and decode_advance over the per-wave partials picks exactly
+    torch.argmax of those stored logits (first index on ties: forced ties too)"""
+    f = get_format(name).fmt
+    torch.manual_seed(7)
+    n, k = 1000 + 8, 512                  # a partial last tile
+    w = torch.randn(n, k, device=cuda) * 0.05
+    w[5] = w[700]                           # duplicate rows -> tied logits
+    blob = ops.quantize(w, f)
+    x = torch.randn(M, k, device=cuda).bfloat16()
+    logits, parts = torch.ops.ipex_llm_amd.gemv_argmax(x, blob, f, n, k, None)
+    ref = ops.lowbit_matmul(x, blob, f, n, k)      # (its own split-K order at M > 1)
+    assert _rel(logits.float(), ref.float()) < 1e-2
+    ids = torch.zeros(M, dtype=torch.long, device=cuda)
+    nxt = torch.zeros_like(ids)
+    pos = torch.zeros_like(ids)
+    bt = torch.zeros(M, 4, dtype=torch.int32, device=cuda)
+    slots = torch.zeros_like(ids)
+    sl = torch.zeros(M, dtype=torch.int32, device=cuda)
+    torch.ops.ipex_llm_amd.decode_advance(None, ids, nxt, pos, bt, 64, slots, sl, None, parts)
+    assert torch.equal(nxt, torch.argmax(logits.float(), -1))
+    # a row whose max sits in the duplicated pair: first index wins
+    x2 = w[700:701].bfloat16().repeat(M, 1) * 4
+    logits2, parts2 = torch.ops.ipex_llm_amd.gemv_argmax(x2, blob, f, n, k, None)
+    torch.ops.ipex_llm_amd.decode_advance(None, ids, nxt, pos, bt, 64, slots, sl, None, parts2)
+    assert torch.equal(nxt, torch.argmax(logits2.float(), -1))
+
+
+def test_decode_argmax_epilogue_matches_logits_argmax_subprocess(cuda):
+    """whole-model greedy decode (graph) with the lm_head argmax epilogue ==
+    the logits-scanning decode_advance (ILLM_ARGMAX_EPI=0) token for token"""
+    import os
+    import subprocess
+    import sys
+    code = r"""
+import torch
+from transformers import LlamaConfig
+from ipex_llm_amd.engine.runner import Engine
+from ipex_llm_amd.models.builder import random_native_model
+cfg = LlamaConfig(vocab_size=1000, hidden_size=512, intermediate_size=1024, num_hidden_layers=2,
+                  num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=1024)
+m = random_native_model(cfg, "sym_int4", "cuda", torch.bfloat16, seed=3)
+prompts = [list(range(1, 40)), list(range(5, 30)), [7] * 20]
+print(Engine(m).generate(prompts, max_new_tokens=12, use_graph=True))
+"""
+    outs = []
+    for flag in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, ILLM_ARGMAX_EPI=flag),
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs.append(r.stdout.strip().splitlines()[-1])
+    assert outs[0] == outs[1]
+
+
+def test_embed_rms_norm_matches_gather_then_norm(cuda):
+    """decode-step entry kernel: embedding gather + RMSNorm (+ zeroing the
+    step's sums-of-squares buffer) == F.embedding then rms_norm, bit for bit;
+    an out-of-vocabulary id is reported through the kernel error word"""
+    torch.manual_seed(9)
+    V, H = 1000, 4096
+    table = torch.randn(V, H, device=cuda).bfloat16()
+    w = (torch.rand(H, device=cuda) + 0.5).bfloat16()
+    ids = torch.tensor([3, 999, 0, 3, 512], device=cuda)
+    z = torch.ones(64, device=cuda)
+    res, x = torch.ops.ipex_llm_amd.embed_rms_norm(ids, table, w, 1e-5, False, z)
+    ref_res = torch.nn.functional.embedding(ids, table)
+    assert torch.equal(res, ref_res)
+    assert torch.equal(x, ops.rms_norm(ref_res, w, 1e-5))
+    assert int(z.count_nonzero()) == 0
+    ops.check_kernel_errors(cuda)
+    torch.ops.ipex_llm_amd.embed_rms_norm(torch.tensor([V + 5], device=cuda), table, w, 1e-5, False, None)
+    with pytest.raises(RuntimeError):
+        ops.check_kernel_errors(cuda)
