@@ -71,7 +71,7 @@ def _cmd(src: str, obj: str):
     common = ["-O3", "-fPIC", "-std=c++17", "-I", CSRC, "-MMD", "-MF", obj + ".d", *_DEFS]
     if src.endswith(".hip"):
         extra = []
-        if os.path.basename(src).startswith(("gemv_", "attn_prefill")):
+        if os.path.basename(src).startswith(("gemv_", "attn_prefill", "gemm_8p")):
             # keep the GEMV epilogue as scalar f32 FMAs: SLP-packed v_pk_fma_f32
             # beside MFMAs costs issue cycles on gfx950 (and blocks v_fma_mix)
             # and MFMA results in VGPRs (no v_accvgpr_read per 64-block readout)

@@ -241,9 +241,11 @@ __global__ void __launch_bounds__(64 * NW, ILLM_ATTN_V3_MINW) attn_decode_v3_ker
   // ---- sequence length and this wave's block-table entry, in flight together
   int len = a.seq_lens[b];
   const int blk = a.block_tables[(size_t)b * a.max_blocks + min(kw0 / a.bs, a.max_blocks - 1)];
-  if ((int64_t)len > (int64_t)a.max_blocks * a.bs || (int64_t)gridDim.x * SK < len) {
+  // coverage is the caller's nominal split grid (nsplit x SPLIT keys), which
+  // the rounded-up v3 grid can exceed: keys past it are reported, not read
+  if ((int64_t)len > (int64_t)a.max_blocks * a.bs || (int64_t)a.nsplit * SPLIT < len) {
     if (split == 0 && threadIdx.x == 0) kerr(a.err, ERR_SEQ_LEN);
-    len = min(min(len, a.max_blocks * a.bs), (int)gridDim.x * SK);
+    len = min(min(len, a.max_blocks * a.bs), a.nsplit * SPLIT);
   }
   const int row = r16 < R ? r16 : 0;
   const int t = row / group, h = kvh * group + row % group;

@@ -39,6 +39,7 @@
 // drain vmcnt before every ds_read, §5 item 4(a)).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../common/quant_block.h"
 #include "gemv_args.h"
@@ -125,7 +126,7 @@ __device__ __forceinline__ uint4 dec8_bf16(uint32_t u, float d, float md, const 
 
 typedef int32_t g8_i32x8 __attribute__((ext_vector_type(8)));
 
-template <int DK>
+template <int DK, int G8S = 0>
 __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   constexpr bool DENSE = DK < 0;          // both operands staged by LDS-DMA (bf16 or fp8)
   constexpr bool FP8 = DK <= G8_FP8;      // 128 k per K-tile, 16x16x128 block-scaled fp8 MFMA
@@ -210,7 +211,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
     }
   };
   // decode half h of k-tile t: this thread's 16 weights = row (wave, r16) of
-  // the half, k 8 g .. 8 g + 7 and 32 + 8 g .. + 7 of the tile
+  // the half, k 8 g .. 8 g + 7 (part 0) and 32 + 8 g .. + 7 (part 1) of the tile
   uint2 cw = make_uint2(0u, 0u);
   uint32_t sd = 0u;
   auto dec_load = [&](int h, int t) {
@@ -221,19 +222,27 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       sd = *(const uint32_t*)(smem + L::SCALES + (c & 1) * 1024 + nl * 4);
     }
   };
-  auto dec_store = [&](int h, int t) {
+  auto dec_vals = [&](int t, int part) -> uint4 {
     if constexpr (!DENSE) {
       const int kh = t & 1;
       const float d = f16_to_f32((uint16_t)(kh ? (sd >> 16) : (sd & 0xffffu)));
       const float md = DK == DK_INT4S ? -136.f * d : 0.f;
       const float2* lut = (const float2*)(smem + (DENSE ? 0 : L::LUT));
-      const uint4 v0 = dec8_bf16<DK>(cw.x, d, md, lut), v1 = dec8_bf16<DK>(cw.y, d, md, lut);
+      return dec8_bf16<DK>(part ? cw.y : cw.x, d, md, lut);
+    }
+    return make_uint4(0u, 0u, 0u, 0u);
+  };
+  auto dec_put = [&](int h, int part, const uint4& v) {
+    if constexpr (!DENSE) {
       const int R = (wave >> 1) * 64 + 32 * h + (wave & 1) * 16 + r16;
       const int sw = (R >> 1) & 7;
-      uint8_t* row = b_img(0) + R * ROWB;
-      *(uint4*)(row + ((g ^ sw) & 7) * 16) = v0;
-      *(uint4*)(row + (((4 + g) ^ sw) & 7) * 16) = v1;
+      *(uint4*)(b_img(0) + R * ROWB + ((((part ? 4 : 0) + g) ^ sw) & 7) * 16) = v;
     }
+  };
+  auto dec_store = [&](int h, int t) {
+    const uint4 v0 = dec_vals(t, 0), v1 = dec_vals(t, 1);
+    dec_put(h, 0, v0);
+    dec_put(h, 1, v1);
   };
 
   // ---- fragment read offsets: image row R + r16, logical chunk 4 s + g at
@@ -292,6 +301,28 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
 #pragma unroll
           for (int mt = 0; mt < 4; mt++)
             acc[nh * 2 + nt][mh * 4 + mt] = mfma16<BF16>(fb[nt][s], f[mt][s], acc[nh * 2 + nt][mh * 4 + mt]);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // the phase's 16 MFMAs with NP decode parts (8 weights each) computed in
+  // their shadow: the decode VALU is placed inside the setprio region (a
+  // scheduling boundary) and interleaved NV per MFMA, so it issues in the
+  // MFMA's vector-issue gaps instead of after the cluster
+  auto mma_dec = [&](const uint4 (&f)[4][2], int mh, int nh, int t, int p0, int np, uint4 (&v)[2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; s++)
+#pragma unroll
+      for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+          acc[nh * 2 + nt][mh * 4 + mt] = mfma16<BF16>(fb[nt][s], f[mt][s], acc[nh * 2 + nt][mh * 4 + mt]);
+    v[0] = dec_vals(t, p0);
+    if (np > 1) v[1] = dec_vals(t, 1);
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, G8S == 1 ? 4 : 2, 0);
     }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -384,6 +415,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       const uint8_t* ai = a_img(u);
       const uint8_t* bi = b_img(u);
       const bool odd = u & 1;
+      uint4 dv[2];
       // phase 0
       read_a(fa0, ai, 0);
       read_b(bi, 0);
@@ -391,7 +423,15 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       barrier();
       wait_lgkm0();
-      mma(fa0, 0, 0);
+      if constexpr (G8S == 2) {                  // second part of B1(u), decoded from phase 3's registers
+        // (unconditional: a computed-but-unstored decode would be sunk into
+        // the branch, out of the MFMA region; u = 0 rewrites tile 0's B1 part
+        // with the prologue's own registers -- the same values)
+        mma_dec(fa0, 0, 0, u, 1, 1, dv);
+        dec_put(1, 1, dv[0]);
+      } else {
+        mma(fa0, 0, 0);
+      }
       barrier();
       // phase 1
       read_a(fa1, ai, 1);
@@ -400,8 +440,15 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       barrier();
       wait_lgkm0();
-      mma(fa1, 1, 0);
-      if (u + 1 < T) dec_store(0, u + 1);
+      if constexpr (G8S == 0) {
+        mma(fa1, 1, 0);
+        if (u + 1 < T) dec_store(0, u + 1);
+      } else {
+        // past the last tile the decode writes a B half nobody reads again
+        mma_dec(fa1, 1, 0, u + 1, 0, G8S == 1 ? 2 : 1, dv);
+        dec_put(0, 0, dv[0]);
+        if (G8S == 1) dec_put(0, 1, dv[1]);
+      }
       barrier();
       // phase 2
       read_b(bi, 1);
@@ -409,7 +456,12 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       barrier();
       wait_lgkm0();
-      mma(fa0, 0, 1);
+      if constexpr (G8S == 2) {                  // second part of B0(u + 1)
+        mma_dec(fa0, 0, 1, u + 1, 1, 1, dv);
+        dec_put(0, 1, dv[0]);
+      } else {
+        mma(fa0, 0, 1);
+      }
       barrier();
       // phase 3
       dec_load(1, u + 1);
@@ -418,8 +470,14 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       barrier();
       wait_lgkm0();
-      mma(fa1, 1, 1);
-      if (u + 1 < T) dec_store(1, u + 1);
+      if constexpr (G8S == 0) {
+        mma(fa1, 1, 1);
+        if (u + 1 < T) dec_store(1, u + 1);
+      } else {
+        mma_dec(fa1, 1, 1, u + 1, 0, G8S == 1 ? 2 : 1, dv);
+        dec_put(1, 0, dv[0]);
+        if (G8S == 1) dec_put(1, 1, dv[1]);
+      }
       barrier();
     }
     if (wr == 0) barrier();                      // close the stagger
@@ -508,8 +566,17 @@ void launch_gemm8p(const G8Args& a, hipStream_t st) {
   if (a.w_fmt == G8_FP8 && a.w_e5m2) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8 - 1>, grid, blk, 0, st, a);
   else if (a.w_fmt == G8_FP8) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8>, grid, blk, 0, st, a);
   else if (a.w_fmt < 0) hipLaunchKernelGGL(g8::gemm8p_kernel<-1>, grid, blk, 0, st, a);
-  else if (fmt_to_dk(a.w_fmt) == DK_INT4S) hipLaunchKernelGGL(g8::gemm8p_kernel<DK_INT4S>, grid, blk, 0, st, a);
-  else hipLaunchKernelGGL(g8::gemm8p_kernel<DK_LUT4>, grid, blk, 0, st, a);
+  else {
+    static const int sched = [] {
+      const char* e = getenv("ILLM_G8_SCHED");
+      return e ? atoi(e) : 0;
+    }();
+    const bool i4 = fmt_to_dk(a.w_fmt) == DK_INT4S;
+    void (*k)(const G8Args) = i4 ? g8::gemm8p_kernel<DK_INT4S, 0> : g8::gemm8p_kernel<DK_LUT4, 0>;
+    if (sched == 1) k = i4 ? g8::gemm8p_kernel<DK_INT4S, 1> : g8::gemm8p_kernel<DK_LUT4, 1>;
+    if (sched == 2) k = i4 ? g8::gemm8p_kernel<DK_INT4S, 2> : g8::gemm8p_kernel<DK_LUT4, 2>;
+    hipLaunchKernelGGL(k, grid, blk, 0, st, a);
+  }
 }
 
 bool gemm8p_supports(int fmt) { return fmt == -1 || fmt_to_dk(fmt) == DK_INT4S || fmt_to_dk(fmt) == DK_LUT4; }

@@ -43,11 +43,16 @@ template <> __device__ __forceinline__ uint16_t from_f32<F16>(float f) { return 
 
 // pack two f32 into one dword of two 16-bit values (lo = a)
 template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b);
+// (one vector conversion: a single v_cvt_pk_bf16_f32 / v_cvt_pkrtz-free
+// v_cvt_f16 pair instead of two scalar converts + shift + or)
+typedef float illm_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 illm_bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 illm_f16x2 __attribute__((ext_vector_type(2)));
 template <> __device__ __forceinline__ uint32_t pack2<BF16>(float a, float b) {
-  return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((illm_f32x2){a, b}, illm_bf16x2));
 }
 template <> __device__ __forceinline__ uint32_t pack2<F16>(float a, float b) {
-  return (uint32_t)f32_to_f16(a) | ((uint32_t)f32_to_f16(b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((illm_f32x2){a, b}, illm_f16x2));
 }
 
 // 16x16x32 MFMA on raw 16-byte fragments

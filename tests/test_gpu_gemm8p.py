@@ -94,3 +94,35 @@ def test_gemm8p_lowbit_glu_epilogue(cuda, qtype, act):
     y = torch.ops.ipex_llm_amd.gemm8p_lowbit(x, blob, f, 2 * I, K, None, False, True, act)
     assert y.shape == (M, I)
     assert _rel(y, ref) < 8e-3
+
+
+_SCHED_CHILD = r"""
+import torch
+from ipex_llm_amd import ops
+from ipex_llm_amd.quantize import get_format
+dev = torch.device("cuda")
+for qt in ("sym_int4", "nf4"):
+    f = get_format(qt).fmt
+    for (M, N, K) in ((256, 256, 128), (300, 520, 384), (1024, 4096, 4096), (3000, 1040, 1024)):
+        torch.manual_seed(M + K)
+        blob = ops.quantize(torch.randn(N, K, device=dev) * 0.05, f)
+        x = torch.randn(M, K, device=dev).bfloat16()
+        wd = torch.ops.ipex_llm_amd.dequantize_device(blob, f, N, K, torch.bfloat16)
+        y = torch.ops.ipex_llm_amd.gemm8p_lowbit(x, blob, f, N, K, None)
+        assert torch.equal(y, torch.ops.ipex_llm_amd.gemm_bf16(x, wd)), (qt, M, N, K)
+        assert torch.equal(y, torch.ops.ipex_llm_amd.gemm8p_lowbit(x, blob, f, N, K, None))
+print("OK")
+"""
+
+
+@pytest.mark.parametrize("sched", ["1", "2"])
+def test_gemm8p_lowbit_decode_schedules_bit_identical(cuda, sched):
+    """the interleaved-decode schedules (ILLM_G8_SCHED, read once per process)
+    produce the same bits as dequantize + the dense kernel"""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, ILLM_G8_SCHED=sched)
+    r = subprocess.run([sys.executable, "-c", _SCHED_CHILD], env=env, capture_output=True, text=True, timeout=240,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
