@@ -140,15 +140,21 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
 
   // ---- block -> (m-block, n-block): XCD remap, then groups of 4 m-blocks
   const int MB = (a.M + 255) / 256, NB = (a.N + 255) / 256;
-  const int total = MB * NB;
-  const int id = mfg::xcd_remap((int)blockIdx.x, total);
+  const int S = DENSE && !FP8 && a.ksplit > 1 ? a.ksplit : 1;
+  const int total = MB * NB * S;
+  // split-K: the S workgroups of one output tile are adjacent ids (one XCD's
+  // L2 serves their shared nothing but keeps the grouping of the tiles intact)
+  const int id0 = mfg::xcd_remap((int)blockIdx.x, total);
+  const int ks = id0 % S, id = id0 / S;
   constexpr int GM = 4;
   const int per_group = GM * NB;
   const int grp = id / per_group, rem = id % per_group;
   const int gm = min(GM, MB - grp * GM);
   const int mb = grp * GM + rem % gm, nb = rem / gm;
   const int m0 = mb * 256, n0 = nb * 256;
-  const int T = FP8 ? a.K / 128 : a.K / 64;
+  const int Tall = FP8 ? a.K / 128 : a.K / 64;
+  const int kt0 = (int)((int64_t)Tall * ks / S);
+  const int T = (int)((int64_t)Tall * (ks + 1) / S) - kt0;   // this workgroup's K-tiles
   constexpr int ES = FP8 ? 1 : 2;         // element bytes
 
   // ---- per-lane LDS-DMA source offsets (bytes; + k-tile via soff) for the
@@ -170,13 +176,13 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   auto a_img = [&](int t) -> uint8_t* { return smem + L::A0 + (t & 1) * L::ASTR; };
   auto b_img = [&](int t) -> uint8_t* { return smem + L::B0 + (t & 1) * L::BSTR; };
   auto stage_a = [&](int h, int t) {          // half-tile A_h of k-tile t -> buffer t & 1
-    const int tt = min(t, T - 1);             // past the end: harmless reload (keeps the vmcnt count)
+    const int tt = kt0 + min(t, T - 1);       // past the end: harmless reload (keeps the vmcnt count)
     const uint8_t* img = a_img(t);
 #pragma unroll
     for (int i = 0; i < 2; i++) dma16(rx, img + ar0[h][i] * ROWB, xo[h][i], tt * 128);
   };
   auto stage_b = [&](int h, int t) {          // dense only
-    const int tt = min(t, T - 1);
+    const int tt = kt0 + min(t, T - 1);
     const uint8_t* img = b_img(t);
 #pragma unroll
     for (int i = 0; i < 2; i++) dma16(rw, img + br0[h][i] * ROWB, wo[h][i], tt * 128);
@@ -485,6 +491,23 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's reloads
 
   // ---- epilogue: lane holds out[m][n .. n + 3], m = m-tile row r16, n = 4 g
+  if (S > 1) {                                 // split-K: f32 partials into the workspace
+#pragma unroll
+    for (int nt = 0; nt < 4; nt++) {
+      const int n = n0 + wc * 64 + nt * 16 + 4 * g;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int mt = 0; mt < 8; mt++) {
+        const int m = m0 + wr * 128 + mt * 16 + r16;
+        if (m >= a.M) continue;
+        float* y = a.ws + (size_t)m * a.N + n;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (n + i < a.N) atomicAdd(y + i, acc[nt][mt][i]);
+      }
+    }
+    return;
+  }
   if (a.glu) {
     // w tiles alternate gate / up every 16 rows (the wave's 64 rows = 2
     // pairs): act(gate) * up in f32, one rounding, out column = pair * 16 + 4 g + i
@@ -560,9 +583,49 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
 
 }  // namespace g8
 
+// split-K epilogue: 4 consecutive outputs per thread (GLU: 4 consecutive
+// outputs of one 16-row gate/up pair), bias, one rounding
+__global__ void __launch_bounds__(256) gemm8p_finish_kernel(const G8Args a) {
+  const int N = a.N, NO = a.glu ? N / 2 : N;
+  const size_t q = (size_t)blockIdx.x * 256 + threadIdx.x;      // group of 4 outputs
+  const int gpr = (NO + 3) / 4;
+  const size_t m = q / gpr;
+  if (m >= (size_t)a.M) return;
+  const int c0 = (int)(q % gpr) * 4;
+  const float* row = a.ws + m * N;
+  uint16_t* y = (uint16_t*)a.out + m * a.ldo;
+  float o[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int c = min(c0 + i, NO - 1);
+    if (a.glu) {
+      const int pr = c / 16, j = c % 16;
+      const float gv = row[pr * 32 + j], uv = row[pr * 32 + 16 + j];
+      o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
+    } else {
+      o[i] = row[c] + (a.bias ? bf16_to_f32(a.bias[c]) : 0.f);
+    }
+  }
+  if (a.out_f32) {
+    float* yf = (float*)a.out + m * a.ldo;
+    for (int i = 0; i < 4 && c0 + i < NO; i++) yf[c0 + i] = o[i];
+  } else if (c0 + 3 < NO && ((a.ldo | c0) & 3) == 0) {
+    *(uint2*)(y + c0) = make_uint2(pack2<BF16>(o[0], o[1]), pack2<BF16>(o[2], o[3]));
+  } else {
+    for (int i = 0; i < 4 && c0 + i < NO; i++) y[c0 + i] = from_f32<BF16>(o[i]);
+  }
+}
+
+void launch_gemm8p_finish(const G8Args& a, hipStream_t st) {
+  const int NO = a.glu ? a.N / 2 : a.N;
+  const size_t groups = (size_t)a.M * ((NO + 3) / 4);
+  hipLaunchKernelGGL(gemm8p_finish_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, a);
+}
+
 void launch_gemm8p(const G8Args& a, hipStream_t st) {
   const int MB = (a.M + 255) / 256, NB = (a.N + 255) / 256;
-  const dim3 grid((unsigned)(MB * NB)), blk(512);
+  const int S = a.w_fmt == -1 && a.ksplit > 1 ? a.ksplit : 1;
+  const dim3 grid((unsigned)(MB * NB * S)), blk(512);
   if (a.w_fmt == G8_FP8 && a.w_e5m2) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8 - 1>, grid, blk, 0, st, a);
   else if (a.w_fmt == G8_FP8) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8>, grid, blk, 0, st, a);
   else if (a.w_fmt < 0) hipLaunchKernelGGL(g8::gemm8p_kernel<-1>, grid, blk, 0, st, a);

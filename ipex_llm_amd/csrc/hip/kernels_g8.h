@@ -22,10 +22,17 @@ struct G8Args {
   const float* sx;
   const float* sw;
   int sw_per_channel, w_e5m2, out_f16;
+  // split-K (dense bf16 only): ksplit > 1 workgroups per output tile, each
+  // over a K-tile range, add f32 partials into ws [M, N] (zeroed by the
+  // caller); launch_gemm8p_finish then applies bias / GLU and rounds
+  int ksplit;
+  float* ws;
 };
 constexpr int G8_FP8 = -2;
 
 void launch_gemm8p(const G8Args& a, hipStream_t st);
+// out = round(ws (+ bias)) or GLU over ws: the split-K epilogue
+void launch_gemm8p_finish(const G8Args& a, hipStream_t st);
 // dense bf16 only, bf16 out, no bias / GLU, K % 128 == 0 (gemm_4w.hip)
 void launch_gemm4w(const G8Args& a, hipStream_t st);
 bool gemm8p_supports(int fmt);

@@ -337,22 +337,46 @@ std::vector<Tensor> x_to_f16_rowscale(const Tensor& x) {
 }  // namespace
 
 // dense bf16 NT GEMM on the 8-phase 256 x 256 kernel (gemm_8p.hip):
+// split-K factor of the dense 8-phase GEMM: a grid of fewer 256 x 256 tiles
+// than CUs (M = 1024: qkv / o / down give 64-96 tiles for 256 CUs) splits K
+// so the launch fills the chip (each split >= 8 K-tiles); full grids keep 1
+static int g8_auto_split(int64_t M, int64_t N, int64_t K) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256), T = K / 64;
+  if (tiles * 2 > cus) return 1;
+  int64_t s = cus / tiles;
+  s = std::min<int64_t>(s, std::min<int64_t>(8, T / 8));
+  return (int)std::max<int64_t>(1, s);
+}
+
 // y[M, N] = x[M, K] @ w[N, K]^T (+ bias), bf16 or f32 out; K % 64 == 0.
+// glu: w rows are 16-row gate/up tile pairs, y [M, N/2] = act(gate) * up.
+// ksplit: -1 auto (g8_auto_split), 1 off, else the split-K factor.
 // kernel = 1: the experimental 4-wave 128 x 128-per-wave kernel
 // (gemm_4w.hip; bf16 out, no bias, K % 128 == 0)
-Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool out_f32, int64_t kernel) {
+Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool out_f32, int64_t kernel,
+                 bool glu, int64_t act, int64_t ksplit) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
               "gemm_bf16: bf16 GPU tensors");
   TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1, "gemm_bf16: w must be [N, K] with unit inner stride");
   const int64_t K = w.size(1), N = w.size(0);
   TORCH_CHECK(x.size(-1) == K && K % 64 == 0 && K > 0, "gemm_bf16: K must match and be a multiple of 64");
+  TORCH_CHECK(!glu || (N % 32 == 0 && !out_f32 && !bias.has_value() && kernel == 0),
+              "gemm_bf16: GLU needs N % 32 == 0, bf16 out, no bias");
   c10::DeviceGuard g(x.device());
   Tensor x2 = x.reshape({-1, K});
   if (x2.stride(1) != 1 || x2.stride(0) % 8 != 0) x2 = x2.contiguous();
   const int64_t M = x2.size(0);
+  const int64_t NO = glu ? N / 2 : N;
   auto shape = x.sizes().vec();
-  shape.back() = N;
-  Tensor out = at::empty({M, N}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  shape.back() = NO;
+  Tensor out = at::empty({M, NO}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   if (M == 0 || N == 0) return out.view(shape);
   TORCH_CHECK(w.stride(0) % 8 == 0, "gemm_bf16: w row stride must be a multiple of 8 elements");
   const int64_t xb = (M - 1) * x2.stride(0) * 2 + K * 2, wb = (N - 1) * w.stride(0) * 2 + K * 2;
@@ -370,17 +394,28 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   a.K = (int)K;
   a.ldx = (int)x2.stride(0);
   a.ldw = (int)w.stride(0);
-  a.ldo = (int)N;
+  a.ldo = (int)NO;
   a.out_f32 = out_f32 ? 1 : 0;
+  a.glu = glu ? 1 : 0;
+  a.act = (int)act;
   a.x_bytes = (uint32_t)xb;
   a.w_bytes = (uint32_t)wb;
   a.w_fmt = -1;
+  const auto st = at::hip::getCurrentHIPStream().stream();
   if (kernel == 1) {
     TORCH_CHECK(!bias.has_value() && !out_f32 && K % 128 == 0, "gemm_bf16(kernel=1): bf16 out, no bias, K % 128 == 0");
-    illm::launch_gemm4w(a, at::hip::getCurrentHIPStream().stream());
-  } else {
-    illm::launch_gemm8p(a, at::hip::getCurrentHIPStream().stream());
+    illm::launch_gemm4w(a, st);
+    return out.view(shape);
   }
+  const int S = ksplit < 0 ? g8_auto_split(M, N, K) : (int)std::max<int64_t>(1, std::min<int64_t>(ksplit, K / 64));
+  Tensor ws;
+  if (S > 1) {
+    ws = at::zeros({M, N}, x.options().dtype(at::kFloat));
+    a.ksplit = S;
+    a.ws = ws.data_ptr<float>();
+  }
+  illm::launch_gemm8p(a, st);
+  if (S > 1) illm::launch_gemm8p_finish(a, st);
   return out.view(shape);
 }
 
@@ -434,7 +469,7 @@ Tensor gemm8p_lowbit(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("mfgemm(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias=None, bool glu=False, int act=0, int tile=-1, int ksplit=0) -> Tensor");
   m.def("x_to_f16_rowscale(Tensor x) -> Tensor[]");
-  m.def("gemm_bf16(Tensor x, Tensor w, Tensor? bias=None, bool out_f32=False, int kernel=0) -> Tensor");
+  m.def("gemm_bf16(Tensor x, Tensor w, Tensor? bias=None, bool out_f32=False, int kernel=0, bool glu=False, int act=0, int ksplit=-1) -> Tensor");
   m.def("gemm8p_lowbit(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias=None, bool out_f32=False, bool glu=False, int act=0) -> Tensor");
   m.def("mfgemm_nn(Tensor g, Tensor w, int fmt, int n, int k, int tile=-1, int ksplit=0) -> Tensor");
   m.def("mfgemm_lora(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias, Tensor la, Tensor lb, float s) -> Tensor[]");

@@ -320,9 +320,9 @@ def _(g, w, fmt, n, k, la, lb, s):
 
 
 @register_fake("ipex_llm_amd::gemm_bf16")
-def _(x, w, bias=None, out_f32=False, kernel=0):
+def _(x, w, bias=None, out_f32=False, kernel=0, glu=False, act=0, ksplit=-1):
     shape = list(x.shape)
-    shape[-1] = w.shape[0]
+    shape[-1] = w.shape[0] // 2 if glu else w.shape[0]
     return x.new_empty(shape, dtype=torch.float32 if out_f32 else x.dtype)
 
 

@@ -169,17 +169,14 @@ def dense_cache_clear() -> None:
 
 def auto_dense_budget(device, cap_gb: float = float("inf")) -> float:
     """Inference default for the prefill shadow (engine construction): an
-    explicit ILLM_PREFILL_DENSE_GB wins; otherwise on a >= 128 GiB device
-    (MI355X: 288 GB HBM3E) up to min(48 GiB, 1/4 of HBM) of dequantized
-    weights stay resident -- a Llama-3-8B INT4 model adds 15 GB next to its
-    4.5 GB of low-bit weights (``cap_gb`` bounds the automatic choice).
-    Returns the budget in GiB."""
+    explicit ILLM_PREFILL_DENSE_GB wins; otherwise 0 -- the model keeps its
+    low-bit footprint only and prefill dequantizes each weight once per GEMM
+    into a transient buffer for the dense 8-phase kernel (``use_g8d``).  A
+    resident shadow (ILLM_PREFILL_DENSE_GB=48 on MI355X: a Llama-3-8B INT4
+    model adds 15 GB next to its 4.5 GB) saves that ~3-4 % dequant pass;
+    ``cap_gb`` bounds an explicit request.  Returns the budget in GiB."""
     env = os.environ.get("ILLM_PREFILL_DENSE_GB")
-    if env is not None:
-        gb = float(env)
-    else:
-        total = torch.cuda.get_device_properties(device).total_memory / 2 ** 30
-        gb = min(48.0, 0.25 * total, cap_gb) if total >= 128 else 0.0
+    gb = min(float(env), cap_gb) if env is not None else 0.0
     if gb * 2 ** 30 > _DENSE_BUDGET:
         set_dense_budget(gb)
     return gb
@@ -265,11 +262,35 @@ def use_g8(x, M: int, n: int, k: int, fmt: int, glu: bool = False) -> bool:
             and hasattr(torch.ops.ipex_llm_amd, "gemm8p_lowbit"))
 
 
+# ---- default prefill path: stream-dequantize + the dense 8-phase GEMM -------
+# The in-LDS-dequant kernel above decodes every weight tile once per 256-row
+# M block (32 times at M = 8192); on gfx950 that decode (~3.5 VALU per weight)
+# competes with the MFMAs for the SIMD's vector issue (an MFMA holds it 8 of
+# its 16 cycles) and the kernel runs at ~0.67x of a dense GEMM
+# (profiles/g8_sched_sweep_r5.jsonl).  Decoding each weight ONCE into a
+# transient bf16 copy (dequantize_device, HBM-bound: ~3-4 % of the GEMM) and
+# running the dense 8-phase kernel (gemm_8p.hip: LDS-DMA, counted vmcnt,
+# split-K for grids smaller than the chip, GLU in the epilogue) keeps the
+# low-bit footprint -- no resident shadow -- and no library GEMM.
+# ILLM_GEMM_G8D=0 falls back to dequantize + hipBLASLt (A/B).
+_G8D = os.environ.get("ILLM_GEMM_G8D", "1") == "1"
+G8D_MIN_M = int(os.environ.get("ILLM_GEMM_G8D_MIN_M", "512"))
+
+
+def use_g8d(x, M: int, n: int, k: int, glu: bool = False) -> bool:
+    return (_G8D and not _USE_LIB and not _USE_FUSED and x.is_cuda and x.dtype == torch.bfloat16
+            and M >= G8D_MIN_M and k % 64 == 0 and (not glu or n % 32 == 0)
+            and hasattr(torch.ops.ipex_llm_amd, "gemm_bf16"))
+
+
 def lowbit_gemm(x, blob, fmt, n, k, bias=None):
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
     if use_g8(x, M, n, k, fmt) and (bias is None or bias.dtype == torch.bfloat16):
         return ops.gemm8p_lowbit(x, blob, fmt, n, k, bias)
+    if use_g8d(x, M, n, k) and (bias is None or bias.dtype == torch.bfloat16):
+        w = _dense_weight(blob, fmt, n, k, x.dtype)
+        return ops.gemm_bf16(x, w, bias)
     if use_engine(M, n, k) and x.dtype in (torch.bfloat16, torch.float16):
         return ops.mfgemm(x, blob, fmt, n, k, bias)
     if use_fused(M, n, k) and hasattr(ops, "gemm"):
@@ -286,6 +307,9 @@ def lowbit_gemm_glu(x, blob, fmt, n, k, act: int = 0):
     M = x.numel() // k
     if use_g8(x, M, n, k, fmt, glu=True):
         return ops.gemm8p_lowbit(x, blob, fmt, n, k, None, False, True, act)
+    if use_g8d(x, M, n, k, glu=True) and act in (0, 1):
+        w = _dense_weight(blob, fmt, n, k, x.dtype)
+        return ops.gemm_bf16(x, w, None, False, 0, True, act)
     if use_engine(M, n, k, glu=True) and x.dtype in (torch.bfloat16, torch.float16):
         return ops.mfgemm(x, blob, fmt, n, k, None, True, act)
     if use_fused(M, n, k) and hasattr(ops, "gemm_glu"):

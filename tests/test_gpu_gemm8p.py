@@ -126,3 +126,40 @@ def test_gemm8p_lowbit_decode_schedules_bit_identical(cuda, sched):
     r = subprocess.run([sys.executable, "-c", _SCHED_CHILD], env=env, capture_output=True, text=True, timeout=240,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("M,N,K,S", [(1024, 4096, 4096, -1), (1024, 6144, 4096, 2), (300, 520, 1024, 3),
+                                     (700, 4096, 14336, 4), (64, 256, 512, 8)])
+def test_gemm_bf16_split_k_matches_fp32(cuda, M, N, K, S):
+    """split-K (f32 partials into a zeroed workspace + the finishing launch):
+    auto and forced factors, ragged shapes, bias"""
+    torch.manual_seed(M + S)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    ref = x.float() @ w.float().t() + b.float()
+    y = torch.ops.ipex_llm_amd.gemm_bf16(x, w, b, False, 0, False, 0, S)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert _rel(y, ref) < 8e-3, (M, N, K, S)
+    y1 = torch.ops.ipex_llm_amd.gemm_bf16(x, w, b, False, 0, False, 0, 1)
+    assert _rel(y, y1) < 8e-3
+
+
+@pytest.mark.parametrize("S", [1, 4])
+@pytest.mark.parametrize("act", [0, 1])
+def test_gemm_bf16_glu_epilogue(cuda, S, act):
+    """dense 8-phase GLU: 16-row gate/up tile pairs, act(gate) * up in the
+    epilogue (S = 1) or in the split-K finishing launch (S = 4)"""
+    import torch.nn.functional as F
+    from ipex_llm_amd.models.decoder import interleave_glu_rows
+    torch.manual_seed(3 + act)
+    M, I, K = 1024, 1024, 2048
+    wg, wu = torch.randn(I, K, device=cuda) * 0.05, torch.randn(I, K, device=cuda) * 0.05
+    w = interleave_glu_rows(wg, wu).bfloat16()
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    hg = (x.float() @ w.float().t()).view(M, I // 16, 2, 16)
+    g_, u_ = hg[:, :, 0].reshape(M, I), hg[:, :, 1].reshape(M, I)
+    ref = (F.silu(g_) if act == 0 else F.gelu(g_, approximate="tanh")) * u_
+    y = torch.ops.ipex_llm_amd.gemm_bf16(x, w, None, False, 0, True, act, S)
+    assert y.shape == (M, I)
+    assert _rel(y, ref) < 8e-3

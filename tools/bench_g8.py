@@ -69,8 +69,16 @@ def main():
                        "vs_dequant_hipblaslt": round(deq / ours, 3), "rel_vs_fp32": round(rel, 6)}
                 if args.dense:
                     dn = timed(lambda: tops.gemm_bf16(x, wd, None))
+                    dn1 = timed(lambda: tops.gemm_bf16(x, wd, None, False, 0, False, 0, 1))
+                    g8d = timed(lambda: tops.gemm_bf16(x, tops.dequantize_device(blob, f, n, k, torch.bfloat16)))
                     rec["dense8p_us"] = round(dn, 1)
+                    rec["dense8p_nosplit_us"] = round(dn1, 1)
                     rec["dense8p_vs_hipblaslt"] = round(lib / dn, 3)
+                    rec["g8d_us"] = round(g8d, 1)
+                    rec["g8d_vs_dequant_hipblaslt"] = round(deq / g8d, 3)
+                    rec["g8d_vs_hipblaslt_dense"] = round(lib / g8d, 3)
+                    yd = tops.gemm_bf16(x, wd, None).float()
+                    rec["dense8p_rel_vs_fp32"] = round(((yd - y2).norm() / y2.norm()).item(), 6)
                 print(json.dumps(rec), flush=True)
                 del w, blob, wd, x, y1, y2
     torch.cuda.synchronize()

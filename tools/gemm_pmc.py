@@ -1,6 +1,8 @@
 """Run one prefill low-bit GEMM shape in a loop (for rocprofv3 --pmc passes).
 
-usage: python tools/gemm_pmc.py [op] [M] [iters]   op in qkv|o|gate_up|down
+usage: python tools/gemm_pmc.py [op] [M] [iters] [impl]   op in qkv|o|gate_up|down
+  impl: fused (ops.gemm, default) | g8 (8-phase low-bit) | g8dense (8-phase on
+  the dequantized weight)
 """
 import os
 import sys
@@ -24,8 +26,16 @@ def main():
     dev = torch.device("cuda")
     b = ops.quantize(torch.randn(n, k, device=dev, dtype=torch.bfloat16) * 0.02, f)
     x = torch.randn(M, k, device=dev, dtype=torch.bfloat16)
+    impl = sys.argv[4] if len(sys.argv) > 4 else "fused"
+    P = torch.ops.ipex_llm_amd
+    wd = P.dequantize_device(b, f, n, k, torch.bfloat16) if impl == "g8dense" else None
     for _ in range(iters):
-        torch.ops.ipex_llm_amd.gemm(x, b, f, n, k, None)
+        if impl == "g8":
+            P.gemm8p_lowbit(x, b, f, n, k, None)
+        elif impl == "g8dense":
+            P.gemm_bf16(x, wd)
+        else:
+            P.gemm(x, b, f, n, k, None)
     torch.cuda.synchronize()
     print("done", op, M, iters)
 
