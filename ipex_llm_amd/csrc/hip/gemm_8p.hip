@@ -333,7 +333,65 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  if constexpr (DENSE) {
+  // (G8S == 3, dense) the phase's 16 MFMAs with its two LDS-DMA pieces
+  // issued after the first 8: the DMA issue (~60-185 cycles a piece inside
+  // a read-heavy phase, MI355X_MICROARCH.md) moves out of the read segment
+  // into the MFMA segment; the wait before the barrier keeps 3 half-tiles in
+  // flight (vmcnt(6)) and so retires the same half-tile as vmcnt(8) after
+  // the issue did
+  auto mma_st = [&](const uint4 (&f)[4][2], int mh, int nh, auto&& stage) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+#pragma unroll
+      for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+          acc[nh * 2 + nt][mh * 4 + mt] = mfma16<BF16>(fb[nt][s], f[mt][s], acc[nh * 2 + nt][mh * 4 + mt]);
+      if (s == 0) stage();
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if constexpr (DENSE && !FP8 && G8S == 3) {
+    stage_a(0, 0);
+    stage_b(0, 0);
+    stage_a(1, 0);
+    stage_b(1, 0);
+    stage_a(0, 1);
+    stage_b(0, 1);
+    wait_vm8();                                  // A0(0), B0(0) landed
+    barrier();
+    if (wr == 1) barrier();
+    for (int u = 0; u < T; u++) {
+      const uint8_t* ai = a_img(u);
+      const uint8_t* bi = b_img(u);
+      read_a(fa0, ai, 0);
+      read_b(bi, 0);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      barrier();
+      wait_lgkm0();
+      mma_st(fa0, 0, 0, [&] { stage_a(1, u + 1); });
+      barrier();
+      read_a(fa1, ai, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      barrier();
+      wait_lgkm0();
+      mma_st(fa1, 1, 0, [&] { stage_b(1, u + 1); });
+      barrier();
+      read_b(bi, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      barrier();
+      wait_lgkm0();
+      mma_st(fa0, 0, 1, [&] { stage_a(0, u + 2); });
+      barrier();
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      barrier();
+      mma_st(fa1, 1, 1, [&] { stage_b(0, u + 2); });
+      barrier();
+    }
+    if (wr == 0) barrier();
+  } else if constexpr (DENSE) {
     // ---- prologue: tile 0 complete, tile 1's A0 / B0 in flight
     stage_a(0, 0);
     stage_b(0, 0);
@@ -628,7 +686,14 @@ void launch_gemm8p(const G8Args& a, hipStream_t st) {
   const dim3 grid((unsigned)(MB * NB * S)), blk(512);
   if (a.w_fmt == G8_FP8 && a.w_e5m2) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8 - 1>, grid, blk, 0, st, a);
   else if (a.w_fmt == G8_FP8) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8>, grid, blk, 0, st, a);
-  else if (a.w_fmt < 0) hipLaunchKernelGGL(g8::gemm8p_kernel<-1>, grid, blk, 0, st, a);
+  else if (a.w_fmt < 0) {
+    static const int dsched = [] {
+      const char* e = getenv("ILLM_G8_DSCHED");
+      return e ? atoi(e) : 0;
+    }();
+    if (dsched == 3) hipLaunchKernelGGL((g8::gemm8p_kernel<-1, 3>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((g8::gemm8p_kernel<-1, 0>), grid, blk, 0, st, a);
+  }
   else {
     static const int sched = [] {
       const char* e = getenv("ILLM_G8_SCHED");

@@ -281,8 +281,9 @@ void launch_glu(bool bf16, const uint16_t* gu, int ld, uint16_t* out, int M, int
                 hipStream_t st);
 void launch_quantize_device(int fmt, int in_kind, const void* w, int64_t n, int64_t k,
                             uint8_t* blob, int search, hipStream_t st);
+// transpose: out is [k, n] (n % 8 == 0) instead of [n, k]
 void launch_dequantize_device(bool bf16, int fmt, const uint8_t* blob, int64_t n, int64_t k,
-                              uint16_t* out, hipStream_t st);
+                              uint16_t* out, hipStream_t st, bool transpose = false);
 void launch_reduce_partials(bool bf16, const float* ws, int nsplit, const uint16_t* bias,
                             uint16_t* out, int M, int N, int ldo, hipStream_t st);
 void launch_moe_topk(const float* logits, int T, int E, int k, int renorm, int scoring,

@@ -149,7 +149,7 @@ constexpr int DQ_CH = 4;                                  // chunks per workgrou
 constexpr int DQ_LD = DQ_CH * CHUNK_K + 8;                // LDS row stride (elements)
 template <typename T, int FMT>
 __global__ void __launch_bounds__(256) dequantize_tiled_kernel(const uint8_t* blob, int64_t n, int64_t k,
-                                                               uint16_t* out) {
+                                                               uint16_t* out, bool tr) {
   constexpr int fmt = FMT;
   constexpr int bits = fmt_bits(fmt);
   __shared__ __attribute__((aligned(16))) uint16_t rows[TILE_N * DQ_LD];
@@ -194,6 +194,23 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(const uint8_t* bl
   __syncthreads();
   // row segment [cg * 512, cg * 512 + 512) of rows t * 16 .. + 15: 64 x 16-B pieces per row
   const int64_t k0 = cg * DQ_CH * CHUNK_K;
+  if (tr) {
+    // transposed [k, n] output (the W^T operand of a grad_x = g W GEMM):
+    // per k, the tile's 16 rows are two 16-B pieces (n % 8 == 0, host-checked)
+#pragma unroll
+    for (int j = 0; j < DQ_CH * CHUNK_K * 2 / 256; j++) {
+      const int v = tid + 256 * j;
+      const int kk = v >> 1, h = v & 1;
+      const int64_t kg = k0 + kk, n0 = t * TILE_N + h * 8;
+      if (kg >= k || n0 + 8 > n) continue;
+      uint32_t pk[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        pk[i] = (uint32_t)rows[(h * 8 + 2 * i) * DQ_LD + kk] | ((uint32_t)rows[(h * 8 + 2 * i + 1) * DQ_LD + kk] << 16);
+      *(uint4*)(out + (size_t)kg * n + n0) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TILE_N * DQ_CH * CHUNK_K / 8 / 256; j++) {
     const int v = tid + 256 * j;
@@ -204,14 +221,14 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(const uint8_t* bl
 }
 
 void launch_dequantize_device(bool bf16, int fmt, const uint8_t* blob, int64_t n, int64_t k,
-                              uint16_t* out, hipStream_t st) {
+                              uint16_t* out, hipStream_t st, bool transpose) {
   const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
   const int64_t nblk = (pad_to(n, TILE_N) / TILE_N) * ((KC + DQ_CH - 1) / DQ_CH);
   dim3 grid((unsigned)nblk);
 #define DQ_CASE(F)                                                                                       \
   case F:                                                                                                \
-    if (bf16) hipLaunchKernelGGL((dequantize_tiled_kernel<BF16, F>), grid, dim3(256), 0, st, blob, n, k, out); \
-    else hipLaunchKernelGGL((dequantize_tiled_kernel<F16, F>), grid, dim3(256), 0, st, blob, n, k, out);     \
+    if (bf16) hipLaunchKernelGGL((dequantize_tiled_kernel<BF16, F>), grid, dim3(256), 0, st, blob, n, k, out, transpose); \
+    else hipLaunchKernelGGL((dequantize_tiled_kernel<F16, F>), grid, dim3(256), 0, st, blob, n, k, out, transpose);     \
     break;
   switch (fmt) {
     DQ_CASE(FMT_SYM_INT4) DQ_CASE(FMT_ASYM_INT4) DQ_CASE(FMT_NF4) DQ_CASE(FMT_FP4) DQ_CASE(FMT_SYM_INT8)

@@ -141,7 +141,7 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("to_fp8_bytes(Tensor x, bool e5m2) -> Tensor");
   // device kernels (ops_hip.cpp)
   m.def("quantize_device(Tensor w, int fmt, bool scale_search) -> Tensor");
-  m.def("dequantize_device(Tensor blob, int fmt, int n, int k, ScalarType dtype) -> Tensor");
+  m.def("dequantize_device(Tensor blob, int fmt, int n, int k, ScalarType dtype, bool transpose=False) -> Tensor");
   m.def("gemv(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias, int epi, int ksplit, int act) -> Tensor");
   m.def("add_rms_norm(Tensor? x, Tensor(b!)? partials, Tensor(a!)? residual, Tensor w, float eps, bool unit_offset, bool store_residual, bool zero_partials=False) -> Tensor");
   m.def("rms_norm_bwd(Tensor x, Tensor g, Tensor w, float eps, bool unit_offset) -> Tensor");

@@ -51,12 +51,14 @@ Tensor quantize_device(const Tensor& w, int64_t fmt, bool scale_search) {
   return blob;
 }
 
-Tensor dequantize_device(const Tensor& blob, int64_t fmt, int64_t n, int64_t k, at::ScalarType dt) {
+// transpose: W^T [k, n] (the operand of grad_x = g W on the NT GEMM)
+Tensor dequantize_device(const Tensor& blob, int64_t fmt, int64_t n, int64_t k, at::ScalarType dt, bool transpose) {
   TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "dequantize_device: bf16/fp16 output");
+  TORCH_CHECK(!transpose || n % 8 == 0, "dequantize_device: transposed output needs n % 8 == 0");
   c10::DeviceGuard g(blob.device());
-  Tensor out = at::empty({n, k}, blob.options().dtype(dt));
+  Tensor out = transpose ? at::empty({k, n}, blob.options().dtype(dt)) : at::empty({n, k}, blob.options().dtype(dt));
   illm::launch_dequantize_device(dt == at::kBFloat16, (int)fmt, blob.data_ptr<uint8_t>(), n, k,
-                                 m16(out), cur_stream());
+                                 m16(out), cur_stream(), transpose);
   return out;
 }
 

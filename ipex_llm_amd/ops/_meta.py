@@ -14,8 +14,8 @@ def _(w, fmt, scale_search):
 
 
 @register_fake("ipex_llm_amd::dequantize_device")
-def _(blob, fmt, n, k, dtype):
-    return blob.new_empty((n, k), dtype=dtype)
+def _(blob, fmt, n, k, dtype, transpose=False):
+    return blob.new_empty((k, n) if transpose else (n, k), dtype=dtype)
 
 
 @register_fake("ipex_llm_amd::gemv")

@@ -8,13 +8,16 @@ Llama-3's 128 K vocabulary that is a 2 GB f32 tensor per 4 K-token step and
 three full passes over it.
 
 MI355X design: the tokens are processed in chunks; per chunk the logits are
-one bf16 GEMM (the library GEMM: it measured faster than our engine and
-8-phase kernels on this shape, profiles/qlora_llama3_8b_r4_*), ``ce_fused_``
+one bf16 GEMM on the dense 8-phase kernel (gemm_8p.hip; ILLM_CE_LIB=1: the
+library GEMM), ``ce_fused_``
 turns them into the per-row loss and, IN PLACE, the logits gradient
 (softmax - onehot) in one read for the row statistics and one read + write
 for the gradient, and the hidden-state gradient is the second GEMM
 (dlogits @ W) of that chunk -- computed during the forward, since the only
-consumer of the loss is a scalar backward.  Nothing of size [tokens, vocab]
+consumer of the loss is a scalar backward.  That second GEMM reduces over
+the vocabulary: on the NT 8-phase kernel its operand is W^T, a transposed copy
+of the frozen head kept for the head's lifetime (1 GB for Llama-3-8B; the
+kernel's split-K fills the chip at 2048-row chunks).  Nothing of size [tokens, vocab]
 outlives a chunk; backward is one scale of the stored [tokens, hidden]
 gradient.  The lm_head weight is frozen here (QLoRA); a trainable head
 falls back to the unfused path.
@@ -27,6 +30,24 @@ from typing import Optional
 import torch
 
 CHUNK = int(os.environ.get("ILLM_CE_CHUNK", "2048"))
+_LIB = os.environ.get("ILLM_CE_LIB", "0") == "1"
+_wt_cache = {}     # id(weight) -> (weakref to weight, version, W^T)
+
+
+def _g8_ok(h, w) -> bool:
+    from .. import ops
+    return (not _LIB and h.is_cuda and ops.native_gpu(h) and h.dtype == torch.bfloat16 and w.dtype == h.dtype
+            and h.shape[1] % 64 == 0 and w.shape[0] % 64 == 0 and hasattr(torch.ops.ipex_llm_amd, "gemm_bf16"))
+
+
+def _transposed(w):
+    import weakref
+    ent = _wt_cache.get(id(w))
+    if ent is not None and ent[0]() is w and ent[1] == w._version:
+        return ent[2]
+    wt = w.t().contiguous()
+    _wt_cache[id(w)] = (weakref.ref(w, lambda r, k=id(w): _wt_cache.pop(k, None)), w._version, wt)
+    return wt
 
 
 class _FusedLinearCE(torch.autograd.Function):
@@ -38,12 +59,17 @@ class _FusedLinearCE(torch.autograd.Function):
         V = weight.shape[0]
         loss_rows = torch.empty(T, device=h.device, dtype=torch.float32)
         grad_h = torch.empty_like(h) if h.requires_grad else None
+        g8 = _g8_ok(h, w)
+        wt = _transposed(w) if g8 and grad_h is not None else None
         for c0 in range(0, T, CHUNK):
             c1 = min(T, c0 + CHUNK)
-            logits = torch.mm(h[c0:c1], w.t())
+            logits = ops.gemm_bf16(h[c0:c1], w) if g8 else torch.mm(h[c0:c1], w.t())
             loss_rows[c0:c1] = ops.ce_fused_(logits, labels[c0:c1], ignore_index, 1.0 if grad_h is not None else 0.0)
             if grad_h is not None:
-                torch.mm(logits, w, out=grad_h[c0:c1])
+                if g8:
+                    grad_h[c0:c1] = ops.gemm_bf16(logits, wt)
+                else:
+                    torch.mm(logits, w, out=grad_h[c0:c1])
             del logits
         if denom is None:
             n_valid = (labels != ignore_index).sum().clamp_(min=1).to(torch.float32)

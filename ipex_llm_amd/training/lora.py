@@ -154,6 +154,52 @@ _GXA_SLICES = os.environ.get("ILLM_LORA_GXA_SLICES", "1") == "1"
 _TN_KERNEL = os.environ.get("ILLM_LORA_TN_KERNEL", "1") == "1"
 
 
+def _skinny(x2: torch.Tensor, W: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
+    """alpha * x2 @ W^T for a rank-r factor W [r, K] (x2 [M, K] -> [M, r]):
+    the LoRA down-projections x A^T and g B.  On the streaming skinny GEMM
+    (csrc/hip/dense_gemv.hip, <= 16 rows per launch) with the roles swapped
+    -- the r factor rows are the "activations", the M token rows the
+    "weight" streamed once -- instead of a library GEMM on a 16 x 16 macro
+    tile; the library GEMM elsewhere"""
+    from .. import ops
+    r, K = W.shape
+    if (_SKINNY and x2.is_cuda and ops.native_gpu(x2) and x2.dtype in (torch.bfloat16, torch.float16)
+            and W.dtype == x2.dtype and x2.is_contiguous() and K % 8 == 0 and r <= 64
+            and x2.shape[0] >= 64):
+        Wc = (W * alpha if alpha != 1.0 else W).contiguous()
+        dl = torch.ops.ipex_llm_amd.dense_linear
+        if r <= 16:
+            return dl(Wc, x2, None).t().contiguous()
+        out = x2.new_empty(x2.shape[0], r)
+        for c0 in range(0, r, 16):
+            out[:, c0:c0 + 16] = dl(Wc[c0:c0 + 16], x2, None).t()
+        return out
+    if alpha == 1.0:
+        return torch.mm(x2, W.t())
+    return torch.addmm(x2.new_empty(()), x2, W.t(), beta=0, alpha=alpha)
+
+
+# ILLM_LORA_SKINNY=0: the rank-r down-projections on the library GEMM (A/B)
+_SKINNY = os.environ.get("ILLM_LORA_SKINNY", "1") == "1"
+
+
+def _g8_bwd_ok(g2: torch.Tensor, base) -> bool:
+    """grad_x = g W on the dense 8-phase GEMM over W^T dequantized straight
+    from the blob (no resident shadow budget: the shadow paths below own it)"""
+    from .. import ops
+    from ..ops.gemm import _DENSE_BUDGET, use_g8d
+    N = base.out_features
+    return (_DENSE_BUDGET <= 0 and base.weight.is_cuda and ops.native_gpu(base.weight)
+            and getattr(base, "g_idx_map", None) is None and N % 64 == 0
+            and use_g8d(g2, g2.shape[0], base.in_features, N))
+
+
+def _g8_grad_x(g2: torch.Tensor, base) -> torch.Tensor:
+    wt = torch.ops.ipex_llm_amd.dequantize_device(base.weight, base.fmt, base.out_features, base.in_features,
+                                                   g2.dtype, True)          # W^T [K, N]
+    return torch.ops.ipex_llm_amd.gemm_bf16(g2, wt)
+
+
 def _base_dense_weight(base, dt):
     """the frozen base weight as the backward GEMM operand: the resident dense
     shadow / a transient dequant on the GPU (as MatMulLowBit), dequant on CPU"""
@@ -182,7 +228,7 @@ class _LoraLowBitFn(torch.autograd.Function):
             bias = bias.to(x2.dtype)
         with torch.no_grad():
             y = ops.lowbit_matmul(x2, base.weight, base.fmt, base.out_features, base.in_features, bias)
-            xa = torch.mm(x2, A.t())
+            xa = _skinny(x2, A)
             _rank_update_(y, xa, B, s)
         ctx.save_for_backward(x2, xa, A, B)
         ctx.base, ctx.s, ctx.shp = base, s, shp
@@ -195,8 +241,7 @@ class _LoraLowBitFn(torch.autograd.Function):
         s = ctx.s
         # the LoRA scale rides on the GEMMs' alpha (beta = 0: the 1-element
         # input is never read) instead of separate [M, r] / [N, r] scale launches
-        z = g2.new_empty(())                               # (no fill launch)
-        gxa = torch.addmm(z, g2, B, beta=0, alpha=s)      # [M, r]
+        gxa = _skinny(g2, B.t(), s)                       # s g B [M, r]
         jobs = ([(gxa, x2, 1.0, False)] if ctx.needs_input_grad[1] else []) + \
             ([(xa, g2, s, True)] if ctx.needs_input_grad[2] else [])
         res = _tn_many(jobs, A.dtype)
@@ -205,7 +250,9 @@ class _LoraLowBitFn(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             base = ctx.base
-            if _engine_nn_ok(base, g2):
+            if _g8_bwd_ok(g2, base):
+                gx = _g8_grad_x(g2, base)
+            elif _engine_nn_ok(base, g2):
                 # g W straight from the low-bit blob (transposed LDS reads in the
                 # engine GEMM, csrc/hip/gemm_mfma_nn.hip): no dense W
                 gx = torch.ops.ipex_llm_amd.mfgemm_nn(g2, base.weight, base.fmt, base.out_features,
@@ -382,7 +429,7 @@ class _LoraGroupFn(torch.autograd.Function):
                 ctx.save_for_backward(x2, xa_all, *AB)
                 ctx.s, ctx.shp, ctx.bases, ctx.kcat = s, shp, bases, (R, x2.dtype)
                 return tuple(ys)
-            xa_all = torch.mm(x2, torch.cat(As, 0).t())          # [M, sum r]
+            xa_all = _skinny(x2, torch.cat(As, 0))              # [M, sum r]
             ys, off = [], 0
             for base, A, B in zip(bases, As, Bs):
                 r = A.shape[0]
@@ -402,7 +449,6 @@ class _LoraGroupFn(torch.autograd.Function):
         x2, xa_all, *AB = ctx.saved_tensors
         As, Bs = AB[0::2], AB[1::2]
         s = ctx.s
-        z = x2.new_empty(())
         jobs, gx, off = [], None, 0
         # every sibling's s g B lands in its column slice of one [M, sum r]
         # buffer (strided GEMM output: no concatenation pass)
@@ -416,15 +462,19 @@ class _LoraGroupFn(torch.autograd.Function):
                 continue
             g2 = g.reshape(-1, g.shape[-1]).to(x2.dtype)
             if _GXA_SLICES:
-                torch.addmm(z, g2, B, beta=0, alpha=s, out=gxa_all[:, off:off + r])
+                gxa_all[:, off:off + r] = _skinny(g2, B.t(), s)
             else:
-                gxas.append(torch.addmm(z, g2, B, beta=0, alpha=s))
+                gxas.append(_skinny(g2, B.t(), s))
             # dB [N, r] (the K-concat forward saved s x A^T: alpha 1)
             jobs.append((xa_all[:, off:off + r], g2, 1.0 if ctx.kcat else s, True))
             if ctx.needs_input_grad[0]:
-                w = (_aug_weight(base, ctx.kcat[0], off, ctx.kcat[1])[:, :base.in_features] if ctx.kcat
-                     else _base_dense_weight(base, x2.dtype))
-                gx = torch.mm(g2, w) if gx is None else gx.addmm_(g2, w)
+                if not ctx.kcat and _g8_bwd_ok(g2, base):
+                    gi = _g8_grad_x(g2, base)
+                    gx = gi if gx is None else gx.add_(gi)
+                else:
+                    w = (_aug_weight(base, ctx.kcat[0], off, ctx.kcat[1])[:, :base.in_features] if ctx.kcat
+                         else _base_dense_weight(base, x2.dtype))
+                    gx = torch.mm(g2, w) if gx is None else gx.addmm_(g2, w)
             off += r
         if not _GXA_SLICES:
             gxa_all = torch.cat(gxas, 1)

@@ -70,7 +70,7 @@ def test_gemm8p_lowbit_matches_dequant_fp32(cuda, qtype, M, N, K):
     assert _rel(y, ref) < 6e-3, (qtype, M, N, K)
     # bit-identical to dequantize-to-bf16 + the dense kernel (same bf16 weights, same order)
     wd = torch.ops.ipex_llm_amd.dequantize_device(blob, f, N, K, torch.bfloat16)
-    assert torch.equal(y, torch.ops.ipex_llm_amd.gemm_bf16(x, wd, b))
+    assert torch.equal(y, torch.ops.ipex_llm_amd.gemm_bf16(x, wd, b, False, 0, False, 0, 1))   # (no split-K)
 
 
 @pytest.mark.parametrize("qtype", ["sym_int4", "nf4"])
@@ -109,20 +109,21 @@ for qt in ("sym_int4", "nf4"):
         x = torch.randn(M, K, device=dev).bfloat16()
         wd = torch.ops.ipex_llm_amd.dequantize_device(blob, f, N, K, torch.bfloat16)
         y = torch.ops.ipex_llm_amd.gemm8p_lowbit(x, blob, f, N, K, None)
-        assert torch.equal(y, torch.ops.ipex_llm_amd.gemm_bf16(x, wd)), (qt, M, N, K)
+        assert torch.equal(y, torch.ops.ipex_llm_amd.gemm_bf16(x, wd, None, False, 0, False, 0, 1)), (qt, M, N, K)
         assert torch.equal(y, torch.ops.ipex_llm_amd.gemm8p_lowbit(x, blob, f, N, K, None))
 print("OK")
 """
 
 
-@pytest.mark.parametrize("sched", ["1", "2"])
-def test_gemm8p_lowbit_decode_schedules_bit_identical(cuda, sched):
-    """the interleaved-decode schedules (ILLM_G8_SCHED, read once per process)
-    produce the same bits as dequantize + the dense kernel"""
+@pytest.mark.parametrize("var,val", [("ILLM_G8_SCHED", "1"), ("ILLM_G8_SCHED", "2"), ("ILLM_G8_DSCHED", "3")])
+def test_gemm8p_lowbit_decode_schedules_bit_identical(cuda, var, val):
+    """the interleaved-decode schedules (ILLM_G8_SCHED) and the dense
+    DMA-in-cluster schedule (ILLM_G8_DSCHED), read once per process: the
+    low-bit kernel == dequantize + the dense kernel, bit for bit"""
     import os
     import subprocess
     import sys
-    env = dict(os.environ, ILLM_G8_SCHED=sched)
+    env = dict(os.environ, **{var: val})
     r = subprocess.run([sys.executable, "-c", _SCHED_CHILD], env=env, capture_output=True, text=True, timeout=240,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

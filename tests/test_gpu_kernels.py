@@ -670,6 +670,20 @@ def test_dequantize_device_kernel(cuda, name, n, k):
         assert torch.allclose(got.float().cpu(), ref.to(dt).float(), atol=1e-3, rtol=1e-2), (name, dt)
 
 
+@pytest.mark.parametrize("name", ["sym_int4", "nf4", "sym_int8", "fp8_e4m3"])
+@pytest.mark.parametrize("n,k", [(64, 384), (48, 640), (4096, 1024)])
+def test_dequantize_device_transposed(cuda, name, n, k):
+    """W^T [k, n] straight from the blob (the grad_x GEMM operand) == the
+    row-major dequant transposed, bit for bit"""
+    f = get_format(name).fmt
+    torch.manual_seed(3)
+    blob = ops.quantize(torch.randn(n, k, device=cuda) * 0.05, f)
+    for dt in (torch.bfloat16, torch.float16):
+        w = torch.ops.ipex_llm_amd.dequantize_device(blob, f, n, k, dt)
+        wt = torch.ops.ipex_llm_amd.dequantize_device(blob, f, n, k, dt, True)
+        assert wt.shape == (k, n) and torch.equal(wt, w.t())
+
+
 def test_decode_oproj_combine_with_deferred_norm(cuda):
     """attention partials merged in the o_proj GEMV prologue (opt-in) on top of
     the deferred norm and the GEMV-epilogue RoPE: same greedy tokens as the

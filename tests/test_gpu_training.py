@@ -274,3 +274,32 @@ def test_lora_kcat_rows_grad_x_matches(cuda, monkeypatch):
     finally:
         G.set_dense_budget(old / 2 ** 30)
         L._aug_cache.clear()
+
+
+@pytest.mark.parametrize("qtype", ["nf4", "sym_int4"])
+def test_qlora_native_backward_pieces_match_fp32(cuda, qtype):
+    """the shadow-free QLoRA backward: grad_x = g W on the dense 8-phase GEMM
+    over W^T dequantized from the blob, and the rank-r down-projections
+    (x A^T, s g B, r = 8 and 24) on the swapped-role skinny GEMM, vs fp32"""
+    import ipex_llm_amd.training.lora as L
+    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
+    torch.manual_seed(7)
+    base = LowBitLinear.from_linear(torch.nn.Linear(1024, 768, bias=False), qtype).to(cuda)
+    g2 = torch.randn(1024, 768, device=cuda).bfloat16()
+    assert L._g8_bwd_ok(g2, base)
+    W = torch.ops.ipex_llm_amd.dequantize_device(base.weight, base.fmt, 768, 1024, torch.bfloat16).float()
+    gx = L._g8_grad_x(g2, base)
+    ref = g2.float() @ W
+    assert gx.shape == (1024, 1024)
+    assert ((gx.float() - ref).norm() / ref.norm()).item() < 8e-3
+    x2 = torch.randn(1024, 1024, device=cuda).bfloat16()
+    for r in (8, 24):
+        A = (torch.randn(r, 1024, device=cuda) * 0.05).bfloat16()
+        xa = L._skinny(x2, A)
+        assert xa.shape == (1024, r) and xa.is_contiguous()
+        ra = x2.float() @ A.float().t()
+        assert ((xa.float() - ra).norm() / ra.norm()).item() < 8e-3
+        B = (torch.randn(768, r, device=cuda) * 0.05).bfloat16()
+        gxa = L._skinny(g2, B.t(), 2.0)
+        rb = 2.0 * (g2.float() @ B.float())
+        assert ((gxa.float() - rb).norm() / rb.norm()).item() < 8e-3

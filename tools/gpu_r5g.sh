@@ -4,10 +4,12 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
-timeout -k 10 120 python -u -m pytest tests/test_gpu_gemm8p.py -q -x --timeout 100 --timeout-method thread > gpurun_out/r5g_g8tests.log 2>&1 || { tail -30 gpurun_out/r5g_g8tests.log; exit 2; }
+timeout -k 10 180 python -u -m pytest tests/test_gpu_gemm8p.py tests/test_gpu_kernels.py tests/test_gpu_training.py -k 'gemm or dequantize_device or lora or qlora' -q -x --timeout 100 --timeout-method thread > gpurun_out/r5g_g8tests.log 2>&1 || { tail -30 gpurun_out/r5g_g8tests.log; exit 2; }
 tail -2 gpurun_out/r5g_g8tests.log
 timeout -k 10 300 python -u tools/bench_g8.py sym_int4 --m 8192,1024 --dense > gpurun_out/r5g_g8d.jsonl 2> gpurun_out/r5g_g8d.err || exit 3
 echo "g8d bench ok"
+ILLM_G8_DSCHED=3 timeout -k 10 300 python -u tools/bench_g8.py sym_int4 --m 8192,1024 --dense > gpurun_out/r5g_g8d_ds3.jsonl 2> gpurun_out/r5g_g8d_ds3.err || exit 3
+echo "g8d dsched3 bench ok"
 bash tools/pmc_g8.sh gate_up 8192 > gpurun_out/r5g_pmc.log 2>&1 || { tail -20 gpurun_out/r5g_pmc.log; exit 3; }
 echo "pmc ok"
 cd /tmp && export TMPDIR=/tmp
