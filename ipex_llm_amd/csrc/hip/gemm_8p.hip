@@ -328,70 +328,12 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, G8S == 1 ? 4 : 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
     }
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // (G8S == 3, dense) the phase's 16 MFMAs with its two LDS-DMA pieces
-  // issued after the first 8: the DMA issue (~60-185 cycles a piece inside
-  // a read-heavy phase, MI355X_MICROARCH.md) moves out of the read segment
-  // into the MFMA segment; the wait before the barrier keeps 3 half-tiles in
-  // flight (vmcnt(6)) and so retires the same half-tile as vmcnt(8) after
-  // the issue did
-  auto mma_st = [&](const uint4 (&f)[4][2], int mh, int nh, auto&& stage) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-#pragma unroll
-      for (int nt = 0; nt < 2; nt++)
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-          acc[nh * 2 + nt][mh * 4 + mt] = mfma16<BF16>(fb[nt][s], f[mt][s], acc[nh * 2 + nt][mh * 4 + mt]);
-      if (s == 0) stage();
-    }
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  if constexpr (DENSE && !FP8 && G8S == 3) {
-    stage_a(0, 0);
-    stage_b(0, 0);
-    stage_a(1, 0);
-    stage_b(1, 0);
-    stage_a(0, 1);
-    stage_b(0, 1);
-    wait_vm8();                                  // A0(0), B0(0) landed
-    barrier();
-    if (wr == 1) barrier();
-    for (int u = 0; u < T; u++) {
-      const uint8_t* ai = a_img(u);
-      const uint8_t* bi = b_img(u);
-      read_a(fa0, ai, 0);
-      read_b(bi, 0);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      barrier();
-      wait_lgkm0();
-      mma_st(fa0, 0, 0, [&] { stage_a(1, u + 1); });
-      barrier();
-      read_a(fa1, ai, 1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      barrier();
-      wait_lgkm0();
-      mma_st(fa1, 1, 0, [&] { stage_b(1, u + 1); });
-      barrier();
-      read_b(bi, 1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      barrier();
-      wait_lgkm0();
-      mma_st(fa0, 0, 1, [&] { stage_a(0, u + 2); });
-      barrier();
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      barrier();
-      mma_st(fa1, 1, 1, [&] { stage_b(0, u + 2); });
-      barrier();
-    }
-    if (wr == 0) barrier();
-  } else if constexpr (DENSE) {
+  if constexpr (DENSE) {
     // ---- prologue: tile 0 complete, tile 1's A0 / B0 in flight
     stage_a(0, 0);
     stage_b(0, 0);
@@ -487,15 +429,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       barrier();
       wait_lgkm0();
-      if constexpr (G8S == 2) {                  // second part of B1(u), decoded from phase 3's registers
-        // (unconditional: a computed-but-unstored decode would be sunk into
-        // the branch, out of the MFMA region; u = 0 rewrites tile 0's B1 part
-        // with the prologue's own registers -- the same values)
-        mma_dec(fa0, 0, 0, u, 1, 1, dv);
-        dec_put(1, 1, dv[0]);
-      } else {
-        mma(fa0, 0, 0);
-      }
+      mma(fa0, 0, 0);
       barrier();
       // phase 1
       read_a(fa1, ai, 1);
@@ -508,10 +442,12 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
         mma(fa1, 1, 0);
         if (u + 1 < T) dec_store(0, u + 1);
       } else {
-        // past the last tile the decode writes a B half nobody reads again
-        mma_dec(fa1, 1, 0, u + 1, 0, G8S == 1 ? 2 : 1, dv);
+        // unconditional: a computed-but-unstored decode would be sunk into a
+        // branch, out of the MFMA region (past the last tile the decode
+        // writes a B half nobody reads again)
+        mma_dec(fa1, 1, 0, u + 1, 0, 2, dv);
         dec_put(0, 0, dv[0]);
-        if (G8S == 1) dec_put(0, 1, dv[1]);
+        dec_put(0, 1, dv[1]);
       }
       barrier();
       // phase 2
@@ -520,12 +456,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       barrier();
       wait_lgkm0();
-      if constexpr (G8S == 2) {                  // second part of B0(u + 1)
-        mma_dec(fa0, 0, 1, u + 1, 1, 1, dv);
-        dec_put(0, 1, dv[0]);
-      } else {
-        mma(fa0, 0, 1);
-      }
+      mma(fa0, 0, 1);
       barrier();
       // phase 3
       dec_load(1, u + 1);
@@ -538,9 +469,9 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
         mma(fa1, 1, 1);
         if (u + 1 < T) dec_store(1, u + 1);
       } else {
-        mma_dec(fa1, 1, 1, u + 1, 0, G8S == 1 ? 2 : 1, dv);
+        mma_dec(fa1, 1, 1, u + 1, 0, 2, dv);
         dec_put(1, 0, dv[0]);
-        if (G8S == 1) dec_put(1, 1, dv[1]);
+        dec_put(1, 1, dv[1]);
       }
       barrier();
     }
@@ -549,7 +480,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's reloads
 
   // ---- epilogue: lane holds out[m][n .. n + 3], m = m-tile row r16, n = 4 g
-  if (S > 1) {                                 // split-K: f32 partials into the workspace
+  if (S > 1) {                                 // split-K: this split's f32 slab of the workspace
 #pragma unroll
     for (int nt = 0; nt < 4; nt++) {
       const int n = n0 + wc * 64 + nt * 16 + 4 * g;
@@ -558,10 +489,14 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       for (int mt = 0; mt < 8; mt++) {
         const int m = m0 + wr * 128 + mt * 16 + r16;
         if (m >= a.M) continue;
-        float* y = a.ws + (size_t)m * a.N + n;
+        float* y = a.ws + ((size_t)ks * a.M + m) * a.N + n;
+        if (n + 3 < a.N && (a.N & 3) == 0) {
+          *(float4*)y = make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-          if (n + i < a.N) atomicAdd(y + i, acc[nt][mt][i]);
+          for (int i = 0; i < 4; i++)
+            if (n + i < a.N) y[i] = acc[nt][mt][i];
+        }
       }
     }
     return;
@@ -650,7 +585,13 @@ __global__ void __launch_bounds__(256) gemm8p_finish_kernel(const G8Args a) {
   const size_t m = q / gpr;
   if (m >= (size_t)a.M) return;
   const int c0 = (int)(q % gpr) * 4;
+  const size_t slab = (size_t)a.M * N;
   const float* row = a.ws + m * N;
+  auto at = [&](int c) {                      // the S slabs of element (m, c), summed in split order
+    float v = row[c];
+    for (int s = 1; s < a.ksplit; s++) v += row[s * slab + c];
+    return v;
+  };
   uint16_t* y = (uint16_t*)a.out + m * a.ldo;
   float o[4];
 #pragma unroll
@@ -658,10 +599,10 @@ __global__ void __launch_bounds__(256) gemm8p_finish_kernel(const G8Args a) {
     const int c = min(c0 + i, NO - 1);
     if (a.glu) {
       const int pr = c / 16, j = c % 16;
-      const float gv = row[pr * 32 + j], uv = row[pr * 32 + 16 + j];
+      const float gv = at(pr * 32 + j), uv = at(pr * 32 + 16 + j);
       o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
     } else {
-      o[i] = row[c] + (a.bias ? bf16_to_f32(a.bias[c]) : 0.f);
+      o[i] = at(c) + (a.bias ? bf16_to_f32(a.bias[c]) : 0.f);
     }
   }
   if (a.out_f32) {
@@ -686,23 +627,17 @@ void launch_gemm8p(const G8Args& a, hipStream_t st) {
   const dim3 grid((unsigned)(MB * NB * S)), blk(512);
   if (a.w_fmt == G8_FP8 && a.w_e5m2) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8 - 1>, grid, blk, 0, st, a);
   else if (a.w_fmt == G8_FP8) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8>, grid, blk, 0, st, a);
-  else if (a.w_fmt < 0) {
-    static const int dsched = [] {
-      const char* e = getenv("ILLM_G8_DSCHED");
-      return e ? atoi(e) : 0;
-    }();
-    if (dsched == 3) hipLaunchKernelGGL((g8::gemm8p_kernel<-1, 3>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((g8::gemm8p_kernel<-1, 0>), grid, blk, 0, st, a);
-  }
+  else if (a.w_fmt < 0) hipLaunchKernelGGL((g8::gemm8p_kernel<-1, 0>), grid, blk, 0, st, a);
   else {
+    // decode interleaved into the MFMA clusters (1, default; +3 % at M = 8192,
+    // profiles/g8_sched_sweep_r5.jsonl) or after them (ILLM_G8_SCHED=0)
     static const int sched = [] {
       const char* e = getenv("ILLM_G8_SCHED");
-      return e ? atoi(e) : 0;
+      return e ? atoi(e) : 1;
     }();
     const bool i4 = fmt_to_dk(a.w_fmt) == DK_INT4S;
-    void (*k)(const G8Args) = i4 ? g8::gemm8p_kernel<DK_INT4S, 0> : g8::gemm8p_kernel<DK_LUT4, 0>;
-    if (sched == 1) k = i4 ? g8::gemm8p_kernel<DK_INT4S, 1> : g8::gemm8p_kernel<DK_LUT4, 1>;
-    if (sched == 2) k = i4 ? g8::gemm8p_kernel<DK_INT4S, 2> : g8::gemm8p_kernel<DK_LUT4, 2>;
+    void (*k)(const G8Args) = i4 ? g8::gemm8p_kernel<DK_INT4S, 1> : g8::gemm8p_kernel<DK_LUT4, 1>;
+    if (sched == 0) k = i4 ? g8::gemm8p_kernel<DK_INT4S, 0> : g8::gemm8p_kernel<DK_LUT4, 0>;
     hipLaunchKernelGGL(k, grid, blk, 0, st, a);
   }
 }

@@ -23,8 +23,9 @@ struct G8Args {
   const float* sw;
   int sw_per_channel, w_e5m2, out_f16;
   // split-K (dense bf16 only): ksplit > 1 workgroups per output tile, each
-  // over a K-tile range, add f32 partials into ws [M, N] (zeroed by the
-  // caller); launch_gemm8p_finish then applies bias / GLU and rounds
+  // over a K-tile range, store f32 partials into slab ks of ws [ksplit, M, N]
+  // (no zeroing, no atomics); launch_gemm8p_finish sums the slabs, applies
+  // bias / GLU and rounds
   int ksplit;
   float* ws;
 };

@@ -410,7 +410,7 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   const int S = ksplit < 0 ? g8_auto_split(M, N, K) : (int)std::max<int64_t>(1, std::min<int64_t>(ksplit, K / 64));
   Tensor ws;
   if (S > 1) {
-    ws = at::zeros({M, N}, x.options().dtype(at::kFloat));
+    ws = at::empty({(int64_t)S, M, N}, x.options().dtype(at::kFloat));
     a.ksplit = S;
     a.ws = ws.data_ptr<float>();
   }

@@ -852,12 +852,13 @@ def enable_training_kernels(model: nn.Module) -> nn.Module:
     if os.environ.get("ILLM_TRAIN_ATTN", "1") == "1":
         from .flash_attn import patch_flash_attention
         patch_flash_attention(model)
-    # the frozen low-bit base dequantized once and kept resident for the
-    # forward and grad_x GEMMs (exactly the per-step dequant's values) when
-    # HBM allows: on a 288 GB MI355X a Llama-3-8B base costs 15 GB and saves
-    # the 448 dequant launches of every step.  ILLM_TRAIN_DENSE_GB=<GiB> sets
-    # the budget, 0 keeps the pure low-bit footprint.
-    gb = os.environ.get("ILLM_TRAIN_DENSE_GB", "auto")
+    # Default: the pure low-bit footprint -- each base GEMM dequantizes its
+    # weight (forward) or W^T (grad_x) into a transient buffer for the dense
+    # 8-phase kernel.  ILLM_TRAIN_DENSE_GB=<GiB> (or "auto": min(48, HBM / 4)
+    # on >= 128 GiB devices) keeps the dequantized base resident instead -- on
+    # a 288 GB MI355X a Llama-3-8B base costs 15 GB and saves the per-step
+    # dequant passes -- and enables the K-concatenated adapter GEMMs.
+    gb = os.environ.get("ILLM_TRAIN_DENSE_GB", "0")
     if gb == "auto":
         total = torch.cuda.get_device_properties(w.device).total_memory / 2 ** 30
         gb = min(48.0, 0.25 * total) if total >= 128 else 0.0

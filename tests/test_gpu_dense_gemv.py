@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M", [1, 2, 3, 5, 8, 13, 16])
-@pytest.mark.parametrize("N,K", [(300, 1024), (4096, 4104), (64, 520)])
+@pytest.mark.parametrize("N,K", [(300, 1024), (4096, 4104), (64, 520), (1000, 4096), (200, 14336)])
 def test_dense_gemv_matches_fp32(dt, M, N, K):
     ops.require()
     torch.manual_seed(M * 7 + N)
@@ -32,3 +32,21 @@ def test_dense_linear_module_uses_kernel():
         got = m(x).float()
     want = torch.nn.functional.linear(x.float(), m.weight.float(), m.bias.float())
     assert ((got - want).norm() / want.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_dense_mfma_rows_independent_of_batch(dt):
+    """the MFMA skinny GEMM (K % 64 == 0): each output column is its own MFMA
+    column, so row m of a 16-row launch equals the 1-row launch bit for bit
+    (the speculative verify's exactness), plain and GLU"""
+    ops.require()
+    torch.manual_seed(5)
+    K, N, I = 4096, 1040, 512
+    w = (torch.randn(N, K, device="cuda") * 0.05).to(dt)
+    wgu = (torch.randn(2 * I, K, device="cuda") * 0.05).to(dt)
+    x = torch.randn(16, K, device="cuda").to(dt)
+    full = torch.ops.ipex_llm_amd.dense_linear(x, w, None)
+    gfull = torch.ops.ipex_llm_amd.dense_glu(x, wgu, 0)
+    for M in (1, 3, 7):
+        assert torch.equal(torch.ops.ipex_llm_amd.dense_linear(x[:M].contiguous(), w, None), full[:M])
+        assert torch.equal(torch.ops.ipex_llm_amd.dense_glu(x[:M].contiguous(), wgu, 0), gfull[:M])

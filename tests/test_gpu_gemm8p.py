@@ -115,11 +115,11 @@ print("OK")
 """
 
 
-@pytest.mark.parametrize("var,val", [("ILLM_G8_SCHED", "1"), ("ILLM_G8_SCHED", "2"), ("ILLM_G8_DSCHED", "3")])
+@pytest.mark.parametrize("var,val", [("ILLM_G8_SCHED", "0"), ("ILLM_G8_SCHED", "1")])
 def test_gemm8p_lowbit_decode_schedules_bit_identical(cuda, var, val):
-    """the interleaved-decode schedules (ILLM_G8_SCHED) and the dense
-    DMA-in-cluster schedule (ILLM_G8_DSCHED), read once per process: the
-    low-bit kernel == dequantize + the dense kernel, bit for bit"""
+    """both decode schedules of the low-bit kernel (ILLM_G8_SCHED: decode after
+    / interleaved into the MFMA clusters, read once per process) == dequantize
+    + the dense kernel, bit for bit"""
     import os
     import subprocess
     import sys

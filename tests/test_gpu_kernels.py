@@ -262,9 +262,10 @@ def test_gemv_rope_epilogue_and_prerot_attention(cuda, B, Hq, Hkv, D):
     if D != 128:
         return                                   # fused-RoPE decode attention: head_dim 128 / 256
     # attention: pre-rotated accumulator vs rotation inside the attention
-    kc = torch.randn(4 * B, Hkv, bs, D, device=cuda).bfloat16()
-    vc = torch.randn(4 * B, Hkv, bs, D, device=cuda).bfloat16()
-    bt = torch.arange(4 * B, dtype=torch.int32, device=cuda).view(B, 4).contiguous()
+    nb = (max(L) + bs - 1) // bs                # block-table row covering the longest sequence
+    kc = torch.randn(nb * B, Hkv, bs, D, device=cuda).bfloat16()
+    vc = torch.randn(nb * B, Hkv, bs, D, device=cuda).bfloat16()
+    bt = torch.arange(nb * B, dtype=torch.int32, device=cuda).view(B, nb).contiguous()
     ns = nsplit_for(max(L))
     kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
     p1, p2 = a_rot * 8, a_raw * 8
