@@ -175,7 +175,8 @@ __global__ void __launch_bounds__(DW * 64) dense_mfma_kernel(const uint16_t* __r
   const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
   auto ld = [&](const uint16_t* p) { return *(const uint4*)p; };
   int64_t s = s0;
-  // two 64-deep steps per iteration, the next pair's weights requested first
+  // two 64-deep steps per iteration, the pair's weights requested first (a
+  // 4-step form measured no faster, profiles/spec_bench_r5_*.jsonl)
   for (; s + 1 < s1; s += 2) {
     const int64_t k = s * 64;
     const uint4 a0 = ld(wg + k), a1 = ld(wg + k + 32), a2 = ld(wg + k + 64), a3 = ld(wg + k + 96);

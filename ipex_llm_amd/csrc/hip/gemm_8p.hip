@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
   // L2 serves their shared nothing but keeps the grouping of the tiles intact)
   const int id0 = mfg::xcd_remap((int)blockIdx.x, total);
   const int ks = id0 % S, id = id0 / S;
-  constexpr int GM = 4;
+  const int GM = a.gm > 0 ? a.gm : 4;
   const int per_group = GM * NB;
   const int grp = id / per_group, rem = id % per_group;
   const int gm = min(GM, MB - grp * GM);
@@ -621,7 +621,15 @@ void launch_gemm8p_finish(const G8Args& a, hipStream_t st) {
   hipLaunchKernelGGL(gemm8p_finish_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st, a);
 }
 
-void launch_gemm8p(const G8Args& a, hipStream_t st) {
+void launch_gemm8p(const G8Args& a0, hipStream_t st) {
+  G8Args a = a0;
+  if (a.gm <= 0) {
+    static const int gm_env = [] {
+      const char* e = getenv("ILLM_G8_GM");
+      return e ? atoi(e) : 0;
+    }();
+    a.gm = gm_env;
+  }
   const int MB = (a.M + 255) / 256, NB = (a.N + 255) / 256;
   const int S = a.w_fmt == -1 && a.ksplit > 1 ? a.ksplit : 1;
   const dim3 grid((unsigned)(MB * NB * S)), blk(512);

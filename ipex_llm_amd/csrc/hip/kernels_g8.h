@@ -28,6 +28,7 @@ struct G8Args {
   // bias / GLU and rounds
   int ksplit;
   float* ws;
+  int gm;                 // m-blocks per rasterization group (0: 4)
 };
 constexpr int G8_FP8 = -2;
 

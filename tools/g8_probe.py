@@ -25,8 +25,26 @@ def timed(fn, it=10):
     return s.elapsed_time(e) / it * 1e3
 
 
+def shapes_only():
+    """(--shapes) the four Llama-3-8B projections at M = 8192 / 1024 on the
+    dense kernel (auto split-K), normal operands: one line per shape"""
+    P = torch.ops.ipex_llm_amd
+    dev = torch.device("cuda")
+    for M in (8192, 1024):
+        for name, N, K in [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336)]:
+            x = torch.randn(M, K, device=dev).bfloat16()
+            w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
+            us = timed(lambda: P.gemm_bf16(x, w))
+            lib = timed(lambda: torch.nn.functional.linear(x, w))
+            print(json.dumps({"gm": os.environ.get("ILLM_G8_GM", "4"), "M": M, "op": name, "us": round(us, 1),
+                              "lib_us": round(lib, 1), "vs_lib": round(lib / us, 3),
+                              "TF": round(2 * M * N * K / us / 1e6, 1)}), flush=True)
+
+
 def main():
     ops.require()
+    if "--shapes" in sys.argv:
+        return shapes_only()
     P = torch.ops.ipex_llm_amd
     dev = torch.device("cuda")
     for M, N, K in [(8192, 28672, 4096), (8192, 4096, 4096)]:
