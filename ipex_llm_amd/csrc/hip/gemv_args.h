@@ -86,7 +86,6 @@ struct GemvArgs {
   // over the full row (sum of squares) and staged for its K slice; workgroup
   // (0, 0) writes h to nres_out (the caller ping-pongs residual buffers).
   const float* nacc;       // [M, K] f32 atomic accumulator of the previous projection
-  int nacc_sc1;            // read nacc with sc1 loads (chained after its producer in one launch)
   const uint16_t* nres;    // [M, K] residual in
   uint16_t* nres_out;      // [M, K] residual out
   const uint16_t* nweight; // [K] norm weight

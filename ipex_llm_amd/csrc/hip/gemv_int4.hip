@@ -5,6 +5,4 @@ template void launch_gemv_dk<DK_INT4S>(bool, int, int, dim3, const GemvArgs&, hi
 template void launch_gemv_dk<DK_INT4A>(bool, int, int, dim3, const GemvArgs&, hipStream_t);
 template void launch_gemv5_dk<DK_INT4S>(bool, int, int, dim3, size_t, const GemvArgs&, hipStream_t);
 template void launch_gemv5_dk<DK_INT4A>(bool, int, int, dim3, size_t, const GemvArgs&, hipStream_t);
-template bool launch_gemv5_chain_dk<DK_INT4S>(bool, int, dim3, size_t, const GemvArgs&, dim3, size_t, const GemvArgs&,
-                                              int*, int*, hipStream_t);
 }  // namespace illm

@@ -21,10 +21,6 @@ void launch_gemv_dk(bool bf16, int mt, int epi, dim3 grid, const GemvArgs& a, hi
 // shmem = gemv5_shmem(rows, chunks per split) <= 159 KiB
 template <int DK>
 void launch_gemv5_dk(bool bf16, int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
-// two dependent decode atomic GEMVs in one launch (lowbit_gemv5.cuh); false: not supported
-template <int DK>
-bool launch_gemv5_chain_dk(bool bf16, int kw, dim3 ga, size_t sha, const GemvArgs& a, dim3 gb, size_t shb,
-                           const GemvArgs& b, int* cnt, int* err, hipStream_t st);
 constexpr int gemv5_x_ld_h(int kw) { return kw + 8; }
 constexpr size_t gemv5_attn_shmem_h(int rows, int cpk, int D, int ns) {
   return (size_t)rows * ((cpk * 128 + D - 1) / D + 1) * (ns + 1) * 4;

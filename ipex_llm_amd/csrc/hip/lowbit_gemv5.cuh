@@ -169,21 +169,8 @@ __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
 #ifndef ILLM_GEMV5_SCL
 #define ILLM_GEMV5_SCL 1
 #endif
-// block coordinates of one GEMV workgroup (blockIdx / gridDim of a plain
-// launch; the virtual ones of a chained launch, below)
-struct G5Blk {
-  int x, y, z, gx, gy, gz;
-};
-// chained launch (lowbit_gemv5_chain_kernel): the second GEMV's workgroups
-// wait for every workgroup of the first after requesting their weights
-struct G5Wait {
-  const int* cnt;       // arrivals of the first GEMV's workgroups
-  int target;           // its workgroup count
-  int* err;             // device error word (a wait that never completes)
-};
-
-template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF, bool SCL>
-__device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, const G5Wait* wt) {
+template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4, bool SCL = ILLM_GEMV5_SCL != 0>
+__global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(const GemvArgs a) {
   // PF: chunks in flight per wave (4; 8 = every chunk of a decode split-K
   // slice of <= 8 chunks requested before the prologue)
   using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;   // MFMA input type
@@ -196,11 +183,22 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r16 = lane & 15;
 
+  // ---- zero a consumed atomic accumulator (its readers ran earlier in the
+  // stream), spread over every workgroup of the grid (up to ~1 MB at M = 8)
+  if (a.nzero) {
+    const int nthr = NW * 64;
+    const size_t nb = (size_t)gridDim.x * gridDim.y * gridDim.z;
+    const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const size_t nv = (size_t)a.nzero_n / 4;
+    for (size_t i = bid * nthr + threadIdx.x; i < nv; i += nb * nthr)
+      ((float4*)a.nzero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
   int Mloc = a.M;
   const uint8_t* wbase = a.w;
   const int32_t* prow = nullptr;
   if constexpr (MOE) {
-    const int e = blk.z;
+    const int e = blockIdx.z;
     const int m0 = a.moe_off[e];
     Mloc = min(16, a.moe_off[e + 1] - m0);
     if (Mloc <= 0) return;                // expert not routed to: the whole block exits
@@ -210,9 +208,9 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
   auto xrow_of = [&](int m) -> int { if constexpr (MOE) return prow[m] / a.moe_xdiv; else return m; };
   auto orow_of = [&](int m) -> int { if constexpr (MOE) return prow[m]; else return m; };
 
-  const int nks = blk.gy;
+  const int nks = gridDim.y;
   const int cpk = a.cpk > 0 ? a.cpk : (a.KC + nks - 1) / nks;
-  const int c0 = blk.y * cpk;
+  const int c0 = blockIdx.y * cpk;
   const int c1 = min(a.KC, c0 + cpk);
   const int kbase = c0 * 128;
   const int kw = (c1 - c0) * 128;
@@ -224,13 +222,13 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
 
   const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
   const int tg = wave / KW, kp = wave % KW;
-  const int tile0 = (blk.x * TG + tg) * TPW;
+  const int tile0 = (blockIdx.x * TG + tg) * TPW;
   const int per = (c1 - c0 + KW - 1) / KW;
   const int wc0 = c0 + kp * per;
   const int wc1 = min(c1, wc0 + per);
   const bool wave_on = tile0 < NT && wc0 < wc1;
   // debug build: the host geometry must cover every output tile and K chunk
-  if (ILLM_DCHECK_FAILS((int64_t)blk.gx * TG * TPW >= NT && (int64_t)nks * cpk >= a.KC && Mloc <= 16, a.err,
+  if (ILLM_DCHECK_FAILS((int64_t)gridDim.x * TG * TPW >= NT && (int64_t)nks * cpk >= a.KC && Mloc <= 16, a.err,
                         ERR_GEOMETRY))
     return;
   const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
@@ -279,32 +277,6 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
 #pragma unroll
     for (int u = 0; u < PF; u++) load_chunk(ring[u], wc0 + u);
   }
-  // chained second GEMV: everything from here on may read what the first
-  // one wrote (or zero what it reads): wait for all of its workgroups
-  if (wt != nullptr) {
-    if (threadIdx.x == 0) {
-      int it = 0;
-      while (__hip_atomic_load(wt->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wt->target) {
-        __builtin_amdgcn_s_sleep(8);
-        if (++it > (1 << 21)) {                 // ~seconds: report, never hang the device
-          kerr(wt->err, ERR_CHAIN);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  // ---- zero a consumed atomic accumulator (its readers ran earlier in the
-  // stream), spread over every workgroup of the grid (up to ~1 MB at M = 8)
-  if (a.nzero) {
-    const int nthr = NW * 64;
-    const size_t nb = (size_t)blk.gx * blk.gy * blk.gz;
-    const size_t bid = ((size_t)blk.z * blk.gy + blk.y) * blk.gx + blk.x;
-    const size_t nv = (size_t)a.nzero_n / 4;
-    for (size_t i = bid * nthr + threadIdx.x; i < nv; i += nb * nthr)
-      ((float4*)a.nzero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-
   if constexpr (DK == DK_LUT4) {
     if (threadIdx.x < 256)
       lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
@@ -351,14 +323,8 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
   __shared__ float ninv[16];
   auto rnd = [](float v) { return to_f32<T>(from_f32<T>(v)); };
   auto ni_h = [&](int m, int k, float* h) {
-    float4 p0, p1;
-    if (a.nacc_sc1) {            // chained after its producer: read past this XCD's L2
-      p0 = ld16_sc1(a.nacc, (size_t)m * a.K + k);
-      p1 = ld16_sc1(a.nacc, (size_t)m * a.K + k + 4);
-    } else {
-      const float4* p = (const float4*)(a.nacc + (size_t)m * a.K + k);
-      p0 = p[0], p1 = p[1];
-    }
+    const float4* p = (const float4*)(a.nacc + (size_t)m * a.K + k);
+    const float4 p0 = p[0], p1 = p[1];
     const uint4 r = *(const uint4*)(a.nres + (size_t)m * a.K + k);
     const float av[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
     const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
@@ -376,7 +342,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
   if (a.nacc && !defer && !(ILLM_GEMV5_ABL & 2)) {
     if (threadIdx.x < 16) ninv[threadIdx.x] = 0.f;
     __syncthreads();
-    const bool wres = a.nres_out != nullptr && blk.x == 0 && blk.y == 0;
+    const bool wres = a.nres_out != nullptr && blockIdx.x == 0 && blockIdx.y == 0;
     const int vpr = a.K / 8;
     uint16_t* xst = (uint16_t*)smem;
     const int ldxs = gemv5_x_ld(kw);
@@ -543,7 +509,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
         ssq += __shfl_xor(ssq, 2, 8);
         ssq += __shfl_xor(ssq, 4, 8);
         if ((v & 7) == 0) atomicAdd(&ninv[m], ssq);
-        if (a.nres_out && blk.x == 0)
+        if (a.nres_out && blockIdx.x == 0)
           *(uint4*)(a.nres_out + (size_t)m * a.K + kbase + kk) =
               make_uint4(pack2<T>(h[0], h[1]), pack2<T>(h[2], h[3]), pack2<T>(h[4], h[5]), pack2<T>(h[6], h[7]));
         const uint4 wq = *(const uint4*)(a.nweight + kbase + kk);
@@ -602,7 +568,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
       __syncthreads();
       if (threadIdx.x < Mloc) ninv[threadIdx.x] = rsqrtf(ninv[threadIdx.x] / (float)a.K + a.neps);
       __syncthreads();
-    } else if (blk.x == 0 && threadIdx.x < Mloc && a.nss) {
+    } else if (blockIdx.x == 0 && threadIdx.x < Mloc && a.nss) {
       __hip_atomic_fetch_add(a.nss + threadIdx.x, ninv[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -747,7 +713,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
         for (int i = 0; i < 4; i++) tbuf[r16 * NC + (tg * TPW + t) * 16 + 4 * g + i] = acc[t][i];
     }
     __syncthreads();
-    const int nb = blk.x * NC;
+    const int nb = blockIdx.x * NC;
     float* ws = (float*)a.out;
     for (int v = threadIdx.x; v < Mloc * NC; v += NW * 64) {
       const int m = v / NC, n = nb + v % NC;
@@ -809,7 +775,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
         for (int i = 0; i < 4; i++)
           if (n0 + i < a.N) __hip_atomic_fetch_add(ws + i, o[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else if constexpr (EPI == EPI_PARTIAL) {
-        float* ws = (float*)a.out + ((size_t)blk.y * a.M + m) * a.N + n0;
+        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
         if (n0 + 3 < a.N && (a.N & 3) == 0) *(float4*)ws = make_float4(o[0], o[1], o[2], o[3]);
         else for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[i];
       } else {
@@ -840,55 +806,8 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
           const int oi = __shfl_xor(abi, off, 64);
           if (ov > abest || (ov == abest && oi < abi)) { abest = ov; abi = oi; }
         }
-        if (g == 0) a.amax[((size_t)blk.x * TG + tg) * a.M + m] = make_float2(abest, __int_as_float(abi));
+        if (g == 0) a.amax[((size_t)blockIdx.x * TG + tg) * a.M + m] = make_float2(abest, __int_as_float(abi));
       }
-    }
-  }
-}
-
-template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4, bool SCL = ILLM_GEMV5_SCL != 0>
-__global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(const GemvArgs a) {
-  gemv5_body<DK, T, EPI, TPW, KW, MOE, NW, PF, SCL>(
-      a, G5Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z},
-      nullptr);
-}
-
-// Two dependent GEMVs of one instantiation in ONE launch (decode: layer l's
-// down projection and layer l + 1's qkv, whose norm-in prologue reads the
-// down accumulator).  Workgroups [0, ga) run the first; each signals after
-// its atomics / stores are done (s_waitcnt vmcnt(0), one agent-scope add).
-// The rest run the second: they request their weight chunks first, then
-// wait for all ga arrivals -- the second GEMV's launch ramp and weight
-// latency overlap the first's tail instead of following it.  Workgroups are
-// dispatched in id order per XCD, so every first-GEMV workgroup is resident
-// before any waiter on its XCD: no deadlock; the wait is bounded anyway
-// (ERR_CHAIN).  The last second-GEMV workgroup resets both counters.
-struct G5Chain {
-  int ga, gax, gay, gbx, gby, gb;
-  int* cnt;                // [0] first-GEMV arrivals, [1] second-GEMV departures
-  int* err;
-};
-template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF, bool SCL>
-__global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW)
-lowbit_gemv5_chain_kernel(const GemvArgs a, const GemvArgs b, const G5Chain c) {
-  const int id = (int)blockIdx.x;
-  if (id < c.ga) {
-    gemv5_body<DK, T, EPI, TPW, KW, MOE, NW, PF, SCL>(
-        a, G5Blk{id % c.gax, (id / c.gax) % c.gay, id / (c.gax * c.gay), c.gax, c.gay, c.ga / (c.gax * c.gay)}, nullptr);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(c.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const int j = id - c.ga;
-  const G5Wait w{c.cnt, c.ga, c.err};
-  gemv5_body<DK, T, EPI, TPW, KW, MOE, NW, PF, SCL>(
-      b, G5Blk{j % c.gbx, (j / c.gbx) % c.gby, j / (c.gbx * c.gby), c.gbx, c.gby, c.gb / (c.gbx * c.gby)}, &w);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (__hip_atomic_fetch_add(c.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c.gb - 1) {
-      __hip_atomic_store(c.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(c.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -968,30 +887,6 @@ void launch_gemv5_dk(bool bf16, int kw, int epi, dim3 grid, size_t shmem, const 
     if (moe) launch5_kw<DK, F16, true>(kw, epi, grid, shmem, a, st);
     else launch5_kw<DK, F16, false>(kw, epi, grid, shmem, a, st);
   }
-}
-
-// chained launch of two decode split-K atomic GEMVs (lowbit_gemv5_chain_kernel):
-// bf16 activations, one k-part per tile group, 8 waves, 4 chunks in flight --
-// the decode projections' instantiation.  Returns false (caller launches the
-// two separately) for anything else.
-template <int DK>
-bool launch_gemv5_chain_dk(bool bf16, int kw, dim3 ga, size_t sha, const GemvArgs& a0, dim3 gb, size_t shb,
-                           const GemvArgs& b0, int* cnt, int* err, hipStream_t st) {
-  auto pf8 = [](const GemvArgs& a) { return a.pf8 && a.cpk > 0 && a.cpk <= 8; };
-  if (!bf16 || kw != 1 || a0.nw != 8 || b0.nw != 8 || a0.moe_off || b0.moe_off || pf8(a0) || pf8(b0)) return false;
-  GemvArgs a = a0, b = b0;
-  using C = typename std::conditional<DK == DK_LUT4, F16, BF16>::type;
-  a.nib_mask = b.nib_mask = 0x000F000Fu;
-  a.nib_magic = b.nib_magic = Raw<C>::k4;
-  auto kern = lowbit_gemv5_chain_kernel<DK, BF16, EPI_ATOMIC, 1, 1, false, 8, 4, false>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-    attr = true;
-  }
-  G5Chain c{(int)(ga.x * ga.y * ga.z), (int)ga.x, (int)ga.y, (int)gb.x, (int)gb.y, (int)(gb.x * gb.y * gb.z), cnt, err};
-  hipLaunchKernelGGL(kern, dim3((unsigned)(c.ga + c.gb)), dim3(8 * 64), sha > shb ? sha : shb, st, a, b, c);
-  return true;
 }
 
 }  // namespace illm

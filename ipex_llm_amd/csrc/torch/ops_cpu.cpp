@@ -161,8 +161,6 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("l3_prefetch(Tensor t, int offset=0, int nbytes=-1, int wgs=1024) -> ()");
   m.def("decode_advance(Tensor? logits, Tensor(a!) ids, Tensor(b!) next_ids, Tensor(c!) pos, Tensor block_tables, int bs, Tensor(d!) slots, Tensor(e!) seq_lens, Tensor? pos_offset=None, Tensor? parts=None) -> ()");
   m.def("gemv_argmax(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias=None) -> (Tensor, Tensor)");
-  m.def("gemv_chain_arm(Tensor like) -> ()");
-  m.def("gemv_chain_flush(Tensor like) -> ()");
   m.def("embed_rms_norm(Tensor ids, Tensor table, Tensor w, float eps, bool unit_offset=False, Tensor(a!)? zero=None) -> (Tensor, Tensor)");
   m.def("rope_kv_fused(Tensor(d!) part, Tensor? bias, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor pos, Tensor block_tables, int tq, Tensor inv_freq, Tensor? q_norm, Tensor? k_norm, float norm_eps, float q_scale, int Hq, int Hkv, int D, int rot_dim, bool interleaved, int kv_fp8, float k_scale, float v_scale, Tensor? pos_offset=None, bool zero_part=False, Tensor? pss=None, int pss_n=0, float pss_eps=0.0) -> ()");
   m.def("attn_prefill(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables, Tensor seq_lens, int Tq, float scale, float softcap, int window, int kv_fp8, float k_scale, float v_scale) -> Tensor");
@@ -188,12 +186,8 @@ at::Tensor kernel_errors_cpu(const at::Tensor& like, bool reset) {
   return at::zeros({4}, like.options().dtype(at::kInt));     // host kernels check shapes up front
 }
 
-void gemv_chain_noop(const at::Tensor&) {}      // host GEMVs launch nothing to chain
-
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
   m.impl("kernel_errors", &kernel_errors_cpu);
-  m.impl("gemv_chain_arm", &gemv_chain_noop);
-  m.impl("gemv_chain_flush", &gemv_chain_noop);
   m.impl("quantize_cpu", &quantize_cpu);
   m.impl("dequantize_cpu", &dequantize_cpu);
   m.impl("repack_to_device", &repack_to_device);

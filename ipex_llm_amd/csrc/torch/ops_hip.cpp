@@ -80,107 +80,17 @@ void launch_gemv_any(int fmt, bool bf16, int mt, int epi, dim3 grid, const illm:
   ILLM_DK_SWITCH(fmt, illm::launch_gemv_dk<DKV>(bf16, mt, epi, grid, a, st));
 }
 int* kernel_err(const c10::Device& dev);
-static int cur_dev() {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  return dev;
-}
-static illm::GemvArgs gemv5_prep(const illm::GemvArgs& a0) {
+void launch_gemv5_any(int fmt, bool bf16, int kw, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a0) {
+  hipStream_t st = cur_stream();
   static const int pf8 = getenv("ILLM_GEMV5_PF8") ? atoi(getenv("ILLM_GEMV5_PF8")) : 0;
   illm::GemvArgs a = a0;
   a.pf8 = pf8;
 #if ILLM_DEVICE_DEBUG
-  a.err = kernel_err(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)cur_dev()));
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  a.err = kernel_err(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)dev));
 #endif
-  return a;
-}
-static void launch_gemv5_now(int fmt, bool bf16, int kw, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a0,
-                             hipStream_t st) {
-  const illm::GemvArgs a = gemv5_prep(a0);
   ILLM_DK_SWITCH(fmt, illm::launch_gemv5_dk<DKV>(bf16, kw, epi, grid, shmem, a, st));
-}
-
-// ---- chained decode GEMVs ----------------------------------------------------
-// gemv_chain_arm(): the NEXT v5 GEMV launch is held back; the launch after it
-// (the caller guarantees no other kernel in between) goes out together with
-// it as one lowbit_gemv5_chain_kernel when both are decode atomic GEMVs of
-// the chained instantiation, else the two go out one after the other, in
-// order.  gemv_chain_flush() sends a held launch on its own.
-namespace {
-struct Held5 {
-  bool has = false;
-  int fmt = 0;
-  bool bf16 = true;
-  int kw = 1, epi = 0;
-  dim3 grid;
-  size_t shmem = 0;
-  illm::GemvArgs a{};
-  hipStream_t st = nullptr;
-};
-thread_local bool g_chain_armed = false;
-thread_local Held5 g_held;
-int* chain_counters(int dev) {
-  static int* p[64] = {};
-  if (p[dev] == nullptr) {
-    TORCH_CHECK(hipMalloc((void**)&p[dev], 64) == hipSuccess, "gemv chain: counter allocation failed");
-    TORCH_CHECK(hipMemset(p[dev], 0, 64) == hipSuccess, "gemv chain: counter reset failed");
-  }
-  return p[dev];
-}
-void flush_held() {
-  if (!g_held.has) return;
-  g_held.has = false;
-  launch_gemv5_now(g_held.fmt, g_held.bf16, g_held.kw, g_held.epi, g_held.grid, g_held.shmem, g_held.a, g_held.st);
-}
-}  // namespace
-
-void launch_gemv5_any(int fmt, bool bf16, int kw, int epi, dim3 grid, size_t shmem, const illm::GemvArgs& a0) {
-  hipStream_t st = cur_stream();
-  if (g_held.has) {
-    Held5 h = g_held;
-    g_held.has = false;
-    bool done = false;
-    if (h.st == st && h.fmt == fmt && h.bf16 == bf16 && h.kw == kw && h.epi == illm::EPI_ATOMIC &&
-        epi == illm::EPI_ATOMIC && illm::fmt_to_dk(fmt) == illm::DK_INT4S) {
-      const illm::GemvArgs pa = gemv5_prep(h.a);
-      illm::GemvArgs pb = gemv5_prep(a0);
-      // the first GEMV's accumulator is written by agent-scope (sc1) atomics,
-      // performed past every XCD's L2, and no L2 held its lines at launch:
-      // plain loads after the wait read the finished sums (an sc1 load per
-      // workgroup of the full rows measured 36 vs 20 us for the pair,
-      // profiles/decode_trace_b8_r5_chain_sc1.txt); ILLM_CHAIN_SC1=1 forces them
-      static const int sc1 = getenv("ILLM_CHAIN_SC1") ? atoi(getenv("ILLM_CHAIN_SC1")) : 0;
-      pb.nacc_sc1 = sc1;
-      const int dev = cur_dev();
-      done = illm::launch_gemv5_chain_dk<illm::DK_INT4S>(
-          bf16, kw, h.grid, h.shmem, pa, grid, shmem, pb, chain_counters(dev),
-          kernel_err(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)dev)), st);
-    }
-    if (!done) {
-      launch_gemv5_now(h.fmt, h.bf16, h.kw, h.epi, h.grid, h.shmem, h.a, h.st);
-      launch_gemv5_now(fmt, bf16, kw, epi, grid, shmem, a0, st);
-    }
-    return;
-  }
-  if (g_chain_armed) {
-    g_chain_armed = false;
-    g_held.has = true;
-    g_held.fmt = fmt, g_held.bf16 = bf16, g_held.kw = kw, g_held.epi = epi;
-    g_held.grid = grid, g_held.shmem = shmem, g_held.a = a0, g_held.st = st;
-    return;
-  }
-  launch_gemv5_now(fmt, bf16, kw, epi, grid, shmem, a0, st);
-}
-
-void gemv_chain_arm(const Tensor& like) {
-  TORCH_CHECK(like.is_cuda(), "gemv_chain_arm: a GPU tensor selects the device");
-  flush_held();
-  g_chain_armed = true;
-}
-void gemv_chain_flush(const Tensor& like) {
-  (void)like;
-  g_chain_armed = false;
-  flush_held();
 }
 
 constexpr size_t kMaxLds = 159 * 1024;
@@ -1714,8 +1624,6 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("moe_route", &moe_route);
   m.impl("quantize_device", &quantize_device);
   m.impl("dequantize_device", &dequantize_device);
-  m.impl("gemv_chain_arm", &gemv_chain_arm);
-  m.impl("gemv_chain_flush", &gemv_chain_flush);
   m.impl("gemv", &gemv);
   m.impl("gemv_accum", &gemv_accum);
   m.impl("gemv_norm_in", &gemv_norm_in);

@@ -183,12 +183,6 @@ DEFER_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_GLU_MAX_M", "4"))
 # profiles/bench_b8_r3_mlpacc*.json): the down GEMV's input staging from the
 # [8, 28672] f32 gate/up slab costs more than the norm launch
 DEFER_MLP_ACC = __import__("os").environ.get("ILLM_DEFER_MLP_ACC", "0") == "1"
-# decode: layer l's down GEMV and layer l + 1's qkv GEMV (whose norm-in
-# prologue reads the down accumulator) go out as ONE chained launch
-# (ops_hip.cpp gemv_chain_arm, lowbit_gemv5.cuh lowbit_gemv5_chain_kernel):
-# the qkv workgroups request their weights while the down GEMV finishes.
-# ILLM_GEMV_CHAIN=0 launches them separately (A/B)
-GEMV_CHAIN = __import__("os").environ.get("ILLM_GEMV_CHAIN", "1") == "1"
 # decode batches up to this size take the fused-RoPE attention (qkv accumulated
 # atomically into one slab read by the attention, re-zeroed by its combine).
 # Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token,
@@ -669,16 +663,6 @@ class NativeCausalLM(nn.Module):
         rope_in = rope_ok and (T <= ROPE_IN_MAX_M or prerot)
         qrope = (self.rope_cache, pos, (s.num_heads + s.num_kv_heads) * s.head_dim, s.head_dim) if prerot else None
         nxt_res = lambda r: res_pp[1] if r is res_pp[0] else res_pp[0]
-
-        def chain_next(li, dn):
-            """the next launch after layer li's down GEMV is layer li + 1's
-            qkv norm-in GEMV (the branch below, nothing launched in between)"""
-            if not (GEMV_CHAIN and norm_in and li + 1 < len(self.layers) and dn.mp_group is None):
-                return False
-            qn = self.layers[li + 1].self_attn.qkv_proj
-            return (isinstance(qn, LowBitLinear) and qn.mp_group is None and T <= ops.GEMV_MAX_M
-                    and (qn.bias is None or qn.bias.dtype == x.dtype) and (T <= ACC_MAX_M or rope_in)
-                    and not _trace.ENABLED and self._capture_q is None)
         zero_next = None                # consumed atomic slab the next accumulating GEMV zeroes
         from ..utils import trace as _trace
         # prefill on the library GEMM path: dense weights of layer li + 1 are
@@ -785,8 +769,6 @@ class NativeCausalLM(nn.Module):
                                              partials=accP.unsqueeze(0), unit_offset=s.norm_unit_offset,
                                              zero_partials=True)
                     act = ops.gemv_glu(xn, gu.weight, gu.fmt, gu.out_features, gu.in_features, s.act)
-                    if chain_next(li, dn):
-                        torch.ops.ipex_llm_amd.gemv_chain_arm(accD)
                     ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=zero_qkv)
                 else:
                     r2 = nxt_res(residual)
@@ -794,8 +776,6 @@ class NativeCausalLM(nn.Module):
                                            s.norm_unit_offset, gu.weight, gu.fmt, gu.out_features, gu.in_features,
                                            True, s.act, zero=zero_qkv, ss=ss_all[2 * li + 1] if defer else None)
                     residual = r2
-                    if chain_next(li, dn):
-                        torch.ops.ipex_llm_amd.gemv_chain_arm(accD)
                     ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=accP)
                 self._reduce(accD, dn)
                 consumed = None
@@ -872,8 +852,6 @@ class NativeCausalLM(nn.Module):
                 if layer.post_feedforward_layernorm is not None:
                     y = ops.rms_norm(y, layer.post_feedforward_layernorm, s.rms_eps, s.norm_unit_offset)
                 x, _ = ops.add_rms_norm(y.contiguous(), residual, nxt, s.rms_eps, unit_offset=s.norm_unit_offset)
-        if GEMV_CHAIN and norm_in and residual.is_cuda:
-            torch.ops.ipex_llm_amd.gemv_chain_flush(residual)     # (nothing held: no-op)
         if zero_next is not None:
             zero_next.zero_()
         if zero_gu is not None:

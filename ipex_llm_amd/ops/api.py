@@ -97,8 +97,7 @@ class KernelError(RuntimeError):
 _KERR_NAMES = {1: "block-table entry outside the KV cache", 2: "cache slot outside the KV cache",
                4: "expert id out of range", 8: "sequence length out of range (block-table row / split grid)",
                16: "token id outside the vocabulary", 32: "launch geometry does not cover the output (debug build)",
-               64: "a peer rank did not answer in time (collective / expert all-to-all timed out)",
-               128: "a chained GEMV launch waited too long for its first half"}
+               64: "a peer rank did not answer in time (collective / expert all-to-all timed out)"}
 
 
 def check_kernel_errors(device=None, reset: bool = True):

@@ -834,59 +834,3 @@ def test_embed_rms_norm_matches_gather_then_norm(cuda):
     torch.ops.ipex_llm_amd.embed_rms_norm(torch.tensor([V + 5], device=cuda), table, w, 1e-5, False, None)
     with pytest.raises(RuntimeError):
         ops.check_kernel_errors(cuda)
-
-
-@pytest.mark.parametrize("M", [1, 8])
-def test_gemv_chain_launch_matches_separate(cuda, M):
-    """down GEMV -> next layer's qkv norm-in GEMV as one chained launch
-    (gemv_chain_arm: the second GEMV's workgroups wait on the first's
-    arrivals, read its accumulator past L2) == the two launches one after the
-    other; the counters come back to zero (a second chained launch works)"""
-    torch.manual_seed(21 + M)
-    f = get_format("sym_int4").fmt
-    H, I, N = 4096, 14336, 6144
-    act = torch.randn(M, I, device=cuda).bfloat16()
-    bd = ops.quantize(torch.randn(H, I, device=cuda) * 0.02, f)
-    bq = ops.quantize(torch.randn(N, H, device=cuda) * 0.02, f)
-    res = torch.randn(M, H, device=cuda).bfloat16()
-    wn = (torch.rand(H, device=cuda) + 0.5).bfloat16()
-    outs = {}
-    for rep, chain in enumerate((False, True, True)):
-        accD = torch.zeros(M, H, device=cuda)
-        part = torch.zeros(M, N, device=cuda)
-        r2 = torch.empty_like(res)
-        if chain:
-            torch.ops.ipex_llm_amd.gemv_chain_arm(accD)
-        ops.gemv_accum(act, bd, f, H, I, accD, 0)
-        ops.gemv_norm_in(accD, res, r2, wn, 1e-5, False, bq, f, N, H, False, acc_out=part)
-        torch.cuda.synchronize()
-        outs[rep] = (accD.clone(), part.clone(), r2.clone())
-    for rep in (1, 2):
-        assert _rel(outs[rep][0], outs[0][0]) < 1e-5
-        assert _rel(outs[rep][1], outs[0][1]) < 1e-4
-        assert torch.equal(outs[rep][2], outs[0][2]) or _rel(outs[rep][2].float(), outs[0][2].float()) < 1e-2
-    torch.ops.ipex_llm_amd.gemv_chain_flush(accD)
-
-
-def test_decode_gemv_chain_matches_unchained(cuda, monkeypatch):
-    """whole-model graph decode with the down -> qkv chained launches vs
-    separate launches: same greedy tokens (up to rare last-bit ties of the
-    atomic order), eager == graph"""
-    from transformers import LlamaConfig
-    from ipex_llm_amd.engine.runner import Engine
-    from ipex_llm_amd.models import decoder as dec
-    from ipex_llm_amd.models.builder import random_native_model
-    cfg = LlamaConfig(vocab_size=1024, hidden_size=4096, intermediate_size=14336, num_hidden_layers=3,
-                      num_attention_heads=32, num_key_value_heads=8, max_position_embeddings=1024)
-    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=4)
-    prompts = [list(range(1, 40)), list(range(5, 60)), list(range(9, 30)), list(range(2, 70))]
-    outs = {}
-    for flag in (False, True):
-        monkeypatch.setattr(dec, "GEMV_CHAIN", flag)
-        outs[flag] = Engine(m).generate(prompts, max_new_tokens=8, use_graph=True)
-    a, b = sum(outs[False], []), sum(outs[True], [])
-    assert sum(x == y for x, y in zip(a, b)) >= 0.95 * len(a)
-    monkeypatch.setattr(dec, "GEMV_CHAIN", True)
-    eager = Engine(m).generate(prompts, max_new_tokens=8, use_graph=False)
-    e, g = sum(eager, []), b
-    assert sum(x == y for x, y in zip(e, g)) >= 0.95 * len(e)
