@@ -39,6 +39,7 @@ class SamplingParams:
     repetition_penalty: float = 1.0
     stop_token_ids: List[int] = field(default_factory=list)
     seed: Optional[int] = None
+    ignore_eos: bool = False          # run to max_new_tokens through EOS (stop_token_ids still stop)
 
 
 @dataclass
@@ -166,7 +167,7 @@ class LLMEngine:
         n = len(r.generated)
         if n >= p.max_new_tokens:
             self._finish(r, "length")
-        elif n >= p.min_new_tokens and (tok in self.eos or tok in p.stop_token_ids):
+        elif n >= p.min_new_tokens and ((tok in self.eos and not p.ignore_eos) or tok in p.stop_token_ids):
             self._finish(r, "stop")
 
     def _pick(self, logits: torch.Tensor, r: Request) -> int:
