@@ -158,7 +158,7 @@ template <typename T, bool GLU>
 __global__ void __launch_bounds__(DW * 64) dense_mfma_kernel(const uint16_t* __restrict__ x, int M, int64_t K,
                                                           const uint16_t* __restrict__ w, int64_t N,
                                                           const uint16_t* __restrict__ bias, int act,
-                                                          uint16_t* __restrict__ out) {
+                                                          uint16_t* __restrict__ out, int trans) {
   __shared__ f32x4 red[DW][GLU ? 2 : 1][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -239,6 +239,10 @@ __global__ void __launch_bounds__(DW * 64) dense_mfma_kernel(const uint16_t* __r
     }
     o[i] = from_f32<T>(v);
   }
+  if (trans) {                                     // out^T [N, M]: the skinny-GEMM caller's [tokens, r]
+    for (int i = 0; i < 4 && n0 + i < N; i++) out[(n0 + i) * M + m] = o[i];
+    return;
+  }
   uint16_t* y = out + (int64_t)m * N + n0;
   if (n0 + 3 < N && (((int64_t)m * N + n0) & 3) == 0) {
     *(uint2*)y = make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
@@ -257,10 +261,10 @@ static bool dense_mfma_on() {
 
 template <typename T>
 static void dg_t(const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t N, const uint16_t* bias,
-                 uint16_t* out, hipStream_t st) {
-  if (dense_mfma_on() && K % 64 == 0 && M <= 16) {
+                 uint16_t* out, hipStream_t st, bool trans) {
+  if (trans || (dense_mfma_on() && K % 64 == 0 && M <= 16)) {
     hipLaunchKernelGGL((dense_mfma_kernel<T, false>), dim3((unsigned)((N + 15) / 16)), dim3(DW * 64), 0, st, x, M, K,
-                       w, N, bias, 0, out);
+                       w, N, bias, 0, out, trans ? 1 : 0);
     return;
   }
   const dim3 grid((unsigned)((N + 3) / 4));
@@ -278,7 +282,7 @@ static void dglu_t(const uint16_t* x, int M, int64_t K, const uint16_t* w, int64
                    hipStream_t st) {
   if (dense_mfma_on() && K % 64 == 0 && M <= 16 && I % 16 == 0) {
     hipLaunchKernelGGL((dense_mfma_kernel<T, true>), dim3((unsigned)(I / 16)), dim3(DW * 64), 0, st, x, M, K, w, I,
-                       nullptr, act, out);
+                       nullptr, act, out, 0);
     return;
   }
   const dim3 grid((unsigned)((I + 3) / 4));
@@ -298,9 +302,9 @@ void launch_dense_glu(bool bf16, const uint16_t* x, int M, int64_t K, const uint
 }
 
 void launch_dense_gemv(bool bf16, const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t N,
-                       const uint16_t* bias, uint16_t* out, hipStream_t st) {
-  if (bf16) dg_t<BF16>(x, M, K, w, N, bias, out, st);
-  else dg_t<F16>(x, M, K, w, N, bias, out, st);
+                       const uint16_t* bias, uint16_t* out, hipStream_t st, bool trans_out) {
+  if (bf16) dg_t<BF16>(x, M, K, w, N, bias, out, st, trans_out);
+  else dg_t<F16>(x, M, K, w, N, bias, out, st, trans_out);
 }
 
 }  // namespace illm

@@ -564,10 +564,18 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
         }
       } else {
         uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n;
-        if (n + 3 < a.N && ((a.ldo | n) & 3) == 0) *(uint2*)y = make_uint2(pack2<BF16>(o0, o1), pack2<BF16>(o2, o3));
-        else {
+        if (n + 3 < a.N && ((a.ldo | n) & 3) == 0) {
+          float q0 = o0, q1 = o1, q2 = o2, q3 = o3;
+          if (a.accum) {                   // y += x w^T: one rounding of (old + sum)
+            const uint2 ov = *(const uint2*)y;
+            q0 += bf16_to_f32(ov.x & 0xffff), q1 += bf16_to_f32(ov.x >> 16);
+            q2 += bf16_to_f32(ov.y & 0xffff), q3 += bf16_to_f32(ov.y >> 16);
+          }
+          *(uint2*)y = make_uint2(pack2<BF16>(q0, q1), pack2<BF16>(q2, q3));
+        } else {
           const float o[4] = {o0, o1, o2, o3};
-          for (int i = 0; i < 4 && n + i < a.N; i++) y[i] = from_f32<BF16>(o[i]);
+          for (int i = 0; i < 4 && n + i < a.N; i++)
+            y[i] = from_f32<BF16>(o[i] + (a.accum ? bf16_to_f32(y[i]) : 0.f));
         }
       }
     }
@@ -609,9 +617,14 @@ __global__ void __launch_bounds__(256) gemm8p_finish_kernel(const G8Args a) {
     float* yf = (float*)a.out + m * a.ldo;
     for (int i = 0; i < 4 && c0 + i < NO; i++) yf[c0 + i] = o[i];
   } else if (c0 + 3 < NO && ((a.ldo | c0) & 3) == 0) {
+    if (a.accum) {
+      const uint2 ov = *(const uint2*)(y + c0);
+      o[0] += bf16_to_f32(ov.x & 0xffff), o[1] += bf16_to_f32(ov.x >> 16);
+      o[2] += bf16_to_f32(ov.y & 0xffff), o[3] += bf16_to_f32(ov.y >> 16);
+    }
     *(uint2*)(y + c0) = make_uint2(pack2<BF16>(o[0], o[1]), pack2<BF16>(o[2], o[3]));
   } else {
-    for (int i = 0; i < 4 && c0 + i < NO; i++) y[c0 + i] = from_f32<BF16>(o[i]);
+    for (int i = 0; i < 4 && c0 + i < NO; i++) y[c0 + i] = from_f32<BF16>(o[i] + (a.accum ? bf16_to_f32(y[c0 + i]) : 0.f));
   }
 }
 

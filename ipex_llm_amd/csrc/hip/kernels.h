@@ -119,7 +119,7 @@ void launch_kq_gemv(int fmt, bool bf16, const uint16_t* x, int M, int64_t K, con
 void launch_dense_glu(bool bf16, const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t I, int act,
                       uint16_t* out, hipStream_t st);
 void launch_dense_gemv(bool bf16, const uint16_t* x, int M, int64_t K, const uint16_t* w, int64_t N,
-                       const uint16_t* bias, uint16_t* out, hipStream_t st);
+                       const uint16_t* bias, uint16_t* out, hipStream_t st, bool trans_out = false);
 
 // ---- fp8 linear (fp8_gemm.hip): torch_fp8 qtypes on the f8f6f4 MFMA --------
 struct Fp8GemmArgs {

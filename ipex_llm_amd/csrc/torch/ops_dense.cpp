@@ -38,6 +38,25 @@ Tensor dense_linear_hip(const Tensor& x, const Tensor& w, const c10::optional<Te
   return y;
 }
 
+// y^T = (x W^T)^T, [N, M]: the skinny GEMM with the roles swapped (training's
+// rank-r projections x A^T: "x" = the r factor rows, "w" = the token rows)
+// written straight in the caller's [tokens, r] layout; K % 64 == 0, <= 16 rows
+Tensor dense_linear_t_hip(const Tensor& x, const Tensor& w) {
+  c10::DeviceGuard g(x.device());
+  const int64_t K = x.size(-1), N = w.size(0);
+  const int64_t M = x.numel() / K;
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.is_contiguous() && x.is_contiguous() && K % 64 == 0 && M <= 16 &&
+                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) &&
+                  w.scalar_type() == x.scalar_type(),
+              "dense_linear_t: one 16-bit dtype, contiguous, K % 64 == 0, <= 16 rows");
+  Tensor y = at::empty({N, M}, x.options());
+  if (M > 0 && N > 0)
+    illm::launch_dense_gemv(x.scalar_type() == at::kBFloat16, (const uint16_t*)x.data_ptr(), (int)M, K,
+                            (const uint16_t*)w.data_ptr(), N, nullptr, (uint16_t*)y.data_ptr(),
+                            at::hip::getCurrentHIPStream().stream(), true);
+  return y;
+}
+
 // act(x Wg^T) * (x Wu^T) over a 16-row tile-interleaved gate/up weight [2I, K]
 Tensor dense_glu_hip(const Tensor& x, const Tensor& w, int64_t act) {
   c10::DeviceGuard g(x.device());
@@ -64,6 +83,7 @@ Tensor dense_glu_hip(const Tensor& x, const Tensor& w, int64_t act) {
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("dense_linear(Tensor x, Tensor w, Tensor? bias) -> Tensor");
   m.def("dense_glu(Tensor x, Tensor w, int act=0) -> Tensor");
+  m.def("dense_linear_t(Tensor x, Tensor w) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
@@ -73,4 +93,5 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CPU, m) {
 TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("dense_linear", &dense_linear_hip);
   m.impl("dense_glu", &dense_glu_hip);
+  m.impl("dense_linear_t", &dense_linear_t_hip);
 }

@@ -361,7 +361,7 @@ static int g8_auto_split(int64_t M, int64_t N, int64_t K) {
 // kernel = 1: the experimental 4-wave 128 x 128-per-wave kernel
 // (gemm_4w.hip; bf16 out, no bias, K % 128 == 0)
 Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool out_f32, int64_t kernel,
-                 bool glu, int64_t act, int64_t ksplit) {
+                 bool glu, int64_t act, int64_t ksplit, const c10::optional<Tensor>& out_opt, bool accumulate) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
               "gemm_bf16: bf16 GPU tensors");
   TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1, "gemm_bf16: w must be [N, K] with unit inner stride");
@@ -376,8 +376,21 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   const int64_t NO = glu ? N / 2 : N;
   auto shape = x.sizes().vec();
   shape.back() = NO;
-  Tensor out = at::empty({M, NO}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
-  if (M == 0 || N == 0) return out.view(shape);
+  Tensor out;
+  int64_t ldo = NO;
+  if (out_opt.has_value()) {
+    // caller's buffer (a row slice of a larger tensor is fine): [M, NO], unit column stride
+    out = *out_opt;
+    TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.size(0) == M && out.size(1) == NO && out.stride(1) == 1 &&
+                    out.scalar_type() == (out_f32 ? at::kFloat : at::kBFloat16),
+                "gemm_bf16: out must be [M, N_out] with unit column stride and the output dtype");
+    ldo = out.stride(0);
+  } else {
+    TORCH_CHECK(!accumulate, "gemm_bf16: accumulate needs out");
+    out = at::empty({M, NO}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  }
+  TORCH_CHECK(!accumulate || (!out_f32 && !glu && kernel == 0), "gemm_bf16: accumulate is bf16 out, no GLU");
+  if (M == 0 || N == 0) return out_opt.has_value() ? out : out.view(shape);
   TORCH_CHECK(w.stride(0) % 8 == 0, "gemm_bf16: w row stride must be a multiple of 8 elements");
   const int64_t xb = (M - 1) * x2.stride(0) * 2 + K * 2, wb = (N - 1) * w.stride(0) * 2 + K * 2;
   TORCH_CHECK(xb < (int64_t)UINT32_MAX && wb < (int64_t)UINT32_MAX, "gemm_bf16: operands over 4 GiB");
@@ -394,16 +407,18 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   a.K = (int)K;
   a.ldx = (int)x2.stride(0);
   a.ldw = (int)w.stride(0);
-  a.ldo = (int)NO;
+  a.ldo = (int)ldo;
   a.out_f32 = out_f32 ? 1 : 0;
   a.glu = glu ? 1 : 0;
   a.act = (int)act;
+  a.accum = accumulate ? 1 : 0;
   a.x_bytes = (uint32_t)xb;
   a.w_bytes = (uint32_t)wb;
   a.w_fmt = -1;
   const auto st = at::hip::getCurrentHIPStream().stream();
   if (kernel == 1) {
     TORCH_CHECK(!bias.has_value() && !out_f32 && K % 128 == 0, "gemm_bf16(kernel=1): bf16 out, no bias, K % 128 == 0");
+    TORCH_CHECK(!out_opt.has_value(), "gemm_bf16(kernel=1): no out");
     illm::launch_gemm4w(a, st);
     return out.view(shape);
   }
@@ -416,7 +431,7 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   }
   illm::launch_gemm8p(a, st);
   if (S > 1) illm::launch_gemm8p_finish(a, st);
-  return out.view(shape);
+  return out_opt.has_value() ? out : out.view(shape);
 }
 
 // low-bit weights (tiled device blob, sym_int4 / nf4 / nf3) decoded to bf16
@@ -469,7 +484,7 @@ Tensor gemm8p_lowbit(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n
 TORCH_LIBRARY_FRAGMENT(ipex_llm_amd, m) {
   m.def("mfgemm(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias=None, bool glu=False, int act=0, int tile=-1, int ksplit=0) -> Tensor");
   m.def("x_to_f16_rowscale(Tensor x) -> Tensor[]");
-  m.def("gemm_bf16(Tensor x, Tensor w, Tensor? bias=None, bool out_f32=False, int kernel=0, bool glu=False, int act=0, int ksplit=-1) -> Tensor");
+  m.def("gemm_bf16(Tensor x, Tensor w, Tensor? bias=None, bool out_f32=False, int kernel=0, bool glu=False, int act=0, int ksplit=-1, Tensor(a!)? out=None, bool accumulate=False) -> Tensor");
   m.def("gemm8p_lowbit(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias=None, bool out_f32=False, bool glu=False, int act=0) -> Tensor");
   m.def("mfgemm_nn(Tensor g, Tensor w, int fmt, int n, int k, int tile=-1, int ksplit=0) -> Tensor");
   m.def("mfgemm_lora(Tensor x, Tensor w, int fmt, int n, int k, Tensor? bias, Tensor la, Tensor lb, float s) -> Tensor[]");

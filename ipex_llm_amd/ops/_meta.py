@@ -320,7 +320,9 @@ def _(g, w, fmt, n, k, la, lb, s):
 
 
 @register_fake("ipex_llm_amd::gemm_bf16")
-def _(x, w, bias=None, out_f32=False, kernel=0, glu=False, act=0, ksplit=-1):
+def _(x, w, bias=None, out_f32=False, kernel=0, glu=False, act=0, ksplit=-1, out=None, accumulate=False):
+    if out is not None:
+        return out
     shape = list(x.shape)
     shape[-1] = w.shape[0] // 2 if glu else w.shape[0]
     return x.new_empty(shape, dtype=torch.float32 if out_f32 else x.dtype)
@@ -342,3 +344,8 @@ def _(xq, sx, w, ws, e5m2):
 def _gemv_argmax(x, blob, fmt, n, k, bias=None):
     M = x.numel() // k
     return x.new_empty(*x.shape[:-1], n), x.new_empty(((n + 15) // 16, M, 2), dtype=torch.float32)
+
+
+@register_fake("ipex_llm_amd::dense_linear_t")
+def _(x, w):
+    return x.new_empty((w.shape[0], x.numel() // x.shape[-1]))

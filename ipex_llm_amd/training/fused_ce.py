@@ -67,7 +67,7 @@ class _FusedLinearCE(torch.autograd.Function):
             loss_rows[c0:c1] = ops.ce_fused_(logits, labels[c0:c1], ignore_index, 1.0 if grad_h is not None else 0.0)
             if grad_h is not None:
                 if g8:
-                    grad_h[c0:c1] = ops.gemm_bf16(logits, wt)
+                    ops.gemm_bf16(logits, wt, None, False, 0, False, 0, -1, grad_h[c0:c1])
                 else:
                     torch.mm(logits, w, out=grad_h[c0:c1])
             del logits

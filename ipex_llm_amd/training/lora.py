@@ -164,16 +164,13 @@ def _skinny(x2: torch.Tensor, W: torch.Tensor, alpha: float = 1.0) -> torch.Tens
     from .. import ops
     r, K = W.shape
     if (_SKINNY and x2.is_cuda and ops.native_gpu(x2) and x2.dtype in (torch.bfloat16, torch.float16)
-            and W.dtype == x2.dtype and x2.is_contiguous() and K % 8 == 0 and r <= 64
+            and W.dtype == x2.dtype and x2.is_contiguous() and K % 64 == 0 and r <= 64
             and x2.shape[0] >= 64):
         Wc = (W * alpha if alpha != 1.0 else W).contiguous()
-        dl = torch.ops.ipex_llm_amd.dense_linear
+        dlt = torch.ops.ipex_llm_amd.dense_linear_t            # [tokens, rows] straight from the kernel
         if r <= 16:
-            return dl(Wc, x2, None).t().contiguous()
-        out = x2.new_empty(x2.shape[0], r)
-        for c0 in range(0, r, 16):
-            out[:, c0:c0 + 16] = dl(Wc[c0:c0 + 16], x2, None).t()
-        return out
+            return dlt(Wc, x2)
+        return torch.cat([dlt(Wc[c0:c0 + 16].contiguous(), x2) for c0 in range(0, r, 16)], 1)
     if alpha == 1.0:
         return torch.mm(x2, W.t())
     return torch.addmm(x2.new_empty(()), x2, W.t(), beta=0, alpha=alpha)
@@ -194,10 +191,13 @@ def _g8_bwd_ok(g2: torch.Tensor, base) -> bool:
             and use_g8d(g2, g2.shape[0], base.in_features, N))
 
 
-def _g8_grad_x(g2: torch.Tensor, base) -> torch.Tensor:
+def _g8_grad_x(g2: torch.Tensor, base, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """g W (+ acc, added in the GEMM epilogue: sibling adapters' grad_x)"""
     wt = torch.ops.ipex_llm_amd.dequantize_device(base.weight, base.fmt, base.out_features, base.in_features,
                                                    g2.dtype, True)          # W^T [K, N]
-    return torch.ops.ipex_llm_amd.gemm_bf16(g2, wt)
+    if acc is None:
+        return torch.ops.ipex_llm_amd.gemm_bf16(g2, wt)
+    return torch.ops.ipex_llm_amd.gemm_bf16(g2, wt, None, False, 0, False, 0, -1, acc, True)
 
 
 def _base_dense_weight(base, dt):
@@ -469,8 +469,7 @@ class _LoraGroupFn(torch.autograd.Function):
             jobs.append((xa_all[:, off:off + r], g2, 1.0 if ctx.kcat else s, True))
             if ctx.needs_input_grad[0]:
                 if not ctx.kcat and _g8_bwd_ok(g2, base):
-                    gi = _g8_grad_x(g2, base)
-                    gx = gi if gx is None else gx.add_(gi)
+                    gx = _g8_grad_x(g2, base, acc=gx)          # siblings accumulate in the GEMM epilogue
                 else:
                     w = (_aug_weight(base, ctx.kcat[0], off, ctx.kcat[1])[:, :base.in_features] if ctx.kcat
                          else _base_dense_weight(base, x2.dtype))
@@ -852,6 +851,8 @@ def enable_training_kernels(model: nn.Module) -> nn.Module:
     if os.environ.get("ILLM_TRAIN_ATTN", "1") == "1":
         from .flash_attn import patch_flash_attention
         patch_flash_attention(model)
+    if os.environ.get("ILLM_TRAIN_ROPE", "1") == "1":
+        _patch_rotary(model)
     # Default: the pure low-bit footprint -- each base GEMM dequantizes its
     # weight (forward) or W^T (grad_x) into a transient buffer for the dense
     # 8-phase kernel.  ILLM_TRAIN_DENSE_GB=<GiB> (or "auto": min(48, HBM / 4)
@@ -869,6 +870,29 @@ def enable_training_kernels(model: nn.Module) -> nn.Module:
             set_dense_budget(gb)
     model._illm_train_dense_gb = gb
     return model
+
+
+def _patch_rotary(model: nn.Module) -> int:
+    """HF rotary-embedding modules (default rope: ``inv_freq``,
+    ``attention_scaling``) compute cos / sin with a batched f32 matmul of the
+    [D/2, 1] frequencies by the [1, T] positions -- a K = 1 library GEMM per
+    forward.  The same products as one broadcast multiply (exact: each entry
+    is a single f32 product either way)."""
+    n = 0
+    for name, m in model.named_modules():
+        if not name.endswith("rotary_emb") or not hasattr(m, "inv_freq") or not hasattr(m, "attention_scaling"):
+            continue
+        if getattr(m, "rope_type", "default") != "default" or getattr(m, "_illm_rope", False):
+            continue
+
+        def fwd(x, position_ids, _m=m):
+            freqs = position_ids[:, :, None].float() * _m.inv_freq.float()[None, None, :]
+            emb = torch.cat((freqs, freqs), dim=-1)
+            return (emb.cos() * _m.attention_scaling).to(x.dtype), (emb.sin() * _m.attention_scaling).to(x.dtype)
+        m.forward = fwd
+        m._illm_rope = True
+        n += 1
+    return n
 
 
 def cast_lora_weight(model: nn.Module, dtype=torch.bfloat16):

@@ -50,3 +50,17 @@ def test_dense_mfma_rows_independent_of_batch(dt):
     for M in (1, 3, 7):
         assert torch.equal(torch.ops.ipex_llm_amd.dense_linear(x[:M].contiguous(), w, None), full[:M])
         assert torch.equal(torch.ops.ipex_llm_amd.dense_glu(x[:M].contiguous(), wgu, 0), gfull[:M])
+
+
+@pytest.mark.parametrize("r", [8, 16])
+def test_dense_linear_t_matches(r):
+    """the transposed-output skinny GEMM (training's x A^T in [tokens, r])"""
+    ops.require()
+    torch.manual_seed(r)
+    x2 = torch.randn(1536, 4096, device="cuda").bfloat16()
+    A = (torch.randn(r, 4096, device="cuda") * 0.05).bfloat16()
+    y = torch.ops.ipex_llm_amd.dense_linear_t(A, x2)
+    assert y.shape == (1536, r) and y.is_contiguous()
+    assert torch.equal(y, torch.ops.ipex_llm_amd.dense_linear(A, x2, None).t().contiguous())
+    ref = x2.float() @ A.float().t()
+    assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2

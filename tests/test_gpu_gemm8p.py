@@ -164,3 +164,26 @@ def test_gemm_bf16_glu_epilogue(cuda, S, act):
     y = torch.ops.ipex_llm_amd.gemm_bf16(x, w, None, False, 0, True, act, S)
     assert y.shape == (M, I)
     assert _rel(y, ref) < 8e-3
+
+
+@pytest.mark.parametrize("S", [1, 3])
+def test_gemm_bf16_out_slice_and_accumulate(cuda, S):
+    """out= a row slice of a larger buffer (strided rows), accumulate=True:
+    out += x w^T with one rounding, plain and split-K"""
+    torch.manual_seed(9 + S)
+    M, N, K = 700, 1024, 2048
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
+    big = torch.randn(M + 50, N + 64, device=cuda).bfloat16()
+    view = big[10:10 + M, 32:32 + N]
+    big0 = big.clone()
+    old = view.float().clone()
+    y = torch.ops.ipex_llm_amd.gemm_bf16(x, w, None, False, 0, False, 0, S, view, True)
+    assert y.data_ptr() == view.data_ptr()
+    ref = old + x.float() @ w.float().t()
+    assert _rel(view, ref) < 8e-3
+    assert torch.equal(big[:10], big0[:10]) and torch.equal(big[10 + M:], big0[10 + M:])
+    assert torch.equal(big[:, :32], big0[:, :32]) and torch.equal(big[:, 32 + N:], big0[:, 32 + N:])
+    z = torch.empty(M, N, device=cuda).bfloat16()
+    torch.ops.ipex_llm_amd.gemm_bf16(x, w, None, False, 0, False, 0, S, z)
+    assert _rel(z, x.float() @ w.float().t()) < 8e-3

@@ -400,3 +400,20 @@ def test_link_lora_groups_skips_cross_attention():
     assert link_lora_groups(peft) == 1
     assert "_lora_group" in m[0].self_attn.q_proj.__dict__
     assert "_lora_group" not in m[0].encoder_attn.q_proj.__dict__
+
+
+def test_rotary_patch_matches_hf():
+    """the training rotary-embedding patch (broadcast multiply instead of the
+    K = 1 f32 matmul) returns HF's cos / sin bit for bit"""
+    from transformers import LlamaConfig
+    from transformers.models.llama.modeling_llama import LlamaRotaryEmbedding
+    from ipex_llm_amd.training.lora import _patch_rotary
+    cfg = LlamaConfig(hidden_size=256, num_attention_heads=4, max_position_embeddings=512, rope_theta=500000.0)
+    holder = torch.nn.Module()
+    holder.rotary_emb = LlamaRotaryEmbedding(cfg)
+    x = torch.randn(2, 7, 256, dtype=torch.bfloat16)
+    pos = torch.tensor([[0, 1, 2, 3, 4, 5, 6], [10, 11, 12, 300, 301, 302, 511]])
+    c0, s0 = holder.rotary_emb(x, pos)
+    assert _patch_rotary(holder) == 1
+    c1, s1 = holder.rotary_emb(x, pos)
+    assert torch.equal(c0, c1) and torch.equal(s0, s1)
