@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
 
   // ---- block -> (m-block, n-block): XCD remap, then groups of 4 m-blocks
   const int MB = (a.M + 255) / 256, NB = (a.N + 255) / 256;
-  const int S = DENSE && !FP8 && a.ksplit > 1 ? a.ksplit : 1;
+  const int S = DENSE && a.ksplit > 1 ? a.ksplit : 1;
   const int total = MB * NB * S;
   // split-K: the S workgroups of one output tile are adjacent ids (one XCD's
   // L2 serves their shared nothing but keeps the grouping of the tiles intact)
@@ -609,9 +609,18 @@ __global__ void __launch_bounds__(256) gemm8p_finish_kernel(const G8Args a) {
       const int pr = c / 16, j = c % 16;
       const float gv = at(pr * 32 + j), uv = at(pr * 32 + 16 + j);
       o[i] = (a.act == 0 ? silu_f(gv) : gelu_tanh_f(gv)) * uv;
+    } else if (a.w_fmt == G8_FP8) {              // fp8: row x column scales, 16-bit bias
+      const float cs = a.sw_per_channel ? a.sw[c] : a.sw[0];
+      o[i] = at(c) * a.sx[m] * cs + (a.bias ? (a.out_f16 ? f16_to_f32(a.bias[c]) : bf16_to_f32(a.bias[c])) : 0.f);
     } else {
       o[i] = at(c) + (a.bias ? bf16_to_f32(a.bias[c]) : 0.f);
     }
+  }
+  if (a.out_f16) {
+    uint16_t* yh = (uint16_t*)a.out + m * a.ldo;
+    if (c0 + 3 < NO && ((a.ldo | c0) & 3) == 0) *(uint2*)(yh + c0) = make_uint2(pack2<F16>(o[0], o[1]), pack2<F16>(o[2], o[3]));
+    else for (int i = 0; i < 4 && c0 + i < NO; i++) yh[c0 + i] = from_f32<F16>(o[i]);
+    return;
   }
   if (a.out_f32) {
     float* yf = (float*)a.out + m * a.ldo;
@@ -626,6 +635,22 @@ __global__ void __launch_bounds__(256) gemm8p_finish_kernel(const G8Args a) {
   } else {
     for (int i = 0; i < 4 && c0 + i < NO; i++) y[c0 + i] = from_f32<BF16>(o[i] + (a.accum ? bf16_to_f32(y[c0 + i]) : 0.f));
   }
+}
+
+int gemm8p_auto_split(int64_t M, int64_t N, int64_t ktiles) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  if (tiles * 2 > cus) return 1;
+  int64_t s = cus / tiles;
+  s = s < 8 ? s : 8;
+  s = s < ktiles / 8 ? s : ktiles / 8;
+  return (int)(s > 1 ? s : 1);
 }
 
 void launch_gemm8p_finish(const G8Args& a, hipStream_t st) {
@@ -644,7 +669,7 @@ void launch_gemm8p(const G8Args& a0, hipStream_t st) {
     a.gm = gm_env;
   }
   const int MB = (a.M + 255) / 256, NB = (a.N + 255) / 256;
-  const int S = a.w_fmt == -1 && a.ksplit > 1 ? a.ksplit : 1;
+  const int S = (a.w_fmt == -1 || a.w_fmt == G8_FP8) && a.ksplit > 1 ? a.ksplit : 1;
   const dim3 grid((unsigned)(MB * NB * S)), blk(512);
   if (a.w_fmt == G8_FP8 && a.w_e5m2) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8 - 1>, grid, blk, 0, st, a);
   else if (a.w_fmt == G8_FP8) hipLaunchKernelGGL(g8::gemm8p_kernel<G8_FP8>, grid, blk, 0, st, a);

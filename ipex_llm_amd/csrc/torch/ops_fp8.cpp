@@ -103,7 +103,18 @@ static void launch_fp8_8p(const Tensor& xq, const Tensor& sx, const Tensor& w, c
   a.sw_per_channel = ws.numel() == N ? 1 : 0;
   a.w_e5m2 = e5m2 ? 1 : 0;
   a.out_f16 = y.scalar_type() == at::kHalf ? 1 : 0;
-  illm::launch_gemm8p(a, at::hip::getCurrentHIPStream().stream());
+  const auto st = at::hip::getCurrentHIPStream().stream();
+  // grids smaller than the chip (M = 1024: qkv / o / down) split K into f32
+  // slabs reduced (with the scales, bias, rounding) by the finishing launch
+  const int S = illm::gemm8p_auto_split(M, N, K / 128);
+  Tensor slabs;
+  if (S > 1) {
+    slabs = at::empty({(int64_t)S, M, N}, y.options().dtype(at::kFloat));
+    a.ksplit = S;
+    a.ws = slabs.data_ptr<float>();
+  }
+  illm::launch_gemm8p(a, st);
+  if (S > 1) illm::launch_gemm8p_finish(a, st);
 }
 
 // kernel-only entry for benchmarks: pre-quantized activations

@@ -339,21 +339,8 @@ std::vector<Tensor> x_to_f16_rowscale(const Tensor& x) {
 // dense bf16 NT GEMM on the 8-phase 256 x 256 kernel (gemm_8p.hip):
 // split-K factor of the dense 8-phase GEMM: a grid of fewer 256 x 256 tiles
 // than CUs (M = 1024: qkv / o / down give 64-96 tiles for 256 CUs) splits K
-// so the launch fills the chip (each split >= 8 K-tiles); full grids keep 1
-static int g8_auto_split(int64_t M, int64_t N, int64_t K) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
-  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256), T = K / 64;
-  if (tiles * 2 > cus) return 1;
-  int64_t s = cus / tiles;
-  s = std::min<int64_t>(s, std::min<int64_t>(8, T / 8));
-  return (int)std::max<int64_t>(1, s);
-}
+// so the launch fills the chip (gemm8p_auto_split); full grids keep 1
+static int g8_auto_split(int64_t M, int64_t N, int64_t K) { return illm::gemm8p_auto_split(M, N, K / 64); }
 
 // y[M, N] = x[M, K] @ w[N, K]^T (+ bias), bf16 or f32 out; K % 64 == 0.
 // glu: w rows are 16-row gate/up tile pairs, y [M, N/2] = act(gate) * up.
