@@ -557,10 +557,16 @@ __global__ void __launch_bounds__(512) gemm8p_kernel(const G8Args a) {
       }
       if (a.out_f32) {
         float* y = (float*)a.out + (size_t)m * a.ldo + n;
-        if (n + 3 < a.N && ((a.ldo | n) & 3) == 0) *(float4*)y = make_float4(o0, o1, o2, o3);
-        else {
+        if (n + 3 < a.N && ((a.ldo | n) & 3) == 0) {
+          float4 v = make_float4(o0, o1, o2, o3);
+          if (a.accum) {
+            const float4 ov = *(const float4*)y;
+            v.x += ov.x, v.y += ov.y, v.z += ov.z, v.w += ov.w;
+          }
+          *(float4*)y = v;
+        } else {
           const float o[4] = {o0, o1, o2, o3};
-          for (int i = 0; i < 4 && n + i < a.N; i++) y[i] = o[i];
+          for (int i = 0; i < 4 && n + i < a.N; i++) y[i] = o[i] + (a.accum ? y[i] : 0.f);
         }
       } else {
         uint16_t* y = (uint16_t*)a.out + (size_t)m * a.ldo + n;
@@ -624,7 +630,7 @@ __global__ void __launch_bounds__(256) gemm8p_finish_kernel(const G8Args a) {
   }
   if (a.out_f32) {
     float* yf = (float*)a.out + m * a.ldo;
-    for (int i = 0; i < 4 && c0 + i < NO; i++) yf[c0 + i] = o[i];
+    for (int i = 0; i < 4 && c0 + i < NO; i++) yf[c0 + i] = o[i] + (a.accum ? yf[c0 + i] : 0.f);
   } else if (c0 + 3 < NO && ((a.ldo | c0) & 3) == 0) {
     if (a.accum) {
       const uint2 ov = *(const uint2*)(y + c0);

@@ -29,7 +29,7 @@ struct G8Args {
   int ksplit;
   float* ws;
   int gm;                 // m-blocks per rasterization group (0: 4)
-  int accum;              // dense bf16 out (no GLU): out += x w^T instead of out =
+  int accum;              // dense, no GLU: out += x w^T instead of out = (bf16: one rounding of old + sum)
 };
 constexpr int G8_FP8 = -2;
 

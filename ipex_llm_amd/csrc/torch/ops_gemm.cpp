@@ -376,7 +376,7 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
     TORCH_CHECK(!accumulate, "gemm_bf16: accumulate needs out");
     out = at::empty({M, NO}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   }
-  TORCH_CHECK(!accumulate || (!out_f32 && !glu && kernel == 0), "gemm_bf16: accumulate is bf16 out, no GLU");
+  TORCH_CHECK(!accumulate || (!glu && kernel == 0), "gemm_bf16: accumulate: no GLU");
   if (M == 0 || N == 0) return out_opt.has_value() ? out : out.view(shape);
   TORCH_CHECK(w.stride(0) % 8 == 0, "gemm_bf16: w row stride must be a multiple of 8 elements");
   const int64_t xb = (M - 1) * x2.stride(0) * 2 + K * 2, wb = (N - 1) * w.stride(0) * 2 + K * 2;

@@ -15,9 +15,9 @@ turns them into the per-row loss and, IN PLACE, the logits gradient
 for the gradient, and the hidden-state gradient is the second GEMM
 (dlogits @ W) of that chunk -- computed during the forward, since the only
 consumer of the loss is a scalar backward.  That second GEMM reduces over
-the vocabulary: on the NT 8-phase kernel its operand is W^T, a transposed copy
-of the frozen head kept for the head's lifetime (1 GB for Llama-3-8B; the
-kernel's split-K fills the chip at 2048-row chunks).  Nothing of size [tokens, vocab]
+the vocabulary: on the NT 8-phase kernel its operand is W^T, transposed one
+vocabulary slice at a time (no resident copy of the head), the slices'
+products accumulated in f32 by the kernel epilogue.  Nothing of size [tokens, vocab]
 outlives a chunk; backward is one scale of the stored [tokens, hidden]
 gradient.  The lm_head weight is frozen here (QLoRA); a trainable head
 falls back to the unfused path.
@@ -30,24 +30,17 @@ from typing import Optional
 import torch
 
 CHUNK = int(os.environ.get("ILLM_CE_CHUNK", "2048"))
+# vocabulary slice of the grad_h GEMM: its W^T operand is transposed per slice
+# (VCHUNK x hidden at a time) instead of a resident transposed copy of the
+# whole head (1 GB for Llama-3-8B)
+VCHUNK = int(os.environ.get("ILLM_CE_VCHUNK", "32768"))
 _LIB = os.environ.get("ILLM_CE_LIB", "0") == "1"
-_wt_cache = {}     # id(weight) -> (weakref to weight, version, W^T)
 
 
 def _g8_ok(h, w) -> bool:
     from .. import ops
     return (not _LIB and h.is_cuda and ops.native_gpu(h) and h.dtype == torch.bfloat16 and w.dtype == h.dtype
             and h.shape[1] % 64 == 0 and w.shape[0] % 64 == 0 and hasattr(torch.ops.ipex_llm_amd, "gemm_bf16"))
-
-
-def _transposed(w):
-    import weakref
-    ent = _wt_cache.get(id(w))
-    if ent is not None and ent[0]() is w and ent[1] == w._version:
-        return ent[2]
-    wt = w.t().contiguous()
-    _wt_cache[id(w)] = (weakref.ref(w, lambda r, k=id(w): _wt_cache.pop(k, None)), w._version, wt)
-    return wt
 
 
 class _FusedLinearCE(torch.autograd.Function):
@@ -59,15 +52,22 @@ class _FusedLinearCE(torch.autograd.Function):
         V = weight.shape[0]
         loss_rows = torch.empty(T, device=h.device, dtype=torch.float32)
         grad_h = torch.empty_like(h) if h.requires_grad else None
-        g8 = _g8_ok(h, w)
-        wt = _transposed(w) if g8 and grad_h is not None else None
+        g8 = _g8_ok(h, w) and V % 64 == 0
         for c0 in range(0, T, CHUNK):
             c1 = min(T, c0 + CHUNK)
             logits = ops.gemm_bf16(h[c0:c1], w) if g8 else torch.mm(h[c0:c1], w.t())
             loss_rows[c0:c1] = ops.ce_fused_(logits, labels[c0:c1], ignore_index, 1.0 if grad_h is not None else 0.0)
             if grad_h is not None:
                 if g8:
-                    ops.gemm_bf16(logits, wt, None, False, 0, False, 0, -1, grad_h[c0:c1])
+                    # dlogits @ W, one vocabulary slice at a time, f32 accumulation
+                    acc = torch.empty(c1 - c0, H, device=h.device, dtype=torch.float32)
+                    for v0 in range(0, V, VCHUNK):
+                        v1 = min(V, v0 + VCHUNK)
+                        wt = w[v0:v1].t().contiguous()                       # [H, v1 - v0]
+                        ops.gemm_bf16(logits[:, v0:v1], wt, None, True, 0, False, 0, -1, acc, v0 > 0)
+                        del wt
+                    grad_h[c0:c1] = acc
+                    del acc
                 else:
                     torch.mm(logits, w, out=grad_h[c0:c1])
             del logits
