@@ -39,8 +39,6 @@ void launch_gemm8p_finish(const G8Args& a, hipStream_t st);
 // split-K factor for a grid of fewer 256 x 256 tiles than half the CUs (each
 // split >= 8 K-tiles; 1 = no split)
 int gemm8p_auto_split(int64_t M, int64_t N, int64_t ktiles);
-// dense bf16 only, bf16 out, no bias / GLU, K % 128 == 0 (gemm_4w.hip)
-void launch_gemm4w(const G8Args& a, hipStream_t st);
 bool gemm8p_supports(int fmt);
 
 }  // namespace illm

@@ -345,8 +345,8 @@ static int g8_auto_split(int64_t M, int64_t N, int64_t K) { return illm::gemm8p_
 // y[M, N] = x[M, K] @ w[N, K]^T (+ bias), bf16 or f32 out; K % 64 == 0.
 // glu: w rows are 16-row gate/up tile pairs, y [M, N/2] = act(gate) * up.
 // ksplit: -1 auto (g8_auto_split), 1 off, else the split-K factor.
-// kernel = 1: the experimental 4-wave 128 x 128-per-wave kernel
-// (gemm_4w.hip; bf16 out, no bias, K % 128 == 0)
+// kernel: 0 (the 4-wave 128 x 128-per-wave variant measured 0.70-0.77x
+// hipBLASLt in round 4 and was removed in round 5)
 Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool out_f32, int64_t kernel,
                  bool glu, int64_t act, int64_t ksplit, const c10::optional<Tensor>& out_opt, bool accumulate) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16,
@@ -354,7 +354,7 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1, "gemm_bf16: w must be [N, K] with unit inner stride");
   const int64_t K = w.size(1), N = w.size(0);
   TORCH_CHECK(x.size(-1) == K && K % 64 == 0 && K > 0, "gemm_bf16: K must match and be a multiple of 64");
-  TORCH_CHECK(!glu || (N % 32 == 0 && !out_f32 && !bias.has_value() && kernel == 0),
+  TORCH_CHECK(!glu || (N % 32 == 0 && !out_f32 && !bias.has_value()),
               "gemm_bf16: GLU needs N % 32 == 0, bf16 out, no bias");
   c10::DeviceGuard g(x.device());
   Tensor x2 = x.reshape({-1, K});
@@ -376,7 +376,7 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
     TORCH_CHECK(!accumulate, "gemm_bf16: accumulate needs out");
     out = at::empty({M, NO}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
   }
-  TORCH_CHECK(!accumulate || (!glu && kernel == 0), "gemm_bf16: accumulate: no GLU");
+  TORCH_CHECK(!accumulate || !glu, "gemm_bf16: accumulate: no GLU");
   if (M == 0 || N == 0) return out_opt.has_value() ? out : out.view(shape);
   TORCH_CHECK(w.stride(0) % 8 == 0, "gemm_bf16: w row stride must be a multiple of 8 elements");
   const int64_t xb = (M - 1) * x2.stride(0) * 2 + K * 2, wb = (N - 1) * w.stride(0) * 2 + K * 2;
@@ -403,12 +403,7 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
   a.w_bytes = (uint32_t)wb;
   a.w_fmt = -1;
   const auto st = at::hip::getCurrentHIPStream().stream();
-  if (kernel == 1) {
-    TORCH_CHECK(!bias.has_value() && !out_f32 && K % 128 == 0, "gemm_bf16(kernel=1): bf16 out, no bias, K % 128 == 0");
-    TORCH_CHECK(!out_opt.has_value(), "gemm_bf16(kernel=1): no out");
-    illm::launch_gemm4w(a, st);
-    return out.view(shape);
-  }
+  TORCH_CHECK(kernel == 0, "gemm_bf16: kernel must be 0");
   const int S = ksplit < 0 ? g8_auto_split(M, N, K) : (int)std::max<int64_t>(1, std::min<int64_t>(ksplit, K / 64));
   Tensor ws;
   if (S > 1) {

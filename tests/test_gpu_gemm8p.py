@@ -22,20 +22,6 @@ def test_gemm_bf16_matches_fp32(cuda, M, N, K):
     assert _rel(y, ref) < 8e-3, (M, N, K)
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (1, 8, 128), (300, 520, 384), (1024, 4096, 4096),
-                                   (4096, 1000, 1024), (2048, 6144, 4096)])
-def test_gemm_bf16_4wave_matches_fp32(cuda, M, N, K):
-    """the 4-wave 128 x 128-per-wave kernel (gemm_4w.hip, kernel=1)"""
-    torch.manual_seed(M + N + 1)
-    x = torch.randn(M, K, device=cuda).bfloat16()
-    w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
-    ref = x.float() @ w.float().t()
-    y = torch.ops.ipex_llm_amd.gemm_bf16(x, w, None, False, 1)
-    assert y.dtype == torch.bfloat16 and y.shape == (M, N)
-    assert _rel(y, ref) < 8e-3, (M, N, K)
-    assert torch.equal(y, torch.ops.ipex_llm_amd.gemm_bf16(x, w, None, False, 1))
-
-
 def test_gemm_bf16_bias_f32_out_strided(cuda):
     torch.manual_seed(5)
     M, N, K = 640, 768, 512

@@ -62,21 +62,16 @@ def main():
             x = torch.randn(M, k, device=dev, dtype=torch.bfloat16)
             w = torch.randn(n, k, device=dev, dtype=torch.bfloat16) * 0.02
             # interleaved rounds in one process (methodology rule 24)
-            ours, lib, w4 = [], [], []
+            ours, lib = [], []
             for _ in range(3):
                 ours.append(timeit(lambda: torch.ops.ipex_llm_amd.gemm_bf16(x, w)))
                 lib.append(timeit(lambda: F.linear(x, w)))
-                w4.append(timeit(lambda: torch.ops.ipex_llm_amd.gemm_bf16(x, w, None, False, 1)))
-            o, l, o4 = min(ours), min(lib), min(w4)
-            y4 = torch.ops.ipex_llm_amd.gemm_bf16(x, w, None, False, 1).float()
+            o, l = min(ours), min(lib)
             y1 = torch.ops.ipex_llm_amd.gemm_bf16(x, w).float()
             y2 = F.linear(x, w).float()
             rel = ((y1 - y2).norm() / y2.norm()).item()
             fl = 2 * M * n * k
-            rel4 = ((y4 - y2).norm() / y2.norm()).item()
             print(json.dumps({"M": M, "op": name, "N": n, "K": k, "ours_us": round(o, 1), "hipblaslt_us": round(l, 1),
-                              "w4_us": round(o4, 1), "w4_TF": round(fl / o4 / 1e6, 1), "w4_speedup": round(l / o4, 3),
-                              "w4_rel_diff": round(rel4, 5),
                               "ours_TF": round(fl / o / 1e6, 1), "lib_TF": round(fl / l / 1e6, 1),
                               "speedup": round(l / o, 3), "rel_diff": round(rel, 5)}), flush=True)
             del x, w
