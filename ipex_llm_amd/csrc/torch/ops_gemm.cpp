@@ -372,6 +372,15 @@ Tensor gemm_bf16(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& 
                     out.scalar_type() == (out_f32 ? at::kFloat : at::kBFloat16),
                 "gemm_bf16: out must be [M, N_out] with unit column stride and the output dtype");
     ldo = out.stride(0);
+    // the epilogue writes while other workgroups still read the operands
+    auto overlaps = [&](const Tensor& t) {
+      const char* o0 = (const char*)out.data_ptr();
+      const char* o1 = o0 + ((M - 1) * ldo + NO) * out.element_size();
+      const char* t0 = (const char*)t.data_ptr();
+      const char* t1 = t0 + t.numel() * t.element_size();
+      return o0 < t1 && t0 < o1;
+    };
+    TORCH_CHECK(!overlaps(x2) && !overlaps(w), "gemm_bf16: out must not overlap x or w");
   } else {
     TORCH_CHECK(!accumulate, "gemm_bf16: accumulate needs out");
     out = at::empty({M, NO}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
