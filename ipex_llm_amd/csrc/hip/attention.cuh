@@ -1169,9 +1169,10 @@ void launch_d(const AttnDecodeArgs& a, hipStream_t st) {
   if constexpr (D == 64 || D == 128) {
     if (v3_ok(a, D)) {
       if constexpr (D == 128) {
-        if (a.rq_part != nullptr) return launch_v3<T, D, true>(a, st);
+        if (a.rq_part != nullptr)
+          return a.rq_prerot && a.rq_bias == nullptr ? launch_v3<T, D, 2>(a, st) : launch_v3<T, D, 1>(a, st);
       }
-      return launch_v3<T, D, false>(a, st);
+      return launch_v3<T, D, 0>(a, st);
     }
   }
   // P V on MFMA (ILLM_ATTN_PVM=0 keeps the per-lane FMA form, for A/B runs)

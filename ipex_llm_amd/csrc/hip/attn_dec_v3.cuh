@@ -34,31 +34,82 @@
 namespace illm {
 
 constexpr int V3_KPW = 32;   // keys per wave
-#ifndef ILLM_ATTN_V3_MINW
-#define ILLM_ATTN_V3_MINW 1
+// waves per SIMD the register allocation must leave room for (hipcc
+// -DILLM_ATTN_V3_MINW=n forces one value): per mode, the most that compiles
+// without scratch spills -- q from memory 4 (118 VGPRs), pre-rotated fused
+// RoPE 3 (156), RoPE applied here 2.  At the default (1) hipcc took 188-276
+// VGPRs: 1-2 waves per SIMD, so the 576 four-wave workgroups of batch 8 ran in
+// more than one round over the 256 CUs
+#ifdef ILLM_ATTN_V3_MINW
+#define ILLM_V3_MINW(RQ) ILLM_ATTN_V3_MINW
+#else
+#define ILLM_V3_MINW(RQ) ((RQ) == 1 ? 2 : (RQ) == 2 ? 3 : 4)
 #endif
 
 // q / k / v of the new token from the qkv GEMV's f32 accumulator (fused
 // RoPE decode, Tq == 1): see attn_decode_v2_kernel (attention.cuh) for the
-// rounding contract; lane (r16, g) gets dims 32 s + 8 g + j, s < KSTEP
-template <typename T, int D>
+// rounding contract; lane (r16, g) gets dims 32 s + 8 g + j, s < KSTEP.
+// Loads and math are split: the kernel issues every accumulator / bias /
+// cos-sin load of the wave (load(), load_cs(), vload()) right behind its K / V
+// loads, straight-line, and only then does the math, so the fused-RoPE path
+// waits once, for the K / V round trip (the previous per-column load-use chain
+// behind a bias branch added one round trip per k-step after the K / V rows
+// arrived: 18.5 vs 14.1 us at batch 8, profiles/attn_dec_v3_r5.jsonl).
+// PRE: the qkv GEMV epilogue already rotated q / k and there is no bias (the
+// decoder's Llama path): no cos / sin, no bias registers.
+template <typename T, int D, bool PRE>
 struct V3Rope {
   static constexpr int KSTEP = D / 32;
-  const AttnDecodeArgs& a;
+  static constexpr int HS = KSTEP / 2;
+  struct Raw {            // the lane's KSTEP x 8 accumulator columns (+ bias)
+    float4 f[KSTEP][2];
+    uint4 bb[KSTEP];
+  };
+  struct CS {             // cos / sin of the lane's rotated dims (fast path)
+    float4 q[HS][4];
+  };
+  const AttnDecodeArgs a;   // by value: a reference member made hipcc copy the kernel arguments to scratch
   int b, g;
-  float rs;
+  float ss;
   int64_t rpos;
-  __device__ V3Rope(const AttnDecodeArgs& a_, int b_, int g_) : a(a_), b(b_), g(g_) {
-    rs = a.rq_ss ? rsqrtf(a.rq_ss[b] / (float)a.rq_ss_n + a.rq_ss_eps) : 1.f;
-    rpos = a.rq_pos[b];
+  __device__ V3Rope(const AttnDecodeArgs& a_, int b_, int g_, bool on) : a(a_), b(b_), g(g_) {
+    ss = on && a.rq_ss ? a.rq_ss[b] : 0.f;
+    rpos = on && !PRE ? a.rq_pos[b] : 0;
   }
+  __device__ float rs() const { return a.rq_ss ? rsqrtf(ss / (float)a.rq_ss_n + a.rq_ss_eps) : 1.f; }
+  __device__ bool fast_rot() const { return !PRE && a.rq_rot == D && !a.rq_interleaved; }
   __device__ static float rnd(float v) { return to_f32<T>(from_f32<T>(v)); }
-  __device__ void raw8(int col0, float* v) const {
-    const float4* p = (const float4*)(a.rq_part + (size_t)b * a.rq_ld + col0);
-    const float4 f0 = p[0], f1 = p[1];
+  // issue the loads of columns col0 + 32 s + 8 g .. + 8 (straight-line: the
+  // bias is read unconditionally from a valid address and selected away)
+  __device__ void load(int col0, Raw& r) const {
+    const float* p = a.rq_part + (size_t)b * a.rq_ld + col0 + 8 * g;
+    const bool hb = a.rq_bias != nullptr;
+    const uint16_t* bp = hb ? a.rq_bias + col0 + 8 * g : (const uint16_t*)p;
+#pragma unroll
+    for (int s = 0; s < KSTEP; s++) {
+      r.f[s][0] = *(const float4*)(p + 32 * s);
+      r.f[s][1] = *(const float4*)(p + 32 * s + 4);
+      if constexpr (!PRE) r.bb[s] = *(const uint4*)(bp + (hb ? 32 * s : 64 * s));
+    }
+  }
+  __device__ void load_cs(CS& c) const {
+    if (!fast_rot() || a.rq_prerot) return;
+    const float4* csp = (const float4*)a.rq_cos_sin + (size_t)rpos * (D / 4);
+#pragma unroll
+    for (int s = 0; s < HS; s++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) c.q[s][e] = csp[(32 * s + 8 * g) / 2 + e];
+  }
+  // the 8 columns at col .. col + 8 (value-row layout), loads only
+  __device__ void vload(int col, float4& f0, float4& f1, uint4& u) const {
+    const float* p = a.rq_part + (size_t)b * a.rq_ld + col;
+    f0 = *(const float4*)p;
+    f1 = *(const float4*)(p + 4);
+    if constexpr (!PRE) u = *(const uint4*)(a.rq_bias ? a.rq_bias + col : (const uint16_t*)p);
+  }
+  __device__ void vals8(const float4& f0, const float4& f1, const uint4& u, float rsv, float* v) const {
     float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (a.rq_bias) {
-      const uint4 u = *(const uint4*)(a.rq_bias + col0);
+    if (!PRE && a.rq_bias) {
       const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
       for (int e = 0; e < 4; e++) {
@@ -68,11 +119,17 @@ struct V3Rope {
     }
     const float f[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
 #pragma unroll
-    for (int j = 0; j < 8; j++) v[j] = rnd(bb[j] + rs * f[j]);
+    for (int j = 0; j < 8; j++) v[j] = rnd(bb[j] + rsv * f[j]);
   }
+  __device__ void vals(const Raw& r, float (&v)[KSTEP][8]) const {
+    const float rsv = rs();
+#pragma unroll
+    for (int s = 0; s < KSTEP; s++) vals8(r.f[s][0], r.f[s][1], r.bb[s], rsv, v[s]);
+  }
+  // general rotary (partial / interleaved): per-element reads, not the hot path
   __device__ float raw1(int col) const {
     float s = a.rq_bias ? to_f32<T>(a.rq_bias[col]) : 0.f;
-    s += rs * a.rq_part[(size_t)b * a.rq_ld + col];
+    s += rs() * a.rq_part[(size_t)b * a.rq_ld + col];
     return rnd(s);
   }
   __device__ float rot1(int col0, int d) const {
@@ -87,12 +144,10 @@ struct V3Rope {
     const float x0 = raw1(col0 + d0), x1 = raw1(col0 + d1);
     return first ? rnd(x0 * c) - rnd(x1 * sn) : rnd(x1 * c) + rnd(x0 * sn);
   }
-  // rotated (q: scaled by scale_out) fragments of the head starting at column col0
-  __device__ void frags(int col0, float scale_out, uint4* outf) const {
-    float v[KSTEP][8];
-#pragma unroll
-    for (int s = 0; s < KSTEP; s++) raw8(col0 + 32 * s + 8 * g, v[s]);
-    if (a.rq_prerot) {
+  // rotated (q: scaled by scale_out) fragments of the head at column col0
+  // from its values v (the lane's dims 32 s + 8 g + j)
+  __device__ void frags(int col0, const float (&v)[KSTEP][8], const CS& c, float scale_out, uint4* outf) const {
+    if (PRE || a.rq_prerot) {
 #pragma unroll
       for (int s = 0; s < KSTEP; s++) {
         uint32_t w[4];
@@ -100,16 +155,14 @@ struct V3Rope {
         for (int j = 0; j < 4; j++) w[j] = pack2<T>(v[s][2 * j] * scale_out, v[s][2 * j + 1] * scale_out);
         outf[s] = make_uint4(w[0], w[1], w[2], w[3]);
       }
-    } else if (a.rq_rot == D && !a.rq_interleaved) {
-      constexpr int HS = KSTEP / 2;
-      const float4* csp = (const float4*)a.rq_cos_sin + (size_t)rpos * (D / 4);
+    } else if (fast_rot()) {
 #pragma unroll
       for (int s = 0; s < HS; s++) {
-        float cc[8], ss[8];
+        float cc[8], sn[8];
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-          const float4 q = csp[(32 * s + 8 * g) / 2 + e];
-          cc[2 * e] = rnd(q.x); ss[2 * e] = rnd(q.y); cc[2 * e + 1] = rnd(q.z); ss[2 * e + 1] = rnd(q.w);
+          const float4 q = c.q[s][e];
+          cc[2 * e] = rnd(q.x); sn[2 * e] = rnd(q.y); cc[2 * e + 1] = rnd(q.z); sn[2 * e + 1] = rnd(q.w);
         }
         uint32_t lo[4], hi[4];
 #pragma unroll
@@ -119,8 +172,8 @@ struct V3Rope {
           for (int t = 0; t < 2; t++) {
             const int j = 2 * e + t;
             const float x0 = v[s][j], x1 = v[s + HS][j];
-            r0[t] = (rnd(x0 * cc[j]) - rnd(x1 * ss[j])) * scale_out;
-            r1[t] = (rnd(x1 * cc[j]) + rnd(x0 * ss[j])) * scale_out;
+            r0[t] = (rnd(x0 * cc[j]) - rnd(x1 * sn[j])) * scale_out;
+            r1[t] = (rnd(x1 * cc[j]) + rnd(x0 * sn[j])) * scale_out;
           }
           lo[e] = pack2<T>(r0[0], r0[1]);
           hi[e] = pack2<T>(r1[0], r1[1]);
@@ -138,12 +191,6 @@ struct V3Rope {
         outf[s] = make_uint4(w[0], w[1], w[2], w[3]);
       }
     }
-  }
-  // the new value row's 8 dims at d0 (no rotation)
-  __device__ uint4 vrow8(int colv, int d0) const {
-    float v[8];
-    raw8(colv + d0, v);
-    return make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
   }
 };
 
@@ -216,9 +263,10 @@ __global__ void __launch_bounds__(256) attn_combine_v3_kernel(const AttnDecodeAr
   v3_combine<T, false>(a, blockIdx.y, blockIdx.x, ns, threadIdx.x, 256);
 }
 
-// grid (splits, Hkv, B), NW waves; RQ: q/k/v from the qkv accumulator (Tq == 1)
-template <typename T, int D, int NW, bool RQ, bool FUSE>
-__global__ void __launch_bounds__(64 * NW, ILLM_ATTN_V3_MINW) attn_decode_v3_kernel(const AttnDecodeArgs a) {
+// grid (splits, Hkv, B), NW waves; RQ: q/k/v from the qkv accumulator (Tq == 1):
+// 1 RoPE applied here (+ bias), 2 pre-rotated by the qkv GEMV and bias-free
+template <typename T, int D, int NW, int RQ, bool FUSE>
+__global__ void __launch_bounds__(64 * NW, ILLM_V3_MINW(RQ)) attn_decode_v3_kernel(const AttnDecodeArgs a) {
   constexpr int KSTEP = D / 32;     // MFMA k-steps over the head dim
   constexpr int DT = D / 16;        // 16-dim output tiles
   constexpr int VU = D / 8;         // 16-B chunks per key row
@@ -226,7 +274,7 @@ __global__ void __launch_bounds__(64 * NW, ILLM_ATTN_V3_MINW) attn_decode_v3_ker
   constexpr int VJ = V3_KPW / KPJ;  // V staging loads per lane
   constexpr int SK = V3_KPW * NW;   // keys per workgroup split
   static_assert(D == 64 || D == 128, "v3: head_dim 64 / 128");
-  static_assert(!RQ || D == 128, "v3: fused RoPE needs head_dim 128");
+  static_assert(RQ == 0 || D == 128, "v3: fused RoPE needs head_dim 128");
   const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, r16 = lane & 15, g = lane >> 4;
   const int wv = threadIdx.x >> 6;
@@ -236,19 +284,29 @@ __global__ void __launch_bounds__(64 * NW, ILLM_ATTN_V3_MINW) attn_decode_v3_ker
 
   __shared__ float smx[NW][16], sml[NW][16];
   __shared__ int s_last;
+  __shared__ __attribute__((aligned(16))) float knew[RQ != 0 ? NW : 1][D];   // the new k row (fused RoPE)
   __shared__ __attribute__((aligned(16))) uint16_t vl[SK * D];   // V tile; then the P V reduction
 
   // ---- sequence length and this wave's block-table entry, in flight together
+  // (fused RoPE: with the row's rms scale, position and the wave's q columns)
   int len = a.seq_lens[b];
   const int blk = a.block_tables[(size_t)b * a.max_blocks + min(kw0 / a.bs, a.max_blocks - 1)];
+  const int row = r16 < R ? r16 : 0;
+  const int t = row / group, h = kvh * group + row % group;
+  const V3Rope<T, D, RQ == 2> rp(a, b, g, RQ != 0);
+  typename V3Rope<T, D, RQ == 2>::Raw qraw;
+  uint4 qpl[KSTEP];
+  if constexpr (RQ == 0) {
+    const uint16_t* qr = a.q + (((size_t)b * a.Tq + t) * a.Hq + h) * D;
+#pragma unroll
+    for (int s = 0; s < KSTEP; s++) qpl[s] = *(const uint4*)(qr + 32 * s + 8 * g);
+  }
   // coverage is the caller's nominal split grid (nsplit x SPLIT keys), which
   // the rounded-up v3 grid can exceed: keys past it are reported, not read
   if ((int64_t)len > (int64_t)a.max_blocks * a.bs || (int64_t)a.nsplit * SPLIT < len) {
     if (split == 0 && threadIdx.x == 0) kerr(a.err, ERR_SEQ_LEN);
     len = min(min(len, a.max_blocks * a.bs), a.nsplit * SPLIT);
   }
-  const int row = r16 < R ? r16 : 0;
-  const int t = row / group, h = kvh * group + row % group;
   const size_t prow = (((size_t)b * a.Hq + h) * a.Tq + t) * a.nsplit + split;
 
   if (k0 >= len) {
@@ -290,23 +348,61 @@ __global__ void __launch_bounds__(64 * NW, ILLM_ATTN_V3_MINW) attn_decode_v3_ker
       for (int j = 0; j < VJ; j++) vm[j] = make_uint4(0, 0, 0, 0);
     }
 
+    // fused RoPE: the wave's q columns, cos / sin and (the wave holding the
+    // new key, position len - 1) the new k / v rows' columns in value-row
+    // layout (lane: 8 dims at d0), requested right behind the K / V rows
+    const bool holds_new = RQ != 0 && ld_on && kw0 + nkw == len;   // wave-uniform
+    const int d0 = 8 * (lane % VU);
+    typename V3Rope<T, D, RQ == 2>::CS cs;
+    float4 kn0, kn1, vn0, vn1;
+    uint4 knb, vnb;
+    if constexpr (RQ != 0) {
+      rp.load(h * D, qraw);
+      rp.load_cs(cs);
+      if (holds_new) {
+        rp.vload((a.Hq + kvh) * D + d0, kn0, kn1, knb);
+        rp.vload((a.Hq + a.Hkv + kvh) * D + d0, vn0, vn1, vnb);
+      }
+    }
+
     // ---- q fragments (lane: row r16, dims 32 s + 8 g .. + 8)
     uint4 qf[KSTEP];
-    if constexpr (RQ) {
-      const V3Rope<T, D> rp(a, b, g);
-      rp.frags(h * D, a.rq_qscale, qf);
+    if constexpr (RQ != 0) {
+      {
+        float v[KSTEP][8];
+        rp.vals(qraw, v);
+        rp.frags(h * D, v, cs, a.rq_qscale, qf);
+      }
       if (r16 >= R)
 #pragma unroll
         for (int s = 0; s < KSTEP; s++) qf[s] = make_uint4(0, 0, 0, 0);
-      if (ld_on && kw0 + nkw == len) {
-        // this wave holds the new key (position len - 1): k / v from the
-        // accumulator replace the not-yet-written cache row in registers and
-        // are appended to the cache for later steps
+      if (holds_new) {
+        // k / v from the accumulator replace the not-yet-written cache row in
+        // registers and are appended to the cache for later steps; the k row
+        // goes through the wave's LDS row to the MFMA layout (lane (kn & 15, g))
         const int kn = nkw - 1;
+        const float rsv = rp.rs();
         const size_t crow = (((size_t)blk * a.Hkv + kvh) * a.bs + (size_t)((len - 1) % a.bs)) * D;
+        if (lane < VU) {
+          float kv[8];
+          rp.vals8(kn0, kn1, knb, rsv, kv);
+          *(float4*)&knew[wv][d0] = make_float4(kv[0], kv[1], kv[2], kv[3]);
+          *(float4*)&knew[wv][d0 + 4] = make_float4(kv[4], kv[5], kv[6], kv[7]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (r16 == (kn & 15)) {
+          float kv[KSTEP][8];
+#pragma unroll
+          for (int s = 0; s < KSTEP; s++) {
+            const float4 u0 = *(const float4*)&knew[wv][32 * s + 8 * g];
+            const float4 u1 = *(const float4*)&knew[wv][32 * s + 8 * g + 4];
+            kv[s][0] = u0.x; kv[s][1] = u0.y; kv[s][2] = u0.z; kv[s][3] = u0.w;
+            kv[s][4] = u1.x; kv[s][5] = u1.y; kv[s][6] = u1.z; kv[s][7] = u1.w;
+          }
           uint4 kq[KSTEP];
-          rp.frags((a.Hq + kvh) * D, 1.f, kq);
+          rp.frags((a.Hq + kvh) * D, kv, cs, 1.f, kq);
 #pragma unroll
           for (int kt = 0; kt < 2; kt++)
             if (kt == (kn >> 4))
@@ -316,8 +412,10 @@ __global__ void __launch_bounds__(64 * NW, ILLM_ATTN_V3_MINW) attn_decode_v3_ker
           for (int s = 0; s < KSTEP; s++) *(uint4*)((uint16_t*)a.k_cache + crow + 32 * s + 8 * g) = kq[s];
         }
         if (lane / VU == kn % KPJ) {
-          const int d0 = 8 * (lane % VU);
-          const uint4 vq = rp.vrow8((a.Hq + a.Hkv + kvh) * D, d0);
+          float vv[8];
+          rp.vals8(vn0, vn1, vnb, rsv, vv);
+          const uint4 vq = make_uint4(pack2<T>(vv[0], vv[1]), pack2<T>(vv[2], vv[3]), pack2<T>(vv[4], vv[5]),
+                                      pack2<T>(vv[6], vv[7]));
 #pragma unroll
           for (int j = 0; j < VJ; j++)
             if (j == kn / KPJ) vm[j] = vq;
@@ -325,12 +423,8 @@ __global__ void __launch_bounds__(64 * NW, ILLM_ATTN_V3_MINW) attn_decode_v3_ker
         }
       }
     } else {
-      const uint16_t* qr = a.q + (((size_t)b * a.Tq + t) * a.Hq + h) * D;
 #pragma unroll
-      for (int s = 0; s < KSTEP; s++) {
-        const uint4 v = *(const uint4*)(qr + 32 * s + 8 * g);
-        qf[s] = r16 < R ? v : make_uint4(0, 0, 0, 0);
-      }
+      for (int s = 0; s < KSTEP; s++) qf[s] = r16 < R ? qpl[s] : make_uint4(0, 0, 0, 0);
     }
 
     // ---- S^T tiles: lane holds (key = 16 kt + 4 g + i, row = r16)
@@ -491,7 +585,7 @@ inline int v3_pick_nw(const AttnDecodeArgs& a) {
   return 4;
 }
 
-template <typename T, int D, int NW, bool RQ>
+template <typename T, int D, int NW, int RQ>
 static void launch_v3_nw(const AttnDecodeArgs& a, hipStream_t st) {
   const int ns = (a.nsplit * SPLIT + V3_KPW * NW - 1) / (V3_KPW * NW);
   dim3 grid(ns, a.Hkv, a.B);
@@ -503,7 +597,7 @@ static void launch_v3_nw(const AttnDecodeArgs& a, hipStream_t st) {
   }
 }
 
-template <typename T, int D, bool RQ>
+template <typename T, int D, int RQ>
 static void launch_v3(const AttnDecodeArgs& a, hipStream_t st) {
   switch (v3_pick_nw(a)) {
     case 1: return launch_v3_nw<T, D, 1, RQ>(a, st);

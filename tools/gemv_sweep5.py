@@ -30,6 +30,8 @@ def main():
     tag = {"kw": os.environ.get("ILLM_GEMV5_KW", "auto"), "ks": os.environ.get("ILLM_GEMV5_KS", "auto"),
            "nw": os.environ.get("ILLM_GEMV5_NW", "auto")}
     shapes = SHAPES_70B if os.environ.get("GEMV_SHAPES") == "70b" else SHAPES
+    if os.environ.get("GEMV_ACC") == "1":      # the decoder's atomic-accumulator form of the projections
+        shapes = [(nm, n, k, "acc" if kd == "part" else kd) for nm, n, k, kd in shapes]
     for name, n, k, kind in shapes:
         if only and name not in only:
             continue
