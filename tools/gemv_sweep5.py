@@ -32,6 +32,8 @@ def main():
     shapes = SHAPES_70B if os.environ.get("GEMV_SHAPES") == "70b" else SHAPES
     if os.environ.get("GEMV_ACC") == "1":      # the decoder's atomic-accumulator form of the projections
         shapes = [(nm, n, k, "acc" if kd == "part" else kd) for nm, n, k, kd in shapes]
+    if os.environ.get("GEMV_STORE1") == "1":   # full-K workgroups writing T outputs (no split-K)
+        shapes = [(nm, n, k, "store1" if kd == "part" else kd) for nm, n, k, kd in shapes]
     for name, n, k, kind in shapes:
         if only and name not in only:
             continue
@@ -51,6 +53,8 @@ def main():
                     return ops.gemv_accum(x, b, f, n, k, acc)
                 if kind == "part":
                     return ops.gemv_partials(x, b, f, n, k, 0)
+                if kind == "store1":            # one workgroup column per output: no split-K
+                    return torch.ops.ipex_llm_amd.gemv(x, b, f, n, k, None, 0, 1, 0)
                 return ops.lowbit_matmul(x, b, f, n, k)
             us = timeit(run)
             print(json.dumps({**tag, "M": M, "op": name, "us": round(us, 2),
