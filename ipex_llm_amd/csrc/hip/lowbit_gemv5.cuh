@@ -346,24 +346,56 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
     const int vpr = a.K / 8;
     uint16_t* xst = (uint16_t*)smem;
     const int ldxs = gemv5_x_ld(kw);
-    for (int m = 0; m < Mloc; m++) {
-      float ss = 0.f;
-#pragma unroll 2
-      for (int v = threadIdx.x; v < vpr; v += NW * 64) {
-        float h[8];
-        ni_h(m, v * 8, h);
+    // every row's loads of a thread's (up to HPF) slots are requested before
+    // the first use: one L2 round trip per HPF slots instead of one per row
+    // (the per-row loop serialised Mloc round trips: at batch 8 the norm-in
+    // GLU cost 24.7 us vs 19.7 on a normed x, profiles/gemv5_defer_r3.jsonl)
+    constexpr int HPF = 4;
+    const int nthr = NW * 64, total = Mloc * vpr;
+    for (int v0 = threadIdx.x; v0 < total; v0 += HPF * nthr) {
+      float4 hp0[HPF], hp1[HPF];
+      uint4 hr[HPF];
+#pragma unroll
+      for (int u = 0; u < HPF; u++) {
+        const int vv = min(v0 + u * nthr, total - 1);
+        const int m = vv / vpr, k = (vv % vpr) * 8;
+        const float4* p = (const float4*)(a.nacc + (size_t)m * a.K + k);
+        hp0[u] = p[0];
+        hp1[u] = p[1];
+        hr[u] = *(const uint4*)(a.nres + (size_t)m * a.K + k);
+      }
+#pragma unroll
+      for (int u = 0; u < HPF; u++) {
+        const int v = v0 + u * nthr;
+        if (v >= total) break;                  // per 8-lane group when vpr % 8 == 0
+        const int m = v / vpr, k = (v % vpr) * 8;
+        const float av[8] = {hp0[u].x, hp0[u].y, hp0[u].z, hp0[u].w, hp1[u].x, hp1[u].y, hp1[u].z, hp1[u].w};
+        const uint32_t rw[4] = {hr[u].x, hr[u].y, hr[u].z, hr[u].w};
+        float h[8], ss = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          h[2 * i] = rnd(rnd(av[2 * i]) + to_f32<T>((uint16_t)(rw[i] & 0xffff)));
+          h[2 * i + 1] = rnd(rnd(av[2 * i + 1]) + to_f32<T>((uint16_t)(rw[i] >> 16)));
+        }
 #pragma unroll
         for (int i = 0; i < 8; i++) ss += h[i] * h[i];
         const uint4 hp =
             make_uint4(pack2<T>(h[0], h[1]), pack2<T>(h[2], h[3]), pack2<T>(h[4], h[5]), pack2<T>(h[6], h[7]));
-        if (wres) *(uint4*)(a.nres_out + (size_t)m * a.K + v * 8) = hp;
+        if (wres) *(uint4*)(a.nres_out + (size_t)m * a.K + k) = hp;
         // this workgroup's K slice: keep h (exact in T) in the x staging area,
         // the staging pass below normalises it in place (no second global read)
-        const int kk = v * 8 - kbase;
+        const int kk = k - kbase;
         if (kk >= 0 && kk < kw) *(uint4*)(xst + m * ldxs + kk) = hp;
+        if ((vpr & 7) == 0) {
+          // the 8 lanes of an 8-vector group share the row: shuffle, one LDS add
+          ss += __shfl_xor(ss, 1, 8);
+          ss += __shfl_xor(ss, 2, 8);
+          ss += __shfl_xor(ss, 4, 8);
+          if ((v & 7) == 0) atomicAdd(&ninv[m], ss);
+        } else {
+          atomicAdd(&ninv[m], ss);
+        }
       }
-      ss = wave_sum(ss);
-      if (lane == 0) atomicAdd(&ninv[m], ss);
     }
     __syncthreads();
     if (threadIdx.x < Mloc) ninv[threadIdx.x] = rsqrtf(ninv[threadIdx.x] / (float)a.K + a.neps);
@@ -426,6 +458,50 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
 #pragma unroll
       for (int u = 0; u < XPF; u++)
         if (v0 + u * nthr < total) commit_x(v0 + u * nthr, to_c(xv[u]));
+    }
+  } else if (!(ILLM_GEMV5_ABL & 2) && a.nacc && !defer && !a.apo && !a.xpart) {
+    // norm-in: h (exact in T) is already in LDS from the prologue; x = w * rnd(h * inv).
+    // The norm weight loads of a thread's XPF slots are requested together (the
+    // generic loop below made each slot's weight load a round trip of its own:
+    // Mloc x vpr / threads of them at batch 8)
+    constexpr int XPF = 4;
+    const int nthr = NW * 64, total = Mloc * vpr;
+    for (int v0 = threadIdx.x; v0 < total; v0 += XPF * nthr) {
+      uint4 wq[XPF];
+#pragma unroll
+      for (int u = 0; u < XPF; u++) {
+        const int vv = min(v0 + u * nthr, total - 1);
+        const int kk = (vv % vpr) * 8;
+        wq[u] = kbase + kk < a.K ? *(const uint4*)(a.nweight + kbase + kk) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < XPF; u++) {
+        const int v = v0 + u * nthr;
+        if (v >= total) break;                  // whole 8-lane groups (vpr % 16 == 0)
+        const int m = v / vpr, kk = (v % vpr) * 8;
+        uint4 val = make_uint4(0, 0, 0, 0);
+        if (kbase + kk < a.K) {
+          const uint4 hq = *(const uint4*)(xs + m * ldx + kk);
+          const uint32_t hw[4] = {hq.x, hq.y, hq.z, hq.w};
+          const uint32_t wv[4] = {wq[u].x, wq[u].y, wq[u].z, wq[u].w};
+          const float inv = ninv[m];
+          uint32_t o4[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            float w0 = to_f32<T>((uint16_t)(wv[i] & 0xffff)), w1 = to_f32<T>((uint16_t)(wv[i] >> 16));
+            if (a.nunit) { w0 = rnd(1.f + w0); w1 = rnd(1.f + w1); }
+            const float h0 = to_f32<T>((uint16_t)(hw[i] & 0xffff)), h1 = to_f32<T>((uint16_t)(hw[i] >> 16));
+            float v0f = rnd(w0 * rnd(h0 * inv)), v1f = rnd(w1 * rnd(h1 * inv));
+            if constexpr (!std::is_same<C, T>::value) {
+              v0f = fminf(fmaxf(v0f, -65504.f), 65504.f);
+              v1f = fminf(fmaxf(v1f, -65504.f), 65504.f);
+            }
+            o4[i] = pack2<C>(v0f, v1f);
+          }
+          val = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+        }
+        commit_x(v, val);
+      }
     }
   } else if (!(ILLM_GEMV5_ABL & 2)) {
     for (int v = threadIdx.x; v < Mloc * vpr; v += NW * 64) {

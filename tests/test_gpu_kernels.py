@@ -88,7 +88,7 @@ def test_gemv_accum_and_zeroing_consumers(cuda, name, M, n):
 
 
 @pytest.mark.parametrize("name", ["sym_int4", "asym_int4", "nf4", "sym_int8"])
-@pytest.mark.parametrize("M", [1, 2, 8])
+@pytest.mark.parametrize("M", [1, 2, 8, 16])
 def test_gemv_norm_in(cuda, name, M):
     """residual-add + RMSNorm folded into the GEMV prologue (decode norm-in
     path) vs add_rms_norm followed by the plain GEMV / GLU GEMV; the residual
