@@ -198,7 +198,7 @@ struct V3Rope {
 // thread -> (row, 16-B quad of D); all of a row's (m, l) and o quads of a
 // 16-split chunk are requested before any is used (one memory round trip for
 // ns <= 16), later chunks rescale online.  SC1: handed over inside the launch.
-template <typename T, bool SC1>
+template <typename T, bool SC1, bool OSC1 = false>
 __device__ __forceinline__ void v3_combine(const AttnDecodeArgs& a, int b, int kvh, int ns, int tid, int nthr) {
   constexpr int CH = 16;
   const int group = a.Hq / a.Hkv, R = group * a.Tq, Q = a.D / 4;
@@ -243,7 +243,13 @@ __device__ __forceinline__ void v3_combine(const AttnDecodeArgs& a, int b, int k
     }
     const float inv = L > 0.f ? 1.f / L : 0.f;
     uint16_t* out = a.out + (((size_t)b * a.Tq + t) * a.Hq + h) * a.D + 4 * q;
-    *(uint2*)out = make_uint2(pack2<T>(o.x * inv, o.y * inv), pack2<T>(o.z * inv, o.w * inv));
+    if constexpr (OSC1) {        // read inside the same launch by other XCDs (attention -> o_proj chain)
+      const unsigned long long v = (unsigned long long)pack2<T>(o.x * inv, o.y * inv) |
+                                   ((unsigned long long)pack2<T>(o.z * inv, o.w * inv) << 32);
+      __hip_atomic_store((unsigned long long*)out, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      *(uint2*)out = make_uint2(pack2<T>(o.x * inv, o.y * inv), pack2<T>(o.z * inv, o.w * inv));
+    }
   }
   if (a.rq_part != nullptr) {
     // fused-RoPE decode: every split of (b, kvh) has read its q / k / v columns
@@ -263,10 +269,24 @@ __global__ void __launch_bounds__(256) attn_combine_v3_kernel(const AttnDecodeAr
   v3_combine<T, false>(a, blockIdx.y, blockIdx.x, ns, threadIdx.x, 256);
 }
 
-// grid (splits, Hkv, B), NW waves; RQ: q/k/v from the qkv accumulator (Tq == 1):
-// 1 RoPE applied here (+ bias), 2 pre-rotated by the qkv GEMV and bias-free
+// LDS of one v3 workgroup (a static object of the plain kernel; a view of the
+// dynamic LDS in the attention -> o_proj chain launch)
+template <int D, int NW, int RQ>
+struct V3Smem {
+  __attribute__((aligned(16))) uint16_t vl[V3_KPW * NW * D];   // V tile; then the P V reduction
+  __attribute__((aligned(16))) float knew[RQ != 0 ? NW : 1][D];  // the new k row (fused RoPE)
+  float smx[NW][16], sml[NW][16];
+  int s_last;
+};
+
+// one (split, kv head, batch row) workgroup of NW waves; nsg = splits in the
+// grid; RQ: q/k/v from the qkv accumulator (Tq == 1): 1 RoPE applied here
+// (+ bias), 2 pre-rotated by the qkv GEMV and bias-free.  done != nullptr
+// (chain launch): the merging workgroup writes its rows write-through and
+// then adds one to *done
 template <typename T, int D, int NW, int RQ, bool FUSE>
-__global__ void __launch_bounds__(64 * NW, ILLM_V3_MINW(RQ)) attn_decode_v3_kernel(const AttnDecodeArgs a) {
+__device__ __forceinline__ void attn_v3_body(const AttnDecodeArgs& a, int split, int kvh, int b, int nsg,
+                                             V3Smem<D, NW, RQ>& sm, int* done) {
   constexpr int KSTEP = D / 32;     // MFMA k-steps over the head dim
   constexpr int DT = D / 16;        // 16-dim output tiles
   constexpr int VU = D / 8;         // 16-B chunks per key row
@@ -275,17 +295,16 @@ __global__ void __launch_bounds__(64 * NW, ILLM_V3_MINW(RQ)) attn_decode_v3_kern
   constexpr int SK = V3_KPW * NW;   // keys per workgroup split
   static_assert(D == 64 || D == 128, "v3: head_dim 64 / 128");
   static_assert(RQ == 0 || D == 128, "v3: fused RoPE needs head_dim 128");
-  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, r16 = lane & 15, g = lane >> 4;
   const int wv = threadIdx.x >> 6;
   const int group = a.Hq / a.Hkv;
   const int R = group * a.Tq;
   const int k0 = split * SK, kw0 = k0 + V3_KPW * wv;
 
-  __shared__ float smx[NW][16], sml[NW][16];
-  __shared__ int s_last;
-  __shared__ __attribute__((aligned(16))) float knew[RQ != 0 ? NW : 1][D];   // the new k row (fused RoPE)
-  __shared__ __attribute__((aligned(16))) uint16_t vl[SK * D];   // V tile; then the P V reduction
+  auto& smx = sm.smx;
+  auto& sml = sm.sml;
+  auto& knew = sm.knew;
+  uint16_t* vl = sm.vl;
 
   // ---- sequence length and this wave's block-table entry, in flight together
   // (fused RoPE: with the row's rms scale, position and the wave's q columns)
@@ -552,13 +571,26 @@ __global__ void __launch_bounds__(64 * NW, ILLM_V3_MINW(RQ)) attn_decode_v3_kern
     if (threadIdx.x == 0) {
       int* ctr = a.v3_counters + (size_t)b * a.Hkv + kvh;
       const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = prev == (int)gridDim.x - 1;
-      if (s_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm.s_last = prev == nsg - 1;
+      if (sm.s_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (!s_last) return;
-    v3_combine<T, true>(a, b, kvh, gridDim.x, threadIdx.x, NW * 64);
+    if (!sm.s_last) return;
+    if (done == nullptr) {
+      v3_combine<T, true>(a, b, kvh, nsg, threadIdx.x, NW * 64);
+    } else {
+      v3_combine<T, true, true>(a, b, kvh, nsg, threadIdx.x, NW * 64);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's output rows are out
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
+}
+
+template <typename T, int D, int NW, int RQ, bool FUSE>
+__global__ void __launch_bounds__(64 * NW, ILLM_V3_MINW(RQ)) attn_decode_v3_kernel(const AttnDecodeArgs a) {
+  __shared__ V3Smem<D, NW, RQ> sm;
+  attn_v3_body<T, D, NW, RQ, FUSE>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, sm, nullptr);
 }
 
 // waves per workgroup: the most (>= 4) that still leaves >= ~2 workgroups per CU

@@ -169,8 +169,44 @@ __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
 #ifndef ILLM_GEMV5_SCL
 #define ILLM_GEMV5_SCL 1
 #endif
-template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4, bool SCL = ILLM_GEMV5_SCL != 0>
-__global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(const GemvArgs a) {
+// x staging by LDS-DMA (buffer_load ... lds: 16 B per lane straight into LDS,
+// no VGPR round trip, every row requested at once) for launches whose x slice
+// needs more than one batch of register-staged loads per thread (the batch-8
+// gate/up GEMV: 64 KB per workgroup, two dependent L2 round trips before).
+// Issued from inline asm like the 8-phase GEMM's (gemm_8p.hip dma16).
+#ifndef ILLM_GEMV5_XDMA
+#define ILLM_GEMV5_XDMA 1
+#endif
+typedef int32_t gv5_rsrc __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ gv5_rsrc gv5_make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t p = (uint64_t)(uintptr_t)base;
+  return gv5_rsrc{(int32_t)(uint32_t)p, (int32_t)((uint32_t)(p >> 32) & 0xffffu), (int32_t)bytes, 0x00020000};
+}
+__device__ __forceinline__ void gv5_dma16(const gv5_rsrc& rs, const void* lds, uint32_t voff) {
+  const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(la), "v"(voff), "s"(rs) : "memory", "m0");
+}
+
+// block coordinates of one GEMV workgroup (blockIdx / gridDim of a plain
+// launch; virtual ones inside a chained launch)
+struct G5Blk {
+  int x, y, z, gx, gy, gz;
+};
+// chained launch (attn_oproj_kernel, attn_dec_v3.cuh + attn_oproj.hip): the
+// GEMV workgroups request their first weight chunks, then wait until the
+// producer's workgroups have all signalled (*cnt == target), and read x
+// through the write-through path; the last to leave resets both counters
+struct G5Wait {
+  int* cnt;             // producer arrivals
+  int target;
+  int* dep;             // departures of this GEMV's workgroups
+  int ndep;             // this GEMV's workgroup count
+  int* err;             // device error word (a wait that never completes)
+};
+
+template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF, bool SCL>
+__device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, const G5Wait* wt) {
   // PF: chunks in flight per wave (4; 8 = every chunk of a decode split-K
   // slice of <= 8 chunks requested before the prologue)
   using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;   // MFMA input type
@@ -183,22 +219,11 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r16 = lane & 15;
 
-  // ---- zero a consumed atomic accumulator (its readers ran earlier in the
-  // stream), spread over every workgroup of the grid (up to ~1 MB at M = 8)
-  if (a.nzero) {
-    const int nthr = NW * 64;
-    const size_t nb = (size_t)gridDim.x * gridDim.y * gridDim.z;
-    const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    const size_t nv = (size_t)a.nzero_n / 4;
-    for (size_t i = bid * nthr + threadIdx.x; i < nv; i += nb * nthr)
-      ((float4*)a.nzero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-
   int Mloc = a.M;
   const uint8_t* wbase = a.w;
   const int32_t* prow = nullptr;
   if constexpr (MOE) {
-    const int e = blockIdx.z;
+    const int e = blk.z;
     const int m0 = a.moe_off[e];
     Mloc = min(16, a.moe_off[e + 1] - m0);
     if (Mloc <= 0) return;                // expert not routed to: the whole block exits
@@ -208,9 +233,9 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
   auto xrow_of = [&](int m) -> int { if constexpr (MOE) return prow[m] / a.moe_xdiv; else return m; };
   auto orow_of = [&](int m) -> int { if constexpr (MOE) return prow[m]; else return m; };
 
-  const int nks = gridDim.y;
+  const int nks = blk.gy;
   const int cpk = a.cpk > 0 ? a.cpk : (a.KC + nks - 1) / nks;
-  const int c0 = blockIdx.y * cpk;
+  const int c0 = blk.y * cpk;
   const int c1 = min(a.KC, c0 + cpk);
   const int kbase = c0 * 128;
   const int kw = (c1 - c0) * 128;
@@ -222,13 +247,13 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
 
   const int NT = (a.N * (EPI == EPI_GLU ? 2 : 1) + 15) / 16;
   const int tg = wave / KW, kp = wave % KW;
-  const int tile0 = (blockIdx.x * TG + tg) * TPW;
+  const int tile0 = (blk.x * TG + tg) * TPW;
   const int per = (c1 - c0 + KW - 1) / KW;
   const int wc0 = c0 + kp * per;
   const int wc1 = min(c1, wc0 + per);
   const bool wave_on = tile0 < NT && wc0 < wc1;
   // debug build: the host geometry must cover every output tile and K chunk
-  if (ILLM_DCHECK_FAILS((int64_t)gridDim.x * TG * TPW >= NT && (int64_t)nks * cpk >= a.KC && Mloc <= 16, a.err,
+  if (ILLM_DCHECK_FAILS((int64_t)blk.gx * TG * TPW >= NT && (int64_t)nks * cpk >= a.KC && Mloc <= 16, a.err,
                         ERR_GEOMETRY))
     return;
   const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
@@ -276,6 +301,35 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
     if constexpr (SCL) load_scl(wc0);
 #pragma unroll
     for (int u = 0; u < PF; u++) load_chunk(ring[u], wc0 + u);
+  }
+  // chained launch: everything from here on may read what the producer wrote
+  // (or zero what it reads): wait for all of its workgroups, bounded
+  if (wt != nullptr) {
+    if (threadIdx.x == 0) {
+      int it = 0;
+      while (__hip_atomic_load(wt->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wt->target) {
+        __builtin_amdgcn_s_sleep(16);
+        if (++it > (1 << 20)) {                 // ~seconds: report, never hang the device
+          kerr(wt->err, ERR_CHAIN);
+          break;
+        }
+      }
+      if (__hip_atomic_fetch_add(wt->dep, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == wt->ndep - 1) {
+        __hip_atomic_store(wt->dep, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(wt->cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- zero a consumed atomic accumulator (its readers ran earlier in the
+  // stream), spread over every workgroup of the grid (up to ~1 MB at M = 8)
+  if (a.nzero) {
+    const int nthr = NW * 64;
+    const size_t nb = (size_t)blk.gx * blk.gy * blk.gz;
+    const size_t bid = ((size_t)blk.z * blk.gy + blk.y) * blk.gx + blk.x;
+    const size_t nv = (size_t)a.nzero_n / 4;
+    for (size_t i = bid * nthr + threadIdx.x; i < nv; i += nb * nthr)
+      ((float4*)a.nzero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if constexpr (DK == DK_LUT4) {
     if (threadIdx.x < 256)
@@ -342,7 +396,7 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
   if (a.nacc && !defer && !(ILLM_GEMV5_ABL & 2)) {
     if (threadIdx.x < 16) ninv[threadIdx.x] = 0.f;
     __syncthreads();
-    const bool wres = a.nres_out != nullptr && blockIdx.x == 0 && blockIdx.y == 0;
+    const bool wres = a.nres_out != nullptr && blk.x == 0 && blk.y == 0;
     const int vpr = a.K / 8;
     uint16_t* xst = (uint16_t*)smem;
     const int ldxs = gemv5_x_ld(kw);
@@ -438,7 +492,40 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
     return val;
   };
   const bool plain_x = !a.apo && !a.xpart && !defer && !a.nacc;
-  if (!(ILLM_GEMV5_ABL & 2) && plain_x) {
+  // LDS-DMA staging: 64-vector (1 KB) row pieces, whole K chunks of a
+  // 16-bit x that needs no conversion, more than one register batch per thread
+  const bool dma_x = ILLM_GEMV5_XDMA && !(ILLM_GEMV5_ABL & 2) && plain_x && !MOE && wt == nullptr &&
+                     std::is_same<C, T>::value &&
+                     (vpr & 63) == 0 && kbase + kw <= a.K && Mloc * vpr > 4 * NW * 64;
+  if (dma_x) {
+    const int per_row = vpr >> 6, nins = Mloc * per_row;
+    const gv5_rsrc rx = gv5_make_rsrc(a.x, (uint32_t)((size_t)a.M * a.ldx * 2));
+    for (int i = wave; i < nins; i += NW) {      // wave-uniform: one 1-KB row piece per instruction
+      const int m = i / per_row, j = i - m * per_row;
+      gv5_dma16(rx, xs + m * ldx + j * 512, (uint32_t)(((size_t)m * a.ldx + kbase + j * 512 + lane * 8) * 2));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // the per-(row, 64-block) sums from the staged rows (8 lanes per block)
+    const int nthr = NW * 64, total = Mloc * vpr;
+    for (int v = threadIdx.x; v < total; v += nthr) {
+      const int m = v / vpr, kk = (v % vpr) * 8;
+      const uint4 val = *(const uint4*)(xs + m * ldx + kk);
+      const uint32_t sw[4] = {val.x, val.y, val.z, val.w};
+      float bsum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; i++) bsum += to_f32<C>((uint16_t)(sw[i] & 0xffff)) + to_f32<C>((uint16_t)(sw[i] >> 16));
+      bsum += __shfl_xor(bsum, 1, 8);
+      bsum += __shfl_xor(bsum, 2, 8);
+      bsum += __shfl_xor(bsum, 4, 8);
+      if ((v & 7) == 0) {
+        const int blk = kk >> 6, nch = c1 - c0;
+        float* rec = (float*)(sxs + m * nch + (blk >> 1));
+        rec[blk & 1] = -OFF * bsum;
+        rec[2 + (blk & 1)] = bsum;
+      }
+    }
+  } else if (!(ILLM_GEMV5_ABL & 2) && plain_x) {
     // plain activations: every load of a thread's (up to XPF) staging slots is
     // requested before the first LDS store / shuffle reduction -- one L2 round
     // trip instead of one per slot (the loop form below serialised them:
@@ -452,8 +539,14 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
       for (int u = 0; u < XPF; u++) {
         const int vv = min(v0 + u * nthr, total - 1);
         const int m = vv / vpr, kk = (vv % vpr) * 8;
-        xv[u] = kbase + kk < a.K ? *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk)
-                                 : make_uint4(0, 0, 0, 0);
+        if (wt != nullptr) {     // chained: x was written by the producer in this launch (other XCDs)
+          const size_t e = (size_t)xrow_of(m) * a.ldx + kbase + kk;
+          const float4 f = ld16_sc1((const float*)a.x, e / 2);
+          xv[u] = kbase + kk < a.K ? __builtin_bit_cast(uint4, f) : make_uint4(0, 0, 0, 0);
+        } else {
+          xv[u] = kbase + kk < a.K ? *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk)
+                                   : make_uint4(0, 0, 0, 0);
+        }
       }
 #pragma unroll
       for (int u = 0; u < XPF; u++)
@@ -585,7 +678,7 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
         ssq += __shfl_xor(ssq, 2, 8);
         ssq += __shfl_xor(ssq, 4, 8);
         if ((v & 7) == 0) atomicAdd(&ninv[m], ssq);
-        if (a.nres_out && blockIdx.x == 0)
+        if (a.nres_out && blk.x == 0)
           *(uint4*)(a.nres_out + (size_t)m * a.K + kbase + kk) =
               make_uint4(pack2<T>(h[0], h[1]), pack2<T>(h[2], h[3]), pack2<T>(h[4], h[5]), pack2<T>(h[6], h[7]));
         const uint4 wq = *(const uint4*)(a.nweight + kbase + kk);
@@ -644,7 +737,7 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
       __syncthreads();
       if (threadIdx.x < Mloc) ninv[threadIdx.x] = rsqrtf(ninv[threadIdx.x] / (float)a.K + a.neps);
       __syncthreads();
-    } else if (blockIdx.x == 0 && threadIdx.x < Mloc && a.nss) {
+    } else if (blk.x == 0 && threadIdx.x < Mloc && a.nss) {
       __hip_atomic_fetch_add(a.nss + threadIdx.x, ninv[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -789,7 +882,7 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
         for (int i = 0; i < 4; i++) tbuf[r16 * NC + (tg * TPW + t) * 16 + 4 * g + i] = acc[t][i];
     }
     __syncthreads();
-    const int nb = blockIdx.x * NC;
+    const int nb = blk.x * NC;
     float* ws = (float*)a.out;
     for (int v = threadIdx.x; v < Mloc * NC; v += NW * 64) {
       const int m = v / NC, n = nb + v % NC;
@@ -851,7 +944,7 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
         for (int i = 0; i < 4; i++)
           if (n0 + i < a.N) __hip_atomic_fetch_add(ws + i, o[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else if constexpr (EPI == EPI_PARTIAL) {
-        float* ws = (float*)a.out + ((size_t)blockIdx.y * a.M + m) * a.N + n0;
+        float* ws = (float*)a.out + ((size_t)blk.y * a.M + m) * a.N + n0;
         if (n0 + 3 < a.N && (a.N & 3) == 0) *(float4*)ws = make_float4(o[0], o[1], o[2], o[3]);
         else for (int i = 0; i < 4 && n0 + i < a.N; i++) ws[i] = o[i];
       } else {
@@ -882,10 +975,17 @@ __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(
           const int oi = __shfl_xor(abi, off, 64);
           if (ov > abest || (ov == abest && oi < abi)) { abest = ov; abi = oi; }
         }
-        if (g == 0) a.amax[((size_t)blockIdx.x * TG + tg) * a.M + m] = make_float2(abest, __int_as_float(abi));
+        if (g == 0) a.amax[((size_t)blk.x * TG + tg) * a.M + m] = make_float2(abest, __int_as_float(abi));
       }
     }
   }
+}
+
+template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4, bool SCL = ILLM_GEMV5_SCL != 0>
+__global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(const GemvArgs a) {
+  gemv5_body<DK, T, EPI, TPW, KW, MOE, NW, PF, SCL>(
+      a, G5Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z},
+      nullptr);
 }
 
 // launch helper: up to 159 KiB of dynamic LDS, attribute set once per instantiation
