@@ -198,7 +198,7 @@ struct V3Rope {
 // thread -> (row, 16-B quad of D); all of a row's (m, l) and o quads of a
 // 16-split chunk are requested before any is used (one memory round trip for
 // ns <= 16), later chunks rescale online.  SC1: handed over inside the launch.
-template <typename T, bool SC1, bool OSC1 = false>
+template <typename T, bool SC1>
 __device__ __forceinline__ void v3_combine(const AttnDecodeArgs& a, int b, int kvh, int ns, int tid, int nthr) {
   constexpr int CH = 16;
   const int group = a.Hq / a.Hkv, R = group * a.Tq, Q = a.D / 4;
@@ -243,13 +243,7 @@ __device__ __forceinline__ void v3_combine(const AttnDecodeArgs& a, int b, int k
     }
     const float inv = L > 0.f ? 1.f / L : 0.f;
     uint16_t* out = a.out + (((size_t)b * a.Tq + t) * a.Hq + h) * a.D + 4 * q;
-    if constexpr (OSC1) {        // read inside the same launch by other XCDs (attention -> o_proj chain)
-      const unsigned long long v = (unsigned long long)pack2<T>(o.x * inv, o.y * inv) |
-                                   ((unsigned long long)pack2<T>(o.z * inv, o.w * inv) << 32);
-      __hip_atomic_store((unsigned long long*)out, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      *(uint2*)out = make_uint2(pack2<T>(o.x * inv, o.y * inv), pack2<T>(o.z * inv, o.w * inv));
-    }
+    *(uint2*)out = make_uint2(pack2<T>(o.x * inv, o.y * inv), pack2<T>(o.z * inv, o.w * inv));
   }
   if (a.rq_part != nullptr) {
     // fused-RoPE decode: every split of (b, kvh) has read its q / k / v columns
@@ -269,8 +263,7 @@ __global__ void __launch_bounds__(256) attn_combine_v3_kernel(const AttnDecodeAr
   v3_combine<T, false>(a, blockIdx.y, blockIdx.x, ns, threadIdx.x, 256);
 }
 
-// LDS of one v3 workgroup (a static object of the plain kernel; a view of the
-// dynamic LDS in the attention -> o_proj chain launch)
+// LDS of one v3 workgroup
 template <int D, int NW, int RQ>
 struct V3Smem {
   __attribute__((aligned(16))) uint16_t vl[V3_KPW * NW * D];   // V tile; then the P V reduction
@@ -281,12 +274,10 @@ struct V3Smem {
 
 // one (split, kv head, batch row) workgroup of NW waves; nsg = splits in the
 // grid; RQ: q/k/v from the qkv accumulator (Tq == 1): 1 RoPE applied here
-// (+ bias), 2 pre-rotated by the qkv GEMV and bias-free.  done != nullptr
-// (chain launch): the merging workgroup writes its rows write-through and
-// then adds one to *done
+// (+ bias), 2 pre-rotated by the qkv GEMV and bias-free
 template <typename T, int D, int NW, int RQ, bool FUSE>
 __device__ __forceinline__ void attn_v3_body(const AttnDecodeArgs& a, int split, int kvh, int b, int nsg,
-                                             V3Smem<D, NW, RQ>& sm, int* done) {
+                                             V3Smem<D, NW, RQ>& sm) {
   constexpr int KSTEP = D / 32;     // MFMA k-steps over the head dim
   constexpr int DT = D / 16;        // 16-dim output tiles
   constexpr int VU = D / 8;         // 16-B chunks per key row
@@ -576,21 +567,14 @@ __device__ __forceinline__ void attn_v3_body(const AttnDecodeArgs& a, int split,
     }
     __syncthreads();
     if (!sm.s_last) return;
-    if (done == nullptr) {
-      v3_combine<T, true>(a, b, kvh, nsg, threadIdx.x, NW * 64);
-    } else {
-      v3_combine<T, true, true>(a, b, kvh, nsg, threadIdx.x, NW * 64);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's output rows are out
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    v3_combine<T, true>(a, b, kvh, nsg, threadIdx.x, NW * 64);
   }
 }
 
 template <typename T, int D, int NW, int RQ, bool FUSE>
 __global__ void __launch_bounds__(64 * NW, ILLM_V3_MINW(RQ)) attn_decode_v3_kernel(const AttnDecodeArgs a) {
   __shared__ V3Smem<D, NW, RQ> sm;
-  attn_v3_body<T, D, NW, RQ, FUSE>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, sm, nullptr);
+  attn_v3_body<T, D, NW, RQ, FUSE>(a, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, sm);
 }
 
 // waves per workgroup: the most (>= 4) that still leaves >= ~2 workgroups per CU

@@ -126,7 +126,7 @@ __device__ __forceinline__ float2 ld8_sc1(const float* p) {
 // ops.check_kernel_errors() (ILLM_CHECK_KERNELS=1: after every engine step).
 // The bad access never happens, so a corrupt table is an error, not a fault.
 enum KernelErr : int { ERR_BLOCK_ID = 1, ERR_SLOT = 2, ERR_EXPERT = 4, ERR_SEQ_LEN = 8, ERR_TOKEN = 16,
-                       ERR_GEOMETRY = 32, ERR_PEER = 64, ERR_CHAIN = 128 };
+                       ERR_GEOMETRY = 32, ERR_PEER = 64 };
 __device__ __forceinline__ void kerr(int* err, int code) {
   if (err != nullptr) atomicOr(err, code);
 }

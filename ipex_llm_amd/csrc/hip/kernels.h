@@ -249,10 +249,6 @@ struct AttnDecodeArgs {
   int* v3_counters;
 };
 void launch_attn_decode(bool bf16, const AttnDecodeArgs& a, hipStream_t st);
-// fused-RoPE v3 decode attention + the o_proj atomic GEMV in one chained launch
-// (attn_oproj.hip); false: not applicable (caller launches the two kernels)
-bool launch_attn_oproj(int dk, bool bf16, const AttnDecodeArgs& aa, const GemvArgs& ga, dim3 ggrid, size_t gshmem,
-                       int* cnt, hipStream_t st);
 
 // ---- prefill / long-query attention over the paged cache (attn_prefill.hip)
 struct AttnPrefillArgs {

@@ -188,25 +188,12 @@ __device__ __forceinline__ void gv5_dma16(const gv5_rsrc& rs, const void* lds, u
                :: "s"(la), "v"(voff), "s"(rs) : "memory", "m0");
 }
 
-// block coordinates of one GEMV workgroup (blockIdx / gridDim of a plain
-// launch; virtual ones inside a chained launch)
+// block coordinates of one GEMV workgroup (blockIdx / gridDim of the launch)
 struct G5Blk {
   int x, y, z, gx, gy, gz;
 };
-// chained launch (attn_oproj_kernel, attn_dec_v3.cuh + attn_oproj.hip): the
-// GEMV workgroups request their first weight chunks, then wait until the
-// producer's workgroups have all signalled (*cnt == target), and read x
-// through the write-through path; the last to leave resets both counters
-struct G5Wait {
-  int* cnt;             // producer arrivals
-  int target;
-  int* dep;             // departures of this GEMV's workgroups
-  int ndep;             // this GEMV's workgroup count
-  int* err;             // device error word (a wait that never completes)
-};
-
 template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF, bool SCL>
-__device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, const G5Wait* wt) {
+__device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) {
   // PF: chunks in flight per wave (4; 8 = every chunk of a decode split-K
   // slice of <= 8 chunks requested before the prologue)
   using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;   // MFMA input type
@@ -301,25 +288,6 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
     if constexpr (SCL) load_scl(wc0);
 #pragma unroll
     for (int u = 0; u < PF; u++) load_chunk(ring[u], wc0 + u);
-  }
-  // chained launch: everything from here on may read what the producer wrote
-  // (or zero what it reads): wait for all of its workgroups, bounded
-  if (wt != nullptr) {
-    if (threadIdx.x == 0) {
-      int it = 0;
-      while (__hip_atomic_load(wt->cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wt->target) {
-        __builtin_amdgcn_s_sleep(16);
-        if (++it > (1 << 20)) {                 // ~seconds: report, never hang the device
-          kerr(wt->err, ERR_CHAIN);
-          break;
-        }
-      }
-      if (__hip_atomic_fetch_add(wt->dep, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == wt->ndep - 1) {
-        __hip_atomic_store(wt->dep, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(wt->cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();
   }
   // ---- zero a consumed atomic accumulator (its readers ran earlier in the
   // stream), spread over every workgroup of the grid (up to ~1 MB at M = 8)
@@ -494,8 +462,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
   const bool plain_x = !a.apo && !a.xpart && !defer && !a.nacc;
   // LDS-DMA staging: 64-vector (1 KB) row pieces, whole K chunks of a
   // 16-bit x that needs no conversion, more than one register batch per thread
-  const bool dma_x = ILLM_GEMV5_XDMA && !(ILLM_GEMV5_ABL & 2) && plain_x && !MOE && wt == nullptr &&
-                     std::is_same<C, T>::value &&
+  const bool dma_x = ILLM_GEMV5_XDMA && !(ILLM_GEMV5_ABL & 2) && plain_x && !MOE && std::is_same<C, T>::value &&
                      (vpr & 63) == 0 && kbase + kw <= a.K && Mloc * vpr > 4 * NW * 64;
   if (dma_x) {
     const int per_row = vpr >> 6, nins = Mloc * per_row;
@@ -539,14 +506,8 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
       for (int u = 0; u < XPF; u++) {
         const int vv = min(v0 + u * nthr, total - 1);
         const int m = vv / vpr, kk = (vv % vpr) * 8;
-        if (wt != nullptr) {     // chained: x was written by the producer in this launch (other XCDs)
-          const size_t e = (size_t)xrow_of(m) * a.ldx + kbase + kk;
-          const float4 f = ld16_sc1((const float*)a.x, e / 2);
-          xv[u] = kbase + kk < a.K ? __builtin_bit_cast(uint4, f) : make_uint4(0, 0, 0, 0);
-        } else {
-          xv[u] = kbase + kk < a.K ? *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk)
-                                   : make_uint4(0, 0, 0, 0);
-        }
+        xv[u] = kbase + kk < a.K ? *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk)
+                                 : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < XPF; u++)
@@ -984,8 +945,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk, 
 template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4, bool SCL = ILLM_GEMV5_SCL != 0>
 __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(const GemvArgs a) {
   gemv5_body<DK, T, EPI, TPW, KW, MOE, NW, PF, SCL>(
-      a, G5Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z},
-      nullptr);
+      a, G5Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z});
 }
 
 // launch helper: up to 159 KiB of dynamic LDS, attribute set once per instantiation

@@ -1071,7 +1071,7 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
     const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin, const Tensor& pos, Tensor& k_cache,
     Tensor& v_cache, const Tensor& block_tables, const Tensor& seq_lens, int64_t nsplit, double scale, double softcap,
     int64_t window, int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt, bool no_combine,
-    const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps, bool prerot, illm::AttnDecodeArgs* prep = nullptr) {
+    const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps, bool prerot) {
   c10::DeviceGuard g(part.device());
   TORCH_CHECK(dt == at::kBFloat16 || dt == at::kHalf, "attn_decode_rope: bf16/fp16 activations");
   TORCH_CHECK(k_cache.scalar_type() == dt && v_cache.scalar_type() == dt, "attn_decode_rope: 16-bit KV cache");
@@ -1138,71 +1138,10 @@ static std::tuple<Tensor, Tensor, Tensor> attn_decode_rope_impl(
     a.rq_ss_n = (int)pss_n;
     a.rq_ss_eps = (float)pss_eps;
   }
-  if (prep != nullptr) {        // the caller launches it (attention -> o_proj chain)
-    *prep = a;
-    return {out, po, pml};
-  }
   illm::launch_attn_decode(dt == at::kBFloat16, a, cur_stream());
   return {out, po, pml};
 }
 
-// decode attention (fused RoPE) and the o projection as one chained launch
-// (csrc/hip/attn_oproj.hip): acc [B, n] f32 += attention @ W^T through split-K
-// atomics, ``zero`` cleared as by gemv_accum.  Where the chain does not apply
-// (not the v3 fused-combine path, format without a chained instantiation) the
-// two kernels are launched back to back.  Returns the attention output.
-Tensor attn_rope_oproj(const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin,
-                       const Tensor& pos, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
-                       const Tensor& seq_lens, int64_t nsplit, double scale, double softcap, int64_t window,
-                       int64_t Hq, int64_t rot_dim, bool interleaved, double q_scale, at::ScalarType dt,
-                       const c10::optional<Tensor>& pss, int64_t pss_n, double pss_eps, bool prerot,
-                       const Tensor& blob, int64_t fmt, int64_t n, int64_t k, Tensor& acc,
-                       const c10::optional<Tensor>& zero) {
-  illm::AttnDecodeArgs aa{};
-  Tensor out = std::get<0>(attn_decode_rope_impl(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens,
-                                                 nsplit, scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dt,
-                                                 false, pss, pss_n, pss_eps, prerot, &aa));
-  const int64_t M = out.size(0);
-  TORCH_CHECK(out.numel() == M * k, "attn_rope_oproj: o_proj in_features != Hq * head_dim");
-  TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat && acc.is_contiguous() && acc.numel() == M * n,
-              "attn_rope_oproj: acc must be contiguous f32 [B, n]");
-  TORCH_CHECK(blob.is_cuda() && blob.numel() >= illm::dev_total_bytes((int)fmt, n, k),
-              "attn_rope_oproj: weight blob too small");
-  const bool bf16 = dt == at::kBFloat16;
-  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
-  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
-  illm::GemvArgs ga{};
-  ga.x = p16(out);
-  ga.M = (int)M;
-  ga.K = (int)k;
-  ga.ldx = (int)k;
-  ga.w = blob.data_ptr<uint8_t>();
-  ga.KC = (int)KC;
-  ga.lut_fmt = (int)fmt;
-  ga.N = (int)n;
-  ga.out = acc.data_ptr();
-  ga.ldo = (int)n;
-  ga.err = aa.err;
-  // 4-wave groups of 4 tiles (the chain's one workgroup shape), the atomic plan's split-K
-  Plan5 p = plan5(M, NT, KC, true, 0, true);
-  p.kw = 1;
-  p.nw = 4;
-  p.gx = (unsigned)((NT + 3) / 4);
-  ga.cpk = (int)p.cpk;
-  ga.nw = 4;
-  set_zero(ga, zero);
-  TORCH_CHECK(p.shmem <= kMaxLds, "attn_rope_oproj: K slice too large for LDS");
-  static std::vector<Tensor> ctr(64);
-  const int di = out.device().index() < 0 ? 0 : out.device().index();
-  if (!ctr[di].defined()) ctr[di] = at::zeros({2}, acc.options().dtype(at::kInt));
-  const dim3 grid(p.gx, (unsigned)p.ks);
-  if (!illm::launch_attn_oproj(illm::fmt_to_dk((int)fmt), bf16, aa, ga, grid, p.shmem, ctr[di].data_ptr<int>(),
-                               cur_stream())) {
-    illm::launch_attn_decode(bf16, aa, cur_stream());
-    launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_ATOMIC, grid, p.shmem, ga);
-  }
-  return out;
-}
 
 Tensor attn_decode_rope(const Tensor& part, const c10::optional<Tensor>& bias, const Tensor& cos_sin,
                         const Tensor& pos, Tensor& k_cache, Tensor& v_cache, const Tensor& block_tables,
@@ -1688,7 +1627,6 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("dequantize_device", &dequantize_device);
   m.impl("gemv", &gemv);
   m.impl("gemv_accum", &gemv_accum);
-  m.impl("attn_rope_oproj", &attn_rope_oproj);
   m.impl("gemv_norm_in", &gemv_norm_in);
   m.impl("gemm_glu", &gemm_glu);
   m.impl("moe_gemm", &moe_gemm);

@@ -183,10 +183,6 @@ DEFER_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_GLU_MAX_M", "4"))
 # profiles/bench_b8_r3_mlpacc*.json): the down GEMV's input staging from the
 # [8, 28672] f32 gate/up slab costs more than the norm launch
 DEFER_MLP_ACC = __import__("os").environ.get("ILLM_DEFER_MLP_ACC", "0") == "1"
-# decode attention + o_proj as ONE launch (csrc/hip/attn_oproj.hip: the o_proj
-# workgroups request their weights while the attention runs, then wait on the
-# attention's merge counter); ILLM_ATTN_OPROJ=1 enables it
-ATTN_OPROJ = __import__("os").environ.get("ILLM_ATTN_OPROJ", "0") == "1"
 # decode batches up to this size take the fused-RoPE attention (qkv accumulated
 # atomically into one slab read by the attention, re-zeroed by its combine).
 # Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token,
@@ -686,10 +682,6 @@ class NativeCausalLM(nn.Module):
             attn = layer.self_attn
             qp = attn.qkv_proj
             ss_q = None
-            # attention and o_proj as one chained launch (ops.attn_rope_oproj)
-            op_ = attn.o_proj
-            ao_chain = (ATTN_OPROJ and rope_in and norm_in and not self._oproj_combine and isinstance(op_, LowBitLinear)
-                        and op_.bias is None and op_.mp_group is None and qp.mp_group is None)
             q = torch.empty(T, s.num_heads, s.head_dim, dtype=x.dtype, device=x.device)
             if x.is_cuda and isinstance(qp, LowBitLinear) and qp.mp_group is None and T <= ops.GEMV_MAX_M \
                     and (qp.bias is None or qp.bias.dtype == x.dtype) and ops.native_gpu(x):
@@ -720,8 +712,6 @@ class NativeCausalLM(nn.Module):
                                       attn.q_norm, attn.k_norm, s.rms_eps, 1.0, cache.kv_fp8, cache.k_scale,
                                       cache.v_scale, meta.pos_offset, zero_part=T <= ACC_MAX_M,
                                       pss=ss_q, pss_n=s.hidden_size, pss_eps=s.rms_eps)
-                elif ao_chain:
-                    a_rope = None               # the o_proj launch below runs the attention (one chained launch)
                 elif not (norm_in and self._oproj_combine and attn.o_proj.bias is None):
                     a_rope = ops.attn_decode_rope(qkv_acc, qp.bias, self.rope_cache, pos, cache.k[li], cache.v[li],
                                                   meta.block_tables, meta.seq_lens, meta.nsplit, s.scale,
@@ -757,12 +747,6 @@ class NativeCausalLM(nn.Module):
                     ops.gemv_attn(po, pml, meta.seq_lens, o.weight, o.fmt, H, o.in_features, accP,
                                   self._oproj_ks, x.dtype, zero=consumed, nw=self._oproj_nw)
                     zero_qkv = qkv_acc
-                elif ao_chain:
-                    ops.attn_rope_oproj(qkv_acc, qp.bias, self.rope_cache, pos, cache.k[li], cache.v[li],
-                                        meta.block_tables, meta.seq_lens, meta.nsplit, s.scale, s.attn_softcap,
-                                        attn.sliding_window, s.num_heads, s.rot_dim, s.rope_interleaved, 1.0,
-                                        x.dtype, ss_q, s.hidden_size, s.rms_eps, prerot, o.weight, o.fmt, H,
-                                        o.in_features, accP, zero=consumed)
                 else:
                     a = a_rope if rope_in else self._attention(li, attn, q, meta, cache)
                     ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)

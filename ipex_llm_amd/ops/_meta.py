@@ -189,12 +189,6 @@ def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit
     return part.new_empty((part.shape[0], 1, Hq, k_cache.shape[3]), dtype=dtype)
 
 
-@register_fake("ipex_llm_amd::attn_rope_oproj")
-def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, Hq,
-      rot_dim, interleaved, q_scale, dtype, pss, pss_n, pss_eps, prerot, blob, fmt, n, k, acc, zero=None):
-    return part.new_empty((part.shape[0], 1, Hq, k_cache.shape[3]), dtype=dtype)
-
-
 @register_fake("ipex_llm_amd::attn_decode_rope_split")
 def _(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap, window, Hq,
       rot_dim, interleaved, q_scale, dtype, pss=None, pss_n=0, pss_eps=0.0, prerot=False):

@@ -18,7 +18,7 @@ __all__ = [
     "fp8_quantize_weight", "dense_linear", "check_kernel_errors", "KernelError", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
-    "moe_align", "moe_gemm", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum", "attn_rope_oproj",
+    "moe_align", "moe_gemm", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
     "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope", "attn_decode_rope_split", "attn_prefill", "moe_group_topk",
 ]
 
@@ -97,8 +97,7 @@ class KernelError(RuntimeError):
 _KERR_NAMES = {1: "block-table entry outside the KV cache", 2: "cache slot outside the KV cache",
                4: "expert id out of range", 8: "sequence length out of range (block-table row / split grid)",
                16: "token id outside the vocabulary", 32: "launch geometry does not cover the output (debug build)",
-               64: "a peer rank did not answer in time (collective / expert all-to-all timed out)",
-               128: "a chained launch waited too long for its producer (attention -> o_proj)"}
+               64: "a peer rank did not answer in time (collective / expert all-to-all timed out)"}
 
 
 def check_kernel_errors(device=None, reset: bool = True):
@@ -609,18 +608,6 @@ def attn_decode_rope(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, s
     return _ops().attn_decode_rope(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit,
                                    scale, softcap, window, Hq, rot_dim, interleaved, q_scale, dtype, pss, pss_n,
                                    pss_eps, prerot)
-
-
-def attn_rope_oproj(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap,
-                    window, Hq: int, rot_dim: int, interleaved: bool, q_scale, dtype, pss, pss_n: int, pss_eps: float,
-                    prerot: bool, blob, fmt, n: int, k: int, acc: torch.Tensor, zero: Optional[torch.Tensor] = None):
-    """attn_decode_rope followed by gemv_accum of its output (the o projection
-    into the f32 accumulator ``acc``), as ONE chained launch on the GPU (the
-    o_proj workgroups request their weights while the attention runs).
-    Returns the attention output [B, 1, Hq, D]."""
-    return _ops().attn_rope_oproj(part, bias, cos_sin, pos, k_cache, v_cache, block_tables, seq_lens, nsplit, scale,
-                                  softcap, window, Hq, rot_dim, interleaved, q_scale, dtype, pss, pss_n, pss_eps,
-                                  prerot, blob, fmt, n, k, acc, zero)
 
 
 def attn_decode_split(q, k_cache, v_cache, block_tables, seq_lens, nsplit, scale, softcap=0.0, window=0,

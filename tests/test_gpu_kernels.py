@@ -279,69 +279,6 @@ def test_gemv_rope_epilogue_and_prerot_attention(cuda, B, Hq, Hkv, D):
     assert int((p1 != 0).sum()) == 0, "qkv accumulator not re-zeroed"
 
 
-@pytest.mark.parametrize("B,prerot,name", [(1, True, "sym_int4"), (8, True, "sym_int4"), (4, False, "sym_int4"),
-                                            (8, True, "asym_int4"), (3, True, "nf4")])
-def test_attn_rope_oproj_chain_matches_two_launches(cuda, B, prerot, name):
-    """decode attention + o_proj as ONE chained launch (attn_oproj.hip) ==
-    attn_decode_rope then gemv_accum: attention output and KV append
-    bit-identical, the o_proj accumulator equal up to the f32 atomic order, the
-    consumed slab zeroed; three launches in a row (the chain counters reset);
-    nf4 has no chained instantiation and takes the two-launch fallback"""
-    from ipex_llm_amd.engine.runner import nsplit_for
-    torch.manual_seed(5)
-    Hq, Hkv, D, bs, H = 32, 8, 128, 64, 1024
-    N, K = (Hq + 2 * Hkv) * D, Hq * D
-    f = get_format(name).fmt
-    wo = ops.quantize(torch.randn(H, K, device=cuda) * 0.02, f)
-    L = [50 + 97 * i for i in range(B)]
-    seq_lens = torch.tensor(L, dtype=torch.int32, device=cuda)
-    pos = (seq_lens - 1).long()
-    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device=cuda).float() / D))
-    fr = torch.arange(1024, device=cuda).float()[:, None] * inv[None]
-    cs = torch.stack([fr.cos(), fr.sin()], -1).contiguous()
-    nb = (max(L) + bs - 1) // bs
-    kc = torch.randn(nb * B, Hkv, bs, D, device=cuda).bfloat16()
-    vc = torch.randn(nb * B, Hkv, bs, D, device=cuda).bfloat16()
-    bt = torch.arange(nb * B, dtype=torch.int32, device=cuda).view(B, nb).contiguous()
-    ns = nsplit_for(max(L))
-    for _ in range(3):
-        part = torch.randn(B, N, device=cuda) * 2
-        p1, p2 = part.clone(), part.clone()
-        kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
-        acc1, acc2 = torch.zeros(B, H, device=cuda), torch.zeros(B, H, device=cuda)
-        z1 = torch.ones(4 * 65, device=cuda)
-        out1 = ops.attn_rope_oproj(p1, None, cs, pos, kc1, vc1, bt, seq_lens, ns, D ** -0.5, 0.0, 0, Hq, D, False,
-                                   1.0, torch.bfloat16, None, 0, 0.0, prerot, wo, f, H, K, acc1, zero=z1)
-        out2 = ops.attn_decode_rope(p2, None, cs, pos, kc2, vc2, bt, seq_lens, ns, D ** -0.5, 0.0, 0, Hq, D, False,
-                                    1.0, torch.bfloat16, prerot=prerot)
-        ops.gemv_accum(out2.reshape(B, K), wo, f, H, K, acc2)
-        torch.cuda.synchronize()
-        assert torch.equal(out1, out2), (B, prerot, name)
-        assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
-        assert _rel(acc1, acc2) < 1e-5, (B, prerot, name)
-        assert z1.abs().max().item() == 0.0
-        assert int((p1 != 0).sum()) == 0, "qkv accumulator not re-zeroed"
-
-
-def test_decode_attn_oproj_chain_model(cuda, monkeypatch):
-    """whole-model greedy decode with the attention -> o_proj chained launch
-    (hipGraph) == the two-launch decode"""
-    from transformers import LlamaConfig
-    import ipex_llm_amd.models.decoder as dec
-    from ipex_llm_amd.engine.runner import Engine
-    from ipex_llm_amd.models.builder import random_native_model
-    cfg = LlamaConfig(vocab_size=512, hidden_size=1024, intermediate_size=2048, num_hidden_layers=3,
-                      num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=1024)
-    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=6)
-    prompts = [list(range(1, 50)), list(range(7, 70)), list(range(3, 40)), [5] * 30]
-    outs = {}
-    for flag in (False, True):
-        monkeypatch.setattr(dec, "ATTN_OPROJ", flag)
-        outs[flag] = Engine(m).generate(prompts, max_new_tokens=8, use_graph=True)
-    same = sum(a == b for a, b in zip(sum(outs[False], []), sum(outs[True], [])))
-    assert same >= 0.95 * len(sum(outs[True], []))       # f32 atomic order only: rare last-bit ties
-
-
 def test_decode_gemv_rope_matches_attention_rope(cuda):
     """whole-model decode (graph): RoPE in the qkv GEMV epilogue vs in the
     attention / rope kernels -- greedy tokens agree up to rare last-bit ties"""
