@@ -321,7 +321,7 @@ void illm_kq_gemm_int(int fmt, const float* x, int64_t m, const uint8_t* w, int6
   std::vector<float> xd((size_t)(m * nb * 4));
   std::vector<int> xs8((size_t)(m * nb * 32));
   quantize_x(x, m, k, xq.data(), xd.data(), xs8.data());
-  const bool v512 = isa == 2 || (isa == 0 && has_vnni512());
+  const bool v512 = (isa == 2 || isa == 0) && has_vnni512();   // a forced 2 on a host without VNNI runs AVX2
   constexpr int64_t RB = 8;
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t r0 = 0; r0 < n; r0 += RB) {

@@ -345,7 +345,7 @@ void illm_cpu_gemm_i8(int fmt, const float* x, int64_t m, const uint8_t* codes, 
   std::vector<int8_t> xq((size_t)(m * k));
   std::vector<float> xd((size_t)(m * nb)), xs((size_t)(m * nb));
   quantize_x(x, m, k, xq.data(), xd.data(), xs.data());
-  const bool v512 = isa == 2 || (isa == 0 && has_vnni512());
+  const bool v512 = (isa == 2 || isa == 0) && has_vnni512();   // a forced 2 on a host without VNNI runs AVX2
   constexpr int64_t RB = 16;
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t r0 = 0; r0 < n; r0 += RB) {
@@ -358,7 +358,7 @@ void illm_cpu_gemm_i8(int fmt, const float* x, int64_t m, const uint8_t* codes, 
 // y[m, n] = x[m, k] @ W[n, k]^T for the LUT / minifloat formats (f32 activations)
 void illm_cpu_gemm_lut(int fmt, const float* x, int64_t m, const uint8_t* codes, const uint16_t* scales,
                        int64_t n, int64_t k, float* y, int isa) {
-  const bool v512 = isa == 2 || (isa == 0 && has_avx512());
+  const bool v512 = (isa == 2 || isa == 0) && has_avx512();
   constexpr int64_t RB = 16;
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t r0 = 0; r0 < n; r0 += RB) {
@@ -375,7 +375,7 @@ void illm_cpu_gemm_q4(int fmt, const float* x, int64_t m, const uint8_t* codes, 
   std::vector<int8_t> xq((size_t)(m * k));
   std::vector<float> xd((size_t)(m * nb)), xs((size_t)(m * nb));
   quantize_x(x, m, k, xq.data(), xd.data(), xs.data());
-  const bool v512 = isa == 2 || (isa == 0 && has_vnni512());
+  const bool v512 = (isa == 2 || isa == 0) && has_vnni512();   // a forced 2 on a host without VNNI runs AVX2
   constexpr int64_t RB = 16;   // output rows per task
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t r0 = 0; r0 < n; r0 += RB) {

@@ -122,6 +122,21 @@ struct GemvArgs {
   // outputs: wave (blockIdx.x * TG + tile group) writes {max, index as int bits}
   // of its columns for every row m to amax[part * M + m] (first index on ties)
   float2* amax;
+  // EPI_ATOMIC norm-out (decode o_proj -> gate/up, no standalone norm launch):
+  // the last of the gridDim.y split-K workgroups of column block blockIdx.x
+  // (ticket lctr[blockIdx.x], reset by that workgroup) reads the block's
+  // finished sums back (sc1), forms h = rnd(rnd(acc) + lres) exactly as
+  // add_rms_norm rounds it, writes lres_out = h and the deferred-norm input
+  // lxo = rnd(w * h), re-zeroes its slice of the accumulator and adds the
+  // rows' sums of squares of h to lss [M]; the GLU GEMV applies
+  // rsqrt(lss / N + eps) in its epilogue (xpss below)
+  int* lctr;
+  const uint16_t* lres;
+  uint16_t* lres_out;
+  const uint16_t* lnw;
+  uint16_t* lxo;
+  float* lss;
+  int lunit;
 };
 
 }  // namespace illm

@@ -177,6 +177,12 @@ __device__ __forceinline__ uint4 ldw16(const uint8_t* p) {
 #ifndef ILLM_GEMV5_XDMA
 #define ILLM_GEMV5_XDMA 1
 #endif
+// x-side loads (activations, norm-in accumulator / residual / weight) issued
+// ahead of the weight ring (gemv5_body); ILLM_GEMV5_EARLYX=0 at build time
+// restores the round-5 order (A/B builds, tools/ab_lib.sh)
+#ifndef ILLM_GEMV5_EARLYX
+#define ILLM_GEMV5_EARLYX 1
+#endif
 typedef int32_t gv5_rsrc __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ gv5_rsrc gv5_make_rsrc(const void* base, uint32_t bytes) {
   const uint64_t p = (uint64_t)(uintptr_t)base;
@@ -188,10 +194,73 @@ __device__ __forceinline__ void gv5_dma16(const gv5_rsrc& rs, const void* lds, u
                :: "s"(la), "v"(voff), "s"(rs) : "memory", "m0");
 }
 
+// per-workgroup timeline stamps (tools/probe/gemv5_probe.hip PROBE_MODE=s,
+// built with its own definition): 0 entry, 1 x staged, 2 chunks computed,
+// 3 epilogue issued.  Empty in the library.
+#ifndef ILLM_GEMV5_STAMP
+#define ILLM_GEMV5_STAMP(i) ((void)0)
+#endif
+
 // block coordinates of one GEMV workgroup (blockIdx / gridDim of the launch)
 struct G5Blk {
   int x, y, z, gx, gy, gz;
 };
+
+// EPI_ATOMIC norm-out epilogue (gemv_args.h lctr ...): the last-arriving
+// split-K workgroup of column block blk.x turns the block's finished f32 sums
+// into the next layer half's inputs, so the standalone residual-add + RMSNorm
+// launch between o_proj and the gate/up GEMV goes away.  Hand-off: the adds
+// are memory-side f32 atomics, every wave waits for its own (vmcnt(0)) before
+// the workgroup's one agent-scope ticket, the last arriver reads the sums with
+// sc1 (L1-bypassing) loads -- the MI355X form used by the fused attention
+// combine (attn_dec_v3.cuh).  Thread v handles 4 consecutive columns of row
+// v / C4; a row's C4 threads are one aligned lane group (shuffle reduce).
+template <typename T>
+__device__ __forceinline__ void gemv5_norm_out(const GemvArgs& a, const G5Blk& blk, int Mloc, int nb, int NC,
+                                               int nthr) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* ctr = a.lctr + blk.x;
+    const int prev = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == blk.gy - 1;
+    if (prev == blk.gy - 1) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  auto rnd = [](float v) { return to_f32<T>(from_f32<T>(v)); };
+  const int C4 = NC / 4;                        // 16 or 32 (host-checked)
+  float* ws = (float*)a.out;
+  for (int v = threadIdx.x; v < Mloc * C4; v += nthr) {
+    const int m = v / C4, n = nb + 4 * (v % C4);
+    float ss = 0.f;
+    if (n < a.N) {                              // N % 4 == 0 (host-checked)
+      const size_t e = (size_t)m * a.N + n;
+      const float4 s = ld16_sc1(ws, e);
+      const uint2 r = *(const uint2*)(a.lres + e);
+      const uint2 w = *(const uint2*)(a.lnw + n);
+      const float sv[4] = {s.x, s.y, s.z, s.w};
+      const uint32_t rw[2] = {r.x, r.y}, ww[2] = {w.x, w.y};
+      float h[4], xo[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t rr = rw[i >> 1], wr = ww[i >> 1];
+        const float rv = to_f32<T>((uint16_t)((i & 1) ? rr >> 16 : rr & 0xffff));
+        float wv = to_f32<T>((uint16_t)((i & 1) ? wr >> 16 : wr & 0xffff));
+        if (a.lunit) wv = rnd(1.f + wv);
+        h[i] = rnd(rnd(sv[i]) + rv);
+        xo[i] = wv * h[i];
+        ss += h[i] * h[i];
+      }
+      *(uint2*)(a.lres_out + e) = make_uint2(pack2<T>(h[0], h[1]), pack2<T>(h[2], h[3]));
+      *(uint2*)(a.lxo + e) = make_uint2(pack2<T>(xo[0], xo[1]), pack2<T>(xo[2], xo[3]));
+      *(float4*)(ws + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (int o = C4 >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, C4);
+    if ((v & (C4 - 1)) == 0) __hip_atomic_fetch_add(a.lss + m, ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF, bool SCL>
 __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) {
   // PF: chunks in flight per wave (4; 8 = every chunk of a decode split-K
@@ -243,6 +312,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
   if (ILLM_DCHECK_FAILS((int64_t)blk.gx * TG * TPW >= NT && (int64_t)nks * cpk >= a.KC && Mloc <= 16, a.err,
                         ERR_GEOMETRY))
     return;
+  ILLM_GEMV5_STAMP(0);
   const size_t TB = (size_t)dk_tile_bytes(DK, a.KC);
   const size_t soff = (size_t)a.KC * dk_code_chunk(DK) + (size_t)g * 16;   // + c * 64: rows 4g..4g+3
   const size_t moff = soff + (size_t)16 * a.KC * 4;
@@ -283,12 +353,11 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
       if constexpr (HASMIN) mnl[t] = ldw16(tb[t] + moff + (size_t)cc * 64);
     }
   };
-  Chunk ring[PF];
-  if (wave_on) {
-    if constexpr (SCL) load_scl(wc0);
-#pragma unroll
-    for (int u = 0; u < PF; u++) load_chunk(ring[u], wc0 + u);
-  }
+  // GLU over a deferred-norm input staged elsewhere (gemv5_norm_out): the
+  // row's sum of squares, requested first, used by the epilogue
+  float xss_raw = 0.f;
+  if constexpr (EPI == EPI_GLU)
+    if (a.xpss != nullptr && a.xpart == nullptr) xss_raw = a.xpss[orow_of(min(r16, Mloc - 1))];
   // ---- zero a consumed atomic accumulator (its readers ran earlier in the
   // stream), spread over every workgroup of the grid (up to ~1 MB at M = 8)
   if (a.nzero) {
@@ -299,6 +368,43 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
     for (size_t i = bid * nthr + threadIdx.x; i < nv; i += nb * nthr)
       ((float4*)a.nzero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+
+  // ---- x staged by LDS-DMA BEFORE the weight ring.  Vector-memory loads
+  // retire in issue order, so x loads issued behind the ring (as before round
+  // 6) could be staged only once every weight chunk had arrived: the LDS
+  // staging, the block sums and the barrier sat behind the HBM round trip
+  // (per-workgroup stamps, profiles/gemv5_stamps_r6.jsonl).  Requested first,
+  // by LDS-DMA (no VGPRs: a register-staged early copy raised the kernel from
+  // 111 to 169 VGPRs and halved the resident workgroups), the staging waits
+  // only for its own pieces (counted vmcnt below).
+  const int xvpr = kw / 8;
+  const bool defer = a.nacc != nullptr && a.ndefer != 0;
+  const bool plain_x = !a.apo && !a.xpart && !defer && !a.nacc;
+  // 16-bit x that needs no conversion, whole K chunks inside K; each row in
+  // 1-KB pieces (64 lanes x 16 B), the last piece lane-masked
+  const bool dma_x = ILLM_GEMV5_XDMA && !(ILLM_GEMV5_ABL & 2) && plain_x && !MOE && std::is_same<C, T>::value &&
+                     kbase + kw <= a.K && (ILLM_GEMV5_EARLYX || Mloc * xvpr > 4 * NW * 64);
+  if (dma_x) {
+    const int per_row = (xvpr + 63) >> 6, nins = Mloc * per_row;
+    const gv5_rsrc rx = gv5_make_rsrc(a.x, (uint32_t)((size_t)a.M * a.ldx * 2));
+    for (int i = wave; i < nins; i += NW) {      // wave-uniform: one row piece per instruction
+      const int m = i / per_row, j = i - m * per_row;
+      if (j * 64 + lane < xvpr)
+        gv5_dma16(rx, xs + m * ldx + j * 512, (uint32_t)(((size_t)m * a.ldx + kbase + j * 512 + lane * 8) * 2));
+    }
+  }
+  asm volatile("" ::: "memory");             // the ring loads stay behind these
+
+  Chunk ring[PF];
+  if (wave_on) {
+    if constexpr (SCL) load_scl(wc0);
+#pragma unroll
+    for (int u = 0; u < PF; u++) load_chunk(ring[u], wc0 + u);
+  }
+  // ring load instructions per thread (the counted wait of the DMA staging)
+  constexpr int RING_LOADS = (SCL ? TPW * (1 + (HASMIN ? 1 : 0)) : 0) +
+                             PF * TPW * (BITS / 4 + (SCL ? 0 : 1 + (HASMIN ? 1 : 0)));
+  static_assert(RING_LOADS < 64, "vmcnt is 6 bits");
   if constexpr (DK == DK_LUT4) {
     if (threadIdx.x < 256)
       lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
@@ -356,7 +462,6 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
       h[2 * i + 1] = rnd(rnd(av[2 * i + 1]) + to_f32<T>((uint16_t)(rw[i] >> 16)));
     }
   };
-  const bool defer = a.nacc != nullptr && a.ndefer != 0;
   if (defer) {                    // per-row sum of squares of this workgroup's K slice (staging below)
     if (threadIdx.x < 16) ninv[threadIdx.x] = 0.f;
     __syncthreads();
@@ -459,19 +564,11 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
     }
     return val;
   };
-  const bool plain_x = !a.apo && !a.xpart && !defer && !a.nacc;
-  // LDS-DMA staging: 64-vector (1 KB) row pieces, whole K chunks of a
-  // 16-bit x that needs no conversion, more than one register batch per thread
-  const bool dma_x = ILLM_GEMV5_XDMA && !(ILLM_GEMV5_ABL & 2) && plain_x && !MOE && std::is_same<C, T>::value &&
-                     (vpr & 63) == 0 && kbase + kw <= a.K && Mloc * vpr > 4 * NW * 64;
   if (dma_x) {
-    const int per_row = vpr >> 6, nins = Mloc * per_row;
-    const gv5_rsrc rx = gv5_make_rsrc(a.x, (uint32_t)((size_t)a.M * a.ldx * 2));
-    for (int i = wave; i < nins; i += NW) {      // wave-uniform: one 1-KB row piece per instruction
-      const int m = i / per_row, j = i - m * per_row;
-      gv5_dma16(rx, xs + m * ldx + j * 512, (uint32_t)(((size_t)m * a.ldx + kbase + j * 512 + lane * 8) * 2));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the row pieces were requested before the weight ring (top): wait for
+    // them only -- every load issued later is one of this thread's ring loads
+    if (ILLM_GEMV5_EARLYX && wave_on) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(RING_LOADS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // the per-(row, 64-block) sums from the staged rows (8 lanes per block)
     const int nthr = NW * 64, total = Mloc * vpr;
@@ -500,18 +597,20 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
     // profiles/gemv5_ablation2_r3.jsonl abl 1 vs 3)
     constexpr int XPF = 4;
     const int nthr = NW * 64, total = Mloc * vpr;
-    for (int v0 = threadIdx.x; v0 < total; v0 += XPF * nthr) {
-      uint4 xv[XPF];
+    {
+      for (int v0 = threadIdx.x; v0 < total; v0 += XPF * nthr) {
+        uint4 xv[XPF];
 #pragma unroll
-      for (int u = 0; u < XPF; u++) {
-        const int vv = min(v0 + u * nthr, total - 1);
-        const int m = vv / vpr, kk = (vv % vpr) * 8;
-        xv[u] = kbase + kk < a.K ? *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk)
-                                 : make_uint4(0, 0, 0, 0);
+        for (int u = 0; u < XPF; u++) {
+          const int vv = min(v0 + u * nthr, total - 1);
+          const int m = vv / vpr, kk = (vv % vpr) * 8;
+          xv[u] = kbase + kk < a.K ? *(const uint4*)(a.x + (size_t)xrow_of(m) * a.ldx + kbase + kk)
+                                   : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < XPF; u++)
+          if (v0 + u * nthr < total) commit_x(v0 + u * nthr, to_c(xv[u]));
       }
-#pragma unroll
-      for (int u = 0; u < XPF; u++)
-        if (v0 + u * nthr < total) commit_x(v0 + u * nthr, to_c(xv[u]));
     }
   } else if (!(ILLM_GEMV5_ABL & 2) && a.nacc && !defer && !a.apo && !a.xpart) {
     // norm-in: h (exact in T) is already in LDS from the prologue; x = w * rnd(h * inv).
@@ -692,6 +791,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
     }
   }
   __syncthreads();
+  ILLM_GEMV5_STAMP(1);
   if (defer) {
     if constexpr (EPI == EPI_GLU) {
       // full K staged here: the row scale is known locally (applied before the activation)
@@ -803,6 +903,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
       if (c + u < c1u) compute_chunk(ring[u], c + u);
   }
 
+  ILLM_GEMV5_STAMP(2);
   if constexpr ((ILLM_GEMV5_ABL & 4) != 0) {
     if (acc[0][0] == 1234.5f) ((float*)a.out)[threadIdx.x] = acc[0][1];
     return;
@@ -861,6 +962,8 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
         __hip_atomic_fetch_add(ws + (size_t)m * a.N + n, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    ILLM_GEMV5_STAMP(3);
+    if (a.lctr != nullptr) gemv5_norm_out<T>(a, blk, Mloc, nb, NC, NW * 64);
     return;
   }
   if (tile0 >= NT) return;
@@ -870,7 +973,9 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
   const int m = orow_of(r16);
   if constexpr (EPI == EPI_GLU) {
     float o[4];
-    const float rs = defer ? ninv[r16] : 1.f;
+    const float rs = defer ? ninv[r16]
+                           : (a.xpss != nullptr && a.xpart == nullptr ? rsqrtf(xss_raw / (float)a.xpss_n + a.xpss_eps)
+                                                                      : 1.f);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const float gv = acc[0][i] * rs, uv = acc[TPW - 1][i] * rs;
@@ -882,6 +987,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
       if (n0 + 3 < a.N) *(uint2*)y = make_uint2(pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]));
       else for (int i = 0; i < 4 && n0 + i < a.N; i++) y[i] = from_f32<T>(o[i]);
     }
+    ILLM_GEMV5_STAMP(3);
   } else {
     float abest = -INFINITY;         // argmax partial (EPI_STORE + a.amax)
     int abi = 0x7fffffff;

@@ -168,6 +168,8 @@ TORCH_LIBRARY(ipex_llm_amd, m) {
   m.def("gemv_attn(Tensor po, Tensor pml, Tensor seq_lens, Tensor blob, int fmt, int n, int k, Tensor(a!)? acc, int ksplit, ScalarType dtype, Tensor(b!)? zero=None, int nw=0) -> Tensor");
   m.def("gemm(Tensor x, Tensor blob, int fmt, int n, int k, Tensor? bias) -> Tensor");
   m.def("gemv_accum(Tensor x, Tensor blob, int fmt, int n, int k, Tensor(a!) acc, int ksplit, Tensor(b!)? zero=None, Tensor? rope_cs=None, Tensor? rope_pos=None, int rope_cols=0, int rope_d=0) -> ()");
+  m.def("gemv_accum_norm(Tensor x, Tensor blob, int fmt, int n, int k, Tensor(a!) acc, Tensor(b!) ctr, Tensor residual, Tensor(c!) res_out, Tensor norm_w, bool unit_offset, Tensor(d!) xo, Tensor(e!) ss, Tensor(f!)? zero=None) -> ()");
+  m.def("gemv_glu_ss(Tensor x, Tensor blob, int fmt, int n, int k, int act, Tensor ss, int ss_n, float eps) -> Tensor");
   m.def("attn_decode_rope(Tensor part, Tensor? bias, Tensor cos_sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int Hq, int rot_dim, bool interleaved, float q_scale, ScalarType dtype, Tensor? pss=None, int pss_n=0, float pss_eps=0.0, bool prerot=False) -> Tensor");
   m.def("attn_decode_rope_split(Tensor part, Tensor? bias, Tensor cos_sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor block_tables, Tensor seq_lens, int nsplit, float scale, float softcap, int window, int Hq, int rot_dim, bool interleaved, float q_scale, ScalarType dtype, Tensor? pss=None, int pss_n=0, float pss_eps=0.0, bool prerot=False) -> (Tensor, Tensor)");
   m.def("gemm_glu(Tensor x, Tensor blob, int fmt, int n, int k, int act) -> Tensor");

@@ -626,6 +626,101 @@ void gemv_accum(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int
   launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_ATOMIC, dim3(p.gx, (unsigned)p.ks), p.shmem, a);
 }
 
+// gemv_accum whose last-arriving split-K workgroup per column block also does
+// the residual add and the deferred RMSNorm staging of the next GEMV's input
+// (lowbit_gemv5.cuh gemv5_norm_out): res_out = rnd(rnd(acc) + residual),
+// xo = rnd(w * res_out), ss[m] += sum of res_out[m]^2, acc re-zeroed.
+// ctr: int32 [>= column blocks], zero on the first call (self-resetting).
+void gemv_accum_norm(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, Tensor& acc,
+                     Tensor& ctr, const Tensor& residual, Tensor& res_out, const Tensor& norm_w, bool unit_offset,
+                     Tensor& xo, Tensor& ss, const c10::optional<Tensor>& zero) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda() && acc.is_cuda(), "gemv_accum_norm: GPU tensors expected");
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  const int64_t M = xc.numel() / k;
+  TORCH_CHECK(M >= 1 && M <= 16, "gemv_accum_norm handles 1..16 rows, got ", M);
+  TORCH_CHECK(n % 4 == 0, "gemv_accum_norm: n must be a multiple of 4");
+  TORCH_CHECK(acc.scalar_type() == at::kFloat && acc.is_contiguous() && acc.numel() == M * n,
+              "gemv_accum_norm: acc must be contiguous f32 [M, n]");
+  TORCH_CHECK(residual.is_contiguous() && res_out.is_contiguous() && xo.is_contiguous() &&
+                  residual.numel() == M * n && res_out.numel() == M * n && xo.numel() == M * n &&
+                  residual.scalar_type() == x.scalar_type() && res_out.scalar_type() == x.scalar_type() &&
+                  xo.scalar_type() == x.scalar_type() && norm_w.scalar_type() == x.scalar_type() &&
+                  norm_w.numel() == n && norm_w.is_contiguous(),
+              "gemv_accum_norm: residual / res_out / xo [M, n] and norm weight [n] in x's dtype");
+  TORCH_CHECK(res_out.data_ptr() != residual.data_ptr(), "gemv_accum_norm: res_out must not alias residual");
+  TORCH_CHECK(ss.scalar_type() == at::kFloat && ss.is_contiguous() && ss.numel() >= M, "gemv_accum_norm: ss f32 [>= M]");
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemv_accum_norm: weight blob too small");
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  illm::GemvArgs a{};
+  a.x = p16(xc);
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.KC = (int)KC;
+  a.lut_fmt = (int)fmt;
+  a.N = (int)n;
+  a.out = acc.data_ptr();
+  a.ldo = (int)n;
+  Plan5 p = plan5(M, NT, KC, true, 0, true);
+  p.kw = 1;                                   // column blocks of nw tiles: 64 / 128 columns
+  p.gx = (unsigned)((NT + p.nw - 1) / p.nw);
+  a.cpk = (int)p.cpk;
+  a.nw = p.nw;
+  set_zero(a, zero);
+  TORCH_CHECK(p.shmem <= kMaxLds, "gemv_accum_norm: K slice too large for LDS");
+  TORCH_CHECK(ctr.scalar_type() == at::kInt && ctr.is_contiguous() && ctr.numel() >= (int64_t)p.gx,
+              "gemv_accum_norm: ctr int32 [>= ", p.gx, "]");
+  a.lctr = ctr.data_ptr<int>();
+  a.lres = p16(residual);
+  a.lres_out = m16(res_out);
+  a.lnw = p16(norm_w);
+  a.lxo = m16(xo);
+  a.lss = ss.data_ptr<float>();
+  a.lunit = unit_offset ? 1 : 0;
+  launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_ATOMIC, dim3(p.gx, (unsigned)p.ks), p.shmem, a);
+}
+
+// gate/up GLU GEMV over a deferred-norm input (gemv_accum_norm's xo): the row
+// scale rsqrt(ss[m] / ss_n + eps) is applied to gate and up before the activation
+Tensor gemv_glu_ss(const Tensor& x, const Tensor& blob, int64_t fmt, int64_t n, int64_t k, int64_t act,
+                   const Tensor& ss, int64_t ss_n, double eps) {
+  TORCH_CHECK(x.is_cuda() && blob.is_cuda() && x.size(-1) == k, "gemv_glu_ss: GPU x [M, k]");
+  c10::DeviceGuard g(x.device());
+  const bool bf16 = is_bf16(x);
+  Tensor xc = x.contiguous();
+  const int64_t M = xc.numel() / k;
+  TORCH_CHECK(M >= 1 && M <= 16 && n % 32 == 0, "gemv_glu_ss: 1..16 rows, n a multiple of 32");
+  TORCH_CHECK(ss.is_cuda() && ss.scalar_type() == at::kFloat && ss.numel() >= M, "gemv_glu_ss: ss f32 [>= M]");
+  TORCH_CHECK(blob.numel() >= illm::dev_total_bytes((int)fmt, n, k), "gemv_glu_ss: weight blob too small");
+  const int64_t NT = illm::pad_to(n, illm::TILE_N) / illm::TILE_N;
+  const int64_t KC = illm::pad_to(k, illm::CHUNK_K) / illm::CHUNK_K;
+  illm::GemvArgs a{};
+  a.x = p16(xc);
+  a.M = (int)M;
+  a.K = (int)k;
+  a.ldx = (int)k;
+  a.w = blob.data_ptr<uint8_t>();
+  a.KC = (int)KC;
+  a.act = (int)act;
+  a.lut_fmt = (int)fmt;
+  a.xpss = ss.data_ptr<float>();
+  a.xpss_n = (int)ss_n;
+  a.xpss_eps = (float)eps;
+  Tensor out = at::empty({M, n / 2}, xc.options());
+  a.N = (int)(n / 2);
+  a.out = out.data_ptr();
+  a.ldo = (int)(n / 2);
+  const Plan5 p = plan5(M, NT / 2, KC, false);
+  TORCH_CHECK(p.shmem <= kMaxLds, "gemv_glu_ss: x slice exceeds LDS");
+  a.nw = p.nw;
+  launch_gemv5_any((int)fmt, bf16, p.kw, illm::EPI_GLU, dim3(p.gx, 1), p.shmem, a);
+  return out;
+}
+
 // down-projection GEMV whose input is act(gate) * up computed on the fly from
 // the gate/up GEMV's split-K slabs or atomic accumulator (saves the GLU
 // epilogue's unsplittable launch and one [M, I] round trip); returns f32
@@ -1627,6 +1722,8 @@ TORCH_LIBRARY_IMPL(ipex_llm_amd, CUDA, m) {
   m.impl("dequantize_device", &dequantize_device);
   m.impl("gemv", &gemv);
   m.impl("gemv_accum", &gemv_accum);
+  m.impl("gemv_accum_norm", &gemv_accum_norm);
+  m.impl("gemv_glu_ss", &gemv_glu_ss);
   m.impl("gemv_norm_in", &gemv_norm_in);
   m.impl("gemm_glu", &gemm_glu);
   m.impl("moe_gemm", &moe_gemm);

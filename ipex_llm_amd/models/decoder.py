@@ -183,6 +183,12 @@ DEFER_GLU_MAX_M = int(__import__("os").environ.get("ILLM_DEFER_GLU_MAX_M", "4"))
 # profiles/bench_b8_r3_mlpacc*.json): the down GEMV's input staging from the
 # [8, 28672] f32 gate/up slab costs more than the norm launch
 DEFER_MLP_ACC = __import__("os").environ.get("ILLM_DEFER_MLP_ACC", "0") == "1"
+# decode batches from this size on (up to DEFER_MAX_M) let the o_proj GEMV's
+# last-arriving split-K workgroups do the residual add and stage the deferred
+# gate/up input (ops.gemv_accum_norm -> ops.gemv_glu_ss): no standalone
+# add_rms_norm launch between attention and MLP (ILLM_ONORM=0 restores it)
+ONORM = __import__("os").environ.get("ILLM_ONORM", "1") != "0"
+ONORM_MIN_M = int(__import__("os").environ.get("ILLM_ONORM_MIN_M", "5"))
 # decode batches up to this size take the fused-RoPE attention (qkv accumulated
 # atomically into one slab read by the attention, re-zeroed by its combine).
 # Measured on MI355X (Llama-3-8B, L=1024): batch 1 1.960 -> 1.910 ms/token,
@@ -396,16 +402,25 @@ class NativeCausalLM(nn.Module):
             acc.copy_(out)
         return acc
 
-    def _acc(self, n: int, t: int, device, tag: str = "") -> torch.Tensor:
+    def _acc(self, n: int, t: int, device, tag: str = "", dtype=torch.float32) -> torch.Tensor:
         """Zeroed f32 [t, n] accumulator for the split-K atomic GEMV
         (ops.gemv_accum); its consumer re-zeroes it after reading (or a later
         launch does, ``tag``-separated buffers of the norm-in path), so one
         buffer per shape serves every layer and every hipGraph replay."""
-        key = (n, t, tag)
+        key = (n, t, tag, dtype)
         buf = self._acc_bufs.get(key)
         if buf is None or buf.device != device:
-            buf = torch.zeros(t, n, dtype=torch.float32, device=device)
+            buf = torch.zeros(t, n, dtype=dtype, device=device)
             self._acc_bufs[key] = buf
+        return buf
+
+    def _ctr(self, device, n: int = 4096) -> torch.Tensor:
+        """int32 tickets of the last-arriver GEMV epilogues (ops.gemv_accum_norm):
+        zero once, every launch's last arriver resets its own"""
+        buf = self._acc_bufs.get(("ctr", device))
+        if buf is None or buf.numel() < n:
+            buf = torch.zeros(n, dtype=torch.int32, device=device)
+            self._acc_bufs[("ctr", device)] = buf
         return buf
 
     # decode (norm-in + fused-RoPE path): attention partials merged in the o_proj
@@ -734,6 +749,9 @@ class NativeCausalLM(nn.Module):
                 H = o.out_features
                 accP, accD = self._acc(H, T, x.device, "P"), self._acc(H, T, x.device, "D")
                 zero_qkv = None
+                onorm = (ONORM and defer and ONORM_MIN_M <= T and not (T > DEFER_GLU_MAX_M and DEFER_MLP_ACC)
+                         and o.mp_group is None and o.bias is None and H % 4 == 0
+                         and not (rope_in and self._oproj_combine and o.bias is None))
                 if rope_in and self._oproj_combine and o.bias is None:
                     # split attention without its combine launch: the o_proj GEMV
                     # merges each head's partials while staging its K slice (head-
@@ -749,10 +767,23 @@ class NativeCausalLM(nn.Module):
                     zero_qkv = qkv_acc
                 else:
                     a = a_rope if rope_in else self._attention(li, attn, q, meta, cache)
-                    ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
+                    if onorm:
+                        # o_proj + residual add + deferred-norm staging of the gate/up input
+                        r2 = nxt_res(residual)
+                        xo = self._acc(H, T, x.device, "XO", self.dtype)
+                        ops.gemv_accum_norm(a, o.weight, o.fmt, H, o.in_features, accP, self._ctr(x.device),
+                                            residual, r2, layer.post_attention_layernorm, s.norm_unit_offset, xo,
+                                            ss_all[2 * li + 1], zero=consumed)
+                        residual = r2
+                    else:
+                        ops.gemv_accum(a, o.weight, o.fmt, H, o.in_features, accP, 0, zero=consumed)
                 self._reduce(accP, o)
                 gu, dn = mlp.gate_up_proj, mlp.down_proj
-                if defer and T > DEFER_GLU_MAX_M and DEFER_MLP_ACC:
+                if onorm:
+                    act = ops.gemv_glu_ss(xo, gu.weight, gu.fmt, gu.out_features, gu.in_features, s.act,
+                                          ss_all[2 * li + 1], s.hidden_size, s.rms_eps)
+                    ops.gemv_accum(act, dn.weight, dn.fmt, dn.out_features, dn.in_features, accD, 0, zero=zero_qkv)
+                elif defer and T > DEFER_GLU_MAX_M and DEFER_MLP_ACC:
                     r2 = nxt_res(residual)
                     gacc = self._acc(gu.out_features, T, x.device, "GU")
                     ss2 = ss_all[2 * li + 1]

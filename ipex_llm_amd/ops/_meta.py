@@ -141,6 +141,16 @@ def _(x, blob, fmt, n, k, acc, ksplit, zero=None, rope_cs=None, rope_pos=None, r
     return None
 
 
+@register_fake("ipex_llm_amd::gemv_accum_norm")
+def _(x, blob, fmt, n, k, acc, ctr, residual, res_out, norm_w, unit_offset, xo, ss, zero=None):
+    return None
+
+
+@register_fake("ipex_llm_amd::gemv_glu_ss")
+def _(x, blob, fmt, n, k, act, ss, ss_n, eps):
+    return x.new_empty((x.numel() // k, n // 2))
+
+
 @register_fake("ipex_llm_amd::gemv_norm_in")
 def _(acc_in, residual, res_out, norm_w, eps, unit_offset, blob, fmt, n, k, epi, act, acc_out=None, zero=None,
       ss=None, rope_cs=None, rope_pos=None, rope_cols=0, rope_d=0):

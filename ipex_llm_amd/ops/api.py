@@ -18,7 +18,7 @@ __all__ = [
     "fp8_quantize_weight", "dense_linear", "check_kernel_errors", "KernelError", "repack_to_device", "repack_from_device", "lowbit_matmul",
     "gemv_partials", "gemv_glu", "add_rms_norm", "rms_norm", "layer_norm", "rope_kv",
     "attn_decode", "glu", "attn_softmax_", "moe_topk", "reduce_partials", "to_fp8_bytes", "GEMV_MAX_M", "gather_kv",
-    "moe_align", "moe_gemm", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum",
+    "moe_align", "moe_gemm", "moe_gemv_glu", "moe_gemv_partials", "moe_combine", "moe_route", "moe_gemv_accum", "rope_kv_fused", "gemv_glu_in", "gemv_accum", "gemv_accum_norm", "gemv_glu_ss",
     "attn_decode_split", "gemv_attn", "gemv_norm_in", "attn_decode_rope", "attn_decode_rope_split", "attn_prefill", "moe_group_topk",
 ]
 
@@ -241,6 +241,43 @@ def gemv_accum(x, blob, fmt, n, k, acc: torch.Tensor, ksplit: int = 0,
         zero.zero_()
     acc += _rope_cols(lowbit_matmul(x, blob, fmt, n, k).float(), rope, x.dtype).view_as(acc)
     return acc
+
+
+def gemv_accum_norm(x, blob, fmt, n, k, acc: torch.Tensor, ctr: torch.Tensor, residual: torch.Tensor,
+                    res_out: torch.Tensor, norm_w: torch.Tensor, unit_offset: bool, xo: torch.Tensor,
+                    ss: torch.Tensor, zero: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``gemv_accum`` whose last split-K workgroup per column block also does
+    the residual add and stages the deferred RMSNorm input of the next GEMV
+    (decode o_proj -> gate/up without a norm launch): res_out = rnd(rnd(x W^T)
+    + residual), xo = rnd(w * res_out), ss[m] += sum(res_out[m]^2); ``acc``
+    (zero on entry) is left zeroed, ``ctr`` int32 tickets (zero on the first
+    call) reset themselves.  The consumer is ``gemv_glu_ss``."""
+    if _native(x):
+        _ops().gemv_accum_norm(x, blob, fmt, n, k, acc, ctr, residual, res_out, norm_w, unit_offset, xo, ss, zero)
+        return xo
+    if zero is not None:
+        zero.zero_()
+    y = lowbit_matmul(x, blob, fmt, n, k).float().view_as(acc) + acc
+    h = (y.to(residual.dtype).float() + residual.float()).to(residual.dtype)
+    res_out.copy_(h.view_as(res_out))
+    w = norm_w.float() + 1.0 if unit_offset else norm_w.float()
+    xo.copy_((w.to(residual.dtype).float() * h.float()).to(residual.dtype).view_as(xo))
+    ss[:h.shape[0]] += h.float().pow(2).sum(-1)
+    acc.zero_()
+    return xo
+
+
+def gemv_glu_ss(x, blob, fmt, n, k, act: int, ss: torch.Tensor, ss_n: int, eps: float) -> torch.Tensor:
+    """act(s x Wg^T) * (s x Wu^T) with s = rsqrt(ss / ss_n + eps) per row: the
+    gate/up GEMV over ``gemv_accum_norm``'s deferred-norm input."""
+    if _native(x):
+        return _ops().gemv_glu_ss(x, blob, fmt, n, k, act, ss, ss_n, eps)
+    from ..models.decoder import deinterleave_glu
+    M = x.numel() // k
+    inv = torch.rsqrt(ss[:M].float() / ss_n + eps)[:, None]
+    g, u = deinterleave_glu(lowbit_matmul(x, blob, fmt, n, k).float())
+    g, u = g * inv, u * inv
+    return ((F.silu(g) if act == 0 else F.gelu(g, approximate="tanh")) * u).to(x.dtype).contiguous()
 
 
 def _rope_cols(y: torch.Tensor, rope, dtype) -> torch.Tensor:

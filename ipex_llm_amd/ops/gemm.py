@@ -109,7 +109,15 @@ class ChargedCache(dict):
         if ent is None:
             return default[0] if default else None
         _dense_bytes[0] -= ent[2]
+        # entries of other caches that view this entry's storage (charged 0) go too:
+        # a surviving view would keep the bytes alive after their refund
+        for c, k in self.__dict__.get("_links", {}).pop(key, ()):
+            c.pop(k)
         return ent
+
+    def link(self, key, other: "ChargedCache", okey):
+        """drop ``other[okey]`` (a view of this entry's shadow) with ``self[key]``"""
+        self.__dict__.setdefault("_links", {}).setdefault(key, []).append((other, okey))
 
     def __delitem__(self, key):
         self.pop(key)

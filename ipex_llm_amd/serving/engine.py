@@ -61,10 +61,27 @@ class LLMEngine:
     def __init__(self, model: NativeCausalLM, max_batch: int = 64, block_size: int = 64,
                  num_blocks: Optional[int] = None, max_model_len: int = 8192, max_prefill_tokens: int = 8192,
                  kv_fp8: int = 0, memory_fraction: float = 0.5, eos_token_id=None, use_graph: bool = True,
-                 enable_prefix_caching: bool = True):
+                 enable_prefix_caching: bool = True, tp_group="auto"):
         ops.require() if model.device.type == "cuda" else None
         self.model = model
         s = model.spec
+        # tensor-parallel serving (reference: vLLM --tensor-parallel-size,
+        # SRC/vllm/xpu/model_convert.py:36-75): one process per GPU, each with its
+        # shard of the model and of the KV cache.  Rank 0 (the driver) owns the
+        # requests and the C++ scheduler and broadcasts each step's plan (token
+        # ids, positions, block tables); every rank runs the same forwards --
+        # the row-parallel all-reduces and the vocab-parallel logits gather
+        # happen inside them -- and only the driver samples.  Ranks > 0 sit in
+        # run_worker().
+        self.tp_group = getattr(model, "tp_group", None) if tp_group == "auto" else tp_group
+        self.tp_world, self.tp_rank = 1, 0
+        if self.tp_group is not None:
+            import torch.distributed as dist
+            self.tp_world, self.tp_rank = dist.get_world_size(self.tp_group), dist.get_rank(self.tp_group)
+            if self.tp_world == 1:
+                self.tp_group = None
+        self.is_driver = self.tp_rank == 0
+        self._stopped = False
         if num_blocks is None:
             per_tok = PagedKVCache.bytes_per_token(len(model.layers), s.num_kv_heads, s.head_dim, model.dtype, kv_fp8)
             if model.device.type == "cuda":
@@ -74,6 +91,8 @@ class LLMEngine:
                 budget = per_tok * max_batch * max_model_len // 4
             num_blocks = max(max_batch, budget // (per_tok * block_size))
             num_blocks = min(num_blocks, max_batch * ((max_model_len + block_size - 1) // block_size))
+            if self.tp_group is not None:      # one block layout on every rank: the smallest pool
+                num_blocks = int(self._tp_reduce_min(num_blocks))
         # one extra block past the scheduler's pool: the scratch target of the
         # padding rows of a captured decode step
         self.cache = model.make_cache(max_model_len, max_batch, block_size, kv_fp8, num_blocks=num_blocks + 1)
@@ -138,7 +157,8 @@ class LLMEngine:
                 self._finish(r, "abort")
 
     def has_work(self) -> bool:
-        return any(not r.finished for r in self.requests.values())
+        # a snapshot: request threads add / pop entries while the loop polls
+        return any(not r.finished for r in list(self.requests.values()))
 
     # ------------------------------------------------------------ step
     def _finish(self, r: Request, reason: str):
@@ -184,6 +204,78 @@ class LLMEngine:
             t[i, :len(x)] = torch.tensor(x, dtype=torch.int32)
         return t.to(self.model.device)
 
+    # ------------------------------------------------------------ tensor parallel
+    def _tp_device(self):
+        import torch.distributed as dist
+        return self.model.device if dist.get_backend(self.tp_group) == "nccl" else torch.device("cpu")
+
+    def _tp_reduce_min(self, v: int) -> int:
+        import torch.distributed as dist
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self._tp_device())
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.tp_group)
+        return int(t.item())
+
+    def _tp_bcast(self, plan: Optional[List[int]]) -> List[int]:
+        """the driver's step plan to every rank (length, then the int64 words)"""
+        import torch.distributed as dist
+        dev, src = self._tp_device(), dist.get_global_rank(self.tp_group, 0)
+        n = torch.tensor([len(plan) if plan is not None else 0], dtype=torch.int64, device=dev)
+        dist.broadcast(n, src, group=self.tp_group)
+        buf = torch.tensor(plan, dtype=torch.int64, device=dev) if plan is not None else \
+            torch.empty(int(n.item()), dtype=torch.int64, device=dev)
+        dist.broadcast(buf, src, group=self.tp_group)
+        return buf.tolist() if plan is None else plan
+
+    @staticmethod
+    def encode_plan(prefill, decode) -> List[int]:
+        """[1, #prefill, #decode, (n, start, #blocks, tokens[start:n], blocks)...,
+        (id, pos, #blocks, blocks)...]; [0] stops the workers"""
+        out = [1, len(prefill), len(decode)]
+        for toks, start, blocks in prefill:
+            out += [len(toks), start, len(blocks)] + list(toks[start:]) + list(blocks)
+        for tok, pos, blocks in decode:
+            out += [tok, pos, len(blocks)] + list(blocks)
+        return out
+
+    @staticmethod
+    def decode_plan(words: List[int]):
+        if not words or words[0] == 0:
+            return None
+        i, prefill, decode = 3, [], []
+        for _ in range(words[1]):
+            n, start, nb = words[i:i + 3]
+            i += 3
+            suffix = words[i:i + n - start]
+            i += n - start
+            prefill.append(([0] * start + suffix, start, words[i:i + nb]))
+            i += nb
+        for _ in range(words[2]):
+            tok, pos, nb = words[i:i + 3]
+            i += 3
+            decode.append((tok, pos, words[i:i + nb]))
+            i += nb
+        return prefill, decode
+
+    @torch.no_grad()
+    def run_worker(self):
+        """ranks > 0: execute the driver's plans until it stops the group"""
+        assert self.tp_group is not None and not self.is_driver, "run_worker: tensor-parallel ranks > 0 only"
+        while True:
+            plan = self.decode_plan(self._tp_bcast(None))
+            if plan is None:
+                return
+            prefill, decode = plan
+            for toks, start, blocks in prefill:
+                self._exec_prefill(toks, start, blocks)
+            if decode:
+                self._exec_decode([d[0] for d in decode], [d[1] for d in decode], [d[2] for d in decode])
+
+    def shutdown(self):
+        """driver: release the tensor-parallel workers (idempotent)"""
+        if self.tp_group is not None and self.is_driver and not self._stopped:
+            self._stopped = True
+            self._tp_bcast([0])
+
     # ------------------------------------------------------------ graph decode
     @staticmethod
     def _bucket(x: int, lo: int = 1) -> int:
@@ -222,9 +314,8 @@ class LLMEngine:
         self._graphs[(Bb, Wb)] = g
         return g
 
-    def _decode_graph(self, rids: List[int], pos_l: List[int]) -> torch.Tensor:
-        B = len(rids)
-        rows = [list(self.sched.blocks(r)) for r in rids]
+    def _decode_graph(self, ids_l: List[int], pos_l: List[int], rows: List[List[int]]) -> torch.Tensor:
+        B = len(ids_l)
         Bb = self._bucket(B)
         Wb = self._bucket(max(len(x) for x in rows), 4)
         g = self._graphs.get((Bb, Wb)) or self._capture(Bb, Wb)
@@ -234,12 +325,43 @@ class LLMEngine:
         pos = torch.zeros(Bb, dtype=torch.long)
         pos[:B] = torch.tensor(pos_l)
         ids = torch.zeros(Bb, dtype=torch.long)
-        ids[:B] = torch.tensor([self.requests[r].tokens[-1] for r in rids])
+        ids[:B] = torch.tensor(ids_l)
         g["bt"].copy_(bt, non_blocking=True)
         g["pos"].copy_(pos, non_blocking=True)
         g["ids"].copy_(ids, non_blocking=True)
         g["graph"].replay()
         return g["logits"][:B]
+
+    def _exec_prefill(self, toks: List[int], start: int, blocks: List[int]) -> torch.Tensor:
+        """forward of toks[start:] over the cached prefix; last-position logits"""
+        m, dev, bs = self.model, self.model.device, self.block_size
+        n = len(toks)
+        tq = n - start
+        bt = torch.tensor([list(blocks)], dtype=torch.int32).to(dev)
+        pos_h = torch.arange(start, n)
+        bl = torch.tensor(list(blocks), dtype=torch.long)
+        slots = (bl[pos_h // bs] * bs + pos_h % bs).to(dev)
+        meta = AttnMeta(1, tq, bt, torch.tensor([n], dtype=torch.int32, device=dev), nsplit_for(n), [n])
+        return m.forward_tokens(torch.tensor(toks[start:], device=dev), pos_h.to(dev), slots, meta,
+                                self.cache, logits_idx=torch.tensor([tq - 1], device=dev))
+
+    def _exec_decode(self, ids_l: List[int], pos_l: List[int], rows: List[List[int]]) -> torch.Tensor:
+        """one decode forward of len(ids_l) sequences (graph bucket or eager)"""
+        m, dev, bs = self.model, self.model.device, self.block_size
+        B = len(ids_l)
+        if self.use_graph and self._bucket(B) <= self._graph_max_b:
+            return self._decode_graph(ids_l, pos_l, rows)
+        w = max(len(x) for x in rows)
+        bt = torch.zeros(B, w, dtype=torch.int32)
+        for i, x in enumerate(rows):
+            bt[i, :len(x)] = torch.tensor(list(x), dtype=torch.int32)
+        bt = bt.to(dev)
+        pos = torch.tensor(pos_l, device=dev)
+        blk = torch.gather(bt, 1, (pos // bs).unsqueeze(1).to(torch.int64)).squeeze(1).long()
+        slots = blk * bs + pos % bs
+        seq_lens = (pos + 1).to(torch.int32)
+        meta = AttnMeta(B, 1, bt, seq_lens, nsplit_for(max(pos_l) + 1), [p + 1 for p in pos_l])
+        return m.forward_tokens(torch.tensor(ids_l, device=dev), pos, slots, meta, self.cache)
 
     @torch.no_grad()
     def step(self) -> int:
@@ -250,6 +372,8 @@ class LLMEngine:
             return self._step()
 
     def _step(self) -> int:
+        if not self.is_driver:
+            raise RuntimeError("LLMEngine.step: tensor-parallel ranks > 0 run run_worker(), not step()")
         t_step = time.perf_counter()
         with self.lock:
             plan = list(self.sched.schedule())
@@ -263,21 +387,20 @@ class LLMEngine:
                 r.finished, r.finish_reason = True, "error: request does not fit in the KV cache"
                 if r.on_token is not None:
                     r.on_token(-1, r)
-            m, dev, bs = self.model, self.model.device, self.block_size
             produced = 0
+            pre = []
             for rid in prefill:
+                toks = self.requests[rid].tokens
+                pre.append((toks, int(self.sched.cached(rid)), list(self.sched.blocks(rid))))
+            dec = [(self.requests[rid].tokens[-1], int(self.sched.cached(rid)), list(self.sched.blocks(rid)))
+                   for rid in decode]
+            if self.tp_group is not None and (pre or dec):
+                self._tp_bcast(self.encode_plan(pre, dec))
+            for rid, (toks, start, blocks) in zip(prefill, pre):
                 r = self.requests[rid]
-                toks = r.tokens
                 n = len(toks)
-                start = int(self.sched.cached(rid))        # prefix already in cached KV blocks
-                tq = n - start
-                bt = self._block_table([rid])
-                pos_h = torch.arange(start, n)
-                blocks = torch.tensor(list(self.sched.blocks(rid)), dtype=torch.long)
-                slots = (blocks[pos_h // bs] * bs + pos_h % bs).to(dev)
-                meta = AttnMeta(1, tq, bt, torch.tensor([n], dtype=torch.int32, device=dev), nsplit_for(n), [n])
-                lg = m.forward_tokens(torch.tensor(toks[start:], device=dev), pos_h.to(dev), slots, meta,
-                                      self.cache, logits_idx=torch.tensor([tq - 1], device=dev))
+                tq = n - start                               # prefix already in cached KV blocks
+                lg = self._exec_prefill(toks, start, blocks)
                 self.sched.advance(rid, tq)
                 self.stats["prefill_tokens"] += tq
                 self.stats["prefix_hit_tokens"] += start
@@ -288,18 +411,7 @@ class LLMEngine:
             if decode:
                 rs = [self.requests[rid] for rid in decode]
                 B = len(rs)
-                pos_l = [int(self.sched.cached(rid)) for rid in decode]
-                if self.use_graph and self._bucket(B) <= self._graph_max_b:
-                    lg = self._decode_graph(decode, pos_l)
-                else:
-                    bt = self._block_table(decode)
-                    pos = torch.tensor(pos_l, device=dev)
-                    blk = torch.gather(bt, 1, (pos // bs).unsqueeze(1).to(torch.int64)).squeeze(1).long()
-                    slots = blk * bs + pos % bs
-                    seq_lens = (pos + 1).to(torch.int32)
-                    meta = AttnMeta(B, 1, bt, seq_lens, nsplit_for(max(pos_l) + 1), [p + 1 for p in pos_l])
-                    ids = torch.tensor([r.tokens[-1] for r in rs], device=dev)
-                    lg = m.forward_tokens(ids, pos, slots, meta, self.cache)
+                lg = self._exec_decode([d[0] for d in dec], [d[1] for d in dec], [d[2] for d in dec])
                 greedy = all(not r.params.do_sample and r.params.repetition_penalty == 1.0 for r in rs)
                 nxt = torch.argmax(lg, -1).tolist() if greedy else None
                 for i, r in enumerate(rs):

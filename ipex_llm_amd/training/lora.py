@@ -163,9 +163,12 @@ def _skinny(x2: torch.Tensor, W: torch.Tensor, alpha: float = 1.0) -> torch.Tens
     tile; the library GEMM elsewhere"""
     from .. import ops
     r, K = W.shape
+    # the factor is pre-scaled in its 16-bit dtype: exact only for a power-of-two
+    # alpha (alpha / r = 16 / 8 ...); any other scale (16 / 12, rsLoRA) keeps the
+    # library GEMM, which applies alpha to the f32 sums (ADVICE r5)
     if (_SKINNY and x2.is_cuda and ops.native_gpu(x2) and x2.dtype in (torch.bfloat16, torch.float16)
             and W.dtype == x2.dtype and x2.is_contiguous() and K % 64 == 0 and r <= 64
-            and x2.shape[0] >= 64):
+            and x2.shape[0] >= 64 and _pow2(alpha)):
         Wc = (W * alpha if alpha != 1.0 else W).contiguous()
         dlt = torch.ops.ipex_llm_amd.dense_linear_t            # [tokens, rows] straight from the kernel
         if r <= 16:
@@ -174,6 +177,12 @@ def _skinny(x2: torch.Tensor, W: torch.Tensor, alpha: float = 1.0) -> torch.Tens
     if alpha == 1.0:
         return torch.mm(x2, W.t())
     return torch.addmm(x2.new_empty(()), x2, W.t(), beta=0, alpha=alpha)
+
+
+def _pow2(a: float) -> bool:
+    """a is +-2^e (multiplying by it is exact in any float format, barring range)"""
+    m, _ = math.frexp(abs(float(a)))
+    return a != 0 and m == 0.5
 
 
 # ILLM_LORA_SKINNY=0: the rank-r down-projections on the library GEMM (A/B)
@@ -383,6 +392,7 @@ def _aug_rows_weight(base, Rp: int, dtype, A=None):
         _dense_cache.pop(dkey)
         _aug_cache.put(key, blob, w, w.numel() * w.element_size())
         _dense_cache.put(dkey, blob, w[:N], 0)
+        _aug_cache.link(key, _dense_cache, dkey)      # the 0-charged view leaves with its storage
         ent = _aug_cache[key]
     w = ent[1]
     if A is not None:
@@ -877,15 +887,25 @@ def _patch_rotary(model: nn.Module) -> int:
     ``attention_scaling``) compute cos / sin with a batched f32 matmul of the
     [D/2, 1] frequencies by the [1, T] positions -- a K = 1 library GEMM per
     forward.  The same products as one broadcast multiply (exact: each entry
-    is a single f32 product either way)."""
+    is a single f32 product either way).
+
+    Only the standard 2-D form ([bs, seq] positions) is replaced: a rotary
+    whose forward takes other positions (Qwen2-VL / Qwen2.5-Omni M-RoPE with
+    [3, bs, seq]) keeps its own forward, and any call whose positions are not
+    2-D falls back to the original forward."""
     n = 0
     for name, m in model.named_modules():
         if not name.endswith("rotary_emb") or not hasattr(m, "inv_freq") or not hasattr(m, "attention_scaling"):
             continue
         if getattr(m, "rope_type", "default") != "default" or getattr(m, "_illm_rope", False):
             continue
+        if "VL" in type(m).__name__ or "Omni" in type(m).__name__ or hasattr(m, "mrope_section"):
+            continue                    # multimodal (3-D M-RoPE) rotaries
+        orig = m.forward
 
-        def fwd(x, position_ids, _m=m):
+        def fwd(x, position_ids, *args, _m=m, _orig=orig, **kw):
+            if position_ids.dim() != 2 or args or kw:
+                return _orig(x, position_ids, *args, **kw)
             freqs = position_ids[:, :, None].float() * _m.inv_freq.float()[None, None, :]
             emb = torch.cat((freqs, freqs), dim=-1)
             return (emb.cos() * _m.attention_scaling).to(x.dtype), (emb.sin() * _m.attention_scaling).to(x.dtype)

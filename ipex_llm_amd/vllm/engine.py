@@ -107,9 +107,20 @@ class IPEXLLMLLMEngine:
     @classmethod
     def from_engine_args(cls, engine_args: EngineArgs, load_in_low_bit: str = "sym_int4", **_):
         a = engine_args
+        tp_group = None
         if a.tensor_parallel_size != 1:
-            raise ValueError("tensor_parallel_size > 1: launch one process per GPU "
-                             "(parallel.autotp / serving.pp_worker), not an in-process engine")
+            # one process per GPU (torchrun --nproc-per-node N ...): every rank
+            # loads its AutoTP shard (the reference's per-rank low-bit convert,
+            # SRC/vllm/xpu/model_convert.py:36-75); rank 0 serves, the others
+            # run engine.run_worker() (see tp_worker_or_driver)
+            import torch.distributed as dist
+            from ..parallel.comm import init_distributed
+            init_distributed()
+            if dist.get_world_size() != a.tensor_parallel_size:
+                raise ValueError(f"tensor_parallel_size={a.tensor_parallel_size} but {dist.get_world_size()} "
+                                 "ranks are running: launch with torchrun --nproc-per-node "
+                                 f"{a.tensor_parallel_size}")
+            tp_group = dist.group.WORLD
         tok = None
         if isinstance(a.model, torch.nn.Module):
             model = a.model
@@ -118,8 +129,9 @@ class IPEXLLMLLMEngine:
             from ..transformers import AutoModelForCausalLM
             dt = {"auto": torch.bfloat16, "bfloat16": torch.bfloat16, "float16": torch.float16,
                   "half": torch.float16}.get(a.dtype, torch.bfloat16)
+            kw = {"tp_group": tp_group} if tp_group is not None else {}
             model = AutoModelForCausalLM.from_pretrained(a.model, load_in_low_bit=load_in_low_bit, torch_dtype=dt,
-                                                         trust_remote_code=a.trust_remote_code)
+                                                         trust_remote_code=a.trust_remote_code, **kw)
             dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
             model = model.to(dev)
             tok = AutoTokenizer.from_pretrained(a.tokenizer or a.model, trust_remote_code=a.trust_remote_code)
@@ -143,6 +155,17 @@ class IPEXLLMLLMEngine:
 
     def get_tokenizer(self):
         return self.tokenizer
+
+    @property
+    def is_driver(self) -> bool:
+        return self.engine.is_driver
+
+    def run_worker(self):
+        """tensor-parallel ranks > 0: replay the driver's steps until it shuts down"""
+        self.engine.run_worker()
+
+    def shutdown(self):
+        self.engine.shutdown()
 
     def _ids(self, prompt: Optional[str], prompt_token_ids: Optional[Sequence[int]]) -> List[int]:
         if prompt_token_ids is not None:
@@ -168,7 +191,8 @@ class IPEXLLMLLMEngine:
             self._text.pop(str(q), None)
             if rid is not None:
                 self.engine.abort(rid)
-                self.engine.requests.pop(rid, None)
+                with self.engine.lock:          # the engine loop thread walks requests
+                    self.engine.requests.pop(rid, None)
 
     def has_unfinished_requests(self) -> bool:
         return self.engine.has_work()
@@ -209,6 +233,18 @@ class IPEXLLMClass:
                           device=device, trust_remote_code=bool(kwargs.get("trust_remote_code", False)))
         self.llm_engine = IPEXLLMLLMEngine.from_engine_args(args, load_in_low_bit=load_in_low_bit)
         self._counter = itertools.count()
+        if tensor_parallel_size > 1:
+            # the same script on every rank (torchrun): ranks > 0 serve the
+            # driver's forwards here and leave when it exits; the driver
+            # releases them at interpreter exit (or llm.shutdown())
+            if not self.llm_engine.is_driver:
+                self.llm_engine.run_worker()
+                raise SystemExit(0)
+            import atexit
+            atexit.register(self.llm_engine.shutdown)
+
+    def shutdown(self):
+        self.llm_engine.shutdown()
 
     def get_tokenizer(self):
         return self.llm_engine.get_tokenizer()
@@ -267,7 +303,8 @@ class IPEXLLMAsyncLLMEngine:
             text = tok.decode(gen, skip_special_tokens=True) if tok is not None else ""
             yield RequestOutput(str(request_id), prompt, pids, [CompletionOutput(0, text, gen, why)], fin)
             if fin:
-                with self._lock:
+                # under the serving engine's own lock: its loop thread walks requests
+                with self._lock, self.engine.engine.lock:
                     self.engine.engine.requests.pop(rid, None)
                     self.engine._rid.pop(str(request_id), None)
                     self.engine._text.pop(str(request_id), None)

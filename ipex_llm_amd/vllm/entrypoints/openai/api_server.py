@@ -1,5 +1,7 @@
 """``python -m ipex_llm_amd.vllm.entrypoints.openai.api_server --model PATH
---load-in-low-bit sym_int4`` -- the reference's vLLM OpenAI server command
+--load-in-low-bit sym_int4 [--tensor-parallel-size N]`` (N > 1: under
+``torchrun --nproc-per-node N``, one process per GPU; rank 0 serves) -- the
+reference's vLLM OpenAI server command
 (``SRC/vllm/xpu/entrypoints/openai/api_server.py``) on the native engine:
 the model is loaded and converted by ``vllm.engine.IPEXLLMLLMEngine``, the
 routes (``/v1/models``, ``/v1/completions``, ``/v1/chat/completions``,
@@ -43,9 +45,17 @@ def main(argv=None):
     ign = unsupported(args)
     if ign:
         log.warning("vLLM flags accepted without effect here: %s", ", ".join(ign))
-    app, _ = build_app_from_args(args)
+    app, eng = build_app_from_args(args)
+    if not eng.is_driver:
+        # --tensor-parallel-size N under torchrun: ranks > 0 only execute the
+        # driver's (rank 0's) step plans; rank 0 alone serves HTTP
+        eng.run_worker()
+        return
     import uvicorn
-    uvicorn.run(app, host=args.host, port=args.port)
+    try:
+        uvicorn.run(app, host=args.host, port=args.port)
+    finally:
+        eng.shutdown()
 
 
 if __name__ == "__main__":

@@ -114,3 +114,55 @@ def test_native_ep_token_sharded_matches_single(world):
     from ipex_llm_amd.models.builder import random_native_model
     single = random_native_model(_mixtral_cfg(), "sym_int8", "cpu", torch.float32, seed=0, std=0.05)
     _run(_worker, world, "ep_a2a", _generate(single))
+
+
+def _serve_tp_worker(rank, world, port, want):
+    """tensor-parallel serving (LLMEngine over a TP-sharded native model):
+    rank 0 runs the scheduler with two concurrent requests and broadcasts each
+    step's plan; the other ranks replay it in run_worker()"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from ipex_llm_amd.parallel.comm import init_distributed
+    init_distributed("gloo")
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.serving.engine import LLMEngine, SamplingParams
+    g = dist.group.WORLD
+    m = random_native_model(_llama_cfg(), "sym_int8", "cpu", torch.float32, seed=0, std=0.05, tp_group=g)
+    eng = LLMEngine(m, max_batch=4, max_model_len=128, block_size=64)
+    assert eng.tp_world == world and eng.is_driver == (rank == 0)
+    if rank == 0:
+        sp = SamplingParams(max_new_tokens=6)
+        rids = [eng.add_request(p, sp) for p in PROMPTS]      # two concurrent requests
+        while any(not eng.requests[r].finished for r in rids):
+            eng.step()
+        out = [eng.requests[r].generated for r in rids]
+        eng.shutdown()
+        assert out == want, (out, want)
+    else:
+        eng.run_worker()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_serving_engine_matches_single(world):
+    """vLLM --tensor-parallel-size equivalent on the serving engine: the TP
+    group's greedy tokens == the unsharded serving engine's"""
+    from ipex_llm_amd.models.builder import random_native_model
+    from ipex_llm_amd.serving.engine import LLMEngine, SamplingParams
+    single = random_native_model(_llama_cfg(), "sym_int8", "cpu", torch.float32, seed=0, std=0.05)
+    want = LLMEngine(single, max_batch=4, max_model_len=128, block_size=64).generate(
+        PROMPTS, SamplingParams(max_new_tokens=6))
+    _run(_serve_tp_worker, world, want)
+
+
+def test_tp_plan_encoding_round_trip():
+    from ipex_llm_amd.serving.engine import LLMEngine
+    pre = [([5, 6, 7, 8, 9], 2, [3, 4]), ([1, 2], 0, [7])]
+    dec = [(11, 40, [0, 1, 2]), (12, 3, [9])]
+    words = LLMEngine.encode_plan(pre, dec)
+    p2, d2 = LLMEngine.decode_plan(words)
+    assert [(t[s:], s, b) for t, s, b in p2] == [(t[s:], s, b) for t, s, b in pre]
+    assert [len(t) for t, _, _ in p2] == [5, 2]
+    assert d2 == dec and LLMEngine.decode_plan([0]) is None

@@ -161,6 +161,73 @@ def test_gemv_norm_in_deferred(cuda, name, M):
     assert _rel(d_def.sum(0), d_ref.sum(0)) < 1e-3
 
 
+@pytest.mark.parametrize("name", ["sym_int4", "nf4"])
+@pytest.mark.parametrize("M", [1, 5, 8, 16])
+@pytest.mark.parametrize("unit", [False, True])
+def test_gemv_accum_norm_then_glu_ss(cuda, name, M, unit):
+    """o_proj GEMV whose last-arriving split-K workgroups do the residual add
+    and the deferred-norm staging (gemv_accum_norm) + the gate/up GEMV that
+    applies the row scale (gemv_glu_ss) vs plain fp32 torch: residual, staged
+    input, sums of squares, the GLU output; the accumulator is left zeroed and
+    the tickets reset (second call on the same buffers agrees)."""
+    from ipex_llm_amd.models.decoder import interleave_glu_rows
+    f = get_format(name).fmt
+    torch.manual_seed(11)
+    K, H, I = 1024, 768, 256
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    wo = torch.randn(H, K, device=cuda) * 0.05
+    blob = ops.quantize(wo, f)
+    res = torch.randn(M, H, device=cuda).bfloat16()
+    wn = (torch.rand(H, device=cuda) + 0.5).bfloat16()
+    gu = ops.quantize(interleave_glu_rows(torch.randn(I, H, device=cuda) * 0.05,
+                                          torch.randn(I, H, device=cuda) * 0.05), f)
+    # fp32 references over the dequantized weights
+    wdq = R.dequantize_device_blob(blob.cpu(), f, H, K).to(cuda).float()
+    y = x.float() @ wdq.t()
+    h_ref = (y.bfloat16().float() + res.float()).bfloat16().float()
+    w_eff = wn.float() + 1.0 if unit else wn.float()
+    inv = torch.rsqrt(h_ref.pow(2).mean(-1, keepdim=True) + 1e-5)
+    xn_ref = h_ref * inv * w_eff
+    gdq = R.dequantize_device_blob(gu.cpu(), f, 2 * I, H).to(cuda).float()
+    from ipex_llm_amd.models.decoder import deinterleave_glu
+    g, u = deinterleave_glu(xn_ref @ gdq.t())
+    act_ref = torch.nn.functional.silu(g) * u
+    acc = torch.zeros(M, H, device=cuda)
+    ctr = torch.zeros(64, dtype=torch.int32, device=cuda)
+    for it in range(2):
+        res_out, xo = torch.empty_like(res), torch.empty_like(res)
+        ss = torch.zeros(M, device=cuda)
+        zero = torch.ones(64, device=cuda)
+        ops.gemv_accum_norm(x, blob, f, H, K, acc, ctr, res, res_out, wn, unit, xo, ss, zero=zero)
+        torch.cuda.synchronize()
+        assert acc.abs().max().item() == 0.0 and int(ctr.abs().max()) == 0 and zero.abs().max().item() == 0.0
+        assert _rel(res_out, h_ref) < 1e-2, (name, M, it)
+        assert _rel(xo, (w_eff * res_out.float()).bfloat16()) < 1e-2
+        assert torch.allclose(ss, res_out.float().pow(2).sum(-1), rtol=1e-4)
+        out = ops.gemv_glu_ss(xo, gu, f, 2 * I, H, 0, ss, H, 1e-5)
+        assert out.shape == (M, I)
+        assert _rel(out, act_ref) < 2e-2, (name, M, it)
+
+
+def test_decode_onorm_matches_standalone_norm(cuda, monkeypatch):
+    """batch-8 decode with the o_proj norm-out epilogue vs the standalone
+    residual-add + RMSNorm launch: greedy tokens agree (rare last-bit ties)"""
+    from transformers import LlamaConfig
+    import ipex_llm_amd.models.decoder as D
+    from ipex_llm_amd.engine.runner import Engine
+    from ipex_llm_amd.models.builder import random_native_model
+    cfg = LlamaConfig(vocab_size=512, hidden_size=512, intermediate_size=1024, num_hidden_layers=3,
+                      num_attention_heads=8, num_key_value_heads=2, max_position_embeddings=1024)
+    m = random_native_model(cfg, "sym_int4", cuda, torch.bfloat16, seed=5)
+    prompts = [list(range(1 + i, 40 + 3 * i)) for i in range(8)]
+    outs = {}
+    for flag in (False, True):
+        monkeypatch.setattr(D, "ONORM", flag)
+        outs[flag] = Engine(m).generate(prompts, max_new_tokens=8, use_graph=True)
+    a, b = sum(outs[False], []), sum(outs[True], [])
+    assert sum(x == y for x, y in zip(a, b)) >= 0.95 * len(a)
+
+
 def test_rope_kv_fused_deferred_scale(cuda):
     """rope_kv_fused with pss == rope_kv_fused over the pre-scaled accumulator"""
     torch.manual_seed(5)

@@ -417,3 +417,82 @@ def test_rotary_patch_matches_hf():
     assert _patch_rotary(holder) == 1
     c1, s1 = holder.rotary_emb(x, pos)
     assert torch.equal(c0, c1) and torch.equal(s0, s1)
+
+
+def test_rotary_patch_skips_mrope():
+    """Qwen2-VL's text rotary reports rope_type 'default' but takes 3-D M-RoPE
+    positions [3, bs, seq]: the patch leaves it alone, and a
+    patched rotary handed non-2-D positions falls back to its own forward"""
+    from transformers import Qwen2VLConfig
+    from transformers.models.qwen2_vl.modeling_qwen2_vl import Qwen2VLRotaryEmbedding
+    from ipex_llm_amd.training.lora import _patch_rotary
+    cfg = Qwen2VLConfig(hidden_size=256, num_attention_heads=4, num_key_value_heads=4,
+                        rope_scaling={"type": "mrope", "mrope_section": [8, 12, 12]})
+    tc = getattr(cfg, "text_config", cfg)
+    holder = torch.nn.Module()
+    holder.rotary_emb = Qwen2VLRotaryEmbedding(tc)
+    x = torch.randn(2, 5, 256, dtype=torch.bfloat16)
+    pos = torch.arange(5).view(1, 1, 5).expand(3, 2, 5).contiguous()
+    c0, s0 = holder.rotary_emb(x, pos)
+    _patch_rotary(holder)
+    c1, s1 = holder.rotary_emb(x, pos)
+    assert c1.shape == c0.shape and torch.equal(c0, c1) and torch.equal(s0, s1)
+
+
+def test_relora_merge_and_save_resume_reproduces_uninterrupted(tmp_path):
+    """ReLoRA merged full-weight checkpoints (reference relora.py:383-471):
+    train -> restart through merge_and_save -> train; a fresh model that
+    resumes from the save (load_weight_checkpoint) + the adapter checkpoint
+    holds exactly the uninterrupted run's low-bit base and adapters, and the
+    saved shards are the fp16 full weights + the merged deltas"""
+    from safetensors.torch import load_file
+    from ipex_llm_amd.training import (LoraConfig, get_peft_model, load_weight_checkpoint, merge_and_save,
+                                       find_lora_modules)
+    from ipex_llm_amd.training.lora import PeftModel
+    cfg = LoraConfig(r=4, lora_alpha=8, target_modules=["q_proj", "v_proj"], training_mode="relora")
+    pm = get_peft_model(_model(tmp_path), cfg)
+    _train(pm, steps=3)
+    src = str(tmp_path / "base")
+    base_sd = load_file(os.path.join(src, "model.safetensors"))
+    deltas = {n + ".weight": m.delta_weight().clone() for n, m in find_lora_modules(pm).items()}
+    dst = str(tmp_path / "ckpt-3" / "relora")
+    merge_and_save(pm, src, dst, reinit=True)
+    saved = load_file(os.path.join(dst, "model.safetensors"))
+    assert set(saved) == set(base_sd)
+    for k, d in deltas.items():
+        assert torch.equal(saved[k], (base_sd[k].float() + d).half())
+    for m in find_lora_modules(pm).values():                      # restarted adapters
+        assert torch.count_nonzero(m.lora_B.weight) == 0
+    # the checkpoint a resumed job would have: adapters right after the restart
+    pm.save_pretrained(str(tmp_path / "adapter"))
+    _train(pm, steps=2)                                           # the uninterrupted run continues
+    # resume: fresh model from the ORIGINAL checkpoint + the merged save + adapters
+    fresh = PeftModel.from_pretrained(_model(tmp_path), str(tmp_path / "adapter"), is_trainable=True)
+    assert load_weight_checkpoint(fresh, dst) == len(deltas)
+    _train(fresh, steps=2)
+    a, b = find_lora_modules(pm), find_lora_modules(fresh)
+    for n in a:
+        assert torch.equal(a[n].base_layer.weight, b[n].base_layer.weight), n
+        assert torch.allclose(a[n].lora_A.weight, b[n].lora_A.weight, atol=1e-6), n
+        assert torch.allclose(a[n].lora_B.weight, b[n].lora_B.weight, atol=1e-6), n
+
+
+def test_relora_callback_writes_and_resumes(tmp_path):
+    """the HF callback: merge_and_save into checkpoint-<step>/relora at each
+    restart, on_train_begin resumes from it"""
+    from types import SimpleNamespace
+    from ipex_llm_amd.training import LoraConfig, get_peft_model
+    from ipex_llm_amd.training.relora import ReLoRACallback, find_lora_modules
+    pm = get_peft_model(_model(tmp_path), LoraConfig(r=4, target_modules=["q_proj"], training_mode="relora"))
+    _train(pm, steps=2)
+    cb = ReLoRACallback(relora_steps=2, base_model=str(tmp_path / "base"))
+    args = SimpleNamespace(output_dir=str(tmp_path / "out"), process_index=0)
+    cb.on_step_begin(args, SimpleNamespace(global_step=2), None, model=pm, optimizer=None)
+    path = tmp_path / "out" / "checkpoint-2" / "relora" / "model.safetensors"
+    assert path.exists() and cb.restarts == 1
+    fresh = get_peft_model(_model(tmp_path), LoraConfig(r=4, target_modules=["q_proj"], training_mode="relora"))
+    ReLoRACallback(relora_steps=2, base_model=str(tmp_path / "base"),
+                   resume_from_checkpoint=str(tmp_path / "out" / "checkpoint-2")).on_train_begin(args, None, None,
+                                                                                                 model=fresh)
+    for n, m in find_lora_modules(pm).items():
+        assert torch.equal(m.base_layer.weight, find_lora_modules(fresh)[n].base_layer.weight)

@@ -12,6 +12,16 @@
 #include <algorithm>
 #include <vector>
 
+#ifdef PROBE_STAMPS
+// per-workgroup timeline of the last launch (PROBE_MODE=s): wall clock at the
+// kernel's hook points (lowbit_gemv5.cuh ILLM_GEMV5_STAMP: 0 entry, 1 x staged,
+// 2 chunks computed, 3 epilogue issued)
+__device__ unsigned long long g_stamps[65536 * 4];
+#define ILLM_GEMV5_STAMP(i)                                                                              \
+  do {                                                                                                   \
+    if (threadIdx.x == 0) g_stamps[((size_t)(blk.z * blk.gy + blk.y) * blk.gx + blk.x) * 4 + (i)] = wall_clock64(); \
+  } while (0)
+#endif
 #include "../../ipex_llm_amd/csrc/hip/lowbit_gemv5.cuh"
 
 using namespace illm;
@@ -57,6 +67,15 @@ int main(int argc, char** argv) {
     for (int M : {1, 8})
       for (int sh : {0, 1, 2, 3, 4})
         for (int ni = 0; ni < 3; ni += 2) cfgs.push_back({sh, M, ni, 0, 0, 0});
+  } else if (mode && mode[0] == 's') {
+    // timelines (PROBE_STAMPS build): production geometry, plain and deferred input
+    for (int M : {1, 8}) {
+      cfgs.push_back({0, M, 0, 0, 0, 0});
+      cfgs.push_back({0, M, 2, 0, 0, 0});
+      cfgs.push_back({1, M, 0, 0, 0, 0});
+      cfgs.push_back({2, M, 0, 0, 0, 0});
+      cfgs.push_back({3, M, 0, 0, 0, 0});
+    }
   } else if (mode && mode[0] == 'd') {
     // deferred vs full-row norm-in vs plain input, production geometry
     for (int M : {1, 2, 4, 8}) {
@@ -168,6 +187,30 @@ int main(int argc, char** argv) {
                "\"us\":%.2f,\"TBps\":%.2f}\n", ILLM_GEMV5_ABL, ILLM_GEMV5_MINW, s.name, M, normin, gx, gy, nwv, kw, us,
                wb / us / 1e6);
         fflush(stdout);
+#ifdef PROBE_STAMPS
+        {
+          const int nwg = (int)(gx * gy);
+          std::vector<unsigned long long> st4((size_t)nwg * 4);
+          CK(hipMemcpyFromSymbol(st4.data(), HIP_SYMBOL(g_stamps), st4.size() * 8, 0, hipMemcpyDeviceToHost));
+          int khz = 0;
+          CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
+          const double tick_us = 1e3 / (double)khz;
+          unsigned long long t0 = ~0ull, tend = 0;
+          for (int b = 0; b < nwg; b++) { t0 = std::min(t0, st4[b * 4]); tend = std::max(tend, st4[b * 4 + 3]); }
+          std::vector<double> d[4];
+          for (int b = 0; b < nwg; b++) {
+            d[0].push_back((st4[b * 4] - t0) * tick_us);
+            for (int j = 1; j < 4; j++) d[j].push_back(((long long)st4[b * 4 + j] - (long long)st4[b * 4 + j - 1]) * tick_us);
+          }
+          auto pct = [](std::vector<double> v, double q) { std::sort(v.begin(), v.end()); return v[(size_t)(q * (v.size() - 1))]; };
+          printf("{\"timeline\":\"%s\",\"M\":%d,\"normin\":%d,\"wgs\":%d,\"span_us\":%.2f,"
+                 "\"start_p50\":%.2f,\"start_max\":%.2f,\"stage_p50\":%.2f,\"stage_p90\":%.2f,"
+                 "\"compute_p50\":%.2f,\"compute_p90\":%.2f,\"epi_p50\":%.2f,\"epi_p90\":%.2f}\n",
+                 s.name, M, normin, nwg, (tend - t0) * tick_us, pct(d[0], 0.5), pct(d[0], 1.0), pct(d[1], 0.5),
+                 pct(d[1], 0.9), pct(d[2], 0.5), pct(d[2], 0.9), pct(d[3], 0.5), pct(d[3], 0.9));
+          fflush(stdout);
+        }
+#endif
         CK(hipGraphExecDestroy(ge));
         CK(hipGraphDestroy(g));
       }
