@@ -23,9 +23,16 @@ q2_k            block_q5_K / q6_K / q2_K), kept as is       210 / 84
 The k-quant rows are the reference's ``block_q5_K`` / ``block_q6_K`` /
 ``block_q2_K`` (``VLLM_PATCH:4928-4966``): the GGUF layouts our k-quant
 kernels read, so they pass through unchanged (merged projections are
-assembled by whole rows).  Its ``block_q4_K`` is NOT the GGUF one (16 bytes
-of 8-bit scales / mins instead of 12 packed 6-bit ones, ``VLLM_PATCH:4935``),
-and ``q5_0`` / ``q5_1`` (sym_int5 / asym_int5), ``fp6`` and ``fp6_k`` have no
+assembled by whole rows).  Its ``block_q4_K`` (148 bytes, ``VLLM_PATCH:4932-4937``)
+is NOT the GGUF one: fp16 d, fp16 dmin, then 16 bytes of 8-bit scales and mins
+instead of 12 packed 6-bit ones, then the 128 bytes of nibbles.  It is
+repacked into the GGUF block (144 bytes) our q4_k kernels read: bytes 0-7 are
+taken as the eight sub-block scales and 8-15 as the eight mins, the nibbles in
+GGUF order (the reference defines no dequantizer for this struct, so the
+order inside the 16 bytes is an assumption -- parity unpinned).  When every
+scale / min is < 64 -- what ggml's 6-bit q4_K quantizer produces -- the repack
+is exact; otherwise the block is decoded and re-quantized (lossy, warned).
+``q5_0`` / ``q5_1`` (sym_int5 / asym_int5), ``fp6`` and ``fp6_k`` have no
 element order in the reference sources: those checkpoints are refused.
 
 Nibble order inside a q4_0 block (``load_qblocks``, ``VLLM_PATCH:3944-3975``):
@@ -76,7 +83,54 @@ _KQ_PASS = (Q.Q5_K, Q.Q6_K, Q.Q2_K)
 
 
 def supported_qtypes():
-    return [Q.qtype_name(q) for q in list(_GGML) + list(_KQ_PASS)]
+    return [Q.qtype_name(q) for q in list(_GGML) + list(_KQ_PASS) + [Q.Q4_K]]
+
+
+def _q4k_ref_to_gguf(raw: torch.Tensor, n: int, k: int) -> torch.Tensor:
+    """reference 148-byte block_q4_K rows -> GGUF 144-byte blocks (see module doc)"""
+    nb = n * (k // 256)
+    blk = raw.view(nb, 148)
+    hdr, sc8, qs = blk[:, :4], blk[:, 4:20], blk[:, 20:]
+    sc, mn = sc8[:, :8].to(torch.int32), sc8[:, 8:].to(torch.int32)
+    if int(sc.max()) >= 64 or int(mn.max()) >= 64:
+        import warnings
+        warnings.warn("reference q4_K block with 8-bit scales >= 64: decoded and re-quantized (lossy)")
+        from .. import ops
+        w = q4k_ref_dequantize(raw, n, k)
+        return ops.kq_quantize(w, Q.get_format(Q.Q4_K).fmt, None).reshape(-1).view(torch.uint8)
+    q = torch.zeros(nb, 12, dtype=torch.int32)
+    q[:, 0:4] = sc[:, 0:4] | ((sc[:, 4:8] >> 4) << 6)
+    q[:, 4:8] = mn[:, 0:4] | ((mn[:, 4:8] >> 4) << 6)
+    q[:, 8:12] = (sc[:, 4:8] & 15) | ((mn[:, 4:8] & 15) << 4)
+    return torch.cat([hdr, q.to(torch.uint8), qs], 1).reshape(-1).contiguous()
+
+
+def _q4k_gguf_to_ref(raw: torch.Tensor, n: int, k: int) -> torch.Tensor:
+    """inverse of :func:`_q4k_ref_to_gguf` (export / tests)"""
+    nb = n * (k // 256)
+    blk = raw.view(nb, 144)
+    hdr, q, qs = blk[:, :4], blk[:, 4:16].to(torch.int32), blk[:, 16:]
+    sc = torch.zeros(nb, 8, dtype=torch.int32)
+    mn = torch.zeros(nb, 8, dtype=torch.int32)
+    sc[:, :4], mn[:, :4] = q[:, 0:4] & 63, q[:, 4:8] & 63
+    sc[:, 4:] = (q[:, 8:12] & 15) | ((q[:, 0:4] >> 6) << 4)
+    mn[:, 4:] = (q[:, 8:12] >> 4) | ((q[:, 4:8] >> 6) << 4)
+    return torch.cat([hdr, sc.to(torch.uint8), mn.to(torch.uint8), qs], 1).reshape(-1).contiguous()
+
+
+def q4k_ref_dequantize(raw: torch.Tensor, n: int, k: int) -> torch.Tensor:
+    """fp32 [n, k] from reference 148-byte q4_K blocks: w = d sc q - dmin mn
+    per 32-element sub-block (GGUF nibble order: byte 32 c + l holds elements
+    64 c + l (low) and 64 c + 32 + l (high))"""
+    nb = n * (k // 256)
+    blk = raw.reshape(-1).view(torch.uint8).view(nb, 148)
+    d = blk[:, 0:2].contiguous().view(torch.float16).float()          # [nb, 1]
+    dm = blk[:, 2:4].contiguous().view(torch.float16).float()
+    sc, mn = blk[:, 4:12].float(), blk[:, 12:20].float()
+    qs = blk[:, 20:].view(nb, 4, 32)
+    e = torch.stack([qs & 15, qs >> 4], 2).reshape(nb, 8, 32).float()   # [nb, sub-block, 32]
+    w = d[:, :, None] * sc[:, :, None] * e - dm[:, :, None] * mn[:, :, None]
+    return w.reshape(n, k)
 
 
 def is_reference_low_bit_dir(path: str) -> bool:
@@ -95,6 +149,12 @@ def is_reference_low_bit_dir(path: str) -> bool:
 def ggml_to_canonical(blob: torch.Tensor, qtype, n: int, k: int) -> torch.Tensor:
     """reference ggml-CPU-layout blob of W[n, k] -> our canonical planar blob"""
     qt = Q.resolve_qtype(qtype)
+    if qt == Q.Q4_K:
+        raw = blob.reshape(-1).contiguous().view(torch.uint8)
+        if k % 256 or raw.numel() != n * (k // 256) * 148:
+            raise ValueError(f"reference q4_K blob has {raw.numel()} bytes, expected {n * (k // 256) * 148} "
+                             f"([{n}, {k}], 148-byte blocks)")
+        return _q4k_ref_to_gguf(raw, n, k)
     if qt in _KQ_PASS:
         from .. import ops
         raw = blob.reshape(-1).contiguous().view(torch.uint8)
@@ -141,6 +201,8 @@ def ggml_to_canonical(blob: torch.Tensor, qtype, n: int, k: int) -> torch.Tensor
 def canonical_to_ggml(blob: torch.Tensor, qtype, n: int, k: int) -> torch.Tensor:
     """inverse of :func:`ggml_to_canonical` (tests / export to the reference layout)"""
     qt = Q.resolve_qtype(qtype)
+    if qt == Q.Q4_K:
+        return _q4k_gguf_to_ref(blob.reshape(-1).view(torch.uint8), n, k)
     if qt in _KQ_PASS:
         return blob.reshape(-1).view(torch.uint8).clone()
     bb, sk, has_min, order = _GGML[qt]
@@ -211,7 +273,7 @@ def convert_reference_state_dict(ref_sd: Dict[str, torch.Tensor], model: torch.n
             return ggml_to_canonical(t, qtype, n, k)
         raise ValueError(f"{key}: expected a low-bit uint8 blob, got {t.dtype}")
 
-    kq = Q.resolve_qtype(qtype) in _KQ_PASS
+    kq = Q.resolve_qtype(qtype) in _KQ_PASS + (Q.Q4_K,)
     for name, mod in model.named_modules():
         if not isinstance(mod, (LowBitLinear, KQuantLinear)):
             continue

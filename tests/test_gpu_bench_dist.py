@@ -50,10 +50,25 @@ def test_bench_dp_with_tp_side():
     assert tp["global_batch"] == 2
 
 
+def _run_single():
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--layers", "2",
+           "--batch", "2", "--prompt-len", "64"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return json.loads(lines[-1])
+
+
 def test_bench_tp():
+    """--tp over 2 ranks: the sharded model's next tokens equal the world-1
+    run's (same weight seed and prompts; bench.py keeps both identical)"""
     out = _run(["--tp", "--no-tp-side"])
     assert out["config"]["parallelism"] == "tp2" and out["scaling"] == "strong" and out["value"] > 0
     assert "tp_side" not in out
+    one = _run_single()
+    assert one["n_gpus"] == 1 and one["config"]["parallelism"] == "dp1"
+    assert out["sample_next_ids"] == one["sample_next_ids"], (out["sample_next_ids"], one["sample_next_ids"])
 
 
 def test_bench_ep_mixtral():

@@ -50,6 +50,34 @@ def test_q4_0_block_bytes_documented_layout():
     assert torch.equal(cw, codes)
 
 
+def test_reference_q4k_layout_round_trip():
+    """the reference's 148-byte block_q4_K (fp16 d, fp16 dmin, 8-bit scales
+    then mins, GGUF nibble order; VLLM_PATCH:4932-4937) <-> our GGUF 144-byte
+    block: exact both ways while the scales fit 6 bits, and its decode formula
+    equals our q4_k dequantization"""
+    from ipex_llm_amd import ops
+    fmt = Q.get_format("q4_k").fmt
+    n, k = 6, 512
+    w = torch.randn(n, k)
+    ours = ops.kq_quantize(w, fmt).reshape(-1).view(torch.uint8)
+    ref = RC.canonical_to_ggml(ours, "q4_k", n, k)
+    assert ref.numel() == n * (k // 256) * 148
+    blk = ref.view(-1, 148)
+    assert int(blk[:, 4:20].max()) < 64                     # 6-bit values carried in bytes
+    assert torch.equal(RC.ggml_to_canonical(ref, "q4_k", n, k), ours)
+    want = ops.kq_dequantize(ours, fmt, n, k).float()
+    torch.testing.assert_close(RC.q4k_ref_dequantize(ref, n, k), want, rtol=1e-5, atol=1e-6)
+    # an 8-bit scale past 6 bits: decoded and re-quantized (close, not exact)
+    big = blk.clone()
+    big[:, 4:12] = (big[:, 4:12].to(torch.int32) * 2).clamp(max=255).to(torch.uint8)
+    big[:, 0:2] = (big[:, 0:2].contiguous().view(torch.float16) / 2).view(torch.uint8)
+    with pytest.warns(UserWarning):
+        conv = RC.ggml_to_canonical(big.reshape(-1), "q4_k", n, k)
+    dq = ops.kq_dequantize(conv, fmt, n, k).float()
+    exact = RC.q4k_ref_dequantize(big.reshape(-1), n, k)
+    assert ((dq - exact).norm() / exact.norm()).item() < 0.08
+
+
 def test_wrong_size_refused():
     with pytest.raises(ValueError):
         RC.ggml_to_canonical(torch.zeros(100, dtype=torch.uint8), "sym_int4", 2, 64)
@@ -96,7 +124,7 @@ def _kq_split_gate_up(blob, n2):
     return t[:, 0].reshape(-1).clone(), t[:, 1].reshape(-1).clone()
 
 
-@pytest.mark.parametrize("qt", ["sym_int4", "asym_int4", "q6_k", "q5_k", "q2_k"])
+@pytest.mark.parametrize("qt", ["sym_int4", "asym_int4", "q6_k", "q5_k", "q2_k", "q4_k"])
 def test_load_reference_checkpoint_logits(tmp_path, qt):
     from transformers import LlamaConfig, LlamaForCausalLM
     from ipex_llm_amd.transformers import AutoModelForCausalLM
