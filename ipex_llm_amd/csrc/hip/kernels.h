@@ -21,7 +21,7 @@ void launch_gemv_dk(bool bf16, int mt, int epi, dim3 grid, const GemvArgs& a, hi
 // shmem = gemv5_shmem(rows, chunks per split) <= 159 KiB
 template <int DK>
 void launch_gemv5_dk(bool bf16, int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
-constexpr int gemv5_x_ld_h(int kw) { return kw + 8; }
+constexpr int gemv5_x_ld_h(int kw) { return (kw + 511) / 512 * 512 + 8; }   // == gemv5_x_ld
 constexpr size_t gemv5_attn_shmem_h(int rows, int cpk, int D, int ns) {
   return (size_t)rows * ((cpk * 128 + D - 1) / D + 1) * (ns + 1) * 4;
 }

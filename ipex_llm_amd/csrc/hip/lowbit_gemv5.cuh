@@ -26,7 +26,10 @@
 //   * scales are stored chunk-major (formats.h): one 16-B load gives the 4
 //     C-fragment rows' (blk0, blk1) scales of a chunk.
 #pragma once
+#include <cstdio>
+#include <mutex>
 #include <type_traits>
+#include <unordered_map>
 
 #include "../common/quant_block.h"
 #include "gemv_args.h"
@@ -126,7 +129,11 @@ __device__ __forceinline__ uint4 raw_a8(uint32_t lo, uint32_t hi) {
 // (row, chunk) float4 {-OFF*sx0, -OFF*sx1, sx0, sx1}, then the KW reduction
 // area [<= 8 waves][2 tiles][64] float4, then (attention-combine prologue only)
 // the split weights [rows][heads of the slice][ans + 1] f32.
-__host__ __device__ constexpr int gemv5_x_ld(int kw) { return kw + 8; }
+// x rows are padded to whole 1-KB LDS-DMA pieces (512 16-bit elements): a
+// row's last piece is issued with every lane active (no exec-masked LDS-DMA)
+// and its tail lands in the row's own padding; + 8 elements keep the 16 rows
+// of a fragment read on distinct banks
+__host__ __device__ constexpr int gemv5_x_ld(int kw) { return (kw + 511) / 512 * 512 + 8; }
 __host__ __device__ constexpr size_t gemv5_shmem(int rows, int cpk) {
   return ((size_t)rows * gemv5_x_ld(cpk * 128) * 2 + 15) / 16 * 16 + (size_t)rows * cpk * 16 + 8 * 2 * 64 * 16;
 }
@@ -261,7 +268,13 @@ __device__ __forceinline__ void gemv5_norm_out(const GemvArgs& a, const G5Blk& b
     if ((v & (C4 - 1)) == 0) __hip_atomic_fetch_add(a.lss + m, ss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF, bool SCL>
+// XM (x mode): 0 = every input form, chosen at run time; 1 = plain 16-bit x
+// staged by LDS-DMA only (the launcher checks the arguments).  A separate
+// instantiation because hipcc's wait insertion is path-insensitive: the
+// loads of the other staging forms, merged at the join, made it drain
+// vmcnt(0) right behind the DMA staging's counted wait, i.e. wait for every
+// weight chunk in flight before the first MFMA (seen in the .s).
+template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF, bool SCL, int XM = 0, int XS = 1>
 __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) {
   // PF: chunks in flight per wave (4; 8 = every chunk of a decode split-K
   // slice of <= 8 chunks requested before the prologue)
@@ -369,51 +382,77 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
       ((float4*)a.nzero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
-  // ---- x staged by LDS-DMA BEFORE the weight ring.  Vector-memory loads
-  // retire in issue order, so x loads issued behind the ring (as before round
-  // 6) could be staged only once every weight chunk had arrived: the LDS
-  // staging, the block sums and the barrier sat behind the HBM round trip
-  // (per-workgroup stamps, profiles/gemv5_stamps_r6.jsonl).  Requested first,
-  // by LDS-DMA (no VGPRs: a register-staged early copy raised the kernel from
-  // 111 to 169 VGPRs and halved the resident workgroups), the staging waits
-  // only for its own pieces (counted vmcnt below).
-  const int xvpr = kw / 8;
-  const bool defer = a.nacc != nullptr && a.ndefer != 0;
-  const bool plain_x = !a.apo && !a.xpart && !defer && !a.nacc;
-  // 16-bit x that needs no conversion, whole K chunks inside K; each row in
-  // 1-KB pieces (64 lanes x 16 B), the last piece lane-masked
-  const bool dma_x = ILLM_GEMV5_XDMA && !(ILLM_GEMV5_ABL & 2) && plain_x && !MOE && std::is_same<C, T>::value &&
-                     kbase + kw <= a.K && (ILLM_GEMV5_EARLYX || Mloc * xvpr > 4 * NW * 64);
+  // ---- x-side loads BEFORE the weight ring.  Vector-memory loads retire in
+  // issue order, so x loads issued behind the ring (as before round 6) could
+  // be staged only once every weight chunk had arrived: the LDS staging, the
+  // block sums and the barrier sat behind the HBM round trip (per-workgroup
+  // stamps, profiles/gemv5_stamps_r6.jsonl).
+  //   XM 1 / 2 (the decode forms, their own instantiations): the thread's XS
+  //   16-B slots of x (XM 1) or of the deferred-norm inputs -- accumulator,
+  //   residual, norm weight (XM 2) -- go to registers first, clamped and
+  //   unconditional; hipcc then waits for exactly these (counted vmcnt).  An
+  //   LDS-DMA form with a hand-counted wait produced NaN once the ring was
+  //   refilled (K >= 2048): LDS-DMA and register loads are not retired in one
+  //   order, so the count cannot isolate the DMA pieces.
+  //   XM 0: x requested first by LDS-DMA, waited for with vmcnt(0).
+  const int xvpr = kw / 8, xtotal = Mloc * xvpr;
+  const bool defer = XM == 2 || (XM == 0 && a.nacc != nullptr && a.ndefer != 0);
+  const bool plain_x = XM == 1 || (XM == 0 && !a.apo && !a.xpart && !defer && !a.nacc);
+  // XM 0 LDS-DMA: 16-bit x that needs no conversion, whole K chunks inside K;
+  // each row in whole 1-KB pieces (64 lanes x 16 B) into its padded LDS row
+  const bool dma_x = XM == 0 && ILLM_GEMV5_XDMA && !(ILLM_GEMV5_ABL & 2) && plain_x && !MOE &&
+                     std::is_same<C, T>::value && kbase + kw <= a.K &&
+                     (ILLM_GEMV5_EARLYX || Mloc * xvpr > 4 * NW * 64);
+  constexpr int XR = XM == 0 ? 1 : XS;
+  uint4 xr[XR], er[XR], ew[XR];
+  float4 ea0[XR], ea1[XR];
+  if constexpr (XM == 1) {
+#pragma unroll
+    for (int u = 0; u < XS; u++) {
+      const int vv = min((int)threadIdx.x + u * NW * 64, xtotal - 1);
+      const int m = vv / xvpr, kk = (vv % xvpr) * 8;
+      xr[u] = *(const uint4*)(a.x + (size_t)m * a.ldx + kbase + kk);
+    }
+  } else if constexpr (XM == 2) {
+#pragma unroll
+    for (int u = 0; u < XS; u++) {
+      const int vv = min((int)threadIdx.x + u * NW * 64, xtotal - 1);
+      const int m = vv / xvpr, k = kbase + (vv % xvpr) * 8;
+      const float4* pa = (const float4*)(a.nacc + (size_t)m * a.K + k);
+      ea0[u] = pa[0];
+      ea1[u] = pa[1];
+      er[u] = *(const uint4*)(a.nres + (size_t)m * a.K + k);
+      ew[u] = *(const uint4*)(a.nweight + k);
+    }
+  }
   if (dma_x) {
     const int per_row = (xvpr + 63) >> 6, nins = Mloc * per_row;
     const gv5_rsrc rx = gv5_make_rsrc(a.x, (uint32_t)((size_t)a.M * a.ldx * 2));
-    for (int i = wave; i < nins; i += NW) {      // wave-uniform: one row piece per instruction
+    for (int i = wave; i < nins; i += NW) {      // wave-uniform: one whole row piece per instruction
       const int m = i / per_row, j = i - m * per_row;
-      if (j * 64 + lane < xvpr)
-        gv5_dma16(rx, xs + m * ldx + j * 512, (uint32_t)(((size_t)m * a.ldx + kbase + j * 512 + lane * 8) * 2));
+      gv5_dma16(rx, xs + m * ldx + j * 512, (uint32_t)(((size_t)m * a.ldx + kbase + j * 512 + lane * 8) * 2));
     }
   }
   asm volatile("" ::: "memory");             // the ring loads stay behind these
 
   Chunk ring[PF];
-  if (wave_on) {
+  // XM 1 / 2: issued unconditionally (clamped, valid addresses) -- behind a
+  // wave_on branch hipcc counted the no-ring path at the join and drained the
+  // ring before staging x
+  if (XM != 0 || wave_on) {
     if constexpr (SCL) load_scl(wc0);
 #pragma unroll
-    for (int u = 0; u < PF; u++) load_chunk(ring[u], wc0 + u);
+    for (int u = 0; u < PF; u++) load_chunk(ring[u], max(wc0, 0) + u);
   }
-  // ring load instructions per thread (the counted wait of the DMA staging)
-  constexpr int RING_LOADS = (SCL ? TPW * (1 + (HASMIN ? 1 : 0)) : 0) +
-                             PF * TPW * (BITS / 4 + (SCL ? 0 : 1 + (HASMIN ? 1 : 0)));
-  static_assert(RING_LOADS < 64, "vmcnt is 6 bits");
   if constexpr (DK == DK_LUT4) {
     if (threadIdx.x < 256)
       lut2[threadIdx.x] = pack2<F16>(hd_lut4(a.lut_fmt, threadIdx.x & 15), hd_lut4(a.lut_fmt, threadIdx.x >> 4));
   }
 
   // ---- attention-combine prologue: per (row, head) split weights exp(m_s - M) / L
-  const int a_h0 = a.apo ? kbase / a.aD : 0;
-  const int a_nh = a.apo ? (kbase + kw - 1) / a.aD - a_h0 + 1 : 0;
-  if (a.apo) {
+  const int a_h0 = XM == 0 && a.apo ? kbase / a.aD : 0;
+  const int a_nh = XM == 0 && a.apo ? (kbase + kw - 1) / a.aD - a_h0 + 1 : 0;
+  if (XM == 0 && a.apo) {
     // 16 lanes per (row, head) pair, one split per lane (all (m, l) loads in
     // flight at once; a serial per-thread loop was latency-bound)
     const int sub = threadIdx.x & 15;
@@ -466,7 +505,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
     if (threadIdx.x < 16) ninv[threadIdx.x] = 0.f;
     __syncthreads();
   }
-  if (a.nacc && !defer && !(ILLM_GEMV5_ABL & 2)) {
+  if (XM == 0 && a.nacc && !defer && !(ILLM_GEMV5_ABL & 2)) {
     if (threadIdx.x < 16) ninv[threadIdx.x] = 0.f;
     __syncthreads();
     const bool wres = a.nres_out != nullptr && blk.x == 0 && blk.y == 0;
@@ -564,11 +603,52 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
     }
     return val;
   };
-  if (dma_x) {
+  if constexpr (XM == 2) {
+    // deferred RMSNorm from the early registers (the generic branch below does
+    // the same from global memory): h = rnd(rnd(acc) + res), x' = rnd(w * h),
+    // the rows' sums of squares into ninv, grid column 0 writes the residual out
+#pragma unroll
+    for (int u = 0; u < XS; u++) {
+      const int v = (int)threadIdx.x + u * NW * 64;
+      if (v >= xtotal) break;                   // whole 8-lane groups (xvpr % 16 == 0)
+      const int m = v / vpr, kk = (v % vpr) * 8;
+      const float av[8] = {ea0[u].x, ea0[u].y, ea0[u].z, ea0[u].w, ea1[u].x, ea1[u].y, ea1[u].z, ea1[u].w};
+      const uint32_t rw[4] = {er[u].x, er[u].y, er[u].z, er[u].w}, wv[4] = {ew[u].x, ew[u].y, ew[u].z, ew[u].w};
+      float h[8], ssq = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        h[2 * i] = rnd(rnd(av[2 * i]) + to_f32<T>((uint16_t)(rw[i] & 0xffff)));
+        h[2 * i + 1] = rnd(rnd(av[2 * i + 1]) + to_f32<T>((uint16_t)(rw[i] >> 16)));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++) ssq += h[i] * h[i];
+      ssq += __shfl_xor(ssq, 1, 8);
+      ssq += __shfl_xor(ssq, 2, 8);
+      ssq += __shfl_xor(ssq, 4, 8);
+      if ((v & 7) == 0) atomicAdd(&ninv[m], ssq);
+      if (a.nres_out && blk.x == 0)
+        *(uint4*)(a.nres_out + (size_t)m * a.K + kbase + kk) =
+            make_uint4(pack2<T>(h[0], h[1]), pack2<T>(h[2], h[3]), pack2<T>(h[4], h[5]), pack2<T>(h[6], h[7]));
+      uint32_t o4[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        float w0 = to_f32<T>((uint16_t)(wv[i] & 0xffff)), w1 = to_f32<T>((uint16_t)(wv[i] >> 16));
+        if (a.nunit) { w0 = rnd(1.f + w0); w1 = rnd(1.f + w1); }
+        o4[i] = pack2<C>(rnd(w0 * h[2 * i]), rnd(w1 * h[2 * i + 1]));
+      }
+      commit_x(v, make_uint4(o4[0], o4[1], o4[2], o4[3]));
+    }
+  } else if constexpr (XM == 1) {
+#pragma unroll
+    for (int u = 0; u < XS; u++) {
+      const int v = (int)threadIdx.x + u * NW * 64;
+      if (v >= xtotal) break;
+      commit_x(v, xr[u]);
+    }
+  } else if (dma_x) {
     // the row pieces were requested before the weight ring (top): wait for
     // them only -- every load issued later is one of this thread's ring loads
-    if (ILLM_GEMV5_EARLYX && wave_on) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(RING_LOADS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // the per-(row, 64-block) sums from the staged rows (8 lanes per block)
     const int nthr = NW * 64, total = Mloc * vpr;
@@ -589,7 +669,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
         rec[2 + (blk & 1)] = bsum;
       }
     }
-  } else if (!(ILLM_GEMV5_ABL & 2) && plain_x) {
+  } else if (XM == 0 && !(ILLM_GEMV5_ABL & 2) && plain_x) {
     // plain activations: every load of a thread's (up to XPF) staging slots is
     // requested before the first LDS store / shuffle reduction -- one L2 round
     // trip instead of one per slot (the loop form below serialised them:
@@ -612,7 +692,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
           if (v0 + u * nthr < total) commit_x(v0 + u * nthr, to_c(xv[u]));
       }
     }
-  } else if (!(ILLM_GEMV5_ABL & 2) && a.nacc && !defer && !a.apo && !a.xpart) {
+  } else if (XM == 0 && !(ILLM_GEMV5_ABL & 2) && a.nacc && !defer && !a.apo && !a.xpart) {
     // norm-in: h (exact in T) is already in LDS from the prologue; x = w * rnd(h * inv).
     // The norm weight loads of a thread's XPF slots are requested together (the
     // generic loop below made each slot's weight load a round trip of its own:
@@ -656,7 +736,7 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
         commit_x(v, val);
       }
     }
-  } else if (!(ILLM_GEMV5_ABL & 2)) {
+  } else if (XM == 0 && !(ILLM_GEMV5_ABL & 2)) {
     for (int v = threadIdx.x; v < Mloc * vpr; v += NW * 64) {
       const int m = v / vpr, kk = (v % vpr) * 8;
       uint4 val = make_uint4(0, 0, 0, 0);
@@ -792,6 +872,9 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
   }
   __syncthreads();
   ILLM_GEMV5_STAMP(1);
+#ifdef ILLM_GEMV5_DUMP
+  ILLM_GEMV5_DUMP();   // debug hook (tools/probe/xm_check.hip: the staged x of workgroup 0)
+#endif
   if (defer) {
     if constexpr (EPI == EPI_GLU) {
       // full K staged here: the row scale is known locally (applied before the activation)
@@ -1048,20 +1131,36 @@ __device__ __forceinline__ void gemv5_body(const GemvArgs& a, const G5Blk& blk) 
   }
 }
 
-template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4, bool SCL = ILLM_GEMV5_SCL != 0>
+template <int DK, typename T, int EPI, int TPW, int KW, bool MOE, int NW, int PF = 4, bool SCL = ILLM_GEMV5_SCL != 0,
+          int XM = 0, int XS = 1>
 __global__ void __launch_bounds__(NW * 64, ILLM_GEMV5_MINW) lowbit_gemv5_kernel(const GemvArgs a) {
-  gemv5_body<DK, T, EPI, TPW, KW, MOE, NW, PF, SCL>(
+  gemv5_body<DK, T, EPI, TPW, KW, MOE, NW, PF, SCL, XM, XS>(
       a, G5Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y, (int)gridDim.z});
 }
 
-// launch helper: up to 159 KiB of dynamic LDS, attribute set once per instantiation
+// launch helper.  A launch over 64 KiB of dynamic LDS first raises the
+// kernel's limit to what it asks for (per kernel: every instantiation has one
+// function type, so a static flag in this template would cover only the first
+// kernel launched); a refused request is cleared so that it does not surface
+// as a later op's error.  ILLM_GEMV5_TRACE=1 prints each launch.
 template <typename K>
 inline void launch5(K kern, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-    attr = true;
+  if (shmem > 64 * 1024) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, size_t> lim;
+    std::lock_guard<std::mutex> g(mu);
+    size_t& l = lim[(const void*)kern];
+    if (l < shmem) {
+      if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem) == hipSuccess)
+        l = shmem;
+      else
+        (void)hipGetLastError();
+    }
   }
+  static const bool trace = getenv("ILLM_GEMV5_TRACE") != nullptr;
+  if (trace)
+    fprintf(stderr, "[gemv5] kern=%p M=%d N=%d K=%d grid=%u,%u,%u nw=%d lds=%zu\n", (const void*)kern, a.M, a.N, a.K,
+            grid.x, grid.y, grid.z, a.nw, shmem);
   hipLaunchKernelGGL(kern, grid, dim3(64 * (a.nw == 8 ? 8 : 4)), shmem, st, a);
 }
 
@@ -1098,12 +1197,69 @@ inline void launch5_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hip
   return launch5_epi_s<DK, T, KW, MOE, NW, false>(epi, grid, shmem, a, st);
 }
 
+// the XM 1 / 2 instantiations (x or the deferred-norm inputs in registers
+// ahead of the weight ring): the decode hot path -- sym_int4, bf16, whole K
+// chunks -- for the geometries plan5 picks there.  Per launch at Llama-3-8B
+// decode shapes (tools/probe/gemv5_probe.hip, profiles/gemv5_xm_forms_r6.txt):
+// o 5.3 -> 4.4 us, qkv 6.0 -> 5.4, down 8.8 -> 8.2, gate/up B=8 18.6 -> 16.2.
+// Not enabled by default (ILLM_GEMV5_XM_RT below): some forms compute wrong
+// outputs, with and without -amdgpu-mfma-vgpr-form.
+#ifndef ILLM_GEMV5_XM
+#define ILLM_GEMV5_XM ILLM_GEMV5_EARLYX
+#endif
+template <int DK, typename T, bool MOE>
+inline bool launch5_xm(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  if constexpr (DK != DK_INT4S || !std::is_same<T, BF16>::value || MOE || !ILLM_GEMV5_XM) {
+    return false;
+  } else {
+    // ILLM_GEMV5_XM_RT (run time): 0 (default) = generic kernels only, 1 = XM 1 only, 2 = XM 1 and 2.
+    // Off by default: tools/probe/xm_check.hip (random inputs, each XM form vs the generic
+    // kernel) finds wrong outputs -- ATOMIC forms at 8 waves and once the ring is refilled
+    // (run-to-run different, gone with -amdgpu-waitcnt-forcezero: a load consumed before it
+    // landed), the XS 2 GLU form at 4 waves (deterministic, also with forcezero, although
+    // its staged x is right).  profiles/gemv5_xm_forms_r6.txt
+    static const int rt = getenv("ILLM_GEMV5_XM_RT") ? atoi(getenv("ILLM_GEMV5_XM_RT")) : 0;
+    if (rt <= 0 || a.apo != nullptr || a.xpart != nullptr || a.K % 128 != 0 || a.pf8 || kw > 2) return false;
+    const int cpk = a.cpk > 0 ? a.cpk : (a.KC + (int)grid.y - 1) / (int)grid.y;
+    const int nthr = a.nw == 8 ? 512 : 256;
+    const int slots = (a.M * cpk * 16 + nthr - 1) / nthr;     // 16-B x vectors per thread
+    const bool w8 = a.nw == 8;
+    static const bool trace = getenv("ILLM_GEMV5_TRACE") != nullptr;
+#define ILLM_XM_LAUNCH(EPI_, TPW_, KW_, PF_, SCL_, XM_, XS_)                                                  \
+    do {                                                                                                      \
+      if (trace) fprintf(stderr, "[gemv5] XM %d XS %d epi %d slots %d cpk %d\n", XM_, XS_, EPI_, slots, cpk); \
+      if (w8) launch5(lowbit_gemv5_kernel<DK, T, EPI_, TPW_, KW_, false, 8, PF_, SCL_, XM_, XS_>, grid, shmem, a, st); \
+      else launch5(lowbit_gemv5_kernel<DK, T, EPI_, TPW_, KW_, false, 4, PF_, SCL_, XM_, XS_>, grid, shmem, a, st);    \
+      return true;                                                                                            \
+    } while (0)
+    const bool glu_ok = kw == 2 && ILLM_GEMV5_SCL && (cpk + 1) / 2 <= 16;
+    if (a.x == nullptr && a.nacc != nullptr && a.ndefer != 0) {
+      // XM 2: deferred-norm input (decode qkv; batch-1 / -2 gate-up)
+      if (rt < 2) return false;
+      if (epi == EPI_ATOMIC && kw == 1 && slots <= 1) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 1);
+      if (epi == EPI_ATOMIC && kw == 1 && slots <= 2) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 2);
+      if (epi == EPI_GLU && glu_ok && slots <= 2) ILLM_XM_LAUNCH(EPI_GLU, 2, 2, ILLM_GEMV5_PFD, true, 2, 2);
+      return false;
+    }
+    if (a.x == nullptr || a.nacc != nullptr) return false;
+    if (epi == EPI_ATOMIC && kw == 1 && slots <= 1) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 1, 1);
+    if (epi == EPI_ATOMIC && kw == 1 && slots <= 2) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 1, 2);
+    if (epi == EPI_STORE && kw == 1 && slots <= 2) ILLM_XM_LAUNCH(EPI_STORE, 1, 1, 4, false, 1, 2);
+    if (epi == EPI_STORE && kw == 1 && slots <= 8) ILLM_XM_LAUNCH(EPI_STORE, 1, 1, 4, false, 1, 8);
+    if (epi == EPI_GLU && glu_ok && slots <= 2) ILLM_XM_LAUNCH(EPI_GLU, 2, 2, ILLM_GEMV5_PFD, true, 1, 2);
+    if (epi == EPI_GLU && glu_ok && slots <= 8) ILLM_XM_LAUNCH(EPI_GLU, 2, 2, ILLM_GEMV5_PFD, true, 1, 8);
+#undef ILLM_XM_LAUNCH
+    return false;
+  }
+}
+
 template <int DK, typename T, bool MOE>
 inline void launch5_kw(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a0, hipStream_t st) {
   using C = typename std::conditional<DK == DK_LUT4, F16, T>::type;
   GemvArgs a = a0;
   a.nib_mask = 0x000F000Fu;
   a.nib_magic = Raw<C>::k4;
+  if (launch5_xm<DK, T, MOE>(kw, epi, grid, shmem, a, st)) return;
   // workgroup size: 4 or 8 waves (a.nw); 8 shares one LDS copy of x among
   // twice the tiles (the x-staging cost of kw > 1 at larger M)
   if (a.nw == 8) {

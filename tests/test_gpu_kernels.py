@@ -901,3 +901,49 @@ def test_embed_rms_norm_matches_gather_then_norm(cuda):
     torch.ops.ipex_llm_amd.embed_rms_norm(torch.tensor([V + 5], device=cuda), table, w, 1e-5, False, None)
     with pytest.raises(RuntimeError):
         ops.check_kernel_errors(cuda)
+
+
+@pytest.mark.parametrize("M", [1, 2, 5, 8])
+def test_decode_gemv_forms_at_llama3_8b_shapes(cuda, M):
+    """the decode GEMV instantiations (generic / XM 1 plain x / XM 2 deferred
+    norm, chosen by shape) at the real Llama-3-8B projection shapes, where
+    the weight ring is refilled (K >= 2048): gate/up GLU, down (K = 14336),
+    qkv norm-in deferred, lm_head-style store -- vs fp32 torch"""
+    from ipex_llm_amd.models.decoder import interleave_glu_rows, deinterleave_glu
+    f = get_format("sym_int4").fmt
+    torch.manual_seed(12)
+    H, I = 4096, 14336
+    deq = lambda b, n, k: R.dequantize_device_blob(b.cpu(), f, n, k).to(cuda).float()   # noqa: E731
+    x = torch.randn(M, H, device=cuda).bfloat16()
+    gu = ops.quantize(interleave_glu_rows(torch.randn(I, H, device=cuda) * 0.02,
+                                          torch.randn(I, H, device=cuda) * 0.02), f)
+    g, u = deinterleave_glu(x.float() @ deq(gu, 2 * I, H).t())
+    y = ops.gemv_glu(x, gu, f, 2 * I, H, 0)
+    assert _rel(y, torch.nn.functional.silu(g) * u) < 1e-2
+    ssx = torch.rand(M, device=cuda) * H + 1.0                 # gemv_glu_ss: the o_proj norm-out consumer
+    inv = torch.rsqrt(ssx / H + 1e-5)[:, None]
+    ys = ops.gemv_glu_ss(x, gu, f, 2 * I, H, 0, ssx, H, 1e-5)
+    assert _rel(ys, torch.nn.functional.silu(g * inv) * (u * inv)) < 1e-2
+    a = torch.randn(M, I, device=cuda).bfloat16()
+    dn = ops.quantize(torch.randn(H, I, device=cuda) * 0.02, f)
+    acc = torch.zeros(M, H, device=cuda)
+    ops.gemv_accum(a, dn, f, H, I, acc)
+    assert _rel(acc, a.float() @ deq(dn, H, I).t()) < 5e-3
+    lm = ops.quantize(torch.randn(8192, H, device=cuda) * 0.02, f)
+    assert _rel(ops.lowbit_matmul(x, lm, f, 8192, H), x.float() @ deq(lm, 8192, H).t()) < 1e-2
+    # qkv over the deferred norm of (residual + accumulator)
+    qkv = ops.quantize(torch.randn(6144, H, device=cuda) * 0.02, f)
+    acc_in = torch.randn(M, H, device=cuda)
+    res = torch.randn(M, H, device=cuda).bfloat16()
+    wn = (torch.rand(H, device=cuda) + 0.5).bfloat16()
+    out, res_out, ss = torch.zeros(M, 6144, device=cuda), torch.empty_like(res), torch.zeros(M, device=cuda)
+    ops.gemv_norm_in(acc_in, res, res_out, wn, 1e-5, False, qkv, f, 6144, H, False, acc_out=out, ss=ss)
+    h = (acc_in.bfloat16().float() + res.float()).bfloat16().float()
+    assert torch.equal(res_out.float(), h)
+    xn = h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + 1e-5) * wn.float()
+    assert _rel(out * torch.rsqrt(ss / H + 1e-5)[:, None], xn @ deq(qkv, 6144, H).t()) < 1e-2
+    if M <= 2:   # the batch-1 / -2 gate/up over the deferred norm (norm-in GLU)
+        y2 = ops.gemv_norm_in(acc_in, res, torch.empty_like(res), wn, 1e-5, False, gu, f, 2 * I, H, True, 0,
+                              ss=torch.zeros(M, device=cuda))
+        g2, u2 = deinterleave_glu(xn @ deq(gu, 2 * I, H).t())
+        assert _rel(y2, torch.nn.functional.silu(g2) * u2) < 1.5e-2

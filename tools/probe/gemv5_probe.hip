@@ -187,6 +187,16 @@ int main(int argc, char** argv) {
                "\"us\":%.2f,\"TBps\":%.2f}\n", ILLM_GEMV5_ABL, ILLM_GEMV5_MINW, s.name, M, normin, gx, gy, nwv, kw, us,
                wb / us / 1e6);
         fflush(stdout);
+        if (s.glu) {
+          // uniform inputs (every weight byte 0x5a, every x 0x3c3c): every
+          // output element must be the same finite value
+          std::vector<uint16_t> yh((size_t)M * (s.N / 2));
+          CK(hipMemcpy(yh.data(), yout, yh.size() * 2, hipMemcpyDeviceToHost));
+          size_t bad = 0;
+          for (size_t i = 0; i < yh.size(); i++) bad += yh[i] != yh[0] || (yh[i] & 0x7f80) == 0x7f80;
+          printf("{\"check\":\"%s\",\"M\":%d,\"first\":\"0x%04x\",\"mismatch\":%zu,\"of\":%zu}\n", s.name, M, yh[0],
+                 bad, yh.size());
+        }
 #ifdef PROBE_STAMPS
         {
           const int nwg = (int)(gx * gy);
