@@ -18,6 +18,7 @@ from __future__ import annotations
 import contextlib
 import os
 import weakref
+from typing import Dict
 
 import torch
 import torch.nn.functional as F
@@ -291,6 +292,47 @@ def use_g8d(x, M: int, n: int, k: int, glu: bool = False) -> bool:
             and hasattr(torch.ops.ipex_llm_amd, "gemm_bf16"))
 
 
+# ---- measured dispatch: dense 8-phase kernel vs the library GEMM -----------
+# Over the same transient bf16 weight, the 8-phase kernel reaches 0.8-0.9x
+# hipBLASLt at M = 8192 and 0.5-0.8x at M = 1024 (profiles/g8d_slab_splitk_sweep_r5.jsonl);
+# end to end the library path took the Llama-3-8B first token from 98.9 to 90.3 ms
+# at B = 8 x 1024 and 19.8 to 18.5 ms at B = 1 (profiles/prefill_lib_ab_r6.jsonl).
+# Each (M, N, K, GLU) shape times both once, outside graph capture (the engine's
+# eager warm-up precedes every prefill capture), and keeps the faster; a shape first
+# seen under capture takes the 8-phase kernel.  ILLM_GEMM_AUTOTUNE=0: always 8-phase.
+_AUTOTUNE = os.environ.get("ILLM_GEMM_AUTOTUNE", "1") == "1"
+_CHOICE: Dict[tuple, str] = {}
+
+
+def _time_ms(fn, reps: int = 3) -> float:
+    fn()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(reps):
+        fn()
+    t1.record()
+    t1.synchronize()
+    return t0.elapsed_time(t1) / reps
+
+
+def _pick(key: tuple, g8d_fn, lib_fn) -> str:
+    c = _CHOICE.get(key)
+    if c is None:
+        if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
+            return "g8d"
+        tg, tl = _time_ms(g8d_fn), _time_ms(lib_fn)
+        c = _CHOICE[key] = "g8d" if tg <= tl else "lib"
+        if os.environ.get("ILLM_GEMM_AUTOTUNE_LOG"):
+            print(f"[gemm] M={key[0]} N={key[1]} K={key[2]} glu={key[3]}: 8-phase {tg * 1e3:.1f} us, "
+                  f"library {tl * 1e3:.1f} us -> {c}", flush=True)
+    return c
+
+
+def gemm_choices() -> Dict[tuple, str]:
+    """the measured per-shape choices so far: (M, N, K, glu, act) -> 'g8d' | 'lib'"""
+    return dict(_CHOICE)
+
+
 def lowbit_gemm(x, blob, fmt, n, k, bias=None):
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
@@ -298,6 +340,8 @@ def lowbit_gemm(x, blob, fmt, n, k, bias=None):
         return ops.gemm8p_lowbit(x, blob, fmt, n, k, bias)
     if use_g8d(x, M, n, k) and (bias is None or bias.dtype == torch.bfloat16):
         w = _dense_weight(blob, fmt, n, k, x.dtype)
+        if _pick((M, n, k, False, 0), lambda: ops.gemm_bf16(x, w, bias), lambda: F.linear(x, w, bias)) == "lib":
+            return F.linear(x, w, bias)
         return ops.gemm_bf16(x, w, bias)
     if use_engine(M, n, k) and x.dtype in (torch.bfloat16, torch.float16):
         return ops.mfgemm(x, blob, fmt, n, k, bias)
@@ -317,6 +361,12 @@ def lowbit_gemm_glu(x, blob, fmt, n, k, act: int = 0):
         return ops.gemm8p_lowbit(x, blob, fmt, n, k, None, False, True, act)
     if use_g8d(x, M, n, k, glu=True) and act in (0, 1):
         w = _dense_weight(blob, fmt, n, k, x.dtype)
+        from .api import glu
+
+        def lib():
+            return glu(F.linear(x, w), act, tile=16)
+        if _pick((M, n, k, True, act), lambda: ops.gemm_bf16(x, w, None, False, 0, True, act), lib) == "lib":
+            return lib()
         return ops.gemm_bf16(x, w, None, False, 0, True, act)
     if use_engine(M, n, k, glu=True) and x.dtype in (torch.bfloat16, torch.float16):
         return ops.mfgemm(x, blob, fmt, n, k, None, True, act)

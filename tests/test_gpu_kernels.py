@@ -947,3 +947,37 @@ def test_decode_gemv_forms_at_llama3_8b_shapes(cuda, M):
                               ss=torch.zeros(M, device=cuda))
         g2, u2 = deinterleave_glu(xn @ deq(gu, 2 * I, H).t())
         assert _rel(y2, torch.nn.functional.silu(g2) * u2) < 1.5e-2
+
+
+@pytest.mark.parametrize("glu", [False, True])
+def test_prefill_gemm_measured_dispatch(cuda, glu):
+    """ops/gemm.py _pick: the 8-phase kernel and the library GEMM over the same
+    transient weight agree with fp32 torch whichever one a shape picks, and the
+    first eager call records a choice"""
+    from ipex_llm_amd.models.decoder import deinterleave_glu, interleave_glu_rows
+    from ipex_llm_amd.ops import gemm as G
+    f = get_format("sym_int4").fmt
+    torch.manual_seed(13)
+    M, n, k = 512, 1024, 2048
+    wf = (interleave_glu_rows(torch.randn(n // 2, k, device=cuda) * 0.02, torch.randn(n // 2, k, device=cuda) * 0.02)
+          if glu else torch.randn(n, k, device=cuda) * 0.02)
+    blob = ops.quantize(wf, f)
+    W = R.dequantize_device_blob(blob.cpu(), f, n, k).to(cuda).float()
+    x = torch.randn(M, k, device=cuda).bfloat16()
+    y32 = x.float() @ W.t()
+    if glu:
+        g, u = deinterleave_glu(y32)
+        y32 = torch.nn.functional.silu(g) * u
+    run = (lambda: G.lowbit_gemm_glu(x, blob, f, n, k, 0)) if glu else (lambda: G.lowbit_gemm(x, blob, f, n, k))
+    saved = dict(G._CHOICE)
+    try:
+        G._CHOICE.clear()
+        y = run()
+        assert (M, n, k, glu, 0) in G.gemm_choices()
+        assert _rel(y, y32) < 1e-2
+        for c in ("g8d", "lib"):
+            G._CHOICE[(M, n, k, glu, 0)] = c
+            assert _rel(run(), y32) < 1e-2, c
+    finally:
+        G._CHOICE.clear()
+        G._CHOICE.update(saved)
