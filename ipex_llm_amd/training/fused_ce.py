@@ -53,6 +53,11 @@ class _FusedLinearCE(torch.autograd.Function):
         loss_rows = torch.empty(T, device=h.device, dtype=torch.float32)
         grad_h = torch.empty_like(h) if h.requires_grad else None
         g8 = _g8_ok(h, w) and V % 64 == 0
+        if g8:
+            # the 8-phase head GEMMs or the library's, whichever this shape measured faster
+            from ..ops.gemm import _pick
+            c = min(T, CHUNK)
+            g8 = _pick((c, V, H, "ce_head", 0), lambda: ops.gemm_bf16(h[:c], w), lambda: torch.mm(h[:c], w.t())) == "g8d"
         for c0 in range(0, T, CHUNK):
             c1 = min(T, c0 + CHUNK)
             logits = ops.gemm_bf16(h[c0:c1], w) if g8 else torch.mm(h[c0:c1], w.t())
