@@ -315,16 +315,18 @@ def _time_ms(fn, reps: int = 3) -> float:
     return t0.elapsed_time(t1) / reps
 
 
-def _pick(key: tuple, g8d_fn, lib_fn) -> str:
+def _pick(key: tuple, g8d_fn, lib_fn, *more) -> str:
+    """'g8d' | 'lib' | 'lib1' ... (the extra candidates ``more``, in order)"""
     c = _CHOICE.get(key)
     if c is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():
             return "g8d"
-        tg, tl = _time_ms(g8d_fn), _time_ms(lib_fn)
-        c = _CHOICE[key] = "g8d" if tg <= tl else "lib"
+        names = ["g8d", "lib"] + [f"lib{i + 1}" for i in range(len(more))]
+        times = [_time_ms(f) for f in (g8d_fn, lib_fn) + more]
+        c = _CHOICE[key] = names[min(range(len(times)), key=times.__getitem__)]
         if os.environ.get("ILLM_GEMM_AUTOTUNE_LOG"):
-            print(f"[gemm] M={key[0]} N={key[1]} K={key[2]} glu={key[3]}: 8-phase {tg * 1e3:.1f} us, "
-                  f"library {tl * 1e3:.1f} us -> {c}", flush=True)
+            print(f"[gemm] M={key[0]} N={key[1]} K={key[2]} glu={key[3]}: "
+                  + ", ".join(f"{n} {t * 1e3:.1f} us" for n, t in zip(names, times)) + f" -> {c}", flush=True)
     return c
 
 

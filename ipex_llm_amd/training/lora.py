@@ -201,19 +201,30 @@ def _g8_bwd_ok(g2: torch.Tensor, base) -> bool:
 
 
 def _g8_grad_x(g2: torch.Tensor, base, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """g W (+ acc, added in the GEMM epilogue: sibling adapters' grad_x); the
-    8-phase kernel or the library GEMM over the same transient W^T, whichever the
-    shape measured faster (ops/gemm.py _pick)"""
+    """g W (+ acc: sibling adapters' grad_x) over a transient dequantized W,
+    whichever form the shape measured faster (ops/gemm.py _pick, the
+    dequantization included): the 8-phase kernel over W^T dequantized
+    transposed (acc added in its epilogue), the library GEMM over W as stored
+    (no transposed dequant, whose 32-B row pieces make it the slower one), or
+    the library over the transposed dequant"""
     from ..ops.gemm import _pick
     ops = torch.ops.ipex_llm_amd
-    wt = ops.dequantize_device(base.weight, base.fmt, base.out_features, base.in_features,
-                               g2.dtype, True)          # W^T [K, N]
-    key = (g2.shape[0], base.in_features, base.out_features, "grad_x", 0)
-    if _pick(key, lambda: ops.gemm_bf16(g2, wt), lambda: torch.mm(g2, wt.t())) == "lib":
-        return torch.mm(g2, wt.t()) if acc is None else acc.addmm_(g2, wt.t())
+    N, K = base.out_features, base.in_features
+
+    def wt():
+        return ops.dequantize_device(base.weight, base.fmt, N, K, g2.dtype, True)      # W^T [K, N]
+
+    def w():
+        return ops.dequantize_device(base.weight, base.fmt, N, K, g2.dtype, False)     # W [N, K]
+    key = (g2.shape[0], K, N, "grad_x", 0)
+    c = _pick(key, lambda: ops.gemm_bf16(g2, wt()), lambda: torch.mm(g2, w()), lambda: torch.mm(g2, wt().t()))
+    if c == "lib":
+        return torch.mm(g2, w()) if acc is None else acc.addmm_(g2, w())
+    if c == "lib1":          # the library over the transposed dequant (its other operand layout)
+        return torch.mm(g2, wt().t()) if acc is None else acc.addmm_(g2, wt().t())
     if acc is None:
-        return ops.gemm_bf16(g2, wt)
-    return ops.gemm_bf16(g2, wt, None, False, 0, False, 0, -1, acc, True)
+        return ops.gemm_bf16(g2, wt())
+    return ops.gemm_bf16(g2, wt(), None, False, 0, False, 0, -1, acc, True)
 
 
 def _base_dense_weight(base, dt):
