@@ -149,7 +149,7 @@ constexpr int DQ_CH = 4;                                  // chunks per workgrou
 constexpr int DQ_LD = DQ_CH * CHUNK_K + 8;                // LDS row stride (elements)
 template <typename T, int FMT>
 __global__ void __launch_bounds__(256) dequantize_tiled_kernel(const uint8_t* blob, int64_t n, int64_t k,
-                                                               uint16_t* out, bool tr) {
+                                                               uint16_t* out) {
   constexpr int fmt = FMT;
   constexpr int bits = fmt_bits(fmt);
   __shared__ __attribute__((aligned(16))) uint16_t rows[TILE_N * DQ_LD];
@@ -194,23 +194,6 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(const uint8_t* bl
   __syncthreads();
   // row segment [cg * 512, cg * 512 + 512) of rows t * 16 .. + 15: 64 x 16-B pieces per row
   const int64_t k0 = cg * DQ_CH * CHUNK_K;
-  if (tr) {
-    // transposed [k, n] output (the W^T operand of a grad_x = g W GEMM):
-    // per k, the tile's 16 rows are two 16-B pieces (n % 8 == 0, host-checked)
-#pragma unroll
-    for (int j = 0; j < DQ_CH * CHUNK_K * 2 / 256; j++) {
-      const int v = tid + 256 * j;
-      const int kk = v >> 1, h = v & 1;
-      const int64_t kg = k0 + kk, n0 = t * TILE_N + h * 8;
-      if (kg >= k || n0 + 8 > n) continue;
-      uint32_t pk[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        pk[i] = (uint32_t)rows[(h * 8 + 2 * i) * DQ_LD + kk] | ((uint32_t)rows[(h * 8 + 2 * i + 1) * DQ_LD + kk] << 16);
-      *(uint4*)(out + (size_t)kg * n + n0) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-    }
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < TILE_N * DQ_CH * CHUNK_K / 8 / 256; j++) {
     const int v = tid + 256 * j;
@@ -220,15 +203,86 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(const uint8_t* bl
   }
 }
 
+// Transposed output [k, n] (the W^T operand of grad_x = g W): a workgroup
+// decodes ONE 128-k chunk of FOUR consecutive 16-row tiles (one per wave) into
+// LDS [64 n][128 k], then stores per k one 128-B run of 64 n values, 8 lanes
+// per run.  The row-block kernel above wrote 32-B runs (its tile's 16 n per k).
+constexpr int DQT_TILES = 4;
+constexpr int DQT_LD = CHUNK_K + 8;
+template <typename T, int FMT>
+__global__ void __launch_bounds__(256) dequantize_tiled_tr_kernel(const uint8_t* blob, int64_t n, int64_t k,
+                                                                  uint16_t* out) {
+  constexpr int fmt = FMT;
+  constexpr int bits = fmt_bits(fmt);
+  __shared__ __attribute__((aligned(16))) uint16_t rows[DQT_TILES * TILE_N * DQT_LD];
+  const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K, NT = pad_to(n, TILE_N) / TILE_N;
+  const int64_t tg = blockIdx.x / KC, c = blockIdx.x % KC;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int r = l & 15, g = l >> 4;
+  const int64_t t = tg * DQT_TILES + w;
+  if (t < NT) {
+    const uint8_t* tile = blob + t * dev_tile_bytes(fmt, KC);
+    const uint8_t* rec = tile + c * dev_code_chunk(fmt);
+    uint32_t wd[bits == 4 ? 4 : 8];
+    {
+      const uint4 q = *(const uint4*)(rec + l * 16);
+      wd[0] = q.x; wd[1] = q.y; wd[2] = q.z; wd[3] = q.w;
+      if constexpr (bits != 4) {
+        const uint4 q1 = *(const uint4*)(rec + (64 + l) * 16);
+        wd[4] = q1.x; wd[5] = q1.y; wd[6] = q1.z; wd[7] = q1.w;
+      }
+    }
+    const uint16_t* sp = (const uint16_t*)(tile + dev_scale_off(fmt, KC, r, c));
+    const uint16_t* mp = fmt_has_min(fmt) ? (const uint16_t*)(tile + dev_min_off(fmt, KC, r, c)) : nullptr;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const int blk = s >> 1;
+      const float d = f16_to_f32(sp[blk]);
+      const float m = fmt_has_min(fmt) ? f16_to_f32(mp[blk]) : 0.f;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        int code;
+        if (bits == 4) code = (wd[s] >> (4 * dev_nib_pos(fmt, j))) & 15;
+        else code = (wd[4 * (s >> 1) + 2 * (s & 1) + (j >> 2)] >> (8 * (j & 3))) & 0xff;
+        v[j] = hd_code_value(fmt, code) * d + m;
+      }
+      *(uint4*)(rows + (w * TILE_N + r) * DQT_LD + 32 * s + 8 * g) =
+          make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
+    }
+  }
+  __syncthreads();
+  const int64_t n0 = tg * DQT_TILES * TILE_N, k0 = c * CHUNK_K;
+#pragma unroll
+  for (int p = 0; p < CHUNK_K * DQT_TILES * TILE_N / 8 / 256; p++) {
+    const int v = tid + 256 * p;
+    const int kk = v >> 3, nl = (v & 7) * 8;
+    const int64_t kg = k0 + kk, ng = n0 + nl;
+    if (kg >= k || ng + 8 > n) continue;
+    uint32_t pk[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      pk[i] = (uint32_t)rows[(nl + 2 * i) * DQT_LD + kk] | ((uint32_t)rows[(nl + 2 * i + 1) * DQT_LD + kk] << 16);
+    *(uint4*)(out + (size_t)kg * n + ng) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+  }
+}
+
 void launch_dequantize_device(bool bf16, int fmt, const uint8_t* blob, int64_t n, int64_t k,
                               uint16_t* out, hipStream_t st, bool transpose) {
   const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
-  const int64_t nblk = (pad_to(n, TILE_N) / TILE_N) * ((KC + DQ_CH - 1) / DQ_CH);
-  dim3 grid((unsigned)nblk);
+  const int64_t NT = pad_to(n, TILE_N) / TILE_N;
+  const int64_t nblk = NT * ((KC + DQ_CH - 1) / DQ_CH);
+  dim3 grid((unsigned)nblk), gridt((unsigned)(((NT + DQT_TILES - 1) / DQT_TILES) * KC));
 #define DQ_CASE(F)                                                                                       \
   case F:                                                                                                \
-    if (bf16) hipLaunchKernelGGL((dequantize_tiled_kernel<BF16, F>), grid, dim3(256), 0, st, blob, n, k, out, transpose); \
-    else hipLaunchKernelGGL((dequantize_tiled_kernel<F16, F>), grid, dim3(256), 0, st, blob, n, k, out, transpose);     \
+    if (transpose) {                                                                                     \
+      if (bf16) hipLaunchKernelGGL((dequantize_tiled_tr_kernel<BF16, F>), gridt, dim3(256), 0, st, blob, n, k, out); \
+      else hipLaunchKernelGGL((dequantize_tiled_tr_kernel<F16, F>), gridt, dim3(256), 0, st, blob, n, k, out);       \
+    } else if (bf16) {                                                                                   \
+      hipLaunchKernelGGL((dequantize_tiled_kernel<BF16, F>), grid, dim3(256), 0, st, blob, n, k, out); \
+    } else {                                                                                             \
+      hipLaunchKernelGGL((dequantize_tiled_kernel<F16, F>), grid, dim3(256), 0, st, blob, n, k, out);  \
+    }                                                                                                    \
     break;
   switch (fmt) {
     DQ_CASE(FMT_SYM_INT4) DQ_CASE(FMT_ASYM_INT4) DQ_CASE(FMT_NF4) DQ_CASE(FMT_FP4) DQ_CASE(FMT_SYM_INT8)
