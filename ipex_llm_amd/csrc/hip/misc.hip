@@ -153,6 +153,14 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(const uint8_t* bl
   constexpr int fmt = FMT;
   constexpr int bits = fmt_bits(fmt);
   __shared__ __attribute__((aligned(16))) uint16_t rows[TILE_N * DQ_LD];
+  // 16-entry code tables (nf4 / fp4 / nf3) from LDS: a dynamically indexed
+  // local array goes to scratch (nf4 ran at 3-4 TB/s vs 5-6 for sym_int4)
+  constexpr bool LUT = fmt == FMT_NF4 || fmt == FMT_FP4 || fmt == FMT_NF3;
+  __shared__ float lut[16];
+  if constexpr (LUT) {
+    if (threadIdx.x < 16) lut[threadIdx.x] = hd_lut4(fmt, threadIdx.x);
+    __syncthreads();
+  }
   const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K;
   const int64_t ncg = (KC + DQ_CH - 1) / DQ_CH;
   const int64_t t = blockIdx.x / ncg, cg = blockIdx.x % ncg;
@@ -185,7 +193,7 @@ __global__ void __launch_bounds__(256) dequantize_tiled_kernel(const uint8_t* bl
         // 4-bit: dword s = k-step s; 8-bit: half h = s / 2, dwords 2 (s % 2) .. + 1
         if (bits == 4) code = (wd[s] >> (4 * dev_nib_pos(fmt, j))) & 15;
         else code = (wd[4 * (s >> 1) + 2 * (s & 1) + (j >> 2)] >> (8 * (j & 3))) & 0xff;
-        v[j] = hd_code_value(fmt, code) * d + m;
+        v[j] = (LUT ? lut[code & 15] : hd_code_value(fmt, code)) * d + m;
       }
       *(uint4*)(rows + r * DQ_LD + w * CHUNK_K + 32 * s + 8 * g) =
           make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
@@ -215,6 +223,14 @@ __global__ void __launch_bounds__(256) dequantize_tiled_tr_kernel(const uint8_t*
   constexpr int fmt = FMT;
   constexpr int bits = fmt_bits(fmt);
   __shared__ __attribute__((aligned(16))) uint16_t rows[DQT_TILES * TILE_N * DQT_LD];
+  // 16-entry code tables (nf4 / fp4 / nf3) from LDS: a dynamically indexed
+  // local array goes to scratch (nf4 ran at 3-4 TB/s vs 5-6 for sym_int4)
+  constexpr bool LUT = fmt == FMT_NF4 || fmt == FMT_FP4 || fmt == FMT_NF3;
+  __shared__ float lut[16];
+  if constexpr (LUT) {
+    if (threadIdx.x < 16) lut[threadIdx.x] = hd_lut4(fmt, threadIdx.x);
+    __syncthreads();
+  }
   const int64_t KC = pad_to(k, CHUNK_K) / CHUNK_K, NT = pad_to(n, TILE_N) / TILE_N;
   const int64_t tg = blockIdx.x / KC, c = blockIdx.x % KC;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -245,7 +261,7 @@ __global__ void __launch_bounds__(256) dequantize_tiled_tr_kernel(const uint8_t*
         int code;
         if (bits == 4) code = (wd[s] >> (4 * dev_nib_pos(fmt, j))) & 15;
         else code = (wd[4 * (s >> 1) + 2 * (s & 1) + (j >> 2)] >> (8 * (j & 3))) & 0xff;
-        v[j] = hd_code_value(fmt, code) * d + m;
+        v[j] = (LUT ? lut[code & 15] : hd_code_value(fmt, code)) * d + m;
       }
       *(uint4*)(rows + (w * TILE_N + r) * DQT_LD + 32 * s + 8 * g) =
           make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
@@ -253,17 +269,24 @@ __global__ void __launch_bounds__(256) dequantize_tiled_tr_kernel(const uint8_t*
   }
   __syncthreads();
   const int64_t n0 = tg * DQT_TILES * TILE_N, k0 = c * CHUNK_K;
+  // each thread: two adjacent k (one 4-B LDS read per n) x 8 n -> two 16-B stores
 #pragma unroll
-  for (int p = 0; p < CHUNK_K * DQT_TILES * TILE_N / 8 / 256; p++) {
+  for (int p = 0; p < CHUNK_K / 2 * DQT_TILES * TILE_N / 8 / 256; p++) {
     const int v = tid + 256 * p;
-    const int kk = v >> 3, nl = (v & 7) * 8;
+    const int kk = (v >> 3) * 2, nl = (v & 7) * 8;
     const int64_t kg = k0 + kk, ng = n0 + nl;
     if (kg >= k || ng + 8 > n) continue;
-    uint32_t pk[4];
+    uint32_t a[8];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
-      pk[i] = (uint32_t)rows[(nl + 2 * i) * DQT_LD + kk] | ((uint32_t)rows[(nl + 2 * i + 1) * DQT_LD + kk] << 16);
-    *(uint4*)(out + (size_t)kg * n + ng) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    for (int i = 0; i < 8; i++) a[i] = *(const uint32_t*)(rows + (nl + i) * DQT_LD + kk);
+    uint32_t lo[4], hi[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      lo[i] = __builtin_amdgcn_perm(a[2 * i + 1], a[2 * i], 0x05040100u);   // low halves: k = kk
+      hi[i] = __builtin_amdgcn_perm(a[2 * i + 1], a[2 * i], 0x07060302u);   // high halves: k = kk + 1
+    }
+    *(uint4*)(out + (size_t)kg * n + ng) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    if (kg + 1 < k) *(uint4*)(out + (size_t)(kg + 1) * n + ng) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
   }
 }
 
