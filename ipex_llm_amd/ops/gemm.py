@@ -315,8 +315,16 @@ def _time_ms(fn, reps: int = 3) -> float:
     return t0.elapsed_time(t1) / reps
 
 
+def _mbucket(M: int) -> int:
+    """rows rounded up to a power of two: serving sees every prompt length, and one
+    timing per bucket keeps the table (and the warm-up cost) bounded"""
+    return 1 << max(0, int(M) - 1).bit_length()
+
+
 def _pick(key: tuple, g8d_fn, lib_fn, *more) -> str:
-    """'g8d' | 'lib' | 'lib1' ... (the extra candidates ``more``, in order)"""
+    """'g8d' | 'lib' | 'lib1' ... (the extra candidates ``more``, in order);
+    key = (M, N, K, kind, act), M bucketed"""
+    key = (_mbucket(key[0]),) + tuple(key[1:])
     c = _CHOICE.get(key)
     if c is None:
         if not _AUTOTUNE or torch.cuda.is_current_stream_capturing():

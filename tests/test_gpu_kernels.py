@@ -973,10 +973,10 @@ def test_prefill_gemm_measured_dispatch(cuda, glu):
     try:
         G._CHOICE.clear()
         y = run()
-        assert (M, n, k, glu, 0) in G.gemm_choices()
+        assert (G._mbucket(M), n, k, glu, 0) in G.gemm_choices()
         assert _rel(y, y32) < 1e-2
         for c in ("g8d", "lib"):
-            G._CHOICE[(M, n, k, glu, 0)] = c
+            G._CHOICE[(G._mbucket(M), n, k, glu, 0)] = c
             assert _rel(run(), y32) < 1e-2, c
     finally:
         G._CHOICE.clear()
