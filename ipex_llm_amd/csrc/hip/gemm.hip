@@ -383,4 +383,59 @@ void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st) {
   }
 }
 
+
+// ---- per-row power-of-two normalisation of 16-bit x to f16 (the f16 MFMA
+// input of the fused prefill GEMM, exact: x = y * rs)
+// one workgroup per row: amax -> power-of-two shift s.t. the row max lands in
+// [2^14, 2^15); y = x * 2^shift exactly in f16, rs = 2^-shift
+__global__ void __launch_bounds__(256) x_to_f16_rowscale_kernel(const uint16_t* x, int64_t ldx, int K, int in_bf16,
+                                                                 uint16_t* y, float* rs) {
+  __shared__ float red[4];
+  const int64_t row = blockIdx.x;
+  const uint16_t* xr = x + row * ldx;
+  uint16_t* yr = y + row * (int64_t)K;
+  float amax = 0.f;
+  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+    const uint4 v = *(const uint4*)(xr + k);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const float lo = in_bf16 ? bf16_to_f32(w[j] & 0xffff) : f16_to_f32(w[j] & 0xffff);
+      const float hi = in_bf16 ? bf16_to_f32(w[j] >> 16) : f16_to_f32(w[j] >> 16);
+      amax = fmaxf(amax, fmaxf(fabsf(lo), fabsf(hi)));
+    }
+  }
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int shift = 0;
+  if (amax > 0.f && amax <= 3.0e38f) {
+    int e;
+    frexpf(amax, &e);              // amax = f * 2^e, f in [0.5, 1)
+    shift = 15 - e;                // amax * 2^shift in [2^14, 2^15)
+    shift = max(-120, min(120, shift));
+  }
+  const float sc = ldexpf(1.f, shift);
+  if (threadIdx.x == 0) rs[row] = ldexpf(1.f, -shift);
+  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+    const uint4 v = *(const uint4*)(xr + k);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const float lo = in_bf16 ? bf16_to_f32(w[j] & 0xffff) : f16_to_f32(w[j] & 0xffff);
+      const float hi = in_bf16 ? bf16_to_f32(w[j] >> 16) : f16_to_f32(w[j] >> 16);
+      o[j] = pack2<F16>(lo * sc, hi * sc);
+    }
+    *(uint4*)(yr + k) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+void launch_x_to_f16_rowscale(bool bf16, const uint16_t* x, int64_t M, int64_t ldx, int K, uint16_t* y, float* rs,
+                              hipStream_t st) {
+  if (M <= 0) return;
+  hipLaunchKernelGGL(x_to_f16_rowscale_kernel, dim3((unsigned)M), dim3(256), 0, st, x, ldx, K, bf16 ? 1 : 0, y, rs);
+}
+
 }  // namespace illm

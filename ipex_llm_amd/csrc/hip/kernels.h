@@ -60,42 +60,6 @@ void launch_lowbit_gemm(bool bf16, int fmt, const GemmArgs& a, hipStream_t st);
 // bf16 -> f16 with saturation at +-65504 (the GEMM's MFMA input type), n % 8 == 0
 void launch_bf16_to_f16_sat(const uint16_t* x, uint16_t* y, int64_t n, hipStream_t st);
 
-// ---- MFMA GEMM engine (gemm_mfma.hip): out[M, N] = x[M, K] . W[N, K]^T --------
-// 512-thread workgroups over 256 x 256 (or 256 x 128 / 128 x 256) output
-// blocks, K in 64-deep LDS stages.  W = the tiled low-bit blob (f16 MFMA, x
-// must be f16: launch_x_to_f16_rowscale) or a dense 16-bit [N][ldw] matrix.
-// Requires K % 128 == 0, N % 16 == 0 (N % 32 == 0 with glu), x / W rows 16-B aligned.
-constexpr int DK_DENSE = 100;
-enum MfgTile : int { MFG_TILE_256x256 = 0, MFG_TILE_256x128 = 1, MFG_TILE_128x256 = 2 };
-struct MfgArgs {
-  const uint16_t* x;       // [M, ldx] MFMA-type activations
-  int M, K, ldx;
-  uint32_t x_bytes;        // bytes of x addressable through the buffer descriptor (M * ldx * 2)
-  const float* rs;         // [M] per-row output scale (x row normalisation) or null
-  const uint8_t* w;        // tiled blob, or dense [N, ldw] 16-bit
-  int N, KC, ldw;
-  uint32_t w_bytes;        // dense: N * ldw * 2
-  const uint16_t* bias;    // [N] 16-bit (bias_bf16 selects the type) or null
-  int bias_bf16;
-  void* out;               // [M, ldo] 16-bit (out_bf16) or f32 slabs [ksplit][slab]
-  int ldo, out_bf16, out_f32;
-  int64_t slab;            // f32 elements between split-K slabs
-  int glu, act, lut_fmt;   // glu: tile-interleaved gate/up weight -> act(gate) * up [M, N / 2]
-  int sps;                 // k-steps (64) per split, even
-  // rank-r update folded into the epilogue (LoRA): out += lora_x[M, rp] . lora_w[N, rp]^T,
-  // both bf16, zero-padded to rp % 32 == 0 (null: none; not with glu / split-K)
-  const uint16_t* lora_x;
-  const uint16_t* lora_w;
-  int lora_rp;
-};
-int mfg_block_n(int tile);
-int mfg_block_m(int tile);
-// fmt < 0: dense weights (dense_bf16 selects bf16 / f16 MFMA); else a low-bit fmt (f16 MFMA)
-void launch_mfgemm(int fmt, bool dense_bf16, int tile, const MfgArgs& a, int ksplit, hipStream_t st);
-// transposed-weight form (gemm_mfma_nn.hip): out[M, a.N] = g[M, a.K] . W[a.K, a.N] where W is
-// the blob / dense matrix of a linear with out_features a.K and in_features a.N (grad_x);
-// a.K % 64 == 0, low-bit: a.N % 256 == 0 (a.KC = a.N / 128)
-void launch_mfgemm_nn(int fmt, bool dense_bf16, int tile, const MfgArgs& a, int ksplit, hipStream_t st);
 // per-row power-of-two normalisation to f16: y = x * 2^s_m (row max in [2^14, 2^15)), rs[m] = 2^-s_m
 void launch_x_to_f16_rowscale(bool bf16, const uint16_t* x, int64_t M, int64_t ldx, int K, uint16_t* y, float* rs,
                               hipStream_t st);

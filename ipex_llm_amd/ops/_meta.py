@@ -249,23 +249,9 @@ def _(like, reset):
     return like.new_empty(4, dtype=torch.int32)
 
 
-@register_fake("ipex_llm_amd::mfgemm")
-def _(x, w, fmt, n, k, bias=None, glu=False, act=0, tile=-1, ksplit=0):
-    shape = list(x.shape)
-    shape[-1] = n // 2 if glu else n
-    return x.new_empty(shape)
-
-
 @register_fake("ipex_llm_amd::x_to_f16_rowscale")
 def _(x):
     return [x.new_empty(x.shape, dtype=torch.float16), x.new_empty((x.shape[0],), dtype=torch.float32)]
-
-
-@register_fake("ipex_llm_amd::mfgemm_nn")
-def _(g, w, fmt, n, k, tile=-1, ksplit=0):
-    shape = list(g.shape)
-    shape[-1] = k
-    return g.new_empty(shape)
 
 
 @register_fake("ipex_llm_amd::ce_fused_")
@@ -309,24 +295,6 @@ def _(q, k, v, out, lse, dout, scale, causal=True):
     return [torch.empty_like(q, memory_format=torch.contiguous_format),
             torch.empty_like(k, memory_format=torch.contiguous_format),
             torch.empty_like(v, memory_format=torch.contiguous_format)]
-
-
-@register_fake("ipex_llm_amd::mfgemm_lora")
-def _(x, w, fmt, n, k, bias, la, lb, s):
-    shape = list(x.shape)
-    shape[-1] = n
-    M = x.numel() // k
-    rp = (la.shape[0] + 31) // 32 * 32
-    return [x.new_empty(shape), x.new_empty((M, rp))]
-
-
-@register_fake("ipex_llm_amd::mfgemm_nn_lora")
-def _(g, w, fmt, n, k, la, lb, s):
-    shape = list(g.shape)
-    shape[-1] = k
-    M = g.numel() // n
-    rp = (la.shape[0] + 31) // 32 * 32
-    return [g.new_empty(shape), g.new_empty((M, rp))]
 
 
 @register_fake("ipex_llm_amd::gemm_bf16")

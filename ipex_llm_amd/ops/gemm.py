@@ -230,23 +230,6 @@ def drop_prefetched() -> None:
     _ready.clear()
 
 
-# ---- the MFMA GEMM engine (csrc/hip/gemm_mfma.hip) ---------------------------
-# 256 x 256 blocks, LDS-DMA staged activations, per-workgroup decode of the
-# blob into LDS: replaces both paths above from ENGINE_MIN_M rows
-# (ILLM_GEMM_ENGINE=0 disables it for A/B runs).
-# Off by default: measured 0.63-0.88x dequant + hipBLASLt at M = 1024-4096
-# (profiles/mfgemm_engine_sweep_r4.jsonl) and 242 vs 167 ms per QLoRA step
-# (profiles/qlora_r4_ab_*.json); the 8-phase GEMM above replaced it.
-_ENGINE = os.environ.get("ILLM_GEMM_ENGINE", "0") == "1"
-ENGINE_MIN_M = int(os.environ.get("ILLM_GEMM_ENGINE_MIN_M", "512"))
-
-
-def use_engine(M: int, n: int, k: int, glu: bool = False) -> bool:
-    return (_ENGINE and not _USE_LIB and not _USE_FUSED and M >= ENGINE_MIN_M and k % 128 == 0
-            and n % (32 if glu else 16) == 0 and _DENSE_BUDGET <= 0
-            and hasattr(torch.ops.ipex_llm_amd, "mfgemm"))
-
-
 # ---- the 8-phase 256 x 256 GEMM (csrc/hip/gemm_8p.hip): bf16 MFMA, weights
 # decoded to bf16 in LDS just in time (bit-identical to dequantize-to-bf16 +
 # GEMM), LDS-DMA activations, counted-vmcnt pipeline, staggered wave-rows.
@@ -353,8 +336,6 @@ def lowbit_gemm(x, blob, fmt, n, k, bias=None):
         if _pick((M, n, k, False, 0), lambda: ops.gemm_bf16(x, w, bias), lambda: F.linear(x, w, bias)) == "lib":
             return F.linear(x, w, bias)
         return ops.gemm_bf16(x, w, bias)
-    if use_engine(M, n, k) and x.dtype in (torch.bfloat16, torch.float16):
-        return ops.mfgemm(x, blob, fmt, n, k, bias)
     if use_fused(M, n, k) and hasattr(ops, "gemm"):
         return ops.gemm(x, blob, fmt, n, k, bias)
     w = _dense_weight(blob, fmt, n, k, x.dtype)
@@ -378,8 +359,6 @@ def lowbit_gemm_glu(x, blob, fmt, n, k, act: int = 0):
         if _pick((M, n, k, True, act), lambda: ops.gemm_bf16(x, w, None, False, 0, True, act), lib) == "lib":
             return lib()
         return ops.gemm_bf16(x, w, None, False, 0, True, act)
-    if use_engine(M, n, k, glu=True) and x.dtype in (torch.bfloat16, torch.float16):
-        return ops.mfgemm(x, blob, fmt, n, k, None, True, act)
     if use_fused(M, n, k) and hasattr(ops, "gemm_glu"):
         return ops.gemm_glu(x, blob, fmt, n, k, act)
     from .api import glu

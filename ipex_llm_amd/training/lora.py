@@ -279,11 +279,6 @@ class _LoraLowBitFn(torch.autograd.Function):
             base = ctx.base
             if _g8_bwd_ok(g2, base):
                 gx = _g8_grad_x(g2, base)
-            elif _engine_nn_ok(base, g2):
-                # g W straight from the low-bit blob (transposed LDS reads in the
-                # engine GEMM, csrc/hip/gemm_mfma_nn.hip): no dense W
-                gx = torch.ops.ipex_llm_amd.mfgemm_nn(g2, base.weight, base.fmt, base.out_features,
-                                                      base.in_features)
             elif _kcat_rows_ok(base, g2, A):
                 # gx = [g | s g B] [W ; A]: the adapter term as r extra K rows of
                 # the grad_x GEMM (row-augmented shadow) instead of a rank-update
@@ -519,69 +514,6 @@ class _LoraGroupFn(torch.autograd.Function):
         return (gx, None, None, *out)
 
 
-class _LoraEngineFn(torch.autograd.Function):
-    """The QLoRA linear entirely on the engine kernels (no library GEMM):
-
-    forward   one pass over x gives the f16 copy + row scales and
-              xa = s x A^T (``mfgemm_lora``); the base GEMM decodes W from the
-              blob and adds xa B^T as extra MFMA steps of its epilogue;
-    backward  one pass over g gives g16 + gxa = s g B; the transposed base
-              GEMM adds gxa A in its epilogue (``mfgemm_nn_lora``);
-              dA = gxa^T x and dB = g^T xa are single-pass token-axis
-              reductions (``skinny_tn``).
-    Reference: LoraLowBitLinear.forward (SRC/transformers/qlora.py:114-143) +
-    MatMulLowBit.backward (SRC/transformers/low_bit_linear.py:553-573)."""
-
-    @staticmethod
-    def forward(ctx, x, A, B, base, s):
-        shp = x.shape
-        x2 = x.reshape(-1, shp[-1])
-        ops = torch.ops.ipex_llm_amd
-        y, xa = ops.mfgemm_lora(x2, base.weight, base.fmt, base.out_features, base.in_features, base.bias,
-                                A, B, float(s))
-        ctx.save_for_backward(x2, xa, A, B)
-        ctx.base, ctx.s, ctx.shp = base, s, shp
-        return y.view(*shp[:-1], y.shape[-1])
-
-    @staticmethod
-    def backward(ctx, g):
-        x2, xa, A, B = ctx.saved_tensors
-        base, r = ctx.base, A.shape[0]
-        ops = torch.ops.ipex_llm_amd
-        g2 = g.reshape(-1, g.shape[-1]).to(x2.dtype).contiguous()
-        gx, gxa = ops.mfgemm_nn_lora(g2, base.weight, base.fmt, base.out_features, base.in_features, A, B,
-                                     float(ctx.s))
-        gA = ops.skinny_tn(gxa[:, :r], x2).to(A.dtype) if ctx.needs_input_grad[1] else None
-        gB = ops.skinny_tn(xa[:, :r], g2).t().to(B.dtype) if ctx.needs_input_grad[2] else None
-        return gx.view(ctx.shp), gA, gB, None, None
-
-
-def _engine_lora_ok(base, x, A) -> bool:
-    from .. import ops
-    from ..ops.gemm import _DENSE_BUDGET, _ENGINE
-    M = x.numel() // max(1, x.shape[-1])
-    return (_ENGINE and _ENGINE_NN and _DENSE_BUDGET <= 0 and x.is_cuda and x.dtype == torch.bfloat16
-            and base.weight.is_cuda and ops.native_gpu(base.weight)
-            and hasattr(torch.ops.ipex_llm_amd, "mfgemm_lora") and M >= 64 and A.shape[0] <= 64
-            and base.out_features % 128 == 0 and base.in_features % 256 == 0
-            and A.dtype == torch.bfloat16)
-
-
-# off by default: the engine NN GEMM measured slower than dequant + hipBLASLt
-# (profiles/qlora_llama3_8b_r4_engine_rocprof.txt)
-_ENGINE_NN = os.environ.get("ILLM_LORA_ENGINE_NN", "0") == "1"
-
-
-def _engine_nn_ok(base, g2) -> bool:
-    """the engine's transposed GEMM covers this backward (GPU blob, shapes)"""
-    from .. import ops
-    from ..ops.gemm import _DENSE_BUDGET
-    return (_ENGINE_NN and _DENSE_BUDGET <= 0 and g2.is_cuda and base.weight.is_cuda
-            and ops.native_gpu(base.weight) and hasattr(torch.ops.ipex_llm_amd, "mfgemm_nn")
-            and g2.shape[0] >= 64 and base.out_features % 128 == 0 and base.in_features % 256 == 0
-            and g2.dtype in (torch.bfloat16, torch.float16))
-
-
 class LoraLinear(nn.Module):
     """base(x) + B(A(dropout(pool(x)))) * scaling over a frozen base layer
     (LowBitLinear -> QLoRA/QA-LoRA, DenseLinear/nn.Linear -> LoRA)."""
@@ -641,8 +573,7 @@ class LoraLinear(nn.Module):
             return out
         mods = grp["mods"]
         if self is not mods[0] or not all(m._fused_ok(x) and not (m.disable_adapters or m.merged) for m in mods) \
-                or len({m.scaling for m in mods}) != 1 or any(_engine_lora_ok(m.base_layer, x, m.lora_A.weight)
-                                                              for m in mods):
+                or len({m.scaling for m in mods}) != 1:
             return None
         ab = []
         for m in mods:
@@ -656,8 +587,6 @@ class LoraLinear(nn.Module):
             y = self._group_forward(x)
             if y is not None:
                 return y
-            if _engine_lora_ok(self.base_layer, x, self.lora_A.weight):
-                return _LoraEngineFn.apply(x, self.lora_A.weight, self.lora_B.weight, self.base_layer, self.scaling)
             return _LoraLowBitFn.apply(x, self.lora_A.weight, self.lora_B.weight, self.base_layer, self.scaling)
         result = self.base_layer(x)
         if self.disable_adapters or self.merged:

@@ -981,3 +981,13 @@ def test_prefill_gemm_measured_dispatch(cuda, glu):
     finally:
         G._CHOICE.clear()
         G._CHOICE.update(saved)
+
+
+def test_x_to_f16_rowscale_exact(cuda):
+    """per-row power-of-two f16 normalisation of the fused prefill GEMM input
+    (csrc/hip/gemm.hip): exact round trip, row max in [2^14, 2^15)"""
+    x = (torch.randn(8, 256, device=cuda) * torch.tensor([1e-6, 1e-2, 1, 30, 1e3, 6e4, 2e5, 1e30],
+                                                          device=cuda)[:, None]).bfloat16()
+    y, rs = torch.ops.ipex_llm_amd.x_to_f16_rowscale(x)
+    assert torch.equal(y.float() * rs[:, None], x.float())
+    assert (y.float().abs().amax(1) < 32768).all() and (y.float().abs().amax(1) >= 16384).all()

@@ -128,41 +128,6 @@ def test_train_flash_attention_fwd_bwd(cuda, B, Hq, Hkv, T, D, causal):
     assert _rel(v.grad, vr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("qtype,r", [("nf4", 8), ("sym_int4", 16), ("nf4", 40)])
-def test_lora_engine_node_matches_fp32(cuda, qtype, r, monkeypatch):
-    """the all-engine QLoRA linear (LoRA in the GEMM epilogues, skinny adapter
-    gradients) vs fp32 torch over the dequantized base (the engine path is
-    opt-in: ILLM_GEMM_ENGINE=1 ILLM_LORA_ENGINE_NN=1)"""
-    import ipex_llm_amd.ops.gemm as G
-    import ipex_llm_amd.training.lora as L
-    monkeypatch.setattr(G, "_ENGINE", True)
-    monkeypatch.setattr(L, "_ENGINE_NN", True)
-    from ipex_llm_amd import ops
-    from ipex_llm_amd.ops import reference as R
-    from ipex_llm_amd.quantize import get_format
-    from ipex_llm_amd.training.lora import _LoraEngineFn, _engine_lora_ok
-    from ipex_llm_amd.transformers.low_bit_linear import LowBitLinear
-    torch.manual_seed(4)
-    M, N, K, s = 300, 768, 1024, 2.0
-    base = LowBitLinear(K, N, qtype, bias=False, device="meta")
-    base.load_dense((torch.randn(N, K, device=cuda) * 0.05).bfloat16(), device=cuda)
-    A = (torch.randn(r, K, device=cuda) * 0.05).bfloat16().requires_grad_(True)
-    B = (torch.randn(N, r, device=cuda) * 0.05).bfloat16().requires_grad_(True)
-    x = torch.randn(2, M // 2, K, device=cuda).bfloat16().requires_grad_(True)
-    assert _engine_lora_ok(base, x, A)
-    y = _LoraEngineFn.apply(x, A, B, base, s)
-    gy = torch.randn_like(y)
-    y.backward(gy)
-    W = R.dequantize_device_blob(base.weight.cpu(), get_format(qtype).fmt, N, K).to(cuda)
-    xr, Ar, Br = (t.detach().float().requires_grad_(True) for t in (x, A, B))
-    yr = xr @ W.t() + s * (xr @ Ar.t()) @ Br.t()
-    yr.backward(gy.float())
-    assert _rel(y, yr) < 1e-2
-    assert _rel(x.grad, xr.grad) < 1e-2
-    assert _rel(A.grad, Ar.grad) < 2e-2
-    assert _rel(B.grad, Br.grad) < 2e-2
-
-
 @pytest.mark.parametrize("M,N,r", [(4096, 4096, 8), (300, 1000, 16), (77, 14336, 24), (64, 4104, 64), (1, 8, 8),
                                    (33, 200, 8)])
 def test_lora_update_matches_fp32(cuda, M, N, r):
