@@ -329,13 +329,18 @@ def gemm_choices() -> Dict[tuple, str]:
 def lowbit_gemm(x, blob, fmt, n, k, bias=None):
     ops = torch.ops.ipex_llm_amd
     M = x.numel() // k
-    if use_g8(x, M, n, k, fmt) and (bias is None or bias.dtype == torch.bfloat16):
+    bf16_bias = bias is None or bias.dtype == torch.bfloat16
+    if use_g8(x, M, n, k, fmt) and bf16_bias:
         return ops.gemm8p_lowbit(x, blob, fmt, n, k, bias)
-    if use_g8d(x, M, n, k) and (bias is None or bias.dtype == torch.bfloat16):
-        w = _dense_weight(blob, fmt, n, k, x.dtype)
-        if _pick((M, n, k, False, 0), lambda: ops.gemm_bf16(x, w, bias), lambda: F.linear(x, w, bias)) == "lib":
-            return F.linear(x, w, bias)
-        return ops.gemm_bf16(x, w, bias)
+    if use_g8d(x, M, n, k) and bf16_bias:
+        # candidates timed with their weight preparation: the 8-phase kernel and
+        # the library over the transient bf16 weight.  (The in-LDS low-bit
+        # 8-phase kernel, no transient weight, lost every Llama-3-8B prefill shape
+        # as a third candidate: 0.55-0.85x, profiles/prefill_choices_b{1,8}_r6.txt.)
+        def dw():
+            return _dense_weight(blob, fmt, n, k, x.dtype)
+        c = _pick((M, n, k, False, 0), lambda: ops.gemm_bf16(x, dw(), bias), lambda: F.linear(x, dw(), bias))
+        return F.linear(x, dw(), bias) if c == "lib" else ops.gemm_bf16(x, dw(), bias)
     if use_fused(M, n, k) and hasattr(ops, "gemm"):
         return ops.gemm(x, blob, fmt, n, k, bias)
     w = _dense_weight(blob, fmt, n, k, x.dtype)
@@ -351,14 +356,15 @@ def lowbit_gemm_glu(x, blob, fmt, n, k, act: int = 0):
     if use_g8(x, M, n, k, fmt, glu=True):
         return ops.gemm8p_lowbit(x, blob, fmt, n, k, None, False, True, act)
     if use_g8d(x, M, n, k, glu=True) and act in (0, 1):
-        w = _dense_weight(blob, fmt, n, k, x.dtype)
         from .api import glu
 
+        def dw():
+            return _dense_weight(blob, fmt, n, k, x.dtype)
+
         def lib():
-            return glu(F.linear(x, w), act, tile=16)
-        if _pick((M, n, k, True, act), lambda: ops.gemm_bf16(x, w, None, False, 0, True, act), lib) == "lib":
-            return lib()
-        return ops.gemm_bf16(x, w, None, False, 0, True, act)
+            return glu(F.linear(x, dw()), act, tile=16)
+        c = _pick((M, n, k, True, act), lambda: ops.gemm_bf16(x, dw(), None, False, 0, True, act), lib)
+        return lib() if c == "lib" else ops.gemm_bf16(x, dw(), None, False, 0, True, act)
     if use_fused(M, n, k) and hasattr(ops, "gemm_glu"):
         return ops.gemm_glu(x, blob, fmt, n, k, act)
     from .api import glu

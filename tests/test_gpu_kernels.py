@@ -958,7 +958,7 @@ def test_prefill_gemm_measured_dispatch(cuda, glu):
     from ipex_llm_amd.ops import gemm as G
     f = get_format("sym_int4").fmt
     torch.manual_seed(13)
-    M, n, k = 512, 1024, 2048
+    M, n, k = 1024, 1024, 2048
     wf = (interleave_glu_rows(torch.randn(n // 2, k, device=cuda) * 0.02, torch.randn(n // 2, k, device=cuda) * 0.02)
           if glu else torch.randn(n, k, device=cuda) * 0.02)
     blob = ops.quantize(wf, f)
