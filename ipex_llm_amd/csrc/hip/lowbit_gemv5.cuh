@@ -1212,13 +1212,15 @@ inline bool launch5_xm(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs&
   if constexpr (DK != DK_INT4S || !std::is_same<T, BF16>::value || MOE || !ILLM_GEMV5_XM) {
     return false;
   } else {
-    // ILLM_GEMV5_XM_RT (run time): 0 (default) = generic kernels only, 1 = XM 1 only, 2 = XM 1 and 2.
-    // Off by default: tools/probe/xm_check.hip (random inputs, each XM form vs the generic
-    // kernel) finds wrong outputs -- ATOMIC forms at 8 waves and once the ring is refilled
-    // (run-to-run different, gone with -amdgpu-waitcnt-forcezero: a load consumed before it
-    // landed), the XS 2 GLU form at 4 waves (deterministic, also with forcezero, although
-    // its staged x is right).  profiles/gemv5_xm_forms_r6.txt
-    static const int rt = getenv("ILLM_GEMV5_XM_RT") ? atoi(getenv("ILLM_GEMV5_XM_RT")) : 0;
+    // ILLM_GEMV5_XM_RT (run time): 0 = generic kernels only, 1 = XM 1 only, 2 (default) = XM 1 and 2.
+    // Only the forms that tools/probe/xm_check.hip (random inputs, each form against the
+    // generic kernel, three repeats) found exact are taken: split-K forms whose wave range
+    // never reaches the steady-state ring loop (cpk < 2 PF; the decode split-K plans: 4-7
+    // chunks), and the 8-slot GLU form.  Wrong outputs were found in the others --
+    // split-K forms once the ring is refilled (run-to-run different) and the 2-slot
+    // GLU form at 4 waves (deterministic) -- and with -amdgpu-mfma-vgpr-form in more
+    // (profiles/gemv5_xm_forms_r6.txt); gemv_int4.hip is built without that flag.
+    static const int rt = getenv("ILLM_GEMV5_XM_RT") ? atoi(getenv("ILLM_GEMV5_XM_RT")) : 2;
     if (rt <= 0 || a.apo != nullptr || a.xpart != nullptr || a.K % 128 != 0 || a.pf8 || kw > 2) return false;
     const int cpk = a.cpk > 0 ? a.cpk : (a.KC + (int)grid.y - 1) / (int)grid.y;
     const int nthr = a.nw == 8 ? 512 : 256;
@@ -1233,20 +1235,17 @@ inline bool launch5_xm(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs&
       return true;                                                                                            \
     } while (0)
     const bool glu_ok = kw == 2 && ILLM_GEMV5_SCL && (cpk + 1) / 2 <= 16;
+    const bool atomic_ok = epi == EPI_ATOMIC && kw == 1 && cpk < 2 * 4;      // PF 4: no ring refill loop
     if (a.x == nullptr && a.nacc != nullptr && a.ndefer != 0) {
-      // XM 2: deferred-norm input (decode qkv; batch-1 / -2 gate-up)
+      // XM 2: deferred-norm input (decode qkv)
       if (rt < 2) return false;
-      if (epi == EPI_ATOMIC && kw == 1 && slots <= 1) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 1);
-      if (epi == EPI_ATOMIC && kw == 1 && slots <= 2) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 2);
-      if (epi == EPI_GLU && glu_ok && slots <= 2) ILLM_XM_LAUNCH(EPI_GLU, 2, 2, ILLM_GEMV5_PFD, true, 2, 2);
+      if (atomic_ok && slots <= 1) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 1);
+      if (atomic_ok && slots <= 2) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 2);
       return false;
     }
     if (a.x == nullptr || a.nacc != nullptr) return false;
-    if (epi == EPI_ATOMIC && kw == 1 && slots <= 1) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 1, 1);
-    if (epi == EPI_ATOMIC && kw == 1 && slots <= 2) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 1, 2);
-    if (epi == EPI_STORE && kw == 1 && slots <= 2) ILLM_XM_LAUNCH(EPI_STORE, 1, 1, 4, false, 1, 2);
-    if (epi == EPI_STORE && kw == 1 && slots <= 8) ILLM_XM_LAUNCH(EPI_STORE, 1, 1, 4, false, 1, 8);
-    if (epi == EPI_GLU && glu_ok && slots <= 2) ILLM_XM_LAUNCH(EPI_GLU, 2, 2, ILLM_GEMV5_PFD, true, 1, 2);
+    if (atomic_ok && slots <= 1) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 1, 1);
+    if (atomic_ok && slots <= 2) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 1, 2);
     if (epi == EPI_GLU && glu_ok && slots <= 8) ILLM_XM_LAUNCH(EPI_GLU, 2, 2, ILLM_GEMV5_PFD, true, 1, 8);
 #undef ILLM_XM_LAUNCH
     return false;
