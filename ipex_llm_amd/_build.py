@@ -76,10 +76,10 @@ def _cmd(src: str, obj: str):
             # beside MFMAs costs issue cycles on gfx950 (and blocks v_fma_mix)
             # and MFMA results in VGPRs (no v_accvgpr_read per 64-block readout)
             extra = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]
-            # not for gemv_int4.hip (the decode XM forms, lowbit_gemv5.cuh launch5_xm):
-            # with the VGPR form hipcc (ROCm 7.2) miscompiles some of them
-            # (profiles/gemv5_xm_forms_r6.txt); without it they time the same
-            if os.path.basename(src) == "gemv_int4.hip":
+            # not for gemv_int4_xm.hip (the decode XM forms, lowbit_gemv5.cuh
+            # launch5_xm_int4s): with the VGPR form hipcc (ROCm 7.2) miscompiles
+            # some of them (profiles/gemv5_xm_forms_r6.txt)
+            if os.path.basename(src) == "gemv_int4_xm.hip":
                 extra = ["-fno-slp-vectorize"]
         return [HIPCC, f"--offload-arch={ARCH}", "-Wno-pass-failed", *extra, *common, "-c", src, "-o", obj]
     if "/cpu/" in src:

@@ -1207,11 +1207,26 @@ inline void launch5_epi(int epi, dim3 grid, size_t shmem, const GemvArgs& a, hip
 #ifndef ILLM_GEMV5_XM
 #define ILLM_GEMV5_XM ILLM_GEMV5_EARLYX
 #endif
+// The XM kernels are instantiated in their own translation unit
+// (gemv_int4_xm.hip, built without -amdgpu-mfma-vgpr-form; the generic kernels
+// keep the flag): launch5_xm_int4s is defined there, or here when
+// ILLM_GEMV5_XM_IMPL is set (that TU, the standalone probes).
+bool launch5_xm_int4s(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st);
+
 template <int DK, typename T, bool MOE>
 inline bool launch5_xm(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
   if constexpr (DK != DK_INT4S || !std::is_same<T, BF16>::value || MOE || !ILLM_GEMV5_XM) {
     return false;
   } else {
+    return launch5_xm_int4s(kw, epi, grid, shmem, a, st);
+  }
+}
+
+#ifdef ILLM_GEMV5_XM_IMPL
+bool launch5_xm_int4s(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a, hipStream_t st) {
+  constexpr int DK = DK_INT4S;
+  using T = BF16;
+  {
     // ILLM_GEMV5_XM_RT (run time): 0 = generic kernels only, 1 = XM 1 only, 2 (default) = XM 1 and 2.
     // Only the forms that tools/probe/xm_check.hip (random inputs, each form against the
     // generic kernel, three repeats) found exact are taken: split-K forms whose wave range
@@ -1251,6 +1266,7 @@ inline bool launch5_xm(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs&
     return false;
   }
 }
+#endif  // ILLM_GEMV5_XM_IMPL
 
 template <int DK, typename T, bool MOE>
 inline void launch5_kw(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& a0, hipStream_t st) {
