@@ -1252,10 +1252,11 @@ bool launch5_xm_int4s(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& 
     const bool glu_ok = kw == 2 && ILLM_GEMV5_SCL && (cpk + 1) / 2 <= 16;
     const bool atomic_ok = epi == EPI_ATOMIC && kw == 1 && cpk < 2 * 4;      // PF 4: no ring refill loop
     if (a.x == nullptr && a.nacc != nullptr && a.ndefer != 0) {
-      // XM 2: deferred-norm input (decode qkv)
+      // XM 2: deferred-norm input (decode qkv; batch-1 / -2 gate/up, 8-slot form)
       if (rt < 2) return false;
       if (atomic_ok && slots <= 1) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 1);
       if (atomic_ok && slots <= 2) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 2);
+      if (epi == EPI_GLU && glu_ok && slots <= 8 && rt >= 3) ILLM_XM_LAUNCH(EPI_GLU, 2, 2, ILLM_GEMV5_PFD, true, 2, 8);
       return false;
     }
     if (a.x == nullptr || a.nacc != nullptr) return false;
