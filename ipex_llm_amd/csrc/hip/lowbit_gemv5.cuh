@@ -1252,7 +1252,8 @@ bool launch5_xm_int4s(int kw, int epi, dim3 grid, size_t shmem, const GemvArgs& 
     const bool glu_ok = kw == 2 && ILLM_GEMV5_SCL && (cpk + 1) / 2 <= 16;
     const bool atomic_ok = epi == EPI_ATOMIC && kw == 1 && cpk < 2 * 4;      // PF 4: no ring refill loop
     if (a.x == nullptr && a.nacc != nullptr && a.ndefer != 0) {
-      // XM 2: deferred-norm input (decode qkv; batch-1 / -2 gate/up, 8-slot form)
+      // XM 2: deferred-norm input (decode qkv).  The 8-slot gate/up form (ILLM_GEMV5_XM_RT=3)
+      // measured slower at batch 1: 1.594-1.597 vs 1.569-1.577 ms (profiles/xm2_glu_ab_r6.jsonl)
       if (rt < 2) return false;
       if (atomic_ok && slots <= 1) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 1);
       if (atomic_ok && slots <= 2) ILLM_XM_LAUNCH(EPI_ATOMIC, 1, 1, 4, false, 2, 2);
